@@ -1,0 +1,101 @@
+"""MultiSURF / MultiSURF* estimator (reference: src/fast_select/MultiSURF.py).
+
+Same scikit-learn surface as the reference class (MultiSURF.py:273-489):
+constructor parameters, ``fit`` / ``transform`` / ``fit_transform``, fitted
+attributes ``n_features_in_``, ``feature_importances_``, ``top_features_``,
+``is_discrete_``, ``effective_backend_``.  ``fit`` validates and preprocesses
+exactly as the reference (MultiSURF.py:384-420) and then makes ONE call into
+the native library (``fs_multisurf_score``), which replaces the reference's
+host callers.
+"""
+from __future__ import annotations
+
+import numpy as np
+from sklearn.base import BaseEstimator, TransformerMixin
+from sklearn.utils.validation import check_is_fitted, validate_data
+
+from . import _base, _lib
+
+
+def _compute_ranges(x: np.ndarray) -> np.ndarray:
+    """MultiSURF.py:141-144."""
+    return (x.max(axis=0) - x.min(axis=0)).astype(np.float32)
+
+
+class MultiSURF(TransformerMixin, BaseEstimator):
+    """MI355X-accelerated feature selection with the MultiSURF algorithm.
+
+    Parameters
+    ----------
+    n_features_to_select : int or float, default=0.2
+        Number (int) or fraction (float in (0, 1]) of top features to select.
+    backend : {'auto', 'gpu', 'cpu'}, default='auto'
+        'gpu' runs the HIP kernels on an AMD Instinct GPU (raises RuntimeError
+        when none is visible), 'cpu' the native multithreaded CPU backend,
+        'auto' the GPU when one is visible.
+    use_star : bool, default=False
+        Run MultiSURF* (far misses are subtracted).
+    discrete_limit : int, default=10
+        Features with at most this many distinct values are discrete.
+    n_jobs : int, default=-1
+        CPU threads for backend='cpu' (-1 = all).
+    verbose : bool, default=False
+        Print progress messages.
+    """
+
+    def __init__(
+        self,
+        n_features_to_select: int | float = 0.2,
+        backend: str = "auto",
+        use_star: bool = False,
+        discrete_limit: int = 10,
+        n_jobs: int = -1,
+        verbose: bool = False,
+    ):
+        self.n_features_to_select = n_features_to_select
+        self.backend = backend
+        self.use_star = use_star
+        self.discrete_limit = discrete_limit
+        self.n_jobs = n_jobs
+        self.verbose = verbose
+
+    def _validate_parameters(self, n_samples, n_features):
+        return _base.resolve_n_select("MultiSURF", self.backend, self.n_features_to_select,
+                                      n_samples, n_features)
+
+    def fit(self, x: np.ndarray, y: np.ndarray):
+        """Score every feature with MultiSURF (or MultiSURF*)."""
+        x, y = validate_data(self, x, y, y_numeric=True, dtype=np.float32, ensure_2d=True)
+        self.n_features_in_ = x.shape[1]
+        n_samples = x.shape[0]
+        n_select = self._validate_parameters(n_samples, self.n_features_in_)
+        self.effective_backend_ = _base.effective_backend(self.backend)
+
+        feature_ranges = _compute_ranges(x)
+        feature_ranges[feature_ranges == 0] = 1
+        recip_full = (1.0 / feature_ranges).astype(np.float32)
+        all_feature_indices = np.arange(self.n_features_in_, dtype=np.int64)
+        is_discrete = _base.discrete_mask(x, self.discrete_limit)
+        self.is_discrete_ = is_discrete
+
+        if self.verbose:
+            name = "MultiSURF*" if self.use_star else "MultiSURF"
+            where = "GPU" if self.effective_backend_ == "gpu" else "CPU"
+            print(f"Running {name} on the {where} now...")
+        scores = _lib.multisurf_score(self.effective_backend_, x, y, recip_full,
+                                      all_feature_indices, self.use_star, is_discrete,
+                                      self.n_jobs)
+        self.feature_importances_ = scores
+        self.top_features_ = _base.top_features(scores, n_select)
+        return self
+
+    def transform(self, x: np.ndarray) -> np.ndarray:
+        """Reduce x to the selected features."""
+        check_is_fitted(self)
+        x = validate_data(self, x, reset=False, dtype=[np.float64, np.float32])
+        return x[:, self.top_features_]
+
+    def fit_transform(self, x: np.ndarray, y: np.ndarray) -> np.ndarray:
+        """Fit to data, then transform it."""
+        self.fit(x, y)
+        return self.transform(x)

@@ -1,0 +1,119 @@
+"""ReliefF estimator (reference: src/fast_select/ReliefF.py:239-453).
+
+``fit`` validates and preprocesses exactly as the reference
+(ReliefF.py:343-380: float64 validation, single-class shortcut, neighbour
+warning, discrete detection, class priors, ranges) and then makes one call to
+``fs_relieff_score``, which replaces ``_relieff_{cpu,gpu}_host_caller``.
+"""
+from __future__ import annotations
+
+import warnings
+
+import numpy as np
+from sklearn.base import BaseEstimator, TransformerMixin
+from sklearn.utils.validation import check_is_fitted, validate_data
+
+from . import _base, _lib
+
+
+class ReliefF(TransformerMixin, BaseEstimator):
+    """MI355X-accelerated feature selection with the ReliefF algorithm.
+
+    Parameters
+    ----------
+    n_features_to_select : int or float, default=0.2
+        Number (int) or fraction (float in (0, 1]) of top features to select.
+    discrete_limit : int, default=10
+        Features with at most this many distinct values are discrete.
+    n_neighbors : int, default=3
+        Nearest hits, and nearest misses per other class, used per sample.
+    backend : {'auto', 'gpu', 'cpu'}, default='auto'
+        Compute backend (see ``MultiSURF``).
+    verbose : bool, default=False
+        Print progress messages.
+    n_jobs : int, default=-1
+        CPU threads for backend='cpu' (-1 = all).
+    """
+
+    def __init__(
+        self,
+        n_features_to_select: int | float = 0.2,
+        discrete_limit: int = 10,
+        n_neighbors: int = 3,
+        backend: str = "auto",
+        verbose: bool = False,
+        n_jobs: int = -1,
+    ):
+        self.n_features_to_select = n_features_to_select
+        self.discrete_limit = discrete_limit
+        self.n_neighbors = n_neighbors
+        self.backend = backend
+        self.verbose = verbose
+        self.n_jobs = n_jobs
+
+    def _validate_parameters(self, n_samples, n_features):
+        if self.backend not in ["auto", "gpu", "cpu"]:
+            raise ValueError("backend must be one of 'auto', 'gpu', or 'cpu'")
+        if n_samples < 2:
+            raise ValueError(
+                f"ReliefF requires at least 2 samples, but got n_samples = {n_samples}")
+        if not (0 < self.n_neighbors < n_samples):
+            raise ValueError(
+                f"n_neighbors ({self.n_neighbors}) must be an integer "
+                f"between 1 and n_samples - 1 ({n_samples - 1}).")
+        return _base.n_select_from(self.n_features_to_select, n_features)
+
+    def fit(self, x: np.ndarray, y: np.ndarray):
+        """Score every feature with ReliefF."""
+        x, y = validate_data(self, x, y, dtype=np.float64, ensure_2d=True, y_numeric=True)
+        self.n_features_in_ = x.shape[1]
+        n_samples = x.shape[0]
+        n_select = self._validate_parameters(n_samples, self.n_features_in_)
+
+        self.classes_, y_encoded = np.unique(y, return_inverse=True)
+        if len(self.classes_) < 2:
+            self.feature_importances_ = np.zeros(self.n_features_in_, dtype=np.float32)
+            self.top_features_ = np.arange(n_select)
+            self.effective_backend_ = "cpu" if self.backend != "gpu" else "gpu"
+            return self
+
+        min_class_size = np.min(np.bincount(y_encoded))
+        if self.n_neighbors >= min_class_size:
+            warnings.warn(
+                f"n_neighbors ({self.n_neighbors}) is greater than or equal to the "
+                f"smallest class size ({min_class_size}).",
+                UserWarning,
+            )
+
+        is_discrete = _base.discrete_mask(x, self.discrete_limit)
+        self.is_discrete_ = is_discrete
+        class_labels, class_counts = np.unique(y, return_counts=True)
+        class_probs = class_counts / len(y)
+        y_enc = np.searchsorted(class_labels, y)
+        feature_ranges = x.max(axis=0) - x.min(axis=0)
+        feature_ranges[is_discrete] = 1.0
+        feature_ranges[feature_ranges == 0] = 1.0
+        recip_full = (1.0 / feature_ranges).astype(np.float32)
+
+        self.effective_backend_ = _base.effective_backend(self.backend)
+        if self.verbose:
+            where = "GPU" if self.effective_backend_ == "gpu" else "CPU"
+            print(f"Running ReliefF on the {where} now...")
+        scores = _lib.relieff_score(self.effective_backend_, x.astype(np.float32),
+                                    y_enc.astype(np.int32), recip_full, is_discrete,
+                                    self.n_neighbors, class_probs.astype(np.float32),
+                                    self.n_jobs)
+        self.feature_importances_ = scores
+        self.top_features_ = _base.top_features(scores, n_select)
+        return self
+
+    def transform(self, x: np.ndarray) -> np.ndarray:
+        """Reduce x to the selected features."""
+        check_is_fitted(self)
+        x = validate_data(self, x, reset=False, dtype=[np.float64, np.float32])
+        return x[:, self.top_features_]
+
+    def fit_transform(self, x: np.ndarray, y: np.ndarray) -> np.ndarray:
+        """Fit to data, then transform it."""
+        self.fit(x, y)
+        return self.transform(x)

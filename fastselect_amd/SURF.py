@@ -1,0 +1,98 @@
+"""SURF / SURF* estimator (reference: src/fast_select/SURF.py:220-425).
+
+``fit`` validates and preprocesses exactly as the reference (SURF.py:330-355)
+and makes one call to ``fs_surf_score``, which replaces
+``_surf_{cpu,gpu}_host_caller``.
+"""
+from __future__ import annotations
+
+import numpy as np
+from sklearn.base import BaseEstimator, TransformerMixin
+from sklearn.utils.validation import check_is_fitted, validate_data
+
+from . import _base, _lib
+
+SURF_GPU_MISSING = ("backend='gpu', but no HIP-enabled GPU is available "
+                    "(this build targets AMD MI355X / gfx950).")
+
+
+class SURF(TransformerMixin, BaseEstimator):
+    """MI355X-accelerated feature selection with SURF / SURF*.
+
+    Parameters
+    ----------
+    n_features_to_select : int or float, default=0.2
+        Number (int) or fraction (float in (0, 1]) of top features to select.
+    backend : {'auto', 'gpu', 'cpu'}, default='auto'
+        Compute backend (see ``MultiSURF``).
+    use_star : bool, default=False
+        Run SURF* (far hits add, far misses subtract).
+    discrete_limit : int, default=10
+        Features with at most this many distinct values are discrete.
+    n_jobs : int, default=-1
+        CPU threads for backend='cpu' (-1 = all).
+    verbose : bool, default=False
+        Print progress messages.
+    """
+
+    def __init__(
+        self,
+        n_features_to_select: int | float = 0.2,
+        backend: str = "auto",
+        use_star: bool = False,
+        discrete_limit: int = 10,
+        n_jobs: int = -1,
+        verbose: bool = False,
+    ):
+        self.n_features_to_select = n_features_to_select
+        self.backend = backend
+        self.use_star = use_star
+        self.discrete_limit = discrete_limit
+        self.n_jobs = n_jobs
+        self.verbose = verbose
+
+    def _validate_parameters(self, n_samples, n_features):
+        return _base.resolve_n_select("SURF", self.backend, self.n_features_to_select,
+                                      n_samples, n_features)
+
+    def fit(self, X: np.ndarray, y: np.ndarray):
+        """Score every feature with SURF (or SURF*)."""
+        X, y = validate_data(self, X, y, y_numeric=True, dtype=np.float64, ensure_2d=True)
+        self.n_features_in_ = X.shape[1]
+        n_samples = X.shape[0]
+        n_select = self._validate_parameters(n_samples, self.n_features_in_)
+
+        if self.backend == "auto":
+            self.effective_backend_ = "gpu" if _lib.gpu_available() else "cpu"
+        elif self.backend == "gpu" and not _lib.gpu_available():
+            raise RuntimeError(SURF_GPU_MISSING)
+        else:
+            self.effective_backend_ = self.backend
+
+        self.is_discrete_ = _base.discrete_mask(X, self.discrete_limit)
+        feature_ranges = X.max(axis=0) - X.min(axis=0)
+        feature_ranges[self.is_discrete_] = 1.0
+        feature_ranges[feature_ranges == 0] = 1.0
+        recip_full = (1.0 / feature_ranges).astype(np.float32)
+
+        algo_name = "SURF*" if self.use_star else "SURF"
+        if self.verbose:
+            print(f"Running {algo_name} on the {self.effective_backend_.upper()} now...")
+        scores = _lib.surf_score(self.effective_backend_, X, y.astype(np.int32), recip_full,
+                                 self.use_star, self.is_discrete_, self.n_jobs)
+        self.feature_importances_ = scores
+        self.top_features_ = _base.top_features(scores, n_select)
+        if self.verbose:
+            print("Feature scoring completed.")
+        return self
+
+    def transform(self, x: np.ndarray) -> np.ndarray:
+        """Reduce x to the selected features."""
+        check_is_fitted(self)
+        x = validate_data(self, x, reset=False, dtype=[np.float64, np.float32])
+        return x[:, self.top_features_]
+
+    def fit_transform(self, X: np.ndarray, y: np.ndarray) -> np.ndarray:
+        """Fit to data, then transform it."""
+        self.fit(X, y)
+        return self.transform(X)

@@ -1,0 +1,60 @@
+"""Shared pieces of the Relief estimators (parameter checks, backend choice,
+feature preprocessing), restating the reference's per-estimator code:
+``_validate_parameters`` (MultiSURF.py:337-366, ReliefF.py:299-335,
+SURF.py:283-312) and the ``backend`` dispatch in each ``fit``.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+
+GPU_MISSING = ("backend='gpu' was selected, but no compatible GPU was found "
+               "(no HIP device is visible; this build targets AMD MI355X / gfx950).")
+
+
+def resolve_n_select(name: str, backend: str, n_features_to_select, n_samples: int,
+                     n_features: int) -> int:
+    """Backend name, sample count and ``n_features_to_select`` checks."""
+    if backend not in ["auto", "gpu", "cpu"]:
+        raise ValueError("backend must be one of 'auto', 'gpu', or 'cpu'")
+    if n_samples < 2:
+        raise ValueError(f"{name} requires at least 2 samples, but got n_samples = {n_samples}")
+    return n_select_from(n_features_to_select, n_features)
+
+
+def n_select_from(n_features_to_select, n_features: int) -> int:
+    if isinstance(n_features_to_select, float):
+        if not 0.0 < n_features_to_select <= 1.0:
+            raise ValueError("If n_features_to_select is a float, it must be in (0, 1].")
+        return max(1, int(n_features_to_select * n_features))
+    if isinstance(n_features_to_select, int):
+        if not 0 < n_features_to_select <= n_features:
+            raise ValueError(
+                f"If n_features_to_select is an int ({n_features_to_select}), "
+                f"it must be > 0 and <= n_features ({n_features}).")
+        return int(n_features_to_select)
+    raise TypeError("n_features_to_select must be an int or a float.")
+
+
+def effective_backend(backend: str) -> str:
+    """'auto' -> 'gpu' when a HIP device is visible, else 'cpu'.  An explicit
+    'gpu' without a device raises instead of falling back."""
+    if backend == "auto":
+        return "gpu" if _lib.gpu_available() else "cpu"
+    if backend == "gpu" and not _lib.gpu_available():
+        raise RuntimeError(GPU_MISSING)
+    return backend
+
+
+def discrete_mask(x: np.ndarray, discrete_limit: int) -> np.ndarray:
+    """``np.unique(x[:, f]).size <= discrete_limit`` per column
+    (MultiSURF.py:416-420, ReliefF.py:366-368, SURF.py:347-350)."""
+    return np.array([np.unique(x[:, f]).size <= discrete_limit for f in range(x.shape[1])],
+                    dtype=bool)
+
+
+def top_features(scores: np.ndarray, n_select: int) -> np.ndarray:
+    """``np.argsort(scores)[::-1][:n_select]`` (MultiSURF.py:443): numpy's own
+    argsort on the float32 scores, so ties order exactly as the reference."""
+    return np.argsort(scores)[::-1][:n_select]

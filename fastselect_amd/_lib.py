@@ -1,0 +1,219 @@
+"""ctypes binding of ``libfastselect_amd.so`` (C ABI: ``include/fastselect_amd.h``).
+
+The shared library holds both the hand-written HIP kernels (gfx950) and the
+native CPU backend.  It is loaded eagerly when the package is imported: if it
+is missing, importing ``fastselect_amd`` fails loudly -- there is no Python or
+PyTorch fallback for the scoring path.
+
+Each ``*_score`` function here replaces one reference host caller
+(``_multisurf_{cpu,gpu}_host_caller`` MultiSURF.py:147-162/256-270,
+``_relieff_{cpu,gpu}_host_caller`` ReliefF.py:127-134/222-236,
+``_surf_{cpu,gpu}_host_caller`` SURF.py:117-128/198-218): plain numpy arrays
+in, float32 scores already divided by n out.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfastselect_amd.so")
+
+FS_OK, FS_EINVAL, FS_ENODEV, FS_EOOM, FS_EHIP, FS_ENOTSUP = 0, -1, -2, -3, -4, -5
+BACKEND_CPU, BACKEND_GPU = 0, 1
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_f64p = ctypes.POINTER(ctypes.c_double)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+_vp = ctypes.c_void_p
+
+# every symbol include/fastselect_amd.h declares (checked by tests/test_abi.py)
+EXPORTED = (
+    "fs_version", "fs_last_error", "fs_device_count", "fs_multisurf_score", "fs_relieff_score",
+    "fs_surf_score", "fs_plan_create", "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2",
+    "fs_plan_info", "fs_plan_kernel_ms", "fs_plan_destroy",
+)
+
+
+def _load() -> ctypes.CDLL:
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"fastselect_amd native library not found at {LIB_PATH}; build it with "
+            "`make -C fastselect_amd/csrc` (or __graft_entry__.build()).")
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.fs_version.restype = ctypes.c_char_p
+    lib.fs_last_error.restype = ctypes.c_char_p
+    lib.fs_device_count.restype = _int
+    lib.fs_multisurf_score.argtypes = [_int, _int, _f32p, _i64, _i64, _f64p, _f32p, _i64p, _i64,
+                                       _int, _u8p, _int, _f32p]
+    lib.fs_relieff_score.argtypes = [_int, _int, _f32p, _i64, _i64, _i32p, _f32p, _u8p, _i64,
+                                     _f32p, _i64, _int, _f32p]
+    lib.fs_surf_score.argtypes = [_int, _int, _f64p, _i64, _i64, _i32p, _f32p, _int, _u8p, _int,
+                                  _f32p]
+    lib.fs_plan_create.argtypes = [ctypes.POINTER(_vp), _int, _int, _f32p, _i64, _i64, _f64p,
+                                   _f32p, _i64p, _i64, _int, _u8p, _int, _int, _int,
+                                   ctypes.c_uint64]
+    lib.fs_plan_pass1.argtypes = [_vp, _vp]
+    lib.fs_plan_select.argtypes = [_vp, _vp, _vp]
+    lib.fs_plan_pass2.argtypes = [_vp, _vp, _vp]
+    lib.fs_plan_info.argtypes = [_vp, _i64p, _f64p]
+    lib.fs_plan_kernel_ms.argtypes = [_vp, _int]
+    lib.fs_plan_kernel_ms.restype = ctypes.c_double
+    lib.fs_plan_destroy.argtypes = [_vp]
+    for name in ("fs_multisurf_score", "fs_relieff_score", "fs_surf_score", "fs_plan_create",
+                 "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_info",
+                 "fs_plan_destroy"):
+        getattr(lib, name).restype = _int
+    return lib
+
+
+_lib = _load()
+
+
+def lib() -> ctypes.CDLL:
+    return _lib
+
+
+def version() -> str:
+    return _lib.fs_version().decode()
+
+
+def device_count() -> int:
+    """Number of visible HIP devices (0 when none)."""
+    return int(_lib.fs_device_count())
+
+
+def gpu_available() -> bool:
+    return device_count() > 0
+
+
+def check(rc: int) -> None:
+    """Map a C return code to the Python exception the estimators raise."""
+    if rc == FS_OK:
+        return
+    msg = _lib.fs_last_error().decode(errors="replace")
+    if rc == FS_EINVAL:
+        raise ValueError(msg)
+    if rc == FS_EOOM:
+        raise MemoryError(msg)
+    raise RuntimeError(msg)
+
+
+def _p(a: np.ndarray, t):
+    return a.ctypes.data_as(t)
+
+
+def _backend_code(backend: str) -> int:
+    if backend == "gpu":
+        return BACKEND_GPU
+    if backend == "cpu":
+        return BACKEND_CPU
+    raise ValueError("backend must be 'cpu' or 'gpu' at the native boundary")
+
+
+def multisurf_score(backend, x, y, recip, feat_idx, use_star, is_discrete, n_jobs=-1, device=0):
+    """Drop-in for ``_multisurf_{cpu,gpu}_host_caller`` (MultiSURF.py:147-162, 256-270)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    n, p = x.shape
+    yv = np.ascontiguousarray(y, dtype=np.float64)
+    rc_ = np.ascontiguousarray(recip, dtype=np.float32)
+    isd = np.ascontiguousarray(is_discrete, dtype=np.uint8)
+    fidx = None if feat_idx is None else np.ascontiguousarray(feat_idx, dtype=np.int64)
+    n_kept = p if fidx is None else fidx.size
+    out = np.zeros(n_kept, dtype=np.float32)
+    check(_lib.fs_multisurf_score(_backend_code(backend), int(device), _p(x, _f32p), n, p,
+                                  _p(yv, _f64p), _p(rc_, _f32p),
+                                  None if fidx is None else _p(fidx, _i64p), n_kept,
+                                  int(bool(use_star)), _p(isd, _u8p), int(n_jobs),
+                                  _p(out, _f32p)))
+    return out
+
+
+def relieff_score(backend, x, y_enc, recip, is_discrete, k, class_probs, n_jobs=-1, device=0):
+    """Drop-in for ``_relieff_{cpu,gpu}_host_caller`` (ReliefF.py:127-134, 222-236)."""
+    x = np.ascontiguousarray(x, dtype=np.float32)
+    n, p = x.shape
+    ye = np.ascontiguousarray(y_enc, dtype=np.int32)
+    rc_ = np.ascontiguousarray(recip, dtype=np.float32)
+    isd = np.ascontiguousarray(is_discrete, dtype=np.uint8)
+    cp = np.ascontiguousarray(class_probs, dtype=np.float32)
+    out = np.zeros(p, dtype=np.float32)
+    check(_lib.fs_relieff_score(_backend_code(backend), int(device), _p(x, _f32p), n, p,
+                                _p(ye, _i32p), _p(rc_, _f32p), _p(isd, _u8p), int(k),
+                                _p(cp, _f32p), cp.size, int(n_jobs), _p(out, _f32p)))
+    return out
+
+
+def surf_score(backend, x, y, recip, use_star, is_discrete, n_jobs=-1, device=0):
+    """Drop-in for ``_surf_{cpu,gpu}_host_caller`` (SURF.py:117-128, 198-218)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    n, p = x.shape
+    yi = np.ascontiguousarray(y, dtype=np.int32)
+    rc_ = np.ascontiguousarray(recip, dtype=np.float32)
+    isd = np.ascontiguousarray(is_discrete, dtype=np.uint8)
+    out = np.zeros(p, dtype=np.float32)
+    check(_lib.fs_surf_score(_backend_code(backend), int(device), _p(x, _f64p), n, p,
+                             _p(yi, _i32p), _p(rc_, _f32p), int(bool(use_star)), _p(isd, _u8p),
+                             int(n_jobs), _p(out, _f32p)))
+    return out
+
+
+class Plan:
+    """A sharded MultiSURF plan (``fs_plan_*``) for one rank.
+
+    Exchange buffers (rowstats[2n], counts[2n], scores[n_kept], float64) are
+    passed by address: device pointers for the GPU backend, host pointers for
+    the CPU backend (see ``fastselect_amd.parallel``).
+    """
+
+    def __init__(self, backend, x, y, recip, is_discrete, use_star=False, feat_idx=None,
+                 rank=0, world=1, n_jobs=-1, device=0, stream=0):
+        x = np.ascontiguousarray(x, dtype=np.float32)
+        self.n, self.p = x.shape
+        yv = np.ascontiguousarray(y, dtype=np.float64)
+        rc_ = np.ascontiguousarray(recip, dtype=np.float32)
+        isd = np.ascontiguousarray(is_discrete, dtype=np.uint8)
+        fidx = None if feat_idx is None else np.ascontiguousarray(feat_idx, dtype=np.int64)
+        self.n_kept = self.p if fidx is None else fidx.size
+        self.backend = backend
+        self._h = _vp()
+        check(_lib.fs_plan_create(ctypes.byref(self._h), _backend_code(backend), int(device),
+                                  _p(x, _f32p), self.n, self.p, _p(yv, _f64p), _p(rc_, _f32p),
+                                  None if fidx is None else _p(fidx, _i64p), self.n_kept,
+                                  int(bool(use_star)), _p(isd, _u8p), int(rank), int(world),
+                                  int(n_jobs), ctypes.c_uint64(int(stream))))
+
+    def pass1(self, rowstats_ptr: int) -> None:
+        check(_lib.fs_plan_pass1(self._h, _vp(rowstats_ptr)))
+
+    def select(self, rowstats_ptr: int, counts_ptr: int) -> None:
+        check(_lib.fs_plan_select(self._h, _vp(rowstats_ptr), _vp(counts_ptr)))
+
+    def pass2(self, counts_ptr: int, scores_ptr: int) -> None:
+        check(_lib.fs_plan_pass2(self._h, _vp(counts_ptr), _vp(scores_ptr)))
+
+    def info(self):
+        tiles = ctypes.c_int64(0)
+        pfe = ctypes.c_double(0.0)
+        check(_lib.fs_plan_info(self._h, ctypes.byref(tiles), ctypes.byref(pfe)))
+        return int(tiles.value), float(pfe.value)
+
+    def kernel_ms(self, which: int) -> float:
+        return float(_lib.fs_plan_kernel_ms(self._h, int(which)))
+
+    def close(self) -> None:
+        if self._h:
+            _lib.fs_plan_destroy(self._h)
+            self._h = _vp()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

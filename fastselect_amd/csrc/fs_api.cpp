@@ -1,0 +1,236 @@
+// fs_api.cpp -- the C ABI (include/fastselect_amd.h): argument validation,
+// backend dispatch, error reporting.  See the header for the reference
+// interface each entry point replaces.
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/fastselect_amd.h"
+#include "fs_internal.h"
+
+namespace fs {
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+}  // namespace fs
+
+using namespace fs;
+
+static int map_prep_rc(int rc) { return rc == 0 ? FS_OK : FS_EINVAL; }
+
+static int check_backend(int backend, int device) {
+  if (backend != FS_BACKEND_CPU && backend != FS_BACKEND_GPU) {
+    set_error("backend must be FS_BACKEND_CPU or FS_BACKEND_GPU");
+    return FS_EINVAL;
+  }
+  if (backend == FS_BACKEND_GPU) {
+    const int nd = gpu::device_count();
+    if (nd <= 0) {
+      set_error("backend='gpu' was selected, but no HIP device (MI355X) is visible");
+      return FS_ENODEV;
+    }
+    if (device < 0 || device >= nd) {
+      set_error("device ordinal out of range");
+      return FS_EINVAL;
+    }
+  }
+  return FS_OK;
+}
+
+extern "C" {
+
+const char* fs_version(void) { return "fastselect_amd 0.1.0 (gfx950)"; }
+
+const char* fs_last_error(void) { return g_last_error.c_str(); }
+
+int fs_device_count(void) { return gpu::device_count(); }
+
+int fs_multisurf_score(int backend, int device, const float* x, int64_t n, int64_t p,
+                       const double* y, const float* recip, const int64_t* feat_idx,
+                       int64_t n_kept, int use_star, const uint8_t* is_discrete, int n_jobs,
+                       float* scores_out) {
+  if (!scores_out) {
+    set_error("scores_out is NULL");
+    return FS_EINVAL;
+  }
+  int rc = check_backend(backend, device);
+  if (rc != FS_OK) return rc;
+  Prepared P;
+  rc = prepare(P, ALGO_MULTISURF, x, 0, n, p, feat_idx, n_kept, recip, is_discrete, n_jobs);
+  if (rc) return map_prep_rc(rc);
+  if (encode_labels_f64(P, y)) return FS_EINVAL;
+  P.use_star = use_star ? 1 : 0;
+  if (backend == FS_BACKEND_GPU) return gpu::multisurf_run(P, x, device, scores_out);
+  std::vector<uint64_t> D;
+  std::vector<float> xs;
+  std::vector<double> rs(2 * n), cnt(2 * n), thr, S(P.n_kept);
+  cpu::multisurf_pass1(P, x, 0, 0, 1, n_jobs, D, xs, rs.data());
+  cpu::multisurf_select(P, D, 0, 1, rs.data(), thr, cnt.data(), n_jobs);
+  cpu::multisurf_pass2(P, D, xs, thr, cnt.data(), 0, 1, n_jobs, S.data());
+  for (int64_t k = 0; k < P.n_kept; k++) scores_out[k] = (float)(S[k] / (double)n);
+  return FS_OK;
+}
+
+int fs_relieff_score(int backend, int device, const float* x, int64_t n, int64_t p,
+                     const int32_t* y_enc, const float* recip, const uint8_t* is_discrete,
+                     int64_t k, const float* class_probs, int64_t n_classes, int n_jobs,
+                     float* scores_out) {
+  if (!scores_out || !y_enc || !class_probs || n_classes < 1 || k < 0) {
+    set_error("invalid ReliefF arguments (scores_out, y_enc, class_probs, n_classes, k)");
+    return FS_EINVAL;
+  }
+  int rc = check_backend(backend, device);
+  if (rc != FS_OK) return rc;
+  Prepared P;
+  rc = prepare(P, ALGO_RELIEFF, x, 0, n, p, nullptr, p, recip, is_discrete, n_jobs);
+  if (rc) return map_prep_rc(rc);
+  P.labels.assign(y_enc, y_enc + n);
+  for (int64_t i = 0; i < n; i++)
+    if (P.labels[i] < 0 || P.labels[i] >= n_classes) {
+      set_error("y_enc entry outside [0, n_classes)");
+      return FS_EINVAL;
+    }
+  P.n_classes = (int32_t)n_classes;
+  P.class_prior.assign(n_classes, 0.0);
+  for (int64_t c = 0; c < n_classes; c++) P.class_prior[c] = (double)class_probs[c];
+  P.k_neighbors = k;
+  if (backend == FS_BACKEND_GPU) return gpu::relieff_run(P, x, device, scores_out);
+  std::vector<double> S(P.n_kept);
+  cpu::relieff_run(P, x, n_jobs, S.data());
+  for (int64_t f = 0; f < P.n_kept; f++) scores_out[f] = (float)(S[f] / (double)n);
+  return FS_OK;
+}
+
+int fs_surf_score(int backend, int device, const double* x, int64_t n, int64_t p,
+                  const int32_t* y, const float* recip, int use_star,
+                  const uint8_t* is_discrete, int n_jobs, float* scores_out) {
+  if (!scores_out) {
+    set_error("scores_out is NULL");
+    return FS_EINVAL;
+  }
+  int rc = check_backend(backend, device);
+  if (rc != FS_OK) return rc;
+  Prepared P;
+  rc = prepare(P, ALGO_SURF, x, 1, n, p, nullptr, p, recip, is_discrete, n_jobs);
+  if (rc) return map_prep_rc(rc);
+  if (encode_labels_i32(P, y)) return FS_EINVAL;
+  P.use_star = use_star ? 1 : 0;
+  if (backend == FS_BACKEND_GPU) return gpu::surf_run(P, x, device, scores_out);
+  std::vector<double> S(P.n_kept);
+  cpu::surf_run(P, x, n_jobs, S.data());
+  for (int64_t f = 0; f < P.n_kept; f++) scores_out[f] = (float)(S[f] / (double)n);
+  return FS_OK;
+}
+
+}  // extern "C"
+
+// ---- sharded MultiSURF plan ------------------------------------------------
+
+struct fs_plan {
+  int backend = FS_BACKEND_CPU;
+  int rank = 0, world = 1, n_jobs = -1;
+  Prepared P;
+  gpu::Plan* g = nullptr;
+  // CPU state
+  std::vector<float> x;
+  std::vector<uint64_t> D;
+  std::vector<float> xs;
+  std::vector<double> thr;
+};
+
+extern "C" {
+
+int fs_plan_create(fs_plan** plan_out, int backend, int device, const float* x, int64_t n,
+                   int64_t p, const double* y, const float* recip, const int64_t* feat_idx,
+                   int64_t n_kept, int use_star, const uint8_t* is_discrete, int rank, int world,
+                   int n_jobs, uint64_t stream) {
+  if (!plan_out) {
+    set_error("plan_out is NULL");
+    return FS_EINVAL;
+  }
+  *plan_out = nullptr;
+  if (world < 1 || rank < 0 || rank >= world) {
+    set_error("invalid rank/world");
+    return FS_EINVAL;
+  }
+  int rc = check_backend(backend, device);
+  if (rc != FS_OK) return rc;
+  fs_plan* pl = new fs_plan();
+  pl->backend = backend;
+  pl->rank = rank;
+  pl->world = world;
+  pl->n_jobs = n_jobs;
+  rc = prepare(pl->P, ALGO_MULTISURF, x, 0, n, p, feat_idx, n_kept, recip, is_discrete, n_jobs);
+  if (rc || encode_labels_f64(pl->P, y)) {
+    delete pl;
+    return FS_EINVAL;
+  }
+  pl->P.use_star = use_star ? 1 : 0;
+  if (backend == FS_BACKEND_GPU) {
+    rc = gpu::plan_create(&pl->g, pl->P, x, 0, device, rank, world, stream);
+    if (rc != FS_OK) {
+      delete pl;
+      return rc;
+    }
+  } else {
+    pl->x.assign(x, x + (size_t)n * p);
+  }
+  *plan_out = pl;
+  return FS_OK;
+}
+
+int fs_plan_pass1(fs_plan* pl, double* rowstats) {
+  if (!pl || !rowstats) {
+    set_error("NULL plan or buffer");
+    return FS_EINVAL;
+  }
+  if (pl->g) return gpu::plan_pass1(pl->g, rowstats);
+  return cpu::multisurf_pass1(pl->P, pl->x.data(), 0, pl->rank, pl->world, pl->n_jobs, pl->D,
+                              pl->xs, rowstats);
+}
+
+int fs_plan_select(fs_plan* pl, const double* rowstats, double* counts) {
+  if (!pl || !rowstats || !counts) {
+    set_error("NULL plan or buffer");
+    return FS_EINVAL;
+  }
+  if (pl->g) return gpu::plan_select(pl->g, rowstats, counts);
+  return cpu::multisurf_select(pl->P, pl->D, pl->rank, pl->world, rowstats, pl->thr, counts,
+                               pl->n_jobs);
+}
+
+int fs_plan_pass2(fs_plan* pl, const double* counts, double* scores) {
+  if (!pl || !counts || !scores) {
+    set_error("NULL plan or buffer");
+    return FS_EINVAL;
+  }
+  if (pl->g) return gpu::plan_pass2(pl->g, counts, scores);
+  return cpu::multisurf_pass2(pl->P, pl->D, pl->xs, pl->thr, counts, pl->rank, pl->world,
+                              pl->n_jobs, scores);
+}
+
+int fs_plan_info(const fs_plan* pl, int64_t* owned_tiles_out, double* pfe) {
+  if (!pl) {
+    set_error("NULL plan");
+    return FS_EINVAL;
+  }
+  if (pl->g) return gpu::plan_info(pl->g, owned_tiles_out, pfe);
+  std::vector<int32_t> bi, bj;
+  owned_tiles(pl->P.n_pad / kTile, pl->rank, pl->world, bi, bj);
+  if (owned_tiles_out) *owned_tiles_out = (int64_t)bi.size();
+  if (pfe) *pfe = 2.0 * (double)bi.size() * kTile * kTile * (double)(pl->P.pc + pl->P.pd);
+  return FS_OK;
+}
+
+double fs_plan_kernel_ms(const fs_plan* pl, int which) {
+  if (!pl || !pl->g) return -1.0;
+  return gpu::plan_kernel_ms(pl->g, which);
+}
+
+int fs_plan_destroy(fs_plan* pl) {
+  if (!pl) return FS_OK;
+  if (pl->g) gpu::plan_destroy(pl->g);
+  delete pl;
+  return FS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,962 @@
+// fs_gpu.hip -- hand-written HIP kernels for gfx950 (MI355X / CDNA4) and the
+// GPU backend of the Relief scoring pipeline (see fs_internal.h).
+//
+// Kernel map (DESIGN.md §3 for rooflines and bytes per unit):
+//   k_quantize      X (row-major) -> xqT (u32, feature-major) + xs (f32,
+//                   row-major), 64x64 LDS transpose.                 HBM-bound
+//   k_dist          pass 1: one 128x128 upper-triangle pair tile per
+//                   workgroup, 8x8 pairs per lane, v_sad_u32 over LDS
+//                   panels staged with global_load_lds (double-buffered),
+//                   exact integer distances.                         VALU-bound
+//   k_rowstats      per-row sum D, sum D^2 over owned tiles.         HBM-bound
+//   k_select_ms     MultiSURF thresholds + near hit / miss counts.   HBM-bound
+//   k_surf_avg      SURF float32 sequential row mean (SURF.py:162).  HBM-bound
+//   k_weights       symmetric pair weights w_ij = W_ij + W_ji per tile.
+//   k_score         pass 2: lanes = features, a 32-row sub-tile of x in
+//                   VGPRs, pair weights in SGPRs (scalar loads),
+//                   acc += w * |a - b| (v_sub_f32 + v_fma_f32 |.|). VALU-bound
+//   k_reduce        deterministic segment sum of pass-2 partials.
+//   k_rf_select     ReliefF: per-row radix select of the k nearest per class.
+//   k_rf_update     ReliefF: neighbour-gather update.
+//
+// No float atomics touch scores: every reduction has a fixed order, so two
+// runs of the same input are bit-identical.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/fastselect_amd.h"
+#include "fs_internal.h"
+
+namespace fs {
+namespace gpu {
+
+#define FS_HIP(expr)                                                                      \
+  do {                                                                                    \
+    hipError_t e_ = (expr);                                                               \
+    if (e_ != hipSuccess) {                                                               \
+      set_error(std::string("HIP error '") + hipGetErrorString(e_) + "' in " #expr);      \
+      return FS_EHIP;                                                                     \
+    }                                                                                     \
+  } while (0)
+
+int device_count() {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return c < 0 ? 0 : c;
+}
+
+// ---------------------------------------------------------------------------
+// Device helpers
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_sad_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+// c + sc * [a != b] for small category codes, without lane masks (a
+// compare would burn an SGPR pair per pair-accumulator).
+__device__ __forceinline__ uint32_t mismatch_u32(uint32_t a, uint32_t b, uint32_t sc, uint32_t c) {
+  uint32_t t, d;
+  asm("v_xor_b32 %1, %2, %3\n\tv_min_u32 %1, %1, 1\n\tv_mad_u32_u24 %0, %1, %4, %5"
+      : "=v"(d), "=&v"(t)
+      : "v"(a), "v"(b), "v"(sc), "v"(c));
+  return d;
+}
+
+__device__ __forceinline__ bool tile_owned(int64_t nb, int64_t bi, int64_t bj, int rank,
+                                           int world) {
+  if (world == 1) return true;
+  const int64_t a = bi < bj ? bi : bj, b = bi < bj ? bj : bi;
+  return tile_linear(nb, a, b) % world == rank;
+}
+
+// Fixed-shape block reduction of doubles (256 threads), deterministic.
+__device__ __forceinline__ double block_sum_256(double v, double* red) {
+  const int tid = threadIdx.x;
+  red[tid] = v;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (tid < s) red[tid] += red[tid + s];
+    __syncthreads();
+  }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// Quantize: X -> xqT (u32, [PW][n_pad]) and xs (f32, [n_pad][PW])
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void k_quantize(
+    const T* __restrict__ x, int64_t n, int64_t n_pad, int64_t p_in, int64_t PW, int64_t pc,
+    int64_t PC, int64_t pd, const int64_t* __restrict__ src_col, const double* __restrict__ off,
+    const double* __restrict__ qs, const double* __restrict__ scl,
+    const int64_t* __restrict__ dtab_off, const double* __restrict__ dtab,
+    uint32_t* __restrict__ xqT, float* __restrict__ xs) {
+  __shared__ uint32_t tile[64][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * 64, i0 = (int64_t)blockIdx.y * 64;
+  const int64_t c = c0 + tx;
+  const int64_t col = src_col[c];
+  const bool is_cont = c < pc;
+  for (int r = ty; r < 64; r += 4) {
+    const int64_t i = i0 + r;
+    uint32_t q = 0;
+    float v = 0.0f;
+    if (i < n && col >= 0) {
+      const double xv = (double)x[i * p_in + col];
+      if (is_cont) {
+        const double u = __dadd_rn(xv, -off[c]);
+        q = (uint32_t)__dadd_rn(__dmul_rn(u, qs[c]), 0.5);
+        v = (float)__dmul_rn(u, scl[c]);
+      } else {
+        int64_t lo = dtab_off[c], hi = dtab_off[c + 1] - 1;
+        while (lo < hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (dtab[mid] < xv) lo = mid + 1;
+          else hi = mid;
+        }
+        q = (uint32_t)(lo - dtab_off[c]);
+        v = (float)q;
+      }
+    }
+    xs[i * PW + c] = v;
+    tile[r][tx] = q;
+  }
+  (void)PC;
+  (void)pd;
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) xqT[(c0 + r) * n_pad + i0 + tx] = tile[tx][r];
+}
+
+// ---------------------------------------------------------------------------
+// Pass 1: exact integer distance tiles
+// ---------------------------------------------------------------------------
+// Workgroup = 256 lanes = one 128x128 tile (bi <= bj).  Lane (tx, ty) owns
+// rows {ty*4 + r, 64 + ty*4 + r} x cols {tx*4 + c, 64 + tx*4 + c} (8x8).
+// Per 16-feature chunk the A panel (rows) and B panel (cols) of xqT, each
+// 16 x 128 u32 = 8 KB, are copied global -> LDS by global_load_lds_dwordx4
+// (each wave moves 2 x 1 KB of A and of B), double-buffered: chunk c+1 is in
+// flight while chunk c is consumed.  u32 accumulators absorb 256 features,
+// then their bits >= 24 move into 16-bit halves of a packed high word, so the
+// final distance D = hi * 2^24 + lo is exact below 2^40.
+// One 16-feature chunk of SADs (continuous) or mismatch counts (discrete)
+// from an LDS panel pair.
+template <bool DISC>
+__device__ __forceinline__ void dist_chunk(const uint32_t* __restrict__ A,
+                                           const uint32_t* __restrict__ B, int tx, int ty,
+                                           uint32_t sc_disc, uint32_t (&acc)[8][8]) {
+#pragma unroll 2
+  for (int k = 0; k < kBK; k++) {
+    const uint4 a0 = *(const uint4*)&A[k * kTile + ty * 4];
+    const uint4 a1 = *(const uint4*)&A[k * kTile + 64 + ty * 4];
+    const uint4 b0 = *(const uint4*)&B[k * kTile + tx * 4];
+    const uint4 b1 = *(const uint4*)&B[k * kTile + 64 + tx * 4];
+    const uint32_t av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const uint32_t bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+#pragma unroll
+      for (int c = 0; c < 8; c++)
+        acc[r][c] = DISC ? mismatch_u32(av[r], bv[c], sc_disc, acc[r][c])
+                         : sad_u32(av[r], bv[c], acc[r][c]);
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void k_dist(const uint32_t* __restrict__ xqT, int64_t n_pad,
+                                                 int nck_cont, int nck_disc, uint32_t sc_disc,
+                                                 const int2* __restrict__ tiles,
+                                                 double* __restrict__ D) {
+  // Two distinct LDS objects (not one indexed array) so the compiler can
+  // prove a pending global_load_lds into one buffer does not alias the
+  // ds_reads of the other and keeps the copy in flight across the compute.
+  __shared__ __attribute__((aligned(16))) uint32_t ldsA0[kBK * kTile], ldsB0[kBK * kTile];
+  __shared__ __attribute__((aligned(16))) uint32_t ldsA1[kBK * kTile], ldsB1[kBK * kTile];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int2 tl = tiles[blockIdx.x];
+  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  const int tx = tid & 15, ty = tid >> 4;
+
+  uint32_t acc[8][8];
+  uint32_t hi[8][4];
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+#pragma unroll
+    for (int c = 0; c < 8; c++) acc[r][c] = 0;
+#pragma unroll
+    for (int c = 0; c < 4; c++) hi[r][c] = 0;
+  }
+
+  // glds lane mapping: instruction s of wave w moves k-rows 2*(2w+s) and
+  // 2*(2w+s)+1; lane l -> k-row offset l/32, 4 u32 at column (l%32)*4.
+  const int krow_l = lane >> 5, col_l = (lane & 31) * 4;
+  auto stage = [&](uint32_t* la_base, uint32_t* lb_base, int ck) {
+    const int64_t k0 = (int64_t)ck * kBK;
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const int ins = wave * 2 + s;
+      const int64_t krow = k0 + ins * 2 + krow_l;
+      const uint32_t* ga = xqT + krow * n_pad + i0 + col_l;
+      const uint32_t* gb = xqT + krow * n_pad + j0 + col_l;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ga,
+                                       (__attribute__((address_space(3))) void*)(la_base + ins * 2 * kTile),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gb,
+                                       (__attribute__((address_space(3))) void*)(lb_base + ins * 2 * kTile),
+                                       16, 0, 0);
+    }
+  };
+
+  auto flush = [&]() {
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+#pragma unroll
+      for (int c = 0; c < 8; c++) {
+        const uint32_t top = acc[r][c] >> kHiShift;
+        acc[r][c] &= (1u << kHiShift) - 1u;
+        hi[r][c >> 1] += (c & 1) ? (top << 16) : top;
+      }
+  };
+
+  // chunk ck lives in buffer ck & 1; chunk ck+1 is copied while ck is consumed
+  auto step = [&](const uint32_t* A, const uint32_t* B, uint32_t* nA, uint32_t* nB, int ck,
+                  int nck) {
+    if (ck + 1 < nck) stage(nA, nB, ck + 1);
+    if (ck < nck_cont) dist_chunk<false>(A, B, tx, ty, sc_disc, acc);
+    else dist_chunk<true>(A, B, tx, ty, sc_disc, acc);
+    if ((ck % kFlushChunks) == kFlushChunks - 1) flush();
+    __syncthreads();
+  };
+
+  const int nck = nck_cont + nck_disc;
+  stage(ldsA0, ldsB0, 0);
+  __syncthreads();
+  for (int ck = 0; ck < nck; ck += 2) {
+    step(ldsA0, ldsB0, ldsA1, ldsB1, ck, nck);
+    if (ck + 1 < nck) step(ldsA1, ldsB1, ldsA0, ldsB0, ck + 1, nck);
+  }
+  flush();
+
+  // Epilogue: D[i][j] for the tile and, off the diagonal, the mirror D[j][i].
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const int64_t i = i0 + ty * 4 + (r & 3) + (r >> 2) * 64;
+    double v[8];
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const uint64_t h = (hi[r][c >> 1] >> ((c & 1) * 16)) & 0xFFFFu;
+      v[c] = (double)((h << kHiShift) + acc[r][c]);
+    }
+    double* row = D + i * n_pad + j0 + tx * 4;
+    *(double2*)(row + 0) = make_double2(v[0], v[1]);
+    *(double2*)(row + 2) = make_double2(v[2], v[3]);
+    *(double2*)(row + 64) = make_double2(v[4], v[5]);
+    *(double2*)(row + 66) = make_double2(v[6], v[7]);
+  }
+  if (tl.x != tl.y) {
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const int64_t j = j0 + tx * 4 + (c & 3) + (c >> 2) * 64;
+      double v[8];
+#pragma unroll
+      for (int r = 0; r < 8; r++) {
+        const uint64_t h = (hi[r][c >> 1] >> ((c & 1) * 16)) & 0xFFFFu;
+        v[r] = (double)((h << kHiShift) + acc[r][c]);
+      }
+      double* row = D + j * n_pad + i0 + ty * 4;
+      *(double2*)(row + 0) = make_double2(v[0], v[1]);
+      *(double2*)(row + 2) = make_double2(v[2], v[3]);
+      *(double2*)(row + 64) = make_double2(v[4], v[5]);
+      *(double2*)(row + 66) = make_double2(v[6], v[7]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// MultiSURF row statistics, thresholds and neighbour counts
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_rowstats(const double* __restrict__ D, int64_t n,
+                                                  int64_t n_pad, int rank, int world,
+                                                  double* __restrict__ rowstats) {
+  __shared__ double red[256];
+  const int64_t i = blockIdx.x;
+  const int64_t nb = n_pad / kTile, bi = i / kTile;
+  const double* row = D + i * n_pad;
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += 256) {
+    if (j == i || !tile_owned(nb, bi, j / kTile, rank, world)) continue;
+    const double d = row[j];
+    s1 += d;
+    s2 += d * d;
+  }
+  s1 = block_sum_256(s1, red);
+  s2 = block_sum_256(s2, red);
+  if (threadIdx.x == 0) {
+    rowstats[2 * i] = s1;
+    rowstats[2 * i + 1] = s2;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_select_ms(const double* __restrict__ D, int64_t n,
+                                                   int64_t n_pad, int rank, int world,
+                                                   const int32_t* __restrict__ lab,
+                                                   const double* __restrict__ rowstats,
+                                                   double* __restrict__ thr,
+                                                   double* __restrict__ counts) {
+  __shared__ double red[256];
+  const int64_t i = blockIdx.x;
+  const int64_t nb = n_pad / kTile, bi = i / kTile;
+  const double t = multisurf_threshold(rowstats[2 * i], rowstats[2 * i + 1], n);
+  const int32_t li = lab[i];
+  const double* row = D + i * n_pad;
+  double h = 0.0, m = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += 256) {
+    if (j == i || !tile_owned(nb, bi, j / kTile, rank, world)) continue;
+    if (row[j] < t) {
+      if (lab[j] == li) h += 1.0;
+      else m += 1.0;
+    }
+  }
+  h = block_sum_256(h, red);
+  m = block_sum_256(m, red);
+  if (threadIdx.x == 0) {
+    thr[i] = t;
+    counts[2 * i] = h;
+    counts[2 * i + 1] = m;
+  }
+}
+
+// SURF: avg_i = float32 sequential sum over j (self included, D_ii = 0) of
+// the float32 distance row, / (n - 1) in float64 (SURF.py:146-163).  Thread
+// i walks column i of the symmetric D so a wave's loads are coalesced.
+__global__ __launch_bounds__(256) void k_surf_avg(const double* __restrict__ D, int64_t n,
+                                                  int64_t n_pad, double inv_sc,
+                                                  double* __restrict__ avg) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.0f;
+  for (int64_t j = 0; j < n; j++) s += (float)(D[j * n_pad + i] * inv_sc);
+  avg[i] = (double)s / (double)(n - 1);
+}
+
+// ---------------------------------------------------------------------------
+// Pair weights per owned tile: Wt[t][jj][ii] = W_ij + W_ji for i < j
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, int64_t n,
+                                                 int64_t n_pad, const int2* __restrict__ tiles,
+                                                 const double* __restrict__ thr,
+                                                 const int32_t* __restrict__ lab,
+                                                 const double* __restrict__ counts, int algo,
+                                                 int use_star, double inv_sc,
+                                                 float* __restrict__ Wt) {
+  const int2 tl = tiles[blockIdx.x];
+  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  float* out = Wt + (int64_t)blockIdx.x * kTile * kTile;
+  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
+    const int jj = e / kTile, ii = e % kTile;
+    const int64_t i = i0 + ii, j = j0 + jj;
+    float w = 0.0f;
+    if (i < n && j < n && (tl.x < tl.y || ii < jj)) {
+      const double d = D[j * n_pad + i];  // == D[i][j]
+      const bool hit = lab[i] == lab[j];
+      double wi, wj;
+      if (algo == ALGO_MULTISURF) {
+        wi = multisurf_weight(d < thr[i], hit, use_star, counts[2 * i], counts[2 * i + 1]);
+        wj = multisurf_weight(d < thr[j], hit, use_star, counts[2 * j], counts[2 * j + 1]);
+      } else {  // SURF: float32 distance against the float64 mean
+        const double df = (double)(float)(d * inv_sc);
+        wi = surf_weight(df < thr[i], hit, use_star);
+        wj = surf_weight(df < thr[j], hit, use_star);
+      }
+      w = (float)(wi + wj);
+    }
+    out[jj * kTile + ii] = w;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Pass 2: weighted per-feature accumulation over owned tiles
+// ---------------------------------------------------------------------------
+// Grid (PW/64 feature blocks, segments of seg_len tiles); 4 waves per
+// workgroup, wave w handles rows w*32 .. w*32+31 of every tile, lane = one
+// feature.  For each column jj the 32 pair weights of that sub-tile are
+// wave-uniform and come through scalar loads; 4 f32 partial sums are folded
+// into a double every 32 columns.
+template <bool DISC>
+__device__ __forceinline__ float pair_term(float a, float b, float w, float acc) {
+  if (DISC) return acc + ((a != b) ? w : 0.0f);
+  return __builtin_fmaf(__builtin_fabsf(a - b), w, acc);
+}
+
+template <bool DISC>
+__device__ __forceinline__ double score_tiles(const float* __restrict__ xs, int64_t PW,
+                                              int64_t c, int wave,
+                                              const int2* __restrict__ tiles,
+                                              const float* __restrict__ Wt, int64_t t_begin,
+                                              int64_t t_end) {
+  double accd = 0.0;
+  for (int64_t t = t_begin; t < t_end; t++) {
+    const int2 tl = tiles[t];
+    const int64_t rbase = (int64_t)tl.x * kTile + wave * kSubRows;
+    float a[kSubRows];
+#pragma unroll
+    for (int r = 0; r < kSubRows; r++) a[r] = xs[(rbase + r) * PW + c];
+    const float* __restrict__ wtile = Wt + t * (kTile * kTile) + wave * kSubRows;
+    const float* __restrict__ xb = xs + (int64_t)tl.y * kTile * PW + c;
+    for (int jb = 0; jb < kTile; jb += 32) {
+      float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f, acc3 = 0.0f;
+#pragma unroll 2
+      for (int jj = jb; jj < jb + 32; jj++) {
+        const float b = xb[(int64_t)jj * PW];
+        const float* __restrict__ w = wtile + jj * kTile;
+#pragma unroll
+        for (int r = 0; r < kSubRows; r += 4) {
+          acc0 = pair_term<DISC>(a[r + 0], b, w[r + 0], acc0);
+          acc1 = pair_term<DISC>(a[r + 1], b, w[r + 1], acc1);
+          acc2 = pair_term<DISC>(a[r + 2], b, w[r + 2], acc2);
+          acc3 = pair_term<DISC>(a[r + 3], b, w[r + 3], acc3);
+        }
+      }
+      accd += ((double)acc0 + (double)acc1) + ((double)acc2 + (double)acc3);
+    }
+  }
+  return accd;
+}
+
+__global__ __launch_bounds__(256) void k_score(const float* __restrict__ xs, int64_t PW,
+                                               int64_t PC, const int2* __restrict__ tiles,
+                                               const float* __restrict__ Wt, int64_t n_tiles,
+                                               int64_t seg_len, double* __restrict__ spart) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t t_begin = (int64_t)blockIdx.y * seg_len;
+  const int64_t t_end = t_begin + seg_len < n_tiles ? t_begin + seg_len : n_tiles;
+  const bool disc = (int64_t)blockIdx.x * 64 >= PC;
+  const double accd = disc ? score_tiles<true>(xs, PW, c, wave, tiles, Wt, t_begin, t_end)
+                           : score_tiles<false>(xs, PW, c, wave, tiles, Wt, t_begin, t_end);
+  red[wave][lane] = accd;
+  __syncthreads();
+  if (wave == 0)
+    spart[(int64_t)blockIdx.y * PW + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+// out[out_pos[c]] = sum over segments of part[seg][c] (fixed order).
+__global__ void k_reduce(const double* __restrict__ part, int64_t nseg, int64_t PW,
+                         const int64_t* __restrict__ out_pos, double* __restrict__ out) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= PW) return;
+  const int64_t o = out_pos[c];
+  if (o < 0) return;
+  double s = 0.0;
+  for (int64_t g = 0; g < nseg; g++) s += part[g * PW + c];
+  out[o] = s;
+}
+
+// ---------------------------------------------------------------------------
+// ReliefF: per-row k-nearest selection per class (radix select on the
+// float32 distance bits, index order among equal keys) and neighbour update
+// ---------------------------------------------------------------------------
+// One workgroup per focal row.  Key of j = bits of (float)(D_ij / SC) (the
+// reference's float32 distance row, ReliefF.py:149-155).  For each class c
+// the k_c-th smallest key T_c is found digit by digit (4 x 8-bit LDS
+// histograms); then wave (c % 4) scans j in ascending order and takes every
+// key < T_c plus the first `need_c` keys == T_c, writing neighbour indices in
+// ascending j (deterministic).
+__global__ __launch_bounds__(256) void k_rf_select(const double* __restrict__ D, int64_t n,
+                                                   int64_t n_pad, double inv_sc,
+                                                   const int32_t* __restrict__ lab,
+                                                   const int64_t* __restrict__ class_count,
+                                                   int n_classes, int64_t k,
+                                                   int32_t* __restrict__ nbr,
+                                                   int32_t* __restrict__ nfound) {
+  extern __shared__ uint32_t sh[];  // hist[n_classes][256], prefix[C], need[C]
+  uint32_t* hist = sh;
+  uint32_t* prefix = sh + n_classes * 256;
+  uint32_t* need = prefix + n_classes;
+  const int64_t i = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int32_t li = lab[i];
+  const double* row = D + i * n_pad;
+  for (int c = tid; c < n_classes; c += 256) {
+    const int64_t members = class_count[c] - (c == li ? 1 : 0);
+    const int64_t kc = members < k ? members : k;
+    prefix[c] = 0;
+    // need = rank (1-based) of the wanted key inside the current bucket;
+    // kc == members: take everything (T = 0xFFFFFFFF, nothing equal needed)
+    need[c] = (uint32_t)kc;
+    if (kc == members) prefix[c] = 0xFFFFFFFFu, need[c] = 0;
+  }
+  __syncthreads();
+  for (int d = 3; d >= 0; d--) {
+    for (int e = tid; e < n_classes * 256; e += 256) hist[e] = 0;
+    __syncthreads();
+    const int sh_hi = 8 * (d + 1);
+    for (int64_t j = tid; j < n; j += 256) {
+      if (j == i) continue;
+      const int32_t c = lab[j];
+      if (need[c] == 0) continue;
+      const uint32_t key = __float_as_uint((float)(row[j] * inv_sc));
+      if (sh_hi < 32 && (key >> sh_hi) != (prefix[c] >> sh_hi)) continue;
+      atomicAdd(&hist[c * 256 + ((key >> (8 * d)) & 0xFF)], 1u);
+    }
+    __syncthreads();
+    for (int c = tid; c < n_classes; c += 256) {
+      if (need[c] == 0) continue;
+      uint32_t cum = 0, b = 0;
+      for (; b < 256; b++) {
+        const uint32_t h = hist[c * 256 + b];
+        if (cum + h >= need[c]) break;
+        cum += h;
+      }
+      prefix[c] |= b << (8 * d);
+      need[c] -= cum;
+    }
+    __syncthreads();
+  }
+  // Ordered collection, one wave per class.
+  const int wave = tid >> 6, lane = tid & 63;
+  for (int c = wave; c < n_classes; c += 4) {
+    const uint32_t T = prefix[c];
+    uint32_t eq_left = need[c];
+    int64_t cnt = 0;
+    int32_t* out = nbr + (i * n_classes + c) * k;
+    for (int64_t j0 = 0; j0 < n; j0 += 64) {
+      const int64_t j = j0 + lane;
+      bool lt = false, eq = false;
+      if (j < n && j != i && lab[j] == c) {
+        const uint32_t key = __float_as_uint((float)(row[j] * inv_sc));
+        lt = key < T;
+        eq = key == T;
+      }
+      const uint64_t meq = __ballot(eq);
+      const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+      // equal keys: only the first eq_left (in j order) are taken
+      const uint32_t eq_rank = (uint32_t)__popcll(meq & below);
+      const bool take_eq = eq && eq_rank < eq_left;
+      const bool take = lt || take_eq;
+      const uint64_t mt = __ballot(take);
+      if (take) out[cnt + __popcll(mt & below)] = (int32_t)j;
+      cnt += __popcll(mt);
+      const uint32_t eq_taken = (uint32_t)__popcll(meq);
+      eq_left = eq_taken >= eq_left ? 0u : eq_left - eq_taken;
+    }
+    if (lane == 0) nfound[i * n_classes + c] = (int32_t)cnt;
+  }
+}
+
+// acc_f(i) = -sum_hits d / h_found + sum_{c != y_i} (P_c / (1 - P_yi)) sum_misses_c d / k
+// (ReliefF.py:177-216).  Grid (PW/64, row blocks of 16); 4 waves per
+// workgroup, wave w handles rows w, w+4, ... of the block.
+__global__ __launch_bounds__(256) void k_rf_update(const float* __restrict__ xs, int64_t n,
+                                                   int64_t PW, int64_t PC,
+                                                   const int32_t* __restrict__ lab,
+                                                   const double* __restrict__ prior,
+                                                   int n_classes, int64_t k,
+                                                   const int32_t* __restrict__ nbr,
+                                                   const int32_t* __restrict__ nfound,
+                                                   double* __restrict__ part) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  const bool disc = (int64_t)blockIdx.x * 64 >= PC;
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.y * 16 + wave; i < n && i < (int64_t)blockIdx.y * 16 + 16;
+       i += 4) {
+    const int32_t li = lab[i];
+    const float a = xs[i * PW + c];
+    double denom = 1.0 - prior[li];
+    if (denom == 0.0) denom = 1.0;
+    for (int cl = 0; cl < n_classes; cl++) {
+      const int32_t found = nfound[i * n_classes + cl];
+      if (found == 0) continue;
+      const double wgt = (cl == li) ? -1.0 / (double)found : (prior[cl] / denom) / (double)k;
+      const int32_t* lst = nbr + (i * n_classes + cl) * k;
+      double s = 0.0;
+      for (int32_t t = 0; t < found; t++) {
+        const float b = xs[(int64_t)lst[t] * PW + c];
+        s += disc ? ((a != b) ? 1.0 : 0.0) : (double)__builtin_fabsf(a - b);
+      }
+      acc += wgt * s;
+    }
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0)
+    part[(int64_t)blockIdx.y * PW + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+struct Plan {
+  Prepared P;
+  int device = 0, rank = 0, world = 1;
+  int x_is_f64 = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int64_t nb = 0, n_tiles = 0, seg_len = 1, nseg = 1;
+  // device buffers
+  void* x = nullptr;
+  int64_t* src_col = nullptr;
+  int64_t* out_pos = nullptr;
+  double *off = nullptr, *qs = nullptr, *scl = nullptr;
+  int64_t* dtab_off = nullptr;
+  double* dtab = nullptr;
+  int32_t* lab = nullptr;
+  uint32_t* xqT = nullptr;
+  float* xs = nullptr;
+  double* D = nullptr;
+  int2* tiles = nullptr;
+  double* thr = nullptr;
+  float* Wt = nullptr;
+  double* spart = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  float ms_dist = -1.0f, ms_score = -1.0f;
+  std::vector<void*> owned;
+};
+
+template <typename T>
+static int dalloc(Plan* g, T** p, size_t count) {
+  void* q = nullptr;
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc(&q, count * sizeof(T));
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    set_error(std::string("hipMalloc of ") + std::to_string(count * sizeof(T)) +
+              " bytes failed: " + hipGetErrorString(e));
+    return FS_EOOM;
+  }
+  g->owned.push_back(q);
+  *p = (T*)q;
+  return FS_OK;
+}
+
+#define FS_TRY(expr)            \
+  do {                          \
+    int rc_ = (expr);           \
+    if (rc_ != FS_OK) return rc_; \
+  } while (0)
+
+template <typename T>
+static int h2d(Plan* g, T* dst, const T* src, size_t count) {
+  if (count == 0) return FS_OK;
+  FS_HIP(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, g->stream));
+  return FS_OK;
+}
+
+void plan_destroy(Plan* g) {
+  if (!g) return;
+  if (g->stream) (void)hipStreamSynchronize(g->stream);
+  for (void* q : g->owned) (void)hipFree(q);
+  for (auto& e : g->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
+  delete g;
+}
+
+int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int device,
+                int rank, int world, uint64_t stream) {
+  *out = nullptr;
+  const int ndev = device_count();
+  if (ndev <= 0) {
+    set_error("backend='gpu' requested but no HIP device is visible");
+    return FS_ENODEV;
+  }
+  if (device < 0 || device >= ndev) {
+    set_error("device ordinal out of range");
+    return FS_EINVAL;
+  }
+  if (world < 1 || rank < 0 || rank >= world) {
+    set_error("invalid rank/world");
+    return FS_EINVAL;
+  }
+  FS_HIP(hipSetDevice(device));
+  Plan* g = new Plan();
+  g->P = P;
+  g->device = device;
+  g->rank = rank;
+  g->world = world;
+  g->x_is_f64 = x_is_f64;
+  if (stream) {
+    g->stream = (hipStream_t)(uintptr_t)stream;
+  } else {
+    if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete g;
+      set_error("hipStreamCreate failed");
+      return FS_EHIP;
+    }
+    g->own_stream = true;
+  }
+  auto fail = [&](int rc) {
+    plan_destroy(g);
+    return rc;
+  };
+  for (auto& e : g->ev)
+    if (hipEventCreate(&e) != hipSuccess) return fail(FS_EHIP);
+  const Prepared& Q = g->P;
+  g->nb = Q.n_pad / kTile;
+  std::vector<int32_t> bi, bj;
+  owned_tiles(g->nb, rank, world, bi, bj);
+  g->n_tiles = (int64_t)bi.size();
+  std::vector<int2> tl(g->n_tiles);
+  for (int64_t t = 0; t < g->n_tiles; t++) tl[t] = make_int2(bi[t], bj[t]);
+  const int64_t nfb = Q.PW / 64;
+  // ~64k pass-2 workgroups: enough to fill 256 CUs and bound tail imbalance.
+  g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + 65535) / 65536);
+  g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
+  const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
+  int rc;
+  if ((rc = dalloc(g, (char**)&g->x, xbytes)) ||
+      (rc = dalloc(g, &g->src_col, Q.PW)) || (rc = dalloc(g, &g->out_pos, Q.PW)) ||
+      (rc = dalloc(g, &g->off, Q.PW)) || (rc = dalloc(g, &g->qs, Q.PW)) ||
+      (rc = dalloc(g, &g->scl, Q.PW)) || (rc = dalloc(g, &g->dtab_off, Q.PW + 1)) ||
+      (rc = dalloc(g, &g->dtab, Q.dtab.size())) || (rc = dalloc(g, &g->lab, Q.n_pad)) ||
+      (rc = dalloc(g, &g->xqT, (size_t)Q.PW * Q.n_pad)) ||
+      (rc = dalloc(g, &g->xs, (size_t)Q.n_pad * Q.PW)) ||
+      (rc = dalloc(g, &g->D, (size_t)Q.n_pad * Q.n_pad)) ||
+      (rc = dalloc(g, &g->tiles, g->n_tiles)) || (rc = dalloc(g, &g->thr, Q.n_pad)))
+    return fail(rc);
+  if (Q.algo != ALGO_RELIEFF) {
+    if ((rc = dalloc(g, &g->Wt, (size_t)g->n_tiles * kTile * kTile)) ||
+        (rc = dalloc(g, &g->spart, (size_t)g->nseg * Q.PW)))
+      return fail(rc);
+  }
+  std::vector<double> qs(Q.PW, 0.0);
+  for (int64_t c = 0; c < Q.PW; c++) qs[c] = Q.scale[c] * Q.SC;
+  std::vector<int32_t> lab(Q.n_pad, -1);
+  std::copy(Q.labels.begin(), Q.labels.end(), lab.begin());
+  if ((rc = h2d(g, (char*)g->x, (const char*)x, xbytes)) ||
+      (rc = h2d(g, g->src_col, Q.src_col.data(), Q.PW)) ||
+      (rc = h2d(g, g->out_pos, Q.out_pos.data(), Q.PW)) ||
+      (rc = h2d(g, g->off, Q.offset.data(), Q.PW)) || (rc = h2d(g, g->qs, qs.data(), Q.PW)) ||
+      (rc = h2d(g, g->scl, Q.scale.data(), Q.PW)) ||
+      (rc = h2d(g, g->dtab_off, Q.dtab_off.data(), Q.PW + 1)) ||
+      (rc = h2d(g, g->dtab, Q.dtab.data(), Q.dtab.size())) ||
+      (rc = h2d(g, g->lab, lab.data(), Q.n_pad)) ||
+      (rc = h2d(g, g->tiles, tl.data(), g->n_tiles)))
+    return fail(rc);
+  if (hipStreamSynchronize(g->stream) != hipSuccess) return fail(FS_EHIP);
+  *out = g;
+  return FS_OK;
+}
+
+static int launch_check(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string("kernel launch failed (") + what + "): " + hipGetErrorString(e));
+    return FS_EHIP;
+  }
+  return FS_OK;
+}
+
+// quantize + pass 1 (distance tiles)
+static int run_quantize_dist(Plan* g) {
+  const Prepared& Q = g->P;
+  FS_HIP(hipSetDevice(g->device));
+  dim3 gq((unsigned)(Q.PW / 64), (unsigned)(Q.n_pad / 64));
+  if (g->x_is_f64)
+    k_quantize<double><<<gq, 256, 0, g->stream>>>(
+        (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, Q.PC, Q.pd, g->src_col, g->off,
+        g->qs, g->scl, g->dtab_off, g->dtab, g->xqT, g->xs);
+  else
+    k_quantize<float><<<gq, 256, 0, g->stream>>>(
+        (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, Q.PC, Q.pd, g->src_col, g->off,
+        g->qs, g->scl, g->dtab_off, g->dtab, g->xqT, g->xs);
+  FS_TRY(launch_check("k_quantize"));
+  if (g->n_tiles > 0) {
+    FS_HIP(hipEventRecord(g->ev[0], g->stream));
+    k_dist<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->xqT, Q.n_pad, (int)(Q.PC / kBK),
+                                                          (int)(Q.PD / kBK), Q.SCu, g->tiles,
+                                                          g->D);
+    FS_TRY(launch_check("k_dist"));
+    FS_HIP(hipEventRecord(g->ev[1], g->stream));
+  }
+  return FS_OK;
+}
+
+static int run_pass2(Plan* g, double* scores_dev) {
+  const Prepared& Q = g->P;
+  const int64_t nfb = Q.PW / 64;
+  FS_HIP(hipMemsetAsync(scores_dev, 0, sizeof(double) * Q.n_kept, g->stream));
+  if (g->n_tiles == 0) return FS_OK;
+  FS_HIP(hipEventRecord(g->ev[2], g->stream));
+  k_score<<<dim3((unsigned)nfb, (unsigned)g->nseg), 256, 0, g->stream>>>(
+      g->xs, Q.PW, Q.PC, g->tiles, g->Wt, g->n_tiles, g->seg_len, g->spart);
+  FS_TRY(launch_check("k_score"));
+  FS_HIP(hipEventRecord(g->ev[3], g->stream));
+  k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(g->spart, g->nseg, Q.PW,
+                                                                   g->out_pos, scores_dev);
+  return launch_check("k_reduce");
+}
+
+int plan_pass1(Plan* g, double* rowstats) {
+  const Prepared& Q = g->P;
+  FS_TRY(run_quantize_dist(g));
+  k_rowstats<<<(unsigned)Q.n, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->rank, g->world,
+                                                   rowstats);
+  FS_TRY(launch_check("k_rowstats"));
+  if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
+  return FS_OK;
+}
+
+int plan_select(Plan* g, const double* rowstats, double* counts) {
+  const Prepared& Q = g->P;
+  FS_HIP(hipSetDevice(g->device));
+  k_select_ms<<<(unsigned)Q.n, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->rank, g->world,
+                                                    g->lab, rowstats, g->thr, counts);
+  FS_TRY(launch_check("k_select_ms"));
+  if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
+  return FS_OK;
+}
+
+int plan_pass2(Plan* g, const double* counts, double* scores) {
+  const Prepared& Q = g->P;
+  FS_HIP(hipSetDevice(g->device));
+  if (g->n_tiles > 0) {
+    k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
+                                                           g->thr, g->lab, counts,
+                                                           ALGO_MULTISURF, Q.use_star,
+                                                           1.0 / Q.SC, g->Wt);
+    FS_TRY(launch_check("k_weights"));
+  }
+  FS_TRY(run_pass2(g, scores));
+  if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
+  return FS_OK;
+}
+
+int plan_info(const Plan* g, int64_t* tiles, double* pfe) {
+  if (tiles) *tiles = g->n_tiles;
+  if (pfe) {
+    // pairs visited by both passes (diagonal tiles count their full 128x128
+    // pass-1 work) x real features
+    *pfe = 2.0 * (double)g->n_tiles * kTile * kTile * (double)(g->P.pc + g->P.pd);
+  }
+  return FS_OK;
+}
+
+double plan_kernel_ms(const Plan* g, int which) {
+  float ms = -1.0f;
+  hipEvent_t a = which == 0 ? g->ev[0] : g->ev[2];
+  hipEvent_t b = which == 0 ? g->ev[1] : g->ev[3];
+  if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1.0;
+  }
+  return (double)ms;
+}
+
+// ---- one-shot runs --------------------------------------------------------
+
+static int finish_scores(Plan* g, double* scores_dev, float* scores_out) {
+  const Prepared& Q = g->P;
+  std::vector<double> h(Q.n_kept);
+  FS_HIP(hipMemcpyAsync(h.data(), scores_dev, sizeof(double) * Q.n_kept, hipMemcpyDeviceToHost,
+                        g->stream));
+  FS_HIP(hipStreamSynchronize(g->stream));
+  for (int64_t k = 0; k < Q.n_kept; k++) scores_out[k] = (float)(h[k] / (double)Q.n);
+  return FS_OK;
+}
+
+int multisurf_run(const Prepared& P, const void* x, int device, float* scores_out) {
+  Plan* g = nullptr;
+  FS_TRY(plan_create(&g, P, x, 0, device, 0, 1, 0));
+  double *rs = nullptr, *cnt = nullptr, *sc = nullptr;
+  int rc;
+  if ((rc = dalloc(g, &rs, 2 * P.n)) || (rc = dalloc(g, &cnt, 2 * P.n)) ||
+      (rc = dalloc(g, &sc, P.n_kept)) || (rc = plan_pass1(g, rs)) ||
+      (rc = plan_select(g, rs, cnt)) || (rc = plan_pass2(g, cnt, sc)) ||
+      (rc = finish_scores(g, sc, scores_out))) {
+    plan_destroy(g);
+    return rc;
+  }
+  plan_destroy(g);
+  return FS_OK;
+}
+
+int surf_run(const Prepared& P, const void* x, int device, float* scores_out) {
+  Plan* g = nullptr;
+  FS_TRY(plan_create(&g, P, x, 1, device, 0, 1, 0));
+  const Prepared& Q = g->P;
+  double* sc = nullptr;
+  int rc = dalloc(g, &sc, Q.n_kept);
+  if (rc == FS_OK) rc = run_quantize_dist(g);
+  if (rc == FS_OK) {
+    k_surf_avg<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad,
+                                                                    1.0 / Q.SC, g->thr);
+    rc = launch_check("k_surf_avg");
+  }
+  if (rc == FS_OK) {
+    k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
+                                                           g->thr, g->lab, nullptr, ALGO_SURF,
+                                                           Q.use_star, 1.0 / Q.SC, g->Wt);
+    rc = launch_check("k_weights");
+  }
+  if (rc == FS_OK) rc = run_pass2(g, sc);
+  if (rc == FS_OK) rc = finish_scores(g, sc, scores_out);
+  plan_destroy(g);
+  return rc;
+}
+
+int relieff_run(const Prepared& P, const void* x, int device, float* scores_out) {
+  if (P.n_classes > 64) {
+    set_error("GPU ReliefF supports at most 64 classes");
+    return FS_ENOTSUP;
+  }
+  Plan* g = nullptr;
+  FS_TRY(plan_create(&g, P, x, 0, device, 0, 1, 0));
+  const Prepared& Q = g->P;
+  const int C = Q.n_classes;
+  const int64_t k = Q.k_neighbors;
+  std::vector<int64_t> cc(C, 0);
+  for (int64_t i = 0; i < Q.n; i++) cc[Q.labels[i]]++;
+  std::vector<double> prior(Q.class_prior);
+  double *sc = nullptr, *dprior = nullptr, *part = nullptr;
+  int64_t* dcc = nullptr;
+  int32_t *nbr = nullptr, *nfound = nullptr;
+  const int64_t nrb = (Q.n + 15) / 16;
+  int rc;
+  if ((rc = dalloc(g, &sc, Q.n_kept)) || (rc = dalloc(g, &dprior, C)) ||
+      (rc = dalloc(g, &part, (size_t)nrb * Q.PW)) || (rc = dalloc(g, &dcc, C)) ||
+      (rc = dalloc(g, &nbr, (size_t)Q.n * C * std::max<int64_t>(k, 1))) ||
+      (rc = dalloc(g, &nfound, (size_t)Q.n * C)) || (rc = h2d(g, dcc, cc.data(), C)) ||
+      (rc = h2d(g, dprior, prior.data(), C)) || (rc = run_quantize_dist(g))) {
+    plan_destroy(g);
+    return rc;
+  }
+  const size_t shbytes = (size_t)C * 256 * 4 + 2 * (size_t)C * 4;
+  k_rf_select<<<(unsigned)Q.n, 256, shbytes, g->stream>>>(g->D, Q.n, Q.n_pad, 1.0 / Q.SC,
+                                                          g->lab, dcc, C, k, nbr, nfound);
+  rc = launch_check("k_rf_select");
+  if (rc == FS_OK) {
+    k_rf_update<<<dim3((unsigned)(Q.PW / 64), (unsigned)nrb), 256, 0, g->stream>>>(
+        g->xs, Q.n, Q.PW, Q.PC, g->lab, dprior, C, k, nbr, nfound, part);
+    rc = launch_check("k_rf_update");
+  }
+  if (rc == FS_OK) {
+    k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(part, nrb, Q.PW,
+                                                                     g->out_pos, sc);
+    rc = launch_check("k_reduce");
+  }
+  if (rc == FS_OK) rc = finish_scores(g, sc, scores_out);
+  plan_destroy(g);
+  return rc;
+}
+
+}  // namespace gpu
+}  // namespace fs

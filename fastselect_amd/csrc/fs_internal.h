@@ -1,0 +1,145 @@
+// fs_internal.h -- shared definitions of the Relief scoring pipeline.
+//
+// Pipeline (every algorithm):
+//   quantize   X (row-major, kernel dtype) -> Xq (integer distance operands)
+//                                          -> Xs (float32 per-feature diffs)
+//   pass 1     D[i][j] = sum_f |q_if - q_jf| (+ SC * [c_if != c_jf] for discrete
+//              features), exact integers, computed once per unordered pair
+//              (upper-triangle 128x128 tiles), stored for both (i,j) and (j,i)
+//   select     per-row neighbourhood: MultiSURF radius mu - sigma/2, SURF mean
+//              radius, ReliefF k nearest hits / misses per class
+//   pass 2     S_f = sum_{i<j} w_ij |xs_if - xs_jf| with w_ij = W_ij + W_ji the
+//              symmetric pair weight (MultiSURF/SURF), or the ReliefF
+//              neighbour gather
+//   finalize   scores = S / n
+//
+// Integer distance unit: one unit of the reference's scaled diff
+// |x_i - x_j| * recip corresponds to SC integer units, SC ~ 2^24 (chosen per
+// problem so that the pass-1 accumulators cannot overflow; see choose_scale).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#if defined(__HIPCC__)
+#define FS_HD __host__ __device__
+#else
+#define FS_HD
+#endif
+
+namespace fs {
+
+enum Algo : int { ALGO_MULTISURF = 0, ALGO_RELIEFF = 1, ALGO_SURF = 2 };
+
+constexpr int kTile = 128;          // pair tile edge (pass 1 / pass 2 / weights)
+constexpr int kBK = 16;             // features per LDS stage in pass 1
+constexpr int kFlushChunks = 16;    // pass-1 u32 window = 256 features
+constexpr int kHiShift = 24;        // pass-1 high part = D >> 24 (16-bit packed)
+constexpr int kFeatPad = 64;        // feature blocks (one wave of lanes in pass 2)
+constexpr int kSubRows = 32;        // pass-2 rows held in registers per sweep
+
+void set_error(const std::string& msg);
+
+// Host-side derived problem description, identical for both backends.
+struct Prepared {
+  int algo = ALGO_MULTISURF;
+  int use_star = 0;
+  int64_t k_neighbors = 0;
+  int64_t n = 0, n_pad = 0;        // samples; n_pad = roundup(n, kTile)
+  int64_t p_in = 0;                // columns of the input X
+  int64_t n_kept = 0;              // scored features (feat_idx)
+  int64_t pc = 0, pd = 0;          // continuous / discrete kept features
+  int64_t PC = 0, PD = 0, PW = 0;  // padded block widths, PW = PC + PD
+  // per permuted column c in [0, PW): source column in X (-1 = padding),
+  // position in the output (kept-feature order, -1 = padding)
+  std::vector<int64_t> src_col, out_pos;
+  std::vector<double> offset;      // continuous: column minimum (kernel dtype)
+  std::vector<double> scale;       // continuous: (double)recip
+  // discrete: per permuted column, [dtab_off[c], dtab_off[c+1]) slice of the
+  // sorted distinct values (kernel dtype widened to double)
+  std::vector<int64_t> dtab_off;
+  std::vector<double> dtab;
+  std::vector<int32_t> labels;     // class code per sample
+  int32_t n_classes = 0;
+  std::vector<double> class_prior; // ReliefF priors (float32 values widened)
+  double SC = 0.0;                 // integer units per scaled-diff unit
+  uint32_t SCu = 0;                // SC as an integer (discrete mismatch cost)
+};
+
+// Build the permutation, label codes, discrete tables and integer scale.
+// x is row-major [n][p_in], float32 (x_is_f64 == 0) or float64.
+int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64_t p_in,
+            const int64_t* feat_idx, int64_t n_kept, const float* recip,
+            const uint8_t* is_discrete, int n_jobs);
+int encode_labels_f64(Prepared& P, const double* y);
+int encode_labels_i32(Prepared& P, const int32_t* y);
+
+// Upper-triangle tile enumeration: t -> (bi, bj), bi <= bj, row-major over
+// the triangle.  Tile t is owned by rank t % world.
+void owned_tiles(int64_t nb, int rank, int world, std::vector<int32_t>& bi,
+                 std::vector<int32_t>& bj);
+FS_HD inline int64_t tile_linear(int64_t nb, int64_t bi, int64_t bj) {
+  // number of tiles in rows < bi is bi*nb - bi*(bi-1)/2
+  return bi * nb - bi * (bi - 1) / 2 + (bj - bi);
+}
+
+int hardware_threads(int n_jobs);
+
+// Thresholds shared by both backends (MultiSURF.py:193-196 in D units).
+FS_HD inline double multisurf_threshold(double s1, double s2, int64_t n) {
+  const double mu = s1 / (double)(n - 1);
+  double var = s2 / (double)(n - 1) - mu * mu;
+  if (var < 0.0) var = 0.0;
+  return mu - 0.5 * __builtin_sqrt(var);
+}
+
+// Pair weight of focal sample i for neighbour j (MultiSURF.py:217-251):
+// near hit -1/H_i, near miss +1/M_i, far miss (star) -1/max(M_i, 1).
+FS_HD inline double multisurf_weight(bool near, bool hit, int use_star, double H, double M) {
+  if (near) return hit ? -1.0 / H : 1.0 / M;
+  if (use_star && !hit) return -1.0 / (M > 0.0 ? M : 1.0);
+  return 0.0;
+}
+
+// SURF pair weight of focal sample i for neighbour j (SURF.py:180-193).
+FS_HD inline double surf_weight(bool near, bool hit, int use_star) {
+  if (near) return hit ? -1.0 : 1.0;
+  if (use_star) return hit ? 1.0 : -1.0;
+  return 0.0;
+}
+
+// ---- CPU backend ---------------------------------------------------------
+namespace cpu {
+int multisurf_pass1(const Prepared& P, const void* x, int x_is_f64, int rank, int world,
+                    int n_jobs, std::vector<uint64_t>& D, std::vector<float>& xs,
+                    double* rowstats);
+int multisurf_select(const Prepared& P, const std::vector<uint64_t>& D, int rank, int world,
+                     const double* rowstats, std::vector<double>& thr, double* counts,
+                     int n_jobs);
+int multisurf_pass2(const Prepared& P, const std::vector<uint64_t>& D,
+                    const std::vector<float>& xs, const std::vector<double>& thr,
+                    const double* counts, int rank, int world, int n_jobs, double* scores);
+int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores);
+int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores);
+}  // namespace cpu
+
+// ---- GPU backend ---------------------------------------------------------
+namespace gpu {
+int device_count();
+struct Plan;
+int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int device,
+                int rank, int world, uint64_t stream);
+int plan_pass1(Plan* g, double* rowstats_dev);
+int plan_select(Plan* g, const double* rowstats_dev, double* counts_dev);
+int plan_pass2(Plan* g, const double* counts_dev, double* scores_dev);
+int plan_info(const Plan* g, int64_t* tiles, double* pfe);
+double plan_kernel_ms(const Plan* g, int which);
+void plan_destroy(Plan* g);
+// Single-GPU one-shot runs (host in/out, scores already divided by n).
+int multisurf_run(const Prepared& P, const void* x, int device, float* scores_out);
+int surf_run(const Prepared& P, const void* x, int device, float* scores_out);
+int relieff_run(const Prepared& P, const void* x, int device, float* scores_out);
+}  // namespace gpu
+
+}  // namespace fs

@@ -1,0 +1,160 @@
+/*
+ * fastselect_amd.h -- C ABI of the MI355X Relief-family scoring engine.
+ *
+ * The reference (GavinLynch04/FastSelect v0.2.0) has no native FFI: its
+ * hot-path boundary is the private Python "host callers" that each estimator's
+ * fit() invokes once per fit.  The one-shot entry points below replace those
+ * callers one-for-one (same arguments and meaning, plus a backend selector),
+ * so the Python estimators call exactly one C function per fit:
+ *
+ *   fs_multisurf_score  replaces _multisurf_cpu_host_caller  (MultiSURF.py:256-270)
+ *                       and      _multisurf_gpu_host_caller  (MultiSURF.py:147-162)
+ *   fs_relieff_score    replaces _relieff_cpu_host_caller    (ReliefF.py:222-236)
+ *                       and      _relieff_gpu_host_caller    (ReliefF.py:127-134)
+ *   fs_surf_score       replaces _surf_cpu_host_caller       (SURF.py:198-218)
+ *                       and      _surf_gpu_host_caller       (SURF.py:117-128)
+ *
+ * Every one-shot call is synchronous, takes caller-owned host arrays that must
+ * stay valid for the duration of the call, and writes scores ALREADY DIVIDED
+ * BY n (as the host callers return them).  Device memory is allocated and
+ * freed inside the call; no pointer to caller memory is retained.
+ *
+ * The fs_plan_* entry points expose the same MultiSURF path split at its
+ * three exchange points (per-row distance moments, per-row neighbour counts,
+ * per-feature score sums) so that one process per GPU can shard the pair
+ * tiles across ranks and sum those three small vectors with a collective
+ * (RCCL all-reduce over xGMI, driven by torch.distributed in
+ * fastselect_amd/parallel.py).  With world == 1 the stages compose to exactly
+ * fs_multisurf_score.
+ *
+ * Errors: every function returns FS_OK (0) or a negative FS_E* code; a
+ * thread-local human-readable message is available from fs_last_error().
+ * The Python layer maps FS_EINVAL -> ValueError, FS_ENODEV / FS_EHIP /
+ * FS_ENOTSUP -> RuntimeError, FS_EOOM -> MemoryError.
+ *
+ * Backends: FS_BACKEND_GPU runs the hand-written HIP kernels for gfx950
+ * (MI355X) and fails with FS_ENODEV when no HIP device is visible -- it never
+ * falls back to the CPU.  FS_BACKEND_CPU runs the native multithreaded CPU
+ * implementation of the same pipeline (the reference's backend='cpu').
+ */
+#ifndef FASTSELECT_AMD_H
+#define FASTSELECT_AMD_H
+
+#include <stdint.h>
+
+#if defined(__GNUC__)
+#define FS_API __attribute__((visibility("default")))
+#else
+#define FS_API
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FS_OK 0
+#define FS_EINVAL (-1)   /* bad argument (shape, pointer, parameter) */
+#define FS_ENODEV (-2)   /* GPU backend requested but no HIP device visible */
+#define FS_EOOM (-3)     /* host or device allocation failed */
+#define FS_EHIP (-4)     /* HIP runtime / kernel launch error */
+#define FS_ENOTSUP (-5)  /* combination not supported by this build */
+
+#define FS_BACKEND_CPU 0
+#define FS_BACKEND_GPU 1
+
+/* Library identity and device discovery. */
+FS_API const char* fs_version(void);
+FS_API const char* fs_last_error(void);
+/* Number of visible HIP devices (0 when none, never negative). */
+FS_API int fs_device_count(void);
+
+/*
+ * MultiSURF / MultiSURF* feature scores.
+ *   x            [n][p] float32, row-major (validated X, MultiSURF.py:384-386)
+ *   y            [n] labels as float64; samples are hits when y[i] == y[j]
+ *   recip        [p] float32 reciprocal feature ranges (MultiSURF.py:409-412)
+ *   feat_idx     [n_kept] feature indices to score, or NULL for all p
+ *                (the reference's feat_idx argument, MultiSURF.py:147,256)
+ *   use_star     nonzero: MultiSURF* (far misses subtract, MultiSURF.py:236-243)
+ *   is_discrete  [p] 0/1 (MultiSURF.py:416-420)
+ *   n_jobs       CPU threads (-1 = all); ignored by the GPU backend
+ *   device       HIP device ordinal for the GPU backend
+ *   scores_out   [n_kept] float32, scores / n
+ */
+FS_API int fs_multisurf_score(int backend, int device, const float* x, int64_t n, int64_t p,
+                       const double* y, const float* recip, const int64_t* feat_idx,
+                       int64_t n_kept, int use_star, const uint8_t* is_discrete, int n_jobs,
+                       float* scores_out);
+
+/*
+ * ReliefF feature scores (ReliefF.py:137-236).
+ *   x            [n][p] float32 (the float32 cast of the float64-validated X, ReliefF.py:400)
+ *   y_enc        [n] int32 class codes in [0, n_classes) (ReliefF.py:375)
+ *   recip        [p] float32 (discrete and zero ranges forced to 1, ReliefF.py:377-380)
+ *   is_discrete  [p] 0/1
+ *   k            n_neighbors (>= 1)
+ *   class_probs  [n_classes] float32 class priors (ReliefF.py:373-374)
+ *   scores_out   [p] float32, scores / n
+ * Neighbour ties at the k-th distance are broken by sample index (the
+ * reference breaks them in numba-quicksort order).
+ */
+FS_API int fs_relieff_score(int backend, int device, const float* x, int64_t n, int64_t p,
+                     const int32_t* y_enc, const float* recip, const uint8_t* is_discrete,
+                     int64_t k, const float* class_probs, int64_t n_classes, int n_jobs,
+                     float* scores_out);
+
+/*
+ * SURF / SURF* feature scores (SURF.py:131-218).
+ *   x            [n][p] float64, row-major (SURF.py:330-332)
+ *   y            [n] int32 labels (y.astype(int32), SURF.py:371)
+ *   recip        [p] float32 (SURF.py:352-355)
+ *   use_star     nonzero: SURF* (far hits add, far misses subtract)
+ *   scores_out   [p] float32, scores / n
+ */
+FS_API int fs_surf_score(int backend, int device, const double* x, int64_t n, int64_t p,
+                  const int32_t* y, const float* recip, int use_star,
+                  const uint8_t* is_discrete, int n_jobs, float* scores_out);
+
+/* ---- Sharded MultiSURF plan (one plan per rank) ------------------------ */
+
+typedef struct fs_plan fs_plan;
+
+/*
+ * Create a plan and upload its inputs (host arrays, same meaning as
+ * fs_multisurf_score).  rank/world select which upper-triangle pair tiles
+ * this plan computes (tile t belongs to rank t % world).  `stream` is a
+ * hipStream_t (0 = the plan's own stream) on which every GPU stage is
+ * enqueued; stages do not synchronise the host unless `stream` is 0.
+ */
+FS_API int fs_plan_create(fs_plan** plan_out, int backend, int device, const float* x, int64_t n,
+                   int64_t p, const double* y, const float* recip, const int64_t* feat_idx,
+                   int64_t n_kept, int use_star, const uint8_t* is_discrete, int rank, int world,
+                   int n_jobs, uint64_t stream);
+
+/*
+ * Stage 1: quantise the resident X, compute this rank's distance tiles and
+ * write this rank's partial per-row moments to rowstats[2n] (sum D, sum D^2;
+ * D in the plan's integer distance unit).  Pointers live in the plan's memory
+ * space: device memory for the GPU backend, host memory for the CPU backend.
+ */
+FS_API int fs_plan_pass1(fs_plan* plan, double* rowstats);
+/* Stage 2: thresholds from the all-reduced rowstats; partial near-hit and
+ * near-miss counts per row -> counts[2n]. */
+FS_API int fs_plan_select(fs_plan* plan, const double* rowstats, double* counts);
+/* Stage 3: pair weights from all-reduced counts; partial per-feature score
+ * sums (NOT divided by n) -> scores[n_kept], in feat_idx order. */
+FS_API int fs_plan_pass2(fs_plan* plan, const double* counts, double* scores);
+/* Number of pair tiles this plan owns and the pair-feature evaluations one
+ * full pass1+pass2 performs on this rank (for throughput accounting). */
+FS_API int fs_plan_info(const fs_plan* plan, int64_t* owned_tiles, double* pair_feature_evals);
+/* Average duration in milliseconds of the last pass1 / pass2 distance and
+ * score kernels, measured with HIP events on the plan's stream (GPU only;
+ * -1 when unavailable).  which: 0 = distance kernel, 1 = score kernel. */
+FS_API double fs_plan_kernel_ms(const fs_plan* plan, int which);
+FS_API int fs_plan_destroy(fs_plan* plan);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FASTSELECT_AMD_H */

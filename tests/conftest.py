@@ -1,0 +1,47 @@
+"""Test configuration.
+
+Markers: ``gpu`` -- needs a visible HIP device (MI355X); run with
+``pytest -m gpu`` on the GPU box.  Everything else runs on CPU in a few
+minutes (``pytest -m "not gpu"``).
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a visible HIP GPU (MI355X)")
+    config.addinivalue_line("markers", "slow: long-running parity case")
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle as O
+    O.build()
+    return O
+
+
+def scale_rel_err(a, ref):
+    """max_f |a_f - ref_f| / max_f |ref_f| (SURVEY.md §8d parity criterion)."""
+    a = np.asarray(a, dtype=np.float64)
+    ref = np.asarray(ref, dtype=np.float64)
+    den = np.abs(ref).max()
+    if den == 0.0:
+        return np.abs(a).max()
+    return np.abs(a - ref).max() / den
+
+
+def assert_parity(a, ref, tol=1e-5, k=None):
+    """Scores within `tol` scale-relative, and identical top-k index sets."""
+    err = scale_rel_err(a, ref)
+    assert err <= tol, f"scale-relative error {err:.3e} > {tol:.1e}"
+    if k is not None:
+        ta = set(np.argsort(np.asarray(a))[::-1][:k].tolist())
+        tr = set(np.argsort(np.asarray(ref))[::-1][:k].tolist())
+        assert ta == tr, f"top-{k} differ: {sorted(ta ^ tr)}"

@@ -1,0 +1,224 @@
+"""GPU parity tests: the HIP path (backend='gpu', through the C ABI) against
+the C oracle (oracle/relief_oracle.c) and against the committed fixtures.
+
+Bar (north_star / SURVEY.md §8d): scores within 1e-5 scale-relative
+(max_f |s_f - ref_f| <= 1e-5 * max_f |ref_f|) and identical top-k index sets.
+Every test here needs a visible HIP device and fails (does not skip) without
+one, so a run can never pass on a CPU fallback.
+"""
+import os
+
+import numpy as np
+import pytest
+from conftest import assert_parity, scale_rel_err
+from sklearn.datasets import make_classification
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module", autouse=True)
+def require_gpu():
+    from fastselect_amd import _lib
+    assert _lib.device_count() >= 1, "no HIP device visible: GPU tests cannot run"
+    assert os.path.dirname(_lib.LIB_PATH).endswith("fastselect_amd")
+
+
+def _fit(est_cls, X, y, **kw):
+    est = est_cls(backend="gpu", n_features_to_select=kw.pop("n_features_to_select", 1), **kw)
+    est.fit(X, y)
+    assert est.effective_backend_ == "gpu"
+    return est.feature_importances_
+
+
+def test_golden_oracle_vectors():
+    from fastselect_amd import SURF, MultiSURF, ReliefF
+    g = np.load(os.path.join(GOLD, "oracle_vectors.npz"))
+    for name in ("a", "b", "c"):
+        X, y = g[f"{name}_X"], g[f"{name}_y"]
+        assert_parity(_fit(MultiSURF, X, y), g[f"{name}_multisurf"], TOL, k=5)
+        assert_parity(_fit(MultiSURF, X, y, use_star=True), g[f"{name}_multisurfstar"], TOL, k=5)
+        assert_parity(_fit(SURF, X, y), g[f"{name}_surf"], TOL, k=5)
+        assert_parity(_fit(SURF, X, y, use_star=True), g[f"{name}_surfstar"], TOL, k=5)
+        for k in (1, 3, 10):
+            assert_parity(_fit(ReliefF, X, y, n_neighbors=k), g[f"{name}_relieff_k{k}"], TOL, k=5)
+
+
+def test_reference_kats_on_gpu():
+    """The reference tests' known answers, on the GPU backend."""
+    from fastselect_amd import SURF, MultiSURF, ReliefF
+    fx = np.load(os.path.join(GOLD, "reference_fixtures.npz"))
+    m = MultiSURF(n_features_to_select=1, backend="gpu", discrete_limit=4).fit(fx["ms_x"], fx["ms_y"])
+    assert set(m.top_features_) == {0}
+    np.testing.assert_allclose(m.feature_importances_[3], 0.0, atol=1e-7)
+    r = ReliefF(n_neighbors=1, n_features_to_select=2, discrete_limit=4, backend="gpu").fit(
+        fx["rs_x"], fx["rs_y"])
+    s = r.feature_importances_
+    assert s[0] > s[1] and s[2] > s[1] and set(r.top_features_) == {0, 2}
+    np.testing.assert_allclose(s[3], 0.0)
+    f = SURF(n_features_to_select=2, backend="gpu", discrete_limit=3).fit(fx["rs_x"], fx["rs_y"])
+    s = f.feature_importances_
+    assert s[0] > s[1] and s[2] > s[1] and set(f.top_features_) == {0, 2}
+    np.testing.assert_allclose(s[3], 0.0, atol=1e-7)
+    for est in (MultiSURF(backend="gpu", n_features_to_select=4),
+                SURF(backend="gpu"), ReliefF(backend="gpu", n_neighbors=2)):
+        x = fx["ms_x"] if isinstance(est, MultiSURF) else fx["rs_x"]
+        est.fit(x, np.zeros(x.shape[0]))
+        assert np.all(est.feature_importances_ <= 1e-7)
+
+
+@pytest.mark.parametrize("star", [False, True])
+def test_cfg1_multisurf(oracle, star):
+    """BASELINE cfg1 (README dataset, n=500 p=1000) vs the oracle; the
+    non-star top-15 also equals the reference's recorded top-15."""
+    import json
+
+    from fastselect_amd import MultiSURF
+    X, y = make_classification(n_samples=500, n_features=1000, n_informative=20,
+                               n_redundant=100, random_state=42)
+    s = _fit(MultiSURF, X, y, use_star=star, n_features_to_select=15)
+    ref = oracle.multisurf_scores(X, y, use_star=star)
+    assert_parity(s, ref, TOL, k=15)
+    if not star:
+        with open(os.path.join(GOLD, "cfg1_reference.json")) as f:
+            assert sorted(np.argsort(s)[::-1][:15].tolist()) == json.load(f)["top15"]
+
+
+@pytest.mark.parametrize("n,p,ncls,seed", [(129, 70, 2, 0), (257, 300, 3, 1), (1000, 2000, 2, 2),
+                                          (384, 5000, 2, 3)])
+def test_multisurf_sizes(oracle, n, p, ncls, seed):
+    from fastselect_amd import MultiSURF
+    X, y = make_classification(n_samples=n, n_features=p, n_informative=20,
+                               n_redundant=min(50, p // 4), n_classes=ncls, random_state=seed)
+    for star in (False, True):
+        assert_parity(_fit(MultiSURF, X, y, use_star=star), oracle.multisurf_scores(X, y, use_star=star),
+                      TOL, k=10)
+
+
+@pytest.mark.parametrize("n,p,seed", [(300, 400, 0), (700, 1500, 1)])
+def test_surf_sizes(oracle, n, p, seed):
+    from fastselect_amd import SURF
+    X, y = make_classification(n_samples=n, n_features=p, n_informative=20, n_redundant=30,
+                               random_state=seed)
+    for star in (False, True):
+        assert_parity(_fit(SURF, X, y, use_star=star), oracle.surf_scores(X, y, use_star=star),
+                      TOL, k=10)
+
+
+@pytest.mark.parametrize("n,p,ncls,k,seed", [(500, 300, 2, 10, 0), (600, 200, 5, 3, 1),
+                                            (300, 100, 3, 40, 2)])
+def test_relieff_sizes(oracle, n, p, ncls, k, seed):
+    from fastselect_amd import ReliefF
+    X, y = make_classification(n_samples=n, n_features=p, n_informative=10, n_redundant=10,
+                               n_classes=ncls, n_clusters_per_class=1, random_state=seed)
+    assert_parity(_fit(ReliefF, X, y, n_neighbors=k), oracle.relieff_scores(X, y, n_neighbors=k),
+                  TOL, k=10)
+
+
+def test_gpu_matches_cpu_backend():
+    """Same integer distances and weights on both product backends: scores
+    differ only by floating-point accumulation order."""
+    from fastselect_amd import SURF, MultiSURF, ReliefF
+    X, y = make_classification(n_samples=400, n_features=600, n_informative=15, random_state=9)
+    X[:, 3] = np.round(X[:, 3])
+    for cls, kw in ((MultiSURF, {}), (MultiSURF, {"use_star": True}), (SURF, {}),
+                    (SURF, {"use_star": True}), (ReliefF, {"n_neighbors": 7})):
+        g = cls(backend="gpu", **kw).fit(X, y).feature_importances_
+        c = cls(backend="cpu", **kw).fit(X, y).feature_importances_
+        assert scale_rel_err(g, c) < 1e-6, (cls.__name__, kw)
+
+
+def test_determinism():
+    from fastselect_amd import MultiSURF
+    X, y = make_classification(n_samples=700, n_features=900, random_state=4)
+    a = MultiSURF(backend="gpu", use_star=True).fit(X, y).feature_importances_
+    b = MultiSURF(backend="gpu", use_star=True).fit(X, y).feature_importances_
+    np.testing.assert_array_equal(a, b)
+
+
+def test_edge_cases(oracle):
+    from fastselect_amd import SURF, MultiSURF, ReliefF
+    rng = np.random.default_rng(11)
+    # n = 2, one feature
+    X = np.array([[0.0], [1.0]])
+    y = np.array([0, 1])
+    assert_parity(_fit(MultiSURF, X, y), oracle.multisurf_scores(X, y), TOL)
+    assert_parity(_fit(SURF, X, y), oracle.surf_scores(X, y), TOL)
+    # all-discrete data with duplicate rows (exact distance ties)
+    X = rng.integers(0, 3, size=(150, 12)).astype(float)
+    X[50:60] = X[0]
+    y = rng.integers(0, 2, 150)
+    assert_parity(_fit(MultiSURF, X, y), oracle.multisurf_scores(X, y), TOL)
+    assert_parity(_fit(SURF, X, y, use_star=True), oracle.surf_scores(X, y, use_star=True), TOL)
+    # mixed: many-level discrete, constant, continuous; discrete_limit large
+    X = np.column_stack([rng.integers(0, 9, 200), np.full(200, 7.0), rng.standard_normal((200, 5))])
+    y = rng.integers(0, 3, 200)
+    assert_parity(_fit(MultiSURF, X, y, discrete_limit=9), oracle.multisurf_scores(X, y, discrete_limit=9), TOL)
+    # k larger than a class
+    X, y = make_classification(n_samples=120, n_features=30, weights=[0.9], random_state=1)
+    with pytest.warns(UserWarning):
+        s = _fit(ReliefF, X, y, n_neighbors=20)
+    assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=20), TOL)
+
+
+def test_feat_idx_subset(oracle):
+    from fastselect_amd import _lib
+    X, y = make_classification(n_samples=260, n_features=90, random_state=3)
+    x = X.astype(np.float32)
+    r = (x.max(0) - x.min(0)).astype(np.float32)
+    recip = (1 / r).astype(np.float32)
+    fidx = np.array([5, 80, 3, 44, 44, 0], dtype=np.int64)
+    g = _lib.multisurf_score("gpu", x, y, recip, fidx, False, np.zeros(90, bool))
+    ref = oracle.multisurf_scores(X, y, feat_idx=fidx)
+    assert_parity(g, ref, TOL)
+
+
+def test_sharded_plans_sum_to_single():
+    """Tile sharding on one GPU: world=3 plans' exchanged partials, summed,
+    reproduce the world=1 result (the RCCL all-reduce is a sum)."""
+    import torch
+
+    from fastselect_amd import _lib
+    X, y = make_classification(n_samples=700, n_features=300, random_state=8)
+    x = X.astype(np.float32)
+    r = (x.max(0) - x.min(0)).astype(np.float32)
+    recip = (1 / r).astype(np.float32)
+    isd = np.zeros(300, bool)
+    n, p = x.shape
+
+    def run(world):
+        plans = [_lib.Plan("gpu", x, y, recip, isd, use_star=True, rank=rk, world=world)
+                 for rk in range(world)]
+        rs = [torch.zeros(2 * n, dtype=torch.float64, device="cuda") for _ in plans]
+        for pl, b in zip(plans, rs):
+            pl.pass1(b.data_ptr())
+        rsum = sum(rs)
+        cn = [torch.zeros(2 * n, dtype=torch.float64, device="cuda") for _ in plans]
+        for pl, b in zip(plans, cn):
+            pl.select(rsum.data_ptr(), b.data_ptr())
+        csum = sum(cn)
+        sc = [torch.zeros(p, dtype=torch.float64, device="cuda") for _ in plans]
+        for pl, b in zip(plans, sc):
+            pl.pass2(csum.data_ptr(), b.data_ptr())
+        torch.cuda.synchronize()
+        return (sum(sc) / n).float().cpu().numpy()
+
+    one = run(1)
+    three = run(3)
+    assert scale_rel_err(three, one) < 1e-6
+    ref = _lib.multisurf_score("gpu", x, y, recip, None, True, isd)
+    assert scale_rel_err(one, ref) < 1e-6
+
+
+def test_large_p_flush_path(oracle):
+    """p >> 256 exercises the packed high-word carry of the pass-1 integer
+    accumulators; distances must stay exact (GPU == CPU backend)."""
+    from fastselect_amd import MultiSURF
+    X, y = make_classification(n_samples=256, n_features=20000, n_informative=20,
+                               n_redundant=50, random_state=6)
+    g = MultiSURF(backend="gpu").fit(X, y).feature_importances_
+    c = MultiSURF(backend="cpu").fit(X, y).feature_importances_
+    assert scale_rel_err(g, c) < 1e-6
+    assert_parity(g, oracle.multisurf_scores(X, y), TOL, k=10)
