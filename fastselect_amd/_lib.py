@@ -41,7 +41,24 @@ EXPORTED = (
 )
 
 
+def _share_hip_runtime_with_torch() -> None:
+    """Load PyTorch's HIP runtime before ours when PyTorch is installed.
+
+    PyTorch-ROCm bundles its own libamdhip64 (SONAME libamdhip64.so.7, the
+    same SONAME as /opt/rocm's).  Whichever copy is mapped first is the one
+    both libraries bind to; if ours came first, torch would map a second HIP
+    runtime and fail with "No HIP GPUs are available".  Importing torch first
+    gives the process exactly one HIP runtime shared by torch (device memory,
+    streams, RCCL via torch.distributed) and the Relief kernels.
+    """
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def _load() -> ctypes.CDLL:
+    _share_hip_runtime_with_torch()
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"fastselect_amd native library not found at {LIB_PATH}; build it with "
@@ -62,7 +79,7 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_pass1.argtypes = [_vp, _vp]
     lib.fs_plan_select.argtypes = [_vp, _vp, _vp]
     lib.fs_plan_pass2.argtypes = [_vp, _vp, _vp]
-    lib.fs_plan_info.argtypes = [_vp, _i64p, _f64p]
+    lib.fs_plan_info.argtypes = [_vp, _i64p, _f64p, _i64p]
     lib.fs_plan_kernel_ms.argtypes = [_vp, _int]
     lib.fs_plan_kernel_ms.restype = ctypes.c_double
     lib.fs_plan_destroy.argtypes = [_vp]
@@ -167,7 +184,7 @@ def surf_score(backend, x, y, recip, use_star, is_discrete, n_jobs=-1, device=0)
 class Plan:
     """A sharded MultiSURF plan (``fs_plan_*``) for one rank.
 
-    Exchange buffers (rowstats[2n], counts[2n], scores[n_kept], float64) are
+    Exchange buffers (rowstats[2n], counts[3n], scores[n_kept], float64) are
     passed by address: device pointers for the GPU backend, host pointers for
     the CPU backend (see ``fastselect_amd.parallel``).
     """
@@ -199,10 +216,13 @@ class Plan:
         check(_lib.fs_plan_pass2(self._h, _vp(counts_ptr), _vp(scores_ptr)))
 
     def info(self):
+        """(owned tiles, pair-feature evaluations per step, rows refined last step)."""
         tiles = ctypes.c_int64(0)
         pfe = ctypes.c_double(0.0)
-        check(_lib.fs_plan_info(self._h, ctypes.byref(tiles), ctypes.byref(pfe)))
-        return int(tiles.value), float(pfe.value)
+        ref = ctypes.c_int64(0)
+        check(_lib.fs_plan_info(self._h, ctypes.byref(tiles), ctypes.byref(pfe),
+                                ctypes.byref(ref)))
+        return int(tiles.value), float(pfe.value), int(ref.value)
 
     def kernel_ms(self, which: int) -> float:
         return float(_lib.fs_plan_kernel_ms(self._h, int(which)))

@@ -62,10 +62,10 @@ int fs_multisurf_score(int backend, int device, const float* x, int64_t n, int64
   if (backend == FS_BACKEND_GPU) return gpu::multisurf_run(P, x, device, scores_out);
   std::vector<uint64_t> D;
   std::vector<float> xs;
-  std::vector<double> rs(2 * n), cnt(2 * n), thr, S(P.n_kept);
+  std::vector<double> rs(2 * n), cnt(3 * n), thr, S(P.n_kept);
   cpu::multisurf_pass1(P, x, 0, 0, 1, n_jobs, D, xs, rs.data());
   cpu::multisurf_select(P, D, 0, 1, rs.data(), thr, cnt.data(), n_jobs);
-  cpu::multisurf_pass2(P, D, xs, thr, cnt.data(), 0, 1, n_jobs, S.data());
+  cpu::multisurf_pass2(P, x, D, xs, thr, cnt.data(), 0, 1, n_jobs, S.data(), nullptr);
   for (int64_t k = 0; k < P.n_kept; k++) scores_out[k] = (float)(S[k] / (double)n);
   return FS_OK;
 }
@@ -135,6 +135,7 @@ struct fs_plan {
   std::vector<uint64_t> D;
   std::vector<float> xs;
   std::vector<double> thr;
+  int64_t refined = 0;
 };
 
 extern "C" {
@@ -204,16 +205,18 @@ int fs_plan_pass2(fs_plan* pl, const double* counts, double* scores) {
     return FS_EINVAL;
   }
   if (pl->g) return gpu::plan_pass2(pl->g, counts, scores);
-  return cpu::multisurf_pass2(pl->P, pl->D, pl->xs, pl->thr, counts, pl->rank, pl->world,
-                              pl->n_jobs, scores);
+  return cpu::multisurf_pass2(pl->P, pl->x.data(), pl->D, pl->xs, pl->thr, counts, pl->rank,
+                              pl->world, pl->n_jobs, scores, &pl->refined);
 }
 
-int fs_plan_info(const fs_plan* pl, int64_t* owned_tiles_out, double* pfe) {
+int fs_plan_info(const fs_plan* pl, int64_t* owned_tiles_out, double* pfe,
+                 int64_t* refined_rows) {
   if (!pl) {
     set_error("NULL plan");
     return FS_EINVAL;
   }
-  if (pl->g) return gpu::plan_info(pl->g, owned_tiles_out, pfe);
+  if (pl->g) return gpu::plan_info(pl->g, owned_tiles_out, pfe, refined_rows);
+  if (refined_rows) *refined_rows = pl->refined;
   std::vector<int32_t> bi, bj;
   owned_tiles(pl->P.n_pad / kTile, pl->rank, pl->world, bi, bj);
   if (owned_tiles_out) *owned_tiles_out = (int64_t)bi.size();

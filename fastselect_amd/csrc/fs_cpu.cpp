@@ -105,6 +105,33 @@ static inline bool owned(int64_t nb, int64_t i, int64_t j, int rank, int world) 
   return tile_linear(nb, a, b) % world == rank;
 }
 
+// Reference-exact distance row of sample i (same arithmetic as
+// k_exact_rows): float32 diffs for float32 X (MultiSURF.py:184-187,
+// ReliefF.py:151-154), float64 diffs for float64 X (SURF.py:153-156), summed
+// in float64.
+static void exact_row(const Prepared& P, const void* x, int x_is_f64, int64_t i,
+                      double* out) {
+  for (int64_t j = 0; j < P.n; j++) {
+    double acc = 0.0;
+    for (int64_t c = 0; c < P.pc; c++) {
+      const int64_t col = P.src_col[c];
+      if (x_is_f64) {
+        const double* X = (const double*)x;
+        acc += std::fabs(X[i * P.p_in + col] - X[j * P.p_in + col]) * P.scale[c];
+      } else {
+        const float* X = (const float*)x;
+        const float dv = std::fabs(X[i * P.p_in + col] - X[j * P.p_in + col]) * (float)P.scale[c];
+        acc += (double)dv;
+      }
+    }
+    for (int64_t c = P.PC; c < P.PC + P.pd; c++) {
+      const int64_t col = P.src_col[c];
+      acc += load_x(x, x_is_f64, i * P.p_in + col) != load_x(x, x_is_f64, j * P.p_in + col) ? 1.0 : 0.0;
+    }
+    out[j] = j == i ? 0.0 : acc;
+  }
+}
+
 int multisurf_pass1(const Prepared& P, const void* x, int x_is_f64, int rank, int world,
                     int n_jobs, std::vector<uint64_t>& D, std::vector<float>& xs,
                     double* rowstats) {
@@ -133,17 +160,21 @@ int multisurf_select(const Prepared& P, const std::vector<uint64_t>& D, int rank
   thr.assign(n, 0.0);
   parallel_for(n, n_jobs, [&](int64_t i) {
     const double t = multisurf_threshold(rowstats[2 * i], rowstats[2 * i + 1], n);
-    double h = 0.0, m = 0.0;
+    const double delta_q = P.amb_delta * P.SC;
+    double h = 0.0, m = 0.0, a = 0.0;
     for (int64_t j = 0; j < n; j++) {
       if (j == i || !owned(nb, i, j, rank, world)) continue;
-      if ((double)D[(size_t)i * n + j] < t) {
+      const double d = (double)D[(size_t)i * n + j];
+      if (d < t) {
         if (P.labels[j] == P.labels[i]) h += 1.0;
         else m += 1.0;
       }
+      if (std::fabs(d - t) < delta_q) a += 1.0;
     }
     thr[i] = t;
-    counts[2 * i] = h;
-    counts[2 * i + 1] = m;
+    counts[3 * i] = h;
+    counts[3 * i + 1] = m;
+    counts[3 * i + 2] = a;
   });
   return FS_OK;
 }
@@ -180,18 +211,52 @@ static void scatter_scores(const Prepared& P, const std::vector<double>& S_perm,
     if (P.out_pos[c] >= 0) scores[P.out_pos[c]] = S_perm[c];
 }
 
-int multisurf_pass2(const Prepared& P, const std::vector<uint64_t>& D,
+int multisurf_pass2(const Prepared& P, const void* x, const std::vector<uint64_t>& D,
                     const std::vector<float>& xs, const std::vector<double>& thr,
-                    const double* counts, int rank, int world, int n_jobs, double* scores) {
+                    const double* counts, int rank, int world, int n_jobs, double* scores,
+                    int64_t* refined_rows) {
   const int64_t n = P.n, nb = P.n_pad / kTile;
+  // Ambiguous rows (all-reduced counts) -> exact rows, thresholds and counts.
+  std::vector<double> H(n), M(n);
+  std::vector<int64_t> rows;
+  for (int64_t i = 0; i < n; i++) {
+    H[i] = counts[3 * i];
+    M[i] = counts[3 * i + 1];
+    if (counts[3 * i + 2] > 0.0) rows.push_back(i);
+  }
+  if (refined_rows) *refined_rows = (int64_t)rows.size();
+  std::vector<int64_t> rmap(n, -1);
+  std::vector<double> Dx(rows.size() * (size_t)n), thrx(rows.size());
+  parallel_for((int64_t)rows.size(), n_jobs, [&](int64_t r) {
+    const int64_t i = rows[r];
+    double* row = Dx.data() + (size_t)r * n;
+    exact_row(P, x, 0, i, row);
+    double s1 = 0.0, s2 = 0.0;
+    for (int64_t j = 0; j < n; j++)
+      if (j != i) {
+        s1 += row[j];
+        s2 += row[j] * row[j];
+      }
+    thrx[r] = multisurf_threshold(s1, s2, n);
+    double h = 0.0, m = 0.0;
+    for (int64_t j = 0; j < n; j++)
+      if (j != i && row[j] < thrx[r]) (P.labels[j] == P.labels[i] ? h : m) += 1.0;
+    H[i] = h;
+    M[i] = m;
+  });
+  for (size_t r = 0; r < rows.size(); r++) rmap[rows[r]] = (int64_t)r;
+  auto near = [&](int64_t i, int64_t j, double dq) {
+    const int64_t r = rmap[i];
+    return r >= 0 ? Dx[(size_t)r * n + j] < thrx[r] : dq < thr[i];
+  };
   std::vector<PairW> pairs;
   for (int64_t i = 0; i < n; i++)
     for (int64_t j = i + 1; j < n; j++) {
       if (!owned(nb, i, j, rank, world)) continue;
       const double d = (double)D[(size_t)i * n + j];
       const bool hit = P.labels[i] == P.labels[j];
-      const double wi = multisurf_weight(d < thr[i], hit, P.use_star, counts[2 * i], counts[2 * i + 1]);
-      const double wj = multisurf_weight(d < thr[j], hit, P.use_star, counts[2 * j], counts[2 * j + 1]);
+      const double wi = multisurf_weight(near(i, j, d), hit, P.use_star, H[i], M[i]);
+      const double wj = multisurf_weight(near(j, i, d), hit, P.use_star, H[j], M[j]);
       const float w = (float)(wi + wj);
       if (w != 0.0f) pairs.push_back({(int32_t)i, (int32_t)j, w});
     }
@@ -213,18 +278,37 @@ int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
   std::vector<float> Df((size_t)n * n);
   for (size_t e = 0; e < Df.size(); e++) Df[e] = (float)((double)D[e] * inv_sc);
   std::vector<double> avg(n);
+  std::vector<char> amb(n, 0);
   parallel_for(n, n_jobs, [&](int64_t i) {
     float s = 0.0f;
     for (int64_t j = 0; j < n; j++) s += Df[(size_t)i * n + j];
+    avg[i] = (double)s / (double)(n - 1);
+    const float af = (float)avg[i];
+    const double band = P.amb_delta + 4.0 * ((double)std::nextafter(af, 3.0e38f) - (double)af);
+    for (int64_t j = 0; j < n && !amb[i]; j++)
+      if (j != i && std::fabs((double)D[(size_t)i * n + j] * inv_sc - avg[i]) < band) amb[i] = 1;
+  });
+  // ambiguous rows: exact float32 distance row and exact sequential mean
+  std::vector<int64_t> rows;
+  for (int64_t i = 0; i < n; i++)
+    if (amb[i]) rows.push_back(i);
+  parallel_for((int64_t)rows.size(), n_jobs, [&](int64_t r) {
+    const int64_t i = rows[r];
+    std::vector<double> row(n);
+    exact_row(P, x, 1, i, row.data());
+    float s = 0.0f;
+    for (int64_t j = 0; j < n; j++) {
+      Df[(size_t)i * n + j] = (float)row[j];
+      s += (float)row[j];
+    }
     avg[i] = (double)s / (double)(n - 1);
   });
   std::vector<PairW> pairs;
   for (int64_t i = 0; i < n; i++)
     for (int64_t j = i + 1; j < n; j++) {
-      const double df = (double)Df[(size_t)i * n + j];
       const bool hit = P.labels[i] == P.labels[j];
-      const float w = (float)(surf_weight(df < avg[i], hit, P.use_star) +
-                              surf_weight(df < avg[j], hit, P.use_star));
+      const float w = (float)(surf_weight((double)Df[(size_t)i * n + j] < avg[i], hit, P.use_star) +
+                              surf_weight((double)Df[(size_t)j * n + i] < avg[j], hit, P.use_star));
       if (w != 0.0f) pairs.push_back({(int32_t)i, (int32_t)j, w});
     }
   std::vector<double> S(P.PW, 0.0);
@@ -263,7 +347,10 @@ int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
       const int64_t kc = std::min<int64_t>(k, (int64_t)v.size());
       if (kc == 0) continue;
       std::partial_sort(v.begin(), v.begin() + kc, v.end());
-      const double wgt = (c == li) ? -1.0 / (double)kc : (P.class_prior[c] / denom) / (double)k;
+      // self is a zero-diff hit when its class has < k other members
+      // (ReliefF.py:144-168: dists[i] = inf sorts last but is still scanned)
+      const int64_t h_found = kc < k ? kc + 1 : k;
+      const double wgt = (c == li) ? -1.0 / (double)h_found : (P.class_prior[c] / denom) / (double)k;
       for (int64_t col = 0; col < P.PW; col++) {
         double s = 0.0;
         for (int64_t t = 0; t < kc; t++) {

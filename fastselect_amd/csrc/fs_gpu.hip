@@ -310,11 +310,17 @@ __global__ __launch_bounds__(256) void k_rowstats(const double* __restrict__ D, 
   }
 }
 
+// Thresholds, near hit / miss counts and the number of "ambiguous" pairs
+// whose quantised distance lies within delta_q of the threshold (their near
+// decision could differ from the reference's; such rows are recomputed with
+// reference-exact arithmetic before the weights are built, see
+// k_exact_rows).  counts[3i .. 3i+2] = (H_i, M_i, A_i), partial over owned
+// tiles.
 __global__ __launch_bounds__(256) void k_select_ms(const double* __restrict__ D, int64_t n,
                                                    int64_t n_pad, int rank, int world,
                                                    const int32_t* __restrict__ lab,
                                                    const double* __restrict__ rowstats,
-                                                   double* __restrict__ thr,
+                                                   double delta_q, double* __restrict__ thr,
                                                    double* __restrict__ counts) {
   __shared__ double red[256];
   const int64_t i = blockIdx.x;
@@ -322,45 +328,162 @@ __global__ __launch_bounds__(256) void k_select_ms(const double* __restrict__ D,
   const double t = multisurf_threshold(rowstats[2 * i], rowstats[2 * i + 1], n);
   const int32_t li = lab[i];
   const double* row = D + i * n_pad;
-  double h = 0.0, m = 0.0;
+  double h = 0.0, m = 0.0, a = 0.0;
   for (int64_t j = threadIdx.x; j < n; j += 256) {
     if (j == i || !tile_owned(nb, bi, j / kTile, rank, world)) continue;
-    if (row[j] < t) {
+    const double d = row[j];
+    if (d < t) {
       if (lab[j] == li) h += 1.0;
       else m += 1.0;
     }
+    if (__builtin_fabs(d - t) < delta_q) a += 1.0;
   }
   h = block_sum_256(h, red);
   m = block_sum_256(m, red);
+  a = block_sum_256(a, red);
   if (threadIdx.x == 0) {
     thr[i] = t;
-    counts[2 * i] = h;
-    counts[2 * i + 1] = m;
+    counts[3 * i] = h;
+    counts[3 * i + 1] = m;
+    counts[3 * i + 2] = a;
   }
 }
 
 // SURF: avg_i = float32 sequential sum over j (self included, D_ii = 0) of
 // the float32 distance row, / (n - 1) in float64 (SURF.py:146-163).  Thread
 // i walks column i of the symmetric D so a wave's loads are coalesced.
+// amb[i] = 1 when some pair sits within delta (+ 4 ulps of the mean) of it.
 __global__ __launch_bounds__(256) void k_surf_avg(const double* __restrict__ D, int64_t n,
-                                                  int64_t n_pad, double inv_sc,
-                                                  double* __restrict__ avg) {
+                                                  int64_t n_pad, double inv_sc, double delta,
+                                                  double* __restrict__ avg,
+                                                  int32_t* __restrict__ amb) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   float s = 0.0f;
   for (int64_t j = 0; j < n; j++) s += (float)(D[j * n_pad + i] * inv_sc);
-  avg[i] = (double)s / (double)(n - 1);
+  const double a = (double)s / (double)(n - 1);
+  avg[i] = a;
+  const float af = (float)a;
+  const double band = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(af) + 1u) - (double)af);
+  int32_t flag = 0;
+  for (int64_t j = 0; j < n && !flag; j++)
+    if (j != i && __builtin_fabs(D[j * n_pad + i] * inv_sc - a) < band) flag = 1;
+  amb[i] = flag;
+}
+
+// Reference-exact distance rows for the ambiguous rows: Dx[r][j] =
+// sum_f diff_f(i, j) accumulated in float64, with diff_f computed exactly as
+// the reference kernels do it (MultiSURF.py:184-187 / ReliefF.py:151-154 in
+// float32, SURF.py:153-156 in float64).  One wave per (row, j); lanes stride
+// the permuted feature columns.
+template <typename T>
+__global__ __launch_bounds__(256) void k_exact_rows(
+    const T* __restrict__ x, int64_t n, int64_t p_in, int64_t PW, int64_t pc, int64_t PC,
+    int64_t pd, const int64_t* __restrict__ src_col, const double* __restrict__ scl,
+    const int32_t* __restrict__ rows, double* __restrict__ Dx) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t r = blockIdx.y;
+  const int64_t i = rows[r];
+  const T* xi = x + i * p_in;
+  for (int64_t j = (int64_t)blockIdx.x * 4 + wave; j < n; j += (int64_t)gridDim.x * 4) {
+    const T* xj = x + j * p_in;
+    double acc = 0.0;
+    for (int64_t c = lane; c < pc; c += 64) {
+      const int64_t col = src_col[c];
+      if (sizeof(T) == 4) {
+        const float dv = __builtin_fabsf((float)xi[col] - (float)xj[col]) * (float)scl[c];
+        acc += (double)dv;
+      } else {
+        acc += __builtin_fabs((double)xi[col] - (double)xj[col]) * scl[c];
+      }
+    }
+    for (int64_t c = PC + lane; c < PC + pd; c += 64) {
+      const int64_t col = src_col[c];
+      acc += (xi[col] != xj[col]) ? 1.0 : 0.0;
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if (lane == 0) Dx[r * n + j] = (j == i) ? 0.0 : acc;
+  }
+}
+
+// Exact MultiSURF statistics of the ambiguous rows: threshold (real units)
+// and full-row near hit / miss counts, which replace the quantised ones.
+__global__ __launch_bounds__(256) void k_exact_ms_stats(const double* __restrict__ Dx,
+                                                        int64_t n,
+                                                        const int32_t* __restrict__ rows,
+                                                        const int32_t* __restrict__ lab,
+                                                        double* __restrict__ thrx,
+                                                        double* __restrict__ cnt) {
+  __shared__ double red[256];
+  const int64_t r = blockIdx.x;
+  const int64_t i = rows[r];
+  const double* row = Dx + r * n;
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += 256) {
+    if (j == i) continue;
+    s1 += row[j];
+    s2 += row[j] * row[j];
+  }
+  s1 = block_sum_256(s1, red);
+  s2 = block_sum_256(s2, red);
+  const double t = multisurf_threshold(s1, s2, n);
+  const int32_t li = lab[i];
+  double h = 0.0, m = 0.0;
+  for (int64_t j = threadIdx.x; j < n; j += 256) {
+    if (j == i || !(row[j] < t)) continue;
+    if (lab[j] == li) h += 1.0;
+    else m += 1.0;
+  }
+  h = block_sum_256(h, red);
+  m = block_sum_256(m, red);
+  if (threadIdx.x == 0) {
+    thrx[r] = t;
+    cnt[2 * i] = h;
+    cnt[2 * i + 1] = m;
+  }
+}
+
+// Exact SURF mean of the ambiguous rows: float32 sequential sum of the
+// float32-rounded exact distances (self = 0), one thread per row.
+__global__ void k_exact_surf_avg(const double* __restrict__ Dx, int64_t n, int64_t nref,
+                                 double* __restrict__ thrx) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= nref) return;
+  float s = 0.0f;
+  for (int64_t j = 0; j < n; j++) s += (float)Dx[r * n + j];
+  thrx[r] = (double)s / (double)(n - 1);
 }
 
 // ---------------------------------------------------------------------------
 // Pair weights per owned tile: Wt[t][jj][ii] = W_ij + W_ji for i < j
 // ---------------------------------------------------------------------------
+// Row i's near decision uses the quantised D against thr[i] unless i is an
+// ambiguous row (rmap[i] = r >= 0), which uses its exact row Dx[r] against
+// thrx[r].  cnt = (H, M) per row after the exact rows were patched in.
+__device__ __forceinline__ bool near_of(int64_t i, int64_t j, double dq, int algo,
+                                        double inv_sc, const double* __restrict__ thr,
+                                        const int32_t* __restrict__ rmap,
+                                        const double* __restrict__ Dx,
+                                        const double* __restrict__ thrx, int64_t n) {
+  const int32_t r = rmap[i];
+  if (algo == ALGO_MULTISURF) {
+    if (r >= 0) return Dx[(int64_t)r * n + j] < thrx[r];
+    return dq < thr[i];
+  }
+  if (r >= 0) return (double)(float)Dx[(int64_t)r * n + j] < thrx[r];
+  return (double)(float)(dq * inv_sc) < thr[i];
+}
+
 __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, int64_t n,
                                                  int64_t n_pad, const int2* __restrict__ tiles,
                                                  const double* __restrict__ thr,
                                                  const int32_t* __restrict__ lab,
-                                                 const double* __restrict__ counts, int algo,
+                                                 const double* __restrict__ cnt, int algo,
                                                  int use_star, double inv_sc,
+                                                 const int32_t* __restrict__ rmap,
+                                                 const double* __restrict__ Dx,
+                                                 const double* __restrict__ thrx,
                                                  float* __restrict__ Wt) {
   const int2 tl = tiles[blockIdx.x];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
@@ -372,19 +495,29 @@ __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, i
     if (i < n && j < n && (tl.x < tl.y || ii < jj)) {
       const double d = D[j * n_pad + i];  // == D[i][j]
       const bool hit = lab[i] == lab[j];
+      const bool ni = near_of(i, j, d, algo, inv_sc, thr, rmap, Dx, thrx, n);
+      const bool nj = near_of(j, i, d, algo, inv_sc, thr, rmap, Dx, thrx, n);
       double wi, wj;
       if (algo == ALGO_MULTISURF) {
-        wi = multisurf_weight(d < thr[i], hit, use_star, counts[2 * i], counts[2 * i + 1]);
-        wj = multisurf_weight(d < thr[j], hit, use_star, counts[2 * j], counts[2 * j + 1]);
-      } else {  // SURF: float32 distance against the float64 mean
-        const double df = (double)(float)(d * inv_sc);
-        wi = surf_weight(df < thr[i], hit, use_star);
-        wj = surf_weight(df < thr[j], hit, use_star);
+        wi = multisurf_weight(ni, hit, use_star, cnt[2 * i], cnt[2 * i + 1]);
+        wj = multisurf_weight(nj, hit, use_star, cnt[2 * j], cnt[2 * j + 1]);
+      } else {
+        wi = surf_weight(ni, hit, use_star);
+        wj = surf_weight(nj, hit, use_star);
       }
       w = (float)(wi + wj);
     }
     out[jj * kTile + ii] = w;
   }
+}
+
+// cnt[2i], cnt[2i+1] = counts[3i], counts[3i+1]
+__global__ void k_counts_hm(const double* __restrict__ counts, int64_t n,
+                            double* __restrict__ cnt) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  cnt[2 * i] = counts[3 * i];
+  cnt[2 * i + 1] = counts[3 * i + 1];
 }
 
 // ---------------------------------------------------------------------------
@@ -585,7 +718,12 @@ __global__ __launch_bounds__(256) void k_rf_update(const float* __restrict__ xs,
     for (int cl = 0; cl < n_classes; cl++) {
       const int32_t found = nfound[i * n_classes + cl];
       if (found == 0) continue;
-      const double wgt = (cl == li) ? -1.0 / (double)found : (prior[cl] / denom) / (double)k;
+      // The reference scans the full argsort order, in which the focal sample
+      // itself (distance inf, last) is taken as a hit whenever its class has
+      // fewer than k other members: it adds a zero diff but counts in
+      // h_found (ReliefF.py:144-168, 211-212).
+      const int64_t h_found = found < k ? (int64_t)found + 1 : k;
+      const double wgt = (cl == li) ? -1.0 / (double)h_found : (prior[cl] / denom) / (double)k;
       const int32_t* lst = nbr + (i * n_classes + cl) * k;
       double s = 0.0;
       for (int32_t t = 0; t < found; t++) {
@@ -626,6 +764,14 @@ struct Plan {
   double* thr = nullptr;
   float* Wt = nullptr;
   double* spart = nullptr;
+  // exact refinement of ambiguous rows
+  int32_t* rmap = nullptr;     // [n_pad] row -> refined slot or -1
+  double* cnt = nullptr;       // [2n] effective (H, M)
+  int32_t* amb = nullptr;      // [n] SURF ambiguity flags
+  int32_t* rows = nullptr;     // [cap] refined row ids
+  double* Dx = nullptr;        // [cap][n] exact distance rows
+  double* thrx = nullptr;      // [cap] exact thresholds
+  int64_t ref_cap = 0, n_refined = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   float ms_dist = -1.0f, ms_score = -1.0f;
   std::vector<void*> owned;
@@ -730,7 +876,9 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       (rc = dalloc(g, &g->xqT, (size_t)Q.PW * Q.n_pad)) ||
       (rc = dalloc(g, &g->xs, (size_t)Q.n_pad * Q.PW)) ||
       (rc = dalloc(g, &g->D, (size_t)Q.n_pad * Q.n_pad)) ||
-      (rc = dalloc(g, &g->tiles, g->n_tiles)) || (rc = dalloc(g, &g->thr, Q.n_pad)))
+      (rc = dalloc(g, &g->tiles, g->n_tiles)) || (rc = dalloc(g, &g->thr, Q.n_pad)) ||
+      (rc = dalloc(g, &g->rmap, Q.n_pad)) || (rc = dalloc(g, &g->cnt, 2 * Q.n_pad)) ||
+      (rc = dalloc(g, &g->amb, Q.n_pad)))
     return fail(rc);
   if (Q.algo != ALGO_RELIEFF) {
     if ((rc = dalloc(g, &g->Wt, (size_t)g->n_tiles * kTile * kTile)) ||
@@ -819,20 +967,66 @@ int plan_select(Plan* g, const double* rowstats, double* counts) {
   const Prepared& Q = g->P;
   FS_HIP(hipSetDevice(g->device));
   k_select_ms<<<(unsigned)Q.n, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->rank, g->world,
-                                                    g->lab, rowstats, g->thr, counts);
+                                                    g->lab, rowstats, Q.amb_delta * Q.SC,
+                                                    g->thr, counts);
   FS_TRY(launch_check("k_select_ms"));
   if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
   return FS_OK;
 }
 
+// Recompute the listed rows with reference-exact arithmetic (Dx, thrx) and
+// publish the row -> slot map.  `rows` is host data.
+static int refine_rows(Plan* g, const std::vector<int32_t>& rows) {
+  const Prepared& Q = g->P;
+  const int64_t nref = (int64_t)rows.size();
+  g->n_refined = nref;
+  std::vector<int32_t> rmap(Q.n_pad, -1);
+  for (int64_t r = 0; r < nref; r++) rmap[rows[r]] = (int32_t)r;
+  FS_TRY(h2d(g, g->rmap, rmap.data(), Q.n_pad));
+  if (nref == 0) return FS_OK;
+  if (nref > g->ref_cap) {
+    int64_t cap = std::max<int64_t>(nref, 2 * g->ref_cap);
+    FS_TRY(dalloc(g, &g->rows, cap));
+    FS_TRY(dalloc(g, &g->Dx, (size_t)cap * Q.n));
+    FS_TRY(dalloc(g, &g->thrx, cap));
+    g->ref_cap = cap;
+  }
+  FS_TRY(h2d(g, g->rows, rows.data(), nref));
+  const unsigned gx = (unsigned)std::min<int64_t>((Q.n + 3) / 4, 1024);
+  if (g->x_is_f64)
+    k_exact_rows<double><<<dim3(gx, (unsigned)nref), 256, 0, g->stream>>>(
+        (const double*)g->x, Q.n, Q.p_in, Q.PW, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, g->rows,
+        g->Dx);
+  else
+    k_exact_rows<float><<<dim3(gx, (unsigned)nref), 256, 0, g->stream>>>(
+        (const float*)g->x, Q.n, Q.p_in, Q.PW, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, g->rows,
+        g->Dx);
+  return launch_check("k_exact_rows");
+}
+
 int plan_pass2(Plan* g, const double* counts, double* scores) {
   const Prepared& Q = g->P;
   FS_HIP(hipSetDevice(g->device));
+  k_counts_hm<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(counts, Q.n, g->cnt);
+  FS_TRY(launch_check("k_counts_hm"));
+  // rows with an ambiguous pair (all-reduced counts: identical on every rank)
+  std::vector<double> hc(3 * Q.n);
+  FS_HIP(hipMemcpyAsync(hc.data(), counts, sizeof(double) * 3 * Q.n, hipMemcpyDeviceToHost,
+                        g->stream));
+  FS_HIP(hipStreamSynchronize(g->stream));
+  std::vector<int32_t> rows;
+  for (int64_t i = 0; i < Q.n; i++)
+    if (hc[3 * i + 2] > 0.0) rows.push_back((int32_t)i);
+  FS_TRY(refine_rows(g, rows));
+  if (!rows.empty()) {
+    k_exact_ms_stats<<<(unsigned)rows.size(), 256, 0, g->stream>>>(g->Dx, Q.n, g->rows, g->lab,
+                                                                  g->thrx, g->cnt);
+    FS_TRY(launch_check("k_exact_ms_stats"));
+  }
   if (g->n_tiles > 0) {
-    k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
-                                                           g->thr, g->lab, counts,
-                                                           ALGO_MULTISURF, Q.use_star,
-                                                           1.0 / Q.SC, g->Wt);
+    k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(
+        g->D, Q.n, Q.n_pad, g->tiles, g->thr, g->lab, g->cnt, ALGO_MULTISURF, Q.use_star,
+        1.0 / Q.SC, g->rmap, g->Dx, g->thrx, g->Wt);
     FS_TRY(launch_check("k_weights"));
   }
   FS_TRY(run_pass2(g, scores));
@@ -840,13 +1034,14 @@ int plan_pass2(Plan* g, const double* counts, double* scores) {
   return FS_OK;
 }
 
-int plan_info(const Plan* g, int64_t* tiles, double* pfe) {
+int plan_info(const Plan* g, int64_t* tiles, double* pfe, int64_t* refined) {
   if (tiles) *tiles = g->n_tiles;
   if (pfe) {
     // pairs visited by both passes (diagonal tiles count their full 128x128
     // pass-1 work) x real features
     *pfe = 2.0 * (double)g->n_tiles * kTile * kTile * (double)(g->P.pc + g->P.pd);
   }
+  if (refined) *refined = g->n_refined;
   return FS_OK;
 }
 
@@ -878,7 +1073,7 @@ int multisurf_run(const Prepared& P, const void* x, int device, float* scores_ou
   FS_TRY(plan_create(&g, P, x, 0, device, 0, 1, 0));
   double *rs = nullptr, *cnt = nullptr, *sc = nullptr;
   int rc;
-  if ((rc = dalloc(g, &rs, 2 * P.n)) || (rc = dalloc(g, &cnt, 2 * P.n)) ||
+  if ((rc = dalloc(g, &rs, 2 * P.n)) || (rc = dalloc(g, &cnt, 3 * P.n)) ||
       (rc = dalloc(g, &sc, P.n_kept)) || (rc = plan_pass1(g, rs)) ||
       (rc = plan_select(g, rs, cnt)) || (rc = plan_pass2(g, cnt, sc)) ||
       (rc = finish_scores(g, sc, scores_out))) {
@@ -897,14 +1092,27 @@ int surf_run(const Prepared& P, const void* x, int device, float* scores_out) {
   int rc = dalloc(g, &sc, Q.n_kept);
   if (rc == FS_OK) rc = run_quantize_dist(g);
   if (rc == FS_OK) {
-    k_surf_avg<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad,
-                                                                    1.0 / Q.SC, g->thr);
+    k_surf_avg<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(
+        g->D, Q.n, Q.n_pad, 1.0 / Q.SC, Q.amb_delta, g->thr, g->amb);
     rc = launch_check("k_surf_avg");
   }
+  std::vector<int32_t> amb(Q.n), rows;
+  if (rc == FS_OK && hipMemcpyAsync(amb.data(), g->amb, sizeof(int32_t) * Q.n,
+                                    hipMemcpyDeviceToHost, g->stream) != hipSuccess)
+    rc = FS_EHIP;
+  if (rc == FS_OK && hipStreamSynchronize(g->stream) != hipSuccess) rc = FS_EHIP;
+  for (int64_t i = 0; i < Q.n; i++)
+    if (amb[i]) rows.push_back((int32_t)i);
+  if (rc == FS_OK) rc = refine_rows(g, rows);
+  if (rc == FS_OK && !rows.empty()) {
+    k_exact_surf_avg<<<(unsigned)((rows.size() + 255) / 256), 256, 0, g->stream>>>(
+        g->Dx, Q.n, (int64_t)rows.size(), g->thrx);
+    rc = launch_check("k_exact_surf_avg");
+  }
   if (rc == FS_OK) {
-    k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
-                                                           g->thr, g->lab, nullptr, ALGO_SURF,
-                                                           Q.use_star, 1.0 / Q.SC, g->Wt);
+    k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(
+        g->D, Q.n, Q.n_pad, g->tiles, g->thr, g->lab, nullptr, ALGO_SURF, Q.use_star,
+        1.0 / Q.SC, g->rmap, g->Dx, g->thrx, g->Wt);
     rc = launch_check("k_weights");
   }
   if (rc == FS_OK) rc = run_pass2(g, sc);

@@ -65,6 +65,10 @@ struct Prepared {
   std::vector<double> class_prior; // ReliefF priors (float32 values widened)
   double SC = 0.0;                 // integer units per scaled-diff unit
   uint32_t SCu = 0;                // SC as an integer (discrete mismatch cost)
+  // Half-width (real distance units) of the band around a row's threshold
+  // inside which a quantised near/far decision is not trusted; rows with a
+  // pair in the band are recomputed with reference-exact arithmetic.
+  double amb_delta = 0.0;
 };
 
 // Build the permutation, label codes, discrete tables and integer scale.
@@ -117,9 +121,10 @@ int multisurf_pass1(const Prepared& P, const void* x, int x_is_f64, int rank, in
 int multisurf_select(const Prepared& P, const std::vector<uint64_t>& D, int rank, int world,
                      const double* rowstats, std::vector<double>& thr, double* counts,
                      int n_jobs);
-int multisurf_pass2(const Prepared& P, const std::vector<uint64_t>& D,
+int multisurf_pass2(const Prepared& P, const void* x, const std::vector<uint64_t>& D,
                     const std::vector<float>& xs, const std::vector<double>& thr,
-                    const double* counts, int rank, int world, int n_jobs, double* scores);
+                    const double* counts, int rank, int world, int n_jobs, double* scores,
+                    int64_t* refined_rows);
 int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores);
 int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores);
 }  // namespace cpu
@@ -133,7 +138,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
 int plan_pass1(Plan* g, double* rowstats_dev);
 int plan_select(Plan* g, const double* rowstats_dev, double* counts_dev);
 int plan_pass2(Plan* g, const double* counts_dev, double* scores_dev);
-int plan_info(const Plan* g, int64_t* tiles, double* pfe);
+int plan_info(const Plan* g, int64_t* tiles, double* pfe, int64_t* refined);
 double plan_kernel_ms(const Plan* g, int which);
 void plan_destroy(Plan* g);
 // Single-GPU one-shot runs (host in/out, scores already divided by n).

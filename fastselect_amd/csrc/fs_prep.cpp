@@ -143,6 +143,13 @@ int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64
   }
   P.SC = sc;
   P.SCu = (uint32_t)sc;
+  // Error model of a quantised distance vs the reference's (float64 sum of
+  // float32-rounded diffs): per continuous feature a rounding error of at
+  // most 1/SC (std ~ 1/sqrt(6)/SC) plus the reference's own float32
+  // rounding (< 1.2e-7 relative).  16 standard deviations of the sum bound
+  // both the distance and the threshold error with a wide margin.
+  const double pcd = (double)P.pc;
+  P.amb_delta = 16.0 * std::sqrt(pcd / 6.0 + 1.0) / sc + 4.0e-7 * std::sqrt(pcd);
   return 0;
 }
 
