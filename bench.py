@@ -1,0 +1,197 @@
+"""Benchmark: MultiSURF feature scoring on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 20000 --p 20000]
+
+For N > 1 launch one process per GPU with torch.distributed.run; the pair
+tiles are sharded round-robin over the ranks and the three small exchange
+vectors are summed with RCCL all-reduces (fastselect_amd/parallel.py).
+
+Workload (BASELINE.json configs[3], the north-star target "MultiSURF on
+20000x20000 fp32"; it fits one GPU, so N=1 runs the same job): make_classification(
+n_samples=20000, n_features=20000, n_informative=20, n_redundant=100,
+random_state=42), X cast to float32 once on the host, MultiSURF (non-star).
+One step = one full scoring pass over the HBM-resident X: quantize, pass 1
+(distance tiles), thresholds/neighbour counts, exact refinement of ambiguous
+rows, pair weights, pass 2 (score accumulation), all-reduces, / n.
+
+Rank 0 prints ONE JSON line: value = n*p / step time (feature-scores/s, the
+whole job across all ranks), a `roofline` object for the dominant kernel
+(VALU bound; algorithmic FLOPs = 2 per pair-feature evaluation)
+measured with HIP events on the stream the kernels run on, and at N=1 a
+`cpu_baseline` from the C oracle (oracle/relief_oracle.c, OpenMP) timed on a
+bounded sample of focal samples of the same data and extrapolated.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# fp32 VALU peak for non-FMA adds/subs: 256 CU x 128 lanes x 2.4 GHz
+# (the 157.3 TFLOP/s spec counts an FMA as 2 FLOPs; MI355X_MICROARCH.md)
+VALU_PEAK_TFLOPS = 78.6
+HBM_PEAK_GBPS = 8000.0
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def make_data(n, p, seed):
+    from sklearn.datasets import make_classification
+    X, y = make_classification(n_samples=n, n_features=p, n_informative=20, n_redundant=100,
+                               random_state=seed)
+    return X.astype(np.float32), y
+
+
+def cpu_baseline(x, y, budget_s=15.0):
+    """Oracle MultiSURF on the first m focal samples, extrapolated to n."""
+    from oracle import oracle as O
+    O.build()
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    threads = min(threads, 16)
+    n, p = x.shape
+    m = threads
+    t0 = time.perf_counter()
+    O.multisurf_scores(x, y, i_range=(0, m), n_jobs=threads)
+    t = time.perf_counter() - t0
+    if t < budget_s / 3:
+        m = int(min(n, max(m, threads * round(budget_s / t))))
+        t0 = time.perf_counter()
+        O.multisurf_scores(x, y, i_range=(0, m), n_jobs=threads)
+        t = time.perf_counter() - t0
+    t_full = t * n / m
+    return {"value": n * p / t_full, "unit": "feature-scores/s", "cores": threads,
+            "kind": "port",
+            "sample": f"oracle MultiSURF (C/OpenMP restatement of the reference backend='cpu') "
+                      f"on focal samples [0, {m}) of the same {n}x{p} data: {t:.2f} s, "
+                      f"extrapolated x{n / m:.1f} to {t_full:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=20000)
+    ap.add_argument("--p", type=int, default=20000)
+    ap.add_argument("--seed", type=int, default=42)
+    ap.add_argument("--star", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    from fastselect_amd import _lib
+    from fastselect_amd.parallel import ShardedMultiSURF
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+
+    t0 = time.perf_counter()
+    x, y = make_data(args.n, args.p, args.seed)
+    ranges = (x.max(axis=0) - x.min(axis=0)).astype(np.float32)
+    ranges[ranges == 0] = 1
+    recip = (1.0 / ranges).astype(np.float32)
+    # make_classification columns are continuous; the estimator's np.unique
+    # discrete detection (host, ~2 s here) is part of fit(), not of a step
+    is_disc = np.zeros(args.p, dtype=bool)
+    log(f"rank {rank}/{world}: data {args.n}x{args.p} ready in {time.perf_counter() - t0:.1f} s")
+
+    job = ShardedMultiSURF(x, y, recip, is_disc, use_star=args.star, backend="gpu", device=local)
+    tiles, _, _ = job.info()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for w in range(args.warmup):
+        job.step()
+        torch.cuda.synchronize()
+        log(f"warmup {w} done")
+    barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    dist_ms, score_ms = [], []
+    for s in range(args.steps):
+        scores = job.step()
+        dist_ms.append(job.kernel_ms(0))
+        score_ms.append(job.kernel_ms(1))
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    _, _, refined = job.info()
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # dominant kernel roofline (rank-local launch; PFE per launch = owned
+    # tiles x 128^2 x p, FLOPs = 2 per PFE)
+    d_ms, s_ms = float(np.mean(dist_ms)), float(np.mean(score_ms))
+    # algorithmic count: unique pairs x features (padding and the duplicated
+    # half of diagonal tiles are executed but not counted)
+    pfe_launch = args.n * (args.n - 1) / 2.0 * args.p / world
+    kern = {"k_dist": d_ms, "k_score": s_ms}
+    dom = max(kern, key=kern.get)
+    achieved = 2.0 * pfe_launch / (kern[dom] * 1e-3) / 1e12
+    # algorithmic HBM bytes of k_dist per launch: both LDS panels of every
+    # owned tile once + the D tile written twice (f64)
+    alg_bytes = {"k_dist": tiles * (2 * 128 * args.p * 4 + 2 * 128 * 128 * 8),
+                 "k_score": tiles * (2 * 128 * args.p * 4 + 128 * 128 * 4)}
+
+    if rank == 0:
+        out = {
+            "metric": "feature-scores/sec (n*p/s) MultiSURF fp32",
+            "value": args.n * args.p / (ms_per_step * 1e-3),
+            "unit": "feature-scores/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "fp32 (u32 exact integer distances)",
+            "data": "synthetic make_classification(n_informative=20, n_redundant=100, random_state=42)",
+            "config": {"workload": f"MultiSURF{'*' if args.star else ''} n={args.n} p={args.p} "
+                                   f"(BASELINE configs[3])",
+                       "n_samples": args.n, "n_features": args.p,
+                       "parallelism": f"pair-tile shard x{world}, RCCL all-reduce"},
+            "roofline": {
+                "bound": "valu", "kernel": dom, "achieved": achieved,
+                "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / VALU_PEAK_TFLOPS,
+                "traffic": None,
+                "flop_per_pfe": 2,
+                "kernel_ms": kern,
+                "pfe_per_launch": pfe_launch,
+                "hbm_alg_GBps": {k: alg_bytes[k] / (kern[k] * 1e-3) / 1e9 for k in kern},
+                "hbm_peak_GBps": HBM_PEAK_GBPS,
+            },
+            "refined_rows": refined,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            log("timing CPU baseline (oracle) ...")
+            out["cpu_baseline"] = cpu_baseline(x, y)
+        print(json.dumps(out), flush=True)
+    job.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -184,7 +184,7 @@ def surf_score(backend, x, y, recip, use_star, is_discrete, n_jobs=-1, device=0)
 class Plan:
     """A sharded MultiSURF plan (``fs_plan_*``) for one rank.
 
-    Exchange buffers (rowstats[2n], counts[3n], scores[n_kept], float64) are
+    Exchange buffers (rowstats[2n], counts[2n], scores[n_kept], float64) are
     passed by address: device pointers for the GPU backend, host pointers for
     the CPU backend (see ``fastselect_amd.parallel``).
     """
@@ -216,7 +216,7 @@ class Plan:
         check(_lib.fs_plan_pass2(self._h, _vp(counts_ptr), _vp(scores_ptr)))
 
     def info(self):
-        """(owned tiles, pair-feature evaluations per step, rows refined last step)."""
+        """(owned tiles, pair-feature evaluations per step, pairs refined last step)."""
         tiles = ctypes.c_int64(0)
         pfe = ctypes.c_double(0.0)
         ref = ctypes.c_int64(0)

@@ -60,12 +60,11 @@ int fs_multisurf_score(int backend, int device, const float* x, int64_t n, int64
   if (encode_labels_f64(P, y)) return FS_EINVAL;
   P.use_star = use_star ? 1 : 0;
   if (backend == FS_BACKEND_GPU) return gpu::multisurf_run(P, x, device, scores_out);
-  std::vector<uint64_t> D;
-  std::vector<float> xs;
-  std::vector<double> rs(2 * n), cnt(3 * n), thr, S(P.n_kept);
-  cpu::multisurf_pass1(P, x, 0, 0, 1, n_jobs, D, xs, rs.data());
-  cpu::multisurf_select(P, D, 0, 1, rs.data(), thr, cnt.data(), n_jobs);
-  cpu::multisurf_pass2(P, x, D, xs, thr, cnt.data(), 0, 1, n_jobs, S.data(), nullptr);
+  cpu::CpuState st;
+  std::vector<double> rs(2 * n), cnt(2 * n), S(P.n_kept);
+  cpu::multisurf_pass1(P, x, 0, 1, n_jobs, st, rs.data());
+  cpu::multisurf_select(P, x, 0, 1, rs.data(), n_jobs, st, cnt.data());
+  cpu::multisurf_pass2(P, st, cnt.data(), 0, 1, n_jobs, S.data());
   for (int64_t k = 0; k < P.n_kept; k++) scores_out[k] = (float)(S[k] / (double)n);
   return FS_OK;
 }
@@ -132,10 +131,7 @@ struct fs_plan {
   gpu::Plan* g = nullptr;
   // CPU state
   std::vector<float> x;
-  std::vector<uint64_t> D;
-  std::vector<float> xs;
-  std::vector<double> thr;
-  int64_t refined = 0;
+  cpu::CpuState st;
 };
 
 extern "C" {
@@ -185,8 +181,8 @@ int fs_plan_pass1(fs_plan* pl, double* rowstats) {
     return FS_EINVAL;
   }
   if (pl->g) return gpu::plan_pass1(pl->g, rowstats);
-  return cpu::multisurf_pass1(pl->P, pl->x.data(), 0, pl->rank, pl->world, pl->n_jobs, pl->D,
-                              pl->xs, rowstats);
+  return cpu::multisurf_pass1(pl->P, pl->x.data(), pl->rank, pl->world, pl->n_jobs, pl->st,
+                              rowstats);
 }
 
 int fs_plan_select(fs_plan* pl, const double* rowstats, double* counts) {
@@ -195,8 +191,8 @@ int fs_plan_select(fs_plan* pl, const double* rowstats, double* counts) {
     return FS_EINVAL;
   }
   if (pl->g) return gpu::plan_select(pl->g, rowstats, counts);
-  return cpu::multisurf_select(pl->P, pl->D, pl->rank, pl->world, rowstats, pl->thr, counts,
-                               pl->n_jobs);
+  return cpu::multisurf_select(pl->P, pl->x.data(), pl->rank, pl->world, rowstats, pl->n_jobs,
+                               pl->st, counts);
 }
 
 int fs_plan_pass2(fs_plan* pl, const double* counts, double* scores) {
@@ -205,8 +201,7 @@ int fs_plan_pass2(fs_plan* pl, const double* counts, double* scores) {
     return FS_EINVAL;
   }
   if (pl->g) return gpu::plan_pass2(pl->g, counts, scores);
-  return cpu::multisurf_pass2(pl->P, pl->x.data(), pl->D, pl->xs, pl->thr, counts, pl->rank,
-                              pl->world, pl->n_jobs, scores, &pl->refined);
+  return cpu::multisurf_pass2(pl->P, pl->st, counts, pl->rank, pl->world, pl->n_jobs, scores);
 }
 
 int fs_plan_info(const fs_plan* pl, int64_t* owned_tiles_out, double* pfe,
@@ -216,7 +211,7 @@ int fs_plan_info(const fs_plan* pl, int64_t* owned_tiles_out, double* pfe,
     return FS_EINVAL;
   }
   if (pl->g) return gpu::plan_info(pl->g, owned_tiles_out, pfe, refined_rows);
-  if (refined_rows) *refined_rows = pl->refined;
+  if (refined_rows) *refined_rows = pl->st.refined;
   std::vector<int32_t> bi, bj;
   owned_tiles(pl->P.n_pad / kTile, pl->rank, pl->world, bi, bj);
   if (owned_tiles_out) *owned_tiles_out = (int64_t)bi.size();

@@ -1,21 +1,22 @@
 // fs_cpu.cpp -- native multithreaded CPU backend (backend='cpu').
 //
-// Runs the same pipeline as the GPU backend (fs_internal.h) with the same
-// integer distances, thresholds and pair weights, on std::threads; only the
-// order of the floating-point score accumulation differs.  Built with
-// -ffp-contract=off so the quantisation rounds exactly like k_quantize.  This is the
-// product's CPU path -- it is NOT the parity oracle (oracle/ restates the
-// reference kernels independently and is never linked here).
+// Runs the same pipeline as the GPU backend (fs_internal.h): the same
+// integer distances, mean correction, thresholds, ambiguous-pair refinement
+// and pair weights, on std::threads; only the order of the floating-point
+// score accumulation differs.  Built with -ffp-contract=off so the
+// quantisation rounds exactly like k_quantize.  This is the product's CPU
+// path -- it is NOT the parity oracle (oracle/ restates the reference kernels
+// independently and is never linked here).
 #include <algorithm>
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <thread>
 
 #include "../../include/fastselect_amd.h"
 #include "fs_internal.h"
-
 
 namespace fs {
 namespace cpu {
@@ -41,12 +42,14 @@ static inline double load_x(const void* x, int x_is_f64, int64_t idx) {
   return x_is_f64 ? ((const double*)x)[idx] : (double)((const float*)x)[idx];
 }
 
-// Same arithmetic as k_quantize (fs_gpu.hip): q = trunc((x - off) * qs + 0.5)
-// with every double operation rounded separately.
+// Same arithmetic as k_quantize (fs_gpu.hip): t = (x - off) * qs,
+// q = trunc(t + 0.5), eps = q - t, every double operation rounded separately.
 static void quantize(const Prepared& P, const void* x, int x_is_f64, int n_jobs,
-                     std::vector<uint32_t>& xq, std::vector<float>& xs) {
+                     std::vector<uint32_t>& xq, std::vector<float>& xs,
+                     std::vector<float>* eps) {
   xq.assign((size_t)P.n * P.PW, 0);
   xs.assign((size_t)P.n * P.PW, 0.0f);
+  if (eps) eps->assign((size_t)P.n * P.PW, 0.0f);
   std::vector<double> qs(P.PW);
   for (int64_t c = 0; c < P.PW; c++) qs[c] = P.scale[c] * P.SC;
   parallel_for(P.n, n_jobs, [&](int64_t i) {
@@ -58,10 +61,10 @@ static void quantize(const Prepared& P, const void* x, int x_is_f64, int n_jobs,
       float v;
       if (c < P.pc) {
         const double u = xv - P.offset[c];
-        double t = u * qs[c];
-        t = t + 0.5;
-        q = (uint32_t)t;
+        const double t = u * qs[c];
+        q = (uint32_t)(t + 0.5);
         v = (float)(u * P.scale[c]);
+        if (eps) (*eps)[(size_t)i * P.PW + c] = (float)((double)q - t);
       } else {
         const double* b = P.dtab.data() + P.dtab_off[c];
         const double* e = P.dtab.data() + P.dtab_off[c + 1];
@@ -74,10 +77,17 @@ static void quantize(const Prepared& P, const void* x, int x_is_f64, int n_jobs,
   });
 }
 
+static inline bool owned(int64_t nb, int64_t i, int64_t j, int rank, int world) {
+  if (world == 1) return true;
+  int64_t a = i / kTile, b = j / kTile;
+  if (a > b) std::swap(a, b);
+  return tile_linear(nb, a, b) % world == rank;
+}
+
 static void distances(const Prepared& P, const std::vector<uint32_t>& xq, int rank, int world,
-                      int n_jobs, std::vector<uint64_t>& D) {
+                      int n_jobs, std::vector<double>& D) {
   const int64_t n = P.n, nb = P.n_pad / kTile;
-  D.assign((size_t)n * n, 0);
+  D.assign((size_t)n * n, 0.0);
   std::vector<int32_t> bi, bj;
   owned_tiles(nb, rank, world, bi, bj);
   parallel_for((int64_t)bi.size(), n_jobs, [&](int64_t t) {
@@ -91,59 +101,105 @@ static void distances(const Prepared& P, const std::vector<uint32_t>& xq, int ra
         uint64_t mism = 0;
         for (int64_t c = P.PC; c < P.PW; c++) mism += a[c] != b[c];
         d += mism * (uint64_t)P.SCu;
-        D[(size_t)i * n + j] = d;
-        D[(size_t)j * n + i] = d;
+        D[(size_t)i * n + j] = (double)d;
+        D[(size_t)j * n + i] = (double)d;
       }
     }
   });
 }
 
-static inline bool owned(int64_t nb, int64_t i, int64_t j, int rank, int world) {
-  if (world == 1) return true;
-  int64_t a = i / kTile, b = j / kTile;
-  if (a > b) std::swap(a, b);
-  return tile_linear(nb, a, b) % world == rank;
-}
-
-// Reference-exact distance row of sample i (same arithmetic as
-// k_exact_rows): float32 diffs for float32 X (MultiSURF.py:184-187,
-// ReliefF.py:151-154), float64 diffs for float64 X (SURF.py:153-156), summed
-// in float64.
-static void exact_row(const Prepared& P, const void* x, int x_is_f64, int64_t i,
-                      double* out) {
-  for (int64_t j = 0; j < P.n; j++) {
-    double acc = 0.0;
-    for (int64_t c = 0; c < P.pc; c++) {
-      const int64_t col = P.src_col[c];
-      if (x_is_f64) {
-        const double* X = (const double*)x;
-        acc += std::fabs(X[i * P.p_in + col] - X[j * P.p_in + col]) * P.scale[c];
-      } else {
-        const float* X = (const float*)x;
-        const float dv = std::fabs(X[i * P.p_in + col] - X[j * P.p_in + col]) * (float)P.scale[c];
-        acc += (double)dv;
-      }
+// Mean correction of k_colrank / k_rowcorr: per continuous column a
+// 4096-bin histogram of q gives midranks, corr[i] = sum_c eps*(2 rank-(n-1)).
+static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
+                            const std::vector<float>& eps, int n_jobs, std::vector<double>& corr) {
+  const int64_t n = P.n;
+  constexpr int kBins = 4096;
+  int shift = 0;
+  while (P.qmax / std::ldexp(1.0, shift) >= (double)kBins) shift++;
+  std::vector<float> term((size_t)n * std::max<int64_t>(P.pc, 1), 0.0f);
+  parallel_for(P.pc, n_jobs, [&](int64_t c) {
+    std::vector<uint32_t> cum(kBins + 1, 0);
+    for (int64_t i = 0; i < n; i++)
+      cum[std::min<int64_t>(xq[(size_t)i * P.PW + c] >> shift, kBins - 1) + 1]++;
+    for (int b = 0; b < kBins; b++) cum[b + 1] += cum[b];
+    for (int64_t i = 0; i < n; i++) {
+      const int64_t b = std::min<int64_t>(xq[(size_t)i * P.PW + c] >> shift, kBins - 1);
+      const double rank = (double)cum[b] + 0.5 * (double)(cum[b + 1] - cum[b] - 1u);
+      term[(size_t)i * P.pc + c] =
+          (float)((double)eps[(size_t)i * P.PW + c] * (2.0 * rank - (double)(n - 1)));
     }
-    for (int64_t c = P.PC; c < P.PC + P.pd; c++) {
-      const int64_t col = P.src_col[c];
-      acc += load_x(x, x_is_f64, i * P.p_in + col) != load_x(x, x_is_f64, j * P.p_in + col) ? 1.0 : 0.0;
-    }
-    out[j] = j == i ? 0.0 : acc;
+  });
+  corr.assign(n, 0.0);
+  for (int64_t i = 0; i < n; i++) {
+    double s = 0.0;
+    for (int64_t c = 0; c < P.pc; c++) s += (double)term[(size_t)i * P.pc + c];
+    corr[i] = s;
   }
 }
 
-int multisurf_pass1(const Prepared& P, const void* x, int x_is_f64, int rank, int world,
-                    int n_jobs, std::vector<uint64_t>& D, std::vector<float>& xs,
-                    double* rowstats) {
+// Reference-exact distance of one pair (same arithmetic as k_exact_pairs):
+// float32 diffs for float32 X (MultiSURF.py:184-187, ReliefF.py:151-154),
+// float64 diffs for float64 X (SURF.py:153-156), summed in float64.
+static double exact_pair(const Prepared& P, const void* x, int x_is_f64, int64_t i, int64_t j) {
+  double acc = 0.0;
+  for (int64_t c = 0; c < P.pc; c++) {
+    const int64_t col = P.src_col[c];
+    if (x_is_f64) {
+      const double* X = (const double*)x;
+      acc += std::fabs(X[i * P.p_in + col] - X[j * P.p_in + col]) * P.scale[c];
+    } else {
+      const float* X = (const float*)x;
+      const float dv = std::fabs(X[i * P.p_in + col] - X[j * P.p_in + col]) * (float)P.scale[c];
+      acc += (double)dv;
+    }
+  }
+  for (int64_t c = P.PC; c < P.PC + P.pd; c++) {
+    const int64_t col = P.src_col[c];
+    acc += load_x(x, x_is_f64, i * P.p_in + col) != load_x(x, x_is_f64, j * P.p_in + col) ? 1.0
+                                                                                          : 0.0;
+  }
+  return acc;
+}
+
+// Flag and refine the ambiguous owned pairs (k_flag_pairs + k_exact_pairs).
+template <typename Amb>
+static int64_t refine_pairs(const Prepared& P, const void* x, int x_is_f64, int rank, int world,
+                            int n_jobs, std::vector<double>& D, Amb&& ambiguous) {
+  const int64_t n = P.n, nb = P.n_pad / kTile;
+  std::vector<std::pair<int32_t, int32_t>> pairs;
+  std::mutex mu;
+  parallel_for(n, n_jobs, [&](int64_t i) {
+    std::vector<std::pair<int32_t, int32_t>> loc;
+    for (int64_t j = i + 1; j < n; j++)
+      if (owned(nb, i, j, rank, world) && ambiguous(i, j, D[(size_t)i * n + j]))
+        loc.push_back({(int32_t)i, (int32_t)j});
+    if (!loc.empty()) {
+      std::lock_guard<std::mutex> g(mu);
+      pairs.insert(pairs.end(), loc.begin(), loc.end());
+    }
+  });
+  parallel_for((int64_t)pairs.size(), n_jobs, [&](int64_t k) {
+    const int64_t i = pairs[k].first, j = pairs[k].second;
+    const double v = exact_pair(P, x, x_is_f64, i, j) * P.SC;
+    D[(size_t)i * n + j] = v;
+    D[(size_t)j * n + i] = v;
+  });
+  return (int64_t)pairs.size();
+}
+
+int multisurf_pass1(const Prepared& P, const void* x, int rank, int world, int n_jobs,
+                    CpuState& S, double* rowstats) {
   std::vector<uint32_t> xq;
-  quantize(P, x, x_is_f64, n_jobs, xq, xs);
-  distances(P, xq, rank, world, n_jobs, D);
+  std::vector<float> eps;
+  quantize(P, x, 0, n_jobs, xq, S.xs, &eps);
+  mean_correction(P, xq, eps, n_jobs, S.corr);
+  distances(P, xq, rank, world, n_jobs, S.D);
   const int64_t n = P.n, nb = P.n_pad / kTile;
   parallel_for(n, n_jobs, [&](int64_t i) {
     double s1 = 0.0, s2 = 0.0;
     for (int64_t j = 0; j < n; j++) {
       if (j == i || !owned(nb, i, j, rank, world)) continue;
-      const double d = (double)D[(size_t)i * n + j];
+      const double d = S.D[(size_t)i * n + j];
       s1 += d;
       s2 += d * d;
     }
@@ -153,28 +209,32 @@ int multisurf_pass1(const Prepared& P, const void* x, int x_is_f64, int rank, in
   return FS_OK;
 }
 
-int multisurf_select(const Prepared& P, const std::vector<uint64_t>& D, int rank, int world,
-                     const double* rowstats, std::vector<double>& thr, double* counts,
-                     int n_jobs) {
+int multisurf_select(const Prepared& P, const void* x, int rank, int world,
+                     const double* rowstats, int n_jobs, CpuState& S, double* counts) {
   const int64_t n = P.n, nb = P.n_pad / kTile;
-  thr.assign(n, 0.0);
-  parallel_for(n, n_jobs, [&](int64_t i) {
-    const double t = multisurf_threshold(rowstats[2 * i], rowstats[2 * i + 1], n);
-    const double delta_q = P.amb_delta * P.SC;
-    double h = 0.0, m = 0.0, a = 0.0;
+  S.thr.assign(n, 0.0);
+  const double nm1 = (double)(n - 1);
+  for (int64_t i = 0; i < n; i++) {  // k_thr_ms
+    const double mu = rowstats[2 * i] / nm1;
+    double var = rowstats[2 * i + 1] / nm1 - mu * mu;
+    if (var < 0.0) var = 0.0;
+    S.thr[i] = (mu - S.corr[i] / nm1) - 0.5 * std::sqrt(var);
+  }
+  const double dq = P.amb_delta * P.SC;
+  S.refined = refine_pairs(P, x, 0, rank, world, n_jobs, S.D, [&](int64_t i, int64_t j, double d) {
+    return std::fabs(d - S.thr[i]) < dq || std::fabs(d - S.thr[j]) < dq;
+  });
+  parallel_for(n, n_jobs, [&](int64_t i) {  // k_count_ms
+    double h = 0.0, m = 0.0;
     for (int64_t j = 0; j < n; j++) {
       if (j == i || !owned(nb, i, j, rank, world)) continue;
-      const double d = (double)D[(size_t)i * n + j];
-      if (d < t) {
+      if (S.D[(size_t)i * n + j] < S.thr[i]) {
         if (P.labels[j] == P.labels[i]) h += 1.0;
         else m += 1.0;
       }
-      if (std::fabs(d - t) < delta_q) a += 1.0;
     }
-    thr[i] = t;
-    counts[3 * i] = h;
-    counts[3 * i + 1] = m;
-    counts[3 * i + 2] = a;
+    counts[2 * i] = h;
+    counts[2 * i + 1] = m;
   });
   return FS_OK;
 }
@@ -211,104 +271,58 @@ static void scatter_scores(const Prepared& P, const std::vector<double>& S_perm,
     if (P.out_pos[c] >= 0) scores[P.out_pos[c]] = S_perm[c];
 }
 
-int multisurf_pass2(const Prepared& P, const void* x, const std::vector<uint64_t>& D,
-                    const std::vector<float>& xs, const std::vector<double>& thr,
-                    const double* counts, int rank, int world, int n_jobs, double* scores,
-                    int64_t* refined_rows) {
+int multisurf_pass2(const Prepared& P, const CpuState& S, const double* counts, int rank,
+                    int world, int n_jobs, double* scores) {
   const int64_t n = P.n, nb = P.n_pad / kTile;
-  // Ambiguous rows (all-reduced counts) -> exact rows, thresholds and counts.
-  std::vector<double> H(n), M(n);
-  std::vector<int64_t> rows;
-  for (int64_t i = 0; i < n; i++) {
-    H[i] = counts[3 * i];
-    M[i] = counts[3 * i + 1];
-    if (counts[3 * i + 2] > 0.0) rows.push_back(i);
-  }
-  if (refined_rows) *refined_rows = (int64_t)rows.size();
-  std::vector<int64_t> rmap(n, -1);
-  std::vector<double> Dx(rows.size() * (size_t)n), thrx(rows.size());
-  parallel_for((int64_t)rows.size(), n_jobs, [&](int64_t r) {
-    const int64_t i = rows[r];
-    double* row = Dx.data() + (size_t)r * n;
-    exact_row(P, x, 0, i, row);
-    double s1 = 0.0, s2 = 0.0;
-    for (int64_t j = 0; j < n; j++)
-      if (j != i) {
-        s1 += row[j];
-        s2 += row[j] * row[j];
-      }
-    thrx[r] = multisurf_threshold(s1, s2, n);
-    double h = 0.0, m = 0.0;
-    for (int64_t j = 0; j < n; j++)
-      if (j != i && row[j] < thrx[r]) (P.labels[j] == P.labels[i] ? h : m) += 1.0;
-    H[i] = h;
-    M[i] = m;
-  });
-  for (size_t r = 0; r < rows.size(); r++) rmap[rows[r]] = (int64_t)r;
-  auto near = [&](int64_t i, int64_t j, double dq) {
-    const int64_t r = rmap[i];
-    return r >= 0 ? Dx[(size_t)r * n + j] < thrx[r] : dq < thr[i];
-  };
   std::vector<PairW> pairs;
   for (int64_t i = 0; i < n; i++)
     for (int64_t j = i + 1; j < n; j++) {
       if (!owned(nb, i, j, rank, world)) continue;
-      const double d = (double)D[(size_t)i * n + j];
+      const double d = S.D[(size_t)i * n + j];
       const bool hit = P.labels[i] == P.labels[j];
-      const double wi = multisurf_weight(near(i, j, d), hit, P.use_star, H[i], M[i]);
-      const double wj = multisurf_weight(near(j, i, d), hit, P.use_star, H[j], M[j]);
+      const double wi =
+          multisurf_weight(d < S.thr[i], hit, P.use_star, counts[2 * i], counts[2 * i + 1]);
+      const double wj =
+          multisurf_weight(d < S.thr[j], hit, P.use_star, counts[2 * j], counts[2 * j + 1]);
       const float w = (float)(wi + wj);
       if (w != 0.0f) pairs.push_back({(int32_t)i, (int32_t)j, w});
     }
-  std::vector<double> S(P.PW, 0.0);
-  weighted_sum(P, xs, pairs, n_jobs, S.data());
-  scatter_scores(P, S, scores);
+  std::vector<double> Sp(P.PW, 0.0);
+  weighted_sum(P, S.xs, pairs, n_jobs, Sp.data());
+  scatter_scores(P, Sp, scores);
   return FS_OK;
 }
 
 int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
   std::vector<uint32_t> xq;
   std::vector<float> xs;
-  std::vector<uint64_t> D;
-  quantize(P, x, 1, n_jobs, xq, xs);
+  std::vector<double> D;
+  quantize(P, x, 1, n_jobs, xq, xs, nullptr);
   distances(P, xq, 0, 1, n_jobs, D);
   const int64_t n = P.n;
   const double inv_sc = 1.0 / P.SC;
   // float32 distance row, float32 sequential mean (SURF.py:146-163)
-  std::vector<float> Df((size_t)n * n);
-  for (size_t e = 0; e < Df.size(); e++) Df[e] = (float)((double)D[e] * inv_sc);
   std::vector<double> avg(n);
-  std::vector<char> amb(n, 0);
   parallel_for(n, n_jobs, [&](int64_t i) {
     float s = 0.0f;
-    for (int64_t j = 0; j < n; j++) s += Df[(size_t)i * n + j];
+    for (int64_t j = 0; j < n; j++) s += (float)(D[(size_t)i * n + j] * inv_sc);
     avg[i] = (double)s / (double)(n - 1);
-    const float af = (float)avg[i];
-    const double band = P.amb_delta + 4.0 * ((double)std::nextafter(af, 3.0e38f) - (double)af);
-    for (int64_t j = 0; j < n && !amb[i]; j++)
-      if (j != i && std::fabs((double)D[(size_t)i * n + j] * inv_sc - avg[i]) < band) amb[i] = 1;
   });
-  // ambiguous rows: exact float32 distance row and exact sequential mean
-  std::vector<int64_t> rows;
-  for (int64_t i = 0; i < n; i++)
-    if (amb[i]) rows.push_back(i);
-  parallel_for((int64_t)rows.size(), n_jobs, [&](int64_t r) {
-    const int64_t i = rows[r];
-    std::vector<double> row(n);
-    exact_row(P, x, 1, i, row.data());
-    float s = 0.0f;
-    for (int64_t j = 0; j < n; j++) {
-      Df[(size_t)i * n + j] = (float)row[j];
-      s += (float)row[j];
-    }
-    avg[i] = (double)s / (double)(n - 1);
+  auto band = [&](int64_t i) {
+    const float a = (float)avg[i];
+    return P.amb_delta + 4.0 * ((double)std::nextafter(a, 3.0e38f) - (double)a);
+  };
+  refine_pairs(P, x, 1, 0, 1, n_jobs, D, [&](int64_t i, int64_t j, double d) {
+    const double df = d * inv_sc;
+    return std::fabs(df - avg[i]) < band(i) || std::fabs(df - avg[j]) < band(j);
   });
   std::vector<PairW> pairs;
   for (int64_t i = 0; i < n; i++)
     for (int64_t j = i + 1; j < n; j++) {
+      const double df = (double)(float)(D[(size_t)i * n + j] * inv_sc);
       const bool hit = P.labels[i] == P.labels[j];
-      const float w = (float)(surf_weight((double)Df[(size_t)i * n + j] < avg[i], hit, P.use_star) +
-                              surf_weight((double)Df[(size_t)j * n + i] < avg[j], hit, P.use_star));
+      const float w = (float)(surf_weight(df < avg[i], hit, P.use_star) +
+                              surf_weight(df < avg[j], hit, P.use_star));
       if (w != 0.0f) pairs.push_back({(int32_t)i, (int32_t)j, w});
     }
   std::vector<double> S(P.PW, 0.0);
@@ -320,8 +334,8 @@ int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
 int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
   std::vector<uint32_t> xq;
   std::vector<float> xs;
-  std::vector<uint64_t> D;
-  quantize(P, x, 0, n_jobs, xq, xs);
+  std::vector<double> D;
+  quantize(P, x, 0, n_jobs, xq, xs, nullptr);
   distances(P, xq, 0, 1, n_jobs, D);
   const int64_t n = P.n, k = P.k_neighbors;
   const int C = P.n_classes;
@@ -332,7 +346,7 @@ int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
     std::vector<std::vector<std::pair<uint32_t, int32_t>>> cand(C);
     for (int64_t j = 0; j < n; j++) {
       if (j == i) continue;
-      const float df = (float)((double)D[(size_t)i * n + j] * inv_sc);
+      const float df = (float)(D[(size_t)i * n + j] * inv_sc);
       uint32_t key;
       std::memcpy(&key, &df, 4);
       cand[P.labels[j]].push_back({key, (int32_t)j});
@@ -350,7 +364,8 @@ int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
       // self is a zero-diff hit when its class has < k other members
       // (ReliefF.py:144-168: dists[i] = inf sorts last but is still scanned)
       const int64_t h_found = kc < k ? kc + 1 : k;
-      const double wgt = (c == li) ? -1.0 / (double)h_found : (P.class_prior[c] / denom) / (double)k;
+      const double wgt =
+          (c == li) ? -1.0 / (double)h_found : (P.class_prior[c] / denom) / (double)k;
       for (int64_t col = 0; col < P.PW; col++) {
         double s = 0.0;
         for (int64_t t = 0; t < kc; t++) {

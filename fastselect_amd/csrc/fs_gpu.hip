@@ -100,11 +100,12 @@ __device__ __forceinline__ double block_sum_256(double v, double* red) {
 template <typename T>
 __global__ __launch_bounds__(256) void k_quantize(
     const T* __restrict__ x, int64_t n, int64_t n_pad, int64_t p_in, int64_t PW, int64_t pc,
-    int64_t PC, int64_t pd, const int64_t* __restrict__ src_col, const double* __restrict__ off,
+    const int64_t* __restrict__ src_col, const double* __restrict__ off,
     const double* __restrict__ qs, const double* __restrict__ scl,
     const int64_t* __restrict__ dtab_off, const double* __restrict__ dtab,
-    uint32_t* __restrict__ xqT, float* __restrict__ xs) {
+    uint32_t* __restrict__ xqT, float* __restrict__ xs, float* __restrict__ epsT) {
   __shared__ uint32_t tile[64][65];
+  __shared__ float etile[64][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int64_t c0 = (int64_t)blockIdx.x * 64, i0 = (int64_t)blockIdx.y * 64;
   const int64_t c = c0 + tx;
@@ -113,12 +114,14 @@ __global__ __launch_bounds__(256) void k_quantize(
   for (int r = ty; r < 64; r += 4) {
     const int64_t i = i0 + r;
     uint32_t q = 0;
-    float v = 0.0f;
+    float v = 0.0f, e = 0.0f;
     if (i < n && col >= 0) {
       const double xv = (double)x[i * p_in + col];
       if (is_cont) {
         const double u = __dadd_rn(xv, -off[c]);
-        q = (uint32_t)__dadd_rn(__dmul_rn(u, qs[c]), 0.5);
+        const double t = __dmul_rn(u, qs[c]);
+        q = (uint32_t)__dadd_rn(t, 0.5);
+        e = (float)((double)q - t);  // rounding error in integer units
         v = (float)__dmul_rn(u, scl[c]);
       } else {
         int64_t lo = dtab_off[c], hi = dtab_off[c + 1] - 1;
@@ -133,11 +136,77 @@ __global__ __launch_bounds__(256) void k_quantize(
     }
     xs[i * PW + c] = v;
     tile[r][tx] = q;
+    etile[r][tx] = e;
   }
-  (void)PC;
-  (void)pd;
   __syncthreads();
-  for (int r = ty; r < 64; r += 4) xqT[(c0 + r) * n_pad + i0 + tx] = tile[tx][r];
+  for (int r = ty; r < 64; r += 4) {
+    xqT[(c0 + r) * n_pad + i0 + tx] = tile[tx][r];
+    epsT[(c0 + r) * n_pad + i0 + tx] = etile[tx][r];
+  }
+}
+
+// Mean-distance correction.  With q = round(t), t = (x - min) * recip * SC,
+// the quantised row mean is biased by (1/(n-1)) sum_f eps_if (2 rank_if -
+// (n-1)) where eps = q - t and rank_if is the rank of sample i in column f
+// (sum_j sign(t_if - t_jf)); the other error terms are random and ~sqrt(n)
+// smaller.  Ranks come from a 4096-bin histogram of q (midrank
+// inside a bin); the rank error it leaves is far below the reference's own
+// float32 rounding.  In place: epsT[c][i] <- eps * (2 rank - (n-1)).
+constexpr int kRankBins = 4096;
+__global__ __launch_bounds__(256) void k_colrank(const uint32_t* __restrict__ xqT, int64_t n,
+                                                 int64_t n_pad, int shift,
+                                                 float* __restrict__ epsT) {
+  __shared__ uint32_t hist[kRankBins];
+  __shared__ uint32_t wsum[4];
+  const int64_t c = blockIdx.x;
+  const uint32_t* q = xqT + c * n_pad;
+  float* e = epsT + c * n_pad;
+  for (int b = threadIdx.x; b < kRankBins; b += 256) hist[b] = 0;
+  __syncthreads();
+  for (int64_t i = threadIdx.x; i < n; i += 256) atomicAdd(&hist[min((int)(q[i] >> shift), kRankBins - 1)], 1u);
+  __syncthreads();
+  // exclusive scan of 4096 bins: 256 threads x 16 bins
+  uint32_t loc[16], run = 0;
+  const int base = threadIdx.x * 16;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    loc[k] = run;
+    run += hist[base + k];
+  }
+  // block scan of the per-thread totals
+  uint32_t v = run;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(v, o);
+    if (lane >= o) v += t;
+  }
+  if (lane == 63) wsum[wave] = v;
+  __syncthreads();
+  uint32_t wpre = 0;
+  for (int w = 0; w < wave; w++) wpre += wsum[w];
+  const uint32_t excl = wpre + v - run;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 16; k++) hist[base + k] = excl + loc[k];  // exclusive cumulative count
+  __syncthreads();
+  // midrank needs the bin count too: cum[b+1] - cum[b]
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    const int b = min((int)(q[i] >> shift), kRankBins - 1);
+    const uint32_t lo = hist[b];
+    const uint32_t hi = b + 1 < kRankBins ? hist[b + 1] : (uint32_t)n;
+    const double rank = (double)lo + 0.5 * (double)(hi - lo - 1u);
+    e[i] = (float)((double)e[i] * (2.0 * rank - (double)(n - 1)));
+  }
+}
+
+// corr[i] = sum over continuous columns of the per-feature bias terms.
+__global__ void k_rowcorr(const float* __restrict__ epsT, int64_t n, int64_t n_pad, int64_t pc,
+                          double* __restrict__ corr) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.0;
+  for (int64_t c = 0; c < pc; c++) s += (double)epsT[c * n_pad + i];
+  corr[i] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -310,84 +379,88 @@ __global__ __launch_bounds__(256) void k_rowstats(const double* __restrict__ D, 
   }
 }
 
-// Thresholds, near hit / miss counts and the number of "ambiguous" pairs
-// whose quantised distance lies within delta_q of the threshold (their near
-// decision could differ from the reference's; such rows are recomputed with
-// reference-exact arithmetic before the weights are built, see
-// k_exact_rows).  counts[3i .. 3i+2] = (H_i, M_i, A_i), partial over owned
-// tiles.
-__global__ __launch_bounds__(256) void k_select_ms(const double* __restrict__ D, int64_t n,
-                                                   int64_t n_pad, int rank, int world,
-                                                   const int32_t* __restrict__ lab,
-                                                   const double* __restrict__ rowstats,
-                                                   double delta_q, double* __restrict__ thr,
-                                                   double* __restrict__ counts) {
-  __shared__ double red[256];
-  const int64_t i = blockIdx.x;
-  const int64_t nb = n_pad / kTile, bi = i / kTile;
-  const double t = multisurf_threshold(rowstats[2 * i], rowstats[2 * i + 1], n);
-  const int32_t li = lab[i];
-  const double* row = D + i * n_pad;
-  double h = 0.0, m = 0.0, a = 0.0;
-  for (int64_t j = threadIdx.x; j < n; j += 256) {
-    if (j == i || !tile_owned(nb, bi, j / kTile, rank, world)) continue;
-    const double d = row[j];
-    if (d < t) {
-      if (lab[j] == li) h += 1.0;
-      else m += 1.0;
-    }
-    if (__builtin_fabs(d - t) < delta_q) a += 1.0;
-  }
-  h = block_sum_256(h, red);
-  m = block_sum_256(m, red);
-  a = block_sum_256(a, red);
-  if (threadIdx.x == 0) {
-    thr[i] = t;
-    counts[3 * i] = h;
-    counts[3 * i + 1] = m;
-    counts[3 * i + 2] = a;
-  }
+// MultiSURF threshold (integer units): the quantised mean corrected by
+// corr[i]/(n-1), minus half the quantised spread (MultiSURF.py:193-196).
+__global__ void k_thr_ms(const double* __restrict__ rowstats, const double* __restrict__ corr,
+                         int64_t n, double* __restrict__ thr) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double nm1 = (double)(n - 1);
+  const double mu = rowstats[2 * i] / nm1;
+  double var = rowstats[2 * i + 1] / nm1 - mu * mu;
+  if (var < 0.0) var = 0.0;
+  thr[i] = (mu - corr[i] / nm1) - 0.5 * __builtin_sqrt(var);
 }
 
 // SURF: avg_i = float32 sequential sum over j (self included, D_ii = 0) of
 // the float32 distance row, / (n - 1) in float64 (SURF.py:146-163).  Thread
 // i walks column i of the symmetric D so a wave's loads are coalesced.
-// amb[i] = 1 when some pair sits within delta (+ 4 ulps of the mean) of it.
 __global__ __launch_bounds__(256) void k_surf_avg(const double* __restrict__ D, int64_t n,
-                                                  int64_t n_pad, double inv_sc, double delta,
-                                                  double* __restrict__ avg,
-                                                  int32_t* __restrict__ amb) {
+                                                  int64_t n_pad, double inv_sc,
+                                                  double* __restrict__ avg) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   float s = 0.0f;
   for (int64_t j = 0; j < n; j++) s += (float)(D[j * n_pad + i] * inv_sc);
-  const double a = (double)s / (double)(n - 1);
-  avg[i] = a;
-  const float af = (float)a;
-  const double band = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(af) + 1u) - (double)af);
-  int32_t flag = 0;
-  for (int64_t j = 0; j < n && !flag; j++)
-    if (j != i && __builtin_fabs(D[j * n_pad + i] * inv_sc - a) < band) flag = 1;
-  amb[i] = flag;
+  avg[i] = (double)s / (double)(n - 1);
 }
 
-// Reference-exact distance rows for the ambiguous rows: Dx[r][j] =
-// sum_f diff_f(i, j) accumulated in float64, with diff_f computed exactly as
-// the reference kernels do it (MultiSURF.py:184-187 / ReliefF.py:151-154 in
-// float32, SURF.py:153-156 in float64).  One wave per (row, j); lanes stride
-// the permuted feature columns.
+// Ambiguous pairs of the owned tiles: the quantised distance lies within the
+// error band of either endpoint's threshold, so the near/far decision could
+// differ from the reference's.  They are appended to `list` (capacity cap,
+// *count may exceed it: the host then grows the list and re-runs).
+// MultiSURF compares D (integer units) with thr; SURF compares the float32
+// distance with the float64 mean, the band widened by 4 float32 ulps of it.
+__global__ __launch_bounds__(256) void k_flag_pairs(const double* __restrict__ D, int64_t n,
+                                                    int64_t n_pad,
+                                                    const int2* __restrict__ tiles,
+                                                    const double* __restrict__ thr, int algo,
+                                                    double inv_sc, double delta,
+                                                    int2* __restrict__ list, int64_t cap,
+                                                    unsigned long long* __restrict__ count) {
+  const int2 tl = tiles[blockIdx.x];
+  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
+    const int jj = e / kTile, ii = e % kTile;
+    const int64_t i = i0 + ii, j = j0 + jj;
+    if (!(i < n && j < n && (tl.x < tl.y || ii < jj))) continue;
+    const double d = D[j * n_pad + i];
+    bool amb;
+    if (algo == ALGO_MULTISURF) {
+      amb = __builtin_fabs(d - thr[i]) < delta || __builtin_fabs(d - thr[j]) < delta;
+    } else {
+      const double df = d * inv_sc;
+      const float ai = (float)thr[i], aj = (float)thr[j];
+      const double bi = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(ai) + 1u) - (double)ai);
+      const double bj = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(aj) + 1u) - (double)aj);
+      amb = __builtin_fabs(df - thr[i]) < bi || __builtin_fabs(df - thr[j]) < bj;
+    }
+    if (amb) {
+      const unsigned long long k = atomicAdd(count, 1ull);
+      if ((int64_t)k < cap) list[k] = make_int2((int)i, (int)j);
+    }
+  }
+}
+
+// Reference-exact distance of each listed pair: sum_f diff_f(i, j) in
+// float64 with diff_f computed exactly as the reference kernels do
+// (MultiSURF.py:184-187 / ReliefF.py:151-154 in float32, SURF.py:153-156 in
+// float64).  One wave per pair, lanes stride the permuted feature columns;
+// the result (in integer units) overwrites both D[i][j] and D[j][i].
 template <typename T>
-__global__ __launch_bounds__(256) void k_exact_rows(
-    const T* __restrict__ x, int64_t n, int64_t p_in, int64_t PW, int64_t pc, int64_t PC,
-    int64_t pd, const int64_t* __restrict__ src_col, const double* __restrict__ scl,
-    const int32_t* __restrict__ rows, double* __restrict__ Dx) {
+__global__ __launch_bounds__(256) void k_exact_pairs(
+    const T* __restrict__ x, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
+    const int64_t* __restrict__ src_col, const double* __restrict__ scl, double sc,
+    const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
+    int64_t n_pad, double* __restrict__ D) {
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int64_t r = blockIdx.y;
-  const int64_t i = rows[r];
-  const T* xi = x + i * p_in;
-  for (int64_t j = (int64_t)blockIdx.x * 4 + wave; j < n; j += (int64_t)gridDim.x * 4) {
-    const T* xj = x + j * p_in;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
+  const int64_t total = (int64_t)*count < cap ? (int64_t)*count : cap;
+  for (int64_t k = wave; k < total; k += nw) {
+    const int2 pr = list[k];
+    const T* xi = x + (int64_t)pr.x * p_in;
+    const T* xj = x + (int64_t)pr.y * p_in;
     double acc = 0.0;
     for (int64_t c = lane; c < pc; c += 64) {
       const int64_t col = src_col[c];
@@ -402,88 +475,53 @@ __global__ __launch_bounds__(256) void k_exact_rows(
       const int64_t col = src_col[c];
       acc += (xi[col] != xj[col]) ? 1.0 : 0.0;
     }
-    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-    if (lane == 0) Dx[r * n + j] = (j == i) ? 0.0 : acc;
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) {
+      const double v = acc * sc;
+      D[(int64_t)pr.x * n_pad + pr.y] = v;
+      D[(int64_t)pr.y * n_pad + pr.x] = v;
+    }
   }
 }
 
-// Exact MultiSURF statistics of the ambiguous rows: threshold (real units)
-// and full-row near hit / miss counts, which replace the quantised ones.
-__global__ __launch_bounds__(256) void k_exact_ms_stats(const double* __restrict__ Dx,
-                                                        int64_t n,
-                                                        const int32_t* __restrict__ rows,
-                                                        const int32_t* __restrict__ lab,
-                                                        double* __restrict__ thrx,
-                                                        double* __restrict__ cnt) {
+// Near hit / miss counts over the owned tiles (D now exact for ambiguous
+// pairs): counts[2i], counts[2i+1].
+__global__ __launch_bounds__(256) void k_count_ms(const double* __restrict__ D, int64_t n,
+                                                  int64_t n_pad, int rank, int world,
+                                                  const int32_t* __restrict__ lab,
+                                                  const double* __restrict__ thr,
+                                                  double* __restrict__ counts) {
   __shared__ double red[256];
-  const int64_t r = blockIdx.x;
-  const int64_t i = rows[r];
-  const double* row = Dx + r * n;
-  double s1 = 0.0, s2 = 0.0;
-  for (int64_t j = threadIdx.x; j < n; j += 256) {
-    if (j == i) continue;
-    s1 += row[j];
-    s2 += row[j] * row[j];
-  }
-  s1 = block_sum_256(s1, red);
-  s2 = block_sum_256(s2, red);
-  const double t = multisurf_threshold(s1, s2, n);
+  const int64_t i = blockIdx.x;
+  const int64_t nb = n_pad / kTile, bi = i / kTile;
+  const double t = thr[i];
   const int32_t li = lab[i];
+  const double* row = D + i * n_pad;
   double h = 0.0, m = 0.0;
   for (int64_t j = threadIdx.x; j < n; j += 256) {
-    if (j == i || !(row[j] < t)) continue;
-    if (lab[j] == li) h += 1.0;
-    else m += 1.0;
+    if (j == i || !tile_owned(nb, bi, j / kTile, rank, world)) continue;
+    if (row[j] < t) {
+      if (lab[j] == li) h += 1.0;
+      else m += 1.0;
+    }
   }
   h = block_sum_256(h, red);
   m = block_sum_256(m, red);
   if (threadIdx.x == 0) {
-    thrx[r] = t;
-    cnt[2 * i] = h;
-    cnt[2 * i + 1] = m;
+    counts[2 * i] = h;
+    counts[2 * i + 1] = m;
   }
-}
-
-// Exact SURF mean of the ambiguous rows: float32 sequential sum of the
-// float32-rounded exact distances (self = 0), one thread per row.
-__global__ void k_exact_surf_avg(const double* __restrict__ Dx, int64_t n, int64_t nref,
-                                 double* __restrict__ thrx) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= nref) return;
-  float s = 0.0f;
-  for (int64_t j = 0; j < n; j++) s += (float)Dx[r * n + j];
-  thrx[r] = (double)s / (double)(n - 1);
 }
 
 // ---------------------------------------------------------------------------
 // Pair weights per owned tile: Wt[t][jj][ii] = W_ij + W_ji for i < j
 // ---------------------------------------------------------------------------
-// Row i's near decision uses the quantised D against thr[i] unless i is an
-// ambiguous row (rmap[i] = r >= 0), which uses its exact row Dx[r] against
-// thrx[r].  cnt = (H, M) per row after the exact rows were patched in.
-__device__ __forceinline__ bool near_of(int64_t i, int64_t j, double dq, int algo,
-                                        double inv_sc, const double* __restrict__ thr,
-                                        const int32_t* __restrict__ rmap,
-                                        const double* __restrict__ Dx,
-                                        const double* __restrict__ thrx, int64_t n) {
-  const int32_t r = rmap[i];
-  if (algo == ALGO_MULTISURF) {
-    if (r >= 0) return Dx[(int64_t)r * n + j] < thrx[r];
-    return dq < thr[i];
-  }
-  if (r >= 0) return (double)(float)Dx[(int64_t)r * n + j] < thrx[r];
-  return (double)(float)(dq * inv_sc) < thr[i];
-}
-
 __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, int64_t n,
                                                  int64_t n_pad, const int2* __restrict__ tiles,
                                                  const double* __restrict__ thr,
                                                  const int32_t* __restrict__ lab,
-                                                 const double* __restrict__ cnt, int algo,
+                                                 const double* __restrict__ counts, int algo,
                                                  int use_star, double inv_sc,
-                                                 const int32_t* __restrict__ rmap,
-                                                 const double* __restrict__ Dx,
-                                                 const double* __restrict__ thrx,
                                                  float* __restrict__ Wt) {
   const int2 tl = tiles[blockIdx.x];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
@@ -495,29 +533,19 @@ __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, i
     if (i < n && j < n && (tl.x < tl.y || ii < jj)) {
       const double d = D[j * n_pad + i];  // == D[i][j]
       const bool hit = lab[i] == lab[j];
-      const bool ni = near_of(i, j, d, algo, inv_sc, thr, rmap, Dx, thrx, n);
-      const bool nj = near_of(j, i, d, algo, inv_sc, thr, rmap, Dx, thrx, n);
       double wi, wj;
       if (algo == ALGO_MULTISURF) {
-        wi = multisurf_weight(ni, hit, use_star, cnt[2 * i], cnt[2 * i + 1]);
-        wj = multisurf_weight(nj, hit, use_star, cnt[2 * j], cnt[2 * j + 1]);
-      } else {
-        wi = surf_weight(ni, hit, use_star);
-        wj = surf_weight(nj, hit, use_star);
+        wi = multisurf_weight(d < thr[i], hit, use_star, counts[2 * i], counts[2 * i + 1]);
+        wj = multisurf_weight(d < thr[j], hit, use_star, counts[2 * j], counts[2 * j + 1]);
+      } else {  // SURF: float32 distance against the float64 mean
+        const double df = (double)(float)(d * inv_sc);
+        wi = surf_weight(df < thr[i], hit, use_star);
+        wj = surf_weight(df < thr[j], hit, use_star);
       }
       w = (float)(wi + wj);
     }
     out[jj * kTile + ii] = w;
   }
-}
-
-// cnt[2i], cnt[2i+1] = counts[3i], counts[3i+1]
-__global__ void k_counts_hm(const double* __restrict__ counts, int64_t n,
-                            double* __restrict__ cnt) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  cnt[2 * i] = counts[3 * i];
-  cnt[2 * i + 1] = counts[3 * i + 1];
 }
 
 // ---------------------------------------------------------------------------
@@ -749,6 +777,7 @@ struct Plan {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   int64_t nb = 0, n_tiles = 0, seg_len = 1, nseg = 1;
+  int rank_shift = 0;
   // device buffers
   void* x = nullptr;
   int64_t* src_col = nullptr;
@@ -759,21 +788,19 @@ struct Plan {
   int32_t* lab = nullptr;
   uint32_t* xqT = nullptr;
   float* xs = nullptr;
+  float* epsT = nullptr;
+  double* corr = nullptr;
   double* D = nullptr;
   int2* tiles = nullptr;
   double* thr = nullptr;
   float* Wt = nullptr;
   double* spart = nullptr;
-  // exact refinement of ambiguous rows
-  int32_t* rmap = nullptr;     // [n_pad] row -> refined slot or -1
-  double* cnt = nullptr;       // [2n] effective (H, M)
-  int32_t* amb = nullptr;      // [n] SURF ambiguity flags
-  int32_t* rows = nullptr;     // [cap] refined row ids
-  double* Dx = nullptr;        // [cap][n] exact distance rows
-  double* thrx = nullptr;      // [cap] exact thresholds
-  int64_t ref_cap = 0, n_refined = 0;
+  // ambiguous-pair refinement
+  int2* list = nullptr;
+  int64_t list_cap = 0;
+  unsigned long long* list_count = nullptr;
+  int64_t n_refined = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  float ms_dist = -1.0f, ms_score = -1.0f;
   std::vector<void*> owned;
 };
 
@@ -793,9 +820,9 @@ static int dalloc(Plan* g, T** p, size_t count) {
   return FS_OK;
 }
 
-#define FS_TRY(expr)            \
-  do {                          \
-    int rc_ = (expr);           \
+#define FS_TRY(expr)              \
+  do {                            \
+    int rc_ = (expr);             \
     if (rc_ != FS_OK) return rc_; \
   } while (0)
 
@@ -803,6 +830,15 @@ template <typename T>
 static int h2d(Plan* g, T* dst, const T* src, size_t count) {
   if (count == 0) return FS_OK;
   FS_HIP(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, g->stream));
+  return FS_OK;
+}
+
+static int launch_check(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string("kernel launch failed (") + what + "): " + hipGetErrorString(e));
+    return FS_EHIP;
+  }
   return FS_OK;
 }
 
@@ -866,6 +902,10 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   // ~64k pass-2 workgroups: enough to fill 256 CUs and bound tail imbalance.
   g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + 65535) / 65536);
   g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
+  // histogram shift so that the largest quantised value lands in bin < 4096
+  const double qmax = Q.qmax;
+  while ((qmax / std::ldexp(1.0, g->rank_shift)) >= (double)kRankBins) g->rank_shift++;
+  g->list_cap = std::max<int64_t>(1 << 16, Q.n * 64);
   const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
   int rc;
   if ((rc = dalloc(g, (char**)&g->x, xbytes)) ||
@@ -875,10 +915,10 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       (rc = dalloc(g, &g->dtab, Q.dtab.size())) || (rc = dalloc(g, &g->lab, Q.n_pad)) ||
       (rc = dalloc(g, &g->xqT, (size_t)Q.PW * Q.n_pad)) ||
       (rc = dalloc(g, &g->xs, (size_t)Q.n_pad * Q.PW)) ||
+      (rc = dalloc(g, &g->epsT, (size_t)Q.PW * Q.n_pad)) || (rc = dalloc(g, &g->corr, Q.n_pad)) ||
       (rc = dalloc(g, &g->D, (size_t)Q.n_pad * Q.n_pad)) ||
       (rc = dalloc(g, &g->tiles, g->n_tiles)) || (rc = dalloc(g, &g->thr, Q.n_pad)) ||
-      (rc = dalloc(g, &g->rmap, Q.n_pad)) || (rc = dalloc(g, &g->cnt, 2 * Q.n_pad)) ||
-      (rc = dalloc(g, &g->amb, Q.n_pad)))
+      (rc = dalloc(g, &g->list, g->list_cap)) || (rc = dalloc(g, &g->list_count, 1)))
     return fail(rc);
   if (Q.algo != ALGO_RELIEFF) {
     if ((rc = dalloc(g, &g->Wt, (size_t)g->n_tiles * kTile * kTile)) ||
@@ -904,29 +944,30 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   return FS_OK;
 }
 
-static int launch_check(const char* what) {
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) {
-    set_error(std::string("kernel launch failed (") + what + "): " + hipGetErrorString(e));
-    return FS_EHIP;
-  }
-  return FS_OK;
-}
-
-// quantize + pass 1 (distance tiles)
+// quantize (+ mean correction terms) and pass 1 (distance tiles)
 static int run_quantize_dist(Plan* g) {
   const Prepared& Q = g->P;
   FS_HIP(hipSetDevice(g->device));
   dim3 gq((unsigned)(Q.PW / 64), (unsigned)(Q.n_pad / 64));
   if (g->x_is_f64)
     k_quantize<double><<<gq, 256, 0, g->stream>>>(
-        (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, Q.PC, Q.pd, g->src_col, g->off,
-        g->qs, g->scl, g->dtab_off, g->dtab, g->xqT, g->xs);
+        (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, g->src_col, g->off, g->qs, g->scl,
+        g->dtab_off, g->dtab, g->xqT, g->xs, g->epsT);
   else
     k_quantize<float><<<gq, 256, 0, g->stream>>>(
-        (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, Q.PC, Q.pd, g->src_col, g->off,
-        g->qs, g->scl, g->dtab_off, g->dtab, g->xqT, g->xs);
+        (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, g->src_col, g->off, g->qs, g->scl,
+        g->dtab_off, g->dtab, g->xqT, g->xs, g->epsT);
   FS_TRY(launch_check("k_quantize"));
+  if (Q.algo == ALGO_MULTISURF) {
+    if (Q.pc > 0) {
+      k_colrank<<<(unsigned)Q.pc, 256, 0, g->stream>>>(g->xqT, Q.n, Q.n_pad, g->rank_shift,
+                                                       g->epsT);
+      FS_TRY(launch_check("k_colrank"));
+    }
+    k_rowcorr<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(g->epsT, Q.n, Q.n_pad, Q.pc,
+                                                                    g->corr);
+    FS_TRY(launch_check("k_rowcorr"));
+  }
   if (g->n_tiles > 0) {
     FS_HIP(hipEventRecord(g->ev[0], g->stream));
     k_dist<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->xqT, Q.n_pad, (int)(Q.PC / kBK),
@@ -936,6 +977,41 @@ static int run_quantize_dist(Plan* g) {
     FS_HIP(hipEventRecord(g->ev[1], g->stream));
   }
   return FS_OK;
+}
+
+// Flag the ambiguous pairs of the owned tiles and recompute them exactly.
+// One host round trip reads the pair count (to grow the list if needed).
+static int refine_pairs(Plan* g, int algo, double delta) {
+  const Prepared& Q = g->P;
+  g->n_refined = 0;
+  if (g->n_tiles == 0) return FS_OK;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
+    k_flag_pairs<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(
+        g->D, Q.n, Q.n_pad, g->tiles, g->thr, algo, 1.0 / Q.SC, delta, g->list, g->list_cap,
+        g->list_count);
+    FS_TRY(launch_check("k_flag_pairs"));
+    unsigned long long cnt = 0;
+    FS_HIP(hipMemcpyAsync(&cnt, g->list_count, sizeof(cnt), hipMemcpyDeviceToHost, g->stream));
+    FS_HIP(hipStreamSynchronize(g->stream));
+    if ((int64_t)cnt <= g->list_cap) {
+      g->n_refined = (int64_t)cnt;
+      break;
+    }
+    g->list_cap = (int64_t)cnt + cnt / 4;
+    FS_TRY(dalloc(g, &g->list, g->list_cap));
+  }
+  if (g->n_refined == 0) return FS_OK;
+  const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
+  if (g->x_is_f64)
+    k_exact_pairs<double><<<grid, 256, 0, g->stream>>>(
+        (const double*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
+        g->list_count, g->list_cap, Q.n_pad, g->D);
+  else
+    k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
+        (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
+        g->list_count, g->list_cap, Q.n_pad, g->D);
+  return launch_check("k_exact_pairs");
 }
 
 static int run_pass2(Plan* g, double* scores_dev) {
@@ -966,67 +1042,25 @@ int plan_pass1(Plan* g, double* rowstats) {
 int plan_select(Plan* g, const double* rowstats, double* counts) {
   const Prepared& Q = g->P;
   FS_HIP(hipSetDevice(g->device));
-  k_select_ms<<<(unsigned)Q.n, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->rank, g->world,
-                                                    g->lab, rowstats, Q.amb_delta * Q.SC,
-                                                    g->thr, counts);
-  FS_TRY(launch_check("k_select_ms"));
+  k_thr_ms<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(rowstats, g->corr, Q.n,
+                                                                 g->thr);
+  FS_TRY(launch_check("k_thr_ms"));
+  FS_TRY(refine_pairs(g, ALGO_MULTISURF, Q.amb_delta * Q.SC));
+  k_count_ms<<<(unsigned)Q.n, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->rank, g->world,
+                                                   g->lab, g->thr, counts);
+  FS_TRY(launch_check("k_count_ms"));
   if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
   return FS_OK;
-}
-
-// Recompute the listed rows with reference-exact arithmetic (Dx, thrx) and
-// publish the row -> slot map.  `rows` is host data.
-static int refine_rows(Plan* g, const std::vector<int32_t>& rows) {
-  const Prepared& Q = g->P;
-  const int64_t nref = (int64_t)rows.size();
-  g->n_refined = nref;
-  std::vector<int32_t> rmap(Q.n_pad, -1);
-  for (int64_t r = 0; r < nref; r++) rmap[rows[r]] = (int32_t)r;
-  FS_TRY(h2d(g, g->rmap, rmap.data(), Q.n_pad));
-  if (nref == 0) return FS_OK;
-  if (nref > g->ref_cap) {
-    int64_t cap = std::max<int64_t>(nref, 2 * g->ref_cap);
-    FS_TRY(dalloc(g, &g->rows, cap));
-    FS_TRY(dalloc(g, &g->Dx, (size_t)cap * Q.n));
-    FS_TRY(dalloc(g, &g->thrx, cap));
-    g->ref_cap = cap;
-  }
-  FS_TRY(h2d(g, g->rows, rows.data(), nref));
-  const unsigned gx = (unsigned)std::min<int64_t>((Q.n + 3) / 4, 1024);
-  if (g->x_is_f64)
-    k_exact_rows<double><<<dim3(gx, (unsigned)nref), 256, 0, g->stream>>>(
-        (const double*)g->x, Q.n, Q.p_in, Q.PW, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, g->rows,
-        g->Dx);
-  else
-    k_exact_rows<float><<<dim3(gx, (unsigned)nref), 256, 0, g->stream>>>(
-        (const float*)g->x, Q.n, Q.p_in, Q.PW, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, g->rows,
-        g->Dx);
-  return launch_check("k_exact_rows");
 }
 
 int plan_pass2(Plan* g, const double* counts, double* scores) {
   const Prepared& Q = g->P;
   FS_HIP(hipSetDevice(g->device));
-  k_counts_hm<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(counts, Q.n, g->cnt);
-  FS_TRY(launch_check("k_counts_hm"));
-  // rows with an ambiguous pair (all-reduced counts: identical on every rank)
-  std::vector<double> hc(3 * Q.n);
-  FS_HIP(hipMemcpyAsync(hc.data(), counts, sizeof(double) * 3 * Q.n, hipMemcpyDeviceToHost,
-                        g->stream));
-  FS_HIP(hipStreamSynchronize(g->stream));
-  std::vector<int32_t> rows;
-  for (int64_t i = 0; i < Q.n; i++)
-    if (hc[3 * i + 2] > 0.0) rows.push_back((int32_t)i);
-  FS_TRY(refine_rows(g, rows));
-  if (!rows.empty()) {
-    k_exact_ms_stats<<<(unsigned)rows.size(), 256, 0, g->stream>>>(g->Dx, Q.n, g->rows, g->lab,
-                                                                  g->thrx, g->cnt);
-    FS_TRY(launch_check("k_exact_ms_stats"));
-  }
   if (g->n_tiles > 0) {
-    k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(
-        g->D, Q.n, Q.n_pad, g->tiles, g->thr, g->lab, g->cnt, ALGO_MULTISURF, Q.use_star,
-        1.0 / Q.SC, g->rmap, g->Dx, g->thrx, g->Wt);
+    k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
+                                                           g->thr, g->lab, counts,
+                                                           ALGO_MULTISURF, Q.use_star,
+                                                           1.0 / Q.SC, g->Wt);
     FS_TRY(launch_check("k_weights"));
   }
   FS_TRY(run_pass2(g, scores));
@@ -1073,7 +1107,7 @@ int multisurf_run(const Prepared& P, const void* x, int device, float* scores_ou
   FS_TRY(plan_create(&g, P, x, 0, device, 0, 1, 0));
   double *rs = nullptr, *cnt = nullptr, *sc = nullptr;
   int rc;
-  if ((rc = dalloc(g, &rs, 2 * P.n)) || (rc = dalloc(g, &cnt, 3 * P.n)) ||
+  if ((rc = dalloc(g, &rs, 2 * P.n)) || (rc = dalloc(g, &cnt, 2 * P.n)) ||
       (rc = dalloc(g, &sc, P.n_kept)) || (rc = plan_pass1(g, rs)) ||
       (rc = plan_select(g, rs, cnt)) || (rc = plan_pass2(g, cnt, sc)) ||
       (rc = finish_scores(g, sc, scores_out))) {
@@ -1092,27 +1126,15 @@ int surf_run(const Prepared& P, const void* x, int device, float* scores_out) {
   int rc = dalloc(g, &sc, Q.n_kept);
   if (rc == FS_OK) rc = run_quantize_dist(g);
   if (rc == FS_OK) {
-    k_surf_avg<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(
-        g->D, Q.n, Q.n_pad, 1.0 / Q.SC, Q.amb_delta, g->thr, g->amb);
+    k_surf_avg<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad,
+                                                                    1.0 / Q.SC, g->thr);
     rc = launch_check("k_surf_avg");
   }
-  std::vector<int32_t> amb(Q.n), rows;
-  if (rc == FS_OK && hipMemcpyAsync(amb.data(), g->amb, sizeof(int32_t) * Q.n,
-                                    hipMemcpyDeviceToHost, g->stream) != hipSuccess)
-    rc = FS_EHIP;
-  if (rc == FS_OK && hipStreamSynchronize(g->stream) != hipSuccess) rc = FS_EHIP;
-  for (int64_t i = 0; i < Q.n; i++)
-    if (amb[i]) rows.push_back((int32_t)i);
-  if (rc == FS_OK) rc = refine_rows(g, rows);
-  if (rc == FS_OK && !rows.empty()) {
-    k_exact_surf_avg<<<(unsigned)((rows.size() + 255) / 256), 256, 0, g->stream>>>(
-        g->Dx, Q.n, (int64_t)rows.size(), g->thrx);
-    rc = launch_check("k_exact_surf_avg");
-  }
+  if (rc == FS_OK) rc = refine_pairs(g, ALGO_SURF, Q.amb_delta);
   if (rc == FS_OK) {
-    k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(
-        g->D, Q.n, Q.n_pad, g->tiles, g->thr, g->lab, nullptr, ALGO_SURF, Q.use_star,
-        1.0 / Q.SC, g->rmap, g->Dx, g->thrx, g->Wt);
+    k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
+                                                           g->thr, g->lab, nullptr, ALGO_SURF,
+                                                           Q.use_star, 1.0 / Q.SC, g->Wt);
     rc = launch_check("k_weights");
   }
   if (rc == FS_OK) rc = run_pass2(g, sc);

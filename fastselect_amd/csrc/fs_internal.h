@@ -69,6 +69,7 @@ struct Prepared {
   // inside which a quantised near/far decision is not trusted; rows with a
   // pair in the band are recomputed with reference-exact arithmetic.
   double amb_delta = 0.0;
+  double qmax = 0.0;               // largest quantised continuous value
 };
 
 // Build the permutation, label codes, discrete tables and integer scale.
@@ -115,16 +116,20 @@ FS_HD inline double surf_weight(bool near, bool hit, int use_star) {
 
 // ---- CPU backend ---------------------------------------------------------
 namespace cpu {
-int multisurf_pass1(const Prepared& P, const void* x, int x_is_f64, int rank, int world,
-                    int n_jobs, std::vector<uint64_t>& D, std::vector<float>& xs,
-                    double* rowstats);
-int multisurf_select(const Prepared& P, const std::vector<uint64_t>& D, int rank, int world,
-                     const double* rowstats, std::vector<double>& thr, double* counts,
-                     int n_jobs);
-int multisurf_pass2(const Prepared& P, const void* x, const std::vector<uint64_t>& D,
-                    const std::vector<float>& xs, const std::vector<double>& thr,
-                    const double* counts, int rank, int world, int n_jobs, double* scores,
-                    int64_t* refined_rows);
+// CPU state of a MultiSURF plan (the GPU keeps the same arrays in HBM).
+struct CpuState {
+  std::vector<double> D;      // n x n distances (integer units; exact for refined pairs)
+  std::vector<float> xs;      // n x PW per-feature operands of pass 2
+  std::vector<double> corr;   // per-row mean correction (see k_colrank)
+  std::vector<double> thr;    // per-row thresholds (integer units)
+  int64_t refined = 0;        // ambiguous pairs recomputed exactly in the last select
+};
+int multisurf_pass1(const Prepared& P, const void* x, int rank, int world, int n_jobs,
+                    CpuState& S, double* rowstats);
+int multisurf_select(const Prepared& P, const void* x, int rank, int world,
+                     const double* rowstats, int n_jobs, CpuState& S, double* counts);
+int multisurf_pass2(const Prepared& P, const CpuState& S, const double* counts, int rank,
+                    int world, int n_jobs, double* scores);
 int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores);
 int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores);
 }  // namespace cpu

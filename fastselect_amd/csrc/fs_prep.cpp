@@ -143,6 +143,7 @@ int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64
   }
   P.SC = sc;
   P.SCu = (uint32_t)sc;
+  P.qmax = std::floor(R * sc + 0.5) + 1.0;
   // Error model of a quantised distance vs the reference's (float64 sum of
   // float32-rounded diffs): per continuous feature a rounding error of at
   // most 1/SC (std ~ 1/sqrt(6)/SC) plus the reference's own float32

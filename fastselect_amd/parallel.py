@@ -1,0 +1,99 @@
+"""Sharded MultiSURF over one process per GPU (torch.distributed).
+
+The reference is single-device; this is the MI355X-native
+multi-GPU path of §8e: the upper-triangle pair tiles are dealt round-robin to
+the ranks (tile t -> rank t % world), every rank holds all of X, and the path
+has exactly three exchange points, each a SUM all-reduce of a small float64
+vector (RCCL over xGMI with the 'nccl' backend, gloo on CPU):
+
+    pass1  -> rowstats[2n]  (sum D, sum D^2 per sample)
+    select -> counts[2n]    (near hits, near misses)
+    pass2  -> scores[p]     (per-feature score sums)
+
+With world == 1 no collective is issued and the result equals
+``MultiSURF.fit`` on one device.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _base, _lib
+
+
+def _dist():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return dist, dist.get_rank(), dist.get_world_size()
+    return None, 0, 1
+
+
+def prepare_inputs(X, y, discrete_limit: int = 10):
+    """The host preprocessing of ``MultiSURF.fit`` (MultiSURF.py:384-420)."""
+    x = np.ascontiguousarray(X, dtype=np.float32)
+    ranges = (x.max(axis=0) - x.min(axis=0)).astype(np.float32)
+    ranges[ranges == 0] = 1
+    recip = (1.0 / ranges).astype(np.float32)
+    return x, np.asarray(y), recip, _base.discrete_mask(x, discrete_limit)
+
+
+class ShardedMultiSURF:
+    """One rank's share of a MultiSURF scoring job.
+
+    backend 'gpu': buffers are CUDA tensors on ``device`` and every kernel runs
+    on torch's current stream, so the all-reduces are stream-ordered with the
+    HIP kernels.  backend 'cpu': host tensors (use the gloo backend).
+    """
+
+    def __init__(self, x, y, recip, is_discrete, use_star=False, backend="gpu", device=0):
+        import torch
+        self.dist, self.rank, self.world = _dist()
+        self.n, self.p = x.shape
+        self.backend = backend
+        if backend == "gpu":
+            torch.cuda.set_device(device)
+            self.tdev = torch.device("cuda", device)
+            stream = torch.cuda.current_stream().cuda_stream
+        else:
+            self.tdev = torch.device("cpu")
+            stream = 0
+        self.plan = _lib.Plan(backend, x, y, recip, is_discrete, use_star=use_star,
+                              rank=self.rank, world=self.world, device=device, stream=stream)
+        f64 = torch.float64
+        self.rowstats = torch.zeros(2 * self.n, dtype=f64, device=self.tdev)
+        self.counts = torch.zeros(2 * self.n, dtype=f64, device=self.tdev)
+        self.scores = torch.zeros(self.p, dtype=f64, device=self.tdev)
+
+    def _allreduce(self, t):
+        if self.dist is not None and self.world > 1:
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+
+    def step(self):
+        """One full scoring pass; returns float32 scores (device tensor)."""
+        self.plan.pass1(self.rowstats.data_ptr())
+        self._allreduce(self.rowstats)
+        self.plan.select(self.rowstats.data_ptr(), self.counts.data_ptr())
+        self._allreduce(self.counts)
+        self.plan.pass2(self.counts.data_ptr(), self.scores.data_ptr())
+        self._allreduce(self.scores)
+        return (self.scores / self.n).float()
+
+    def info(self):
+        return self.plan.info()
+
+    def kernel_ms(self, which: int) -> float:
+        return self.plan.kernel_ms(which)
+
+    def close(self):
+        self.plan.close()
+
+
+def multisurf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", device=0):
+    """Score X on this rank's share of the tiles and return the full float32
+    score vector (identical on every rank)."""
+    x, yv, recip, isd = prepare_inputs(X, y, discrete_limit)
+    job = ShardedMultiSURF(x, yv, recip, isd, use_star=use_star, backend=backend, device=device)
+    try:
+        s = job.step()
+        return s.cpu().numpy()
+    finally:
+        job.close()

@@ -138,21 +138,20 @@ FS_API int fs_plan_create(fs_plan** plan_out, int backend, int device, const flo
  * space: device memory for the GPU backend, host memory for the CPU backend.
  */
 FS_API int fs_plan_pass1(fs_plan* plan, double* rowstats);
-/* Stage 2: thresholds from the all-reduced rowstats; partial per-row
- * (near hits, near misses, ambiguous pairs) -> counts[3n].  A pair is
- * ambiguous when its quantised distance lies so close to the row threshold
- * that the near/far decision is not certain; after the all-reduce every rank
- * recomputes those rows with reference-exact arithmetic in stage 3. */
+/* Stage 2: thresholds from the all-reduced rowstats (plus the rank-local mean
+ * correction), exact recomputation of this rank's ambiguous pairs (pairs whose
+ * quantised distance lies so close to a threshold that the near/far decision
+ * is not certain), then partial per-row (near hits, near misses) -> counts[2n]. */
 FS_API int fs_plan_select(fs_plan* plan, const double* rowstats, double* counts);
-/* Stage 3: exact recomputation of ambiguous rows, pair weights from the
- * all-reduced counts[3n]; partial per-feature score sums (NOT divided by n)
- * -> scores[n_kept], in feat_idx order. */
+/* Stage 3: pair weights from the all-reduced counts[2n]; partial per-feature
+ * score sums (NOT divided by n) -> scores[n_kept], in feat_idx order. */
 FS_API int fs_plan_pass2(fs_plan* plan, const double* counts, double* scores);
 /* Number of pair tiles this plan owns, the pair-feature evaluations one full
  * pass1+pass2 performs on this rank (throughput accounting) and the number of
- * rows the last stage 3 recomputed exactly.  NULL outputs are skipped. */
+ * ambiguous pairs the last stage 2 recomputed exactly.  NULL outputs are
+ * skipped. */
 FS_API int fs_plan_info(const fs_plan* plan, int64_t* owned_tiles, double* pair_feature_evals,
-                        int64_t* refined_rows);
+                        int64_t* refined_pairs);
 /* Average duration in milliseconds of the last pass1 / pass2 distance and
  * score kernels, measured with HIP events on the plan's stream (GPU only;
  * -1 when unavailable).  which: 0 = distance kernel, 1 = score kernel. */

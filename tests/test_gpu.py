@@ -195,7 +195,7 @@ def test_sharded_plans_sum_to_single():
         for pl, b in zip(plans, rs):
             pl.pass1(b.data_ptr())
         rsum = sum(rs)
-        cn = [torch.zeros(3 * n, dtype=torch.float64, device="cuda") for _ in plans]
+        cn = [torch.zeros(2 * n, dtype=torch.float64, device="cuda") for _ in plans]
         for pl, b in zip(plans, cn):
             pl.select(rsum.data_ptr(), b.data_ptr())
         csum = sum(cn)
