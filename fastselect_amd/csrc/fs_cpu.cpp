@@ -294,32 +294,32 @@ int multisurf_pass2(const Prepared& P, const CpuState& S, const double* counts, 
 }
 
 int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
+  // SURF compares float32-rounded distances with a float32 sequential mean,
+  // so distances are accumulated in float64 from float64 diffs (as
+  // k_dist_f64 does; exact to ~1e-16, SURF.py:146-160) rather than quantised.
   std::vector<uint32_t> xq;
   std::vector<float> xs;
-  std::vector<double> D;
   quantize(P, x, 1, n_jobs, xq, xs, nullptr);
-  distances(P, xq, 0, 1, n_jobs, D);
   const int64_t n = P.n;
-  const double inv_sc = 1.0 / P.SC;
-  // float32 distance row, float32 sequential mean (SURF.py:146-163)
+  std::vector<float> Df((size_t)n * n, 0.0f);
+  parallel_for(n, n_jobs, [&](int64_t i) {
+    for (int64_t j = i + 1; j < n; j++) {
+      const float d = (float)exact_pair(P, x, 1, i, j);
+      Df[(size_t)i * n + j] = d;
+      Df[(size_t)j * n + i] = d;
+    }
+  });
+  // float32 sequential mean (SURF.py:162-163)
   std::vector<double> avg(n);
   parallel_for(n, n_jobs, [&](int64_t i) {
     float s = 0.0f;
-    for (int64_t j = 0; j < n; j++) s += (float)(D[(size_t)i * n + j] * inv_sc);
+    for (int64_t j = 0; j < n; j++) s += Df[(size_t)i * n + j];
     avg[i] = (double)s / (double)(n - 1);
-  });
-  auto band = [&](int64_t i) {
-    const float a = (float)avg[i];
-    return P.amb_delta + 4.0 * ((double)std::nextafter(a, 3.0e38f) - (double)a);
-  };
-  refine_pairs(P, x, 1, 0, 1, n_jobs, D, [&](int64_t i, int64_t j, double d) {
-    const double df = d * inv_sc;
-    return std::fabs(df - avg[i]) < band(i) || std::fabs(df - avg[j]) < band(j);
   });
   std::vector<PairW> pairs;
   for (int64_t i = 0; i < n; i++)
     for (int64_t j = i + 1; j < n; j++) {
-      const double df = (double)(float)(D[(size_t)i * n + j] * inv_sc);
+      const double df = (double)Df[(size_t)i * n + j];
       const bool hit = P.labels[i] == P.labels[j];
       const float w = (float)(surf_weight(df < avg[i], hit, P.use_star) +
                               surf_weight(df < avg[j], hit, P.use_star));

@@ -355,6 +355,144 @@ __global__ __launch_bounds__(256, 2) void k_dist(const uint32_t* __restrict__ xq
 }
 
 // ---------------------------------------------------------------------------
+// Pass 1, float64 variant (SURF): D[i][j] = sum_f |x'_if - x'_jf| in float64
+// ---------------------------------------------------------------------------
+// SURF's neighbourhood test compares the float32-rounded distance with a
+// float32 sequential mean (SURF.py:158-176), so its distances must round to
+// exactly the reference's float32 values; integer quantisation cannot
+// promise that, float64 accumulation of float64 diffs can (error ~1e-16).
+// x' = (x - min) * recip in float64 (feature-major), discrete columns hold
+// category codes.  Same 128x128 tile / 8x8-per-lane layout as k_dist; each
+// 16-feature panel is 16 KB (one k-row = one 1 KB global_load_lds_dwordx4).
+// 512 lanes per tile: lane (tx, ty) = (tid % 32, tid / 32) owns rows
+// {ty*4 + r, 64 + ty*4 + r} x cols {tx*4 + c} (8 x 4 float64 accumulators).
+template <bool DISC>
+__device__ __forceinline__ void dist_chunk_f64(const double* __restrict__ A,
+                                               const double* __restrict__ B, int tx, int ty,
+                                               double (&acc)[8][4]) {
+#pragma unroll 2
+  for (int k = 0; k < kBK; k++) {
+    const double4 a0 = *(const double4*)&A[k * kTile + ty * 4];
+    const double4 a1 = *(const double4*)&A[k * kTile + 64 + ty * 4];
+    const double4 b0 = *(const double4*)&B[k * kTile + tx * 4];
+    const double av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    const double bv[4] = {b0.x, b0.y, b0.z, b0.w};
+#pragma unroll
+    for (int r = 0; r < 8; r++)
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+        // codes are small integers: [a != b] == min(|a - b|, 1) without lane masks
+        acc[r][c] += DISC ? __builtin_fmin(__builtin_fabs(av[r] - bv[c]), 1.0)
+                          : __builtin_fabs(av[r] - bv[c]);
+  }
+}
+
+__global__ __launch_bounds__(512, 2) void k_dist_f64(const double* __restrict__ xT, int64_t n_pad,
+                                                     int nck_cont, int nck_disc,
+                                                     const int2* __restrict__ tiles,
+                                                     double* __restrict__ D) {
+  __shared__ __attribute__((aligned(16))) double ldsA0[kBK * kTile], ldsB0[kBK * kTile];
+  __shared__ __attribute__((aligned(16))) double ldsA1[kBK * kTile], ldsB1[kBK * kTile];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int2 tl = tiles[blockIdx.x];
+  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  const int tx = tid & 31, ty = tid >> 5;
+  double acc[8][4];
+#pragma unroll
+  for (int r = 0; r < 8; r++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) acc[r][c] = 0.0;
+  // 8 waves; instruction s of wave w moves k-row 2w+s (1 KB): lane l ->
+  // doubles 2l, 2l+1 of that row
+  auto stage = [&](double* la, double* lb, int ck) {
+    const int64_t k0 = (int64_t)ck * kBK;
+#pragma unroll
+    for (int s = 0; s < 2; s++) {
+      const int krow = wave * 2 + s;
+      const double* ga = xT + (k0 + krow) * n_pad + i0 + 2 * lane;
+      const double* gb = xT + (k0 + krow) * n_pad + j0 + 2 * lane;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ga,
+                                       (__attribute__((address_space(3))) void*)(la + krow * kTile),
+                                       16, 0, 0);
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gb,
+                                       (__attribute__((address_space(3))) void*)(lb + krow * kTile),
+                                       16, 0, 0);
+    }
+  };
+  const int nck = nck_cont + nck_disc;
+  stage(ldsA0, ldsB0, 0);
+  __syncthreads();
+  for (int ck = 0; ck < nck; ck += 2) {
+    if (ck + 1 < nck) stage(ldsA1, ldsB1, ck + 1);
+    if (ck < nck_cont) dist_chunk_f64<false>(ldsA0, ldsB0, tx, ty, acc);
+    else dist_chunk_f64<true>(ldsA0, ldsB0, tx, ty, acc);
+    __syncthreads();
+    if (ck + 1 < nck) {
+      if (ck + 2 < nck) stage(ldsA0, ldsB0, ck + 2);
+      if (ck + 1 < nck_cont) dist_chunk_f64<false>(ldsA1, ldsB1, tx, ty, acc);
+      else dist_chunk_f64<true>(ldsA1, ldsB1, tx, ty, acc);
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    const int64_t i = i0 + ty * 4 + (r & 3) + (r >> 2) * 64;
+    double* row = D + i * n_pad + j0 + tx * 4;
+    *(double2*)(row + 0) = make_double2(acc[r][0], acc[r][1]);
+    *(double2*)(row + 2) = make_double2(acc[r][2], acc[r][3]);
+  }
+  if (tl.x != tl.y) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const int64_t j = j0 + tx * 4 + c;
+      double* row = D + j * n_pad + i0 + ty * 4;
+      *(double2*)(row + 0) = make_double2(acc[0][c], acc[1][c]);
+      *(double2*)(row + 2) = make_double2(acc[2][c], acc[3][c]);
+      *(double2*)(row + 64) = make_double2(acc[4][c], acc[5][c]);
+      *(double2*)(row + 66) = make_double2(acc[6][c], acc[7][c]);
+    }
+  }
+}
+
+// x (float64, row-major) -> xT64 (float64, feature-major: scaled values or
+// category codes) + xs (float32 pass-2 operands).
+__global__ __launch_bounds__(256) void k_quantize_f64(
+    const double* __restrict__ x, int64_t n, int64_t n_pad, int64_t p_in, int64_t PW, int64_t pc,
+    const int64_t* __restrict__ src_col, const double* __restrict__ off,
+    const double* __restrict__ scl, const int64_t* __restrict__ dtab_off,
+    const double* __restrict__ dtab, double* __restrict__ xT, float* __restrict__ xs) {
+  __shared__ double tile[64][65];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * 64, i0 = (int64_t)blockIdx.y * 64;
+  const int64_t c = c0 + tx;
+  const int64_t col = src_col[c];
+  for (int r = ty; r < 64; r += 4) {
+    const int64_t i = i0 + r;
+    double v = 0.0;
+    if (i < n && col >= 0) {
+      const double xv = x[i * p_in + col];
+      if (c < pc) {
+        v = __dmul_rn(__dadd_rn(xv, -off[c]), scl[c]);
+      } else {
+        int64_t lo = dtab_off[c], hi = dtab_off[c + 1] - 1;
+        while (lo < hi) {
+          const int64_t mid = (lo + hi) >> 1;
+          if (dtab[mid] < xv) lo = mid + 1;
+          else hi = mid;
+        }
+        v = (double)(lo - dtab_off[c]);
+      }
+    }
+    xs[i * PW + c] = (float)v;
+    tile[r][tx] = v;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) xT[(c0 + r) * n_pad + i0 + tx] = tile[tx][r];
+}
+
+// ---------------------------------------------------------------------------
 // MultiSURF row statistics, thresholds and neighbour counts
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_rowstats(const double* __restrict__ D, int64_t n,
@@ -790,6 +928,7 @@ struct Plan {
   float* xs = nullptr;
   float* epsT = nullptr;
   double* corr = nullptr;
+  double* xT64 = nullptr;      // SURF: float64 feature-major operands
   double* D = nullptr;
   int2* tiles = nullptr;
   double* thr = nullptr;
@@ -913,13 +1052,18 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       (rc = dalloc(g, &g->off, Q.PW)) || (rc = dalloc(g, &g->qs, Q.PW)) ||
       (rc = dalloc(g, &g->scl, Q.PW)) || (rc = dalloc(g, &g->dtab_off, Q.PW + 1)) ||
       (rc = dalloc(g, &g->dtab, Q.dtab.size())) || (rc = dalloc(g, &g->lab, Q.n_pad)) ||
-      (rc = dalloc(g, &g->xqT, (size_t)Q.PW * Q.n_pad)) ||
-      (rc = dalloc(g, &g->xs, (size_t)Q.n_pad * Q.PW)) ||
-      (rc = dalloc(g, &g->epsT, (size_t)Q.PW * Q.n_pad)) || (rc = dalloc(g, &g->corr, Q.n_pad)) ||
+      (rc = dalloc(g, &g->xs, (size_t)Q.n_pad * Q.PW)) || (rc = dalloc(g, &g->corr, Q.n_pad)) ||
       (rc = dalloc(g, &g->D, (size_t)Q.n_pad * Q.n_pad)) ||
       (rc = dalloc(g, &g->tiles, g->n_tiles)) || (rc = dalloc(g, &g->thr, Q.n_pad)) ||
       (rc = dalloc(g, &g->list, g->list_cap)) || (rc = dalloc(g, &g->list_count, 1)))
     return fail(rc);
+  if (Q.algo == ALGO_SURF) {
+    if ((rc = dalloc(g, &g->xT64, (size_t)Q.PW * Q.n_pad))) return fail(rc);
+  } else {
+    if ((rc = dalloc(g, &g->xqT, (size_t)Q.PW * Q.n_pad)) ||
+        (rc = dalloc(g, &g->epsT, (size_t)Q.PW * Q.n_pad)))
+      return fail(rc);
+  }
   if (Q.algo != ALGO_RELIEFF) {
     if ((rc = dalloc(g, &g->Wt, (size_t)g->n_tiles * kTile * kTile)) ||
         (rc = dalloc(g, &g->spart, (size_t)g->nseg * Q.PW)))
@@ -949,6 +1093,20 @@ static int run_quantize_dist(Plan* g) {
   const Prepared& Q = g->P;
   FS_HIP(hipSetDevice(g->device));
   dim3 gq((unsigned)(Q.PW / 64), (unsigned)(Q.n_pad / 64));
+  if (Q.algo == ALGO_SURF) {
+    k_quantize_f64<<<gq, 256, 0, g->stream>>>((const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW,
+                                              Q.pc, g->src_col, g->off, g->scl, g->dtab_off,
+                                              g->dtab, g->xT64, g->xs);
+    FS_TRY(launch_check("k_quantize_f64"));
+    if (g->n_tiles > 0) {
+      FS_HIP(hipEventRecord(g->ev[0], g->stream));
+      k_dist_f64<<<(unsigned)g->n_tiles, 512, 0, g->stream>>>(
+          g->xT64, Q.n_pad, (int)(Q.PC / kBK), (int)(Q.PD / kBK), g->tiles, g->D);
+      FS_TRY(launch_check("k_dist_f64"));
+      FS_HIP(hipEventRecord(g->ev[1], g->stream));
+    }
+    return FS_OK;
+  }
   if (g->x_is_f64)
     k_quantize<double><<<gq, 256, 0, g->stream>>>(
         (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, g->src_col, g->off, g->qs, g->scl,
@@ -1124,17 +1282,16 @@ int surf_run(const Prepared& P, const void* x, int device, float* scores_out) {
   const Prepared& Q = g->P;
   double* sc = nullptr;
   int rc = dalloc(g, &sc, Q.n_kept);
-  if (rc == FS_OK) rc = run_quantize_dist(g);
+  if (rc == FS_OK) rc = run_quantize_dist(g);  // float64 distances, real units
   if (rc == FS_OK) {
-    k_surf_avg<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad,
-                                                                    1.0 / Q.SC, g->thr);
+    k_surf_avg<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, 1.0,
+                                                                    g->thr);
     rc = launch_check("k_surf_avg");
   }
-  if (rc == FS_OK) rc = refine_pairs(g, ALGO_SURF, Q.amb_delta);
   if (rc == FS_OK) {
     k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
                                                            g->thr, g->lab, nullptr, ALGO_SURF,
-                                                           Q.use_star, 1.0 / Q.SC, g->Wt);
+                                                           Q.use_star, 1.0, g->Wt);
     rc = launch_check("k_weights");
   }
   if (rc == FS_OK) rc = run_pass2(g, sc);
