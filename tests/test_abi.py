@@ -1,0 +1,88 @@
+"""The C ABI (include/fastselect_amd.h): the in-tree library loads, exports
+every declared symbol, and reports errors the documented way.  No GPU compute
+here (the container has no GPU)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "fastselect_amd.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"FS_API\s+[\w\s\*]+?\b(fs_\w+)\s*\(", text)))
+
+
+def test_header_declares_expected_api():
+    from fastselect_amd import _lib
+    assert declared_symbols() == sorted(_lib.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol():
+    from fastselect_amd import _lib
+    assert os.path.dirname(_lib.LIB_PATH) == os.path.join(ROOT, "fastselect_amd")
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared_symbols():
+        assert hasattr(lib, name), f"{name} not exported"
+
+
+def test_version_and_device_count():
+    from fastselect_amd import _lib
+    assert "fastselect_amd" in _lib.version()
+    assert _lib.device_count() >= 0
+
+
+def test_gpu_backend_without_device_is_an_error():
+    from fastselect_amd import _lib
+    if _lib.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    x = np.random.default_rng(0).standard_normal((10, 3)).astype(np.float32)
+    with pytest.raises(RuntimeError, match="no HIP device"):
+        _lib.multisurf_score("gpu", x, np.arange(10) % 2, np.ones(3, np.float32), None, False,
+                             np.zeros(3, bool))
+
+
+def test_invalid_arguments_raise_value_error():
+    from fastselect_amd import _lib
+    x = np.zeros((1, 3), np.float32)  # n < 2
+    with pytest.raises(ValueError):
+        _lib.multisurf_score("cpu", x, [0], np.ones(3, np.float32), None, False,
+                             np.zeros(3, bool))
+    x = np.random.default_rng(0).standard_normal((5, 3)).astype(np.float32)
+    with pytest.raises(ValueError):  # feat_idx out of range
+        _lib.multisurf_score("cpu", x, np.arange(5) % 2, np.ones(3, np.float32),
+                             np.array([0, 7]), False, np.zeros(3, bool))
+    with pytest.raises(ValueError):  # y_enc outside [0, n_classes)
+        _lib.relieff_score("cpu", x, np.array([0, 1, 2, 0, 1]), np.ones(3, np.float32),
+                           np.zeros(3, bool), 1, np.array([0.5, 0.5], np.float32))
+    lib = _lib.lib()
+    rc = lib.fs_multisurf_score(7, 0, None, 0, 0, None, None, None, 0, 0, None, -1,
+                                (ctypes.c_float * 1)())
+    assert rc == _lib.FS_EINVAL
+    assert b"backend" in lib.fs_last_error()
+
+
+def test_plan_lifecycle_cpu():
+    """fs_plan_* on the CPU backend: stages compose to fs_multisurf_score."""
+    from fastselect_amd import _lib
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((150, 9)).astype(np.float32)
+    y = (x[:, 0] + 0.3 * rng.standard_normal(150) > 0).astype(float)
+    r = (x.max(0) - x.min(0)).astype(np.float32)
+    recip = (1 / r).astype(np.float32)
+    isd = np.zeros(9, bool)
+    pl = _lib.Plan("cpu", x, y, recip, isd)
+    rs, cn, sc = np.zeros(300), np.zeros(300), np.zeros(9)
+    pl.pass1(rs.ctypes.data)
+    pl.select(rs.ctypes.data, cn.ctypes.data)
+    pl.pass2(cn.ctypes.data, sc.ctypes.data)
+    tiles, pfe, refined = pl.info()
+    assert tiles == 3 and pfe == 2 * 3 * 128 * 128 * 9 and refined >= 0
+    assert pl.kernel_ms(0) == -1.0
+    pl.close()
+    one = _lib.multisurf_score("cpu", x, y, recip, None, False, isd)
+    np.testing.assert_allclose((sc / 150).astype(np.float32), one, rtol=0, atol=1e-7)

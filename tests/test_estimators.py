@@ -1,0 +1,303 @@
+"""scikit-learn surface of the estimators, mirroring the reference's own
+behaviour tests (tests/test_multisurf.py, test_relieff.py, test_surf.py,
+test_turf.py) on this package.  CPU backend (the container has no GPU); the
+same checks run on the GPU backend in tests/test_gpu.py.
+"""
+import numpy as np
+import pytest
+from numpy.testing import assert_allclose, assert_array_equal
+from sklearn.base import BaseEstimator, TransformerMixin
+from sklearn.exceptions import NotFittedError
+from sklearn.utils.estimator_checks import check_estimator
+
+from fastselect_amd import SURF, MultiSURF, ReliefF, TuRF, _lib
+
+
+@pytest.fixture
+def ms_data():
+    """test_multisurf.py:10-34"""
+    X = np.array([
+        [1.1, 5.0, 10, 3.0], [1.2, 4.0, 10, 3.0], [2.3, 6.0, 10, 3.0], [2.5, 5.5, 10, 3.0],
+        [1.5, 4.5, 20, 3.0], [8.8, 5.0, 20, 3.0], [8.9, 4.0, 20, 3.0], [9.5, 6.0, 20, 3.0],
+        [10.5, 4.5, 20, 3.0], [10.5, 4.5, 10, 3.0]], dtype=np.float32)
+    return X, np.array([0, 0, 0, 0, 0, 1, 1, 1, 1, 1], dtype=np.int32)
+
+
+@pytest.fixture
+def rs_data():
+    """test_relieff.py:10-32 / test_surf.py:11-33"""
+    X = np.array([
+        [0.1, 5.0, 10, 3.0], [0.2, 4.0, 10, 3.0], [0.3, 6.0, 10, 3.0],
+        [10.8, 5.0, 20, 3.0], [10.9, 4.0, 20, 3.0], [11.0, 6.0, 20, 3.0]], dtype=np.float32)
+    return X, np.array([0, 0, 0, 1, 1, 1], dtype=np.int32)
+
+
+NO_GPU = _lib.device_count() == 0
+
+# ---------------------------------------------------------------- MultiSURF
+
+
+def test_ms_feature_importance_ranking(ms_data):
+    X, y = ms_data
+    m = MultiSURF(n_features_to_select=1, backend="cpu", discrete_limit=4).fit(X, y)
+    assert set(m.top_features_) == {0}
+    assert_allclose(m.feature_importances_[3], 0.0, atol=1e-7)
+
+
+def test_ms_sklearn_api_compliance():
+    check_estimator(MultiSURF())
+
+
+def test_ms_fit_transform_shape(ms_data):
+    X, y = ms_data
+    assert MultiSURF(n_features_to_select=3, backend="cpu").fit_transform(X, y).shape == (10, 3)
+
+
+@pytest.mark.parametrize("est", [MultiSURF, SURF])
+def test_discrete_limit(est):
+    X = np.array([[i, i % 3] for i in range(11)] * 2, dtype=np.float32)
+    y = np.array([0] * 11 + [1] * 11, dtype=np.int32)
+    assert_array_equal(est(discrete_limit=10, backend="cpu", n_features_to_select=2)
+                       .fit(X, y).is_discrete_, [False, True])
+    assert_array_equal(est(discrete_limit=12, backend="cpu", n_features_to_select=2)
+                       .fit(X, y).is_discrete_, [True, True])
+
+
+@pytest.mark.parametrize("est", [MultiSURF, SURF, ReliefF])
+def test_not_fitted(est, ms_data):
+    with pytest.raises(NotFittedError):
+        est().transform(ms_data[0])
+
+
+@pytest.mark.parametrize("est", [MultiSURF, SURF, ReliefF])
+@pytest.mark.parametrize("bad", [-1, 0, 100])
+def test_invalid_n_features_to_select(est, rs_data, bad):
+    X, y = rs_data
+    with pytest.raises(ValueError):
+        est(n_features_to_select=bad).fit(X, y)
+    with pytest.raises(ValueError):
+        est(n_features_to_select=1.1).fit(X, y)
+    with pytest.raises(TypeError):
+        est(n_features_to_select="hi").fit(X, y)
+
+
+def test_ms_verbose(ms_data, capsys):
+    X, y = ms_data
+    for kw, text in (({}, "Running MultiSURF"), ({"use_star": True}, "Running MultiSURF*"),
+                     ({"backend": "cpu"}, "Running MultiSURF"),
+                     ({"backend": "cpu", "use_star": True}, "Running MultiSURF*")):
+        MultiSURF(verbose=True, **kw).fit(X, y)
+        assert text in capsys.readouterr().out
+
+
+@pytest.mark.parametrize("est", [MultiSURF, SURF, ReliefF])
+def test_bad_backend(est, rs_data):
+    with pytest.raises(ValueError):
+        est(n_features_to_select=4, backend="tpu").fit(*rs_data)
+
+
+@pytest.mark.skipif(not NO_GPU, reason="a GPU is visible")
+def test_gpu_backend_without_gpu(ms_data, rs_data):
+    """test_multisurf.py:170-178, test_surf.py:124-132: RuntimeError, never a
+    silent CPU fallback (also for ReliefF, which the reference left unchecked)."""
+    with pytest.raises(RuntimeError, match="no compatible GPU"):
+        MultiSURF(backend="gpu", n_features_to_select=2).fit(*ms_data)
+    with pytest.raises(RuntimeError, match="no HIP-enabled GPU is available"):
+        SURF(backend="gpu").fit(*rs_data)
+    with pytest.raises(RuntimeError, match="no compatible GPU"):
+        ReliefF(backend="gpu", n_neighbors=1).fit(*rs_data)
+
+
+@pytest.mark.parametrize("est", [MultiSURF, SURF])
+def test_nan_input(est, ms_data):
+    X, y = ms_data
+    X = X.copy()
+    X[0, 0] = np.nan
+    with pytest.raises(ValueError, match="Input X contains NaN"):
+        est(backend="cpu", n_features_to_select=2).fit(X, y)
+
+
+@pytest.mark.parametrize("est", [MultiSURF, SURF])
+def test_single_class(est, ms_data):
+    X, _ = ms_data
+    m = est(backend="cpu", n_features_to_select=4).fit(X, np.zeros(X.shape[0]))
+    assert np.all(m.feature_importances_ <= 1e-7)
+
+
+def test_auto_backend_resolution(ms_data):
+    m = MultiSURF(n_features_to_select=2).fit(*ms_data)
+    assert m.effective_backend_ == ("cpu" if NO_GPU else "gpu")
+
+# ------------------------------------------------------------------ ReliefF
+
+
+def test_rf_feature_importance_ranking(rs_data):
+    X, y = rs_data
+    t = ReliefF(n_neighbors=1, n_features_to_select=2, discrete_limit=4, backend="cpu").fit(X, y)
+    s = t.feature_importances_
+    assert s[0] > s[1] and s[2] > s[1]
+    assert_allclose(s[3], 0.0)
+    assert set(t.top_features_) == {0, 2}
+
+
+def test_rf_zero_range_feature(rs_data):
+    t = ReliefF(n_neighbors=1, n_features_to_select=4, backend="cpu").fit(*rs_data)
+    assert_allclose(t.feature_importances_[3], 0.0)
+
+
+def test_rf_sklearn_api_compliance():
+    check_estimator(ReliefF())
+
+
+def test_rf_fit_transform_shape(rs_data):
+    Xt = ReliefF(n_features_to_select=2, n_neighbors=2).fit_transform(*rs_data)
+    assert Xt.shape == (6, 2)
+
+
+def test_rf_discrete_limit():
+    X = np.array([[i, i % 3] for i in range(11)] * 2)
+    y = np.array([0] * 11 + [1] * 11)
+    assert_array_equal(ReliefF(discrete_limit=10, n_features_to_select=2, n_neighbors=1)
+                       .fit(X, y).is_discrete_, [False, True])
+    assert_array_equal(ReliefF(discrete_limit=12, n_features_to_select=2, n_neighbors=1)
+                       .fit(X, y).is_discrete_, [True, True])
+
+
+@pytest.mark.parametrize("bad_k", [-1, 0])
+def test_rf_invalid_n_neighbors(rs_data, bad_k):
+    with pytest.raises(ValueError):
+        ReliefF(n_neighbors=bad_k).fit(*rs_data)
+
+
+def test_rf_transform_wrong_width(rs_data):
+    X, y = rs_data
+    t = ReliefF(n_features_to_select=4, n_neighbors=2).fit(X, y)
+    with pytest.raises(ValueError):
+        t.transform(X[:, :-1])
+
+
+def test_rf_verbose(rs_data, capsys):
+    ReliefF(verbose=True).fit(*rs_data)
+    assert "Running ReliefF" in capsys.readouterr().out
+    ReliefF(verbose=True, backend="cpu").fit(*rs_data)
+    assert "Running ReliefF" in capsys.readouterr().out
+
+
+def test_rf_insufficient_neighbors_warning(rs_data):
+    with pytest.warns(UserWarning, match="is greater than or equal to the smallest class size"):
+        ReliefF(n_neighbors=5).fit(*rs_data)
+
+
+def test_rf_single_class(rs_data):
+    X, _ = rs_data
+    m = ReliefF(backend="cpu", n_neighbors=2).fit(X, np.zeros(6))
+    assert np.all(np.isfinite(m.feature_importances_))
+    assert np.all(m.feature_importances_ <= 0)
+
+# --------------------------------------------------------------------- SURF
+
+
+def test_surf_feature_importance_ranking(rs_data):
+    m = SURF(n_features_to_select=2, backend="cpu", discrete_limit=3).fit(*rs_data)
+    s = m.feature_importances_
+    assert s[0] > s[1] and s[2] > s[1]
+    assert_allclose(s[3], 0.0, atol=1e-7)
+    assert set(m.top_features_) == {0, 2}
+
+
+def test_surf_sklearn_api_compliance():
+    check_estimator(SURF())
+
+
+def test_surf_fit_transform_shape(rs_data):
+    assert SURF(n_features_to_select=2, backend="cpu").fit_transform(*rs_data).shape == (6, 2)
+
+
+def test_surf_verbose(rs_data, capsys):
+    SURF(verbose=True).fit(*rs_data)
+    assert "Running SURF" in capsys.readouterr().out
+    SURF(verbose=True, backend="cpu", use_star=True).fit(*rs_data)
+    assert "Running SURF*" in capsys.readouterr().out
+
+# --------------------------------------------------------------------- TuRF
+
+
+class MockReliefEstimator(BaseEstimator, TransformerMixin):
+    """test_turf.py:8-16"""
+
+    def fit(self, X, y=None):
+        self.feature_importances_ = np.linspace(1, 0, X.shape[1])
+        return self
+
+    def transform(self, X):
+        return X
+
+
+@pytest.fixture
+def turf_data():
+    rng = np.random.default_rng(0)
+    return rng.random((100, 20)), rng.integers(0, 2, 100)
+
+
+def test_turf_sklearn_compatibility():
+    check_estimator(TuRF(estimator=MockReliefEstimator(), n_features_to_select=2))
+
+
+def test_turf_basic(turf_data):
+    X, y = turf_data
+    t = TuRF(estimator=MockReliefEstimator(), n_features_to_select=5).fit(X, y)
+    Xt = t.transform(X)
+    assert t.n_features_in_ == 20 and len(t.top_features_) == 5 and Xt.shape == (100, 5)
+    np.testing.assert_array_equal(Xt, t.fit_transform(X, y))
+
+
+def test_turf_attributes(turf_data):
+    X, y = turf_data
+    t = TuRF(estimator=MockReliefEstimator(), n_features_to_select=7).fit(X, y)
+    assert t.feature_importances_.shape == (20,)
+    assert t.feature_importances_[0] > t.feature_importances_[-1]
+    np.testing.assert_array_equal(t.top_features_, np.arange(7))
+
+
+def test_turf_n_iterations(turf_data):
+    t = TuRF(estimator=MockReliefEstimator(), n_features_to_select=10, n_iterations=1,
+             pct_remove=0.1).fit(*turf_data)
+    assert len(t.top_features_) == 18
+
+
+def test_turf_removes_at_least_one(turf_data):
+    t = TuRF(estimator=MockReliefEstimator(), n_features_to_select=1, pct_remove=0.001)
+    assert len(t.fit(*turf_data).top_features_) == 1
+
+
+def test_turf_no_overshoot():
+    rng = np.random.default_rng(1)
+    t = TuRF(estimator=MockReliefEstimator(), n_features_to_select=10, pct_remove=0.2)
+    assert len(t.fit(rng.random((50, 11)), rng.integers(0, 2, 50)).top_features_) == 10
+
+
+def test_turf_verbose(turf_data, capsys):
+    TuRF(estimator=MockReliefEstimator(), n_features_to_select=15, verbose=True).fit(*turf_data)
+    out = capsys.readouterr().out
+    assert "Iteration" in out and "features remaining" in out
+
+
+def test_turf_errors(turf_data):
+    for bad in (0, 1, 1.1):
+        with pytest.raises(ValueError, match="pct_remove must be between 0 and 1"):
+            TuRF(estimator=MockReliefEstimator(), pct_remove=bad).fit(*turf_data)
+    with pytest.raises(NotFittedError):
+        TuRF(estimator=MockReliefEstimator()).transform(turf_data[0])
+    t = TuRF(estimator=MockReliefEstimator(), n_features_to_select=5).fit(*turf_data)
+    with pytest.raises(ValueError, match="X has 21 features, but TuRF is expecting 20"):
+        t.transform(np.random.default_rng(2).random((10, 21)))
+
+
+def test_turf_over_multisurf():
+    """TuRF driving the native MultiSURF (TuRF.py:87,111)."""
+    from sklearn.datasets import make_classification
+    X, y = make_classification(n_samples=120, n_features=30, n_informative=4, n_redundant=0,
+                               shuffle=False, random_state=0)
+    t = TuRF(estimator=MultiSURF(backend="cpu"), n_features_to_select=4, pct_remove=0.3).fit(X, y)
+    assert len(t.top_features_) == 4
+    assert len(set(t.top_features_.tolist()) & {0, 1, 2, 3}) >= 3

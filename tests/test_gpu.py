@@ -225,3 +225,12 @@ def test_large_p_flush_path(oracle):
     c = MultiSURF(backend="cpu").fit(X, y).feature_importances_
     assert scale_rel_err(g, c) < 1e-6
     assert_parity(g, oracle.multisurf_scores(X, y), TOL, k=10)
+
+
+@pytest.mark.parametrize("name", ["MultiSURF", "ReliefF", "SURF"])
+def test_sklearn_api_compliance_gpu(name):
+    """The 47 scikit-learn estimator checks with every fit on the GPU."""
+    from sklearn.utils.estimator_checks import check_estimator
+
+    import fastselect_amd
+    check_estimator(getattr(fastselect_amd, name)(backend="gpu"))

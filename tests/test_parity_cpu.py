@@ -1,0 +1,131 @@
+"""CPU-side parity: the product's native CPU backend (same pipeline as the HIP
+path: integer distances, mean correction, ambiguous-pair refinement, pair
+weights) against the oracle, and the sharded multi-rank path over gloo.
+
+Bar: 1e-5 scale-relative and identical top-k.
+"""
+import os
+import socket
+import warnings
+
+import numpy as np
+import pytest
+from conftest import assert_parity, scale_rel_err
+from sklearn.datasets import make_classification
+
+from fastselect_amd import SURF, MultiSURF, ReliefF, _lib
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+TOL = 1e-5
+
+
+def test_golden_vectors_cpu_backend():
+    g = np.load(os.path.join(GOLD, "oracle_vectors.npz"))
+    for name in ("a", "b", "c"):
+        X, y = g[f"{name}_X"], g[f"{name}_y"]
+        assert_parity(MultiSURF(backend="cpu").fit(X, y).feature_importances_,
+                      g[f"{name}_multisurf"], TOL, k=5)
+        assert_parity(MultiSURF(backend="cpu", use_star=True).fit(X, y).feature_importances_,
+                      g[f"{name}_multisurfstar"], TOL, k=5)
+        assert_parity(SURF(backend="cpu").fit(X, y).feature_importances_,
+                      g[f"{name}_surf"], TOL, k=5)
+        assert_parity(SURF(backend="cpu", use_star=True).fit(X, y).feature_importances_,
+                      g[f"{name}_surfstar"], TOL, k=5)
+        for k in (1, 3, 10):
+            assert_parity(ReliefF(backend="cpu", n_neighbors=k).fit(X, y).feature_importances_,
+                          g[f"{name}_relieff_k{k}"], TOL, k=5)
+
+
+@pytest.mark.parametrize("seed", [1, 11])
+def test_surf_mean_sensitivity(oracle, seed):
+    """SURF's float32 sequential row mean: 1-ulp distance errors used to flip
+    near/far decisions on these inputs."""
+    X, y = make_classification(n_samples=700, n_features=1500, n_informative=20,
+                               n_redundant=30, random_state=seed)
+    X = X + np.random.default_rng(seed).standard_normal(X.shape) * 1e-9
+    assert_parity(SURF(backend="cpu").fit(X, y).feature_importances_, oracle.surf_scores(X, y),
+                  TOL, k=10)
+
+
+def test_multisurf_threshold_flip_case(oracle):
+    """n=384, p=5000: one pair sits 7e-7 from its row threshold; quantised
+    distances alone flip it (6e-4 score error).  Refinement must fix it."""
+    X, y = make_classification(n_samples=384, n_features=5000, n_informative=20,
+                               n_redundant=50, random_state=3)
+    assert_parity(MultiSURF(backend="cpu").fit(X, y).feature_importances_,
+                  oracle.multisurf_scores(X, y), TOL, k=10)
+
+
+def test_relieff_small_class_self_hit(oracle):
+    """A class with fewer than k other members: the reference also counts the
+    focal sample itself as a (zero-diff) hit (ReliefF.py:144-168)."""
+    X, y = make_classification(n_samples=120, n_features=30, weights=[0.9], random_state=1)
+    for k in (10, 12, 20, 119):
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", UserWarning)
+            s = ReliefF(backend="cpu", n_neighbors=k).fit(X, y).feature_importances_
+        assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=k), TOL)
+
+
+def _sharded_cpu(x, y, recip, isd, world, use_star):
+    n, p = x.shape
+    plans = [_lib.Plan("cpu", x, y, recip, isd, use_star=use_star, rank=r, world=world)
+             for r in range(world)]
+    rs = [np.zeros(2 * n) for _ in plans]
+    for pl, b in zip(plans, rs):
+        pl.pass1(b.ctypes.data)
+    rsum = np.sum(rs, axis=0)
+    cn = [np.zeros(2 * n) for _ in plans]
+    for pl, b in zip(plans, cn):
+        pl.select(rsum.ctypes.data, b.ctypes.data)
+    csum = np.sum(cn, axis=0)
+    sc = [np.zeros(p) for _ in plans]
+    for pl, b in zip(plans, sc):
+        pl.pass2(csum.ctypes.data, b.ctypes.data)
+    return (np.sum(sc, axis=0) / n).astype(np.float32)
+
+
+@pytest.mark.parametrize("world", [2, 3, 5])
+def test_tile_sharding_sums_to_single(world):
+    X, y = make_classification(n_samples=450, n_features=40, random_state=world)
+    x = X.astype(np.float32)
+    r = (x.max(0) - x.min(0)).astype(np.float32)
+    recip = (1 / r).astype(np.float32)
+    isd = np.zeros(40, bool)
+    for star in (False, True):
+        one = _lib.multisurf_score("cpu", x, y, recip, None, star, isd)
+        many = _sharded_cpu(x, y, recip, isd, world, star)
+        assert scale_rel_err(many, one) < 1e-6
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _gloo_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fastselect_amd.parallel import multisurf_scores
+    X, y = make_classification(n_samples=300, n_features=50, random_state=0)
+    s = multisurf_scores(X, y, use_star=True, backend="cpu")
+    np.save(f"{out_path}.{rank}.npy", s)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_matches_single(tmp_path):
+    """The N>1 path end to end: two processes, gloo all-reduces of the three
+    exchange vectors (the RCCL path on GPUs), equal to one process."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "scores")
+    mp.spawn(_gloo_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    a, b = np.load(out + ".0.npy"), np.load(out + ".1.npy")
+    np.testing.assert_array_equal(a, b)
+    X, y = make_classification(n_samples=300, n_features=50, random_state=0)
+    ref = MultiSURF(backend="cpu", use_star=True).fit(X, y).feature_importances_
+    assert scale_rel_err(a, ref) < 1e-6
