@@ -16,7 +16,7 @@ rows, pair weights, pass 2 (score accumulation), all-reduces, / n.
 
 Rank 0 prints ONE JSON line: value = n*p / step time (feature-scores/s, the
 whole job across all ranks), a `roofline` object for the dominant kernel
-(VALU bound; algorithmic FLOPs = 2 per pair-feature evaluation)
+(VALU bound; 4 FMA-equivalent FLOPs per pair-feature evaluation)
 measured with HIP events on the stream the kernels run on, and at N=1 a
 `cpu_baseline` from the C oracle (oracle/relief_oracle.c, OpenMP) timed on a
 bounded sample of focal samples of the same data and extrapolated.
@@ -34,10 +34,32 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# fp32 VALU peak for non-FMA adds/subs: 256 CU x 128 lanes x 2.4 GHz
-# (the 157.3 TFLOP/s spec counts an FMA as 2 FLOPs; MI355X_MICROARCH.md)
-VALU_PEAK_TFLOPS = 78.6
+# Peak FP32 vector rate, MI355X_MICROARCH.md: 157.3 TFLOP/s = 256 CU x 4 SIMD x
+# 64 lanes / 2 cycles per wave64 v_fma_f32 x 2 FLOP x 2.4 GHz.  Both hot
+# kernels spend 2 full-rate VALU issue slots per pair-feature evaluation (PFE):
+# k_score v_sub_f32 + v_fma_f32, k_dist one half-rate v_sad_u32.  Two issue
+# slots are the cost of two FMAs, so one PFE is priced at 4 FMA-equivalent
+# FLOPs against that peak ("Kernels").
+VALU_PEAK_TFLOPS = 157.3
+FLOP_PER_PFE = 4
 HBM_PEAK_GBPS = 8000.0
+TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def pmc_traffic(kernel, n, p, world):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (tools/summarize_prof.py), if it was taken on this workload."""
+    try:
+        with open(TRAFFIC_FILE) as f:
+            t = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    if t.get("n") != n or t.get("p") != p or t.get("world", 1) != world:
+        return None, None
+    k = t.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k["hbm_bytes_per_launch"], t.get("source")
 
 
 def log(msg):
@@ -63,7 +85,7 @@ def cpu_baseline(x, y, budget_s=15.0):
     O.multisurf_scores(x, y, i_range=(0, m), n_jobs=threads)
     t = time.perf_counter() - t0
     if t < budget_s / 3:
-        m = int(min(n, max(m, threads * round(budget_s / t))))
+        m = int(min(n, max(m, threads * round(budget_s / t * m / threads))))
         t0 = time.perf_counter()
         O.multisurf_scores(x, y, i_range=(0, m), n_jobs=threads)
         t = time.perf_counter() - t0
@@ -140,19 +162,19 @@ def main():
     elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
 
-    # dominant kernel roofline (rank-local launch; PFE per launch = owned
-    # tiles x 128^2 x p, FLOPs = 2 per PFE)
+    # dominant kernel roofline (rank-local launch).  Algorithmic count: unique
+    # pairs x features / world (padding and the duplicated half of diagonal
+    # tiles are executed but not counted).
     d_ms, s_ms = float(np.mean(dist_ms)), float(np.mean(score_ms))
-    # algorithmic count: unique pairs x features (padding and the duplicated
-    # half of diagonal tiles are executed but not counted)
     pfe_launch = args.n * (args.n - 1) / 2.0 * args.p / world
     kern = {"k_dist": d_ms, "k_score": s_ms}
     dom = max(kern, key=kern.get)
-    achieved = 2.0 * pfe_launch / (kern[dom] * 1e-3) / 1e12
-    # algorithmic HBM bytes of k_dist per launch: both LDS panels of every
-    # owned tile once + the D tile written twice (f64)
+    achieved = FLOP_PER_PFE * pfe_launch / (kern[dom] * 1e-3) / 1e12
+    # algorithmic bytes one launch moves from HBM/L2 into the CUs: both row
+    # panels of every owned tile once (+ D write for k_dist, Wt read for k_score)
     alg_bytes = {"k_dist": tiles * (2 * 128 * args.p * 4 + 2 * 128 * 128 * 8),
                  "k_score": tiles * (2 * 128 * args.p * 4 + 128 * 128 * 4)}
+    traffic, traffic_src = pmc_traffic(dom, args.n, args.p, world)
 
     if rank == 0:
         out = {
@@ -166,7 +188,9 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "fp32 (u32 exact integer distances)",
+            "dtype": "fp32",
+            "arith": "pass 1: u32 integer L1 distances (exact); pass 2: f32 diffs x f32 pair "
+                     "weights, f64 accumulation",
             "data": "synthetic make_classification(n_informative=20, n_redundant=100, random_state=42)",
             "config": {"workload": f"MultiSURF{'*' if args.star else ''} n={args.n} p={args.p} "
                                    f"(BASELINE configs[3])",
@@ -175,14 +199,16 @@ def main():
             "roofline": {
                 "bound": "valu", "kernel": dom, "achieved": achieved,
                 "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / VALU_PEAK_TFLOPS,
-                "traffic": None,
-                "flop_per_pfe": 2,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "flop_per_pfe": FLOP_PER_PFE,
+                "pfe_per_s": pfe_launch / (kern[dom] * 1e-3),
                 "kernel_ms": kern,
                 "pfe_per_launch": pfe_launch,
                 "hbm_alg_GBps": {k: alg_bytes[k] / (kern[k] * 1e-3) / 1e9 for k in kern},
                 "hbm_peak_GBps": HBM_PEAK_GBPS,
             },
-            "refined_rows": refined,
+            "refined_pairs": refined,
         }
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline (oracle) ...")

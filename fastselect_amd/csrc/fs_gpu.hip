@@ -200,13 +200,25 @@ __global__ __launch_bounds__(256) void k_colrank(const uint32_t* __restrict__ xq
 }
 
 // corr[i] = sum over continuous columns of the per-feature bias terms.
-__global__ void k_rowcorr(const float* __restrict__ epsT, int64_t n, int64_t n_pad, int64_t pc,
-                          double* __restrict__ corr) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
+// Workgroup = 64 rows x 16 waves; wave w sums columns w, w+16, ... (one
+// coalesced 256-byte read per column), then the 16 partials are added in a
+// fixed order (deterministic).
+__global__ __launch_bounds__(1024) void k_rowcorr(const float* __restrict__ epsT, int64_t n,
+                                                  int64_t n_pad, int64_t pc,
+                                                  double* __restrict__ corr) {
+  __shared__ double part[16][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;  // < n_pad
   double s = 0.0;
-  for (int64_t c = 0; c < pc; c++) s += (double)epsT[c * n_pad + i];
-  corr[i] = s;
+  for (int64_t c = wave; c < pc; c += 16) s += (double)epsT[c * n_pad + i];
+  part[wave][lane] = s;
+  __syncthreads();
+  if (wave == 0 && i < n) {
+    double t = 0.0;
+#pragma unroll
+    for (int w = 0; w < 16; w++) t += part[w][lane];
+    corr[i] = t;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -689,69 +701,133 @@ __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, i
 // ---------------------------------------------------------------------------
 // Pass 2: weighted per-feature accumulation over owned tiles
 // ---------------------------------------------------------------------------
-// Grid (PW/64 feature blocks, segments of seg_len tiles); 4 waves per
-// workgroup, wave w handles rows w*32 .. w*32+31 of every tile, lane = one
-// feature.  For each column jj the 32 pair weights of that sub-tile are
-// wave-uniform and come through scalar loads; 4 f32 partial sums are folded
-// into a double every 32 columns.
+// Grid (ceil(PW/128) feature blocks, segments of seg_len tiles); 4 waves per
+// workgroup, wave w handles rows w*32 .. w*32+31 of every tile; lane l scores
+// the two features c0 = blk*128 + l and c1 = c0 + 64 (each half is wholly
+// continuous or wholly discrete because PC is a multiple of 64).  For each
+// column jj the 32 pair weights of the wave's sub-tile are wave-uniform and
+// live in SGPRs; they feed 2 x 32 (sub, fma|.|) pairs.  Software pipeline:
+// the next column's weights are requested (s_load) right after the current
+// column's have been consumed once, and the B values run two columns ahead
+// (in-order vector loads), so neither latency is exposed.  A rows stay in
+// VGPRs across consecutive tiles of the same row block.  Per feature, 4 f32
+// partial sums are folded into a double every 32 columns.
 template <bool DISC>
 __device__ __forceinline__ float pair_term(float a, float b, float w, float acc) {
   if (DISC) return acc + ((a != b) ? w : 0.0f);
   return __builtin_fmaf(__builtin_fabsf(a - b), w, acc);
 }
 
-template <bool DISC>
-__device__ __forceinline__ double score_tiles(const float* __restrict__ xs, int64_t PW,
-                                              int64_t c, int wave,
-                                              const int2* __restrict__ tiles,
-                                              const float* __restrict__ Wt, int64_t t_begin,
-                                              int64_t t_end) {
-  double accd = 0.0;
+// Order point: everything computing `v` happens before, and no memory access
+// moves across (so a scalar load placed after it is issued after the wait
+// for the weights `v` depends on).
+#define FS_ORDER_AFTER(v) asm volatile("" : "+v"(v)::"memory")
+
+template <bool D0, bool D1, bool TWO>
+__device__ __forceinline__ void score_column(const float (&a0)[kSubRows],
+                                             const float (&a1)[kSubRows],
+                                             const float* __restrict__ w, float b0, float b1,
+                                             float (&acc)[8], const float* __restrict__ wnext,
+                                             float (&wn)[kSubRows]) {
+  acc[0] = pair_term<D0>(a0[0], b0, w[0], acc[0]);
+  FS_ORDER_AFTER(acc[0]);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int r = 0; r < kSubRows; r++) wn[r] = wnext[r];
+  __builtin_amdgcn_sched_barrier(0);  // issue the s_loads here, not later
+#pragma unroll
+  for (int r = 0; r < kSubRows; r++) {
+    if (r != 0) acc[r & 3] = pair_term<D0>(a0[r], b0, w[r], acc[r & 3]);
+    if (TWO) acc[4 + (r & 3)] = pair_term<D1>(a1[r], b1, w[r], acc[4 + (r & 3)]);
+  }
+  // keep the next column's arithmetic (which waits for wn) below this point
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool D0, bool D1, bool TWO>
+__device__ __forceinline__ void score_tiles(const float* __restrict__ xs, int64_t PW,
+                                            int64_t c0, int wave,
+                                            const int2* __restrict__ tiles,
+                                            const float* __restrict__ Wt, int64_t t_begin,
+                                            int64_t t_end, double& out0, double& out1) {
+  double s0 = 0.0, s1 = 0.0;
+  float a0[kSubRows], a1[kSubRows];
+  int cur_bi = -1;
+  // wA always holds column 0 of the current tile: the last prefetch of a
+  // tile is column 0 of the next one (tiles of a segment are consecutive).
+  float wA[kSubRows], wB[kSubRows];
+  {
+    const float* __restrict__ w0 = Wt + t_begin * (kTile * kTile) + wave * kSubRows;
+#pragma unroll
+    for (int r = 0; r < kSubRows; r++) wA[r] = w0[r];
+  }
   for (int64_t t = t_begin; t < t_end; t++) {
     const int2 tl = tiles[t];
-    const int64_t rbase = (int64_t)tl.x * kTile + wave * kSubRows;
-    float a[kSubRows];
+    if (tl.x != cur_bi) {
+      cur_bi = tl.x;
+      const float* __restrict__ xa = xs + ((int64_t)tl.x * kTile + wave * kSubRows) * PW + c0;
 #pragma unroll
-    for (int r = 0; r < kSubRows; r++) a[r] = xs[(rbase + r) * PW + c];
-    const float* __restrict__ wtile = Wt + t * (kTile * kTile) + wave * kSubRows;
-    const float* __restrict__ xb = xs + (int64_t)tl.y * kTile * PW + c;
-    for (int jb = 0; jb < kTile; jb += 32) {
-      float acc0 = 0.0f, acc1 = 0.0f, acc2 = 0.0f, acc3 = 0.0f;
-#pragma unroll 2
-      for (int jj = jb; jj < jb + 32; jj++) {
-        const float b = xb[(int64_t)jj * PW];
-        const float* __restrict__ w = wtile + jj * kTile;
-#pragma unroll
-        for (int r = 0; r < kSubRows; r += 4) {
-          acc0 = pair_term<DISC>(a[r + 0], b, w[r + 0], acc0);
-          acc1 = pair_term<DISC>(a[r + 1], b, w[r + 1], acc1);
-          acc2 = pair_term<DISC>(a[r + 2], b, w[r + 2], acc2);
-          acc3 = pair_term<DISC>(a[r + 3], b, w[r + 3], acc3);
-        }
+      for (int r = 0; r < kSubRows; r++) {
+        a0[r] = xa[(int64_t)r * PW];
+        a1[r] = TWO ? xa[(int64_t)r * PW + 64] : 0.0f;
       }
-      accd += ((double)acc0 + (double)acc1) + ((double)acc2 + (double)acc3);
+    }
+    const float* __restrict__ wt = Wt + t * (kTile * kTile) + wave * kSubRows;
+    const float* __restrict__ xb = xs + (int64_t)tl.y * kTile * PW + c0;
+    float bA0 = xb[0], bA1 = TWO ? xb[64] : 0.0f;
+    float bB0 = xb[PW], bB1 = TWO ? xb[PW + 64] : 0.0f;
+    // The prefetches of the last column pair reach 2 rows past the tile (xs
+    // has 2 spare rows) and column 0 of tile t+1 (Wt has a spare tile).
+    const float* __restrict__ xn = xb + 2 * PW;
+    const float* __restrict__ wn = wt + kTile;
+    for (int jb = 0; jb < kTile; jb += 32) {
+      float acc[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+      for (int jj = 0; jj < 32; jj += 2) {
+        const float cA0 = xn[0], cA1 = TWO ? xn[64] : 0.0f;
+        const float cB0 = xn[PW], cB1 = TWO ? xn[PW + 64] : 0.0f;
+        score_column<D0, D1, TWO>(a0, a1, wA, bA0, bA1, acc, wn, wB);
+        score_column<D0, D1, TWO>(a0, a1, wB, bB0, bB1, acc, wn + kTile, wA);
+        bA0 = cA0; bA1 = cA1; bB0 = cB0; bB1 = cB1;
+        xn += 2 * PW;
+        wn += 2 * kTile;
+      }
+      s0 += ((double)acc[0] + (double)acc[1]) + ((double)acc[2] + (double)acc[3]);
+      if (TWO) s1 += ((double)acc[4] + (double)acc[5]) + ((double)acc[6] + (double)acc[7]);
     }
   }
-  return accd;
+  out0 = s0;
+  out1 = s1;
 }
 
 __global__ __launch_bounds__(256) void k_score(const float* __restrict__ xs, int64_t PW,
                                                int64_t PC, const int2* __restrict__ tiles,
                                                const float* __restrict__ Wt, int64_t n_tiles,
                                                int64_t seg_len, double* __restrict__ spart) {
-  __shared__ double red[4][64];
+  __shared__ double red[2][4][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  const int64_t f0 = (int64_t)blockIdx.x * 128;
+  const int64_t c0 = f0 + lane;
   const int64_t t_begin = (int64_t)blockIdx.y * seg_len;
   const int64_t t_end = t_begin + seg_len < n_tiles ? t_begin + seg_len : n_tiles;
-  const bool disc = (int64_t)blockIdx.x * 64 >= PC;
-  const double accd = disc ? score_tiles<true>(xs, PW, c, wave, tiles, Wt, t_begin, t_end)
-                           : score_tiles<false>(xs, PW, c, wave, tiles, Wt, t_begin, t_end);
-  red[wave][lane] = accd;
+  const bool two = f0 + 64 < PW;
+  const bool d0 = f0 >= PC, d1 = f0 + 64 >= PC;
+  double s0 = 0.0, s1 = 0.0;
+  if (two) {
+    if (!d1) score_tiles<false, false, true>(xs, PW, c0, wave, tiles, Wt, t_begin, t_end, s0, s1);
+    else if (d0) score_tiles<true, true, true>(xs, PW, c0, wave, tiles, Wt, t_begin, t_end, s0, s1);
+    else score_tiles<false, true, true>(xs, PW, c0, wave, tiles, Wt, t_begin, t_end, s0, s1);
+  } else {
+    if (d0) score_tiles<true, true, false>(xs, PW, c0, wave, tiles, Wt, t_begin, t_end, s0, s1);
+    else score_tiles<false, false, false>(xs, PW, c0, wave, tiles, Wt, t_begin, t_end, s0, s1);
+  }
+  red[0][wave][lane] = s0;
+  red[1][wave][lane] = s1;
   __syncthreads();
-  if (wave == 0)
-    spart[(int64_t)blockIdx.y * PW + c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (wave < 2 && (wave == 0 || two)) {
+    const double v = (red[wave][0][lane] + red[wave][1][lane]) + (red[wave][2][lane] + red[wave][3][lane]);
+    spart[(int64_t)blockIdx.y * PW + c0 + wave * 64] = v;
+  }
 }
 
 // out[out_pos[c]] = sum over segments of part[seg][c] (fixed order).
@@ -1037,7 +1113,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   g->n_tiles = (int64_t)bi.size();
   std::vector<int2> tl(g->n_tiles);
   for (int64_t t = 0; t < g->n_tiles; t++) tl[t] = make_int2(bi[t], bj[t]);
-  const int64_t nfb = Q.PW / 64;
+  const int64_t nfb = (Q.PW + 127) / 128;
   // ~64k pass-2 workgroups: enough to fill 256 CUs and bound tail imbalance.
   g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + 65535) / 65536);
   g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
@@ -1052,7 +1128,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       (rc = dalloc(g, &g->off, Q.PW)) || (rc = dalloc(g, &g->qs, Q.PW)) ||
       (rc = dalloc(g, &g->scl, Q.PW)) || (rc = dalloc(g, &g->dtab_off, Q.PW + 1)) ||
       (rc = dalloc(g, &g->dtab, Q.dtab.size())) || (rc = dalloc(g, &g->lab, Q.n_pad)) ||
-      (rc = dalloc(g, &g->xs, (size_t)Q.n_pad * Q.PW)) || (rc = dalloc(g, &g->corr, Q.n_pad)) ||
+      (rc = dalloc(g, &g->xs, (size_t)(Q.n_pad + 2) * Q.PW)) || (rc = dalloc(g, &g->corr, Q.n_pad)) ||
       (rc = dalloc(g, &g->D, (size_t)Q.n_pad * Q.n_pad)) ||
       (rc = dalloc(g, &g->tiles, g->n_tiles)) || (rc = dalloc(g, &g->thr, Q.n_pad)) ||
       (rc = dalloc(g, &g->list, g->list_cap)) || (rc = dalloc(g, &g->list_count, 1)))
@@ -1065,7 +1141,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       return fail(rc);
   }
   if (Q.algo != ALGO_RELIEFF) {
-    if ((rc = dalloc(g, &g->Wt, (size_t)g->n_tiles * kTile * kTile)) ||
+    if ((rc = dalloc(g, &g->Wt, (size_t)(g->n_tiles + 1) * kTile * kTile)) ||
         (rc = dalloc(g, &g->spart, (size_t)g->nseg * Q.PW)))
       return fail(rc);
   }
@@ -1122,8 +1198,8 @@ static int run_quantize_dist(Plan* g) {
                                                        g->epsT);
       FS_TRY(launch_check("k_colrank"));
     }
-    k_rowcorr<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(g->epsT, Q.n, Q.n_pad, Q.pc,
-                                                                    g->corr);
+    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, g->stream>>>(g->epsT, Q.n, Q.n_pad, Q.pc,
+                                                                 g->corr);
     FS_TRY(launch_check("k_rowcorr"));
   }
   if (g->n_tiles > 0) {
@@ -1174,7 +1250,7 @@ static int refine_pairs(Plan* g, int algo, double delta) {
 
 static int run_pass2(Plan* g, double* scores_dev) {
   const Prepared& Q = g->P;
-  const int64_t nfb = Q.PW / 64;
+  const int64_t nfb = (Q.PW + 127) / 128;
   FS_HIP(hipMemsetAsync(scores_dev, 0, sizeof(double) * Q.n_kept, g->stream));
   if (g->n_tiles == 0) return FS_OK;
   FS_HIP(hipEventRecord(g->ev[2], g->stream));

@@ -11,6 +11,7 @@ usage: python tools/summarize_prof.py gpurun_out/prof_r01 profiles/r01
 """
 import csv
 import json
+import os
 import shutil
 import sys
 
@@ -41,6 +42,14 @@ def main(src, out):
     bench = json.load(open(f"{src}/bench_trace.json"))
     with open(f"{out}_summary.json", "w") as f:
         json.dump({"bench": bench, "kernels": stats}, f, indent=1)
+    # the per-launch HBM bytes bench.py reports as roofline.traffic
+    cfg = bench["config"]
+    traffic = {"n": cfg["n_samples"], "p": cfg["n_features"], "world": bench["n_gpus"],
+               "source": f"{out}_summary.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, KiB x 1024)",
+               "kernels": {k: {"hbm_bytes_per_launch": s["hbm_bytes_per_launch"], "avg_ms": s["avg_ms"]}
+                           for k, s in stats.items() if "hbm_bytes_per_launch" in s and k.startswith("k_")}}
+    with open(os.path.join(os.path.dirname(out), "pmc_traffic.json"), "w") as f:
+        json.dump(traffic, f, indent=1)
     for k, s in sorted(stats.items(), key=lambda kv: -kv[1]["avg_ms"])[:12]:
         print(f"{k:28s} {s['avg_ms']:10.3f} ms  {s.get('hbm_GBps', float('nan')):8.1f} GB/s")
 
