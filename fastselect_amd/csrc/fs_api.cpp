@@ -8,9 +8,28 @@
 #include "../../include/fastselect_amd.h"
 #include "fs_internal.h"
 
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+
 namespace fs {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
+
+bool trace_on() {
+  static const bool on = std::getenv("FS_TRACE") != nullptr;
+  return on;
+}
+
+void trace_mark(const char* phase) {
+  if (!trace_on()) return;
+  using clk = std::chrono::steady_clock;
+  static thread_local clk::time_point last = clk::now();
+  const clk::time_point now = clk::now();
+  std::fprintf(stderr, "[fs_trace] %-22s %9.3f ms\n", phase,
+               std::chrono::duration<double, std::milli>(now - last).count());
+  last = now;
+}
 }  // namespace fs
 
 using namespace fs;
@@ -55,7 +74,9 @@ int fs_multisurf_score(int backend, int device, const float* x, int64_t n, int64
   int rc = check_backend(backend, device);
   if (rc != FS_OK) return rc;
   Prepared P;
+  trace_mark("multisurf: enter");
   rc = prepare(P, ALGO_MULTISURF, x, 0, n, p, feat_idx, n_kept, recip, is_discrete, n_jobs);
+  trace_mark("prepare (host)");
   if (rc) return map_prep_rc(rc);
   if (encode_labels_f64(P, y)) return FS_EINVAL;
   P.use_star = use_star ? 1 : 0;
@@ -80,7 +101,9 @@ int fs_relieff_score(int backend, int device, const float* x, int64_t n, int64_t
   int rc = check_backend(backend, device);
   if (rc != FS_OK) return rc;
   Prepared P;
+  trace_mark("relieff: enter");
   rc = prepare(P, ALGO_RELIEFF, x, 0, n, p, nullptr, p, recip, is_discrete, n_jobs);
+  trace_mark("prepare (host)");
   if (rc) return map_prep_rc(rc);
   P.labels.assign(y_enc, y_enc + n);
   for (int64_t i = 0; i < n; i++)
@@ -109,7 +132,9 @@ int fs_surf_score(int backend, int device, const double* x, int64_t n, int64_t p
   int rc = check_backend(backend, device);
   if (rc != FS_OK) return rc;
   Prepared P;
+  trace_mark("surf: enter");
   rc = prepare(P, ALGO_SURF, x, 1, n, p, nullptr, p, recip, is_discrete, n_jobs);
+  trace_mark("prepare (host)");
   if (rc) return map_prep_rc(rc);
   if (encode_labels_i32(P, y)) return FS_EINVAL;
   P.use_star = use_star ? 1 : 0;

@@ -1060,11 +1060,13 @@ static int launch_check(const char* what) {
 void plan_destroy(Plan* g) {
   if (!g) return;
   if (g->stream) (void)hipStreamSynchronize(g->stream);
+  trace_mark("kernels (to sync)");
   for (void* q : g->owned) (void)hipFree(q);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
   if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
   delete g;
+  trace_mark("plan: free");
 }
 
 int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int device,
@@ -1123,6 +1125,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   g->list_cap = std::max<int64_t>(1 << 16, Q.n * 64);
   const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
   int rc;
+  trace_mark("plan: host setup");
   if ((rc = dalloc(g, (char**)&g->x, xbytes)) ||
       (rc = dalloc(g, &g->src_col, Q.PW)) || (rc = dalloc(g, &g->out_pos, Q.PW)) ||
       (rc = dalloc(g, &g->off, Q.PW)) || (rc = dalloc(g, &g->qs, Q.PW)) ||
@@ -1145,6 +1148,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
         (rc = dalloc(g, &g->spart, (size_t)g->nseg * Q.PW)))
       return fail(rc);
   }
+  trace_mark("plan: hipMalloc");
   std::vector<double> qs(Q.PW, 0.0);
   for (int64_t c = 0; c < Q.PW; c++) qs[c] = Q.scale[c] * Q.SC;
   std::vector<int32_t> lab(Q.n_pad, -1);
@@ -1160,6 +1164,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       (rc = h2d(g, g->tiles, tl.data(), g->n_tiles)))
     return fail(rc);
   if (hipStreamSynchronize(g->stream) != hipSuccess) return fail(FS_EHIP);
+  trace_mark("plan: H2D");
   *out = g;
   return FS_OK;
 }

@@ -40,6 +40,10 @@ constexpr int kFeatPad = 64;        // feature blocks (one wave of lanes in pass
 constexpr int kSubRows = 32;        // pass-2 rows held in registers per sweep
 
 void set_error(const std::string& msg);
+// Phase timing on stderr when the environment sets FS_TRACE (host wall clock;
+// callers synchronise the stream first where device time matters).
+bool trace_on();
+void trace_mark(const char* phase);
 
 // Host-side derived problem description, identical for both backends.
 struct Prepared {

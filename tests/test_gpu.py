@@ -166,6 +166,31 @@ def test_edge_cases(oracle):
     assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=20), TOL)
 
 
+@pytest.mark.parametrize("n,pc,pd", [(400, 150, 70), (333, 64, 200), (260, 300, 10)])
+def test_mixed_feature_blocks(oracle, n, pc, pd):
+    """Continuous and discrete columns in every pass-2 block layout: a
+    128-feature block wholly continuous, wholly discrete, half-and-half, and
+    a trailing single 64-feature half (continuous-first permutation padded to
+    64 per kind)."""
+    from fastselect_amd import SURF, MultiSURF, ReliefF
+    rng = np.random.default_rng(n + pc)
+    Xc, y = make_classification(n_samples=n, n_features=pc, n_informative=min(10, pc),
+                                n_redundant=0, random_state=pc)
+    Xd = rng.integers(0, 4, size=(n, pd)).astype(float)
+    Xd[:, 0] = (y + rng.integers(0, 2, n)) % 3   # an informative discrete column
+    X = np.empty((n, pc + pd))
+    perm = rng.permutation(pc + pd)               # interleave the two kinds
+    X[:, perm[:pc]] = Xc
+    X[:, perm[pc:]] = Xd
+    for star in (False, True):
+        assert_parity(_fit(MultiSURF, X, y, use_star=star),
+                      oracle.multisurf_scores(X, y, use_star=star), TOL, k=10)
+        assert_parity(_fit(SURF, X, y, use_star=star), oracle.surf_scores(X, y, use_star=star),
+                      TOL, k=10)
+    assert_parity(_fit(ReliefF, X, y, n_neighbors=5), oracle.relieff_scores(X, y, n_neighbors=5),
+                  TOL, k=10)
+
+
 def test_feat_idx_subset(oracle):
     from fastselect_amd import _lib
     X, y = make_classification(n_samples=260, n_features=90, random_state=3)
