@@ -17,11 +17,6 @@ from sklearn.utils.validation import check_is_fitted, validate_data
 from . import _base, _lib
 
 
-def _compute_ranges(x: np.ndarray) -> np.ndarray:
-    """MultiSURF.py:141-144."""
-    return (x.max(axis=0) - x.min(axis=0)).astype(np.float32)
-
-
 class MultiSURF(TransformerMixin, BaseEstimator):
     """MI355X-accelerated feature selection with the MultiSURF algorithm.
 
@@ -71,11 +66,12 @@ class MultiSURF(TransformerMixin, BaseEstimator):
         n_select = self._validate_parameters(n_samples, self.n_features_in_)
         self.effective_backend_ = _base.effective_backend(self.backend)
 
-        feature_ranges = _compute_ranges(x)
+        is_discrete, col_min, col_max = _base.column_preprocess(x, self.discrete_limit,
+                                                                self.effective_backend_)
+        feature_ranges = (col_max - col_min).astype(np.float32)  # _compute_ranges
         feature_ranges[feature_ranges == 0] = 1
         recip_full = (1.0 / feature_ranges).astype(np.float32)
         all_feature_indices = np.arange(self.n_features_in_, dtype=np.int64)
-        is_discrete = _base.discrete_mask(x, self.discrete_limit)
         self.is_discrete_ = is_discrete
 
         if self.verbose:

@@ -85,12 +85,15 @@ class ReliefF(TransformerMixin, BaseEstimator):
                 UserWarning,
             )
 
-        is_discrete = _base.discrete_mask(x, self.discrete_limit)
+        # preprocessing runs where the scoring will (the backend itself is
+        # resolved below, after these steps, as in the reference)
+        where = "gpu" if self.backend != "cpu" and _lib.gpu_available() else "cpu"
+        is_discrete, col_min, col_max = _base.column_preprocess(x, self.discrete_limit, where)
         self.is_discrete_ = is_discrete
         class_labels, class_counts = np.unique(y, return_counts=True)
         class_probs = class_counts / len(y)
         y_enc = np.searchsorted(class_labels, y)
-        feature_ranges = x.max(axis=0) - x.min(axis=0)
+        feature_ranges = col_max - col_min
         feature_ranges[is_discrete] = 1.0
         feature_ranges[feature_ranges == 0] = 1.0
         recip_full = (1.0 / feature_ranges).astype(np.float32)

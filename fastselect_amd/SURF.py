@@ -69,8 +69,9 @@ class SURF(TransformerMixin, BaseEstimator):
         else:
             self.effective_backend_ = self.backend
 
-        self.is_discrete_ = _base.discrete_mask(X, self.discrete_limit)
-        feature_ranges = X.max(axis=0) - X.min(axis=0)
+        self.is_discrete_, col_min, col_max = _base.column_preprocess(
+            X, self.discrete_limit, self.effective_backend_)
+        feature_ranges = col_max - col_min
         feature_ranges[self.is_discrete_] = 1.0
         feature_ranges[feature_ranges == 0] = 1.0
         recip_full = (1.0 / feature_ranges).astype(np.float32)

@@ -47,11 +47,24 @@ def effective_backend(backend: str) -> str:
     return backend
 
 
-def discrete_mask(x: np.ndarray, discrete_limit: int) -> np.ndarray:
-    """``np.unique(x[:, f]).size <= discrete_limit`` per column
-    (MultiSURF.py:416-420, ReliefF.py:366-368, SURF.py:347-350)."""
-    return np.array([np.unique(x[:, f]).size <= discrete_limit for f in range(x.shape[1])],
-                    dtype=bool)
+def column_preprocess(x: np.ndarray, discrete_limit, backend: str):
+    """The per-column preprocessing of the reference's fit(): returns
+    (is_discrete, colmin, colmax) with is_discrete[f] =
+    ``np.unique(x[:, f]).size <= discrete_limit`` (MultiSURF.py:416-420,
+    ReliefF.py:366-368, SURF.py:347-350) and colmin / colmax = x.min(0) /
+    x.max(0) in x's dtype.  Computed by ``fs_column_stats`` on the device the
+    estimator scores on ('gpu': HIP kernels; 'cpu': native threads)."""
+    cap = max(0, int(np.floor(discrete_limit)))
+    where = backend
+    if where == "gpu" and cap > _lib.GPU_STATS_MAX_CAP:
+        where = "cpu"  # hash set beyond the GPU kernel's LDS table
+    mn, mx, nd = _lib.column_stats(where, x, cap)
+    return nd <= discrete_limit, mn, mx
+
+
+def discrete_mask(x: np.ndarray, discrete_limit: int, backend: str = "cpu") -> np.ndarray:
+    """``np.unique(x[:, f]).size <= discrete_limit`` per column."""
+    return column_preprocess(x, discrete_limit, backend)[0]
 
 
 def top_features(scores: np.ndarray, n_select: int) -> np.ndarray:

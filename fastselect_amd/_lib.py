@@ -35,8 +35,8 @@ _vp = ctypes.c_void_p
 
 # every symbol include/fastselect_amd.h declares (checked by tests/test_abi.py)
 EXPORTED = (
-    "fs_version", "fs_last_error", "fs_device_count", "fs_multisurf_score", "fs_relieff_score",
-    "fs_surf_score", "fs_plan_create", "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2",
+    "fs_version", "fs_last_error", "fs_device_count", "fs_column_stats", "fs_multisurf_score",
+    "fs_relieff_score", "fs_surf_score", "fs_plan_create", "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2",
     "fs_plan_info", "fs_plan_kernel_ms", "fs_plan_destroy",
 )
 
@@ -67,6 +67,7 @@ def _load() -> ctypes.CDLL:
     lib.fs_version.restype = ctypes.c_char_p
     lib.fs_last_error.restype = ctypes.c_char_p
     lib.fs_device_count.restype = _int
+    lib.fs_column_stats.argtypes = [_int, _int, _vp, _int, _i64, _i64, _i64, _vp, _vp, _i64p]
     lib.fs_multisurf_score.argtypes = [_int, _int, _f32p, _i64, _i64, _f64p, _f32p, _i64p, _i64,
                                        _int, _u8p, _int, _f32p]
     lib.fs_relieff_score.argtypes = [_int, _int, _f32p, _i64, _i64, _i32p, _f32p, _u8p, _i64,
@@ -83,7 +84,7 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_kernel_ms.argtypes = [_vp, _int]
     lib.fs_plan_kernel_ms.restype = ctypes.c_double
     lib.fs_plan_destroy.argtypes = [_vp]
-    for name in ("fs_multisurf_score", "fs_relieff_score", "fs_surf_score", "fs_plan_create",
+    for name in ("fs_column_stats", "fs_multisurf_score", "fs_relieff_score", "fs_surf_score", "fs_plan_create",
                  "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_info",
                  "fs_plan_destroy"):
         getattr(lib, name).restype = _int
@@ -132,6 +133,27 @@ def _backend_code(backend: str) -> int:
     if backend == "cpu":
         return BACKEND_CPU
     raise ValueError("backend must be 'cpu' or 'gpu' at the native boundary")
+
+
+GPU_STATS_MAX_CAP = 8191
+
+
+def column_stats(backend, x, count_cap, device=0):
+    """Column minima, maxima and distinct-value counts (capped at
+    ``count_cap + 1``) of a float32 / float64 matrix (``fs_column_stats``):
+    the ``x.min(0)``, ``x.max(0)`` and ``np.unique(x[:, f]).size`` of the
+    reference's fit() (MultiSURF.py:141-144, 409-420)."""
+    x = np.ascontiguousarray(x)
+    if x.dtype not in (np.float32, np.float64):
+        x = x.astype(np.float64)
+    n, p = x.shape
+    mn = np.empty(p, dtype=x.dtype)
+    mx = np.empty(p, dtype=x.dtype)
+    nd = np.empty(p, dtype=np.int64)
+    check(_lib.fs_column_stats(_backend_code(backend), int(device), x.ctypes.data,
+                               int(x.dtype == np.float64), n, p, int(count_cap), mn.ctypes.data,
+                               mx.ctypes.data, _p(nd, _i64p)))
+    return mn, mx, nd
 
 
 def multisurf_score(backend, x, y, recip, feat_idx, use_star, is_discrete, n_jobs=-1, device=0):

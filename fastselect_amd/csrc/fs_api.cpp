@@ -63,6 +63,25 @@ const char* fs_last_error(void) { return g_last_error.c_str(); }
 
 int fs_device_count(void) { return gpu::device_count(); }
 
+int fs_column_stats(int backend, int device, const void* x, int x_is_f64, int64_t n, int64_t p,
+                    int64_t count_cap, void* colmin_out, void* colmax_out,
+                    int64_t* ndistinct_out) {
+  int rc = check_backend(backend, device);
+  if (rc != FS_OK) return rc;
+  if (!x || !colmin_out || !colmax_out || !ndistinct_out || n < 1 || p < 1 || count_cap < 0) {
+    set_error("fs_column_stats: need x, outputs, n >= 1, p >= 1 and count_cap >= 0");
+    return FS_EINVAL;
+  }
+  const int f64 = x_is_f64 ? 1 : 0;
+  trace_mark("column_stats: enter");
+  if (backend == FS_BACKEND_GPU)
+    rc = gpu::column_stats(x, f64, n, p, count_cap, device, colmin_out, colmax_out, ndistinct_out);
+  else
+    rc = cpu::column_stats(x, f64, n, p, count_cap, -1, colmin_out, colmax_out, ndistinct_out);
+  trace_mark("column_stats");
+  return rc;
+}
+
 int fs_multisurf_score(int backend, int device, const float* x, int64_t n, int64_t p,
                        const double* y, const float* recip, const int64_t* feat_idx,
                        int64_t n_kept, int use_star, const uint8_t* is_discrete, int n_jobs,
@@ -75,7 +94,8 @@ int fs_multisurf_score(int backend, int device, const float* x, int64_t n, int64
   if (rc != FS_OK) return rc;
   Prepared P;
   trace_mark("multisurf: enter");
-  rc = prepare(P, ALGO_MULTISURF, x, 0, n, p, feat_idx, n_kept, recip, is_discrete, n_jobs);
+  rc = prepare(P, ALGO_MULTISURF, x, 0, n, p, feat_idx, n_kept, recip, is_discrete, n_jobs,
+               backend == FS_BACKEND_GPU);
   trace_mark("prepare (host)");
   if (rc) return map_prep_rc(rc);
   if (encode_labels_f64(P, y)) return FS_EINVAL;
@@ -102,7 +122,8 @@ int fs_relieff_score(int backend, int device, const float* x, int64_t n, int64_t
   if (rc != FS_OK) return rc;
   Prepared P;
   trace_mark("relieff: enter");
-  rc = prepare(P, ALGO_RELIEFF, x, 0, n, p, nullptr, p, recip, is_discrete, n_jobs);
+  rc = prepare(P, ALGO_RELIEFF, x, 0, n, p, nullptr, p, recip, is_discrete, n_jobs,
+               backend == FS_BACKEND_GPU);
   trace_mark("prepare (host)");
   if (rc) return map_prep_rc(rc);
   P.labels.assign(y_enc, y_enc + n);
@@ -133,7 +154,8 @@ int fs_surf_score(int backend, int device, const double* x, int64_t n, int64_t p
   if (rc != FS_OK) return rc;
   Prepared P;
   trace_mark("surf: enter");
-  rc = prepare(P, ALGO_SURF, x, 1, n, p, nullptr, p, recip, is_discrete, n_jobs);
+  rc = prepare(P, ALGO_SURF, x, 1, n, p, nullptr, p, recip, is_discrete, n_jobs,
+               backend == FS_BACKEND_GPU);
   trace_mark("prepare (host)");
   if (rc) return map_prep_rc(rc);
   if (encode_labels_i32(P, y)) return FS_EINVAL;
@@ -181,7 +203,8 @@ int fs_plan_create(fs_plan** plan_out, int backend, int device, const float* x, 
   pl->rank = rank;
   pl->world = world;
   pl->n_jobs = n_jobs;
-  rc = prepare(pl->P, ALGO_MULTISURF, x, 0, n, p, feat_idx, n_kept, recip, is_discrete, n_jobs);
+  rc = prepare(pl->P, ALGO_MULTISURF, x, 0, n, p, feat_idx, n_kept, recip, is_discrete, n_jobs,
+               backend == FS_BACKEND_GPU);
   if (rc || encode_labels_f64(pl->P, y)) {
     delete pl;
     return FS_EINVAL;

@@ -102,7 +102,7 @@ __global__ __launch_bounds__(256) void k_quantize(
     const T* __restrict__ x, int64_t n, int64_t n_pad, int64_t p_in, int64_t PW, int64_t pc,
     const int64_t* __restrict__ src_col, const double* __restrict__ off,
     const double* __restrict__ qs, const double* __restrict__ scl,
-    const int64_t* __restrict__ dtab_off, const double* __restrict__ dtab,
+    const int64_t* __restrict__ dtab_off, const double* __restrict__ dtab, int disc_bits,
     uint32_t* __restrict__ xqT, float* __restrict__ xs, float* __restrict__ epsT) {
   __shared__ uint32_t tile[64][65];
   __shared__ float etile[64][65];
@@ -123,6 +123,13 @@ __global__ __launch_bounds__(256) void k_quantize(
         q = (uint32_t)__dadd_rn(t, 0.5);
         e = (float)((double)q - t);  // rounding error in integer units
         v = (float)__dmul_rn(u, scl[c]);
+      } else if (disc_bits) {
+        // float32 X: the value's bits are its code (-0.0 folded into +0.0);
+        // discrete features only ever compare codes for equality
+        float xf = (float)xv;
+        if (xf == 0.0f) xf = 0.0f;
+        q = __float_as_uint(xf);
+        v = xf;
       } else {
         int64_t lo = dtab_off[c], hi = dtab_off[c + 1] - 1;
         while (lo < hi) {
@@ -1119,9 +1126,6 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   // ~64k pass-2 workgroups: enough to fill 256 CUs and bound tail imbalance.
   g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + 65535) / 65536);
   g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
-  // histogram shift so that the largest quantised value lands in bin < 4096
-  const double qmax = Q.qmax;
-  while ((qmax / std::ldexp(1.0, g->rank_shift)) >= (double)kRankBins) g->rank_shift++;
   g->list_cap = std::max<int64_t>(1 << 16, Q.n * 64);
   const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
   int rc;
@@ -1149,12 +1153,29 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       return fail(rc);
   }
   trace_mark("plan: hipMalloc");
+  if ((rc = h2d(g, (char*)g->x, (const char*)x, xbytes))) return fail(rc);
+  if (!Q.ranges_ready) {
+    // continuous column ranges measured on the device
+    const size_t esz = x_is_f64 ? 8 : 4;
+    std::vector<char> mn((size_t)Q.p_in * esz), mx((size_t)Q.p_in * esz);
+    if ((rc = column_minmax(g->x, x_is_f64, Q.n, Q.p_in, mn.data(), mx.data(), g->stream)))
+      return fail(rc);
+    std::vector<double> cmin((size_t)Q.pc), cmax((size_t)Q.pc);
+    for (int64_t c = 0; c < Q.pc; c++) {
+      const int64_t col = Q.src_col[c];
+      cmin[c] = x_is_f64 ? ((const double*)mn.data())[col] : (double)((const float*)mn.data())[col];
+      cmax[c] = x_is_f64 ? ((const double*)mx.data())[col] : (double)((const float*)mx.data())[col];
+    }
+    if (finalize_scale(g->P, cmin.data(), cmax.data())) return fail(FS_EINVAL);
+    trace_mark("plan: device ranges");
+  }
+  // histogram shift so that the largest quantised value lands in bin < 4096
+  while ((Q.qmax / std::ldexp(1.0, g->rank_shift)) >= (double)kRankBins) g->rank_shift++;
   std::vector<double> qs(Q.PW, 0.0);
   for (int64_t c = 0; c < Q.PW; c++) qs[c] = Q.scale[c] * Q.SC;
   std::vector<int32_t> lab(Q.n_pad, -1);
   std::copy(Q.labels.begin(), Q.labels.end(), lab.begin());
-  if ((rc = h2d(g, (char*)g->x, (const char*)x, xbytes)) ||
-      (rc = h2d(g, g->src_col, Q.src_col.data(), Q.PW)) ||
+  if ((rc = h2d(g, g->src_col, Q.src_col.data(), Q.PW)) ||
       (rc = h2d(g, g->out_pos, Q.out_pos.data(), Q.PW)) ||
       (rc = h2d(g, g->off, Q.offset.data(), Q.PW)) || (rc = h2d(g, g->qs, qs.data(), Q.PW)) ||
       (rc = h2d(g, g->scl, Q.scale.data(), Q.PW)) ||
@@ -1191,11 +1212,11 @@ static int run_quantize_dist(Plan* g) {
   if (g->x_is_f64)
     k_quantize<double><<<gq, 256, 0, g->stream>>>(
         (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, g->src_col, g->off, g->qs, g->scl,
-        g->dtab_off, g->dtab, g->xqT, g->xs, g->epsT);
+        g->dtab_off, g->dtab, Q.disc_bits, g->xqT, g->xs, g->epsT);
   else
     k_quantize<float><<<gq, 256, 0, g->stream>>>(
         (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, g->src_col, g->off, g->qs, g->scl,
-        g->dtab_off, g->dtab, g->xqT, g->xs, g->epsT);
+        g->dtab_off, g->dtab, Q.disc_bits, g->xqT, g->xs, g->epsT);
   FS_TRY(launch_check("k_quantize"));
   if (Q.algo == ALGO_MULTISURF) {
     if (Q.pc > 0) {

@@ -74,13 +74,24 @@ struct Prepared {
   // pair in the band are recomputed with reference-exact arithmetic.
   double amb_delta = 0.0;
   double qmax = 0.0;               // largest quantised continuous value
+  // 0 while the continuous column ranges are still to be measured (the GPU
+  // backend measures them on the device, then calls finalize_scale)
+  int ranges_ready = 1;
+  // discrete columns of a float32 X are coded by their value bits (equality
+  // is all the kernels use), so no value tables are built on the host
+  int disc_bits = 0;
 };
 
 // Build the permutation, label codes, discrete tables and integer scale.
 // x is row-major [n][p_in], float32 (x_is_f64 == 0) or float64.
+// With device_ranges != 0 the continuous column minima/maxima (and, for a
+// float32 X, the discrete value tables) are left to the GPU backend.
 int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64_t p_in,
             const int64_t* feat_idx, int64_t n_kept, const float* recip,
-            const uint8_t* is_discrete, int n_jobs);
+            const uint8_t* is_discrete, int n_jobs, int device_ranges = 0);
+// Offsets, integer scale and error band from the per-permuted-column minima
+// and maxima of the continuous columns (c in [0, pc)).
+int finalize_scale(Prepared& P, const double* cmin, const double* cmax);
 int encode_labels_f64(Prepared& P, const double* y);
 int encode_labels_i32(Prepared& P, const int32_t* y);
 
@@ -136,11 +147,19 @@ int multisurf_pass2(const Prepared& P, const CpuState& S, const double* counts, 
                     int world, int n_jobs, double* scores);
 int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores);
 int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores);
+int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap, int n_jobs,
+                 void* colmin, void* colmax, int64_t* ndistinct);
 }  // namespace cpu
 
 // ---- GPU backend ---------------------------------------------------------
 namespace gpu {
 int device_count();
+int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap, int device,
+                 void* colmin, void* colmax, int64_t* ndistinct);
+// Column minima / maxima of a device-resident X, copied to host arrays in
+// x's dtype; runs on `stream` (a hipStream_t) and synchronises it.
+int column_minmax(const void* dx, int x_is_f64, int64_t n, int64_t p, void* hmin, void* hmax,
+                  void* stream);
 struct Plan;
 int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int device,
                 int rank, int world, uint64_t stream);

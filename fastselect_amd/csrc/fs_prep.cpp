@@ -7,8 +7,11 @@
 // is_discrete exactly as the reference does.
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <thread>
+#include <unordered_set>
 
+#include "../../include/fastselect_amd.h"
 #include "fs_internal.h"
 
 namespace fs {
@@ -39,7 +42,7 @@ void owned_tiles(int64_t nb, int rank, int world, std::vector<int32_t>& bi,
 
 int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64_t p_in,
             const int64_t* feat_idx, int64_t n_kept, const float* recip,
-            const uint8_t* is_discrete, int n_jobs) {
+            const uint8_t* is_discrete, int n_jobs, int device_ranges) {
   if (!x || !recip || !is_discrete || n < 2 || p_in < 1) {
     set_error("invalid problem: need x, recip, is_discrete, n >= 2 and p >= 1");
     return -1;
@@ -83,52 +86,66 @@ int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64
     P.src_col[P.PC + c] = feat_idx ? feat_idx[disc[c]] : disc[c];
   }
 
-  // Column minima / maxima of continuous columns (threads over columns).
-  std::vector<double> cmax(P.PW, 0.0);
-  const int nt = std::max(1, std::min<int>(hardware_threads(n_jobs), (int)std::max<int64_t>(1, P.pc)));
-  {
+  for (int64_t c = 0; c < P.pc; c++) P.scale[c] = (double)recip[P.src_col[c]];
+  P.disc_bits = (device_ranges && !x_is_f64) ? 1 : 0;
+  const int nthreads = hardware_threads(n_jobs);
+
+  // Discrete value tables (sorted distinct values, float equality
+  // semantics), one column per task.
+  if (!P.disc_bits && P.pd > 0) {
+    std::vector<std::vector<double>> tabs((size_t)P.pd);
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, P.pd));
     std::vector<std::thread> th;
     for (int t = 0; t < nt; t++)
       th.emplace_back([&, t]() {
-        for (int64_t c = t; c < P.pc; c += nt) {
-          const int64_t col = P.src_col[c];
-          double lo = load_x(x, x_is_f64, col), hi = lo;
-          for (int64_t i = 1; i < n; i++) {
-            const double v = load_x(x, x_is_f64, i * p_in + col);
-            lo = v < lo ? v : lo;
-            hi = v > hi ? v : hi;
-          }
-          P.offset[c] = lo;
-          cmax[c] = hi;
-          P.scale[c] = (double)recip[col];
+        std::vector<double> v((size_t)n);
+        for (int64_t k = t; k < P.pd; k += nt) {
+          const int64_t col = P.src_col[P.PC + k];
+          for (int64_t i = 0; i < n; i++) v[i] = load_x(x, x_is_f64, i * p_in + col);
+          std::sort(v.begin(), v.end());
+          std::vector<double>& u = tabs[k];
+          for (double a : v)
+            if (u.empty() || a != u.back()) u.push_back(a);
         }
       });
     for (auto& t : th) t.join();
+    for (int64_t k = 0; k < P.pd; k++) {
+      P.dtab_off[P.PC + k] = (int64_t)P.dtab.size();
+      P.dtab.insert(P.dtab.end(), tabs[k].begin(), tabs[k].end());
+    }
   }
+  // Slices are contiguous in column order: slice c ends where c+1 starts.
+  for (int64_t c = P.PC + P.pd; c <= P.PW; c++) P.dtab_off[c] = (int64_t)P.dtab.size();
+
+  if (device_ranges) {
+    P.ranges_ready = 0;
+    return 0;
+  }
+  // Column minima / maxima on the host: all columns, streamed by row blocks.
+  const size_t esz = x_is_f64 ? 8 : 4;
+  std::vector<char> mn((size_t)p_in * esz), mx((size_t)p_in * esz);
+  std::vector<int64_t> nd((size_t)p_in);
+  cpu::column_stats(x, x_is_f64, n, p_in, 0, n_jobs, mn.data(), mx.data(), nd.data());
+  std::vector<double> cmin((size_t)P.pc), cmax((size_t)P.pc);
+  for (int64_t c = 0; c < P.pc; c++) {
+    const int64_t col = P.src_col[c];
+    cmin[c] = x_is_f64 ? ((const double*)mn.data())[col] : (double)((const float*)mn.data())[col];
+    cmax[c] = x_is_f64 ? ((const double*)mx.data())[col] : (double)((const float*)mx.data())[col];
+  }
+  return finalize_scale(P, cmin.data(), cmax.data());
+}
+
+int finalize_scale(Prepared& P, const double* cmin, const double* cmax) {
   double R = 0.0;
   for (int64_t c = 0; c < P.pc; c++) {
-    const double r = (cmax[c] - P.offset[c]) * P.scale[c];
+    P.offset[c] = cmin[c];
+    const double r = (cmax[c] - cmin[c]) * P.scale[c];
     if (!(r >= 0.0) || std::isinf(r)) {
       set_error("non-finite or negative scaled feature range (check recip)");
       return -1;
     }
     R = r > R ? r : R;
   }
-  // Discrete value tables (sorted distinct values, float equality semantics).
-  for (int64_t c = P.PC; c < P.PC + P.pd; c++) {
-    const int64_t col = P.src_col[c];
-    std::vector<double> v((size_t)n);
-    for (int64_t i = 0; i < n; i++) v[i] = load_x(x, x_is_f64, i * p_in + col);
-    std::sort(v.begin(), v.end());
-    std::vector<double> u;
-    for (double a : v)
-      if (u.empty() || a != u.back()) u.push_back(a);
-    P.dtab_off[c] = (int64_t)P.dtab.size();
-    P.dtab.insert(P.dtab.end(), u.begin(), u.end());
-  }
-  // Slices are contiguous in column order: slice c ends where c+1 starts.
-  for (int64_t c = P.PC + P.pd; c <= P.PW; c++) P.dtab_off[c] = (int64_t)P.dtab.size();
-
   // Integer distance scale.  Per-feature |q_a - q_b| <= Rm*SC + 1 must keep
   // (a) a 256-feature window on top of a 24-bit remainder inside u32 and
   // (b) the whole distance below 2^40 (16-bit high part above bit 24).
@@ -151,8 +168,69 @@ int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64
   // both the distance and the threshold error with a wide margin.
   const double pcd = (double)P.pc;
   P.amb_delta = 16.0 * std::sqrt(pcd / 6.0 + 1.0) / sc + 4.0e-7 * std::sqrt(pcd);
+  P.ranges_ready = 1;
   return 0;
 }
+
+namespace cpu {
+
+// Host column statistics (the CPU backend of fs_column_stats).  Threads own
+// blocks of 64 adjacent columns and stream the rows, so every row segment is
+// read once and contiguously; a column stops collecting values once it has
+// more than `cap` distinct ones.
+template <typename T>
+static void colstats_block(const T* x, int64_t n, int64_t p, int64_t cap, int64_t c0, int64_t c1,
+                           T* mn, T* mx, int64_t* nd) {
+  const int64_t w = c1 - c0;
+  std::vector<std::vector<uint64_t>> small(w);
+  std::vector<std::unordered_set<uint64_t>> big(cap > 32 ? w : 0);
+  std::vector<int64_t> cnt(w, 0);
+  for (int64_t c = c0; c < c1; c++) mn[c] = mx[c] = x[c];
+  for (int64_t i = 0; i < n; i++) {
+    const T* row = x + i * p;
+    for (int64_t c = c0; c < c1; c++) {
+      const T v = row[c];
+      mn[c] = v < mn[c] ? v : mn[c];
+      mx[c] = v > mx[c] ? v : mx[c];
+      const int64_t k = c - c0;
+      if (cnt[k] > cap) continue;
+      double d = (double)v;
+      if (d == 0.0) d = 0.0;  // np.unique: -0.0 == +0.0
+      uint64_t key;
+      std::memcpy(&key, &d, 8);
+      if (cap > 32) {
+        if (big[k].insert(key).second) cnt[k]++;
+      } else if (std::find(small[k].begin(), small[k].end(), key) == small[k].end()) {
+        small[k].push_back(key);
+        cnt[k]++;
+      }
+    }
+  }
+  for (int64_t c = c0; c < c1; c++) nd[c] = std::min(cnt[c - c0], cap + 1);
+}
+
+int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap, int n_jobs,
+                 void* colmin, void* colmax, int64_t* ndistinct) {
+  const int64_t nblk = (p + 63) / 64;
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(hardware_threads(n_jobs), nblk));
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; t++)
+    th.emplace_back([&, t]() {
+      for (int64_t b = t; b < nblk; b += nt) {
+        const int64_t c0 = b * 64, c1 = std::min(p, c0 + 64);
+        if (x_is_f64)
+          colstats_block((const double*)x, n, p, cap, c0, c1, (double*)colmin, (double*)colmax,
+                         ndistinct);
+        else
+          colstats_block((const float*)x, n, p, cap, c0, c1, (float*)colmin, (float*)colmax,
+                         ndistinct);
+      }
+    });
+  for (auto& t : th) t.join();
+  return FS_OK;
+}
+
+}  // namespace cpu
 
 int encode_labels_f64(Prepared& P, const double* y) {
   if (!y) {

@@ -27,13 +27,15 @@ def _dist():
     return None, 0, 1
 
 
-def prepare_inputs(X, y, discrete_limit: int = 10):
-    """The host preprocessing of ``MultiSURF.fit`` (MultiSURF.py:384-420)."""
+def prepare_inputs(X, y, discrete_limit: int = 10, backend: str = "cpu"):
+    """The preprocessing of ``MultiSURF.fit`` (MultiSURF.py:384-420), with the
+    column statistics computed on ``backend``."""
     x = np.ascontiguousarray(X, dtype=np.float32)
-    ranges = (x.max(axis=0) - x.min(axis=0)).astype(np.float32)
+    isd, mn, mx = _base.column_preprocess(x, discrete_limit, backend)
+    ranges = (mx - mn).astype(np.float32)
     ranges[ranges == 0] = 1
     recip = (1.0 / ranges).astype(np.float32)
-    return x, np.asarray(y), recip, _base.discrete_mask(x, discrete_limit)
+    return x, np.asarray(y), recip, isd
 
 
 class ShardedMultiSURF:
@@ -90,7 +92,7 @@ class ShardedMultiSURF:
 def multisurf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", device=0):
     """Score X on this rank's share of the tiles and return the full float32
     score vector (identical on every rank)."""
-    x, yv, recip, isd = prepare_inputs(X, y, discrete_limit)
+    x, yv, recip, isd = prepare_inputs(X, y, discrete_limit, backend)
     job = ShardedMultiSURF(x, yv, recip, isd, use_star=use_star, backend=backend, device=device)
     try:
         s = job.step()

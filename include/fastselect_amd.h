@@ -115,6 +115,24 @@ FS_API int fs_surf_score(int backend, int device, const double* x, int64_t n, in
                   const int32_t* y, const float* recip, int use_star,
                   const uint8_t* is_discrete, int n_jobs, float* scores_out);
 
+/*
+ * Per-column statistics of X: the preprocessing each reference fit() runs on
+ * the host before scoring -- x.min(axis=0), x.max(axis=0) and, per column,
+ * np.unique(x[:, f]).size compared with discrete_limit (MultiSURF.py:141-144,
+ * 409-420; ReliefF.py:366-380; SURF.py:347-355).
+ *   x            [n][p] row-major, float32 (x_is_f64 = 0) or float64 (1)
+ *   count_cap    distinct values are counted exactly up to count_cap (pass
+ *                discrete_limit); a column with more reports count_cap + 1.
+ *                The GPU backend supports count_cap <= 8191 (FS_ENOTSUP above)
+ *   colmin_out, colmax_out  [p] in x's dtype
+ *   ndistinct_out           [p] min(distinct values, count_cap + 1)
+ * Equality is numpy's: -0.0 and +0.0 are one value; X must be finite (the
+ * estimators validate it first, as the reference does).
+ */
+FS_API int fs_column_stats(int backend, int device, const void* x, int x_is_f64, int64_t n,
+                           int64_t p, int64_t count_cap, void* colmin_out, void* colmax_out,
+                           int64_t* ndistinct_out);
+
 /* ---- Sharded MultiSURF plan (one plan per rank) ------------------------ */
 
 typedef struct fs_plan fs_plan;

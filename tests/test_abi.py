@@ -86,3 +86,42 @@ def test_plan_lifecycle_cpu():
     pl.close()
     one = _lib.multisurf_score("cpu", x, y, recip, None, False, isd)
     np.testing.assert_allclose((sc / 150).astype(np.float32), one, rtol=0, atol=1e-7)
+
+
+def _np_stats(x, cap):
+    nd = np.array([min(np.unique(x[:, f]).size, cap + 1) for f in range(x.shape[1])])
+    return x.min(axis=0), x.max(axis=0), nd
+
+
+def column_stats_cases():
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((300, 70))
+    x[:, 0] = rng.integers(0, 3, 300)               # 3 levels
+    x[:, 1] = 7.5                                   # constant
+    x[:, 2] = rng.choice([-0.0, 0.0, 1.0], 300)     # signed zeros are one value
+    x[:, 3] = rng.integers(0, 11, 300)              # exactly 11 levels
+    x[:, 4] = rng.integers(0, 40, 300)              # many levels (> 32: hash path)
+    x[:5, 5] = 1e30                                 # huge values
+    return x
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("cap", [0, 2, 10, 11, 50])
+def test_column_stats_cpu_matches_numpy(dtype, cap):
+    from fastselect_amd import _lib
+    x = column_stats_cases().astype(dtype)
+    mn, mx, nd = _lib.column_stats("cpu", x, cap)
+    emn, emx, end = _np_stats(x, cap)
+    assert mn.dtype == dtype and mx.dtype == dtype
+    np.testing.assert_array_equal(mn, emn)
+    np.testing.assert_array_equal(mx, emx)
+    np.testing.assert_array_equal(nd, end)
+
+
+def test_column_preprocess_is_reference_discrete_mask():
+    from fastselect_amd import _base
+    x = column_stats_cases()
+    for limit in (-1, 0, 3, 10, 11, 12.5, 40):
+        isd, _, _ = _base.column_preprocess(x, limit, "cpu")
+        ref = np.array([np.unique(x[:, f]).size <= limit for f in range(x.shape[1])])
+        np.testing.assert_array_equal(isd, ref)

@@ -191,6 +191,28 @@ def test_mixed_feature_blocks(oracle, n, pc, pd):
                   TOL, k=10)
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_column_stats_gpu_matches_numpy(dtype):
+    """GPU column statistics (fs_column_stats) == numpy min / max / np.unique
+    counts, for caps on both sides of every column's level count, shapes
+    that are not multiples of the kernels' blocks, and the LDS hash set at
+    its largest supported cap."""
+    from test_abi import _np_stats, column_stats_cases
+
+    from fastselect_amd import _lib
+    x = column_stats_cases().astype(dtype)
+    big = np.random.default_rng(1).integers(0, 5000, size=(9000, 3)).astype(dtype)
+    for data in (x, big, x[:1], x[:, :1]):
+        for cap in (0, 2, 10, 11, 50, 8191):
+            mn, mx, nd = _lib.column_stats("gpu", data, cap)
+            emn, emx, end = _np_stats(data, cap)
+            np.testing.assert_array_equal(mn, emn)
+            np.testing.assert_array_equal(mx, emx)
+            np.testing.assert_array_equal(nd, end)
+    with pytest.raises(RuntimeError):
+        _lib.column_stats("gpu", x, 8192)
+
+
 def test_feat_idx_subset(oracle):
     from fastselect_amd import _lib
     X, y = make_classification(n_samples=260, n_features=90, random_state=3)

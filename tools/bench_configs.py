@@ -3,10 +3,10 @@
     python tools/bench_configs.py [--only cfg2,cfg3,...] [--repeat 2]
 
 Per config: the one-shot C-ABI call (device alloc + H2D + all kernels + D2H,
-the same call an estimator's fit makes) and, for the MultiSURF configs, the
-kernel-only step of a resident plan.  Prints one JSON line per config.
+the same call an estimator's fit makes), the estimator's whole fit() and,
+for the MultiSURF configs, the kernel-only step of a resident plan.  Prints one JSON line per config.
 Data: make_classification(n_informative=20, n_redundant=R, random_state=42)
-as in SURVEY.md §8d; the estimator-level discrete detection is not timed.
+as in SURVEY.md §8d.
 """
 import argparse
 import json
@@ -66,6 +66,16 @@ def main():
             times.append(time.perf_counter() - t0)
         out = {"config": name, **c, "oneshot_s": min(times), "feature_scores_per_s": n * p / min(times),
                "data_s": t_data}
+        # estimator fit(): validation, column statistics, scoring, ranking
+        import fastselect_amd as F
+        est = {"multisurf": lambda: F.MultiSURF(backend="gpu", use_star=star, n_features_to_select=10),
+               "surf": lambda: F.SURF(backend="gpu", use_star=star, n_features_to_select=10),
+               "relieff": lambda: F.ReliefF(backend="gpu", n_neighbors=c.get("k", 10),
+                                            n_features_to_select=10)}[c["algo"]]
+        Xin = x32 if c["algo"] == "multisurf" else X
+        t0 = time.perf_counter()
+        est().fit(Xin, y)
+        out["fit_s"] = time.perf_counter() - t0
         if c["algo"] == "multisurf":
             import torch
 
