@@ -7,6 +7,7 @@ import numpy as np
 import pytest
 from numpy.testing import assert_allclose, assert_array_equal
 from sklearn.base import BaseEstimator, TransformerMixin
+from sklearn.datasets import make_classification
 from sklearn.exceptions import NotFittedError
 from sklearn.utils.estimator_checks import check_estimator
 
@@ -301,3 +302,26 @@ def test_turf_over_multisurf():
     t = TuRF(estimator=MultiSURF(backend="cpu"), n_features_to_select=4, pct_remove=0.3).fit(X, y)
     assert len(t.top_features_) == 4
     assert len(set(t.top_features_.tolist()) & {0, 1, 2, 3}) >= 3
+
+
+# ---- SURFstar / MultiSURFstar (scikit-rebate names) ----
+
+@pytest.mark.parametrize("names", [("SURFstar", "SURF"), ("MultiSURFstar", "MultiSURF")])
+def test_star_aliases_equal_use_star(names):
+    import fastselect_amd as F
+    from sklearn.base import clone
+    X, y = make_classification(n_samples=120, n_features=25, random_state=2)
+    star_cls, base_cls = (getattr(F, n) for n in names)
+    a = star_cls(backend="cpu", n_features_to_select=5).fit(X, y)
+    b = base_cls(backend="cpu", use_star=True, n_features_to_select=5).fit(X, y)
+    np.testing.assert_array_equal(a.feature_importances_, b.feature_importances_)
+    np.testing.assert_array_equal(a.top_features_, b.top_features_)
+    assert "use_star" not in a.get_params()
+    assert clone(a).use_star is True
+
+
+@pytest.mark.parametrize("name", ["SURFstar", "MultiSURFstar"])
+def test_star_aliases_sklearn_api(name):
+    import fastselect_amd as F
+    from sklearn.utils.estimator_checks import check_estimator
+    check_estimator(getattr(F, name)(backend="cpu"))
