@@ -331,6 +331,101 @@ int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
   return FS_OK;
 }
 
+// The reference's float32 distance key of (i, j) (ReliefF.py:145-155):
+// float32 diffs accumulated in float64 in feature order, stored as float32.
+static float relieff_exact_key(const Prepared& P, const float* x, int64_t i, int64_t j) {
+  const float* xi = x + i * P.p_in;
+  const float* xj = x + j * P.p_in;
+  double d = 0.0;
+  for (int64_t f = 0; f < P.p_in; f++) {
+    if (P.disc_in[f]) d += xi[f] != xj[f] ? 1.0 : 0.0;
+    else d += (double)(std::fabs(xi[f] - xj[f]) * P.recip_in[f]);
+  }
+  return (float)d;
+}
+
+// ReliefF neighbour selection for focal row i (ReliefF.py:157-175), same
+// pipeline as the GPU: quantised keys, exact keys for every candidate near
+// a class's k-th distance, then -- only when several candidates share the
+// k-th distance exactly -- numba's quicksort order over the exact row.
+// nbr[c] receives the chosen neighbours of class c.
+static void relieff_select_row(const Prepared& P, const float* x, const std::vector<double>& D,
+                               int64_t i, std::vector<std::vector<int32_t>>& nbr) {
+  const int64_t n = P.n, k = P.k_neighbors;
+  const int C = P.n_classes;
+  const double inv_sc = 1.0 / P.SC;
+  std::vector<float> key((size_t)n);
+  for (int64_t j = 0; j < n; j++) key[j] = (float)(D[(size_t)i * n + j] * inv_sc);
+  key[i] = INFINITY;
+  const int32_t li = P.labels[i];
+  std::vector<std::vector<int32_t>> members(C);
+  for (int64_t j = 0; j < n; j++)
+    if (j != i) members[P.labels[j]].push_back((int32_t)j);
+  std::vector<float> T(C, INFINITY);
+  std::vector<int64_t> need(C, 0), eq(C, 0);
+  std::vector<uint8_t> exact((size_t)n, 0);
+  auto kth = [&](int c, int64_t kc) {
+    std::vector<float> v;
+    v.reserve(members[c].size());
+    for (int32_t j : members[c]) v.push_back(key[j]);
+    std::nth_element(v.begin(), v.begin() + (kc - 1), v.end());
+    return v[kc - 1];
+  };
+  bool tie = false;
+  for (int c = 0; c < C; c++) {
+    const int64_t kc = std::min<int64_t>(k, (int64_t)members[c].size());
+    if (kc == 0 || kc == (int64_t)members[c].size()) continue;  // take all
+    // exact keys for every candidate within the quantisation band of T
+    const float t0 = kth(c, kc);
+    const double band = 2.0 * (P.amb_delta + (double)t0 * 1.2e-7);
+    for (int32_t j : members[c])
+      if (std::fabs((double)key[j] - (double)t0) <= band) {
+        key[j] = relieff_exact_key(P, x, i, j);
+        exact[j] = 1;
+      }
+    T[c] = kth(c, kc);
+    int64_t lt = 0;
+    for (int32_t j : members[c]) {
+      lt += key[j] < T[c];
+      eq[c] += key[j] == T[c];
+    }
+    need[c] = kc - lt;
+    tie = tie || eq[c] > need[c];
+  }
+  std::vector<std::vector<int32_t>> tied(C);
+  if (tie) {
+    // numba's order decides: replay its quicksort over the exact row
+    if (P.pc > 0)
+      for (int64_t j = 0; j < n; j++)
+        if (j != i && !exact[j]) key[j] = relieff_exact_key(P, x, i, j);
+    std::vector<int32_t> R((size_t)n);
+    auto is_tied = [&](int32_t j) {
+      const int c = P.labels[j];
+      return j != i && eq[c] > need[c] && key[j] == T[c];
+    };
+    numba_argsort_focus(n, R.data(), [&](int32_t j) { return key[j]; }, is_tied);
+    for (int64_t t = 0; t < n; t++)
+      if (is_tied(R[t])) tied[P.labels[R[t]]].push_back(R[t]);
+  }
+  for (int c = 0; c < C; c++) {
+    nbr[c].clear();
+    const int64_t kc = std::min<int64_t>(k, (int64_t)members[c].size());
+    if (kc == (int64_t)members[c].size()) {
+      nbr[c] = members[c];
+      continue;
+    }
+    for (int32_t j : members[c])
+      if (key[j] < T[c]) nbr[c].push_back(j);
+    if (eq[c] > need[c]) {
+      for (int64_t t = 0; t < need[c]; t++) nbr[c].push_back(tied[c][t]);
+    } else {
+      for (int32_t j : members[c])
+        if (key[j] == T[c]) nbr[c].push_back(j);
+    }
+  }
+  (void)li;
+}
+
 int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
   std::vector<uint32_t> xq;
   std::vector<float> xs;
@@ -339,28 +434,20 @@ int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
   distances(P, xq, 0, 1, n_jobs, D);
   const int64_t n = P.n, k = P.k_neighbors;
   const int C = P.n_classes;
-  const double inv_sc = 1.0 / P.SC;
   // per-row partial sums, folded in row order for determinism
   std::vector<double> part((size_t)n * P.PW, 0.0);
   parallel_for(n, n_jobs, [&](int64_t i) {
-    std::vector<std::vector<std::pair<uint32_t, int32_t>>> cand(C);
-    for (int64_t j = 0; j < n; j++) {
-      if (j == i) continue;
-      const float df = (float)(D[(size_t)i * n + j] * inv_sc);
-      uint32_t key;
-      std::memcpy(&key, &df, 4);
-      cand[P.labels[j]].push_back({key, (int32_t)j});
-    }
+    std::vector<std::vector<int32_t>> nbr(C);
+    relieff_select_row(P, (const float*)x, D, i, nbr);
     const int32_t li = P.labels[i];
     double denom = 1.0 - P.class_prior[li];
     if (denom == 0.0) denom = 1.0;
     double* out = part.data() + (size_t)i * P.PW;
     const float* a = xs.data() + (size_t)i * P.PW;
     for (int c = 0; c < C; c++) {
-      auto& v = cand[c];
-      const int64_t kc = std::min<int64_t>(k, (int64_t)v.size());
+      const std::vector<int32_t>& v = nbr[c];
+      const int64_t kc = (int64_t)v.size();
       if (kc == 0) continue;
-      std::partial_sort(v.begin(), v.begin() + kc, v.end());
       // self is a zero-diff hit when its class has < k other members
       // (ReliefF.py:144-168: dists[i] = inf sorts last but is still scanned)
       const int64_t h_found = kc < k ? kc + 1 : k;
@@ -369,7 +456,7 @@ int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
       for (int64_t col = 0; col < P.PW; col++) {
         double s = 0.0;
         for (int64_t t = 0; t < kc; t++) {
-          const float* b = xs.data() + (size_t)v[t].second * P.PW;
+          const float* b = xs.data() + (size_t)v[t] * P.PW;
           s += col < P.PC ? (double)std::fabs(a[col] - b[col]) : (a[col] != b[col] ? 1.0 : 0.0);
         }
         out[col] += wgt * s;

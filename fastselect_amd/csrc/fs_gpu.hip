@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
     const T* __restrict__ x, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
     const int64_t* __restrict__ src_col, const double* __restrict__ scl, double sc,
     const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
-    int64_t n_pad, double* __restrict__ D) {
+    int64_t n_pad, int mark_f32, double* __restrict__ D) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
@@ -634,7 +635,10 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
     }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (lane == 0) {
-      const double v = acc * sc;
+      // MultiSURF: exact distance in integer units.  ReliefF (mark_f32): the
+      // reference's float32 key, stored negated so k_rf_select knows it is
+      // exact (a zero key stays +0 and reads back the same either way).
+      const double v = mark_f32 ? -(double)(float)acc : acc * sc;
       D[(int64_t)pr.x * n_pad + pr.y] = v;
       D[(int64_t)pr.y * n_pad + pr.x] = v;
     }
@@ -853,17 +857,29 @@ __global__ void k_reduce(const double* __restrict__ part, int64_t nseg, int64_t 
 // ReliefF: per-row k-nearest selection per class (radix select on the
 // float32 distance bits, index order among equal keys) and neighbour update
 // ---------------------------------------------------------------------------
-// One workgroup per focal row.  Key of j = bits of (float)(D_ij / SC) (the
-// reference's float32 distance row, ReliefF.py:149-155).  For each class c
-// the k_c-th smallest key T_c is found digit by digit (4 x 8-bit LDS
-// histograms); then wave (c % 4) scans j in ascending order and takes every
-// key < T_c plus the first `need_c` keys == T_c, writing neighbour indices in
-// ascending j (deterministic).
+// The key of j is the reference's float32 distance row (ReliefF.py:149-155):
+// float32(D_ij / SC) from the quantised distance, or the exact reference key
+// where k_exact_pairs stored one (negative D, see k_exact_pairs).
+__device__ __forceinline__ uint32_t rf_key(double d, double inv_sc) {
+  return __float_as_uint(d < 0.0 ? (float)(-d) : (float)(d * inv_sc));
+}
+
+// One workgroup per focal row.  For each class c the k_c-th smallest key T_c
+// is found digit by digit (4 x 8-bit LDS histograms) -> tkey[i][c], and
+// tneed[i][c] = how many keys equal to T_c belong to the k_c nearest (0 when
+// the class is taken whole).  With `collect`, wave (c % 4) then scans j in
+// ascending order and takes every key < T_c plus the first tneed keys ==
+// T_c (index order; rows where more keys equal T_c than are needed are
+// re-ordered the reference's way by k_rf_ties), and teq[i][c] counts the
+// keys equal to T_c.
 __global__ __launch_bounds__(256) void k_rf_select(const double* __restrict__ D, int64_t n,
                                                    int64_t n_pad, double inv_sc,
                                                    const int32_t* __restrict__ lab,
                                                    const int64_t* __restrict__ class_count,
-                                                   int n_classes, int64_t k,
+                                                   int n_classes, int64_t k, int collect,
+                                                   uint32_t* __restrict__ tkey,
+                                                   int32_t* __restrict__ tneed,
+                                                   int32_t* __restrict__ teq,
                                                    int32_t* __restrict__ nbr,
                                                    int32_t* __restrict__ nfound) {
   extern __shared__ uint32_t sh[];  // hist[n_classes][256], prefix[C], need[C]
@@ -892,7 +908,7 @@ __global__ __launch_bounds__(256) void k_rf_select(const double* __restrict__ D,
       if (j == i) continue;
       const int32_t c = lab[j];
       if (need[c] == 0) continue;
-      const uint32_t key = __float_as_uint((float)(row[j] * inv_sc));
+      const uint32_t key = rf_key(row[j], inv_sc);
       if (sh_hi < 32 && (key >> sh_hi) != (prefix[c] >> sh_hi)) continue;
       atomicAdd(&hist[c * 256 + ((key >> (8 * d)) & 0xFF)], 1u);
     }
@@ -910,18 +926,23 @@ __global__ __launch_bounds__(256) void k_rf_select(const double* __restrict__ D,
     }
     __syncthreads();
   }
+  for (int c = tid; c < n_classes; c += 256) {
+    tkey[i * n_classes + c] = prefix[c];
+    tneed[i * n_classes + c] = (int32_t)need[c];
+  }
+  if (!collect) return;
   // Ordered collection, one wave per class.
   const int wave = tid >> 6, lane = tid & 63;
   for (int c = wave; c < n_classes; c += 4) {
     const uint32_t T = prefix[c];
     uint32_t eq_left = need[c];
-    int64_t cnt = 0;
+    int64_t cnt = 0, n_eq = 0;
     int32_t* out = nbr + (i * n_classes + c) * k;
     for (int64_t j0 = 0; j0 < n; j0 += 64) {
       const int64_t j = j0 + lane;
       bool lt = false, eq = false;
       if (j < n && j != i && lab[j] == c) {
-        const uint32_t key = __float_as_uint((float)(row[j] * inv_sc));
+        const uint32_t key = rf_key(row[j], inv_sc);
         lt = key < T;
         eq = key == T;
       }
@@ -935,9 +956,122 @@ __global__ __launch_bounds__(256) void k_rf_select(const double* __restrict__ D,
       if (take) out[cnt + __popcll(mt & below)] = (int32_t)j;
       cnt += __popcll(mt);
       const uint32_t eq_taken = (uint32_t)__popcll(meq);
+      n_eq += eq_taken;
       eq_left = eq_taken >= eq_left ? 0u : eq_left - eq_taken;
     }
-    if (lane == 0) nfound[i * n_classes + c] = (int32_t)cnt;
+    if (lane == 0) {
+      nfound[i * n_classes + c] = (int32_t)cnt;
+      teq[i * n_classes + c] = (int32_t)n_eq;
+    }
+  }
+}
+
+// Candidates whose quantised key lies within `band` of their class's k-th
+// key T (tkey from a first k_rf_select) go to the exact-pair list: after
+// k_exact_pairs stores their reference keys, a second selection is exact.
+__global__ __launch_bounds__(256) void k_rf_flag(const double* __restrict__ D, int64_t n,
+                                                 int64_t n_pad, double inv_sc,
+                                                 const int32_t* __restrict__ lab,
+                                                 int n_classes,
+                                                 const uint32_t* __restrict__ tkey,
+                                                 const int32_t* __restrict__ tneed,
+                                                 double band_abs, double band_rel,
+                                                 int2* __restrict__ list, int64_t cap,
+                                                 unsigned long long* __restrict__ count) {
+  const int64_t i = blockIdx.x;
+  const double* row = D + i * n_pad;
+  for (int64_t j = threadIdx.x; j < n; j += 256) {
+    if (j == i) continue;
+    const int32_t c = lab[j];
+    if (tneed[i * n_classes + c] == 0) continue;  // class taken whole
+    const double T = (double)__uint_as_float(tkey[i * n_classes + c]);
+    const double kv = (double)__uint_as_float(rf_key(row[j], inv_sc));
+    if (fabs(kv - T) <= band_abs + band_rel * T) {
+      const unsigned long long slot = atomicAdd(count, 1ull);
+      if ((int64_t)slot < cap) list[slot] = make_int2((int)i, (int)j);
+    }
+  }
+}
+
+// Exact reference keys of whole rows (tie rows of a problem with continuous
+// features): grid (tie rows, ceil(n / 4)), one wave per (row, j).  With no
+// continuous features the quantised keys are already exact and are copied.
+template <typename T>
+__global__ __launch_bounds__(256) void k_rf_exact_rows(
+    const T* __restrict__ x, int64_t n, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
+    const int64_t* __restrict__ src_col, const double* __restrict__ scl,
+    const int32_t* __restrict__ rows, const double* __restrict__ D, int64_t n_pad, double inv_sc,
+    float* __restrict__ keys) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = blockIdx.x;
+  const int64_t i = rows[r];
+  const int64_t j = (int64_t)blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (j >= n) return;
+  float kv;
+  if (pc == 0) {
+    kv = __uint_as_float(rf_key(D[i * n_pad + j], inv_sc));
+  } else {
+    const T* xi = x + i * p_in;
+    const T* xj = x + j * p_in;
+    double acc = 0.0;
+    for (int64_t c = lane; c < pc; c += 64) {
+      const int64_t col = src_col[c];
+      acc += (double)(__builtin_fabsf((float)xi[col] - (float)xj[col]) * (float)scl[c]);
+    }
+    for (int64_t c = PC + lane; c < PC + pd; c += 64) {
+      const int64_t col = src_col[c];
+      acc += (xi[col] != xj[col]) ? 1.0 : 0.0;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    kv = (float)acc;
+  }
+  if (lane == 0) keys[r * n + j] = (j == i) ? __builtin_inff() : kv;
+}
+
+// Rows where more neighbours share a class's k-th distance than are needed:
+// replay numba's quicksort over the row's exact keys (numba_argsort_focus)
+// and take the tied neighbours in its order (ReliefF.py:157-175).  One
+// thread per row; R is per-row scratch.
+__global__ __launch_bounds__(64) void k_rf_ties(const int32_t* __restrict__ rows, int64_t n_rows,
+                                                int64_t n, const float* __restrict__ keys,
+                                                const int32_t* __restrict__ lab, int n_classes,
+                                                int64_t k, const uint32_t* __restrict__ tkey,
+                                                const int32_t* __restrict__ tneed,
+                                                const int32_t* __restrict__ teq,
+                                                int32_t* __restrict__ R_all,
+                                                int32_t* __restrict__ nbr,
+                                                int* __restrict__ status) {
+  const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (r >= n_rows) return;
+  const int64_t i = rows[r];
+  const float* key = keys + r * n;
+  int32_t* R = R_all + r * n;
+  const uint32_t* Ti = tkey + i * n_classes;
+  const int32_t* need = tneed + i * n_classes;
+  const int32_t* eq = teq + i * n_classes;
+  auto tied = [&](int32_t j) {
+    const int c = lab[j];
+    return j != i && eq[c] > need[c] && __float_as_uint(key[j]) == Ti[c];
+  };
+  if (numba_argsort_focus(n, R, [&](int32_t j) { return key[j]; }, tied) != 0) {
+    atomicExch(status, 1);
+    return;
+  }
+  for (int c = 0; c < n_classes; c++) {
+    if (!(eq[c] > need[c])) continue;
+    int32_t* out = nbr + (i * n_classes + c) * k;
+    const float T = __uint_as_float(Ti[c]);
+    int64_t cnt = 0;
+    for (int64_t j = 0; j < n; j++)
+      if (j != i && lab[j] == c && key[j] < T) out[cnt++] = (int32_t)j;
+    int64_t taken = 0;
+    for (int64_t t = 0; t < n && taken < need[c]; t++) {
+      const int32_t j = R[t];
+      if (lab[j] == c && tied(j)) {
+        out[cnt++] = j;
+        taken++;
+      }
+    }
   }
 }
 
@@ -1022,6 +1156,7 @@ struct Plan {
   int64_t list_cap = 0;
   unsigned long long* list_count = nullptr;
   int64_t n_refined = 0;
+  int64_t n_tie_rows = 0;      // ReliefF rows re-ordered by k_rf_ties
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<void*> owned;
 };
@@ -1266,11 +1401,11 @@ static int refine_pairs(Plan* g, int algo, double delta) {
   if (g->x_is_f64)
     k_exact_pairs<double><<<grid, 256, 0, g->stream>>>(
         (const double*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, g->D);
+        g->list_count, g->list_cap, Q.n_pad, 0, g->D);
   else
     k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
         (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, g->D);
+        g->list_count, g->list_cap, Q.n_pad, 0, g->D);
   return launch_check("k_exact_pairs");
 }
 
@@ -1402,6 +1537,100 @@ int surf_run(const Prepared& P, const void* x, int device, float* scores_out) {
   return rc;
 }
 
+// ReliefF neighbour selection on the resident distances: quantised keys,
+// exact reference keys for every candidate near a class's k-th key, exact
+// selection, then numba's quicksort order for rows with ties at the k-th key.
+static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nfound) {
+  const Prepared& Q = g->P;
+  const int C = Q.n_classes;
+  const int64_t k = Q.k_neighbors, n = Q.n;
+  const double inv_sc = 1.0 / Q.SC;
+  uint32_t* tkey = nullptr;
+  int32_t *tneed = nullptr, *teq = nullptr;
+  FS_TRY(dalloc(g, &tkey, (size_t)n * C));
+  FS_TRY(dalloc(g, &tneed, (size_t)n * C));
+  FS_TRY(dalloc(g, &teq, (size_t)n * C));
+  const size_t shbytes = (size_t)C * 256 * 4 + 2 * (size_t)C * 4;
+  // 1. k-th keys from the quantised distances
+  k_rf_select<<<(unsigned)n, 256, shbytes, g->stream>>>(g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C,
+                                                        k, 0, tkey, tneed, teq, nbr, nfound);
+  FS_TRY(launch_check("k_rf_select"));
+  // 2. exact keys inside the band (quantisation error + float32 rounding)
+  const double band_abs = 2.0 * Q.amb_delta, band_rel = 2.0 * 1.2e-7;
+  g->n_refined = 0;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
+    k_rf_flag<<<(unsigned)n, 256, 0, g->stream>>>(g->D, n, Q.n_pad, inv_sc, g->lab, C, tkey,
+                                                  tneed, band_abs, band_rel, g->list,
+                                                  g->list_cap, g->list_count);
+    FS_TRY(launch_check("k_rf_flag"));
+    unsigned long long cnt = 0;
+    FS_HIP(hipMemcpyAsync(&cnt, g->list_count, sizeof(cnt), hipMemcpyDeviceToHost, g->stream));
+    FS_HIP(hipStreamSynchronize(g->stream));
+    if ((int64_t)cnt <= g->list_cap) {
+      g->n_refined = (int64_t)cnt;
+      break;
+    }
+    g->list_cap = (int64_t)cnt + cnt / 4;
+    FS_TRY(dalloc(g, &g->list, g->list_cap));
+  }
+  if (g->n_refined > 0) {
+    const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
+    k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
+        (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
+        g->list_count, g->list_cap, Q.n_pad, 1, g->D);
+    FS_TRY(launch_check("k_exact_pairs"));
+  }
+  // 3. exact selection
+  k_rf_select<<<(unsigned)n, 256, shbytes, g->stream>>>(g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C,
+                                                        k, 1, tkey, tneed, teq, nbr, nfound);
+  FS_TRY(launch_check("k_rf_select"));
+  // 4. rows with more neighbours at the k-th key than needed
+  std::vector<int32_t> hneed((size_t)n * C), heq((size_t)n * C);
+  FS_HIP(hipMemcpyAsync(hneed.data(), tneed, hneed.size() * 4, hipMemcpyDeviceToHost, g->stream));
+  FS_HIP(hipMemcpyAsync(heq.data(), teq, heq.size() * 4, hipMemcpyDeviceToHost, g->stream));
+  FS_HIP(hipStreamSynchronize(g->stream));
+  std::vector<int32_t> tie_rows;
+  for (int64_t i = 0; i < n; i++)
+    for (int c = 0; c < C; c++)
+      if (hneed[i * C + c] > 0 && heq[i * C + c] > hneed[i * C + c]) {
+        tie_rows.push_back((int32_t)i);
+        break;
+      }
+  g->n_tie_rows = (int64_t)tie_rows.size();
+  if (tie_rows.empty()) return FS_OK;
+  // batches bounded to ~512 MB of per-row scratch (keys + permutation)
+  const int64_t batch = std::max<int64_t>(1, std::min<int64_t>((int64_t)tie_rows.size(),
+                                                               (int64_t)(512ll << 20) / (8 * n)));
+  int32_t *drows = nullptr, *R = nullptr;
+  float* keys = nullptr;
+  int* status = nullptr;
+  FS_TRY(dalloc(g, &drows, (size_t)batch));
+  FS_TRY(dalloc(g, &R, (size_t)batch * n));
+  FS_TRY(dalloc(g, &keys, (size_t)batch * n));
+  FS_TRY(dalloc(g, &status, 1));
+  FS_HIP(hipMemsetAsync(status, 0, sizeof(int), g->stream));
+  for (int64_t r0 = 0; r0 < (int64_t)tie_rows.size(); r0 += batch) {
+    const int64_t nr = std::min<int64_t>(batch, (int64_t)tie_rows.size() - r0);
+    FS_TRY(h2d(g, drows, tie_rows.data() + r0, (size_t)nr));
+    k_rf_exact_rows<float><<<dim3((unsigned)nr, (unsigned)((n + 3) / 4)), 256, 0, g->stream>>>(
+        (const float*)g->x, n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, drows, g->D,
+        Q.n_pad, inv_sc, keys);
+    FS_TRY(launch_check("k_rf_exact_rows"));
+    k_rf_ties<<<(unsigned)((nr + 63) / 64), 64, 0, g->stream>>>(drows, nr, n, keys, g->lab, C, k,
+                                                                tkey, tneed, teq, R, nbr, status);
+    FS_TRY(launch_check("k_rf_ties"));
+  }
+  int hstatus = 0;
+  FS_HIP(hipMemcpyAsync(&hstatus, status, sizeof(int), hipMemcpyDeviceToHost, g->stream));
+  FS_HIP(hipStreamSynchronize(g->stream));
+  if (hstatus != 0) {
+    set_error("ReliefF tie ordering: quicksort stack overflow");
+    return FS_EHIP;
+  }
+  return FS_OK;
+}
+
 int relieff_run(const Prepared& P, const void* x, int device, float* scores_out) {
   if (P.n_classes > 64) {
     set_error("GPU ReliefF supports at most 64 classes");
@@ -1424,19 +1653,19 @@ int relieff_run(const Prepared& P, const void* x, int device, float* scores_out)
       (rc = dalloc(g, &part, (size_t)nrb * Q.PW)) || (rc = dalloc(g, &dcc, C)) ||
       (rc = dalloc(g, &nbr, (size_t)Q.n * C * std::max<int64_t>(k, 1))) ||
       (rc = dalloc(g, &nfound, (size_t)Q.n * C)) || (rc = h2d(g, dcc, cc.data(), C)) ||
-      (rc = h2d(g, dprior, prior.data(), C)) || (rc = run_quantize_dist(g))) {
+      (rc = h2d(g, dprior, prior.data(), C)) || (rc = run_quantize_dist(g)) ||
+      (rc = relieff_select(g, dcc, nbr, nfound))) {
     plan_destroy(g);
     return rc;
   }
-  const size_t shbytes = (size_t)C * 256 * 4 + 2 * (size_t)C * 4;
-  k_rf_select<<<(unsigned)Q.n, 256, shbytes, g->stream>>>(g->D, Q.n, Q.n_pad, 1.0 / Q.SC,
-                                                          g->lab, dcc, C, k, nbr, nfound);
-  rc = launch_check("k_rf_select");
-  if (rc == FS_OK) {
-    k_rf_update<<<dim3((unsigned)(Q.PW / 64), (unsigned)nrb), 256, 0, g->stream>>>(
-        g->xs, Q.n, Q.PW, Q.PC, g->lab, dprior, C, k, nbr, nfound, part);
-    rc = launch_check("k_rf_update");
+  if (trace_on()) {
+    (void)hipStreamSynchronize(g->stream);
+    std::fprintf(stderr, "[fs_trace] relieff: %lld exact pairs, %lld tie rows\n",
+                 (long long)g->n_refined, (long long)g->n_tie_rows);
   }
+  k_rf_update<<<dim3((unsigned)(Q.PW / 64), (unsigned)nrb), 256, 0, g->stream>>>(
+      g->xs, Q.n, Q.PW, Q.PC, g->lab, dprior, C, k, nbr, nfound, part);
+  rc = launch_check("k_rf_update");
   if (rc == FS_OK) {
     k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(part, nrb, Q.PW,
                                                                      g->out_pos, sc);

@@ -59,6 +59,10 @@ struct Prepared {
   // position in the output (kept-feature order, -1 = padding)
   std::vector<int64_t> src_col, out_pos;
   std::vector<double> offset;      // continuous: column minimum (kernel dtype)
+  // per input column: recip and discreteness as given (the reference's
+  // feature order, used where its arithmetic is replayed exactly)
+  std::vector<float> recip_in;
+  std::vector<uint8_t> disc_in;
   std::vector<double> scale;       // continuous: (double)recip
   // discrete: per permuted column, [dtab_off[c], dtab_off[c+1]) slice of the
   // sorted distinct values (kernel dtype widened to double)
@@ -127,6 +131,91 @@ FS_HD inline double surf_weight(bool near, bool hit, int use_star) {
   if (near) return hit ? -1.0 : 1.0;
   if (use_star) return hit ? 1.0 : -1.0;
   return 0.0;
+}
+
+// ---- numba's quicksort argsort (ReliefF neighbour ties) ------------------
+// The reference orders each ReliefF distance row with np.argsort inside
+// @njit (ReliefF.py:157), i.e. numba's non-stable quicksort (numba 0.54.1
+// numba/misc/quicksort.py: median-of-three pivot, Hoare partition with the
+// pivot parked at `high`, larger side pushed, insertion sort below 15
+// elements; floats compared with `<`, no NaNs here).  Which of several
+// neighbours at exactly the k-th distance it takes depends on that order.
+// This is the same algorithm over R (the index permutation), except that a
+// sub-range holding no "interesting" element (interesting(j): a neighbour
+// whose key equals a tied k-th distance) is dropped instead of sorted:
+// ranges are disjoint once split, so the final relative order of the
+// interesting elements is exactly numba's, at ~2n work instead of n log n.
+// key(j) and interesting(j) take the sample index.  Returns 0, or -1 if the
+// explicit stack (numba's MAX_STACK = 100) would overflow.
+template <typename KeyFn, typename InterestFn>
+FS_HD inline int numba_argsort_focus(int64_t len, int32_t* R, KeyFn key, InterestFn interesting) {
+  for (int64_t t = 0; t < len; t++) R[t] = (int32_t)t;
+  if (len < 2) return 0;
+  constexpr int kSmall = 15, kMaxStack = 100;
+  int64_t st_lo[kMaxStack], st_hi[kMaxStack];
+  int ns = 1;
+  st_lo[0] = 0;
+  st_hi[0] = len - 1;
+  auto has_interest = [&](int64_t lo, int64_t hi) {
+    for (int64_t t = lo; t <= hi; t++)
+      if (interesting(R[t])) return true;
+    return false;
+  };
+  while (ns > 0) {
+    ns--;
+    int64_t low = st_lo[ns], high = st_hi[ns];
+    bool live = true;
+    while (high - low >= kSmall) {
+      const int64_t mid = (low + high) >> 1;
+      int32_t tmp;
+      if (key(R[mid]) < key(R[low])) { tmp = R[low]; R[low] = R[mid]; R[mid] = tmp; }
+      if (key(R[high]) < key(R[mid])) { tmp = R[high]; R[high] = R[mid]; R[mid] = tmp; }
+      if (key(R[mid]) < key(R[low])) { tmp = R[low]; R[low] = R[mid]; R[mid] = tmp; }
+      const float pivot = key(R[mid]);
+      tmp = R[high]; R[high] = R[mid]; R[mid] = tmp;
+      int64_t i = low, j = high - 1;
+      while (true) {
+        while (i < high && key(R[i]) < pivot) i++;
+        while (j >= low && pivot < key(R[j])) j--;
+        if (i >= j) break;
+        tmp = R[i]; R[i] = R[j]; R[j] = tmp;
+        i++;
+        j--;
+      }
+      tmp = R[i]; R[i] = R[high]; R[high] = tmp;
+      // numba pushes the larger side and keeps partitioning the smaller one
+      int64_t push_lo, push_hi, keep_lo, keep_hi;
+      if (high - i > i - low) {
+        push_lo = i + 1; push_hi = high; keep_lo = low; keep_hi = i - 1;
+      } else {
+        push_lo = low; push_hi = i - 1; keep_lo = i + 1; keep_hi = high;
+      }
+      if (push_hi >= push_lo && has_interest(push_lo, push_hi)) {
+        if (ns >= kMaxStack) return -1;
+        st_lo[ns] = push_lo;
+        st_hi[ns] = push_hi;
+        ns++;
+      }
+      low = keep_lo;
+      high = keep_hi;
+      if (high < low || !has_interest(low, high)) {
+        live = false;
+        break;
+      }
+    }
+    if (!live) continue;
+    for (int64_t i = low + 1; i <= high; i++) {  // insertion sort [low, high]
+      const int32_t kk = R[i];
+      const float v = key(kk);
+      int64_t j = i;
+      while (j > low && v < key(R[j - 1])) {
+        R[j] = R[j - 1];
+        j--;
+      }
+      R[j] = kk;
+    }
+  }
+  return 0;
 }
 
 // ---- CPU backend ---------------------------------------------------------

@@ -87,6 +87,8 @@ int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64
   }
 
   for (int64_t c = 0; c < P.pc; c++) P.scale[c] = (double)recip[P.src_col[c]];
+  P.recip_in.assign(recip, recip + p_in);
+  P.disc_in.assign(is_discrete, is_discrete + p_in);
   P.disc_bits = (device_ranges && !x_is_f64) ? 1 : 0;
   const int nthreads = hardware_threads(n_jobs);
 

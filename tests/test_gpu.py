@@ -120,6 +120,39 @@ def test_relieff_sizes(oracle, n, p, ncls, k, seed):
                   TOL, k=10)
 
 
+@pytest.mark.parametrize("kind", ["discrete", "mixed", "duplicates"])
+@pytest.mark.parametrize("k", [1, 3, 10])
+def test_relieff_boundary_ties_follow_numba_quicksort(oracle, kind, k):
+    """Neighbours tied at exactly the k-th distance are taken in numba's
+    quicksort order (k_rf_ties replays it on the device)."""
+    from fastselect_amd import ReliefF
+    rng = np.random.default_rng(k)
+    n = 400
+    if kind == "discrete":
+        X = rng.integers(0, 3, size=(n, 12)).astype(float)
+    elif kind == "mixed":
+        X = np.column_stack([rng.integers(0, 3, size=(n, 8)),
+                             np.round(rng.standard_normal((n, 3)), 1)])
+    else:
+        X = rng.standard_normal((n, 20))
+        X[200:260] = X[0:60]
+    y = rng.integers(0, 3, n)
+    dl = 3 if kind != "duplicates" else 10
+    s = _fit(ReliefF, X, y, n_neighbors=k, discrete_limit=dl)
+    assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=k, discrete_limit=dl), TOL)
+
+
+def test_relieff_large_n_boundary(oracle):
+    """n large enough that k-th-neighbour keys crowd within float32 ulps:
+    the exact-key band must make every selection the reference's."""
+    from fastselect_amd import ReliefF
+    X, y = make_classification(n_samples=4000, n_features=400, n_informative=20,
+                               n_redundant=50, n_classes=3, n_clusters_per_class=1,
+                               random_state=42)
+    s = _fit(ReliefF, X, y, n_neighbors=10)
+    assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=10), TOL, k=10)
+
+
 def test_gpu_matches_cpu_backend():
     """Same integer distances and weights on both product backends: scores
     differ only by floating-point accumulation order."""

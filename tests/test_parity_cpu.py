@@ -129,3 +129,24 @@ def test_gloo_world2_matches_single(tmp_path):
     X, y = make_classification(n_samples=300, n_features=50, random_state=0)
     ref = MultiSURF(backend="cpu", use_star=True).fit(X, y).feature_importances_
     assert scale_rel_err(a, ref) < 1e-6
+
+
+@pytest.mark.parametrize("kind", ["discrete", "mixed", "duplicates"])
+@pytest.mark.parametrize("k", [1, 3, 10])
+def test_relieff_boundary_ties_follow_numba_quicksort(oracle, kind, k):
+    """Neighbours tied at exactly the k-th distance: the reference takes them
+    in numba-quicksort order (ReliefF.py:157); SURVEY.md §8f row 3."""
+    rng = np.random.default_rng(k)
+    n = 400
+    if kind == "discrete":      # integer distances: ties in almost every row
+        X = rng.integers(0, 3, size=(n, 12)).astype(float)
+    elif kind == "mixed":       # a few coarse continuous columns + discrete
+        X = np.column_stack([rng.integers(0, 3, size=(n, 8)),
+                             np.round(rng.standard_normal((n, 3)), 1)])
+    else:                       # exact duplicate samples
+        X = rng.standard_normal((n, 20))
+        X[200:260] = X[0:60]
+    y = rng.integers(0, 3, n)
+    dl = 3 if kind != "duplicates" else 10
+    s = ReliefF(backend="cpu", n_neighbors=k, discrete_limit=dl).fit(X, y).feature_importances_
+    assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=k, discrete_limit=dl), TOL)
