@@ -399,11 +399,17 @@ static void relieff_select_row(const Prepared& P, const float* x, const std::vec
       for (int64_t j = 0; j < n; j++)
         if (j != i && !exact[j]) key[j] = relieff_exact_key(P, x, i, j);
     std::vector<int32_t> R((size_t)n);
+    for (int64_t j = 0; j < n; j++) R[j] = (int32_t)j;
     auto is_tied = [&](int32_t j) {
       const int c = P.labels[j];
       return j != i && eq[c] > need[c] && key[j] == T[c];
     };
-    numba_argsort_focus(n, R.data(), [&](int32_t j) { return key[j]; }, is_tied);
+    numba_argsort_focus(n, R.data(), [&](int32_t j) { return key[j]; },
+                        [&](int64_t lo, int64_t hi) {
+                          for (int64_t t = lo; t <= hi; t++)
+                            if (is_tied(R[t])) return true;
+                          return false;
+                        });
     for (int64_t t = 0; t < n; t++)
       if (is_tied(R[t])) tied[P.labels[R[t]]].push_back(R[t]);
   }

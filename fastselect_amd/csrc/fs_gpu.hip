@@ -637,8 +637,8 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
     if (lane == 0) {
       // MultiSURF: exact distance in integer units.  ReliefF (mark_f32): the
       // reference's float32 key, stored negated so k_rf_select knows it is
-      // exact (a zero key stays +0 and reads back the same either way).
-      const double v = mark_f32 ? -(double)(float)acc : acc * sc;
+      // exact (a zero key is stored as +0, never -0, whose bits would sort last).
+      const double v = mark_f32 ? (acc > 0.0 ? -(double)(float)acc : 0.0) : acc * sc;
       D[(int64_t)pr.x * n_pad + pr.y] = v;
       D[(int64_t)pr.y * n_pad + pr.x] = v;
     }
@@ -1031,9 +1031,154 @@ __global__ __launch_bounds__(256) void k_rf_exact_rows(
 // Rows where more neighbours share a class's k-th distance than are needed:
 // replay numba's quicksort over the row's exact keys (numba_argsort_focus)
 // and take the tied neighbours in its order (ReliefF.py:157-175).  One
-// thread per row; R is per-row scratch.
-__global__ __launch_bounds__(64) void k_rf_ties(const int32_t* __restrict__ rows, int64_t n_rows,
-                                                int64_t n, const float* __restrict__ keys,
+// workgroup (one wave) per row: the lanes stage the row into LDS when it fits
+// (8 bytes per sample, n <= 20480) and lane 0 runs the sequential sort there;
+// larger rows sort in their global scratch.
+constexpr int64_t kTieLdsMaxN = 20480;
+
+// numba_argsort_focus (fs_internal.h) for one wave: same ranges, pivots,
+// swaps and result, but each Hoare partition is computed from its stop lists
+// instead of element by element.  In numba's loop the m-th swap exchanges
+// the m-th "left stop" (ascending position with key >= pivot) with the m-th
+// "right stop" (descending position with key <= pivot) of the untouched
+// window between the previous pair, and the loop ends at the first m where
+// that left stop is not below that right stop; the pivot then goes to the
+// m-th left stop, or to the previous right stop when the window has none
+// (that position now holds a swapped element >= pivot), or to `high` when no
+// swap happened.  A round collects up to 64 stops per side with ballots and
+// performs up to 64 swaps at once.  All lanes run the control flow in
+// lockstep; bufL/bufR are 64-entry LDS scratch.
+template <typename KeyFn>
+__device__ int wave_argsort_focus(int64_t len, int32_t* R, KeyFn key, int32_t* bufL,
+                                  int32_t* bufR) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  auto has_interest = [&](int64_t lo, int64_t hi) {
+    for (int64_t t0 = lo; t0 <= hi; t0 += 64) {
+      const int64_t t = t0 + lane;
+      if (__ballot(t <= hi && R[t] < 0) != 0ull) return true;
+    }
+    return false;
+  };
+  // up to 64 stops of one side inside [a, b], in scan order, into buf;
+  // returns how many
+  auto collect = [&](int64_t a, int64_t b, float pivot, bool left, int32_t* buf) {
+    int cnt = 0;
+    for (int64_t c0 = 0; cnt < 64 && c0 <= b - a; c0 += 64) {
+      const int64_t t = left ? a + c0 + lane : b - c0 - lane;
+      bool stop = false;
+      if (left ? t <= b : t >= a) {
+        const float kv = key(R[t]);
+        stop = left ? !(kv < pivot) : !(pivot < kv);
+      }
+      const uint64_t m = __ballot(stop);
+      const int rank = cnt + __popcll(m & below);
+      if (stop && rank < 64) buf[rank] = (int32_t)t;
+      cnt += __popcll(m);
+    }
+    __syncthreads();
+    return cnt < 64 ? cnt : 64;
+  };
+  if (len < 2) return 0;
+  constexpr int kSmall = 15, kMaxStack = 100;
+  __shared__ int64_t st_lo[kMaxStack], st_hi[kMaxStack];
+  int ns = 1;
+  st_lo[0] = 0;
+  st_hi[0] = len - 1;
+  __syncthreads();
+  while (ns > 0) {
+    ns--;
+    int64_t low = st_lo[ns], high = st_hi[ns];
+    bool live = true;
+    while (high - low >= kSmall) {
+      const int64_t mid = (low + high) >> 1;
+      // median of three and pivot stash: identical on every lane, one writer
+      int32_t rl = R[low], rm = R[mid], rh = R[high], tmp;
+      if (key(rm) < key(rl)) { tmp = rl; rl = rm; rm = tmp; }
+      if (key(rh) < key(rm)) { tmp = rh; rh = rm; rm = tmp; }
+      if (key(rm) < key(rl)) { tmp = rl; rl = rm; rm = tmp; }
+      const float pivot = key(rm);
+      __syncthreads();
+      if (lane == 0) {
+        R[low] = rl;
+        R[mid] = rh;   // stash: R[high] <-> R[mid]
+        R[high] = rm;
+      }
+      __syncthreads();
+      // partition [low, high - 1] around pivot
+      int64_t a = low, b = high - 1, jprev = high, ifinal = -1;
+      while (ifinal < 0) {
+        const int cl = collect(a, b, pivot, true, bufL);
+        const int cr = collect(a, b, pivot, false, bufR);
+        const int64_t Lm = lane < cl ? bufL[lane] : INT64_MAX;
+        const int64_t Rm = lane < cr ? bufR[lane] : -1;
+        const uint64_t fail = __ballot(!(Lm < Rm));
+        const int f = fail ? (int)__builtin_ctzll(fail) : 64;
+        // swaps m < f, all positions distinct: read, then write
+        int32_t vl = 0, vr = 0;
+        if (lane < f) { vl = R[Lm]; vr = R[Rm]; }
+        __syncthreads();
+        if (lane < f) { R[Lm] = vr; R[Rm] = vl; }
+        __syncthreads();
+        if (f < 64) {
+          const int64_t jlast = f > 0 ? (int64_t)bufR[f - 1] : jprev;
+          ifinal = f < cl ? (int64_t)bufL[f] : jlast;
+          if (ifinal > jlast) ifinal = jlast;
+        } else {
+          a = (int64_t)bufL[63] + 1;
+          b = (int64_t)bufR[63] - 1;
+          jprev = bufR[63];
+        }
+        __syncthreads();
+      }
+      const int64_t i = ifinal;
+      {
+        const int32_t ri = R[i], rh2 = R[high];
+        __syncthreads();
+        if (lane == 0) { R[i] = rh2; R[high] = ri; }
+        __syncthreads();
+      }
+      int64_t push_lo, push_hi, keep_lo, keep_hi;
+      if (high - i > i - low) {
+        push_lo = i + 1; push_hi = high; keep_lo = low; keep_hi = i - 1;
+      } else {
+        push_lo = low; push_hi = i - 1; keep_lo = i + 1; keep_hi = high;
+      }
+      if (push_hi >= push_lo && has_interest(push_lo, push_hi)) {
+        if (ns >= kMaxStack) return -1;
+        __syncthreads();
+        if (lane == 0) { st_lo[ns] = push_lo; st_hi[ns] = push_hi; }
+        __syncthreads();
+        ns++;
+      }
+      low = keep_lo;
+      high = keep_hi;
+      if (high < low || !has_interest(low, high)) {
+        live = false;
+        break;
+      }
+    }
+    if (!live) continue;
+    if (lane == 0) {  // insertion sort [low, high]
+      for (int64_t i = low + 1; i <= high; i++) {
+        const int32_t kk = R[i];
+        const float v = key(kk);
+        int64_t j = i;
+        while (j > low && v < key(R[j - 1])) {
+          R[j] = R[j - 1];
+          j--;
+        }
+        R[j] = kk;
+      }
+    }
+    __syncthreads();
+  }
+  return 0;
+}
+
+template <bool IN_LDS>
+__global__ __launch_bounds__(64) void k_rf_ties(const int32_t* __restrict__ rows, int64_t n,
+                                                const float* __restrict__ keys_all,
                                                 const int32_t* __restrict__ lab, int n_classes,
                                                 int64_t k, const uint32_t* __restrict__ tkey,
                                                 const int32_t* __restrict__ tneed,
@@ -1041,36 +1186,69 @@ __global__ __launch_bounds__(64) void k_rf_ties(const int32_t* __restrict__ rows
                                                 int32_t* __restrict__ R_all,
                                                 int32_t* __restrict__ nbr,
                                                 int* __restrict__ status) {
-  const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (r >= n_rows) return;
+  extern __shared__ uint32_t tie_lds[];
+  __shared__ int sort_rc;
+  const int lane = threadIdx.x;
+  const int64_t r = blockIdx.x;
   const int64_t i = rows[r];
-  const float* key = keys + r * n;
+  const float* key = keys_all + r * n;
   int32_t* R = R_all + r * n;
+  if (IN_LDS) {
+    float* kl = (float*)tie_lds;
+    for (int64_t j = lane; j < n; j += 64) kl[j] = key[j];
+    key = kl;
+    R = (int32_t*)(tie_lds + n);
+  }
   const uint32_t* Ti = tkey + i * n_classes;
   const int32_t* need = tneed + i * n_classes;
   const int32_t* eq = teq + i * n_classes;
-  auto tied = [&](int32_t j) {
+  // handle = sample index, sign bit set for a tied candidate (its key equals
+  // the k-th key of its class, in a class with more such keys than needed):
+  // the sort then tests "interesting" without touching the labels
+  for (int64_t j = lane; j < n; j += 64) {
     const int c = lab[j];
-    return j != i && eq[c] > need[c] && __float_as_uint(key[j]) == Ti[c];
-  };
-  if (numba_argsort_focus(n, R, [&](int32_t j) { return key[j]; }, tied) != 0) {
-    atomicExch(status, 1);
+    const bool t = j != i && eq[c] > need[c] && __float_as_uint(key[j]) == Ti[c];
+    R[j] = (int32_t)((uint32_t)j | (t ? 0x80000000u : 0u));
+  }
+  __syncthreads();
+  // the whole wave sorts (partitions from ballot-collected stop lists)
+  {
+    __shared__ int32_t bufL[64], bufR[64];
+    const int rc = wave_argsort_focus(
+        n, R, [&](int32_t h) { return key[h & 0x7FFFFFFF]; }, bufL, bufR);
+    if (lane == 0) sort_rc = rc;
+  }
+  __syncthreads();
+  if (sort_rc != 0) {
+    if (lane == 0) atomicExch(status, 1);
     return;
   }
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   for (int c = 0; c < n_classes; c++) {
     if (!(eq[c] > need[c])) continue;
     int32_t* out = nbr + (i * n_classes + c) * k;
     const float T = __uint_as_float(Ti[c]);
     int64_t cnt = 0;
-    for (int64_t j = 0; j < n; j++)
-      if (j != i && lab[j] == c && key[j] < T) out[cnt++] = (int32_t)j;
-    int64_t taken = 0;
-    for (int64_t t = 0; t < n && taken < need[c]; t++) {
-      const int32_t j = R[t];
-      if (lab[j] == c && tied(j)) {
-        out[cnt++] = j;
-        taken++;
-      }
+    // every key < T of class c, in index order
+    for (int64_t j0 = 0; j0 < n; j0 += 64) {
+      const int64_t j = j0 + lane;
+      const bool take = j < n && j != i && lab[j] == c && key[j] < T;
+      const uint64_t m = __ballot(take);
+      if (take) out[cnt + __popcll(m & below)] = (int32_t)j;
+      cnt += __popcll(m);
+    }
+    // then the first need[c] tied keys of class c in numba's order
+    int64_t left = need[c];
+    for (int64_t t0 = 0; t0 < n && left > 0; t0 += 64) {
+      const int64_t t = t0 + lane;
+      const int32_t h = t < n ? R[t] : 0;
+      const bool take = h < 0 && lab[h & 0x7FFFFFFF] == c;
+      const uint64_t m = __ballot(take);
+      const int64_t rank = __popcll(m & below);
+      if (take && rank < left) out[cnt + rank] = h & 0x7FFFFFFF;
+      const int64_t got = __popcll(m);
+      cnt += got < left ? got : left;
+      left -= got < left ? got : left;
     }
   }
 }
@@ -1610,6 +1788,9 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   FS_TRY(dalloc(g, &keys, (size_t)batch * n));
   FS_TRY(dalloc(g, &status, 1));
   FS_HIP(hipMemsetAsync(status, 0, sizeof(int), g->stream));
+  if (n <= kTieLdsMaxN)
+    FS_HIP(hipFuncSetAttribute((const void*)k_rf_ties<true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(8 * n)));
   for (int64_t r0 = 0; r0 < (int64_t)tie_rows.size(); r0 += batch) {
     const int64_t nr = std::min<int64_t>(batch, (int64_t)tie_rows.size() - r0);
     FS_TRY(h2d(g, drows, tie_rows.data() + r0, (size_t)nr));
@@ -1617,8 +1798,12 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
         (const float*)g->x, n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, drows, g->D,
         Q.n_pad, inv_sc, keys);
     FS_TRY(launch_check("k_rf_exact_rows"));
-    k_rf_ties<<<(unsigned)((nr + 63) / 64), 64, 0, g->stream>>>(drows, nr, n, keys, g->lab, C, k,
-                                                                tkey, tneed, teq, R, nbr, status);
+    if (n <= kTieLdsMaxN)
+      k_rf_ties<true><<<(unsigned)nr, 64, (size_t)8 * n, g->stream>>>(
+          drows, n, keys, g->lab, C, k, tkey, tneed, teq, R, nbr, status);
+    else
+      k_rf_ties<false><<<(unsigned)nr, 64, 0, g->stream>>>(drows, n, keys, g->lab, C, k, tkey,
+                                                           tneed, teq, R, nbr, status);
     FS_TRY(launch_check("k_rf_ties"));
   }
   int hstatus = 0;

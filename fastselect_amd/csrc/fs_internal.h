@@ -145,22 +145,20 @@ FS_HD inline double surf_weight(bool near, bool hit, int use_star) {
 // whose key equals a tied k-th distance) is dropped instead of sorted:
 // ranges are disjoint once split, so the final relative order of the
 // interesting elements is exactly numba's, at ~2n work instead of n log n.
-// key(j) and interesting(j) take the sample index.  Returns 0, or -1 if the
-// explicit stack (numba's MAX_STACK = 100) would overflow.
-template <typename KeyFn, typename InterestFn>
-FS_HD inline int numba_argsort_focus(int64_t len, int32_t* R, KeyFn key, InterestFn interesting) {
-  for (int64_t t = 0; t < len; t++) R[t] = (int32_t)t;
+// R holds one handle per element in the initial order (R[t] = element t,
+// possibly tagged); key(h) takes a handle and has_interest(lo, hi) tells
+// whether R[lo..hi] holds an interesting element.  Returns 0, or -1 if the
+// explicit stack (numba's MAX_STACK = 100) would overflow.  On the GPU every
+// lane of a wave may run it in lockstep (identical values, identical stores)
+// so that has_interest can scan with the whole wave.
+template <typename KeyFn, typename RangeFn>
+FS_HD inline int numba_argsort_focus(int64_t len, int32_t* R, KeyFn key, RangeFn has_interest) {
   if (len < 2) return 0;
   constexpr int kSmall = 15, kMaxStack = 100;
   int64_t st_lo[kMaxStack], st_hi[kMaxStack];
   int ns = 1;
   st_lo[0] = 0;
   st_hi[0] = len - 1;
-  auto has_interest = [&](int64_t lo, int64_t hi) {
-    for (int64_t t = lo; t <= hi; t++)
-      if (interesting(R[t])) return true;
-    return false;
-  };
   while (ns > 0) {
     ns--;
     int64_t low = st_lo[ns], high = st_hi[ns];

@@ -142,6 +142,17 @@ def test_relieff_boundary_ties_follow_numba_quicksort(oracle, kind, k):
     assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=k, discrete_limit=dl), TOL)
 
 
+def test_relieff_ties_large_rows(oracle):
+    """Tie replay on rows long enough for many 64-wide partition rounds and
+    deep recursion (all-discrete data: ties in every row), CPU == GPU == oracle."""
+    from fastselect_amd import ReliefF
+    rng = np.random.default_rng(5)
+    X = rng.integers(0, 4, size=(3000, 15)).astype(float)
+    y = rng.integers(0, 2, 3000)
+    s = _fit(ReliefF, X, y, n_neighbors=10, discrete_limit=4)
+    assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=10, discrete_limit=4), TOL)
+
+
 def test_relieff_large_n_boundary(oracle):
     """n large enough that k-th-neighbour keys crowd within float32 ulps:
     the exact-key band must make every selection the reference's."""
