@@ -872,7 +872,8 @@ __device__ __forceinline__ uint32_t rf_key(double d, double inv_sc) {
 // T_c (index order; rows where more keys equal T_c than are needed are
 // re-ordered the reference's way by k_rf_ties), and teq[i][c] counts the
 // keys equal to T_c.
-__global__ __launch_bounds__(256) void k_rf_select(const double* __restrict__ D, int64_t n,
+template <bool STAGE>
+__global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D, int64_t n,
                                                    int64_t n_pad, double inv_sc,
                                                    const int32_t* __restrict__ lab,
                                                    const int64_t* __restrict__ class_count,
@@ -882,58 +883,138 @@ __global__ __launch_bounds__(256) void k_rf_select(const double* __restrict__ D,
                                                    int32_t* __restrict__ teq,
                                                    int32_t* __restrict__ nbr,
                                                    int32_t* __restrict__ nfound) {
-  extern __shared__ uint32_t sh[];  // hist[n_classes][256], prefix[C], need[C]
+  // hist[n_classes][256], prefix[C], need[C], then (STAGE) the row's keys
+  extern __shared__ uint32_t sh[];
   uint32_t* hist = sh;
   uint32_t* prefix = sh + n_classes * 256;
   uint32_t* need = prefix + n_classes;
+  uint32_t* keys = need + n_classes;
+  uint8_t* labs = (uint8_t*)(keys + n);  // STAGE: class codes (< 64)
   const int64_t i = blockIdx.x;
   const int tid = threadIdx.x;
+  const int nt = blockDim.x, nwaves = nt >> 6;
   const int32_t li = lab[i];
   const double* row = D + i * n_pad;
-  for (int c = tid; c < n_classes; c += 256) {
+  // STAGE: the row's float32 keys are read from HBM once into LDS (the five
+  // sweeps below then cost no HBM traffic)
+  auto key_of = [&](int64_t j) { return STAGE ? keys[j] : rf_key(row[j], inv_sc); };
+  auto lab_of = [&](int64_t j) { return STAGE ? (int32_t)labs[j] : lab[j]; };
+  // Key range of the row: bits above the highest bit in which two keys
+  // differ are common to all of them, so the radix passes start below it
+  // (a row's distances share their float exponent or nearly: starting at
+  // bit 31 would pile every key into one or two bins of the first pass).
+  __shared__ uint32_t red_or[16], red_and[16];
+  uint32_t kor = 0u, kand = 0xFFFFFFFFu;
+  // 8 independent loads in flight per thread (one workgroup per CU when
+  // staging: the row read is latency-bound otherwise)
+  constexpr int kU = 8;
+  for (int64_t j0 = tid; j0 < n; j0 += (int64_t)kU * nt) {
+    double dv[kU];
+    int32_t lv[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int64_t j = j0 + (int64_t)u * nt;
+      dv[u] = j < n ? row[j] : 0.0;
+      lv[u] = (STAGE && j < n) ? lab[j] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int64_t j = j0 + (int64_t)u * nt;
+      if (j >= n) continue;
+      const uint32_t kv = rf_key(dv[u], inv_sc);
+      if (STAGE) {
+        keys[j] = kv;
+        labs[j] = (uint8_t)lv[u];
+      }
+      if (j != i) {
+        kor |= kv;
+        kand &= kv;
+      }
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    kor |= __shfl_xor(kor, o);
+    kand &= __shfl_xor(kand, o);
+  }
+  if ((tid & 63) == 0) {
+    red_or[tid >> 6] = kor;
+    red_and[tid >> 6] = kand;
+  }
+  __syncthreads();
+  kor = 0u;
+  kand = 0xFFFFFFFFu;
+  for (int w = 0; w < nwaves; w++) {
+    kor |= red_or[w];
+    kand &= red_and[w];
+  }
+  const uint32_t diff = kor & ~kand;  // bits that are not common
+  const int top = diff ? 31 - __builtin_clz(diff) : 0;
+  const int d_start = top / 8;
+  const uint32_t common = d_start >= 3 ? 0u : (kand & (0xFFFFFFFFu << (8 * (d_start + 1))));
+  for (int c = tid; c < n_classes; c += nt) {
     const int64_t members = class_count[c] - (c == li ? 1 : 0);
     const int64_t kc = members < k ? members : k;
-    prefix[c] = 0;
+    prefix[c] = common;
     // need = rank (1-based) of the wanted key inside the current bucket;
     // kc == members: take everything (T = 0xFFFFFFFF, nothing equal needed)
     need[c] = (uint32_t)kc;
     if (kc == members) prefix[c] = 0xFFFFFFFFu, need[c] = 0;
   }
   __syncthreads();
-  for (int d = 3; d >= 0; d--) {
-    for (int e = tid; e < n_classes * 256; e += 256) hist[e] = 0;
+  for (int d = d_start; d >= 0; d--) {
+    for (int e = tid; e < n_classes * 256; e += nt) hist[e] = 0;
     __syncthreads();
     const int sh_hi = 8 * (d + 1);
-    for (int64_t j = tid; j < n; j += 256) {
+    for (int64_t j = tid; j < n; j += nt) {
       if (j == i) continue;
-      const int32_t c = lab[j];
+      const int32_t c = lab_of(j);
       if (need[c] == 0) continue;
-      const uint32_t key = rf_key(row[j], inv_sc);
+      const uint32_t key = key_of(j);
       if (sh_hi < 32 && (key >> sh_hi) != (prefix[c] >> sh_hi)) continue;
       atomicAdd(&hist[c * 256 + ((key >> (8 * d)) & 0xFF)], 1u);
     }
     __syncthreads();
-    for (int c = tid; c < n_classes; c += 256) {
-      if (need[c] == 0) continue;
-      uint32_t cum = 0, b = 0;
-      for (; b < 256; b++) {
-        const uint32_t h = hist[c * 256 + b];
-        if (cum + h >= need[c]) break;
-        cum += h;
+    // per class (one wave each): the bucket holding the need-th key, by a
+    // wave prefix sum over 4 bins per lane
+    {
+      const int wv = tid >> 6, ln = tid & 63;
+      for (int c = wv; c < n_classes; c += nwaves) {
+        const uint32_t nd = need[c];
+        if (nd == 0) continue;
+        const uint32_t* hc = hist + c * 256 + 4 * ln;
+        const uint32_t h0 = hc[0], h1 = hc[1], h2 = hc[2], h3 = hc[3];
+        const uint32_t tot = h0 + h1 + h2 + h3;
+        uint32_t incl = tot;
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t t = __shfl_up(incl, o);
+          if (ln >= o) incl += t;
+        }
+        const uint32_t excl = incl - tot;
+        // the first lane whose inclusive sum reaches nd owns the bucket
+        const uint64_t m = __ballot(incl >= nd);
+        const int owner = (int)__builtin_ctzll(m);
+        if (ln == owner) {
+          uint32_t cum = excl, b = 4 * ln;
+          const uint32_t hv[4] = {h0, h1, h2, h3};
+          for (int q = 0; q < 4; q++, b++) {
+            if (cum + hv[q] >= nd) break;
+            cum += hv[q];
+          }
+          prefix[c] |= b << (8 * d);
+          need[c] = nd - cum;
+        }
       }
-      prefix[c] |= b << (8 * d);
-      need[c] -= cum;
     }
     __syncthreads();
   }
-  for (int c = tid; c < n_classes; c += 256) {
+  for (int c = tid; c < n_classes; c += nt) {
     tkey[i * n_classes + c] = prefix[c];
     tneed[i * n_classes + c] = (int32_t)need[c];
   }
   if (!collect) return;
   // Ordered collection, one wave per class.
   const int wave = tid >> 6, lane = tid & 63;
-  for (int c = wave; c < n_classes; c += 4) {
+  for (int c = wave; c < n_classes; c += nwaves) {
     const uint32_t T = prefix[c];
     uint32_t eq_left = need[c];
     int64_t cnt = 0, n_eq = 0;
@@ -941,8 +1022,8 @@ __global__ __launch_bounds__(256) void k_rf_select(const double* __restrict__ D,
     for (int64_t j0 = 0; j0 < n; j0 += 64) {
       const int64_t j = j0 + lane;
       bool lt = false, eq = false;
-      if (j < n && j != i && lab[j] == c) {
-        const uint32_t key = rf_key(row[j], inv_sc);
+      if (j < n && j != i && lab_of(j) == c) {
+        const uint32_t key = key_of(j);
         lt = key < T;
         eq = key == T;
       }
@@ -1729,10 +1810,22 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   FS_TRY(dalloc(g, &tneed, (size_t)n * C));
   FS_TRY(dalloc(g, &teq, (size_t)n * C));
   const size_t shbytes = (size_t)C * 256 * 4 + 2 * (size_t)C * 4;
+  const size_t shstage = shbytes + (size_t)n * 5;
+  const bool stage = shstage <= 160 * 1024;
+  if (stage)
+    FS_HIP(hipFuncSetAttribute((const void*)k_rf_select<true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shstage));
+  auto select = [&](int collect) {
+    if (stage)
+      k_rf_select<true><<<(unsigned)n, 1024, shstage, g->stream>>>(
+          g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, tkey, tneed, teq, nbr, nfound);
+    else
+      k_rf_select<false><<<(unsigned)n, 256, shbytes, g->stream>>>(
+          g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, tkey, tneed, teq, nbr, nfound);
+    return launch_check("k_rf_select");
+  };
   // 1. k-th keys from the quantised distances
-  k_rf_select<<<(unsigned)n, 256, shbytes, g->stream>>>(g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C,
-                                                        k, 0, tkey, tneed, teq, nbr, nfound);
-  FS_TRY(launch_check("k_rf_select"));
+  FS_TRY(select(0));
   // 2. exact keys inside the band (quantisation error + float32 rounding)
   const double band_abs = 2.0 * Q.amb_delta, band_rel = 2.0 * 1.2e-7;
   g->n_refined = 0;
@@ -1760,9 +1853,7 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
     FS_TRY(launch_check("k_exact_pairs"));
   }
   // 3. exact selection
-  k_rf_select<<<(unsigned)n, 256, shbytes, g->stream>>>(g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C,
-                                                        k, 1, tkey, tneed, teq, nbr, nfound);
-  FS_TRY(launch_check("k_rf_select"));
+  FS_TRY(select(1));
   // 4. rows with more neighbours at the k-th key than needed
   std::vector<int32_t> hneed((size_t)n * C), heq((size_t)n * C);
   FS_HIP(hipMemcpyAsync(hneed.data(), tneed, hneed.size() * 4, hipMemcpyDeviceToHost, g->stream));
