@@ -85,6 +85,14 @@ class MultiSURF(TransformerMixin, BaseEstimator):
         self.top_features_ = _base.top_features(scores, n_select)
         return self
 
+    def _resident_scorer(self, x, y):
+        """A scorer for TuRF that keeps X resident (on the GPU for the GPU
+        backend) and re-scores column subsets through feat_idx, which the
+        reference's kernels support for exactly this (MultiSURF.py:147,256):
+        ``refit(active)`` leaves this estimator as ``fit(X[:, active], y)``
+        would, without copying or re-uploading X."""
+        return _ResidentMultiSURF(self, x, y)
+
     def transform(self, x: np.ndarray) -> np.ndarray:
         """Reduce x to the selected features."""
         check_is_fitted(self)
@@ -95,3 +103,43 @@ class MultiSURF(TransformerMixin, BaseEstimator):
         """Fit to data, then transform it."""
         self.fit(x, y)
         return self.transform(x)
+
+
+class _ResidentMultiSURF:
+    """See ``MultiSURF._resident_scorer``."""
+
+    def __init__(self, est: MultiSURF, x, y):
+        self.est = est
+        x, y = validate_data(est, x, y, y_numeric=True, dtype=np.float32, ensure_2d=True)
+        est.effective_backend_ = _base.effective_backend(est.backend)
+        self.n = x.shape[0]
+        self.is_discrete, col_min, col_max = _base.column_preprocess(
+            x, est.discrete_limit, est.effective_backend_)
+        ranges = (col_max - col_min).astype(np.float32)
+        ranges[ranges == 0] = 1
+        recip = (1.0 / ranges).astype(np.float32)
+        from .parallel import ShardedMultiSURF
+        self.job = ShardedMultiSURF(x, y, recip, self.is_discrete, use_star=est.use_star,
+                                    backend=est.effective_backend_, shard=False)
+        self.active = None
+
+    def refit(self, active: np.ndarray):
+        est = self.est
+        active = np.asarray(active, dtype=np.int64)
+        n_select = est._validate_parameters(self.n, active.size)
+        est.n_features_in_ = active.size
+        if est.verbose:
+            name = "MultiSURF*" if est.use_star else "MultiSURF"
+            where = "GPU" if est.effective_backend_ == "gpu" else "CPU"
+            print(f"Running {name} on the {where} now...")
+        if self.active is None or not np.array_equal(active, self.active):
+            self.job.set_features(active)
+            self.active = active
+        scores = self.job.step().cpu().numpy()
+        est.is_discrete_ = self.is_discrete[active]
+        est.feature_importances_ = scores
+        est.top_features_ = _base.top_features(scores, n_select)
+        return est
+
+    def close(self):
+        self.job.close()

@@ -47,24 +47,39 @@ class TuRF(TransformerMixin, BaseEstimator):
             raise ValueError("pct_remove must be between 0 and 1.")
 
         scorer = clone(self.estimator)
-        scorer.fit(X, y)
-        self.feature_importances_ = scorer.feature_importances_.copy()
-
         active = np.arange(self.n_features_in_)
-        scores = self.feature_importances_.copy()
-        rounds = 0
-        while len(active) > self.n_features_to_select:
-            if self.n_iterations is not None and rounds >= self.n_iterations:
-                break
-            drop = max(1, int(len(active) * self.pct_remove))
-            drop = min(drop, len(active) - self.n_features_to_select)
-            worst = np.argsort(scores)[:drop]
-            active = np.delete(active, worst)
-            if self.verbose:
-                print(f"Iteration {rounds}: {len(active)} features remaining.")
-            scorer.fit(X[:, active], y)
-            scores = scorer.feature_importances_
-            rounds += 1
+        # Estimators that can keep X resident re-score column subsets in place
+        # (MultiSURF: feat_idx on a device-resident plan);
+        # any other estimator is refit on X[:, active] as the reference does.
+        resident = getattr(scorer, "_resident_scorer", None)
+        runner = resident(X, y) if resident is not None else None
+        try:
+            if runner is not None:
+                runner.refit(active)
+            else:
+                scorer.fit(X, y)
+            self.feature_importances_ = scorer.feature_importances_.copy()
+
+            scores = self.feature_importances_.copy()
+            rounds = 0
+            while len(active) > self.n_features_to_select:
+                if self.n_iterations is not None and rounds >= self.n_iterations:
+                    break
+                drop = max(1, int(len(active) * self.pct_remove))
+                drop = min(drop, len(active) - self.n_features_to_select)
+                worst = np.argsort(scores)[:drop]
+                active = np.delete(active, worst)
+                if self.verbose:
+                    print(f"Iteration {rounds}: {len(active)} features remaining.")
+                if runner is not None:
+                    runner.refit(active)
+                else:
+                    scorer.fit(X[:, active], y)
+                scores = scorer.feature_importances_
+                rounds += 1
+        finally:
+            if runner is not None:
+                runner.close()
 
         ranked = active[np.argsort(scores)[::-1]]
         self.top_features_ = np.sort(ranked)

@@ -36,7 +36,8 @@ _vp = ctypes.c_void_p
 # every symbol include/fastselect_amd.h declares (checked by tests/test_abi.py)
 EXPORTED = (
     "fs_version", "fs_last_error", "fs_device_count", "fs_column_stats", "fs_multisurf_score",
-    "fs_relieff_score", "fs_surf_score", "fs_plan_create", "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2",
+    "fs_relieff_score", "fs_surf_score", "fs_plan_create", "fs_plan_set_features",
+    "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2",
     "fs_plan_info", "fs_plan_kernel_ms", "fs_plan_destroy",
 )
 
@@ -77,6 +78,7 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_create.argtypes = [ctypes.POINTER(_vp), _int, _int, _f32p, _i64, _i64, _f64p,
                                    _f32p, _i64p, _i64, _int, _u8p, _int, _int, _int,
                                    ctypes.c_uint64]
+    lib.fs_plan_set_features.argtypes = [_vp, _i64p, _i64]
     lib.fs_plan_pass1.argtypes = [_vp, _vp]
     lib.fs_plan_select.argtypes = [_vp, _vp, _vp]
     lib.fs_plan_pass2.argtypes = [_vp, _vp, _vp]
@@ -84,9 +86,9 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_kernel_ms.argtypes = [_vp, _int]
     lib.fs_plan_kernel_ms.restype = ctypes.c_double
     lib.fs_plan_destroy.argtypes = [_vp]
-    for name in ("fs_column_stats", "fs_multisurf_score", "fs_relieff_score", "fs_surf_score", "fs_plan_create",
-                 "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_info",
-                 "fs_plan_destroy"):
+    for name in ("fs_column_stats", "fs_multisurf_score", "fs_relieff_score", "fs_surf_score",
+                 "fs_plan_create", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
+                 "fs_plan_pass2", "fs_plan_info", "fs_plan_destroy"):
         getattr(lib, name).restype = _int
     return lib
 
@@ -227,6 +229,14 @@ class Plan:
                                   None if fidx is None else _p(fidx, _i64p), self.n_kept,
                                   int(bool(use_star)), _p(isd, _u8p), int(rank), int(world),
                                   int(n_jobs), ctypes.c_uint64(int(stream))))
+
+    def set_features(self, feat_idx) -> None:
+        """Score another feature subset of the resident samples next
+        (``fs_plan_set_features``); pass2 then returns len(feat_idx) sums."""
+        fidx = None if feat_idx is None else np.ascontiguousarray(feat_idx, dtype=np.int64)
+        self.n_kept = self.p if fidx is None else fidx.size
+        check(_lib.fs_plan_set_features(self._h, None if fidx is None else _p(fidx, _i64p),
+                                        self.n_kept))
 
     def pass1(self, rowstats_ptr: int) -> None:
         check(_lib.fs_plan_pass1(self._h, _vp(rowstats_ptr)))

@@ -223,6 +223,33 @@ int fs_plan_create(fs_plan** plan_out, int backend, int device, const float* x, 
   return FS_OK;
 }
 
+int fs_plan_set_features(fs_plan* pl, const int64_t* feat_idx, int64_t n_kept) {
+  if (!pl) {
+    set_error("plan is NULL");
+    return FS_EINVAL;
+  }
+  const Prepared& O = pl->P;
+  const bool gpu = pl->backend == FS_BACKEND_GPU;
+  // the GPU plan keeps X and its column ranges on the device; the CPU plan
+  // keeps its own copy of X
+  const void* x = gpu ? nullptr : (const void*)pl->x.data();
+  Prepared P;
+  int rc = prepare(P, O.algo, x, 0, O.n, O.p_in, feat_idx, n_kept, O.recip_in.data(),
+                   O.disc_in.data(), pl->n_jobs, gpu);
+  if (rc) return map_prep_rc(rc);
+  P.labels = O.labels;
+  P.n_classes = O.n_classes;
+  P.class_prior = O.class_prior;
+  P.use_star = O.use_star;
+  P.k_neighbors = O.k_neighbors;
+  if (gpu) {
+    rc = gpu::plan_set_features(pl->g, P);
+    if (rc != FS_OK) return rc;
+  }
+  pl->P = P;
+  return FS_OK;
+}
+
 int fs_plan_pass1(fs_plan* pl, double* rowstats) {
   if (!pl || !rowstats) {
     set_error("NULL plan or buffer");

@@ -1417,7 +1417,10 @@ struct Plan {
   int64_t n_refined = 0;
   int64_t n_tie_rows = 0;      // ReliefF rows re-ordered by k_rf_ties
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  std::vector<void*> owned;
+  std::vector<void*> owned;         // buffers sized by n (live as long as the plan)
+  std::vector<void*> owned_layout;  // buffers sized by the feature layout (PW)
+  bool layout_alloc = false;        // dalloc target: owned_layout
+  std::vector<char> colmin, colmax; // per input column, x's dtype (device-measured)
 };
 
 template <typename T>
@@ -1431,7 +1434,7 @@ static int dalloc(Plan* g, T** p, size_t count) {
               " bytes failed: " + hipGetErrorString(e));
     return FS_EOOM;
   }
-  g->owned.push_back(q);
+  (g->layout_alloc ? g->owned_layout : g->owned).push_back(q);
   *p = (T*)q;
   return FS_OK;
 }
@@ -1463,11 +1466,79 @@ void plan_destroy(Plan* g) {
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   trace_mark("kernels (to sync)");
   for (void* q : g->owned) (void)hipFree(q);
+  for (void* q : g->owned_layout) (void)hipFree(q);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
   if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
   delete g;
   trace_mark("plan: free");
+}
+
+// Feature-layout part of a plan: everything sized by the kept features
+// (permutation tables, quantised operands, pass-2 partials), rebuilt when
+// the plan is re-targeted to another feature subset (fs_plan_set_features).
+static int plan_layout(Plan* g) {
+  Prepared& Q = g->P;
+  FS_HIP(hipStreamSynchronize(g->stream));
+  for (void* q : g->owned_layout) (void)hipFree(q);
+  g->owned_layout.clear();
+  int rc;
+  if (!Q.ranges_ready) {
+    // continuous column ranges, measured on the device once per plan
+    const size_t esz = g->x_is_f64 ? 8 : 4;
+    if (g->colmin.empty()) {
+      g->colmin.resize((size_t)Q.p_in * esz);
+      g->colmax.resize((size_t)Q.p_in * esz);
+      if ((rc = column_minmax(g->x, g->x_is_f64, Q.n, Q.p_in, g->colmin.data(), g->colmax.data(),
+                              g->stream))) {
+        g->colmin.clear();
+        return rc;
+      }
+      trace_mark("plan: device ranges");
+    }
+    std::vector<double> cmin((size_t)Q.pc), cmax((size_t)Q.pc);
+    for (int64_t c = 0; c < Q.pc; c++) {
+      const int64_t col = Q.src_col[c];
+      cmin[c] = g->x_is_f64 ? ((const double*)g->colmin.data())[col]
+                            : (double)((const float*)g->colmin.data())[col];
+      cmax[c] = g->x_is_f64 ? ((const double*)g->colmax.data())[col]
+                            : (double)((const float*)g->colmax.data())[col];
+    }
+    if (finalize_scale(Q, cmin.data(), cmax.data())) return FS_EINVAL;
+  }
+  const int64_t nfb = (Q.PW + 127) / 128;
+  // ~64k pass-2 workgroups: enough to fill 256 CUs and bound tail imbalance.
+  g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + 65535) / 65536);
+  g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
+  // histogram shift so that the largest quantised value lands in bin < 4096
+  g->rank_shift = 0;
+  while ((Q.qmax / std::ldexp(1.0, g->rank_shift)) >= (double)kRankBins) g->rank_shift++;
+  g->layout_alloc = true;
+  rc = FS_OK;
+  if ((rc = dalloc(g, &g->src_col, Q.PW)) || (rc = dalloc(g, &g->out_pos, Q.PW)) ||
+      (rc = dalloc(g, &g->off, Q.PW)) || (rc = dalloc(g, &g->qs, Q.PW)) ||
+      (rc = dalloc(g, &g->scl, Q.PW)) || (rc = dalloc(g, &g->dtab_off, Q.PW + 1)) ||
+      (rc = dalloc(g, &g->dtab, Q.dtab.size())) ||
+      (rc = dalloc(g, &g->xs, (size_t)(Q.n_pad + 2) * Q.PW))) {
+  } else if (Q.algo == ALGO_SURF) {
+    rc = dalloc(g, &g->xT64, (size_t)Q.PW * Q.n_pad);
+  } else if ((rc = dalloc(g, &g->xqT, (size_t)Q.PW * Q.n_pad)) == FS_OK) {
+    rc = dalloc(g, &g->epsT, (size_t)Q.PW * Q.n_pad);
+  }
+  if (rc == FS_OK && Q.algo != ALGO_RELIEFF) rc = dalloc(g, &g->spart, (size_t)g->nseg * Q.PW);
+  g->layout_alloc = false;
+  if (rc) return rc;
+  std::vector<double> qs(Q.PW, 0.0);
+  for (int64_t c = 0; c < Q.PW; c++) qs[c] = Q.scale[c] * Q.SC;
+  if ((rc = h2d(g, g->src_col, Q.src_col.data(), Q.PW)) ||
+      (rc = h2d(g, g->out_pos, Q.out_pos.data(), Q.PW)) ||
+      (rc = h2d(g, g->off, Q.offset.data(), Q.PW)) || (rc = h2d(g, g->qs, qs.data(), Q.PW)) ||
+      (rc = h2d(g, g->scl, Q.scale.data(), Q.PW)) ||
+      (rc = h2d(g, g->dtab_off, Q.dtab_off.data(), Q.PW + 1)) ||
+      (rc = h2d(g, g->dtab, Q.dtab.data(), Q.dtab.size())))
+    return rc;
+  FS_HIP(hipStreamSynchronize(g->stream));
+  return FS_OK;
 }
 
 int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int device,
@@ -1516,72 +1587,36 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   g->n_tiles = (int64_t)bi.size();
   std::vector<int2> tl(g->n_tiles);
   for (int64_t t = 0; t < g->n_tiles; t++) tl[t] = make_int2(bi[t], bj[t]);
-  const int64_t nfb = (Q.PW + 127) / 128;
-  // ~64k pass-2 workgroups: enough to fill 256 CUs and bound tail imbalance.
-  g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + 65535) / 65536);
-  g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
   g->list_cap = std::max<int64_t>(1 << 16, Q.n * 64);
   const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
   int rc;
   trace_mark("plan: host setup");
-  if ((rc = dalloc(g, (char**)&g->x, xbytes)) ||
-      (rc = dalloc(g, &g->src_col, Q.PW)) || (rc = dalloc(g, &g->out_pos, Q.PW)) ||
-      (rc = dalloc(g, &g->off, Q.PW)) || (rc = dalloc(g, &g->qs, Q.PW)) ||
-      (rc = dalloc(g, &g->scl, Q.PW)) || (rc = dalloc(g, &g->dtab_off, Q.PW + 1)) ||
-      (rc = dalloc(g, &g->dtab, Q.dtab.size())) || (rc = dalloc(g, &g->lab, Q.n_pad)) ||
-      (rc = dalloc(g, &g->xs, (size_t)(Q.n_pad + 2) * Q.PW)) || (rc = dalloc(g, &g->corr, Q.n_pad)) ||
+  if ((rc = dalloc(g, (char**)&g->x, xbytes)) || (rc = dalloc(g, &g->lab, Q.n_pad)) ||
+      (rc = dalloc(g, &g->corr, Q.n_pad)) ||
       (rc = dalloc(g, &g->D, (size_t)Q.n_pad * Q.n_pad)) ||
       (rc = dalloc(g, &g->tiles, g->n_tiles)) || (rc = dalloc(g, &g->thr, Q.n_pad)) ||
       (rc = dalloc(g, &g->list, g->list_cap)) || (rc = dalloc(g, &g->list_count, 1)))
     return fail(rc);
-  if (Q.algo == ALGO_SURF) {
-    if ((rc = dalloc(g, &g->xT64, (size_t)Q.PW * Q.n_pad))) return fail(rc);
-  } else {
-    if ((rc = dalloc(g, &g->xqT, (size_t)Q.PW * Q.n_pad)) ||
-        (rc = dalloc(g, &g->epsT, (size_t)Q.PW * Q.n_pad)))
-      return fail(rc);
-  }
-  if (Q.algo != ALGO_RELIEFF) {
-    if ((rc = dalloc(g, &g->Wt, (size_t)(g->n_tiles + 1) * kTile * kTile)) ||
-        (rc = dalloc(g, &g->spart, (size_t)g->nseg * Q.PW)))
-      return fail(rc);
-  }
+  if (Q.algo != ALGO_RELIEFF &&
+      (rc = dalloc(g, &g->Wt, (size_t)(g->n_tiles + 1) * kTile * kTile)))
+    return fail(rc);
   trace_mark("plan: hipMalloc");
-  if ((rc = h2d(g, (char*)g->x, (const char*)x, xbytes))) return fail(rc);
-  if (!Q.ranges_ready) {
-    // continuous column ranges measured on the device
-    const size_t esz = x_is_f64 ? 8 : 4;
-    std::vector<char> mn((size_t)Q.p_in * esz), mx((size_t)Q.p_in * esz);
-    if ((rc = column_minmax(g->x, x_is_f64, Q.n, Q.p_in, mn.data(), mx.data(), g->stream)))
-      return fail(rc);
-    std::vector<double> cmin((size_t)Q.pc), cmax((size_t)Q.pc);
-    for (int64_t c = 0; c < Q.pc; c++) {
-      const int64_t col = Q.src_col[c];
-      cmin[c] = x_is_f64 ? ((const double*)mn.data())[col] : (double)((const float*)mn.data())[col];
-      cmax[c] = x_is_f64 ? ((const double*)mx.data())[col] : (double)((const float*)mx.data())[col];
-    }
-    if (finalize_scale(g->P, cmin.data(), cmax.data())) return fail(FS_EINVAL);
-    trace_mark("plan: device ranges");
-  }
-  // histogram shift so that the largest quantised value lands in bin < 4096
-  while ((Q.qmax / std::ldexp(1.0, g->rank_shift)) >= (double)kRankBins) g->rank_shift++;
-  std::vector<double> qs(Q.PW, 0.0);
-  for (int64_t c = 0; c < Q.PW; c++) qs[c] = Q.scale[c] * Q.SC;
   std::vector<int32_t> lab(Q.n_pad, -1);
   std::copy(Q.labels.begin(), Q.labels.end(), lab.begin());
-  if ((rc = h2d(g, g->src_col, Q.src_col.data(), Q.PW)) ||
-      (rc = h2d(g, g->out_pos, Q.out_pos.data(), Q.PW)) ||
-      (rc = h2d(g, g->off, Q.offset.data(), Q.PW)) || (rc = h2d(g, g->qs, qs.data(), Q.PW)) ||
-      (rc = h2d(g, g->scl, Q.scale.data(), Q.PW)) ||
-      (rc = h2d(g, g->dtab_off, Q.dtab_off.data(), Q.PW + 1)) ||
-      (rc = h2d(g, g->dtab, Q.dtab.data(), Q.dtab.size())) ||
+  if ((rc = h2d(g, (char*)g->x, (const char*)x, xbytes)) ||
       (rc = h2d(g, g->lab, lab.data(), Q.n_pad)) ||
       (rc = h2d(g, g->tiles, tl.data(), g->n_tiles)))
     return fail(rc);
-  if (hipStreamSynchronize(g->stream) != hipSuccess) return fail(FS_EHIP);
-  trace_mark("plan: H2D");
+  if ((rc = plan_layout(g))) return fail(rc);
+  trace_mark("plan: H2D + layout");
   *out = g;
   return FS_OK;
+}
+
+int plan_set_features(Plan* g, const Prepared& P) {
+  FS_HIP(hipSetDevice(g->device));
+  g->P = P;
+  return plan_layout(g);
 }
 
 // quantize (+ mean correction terms) and pass 1 (distance tiles)

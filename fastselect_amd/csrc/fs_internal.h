@@ -250,6 +250,9 @@ int column_minmax(const void* dx, int x_is_f64, int64_t n, int64_t p, void* hmin
 struct Plan;
 int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int device,
                 int rank, int world, uint64_t stream);
+// Re-target a plan (resident X, distances storage) to another feature
+// subset: P is the new layout (same samples, labels and algorithm).
+int plan_set_features(Plan* g, const Prepared& P);
 int plan_pass1(Plan* g, double* rowstats_dev);
 int plan_select(Plan* g, const double* rowstats_dev, double* counts_dev);
 int plan_pass2(Plan* g, const double* counts_dev, double* scores_dev);

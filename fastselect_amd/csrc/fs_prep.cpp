@@ -43,7 +43,10 @@ void owned_tiles(int64_t nb, int rank, int world, std::vector<int32_t>& bi,
 int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64_t p_in,
             const int64_t* feat_idx, int64_t n_kept, const float* recip,
             const uint8_t* is_discrete, int n_jobs, int device_ranges) {
-  if (!x || !recip || !is_discrete || n < 2 || p_in < 1) {
+  // x may be NULL only when nothing here reads it: ranges left to the
+  // device and a float32 X (discrete columns coded by their bits)
+  const bool x_needed = !(device_ranges && !x_is_f64);
+  if ((!x && x_needed) || !recip || !is_discrete || n < 2 || p_in < 1) {
     set_error("invalid problem: need x, recip, is_discrete, n >= 2 and p >= 1");
     return -1;
   }

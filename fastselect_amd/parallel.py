@@ -46,9 +46,10 @@ class ShardedMultiSURF:
     HIP kernels.  backend 'cpu': host tensors (use the gloo backend).
     """
 
-    def __init__(self, x, y, recip, is_discrete, use_star=False, backend="gpu", device=0):
+    def __init__(self, x, y, recip, is_discrete, use_star=False, backend="gpu", device=0,
+                 shard=True):
         import torch
-        self.dist, self.rank, self.world = _dist()
+        self.dist, self.rank, self.world = _dist() if shard else (None, 0, 1)
         self.n, self.p = x.shape
         self.backend = backend
         if backend == "gpu":
@@ -64,6 +65,15 @@ class ShardedMultiSURF:
         self.rowstats = torch.zeros(2 * self.n, dtype=f64, device=self.tdev)
         self.counts = torch.zeros(2 * self.n, dtype=f64, device=self.tdev)
         self.scores = torch.zeros(self.p, dtype=f64, device=self.tdev)
+
+    def set_features(self, feat_idx):
+        """Score another feature subset of the resident samples from the next
+        step on (fs_plan_set_features: X stays on the device)."""
+        import torch
+        self.plan.set_features(feat_idx)
+        n_kept = self.plan.n_kept
+        if self.scores.numel() != n_kept:
+            self.scores = torch.zeros(n_kept, dtype=torch.float64, device=self.tdev)
 
     def _allreduce(self, t):
         if self.dist is not None and self.world > 1:

@@ -150,6 +150,16 @@ FS_API int fs_plan_create(fs_plan** plan_out, int backend, int device, const flo
                    int n_jobs, uint64_t stream);
 
 /*
+ * Re-target the plan to another feature subset of the same samples
+ * (feat_idx[n_kept] into the original columns, NULL = all), keeping X and
+ * its column ranges resident: the next pass1/select/pass2 score the subset
+ * exactly as a fresh plan on X[:, feat_idx] would (the reference scores such
+ * subsets through feat_idx, MultiSURF.py:147,256; TuRF refits on them,
+ * TuRF.py:93-115).  The scores vector of pass2 then has n_kept entries.
+ */
+FS_API int fs_plan_set_features(fs_plan* plan, const int64_t* feat_idx, int64_t n_kept);
+
+/*
  * Stage 1: quantise the resident X, compute this rank's distance tiles and
  * write this rank's partial per-row moments to rowstats[2n] (sum D, sum D^2;
  * D in the plan's integer distance unit).  Pointers live in the plan's memory

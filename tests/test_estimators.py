@@ -325,3 +325,32 @@ def test_star_aliases_sklearn_api(name):
     import fastselect_amd as F
     from sklearn.utils.estimator_checks import check_estimator
     check_estimator(getattr(F, name)(backend="cpu"))
+
+
+# ---- TuRF over a resident MultiSURF plan -------------
+
+class _RefitMultiSURF(MultiSURF):
+    """MultiSURF without the resident fast path: TuRF refits on X[:, active]."""
+    _resident_scorer = None
+
+
+@pytest.mark.parametrize("star", [False, True])
+def test_turf_resident_plan_equals_refits(star):
+    X, y = make_classification(n_samples=150, n_features=60, n_informative=6,
+                               random_state=3)
+    X[:, 5] = np.round(X[:, 5])  # a discrete column in the mix
+    kw = dict(n_features_to_select=8, pct_remove=0.2)
+    fast = TuRF(MultiSURF(backend="cpu", use_star=star, discrete_limit=12), **kw).fit(X, y)
+    slow = TuRF(_RefitMultiSURF(backend="cpu", use_star=star, discrete_limit=12), **kw).fit(X, y)
+    assert_array_equal(fast.top_features_, slow.top_features_)
+    assert_allclose(fast.feature_importances_, slow.feature_importances_, rtol=0, atol=1e-7)
+
+
+def test_turf_resident_plan_validates_like_refit():
+    """An int n_features_to_select larger than a later subset raises the
+    base estimator's ValueError in both paths."""
+    X, y = make_classification(n_samples=80, n_features=30, random_state=1)
+    for est in (MultiSURF(backend="cpu", n_features_to_select=25),
+                _RefitMultiSURF(backend="cpu", n_features_to_select=25)):
+        with pytest.raises(ValueError, match="n_features"):
+            TuRF(est, n_features_to_select=5, pct_remove=0.3).fit(X, y)

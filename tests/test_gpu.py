@@ -325,3 +325,50 @@ def test_sklearn_api_compliance_gpu(name):
 
     import fastselect_amd
     check_estimator(getattr(fastselect_amd, name)(backend="gpu"))
+
+
+def test_plan_set_features_matches_fresh_scoring(oracle):
+    """A resident plan re-targeted to feature subsets (fs_plan_set_features)
+    scores each subset as a fresh call with that feat_idx, and as the oracle."""
+    import torch
+
+    from fastselect_amd import _lib
+    X, y = make_classification(n_samples=500, n_features=300, random_state=12)
+    X[:, 7] = np.round(X[:, 7])
+    x = X.astype(np.float32)
+    r = (x.max(0) - x.min(0)).astype(np.float32)
+    recip = (1 / r).astype(np.float32)
+    isd = oracle.is_discrete_mask(x, 10)
+    assert isd[7] and isd.sum() == 1
+    n = x.shape[0]
+    plan = _lib.Plan("gpu", x, y, recip, isd, use_star=True)
+    rng = np.random.default_rng(0)
+    for size in (300, 250, 130, 64, 3):
+        fidx = np.sort(rng.choice(300, size, replace=False)) if size < 300 else None
+        plan.set_features(fidx)
+        rs = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
+        cn = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
+        sc = torch.zeros(plan.n_kept, dtype=torch.float64, device="cuda")
+        plan.pass1(rs.data_ptr())
+        plan.select(rs.data_ptr(), cn.data_ptr())
+        plan.pass2(cn.data_ptr(), sc.data_ptr())
+        got = (sc / n).float().cpu().numpy()
+        fresh = _lib.multisurf_score("gpu", x, y, recip, fidx, True, isd)
+        assert scale_rel_err(got, fresh) < 1e-6
+        ref = oracle.multisurf_scores(X, y, use_star=True, feat_idx=fidx, discrete_limit=10)
+        assert_parity(got, ref, TOL)
+    plan.close()
+
+
+def test_turf_resident_gpu_equals_refits():
+    from fastselect_amd import TuRF, MultiSURF
+
+    class Refit(MultiSURF):
+        _resident_scorer = None
+
+    X, y = make_classification(n_samples=400, n_features=200, n_informative=10, random_state=2)
+    kw = dict(n_features_to_select=10, pct_remove=0.25)
+    fast = TuRF(MultiSURF(backend="gpu"), **kw).fit(X, y)
+    slow = TuRF(Refit(backend="gpu"), **kw).fit(X, y)
+    np.testing.assert_array_equal(fast.top_features_, slow.top_features_)
+    np.testing.assert_allclose(fast.feature_importances_, slow.feature_importances_, atol=1e-7)
