@@ -27,6 +27,8 @@ CONFIGS = {
     "cfg4": dict(algo="multisurf", n=20000, p=20000, R=100),
     "cfg5s": dict(algo="surf", n=10000, p=50000, R=100, star=True),
     "cfg5m": dict(algo="multisurf", n=10000, p=50000, R=100, star=True),
+    # TuRF over MultiSURF on cfg2's data: device-resident re-targeting vs refits
+    "turf2": dict(algo="turf", n=5000, p=5000, R=100),
 }
 
 
@@ -52,6 +54,20 @@ def main():
         recip = (1 / r).astype(np.float32)
         isd = np.zeros(p, bool)
         star = c.get("star", False)
+        if c["algo"] == "turf":
+            import fastselect_amd as F
+
+            class Refit(F.MultiSURF):
+                _resident_scorer = None
+
+            out = {"config": name, **c, "data_s": t_data}
+            for label, base in (("resident", F.MultiSURF), ("refit", Refit)):
+                t0 = time.perf_counter()
+                tf = F.TuRF(base(backend="gpu"), n_features_to_select=10, pct_remove=0.1).fit(X, y)
+                out[f"{label}_s"] = time.perf_counter() - t0
+                out[f"{label}_top"] = tf.top_features_.tolist()
+            print(json.dumps(out), flush=True)
+            continue
         times = []
         for _ in range(args.repeat):
             t0 = time.perf_counter()
