@@ -553,13 +553,25 @@ __global__ void k_thr_ms(const double* __restrict__ rowstats, const double* __re
 // SURF: avg_i = float32 sequential sum over j (self included, D_ii = 0) of
 // the float32 distance row, / (n - 1) in float64 (SURF.py:146-163).  Thread
 // i walks column i of the symmetric D so a wave's loads are coalesced.
-__global__ __launch_bounds__(256) void k_surf_avg(const double* __restrict__ D, int64_t n,
-                                                  int64_t n_pad, double inv_sc,
-                                                  double* __restrict__ avg) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+// One lane per row; D is symmetric, so lane i reads column i (coalesced
+// across lanes).  The float32 sum stays strictly sequential in j (the
+// reference's order); 16 loads are issued ahead of the adds that use them.
+__global__ __launch_bounds__(64) void k_surf_avg(const double* __restrict__ D, int64_t n,
+                                                 int64_t n_pad, double inv_sc,
+                                                 double* __restrict__ avg) {
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= n) return;
+  constexpr int kU = 16;
   float s = 0.0f;
-  for (int64_t j = 0; j < n; j++) s += (float)(D[j * n_pad + i] * inv_sc);
+  int64_t j = 0;
+  for (; j + kU <= n; j += kU) {
+    double v[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) v[u] = D[(j + u) * n_pad + i];
+#pragma unroll
+    for (int u = 0; u < kU; u++) s += (float)(v[u] * inv_sc);
+  }
+  for (; j < n; j++) s += (float)(D[j * n_pad + i] * inv_sc);
   avg[i] = (double)s / (double)(n - 1);
 }
 
@@ -1815,8 +1827,8 @@ int surf_run(const Prepared& P, const void* x, int device, float* scores_out) {
   int rc = dalloc(g, &sc, Q.n_kept);
   if (rc == FS_OK) rc = run_quantize_dist(g);  // float64 distances, real units
   if (rc == FS_OK) {
-    k_surf_avg<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, 1.0,
-                                                                    g->thr);
+    k_surf_avg<<<(unsigned)((Q.n + 63) / 64), 64, 0, g->stream>>>(g->D, Q.n, Q.n_pad, 1.0,
+                                                                  g->thr);
     rc = launch_check("k_surf_avg");
   }
   if (rc == FS_OK) {
