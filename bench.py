@@ -1,6 +1,6 @@
 """Benchmark: MultiSURF feature scoring on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--n 20000 --p 20000]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--samples 20000 --features 20000]
 
 For N > 1 launch one process per GPU with torch.distributed.run; the pair
 tiles are sharded round-robin over the ranks and the three small exchange
@@ -102,11 +102,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=20000)
-    ap.add_argument("--p", type=int, default=20000)
+    ap.add_argument("--samples", type=int, default=20000)
+    ap.add_argument("--features", type=int, default=20000)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--star", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; "
+                         "gloo only to rehearse several ranks on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -117,21 +120,25 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    # one GPU per local rank; ranks beyond the visible GPUs share them (only
+    # meaningful for a gloo rehearsal)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     t0 = time.perf_counter()
-    x, y = make_data(args.n, args.p, args.seed)
+    x, y = make_data(args.samples, args.features, args.seed)
     ranges = (x.max(axis=0) - x.min(axis=0)).astype(np.float32)
     ranges[ranges == 0] = 1
     recip = (1.0 / ranges).astype(np.float32)
     # make_classification columns are continuous; the estimator's np.unique
     # discrete detection (host, ~2 s here) is part of fit(), not of a step
-    is_disc = np.zeros(args.p, dtype=bool)
-    log(f"rank {rank}/{world}: data {args.n}x{args.p} ready in {time.perf_counter() - t0:.1f} s")
+    is_disc = np.zeros(args.features, dtype=bool)
+    log(f"rank {rank}/{world}: data {args.samples}x{args.features} ready in {time.perf_counter() - t0:.1f} s")
 
     job = ShardedMultiSURF(x, y, recip, is_disc, use_star=args.star, backend="gpu", device=local)
     tiles, _, _ = job.info()
@@ -166,20 +173,20 @@ def main():
     # pairs x features / world (padding and the duplicated half of diagonal
     # tiles are executed but not counted).
     d_ms, s_ms = float(np.mean(dist_ms)), float(np.mean(score_ms))
-    pfe_launch = args.n * (args.n - 1) / 2.0 * args.p / world
+    pfe_launch = args.samples * (args.samples - 1) / 2.0 * args.features / world
     kern = {"k_dist": d_ms, "k_score": s_ms}
     dom = max(kern, key=kern.get)
     achieved = FLOP_PER_PFE * pfe_launch / (kern[dom] * 1e-3) / 1e12
     # algorithmic bytes one launch moves from HBM/L2 into the CUs: both row
     # panels of every owned tile once (+ D write for k_dist, Wt read for k_score)
-    alg_bytes = {"k_dist": tiles * (2 * 128 * args.p * 4 + 2 * 128 * 128 * 8),
-                 "k_score": tiles * (2 * 128 * args.p * 4 + 128 * 128 * 4)}
-    traffic, traffic_src = pmc_traffic(dom, args.n, args.p, world)
+    alg_bytes = {"k_dist": tiles * (2 * 128 * args.features * 4 + 2 * 128 * 128 * 8),
+                 "k_score": tiles * (2 * 128 * args.features * 4 + 128 * 128 * 4)}
+    traffic, traffic_src = pmc_traffic(dom, args.samples, args.features, world)
 
     if rank == 0:
         out = {
             "metric": "feature-scores/sec (n*p/s) MultiSURF fp32",
-            "value": args.n * args.p / (ms_per_step * 1e-3),
+            "value": args.samples * args.features / (ms_per_step * 1e-3),
             "unit": "feature-scores/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -192,10 +199,12 @@ def main():
             "arith": "pass 1: u32 integer L1 distances (exact); pass 2: f32 diffs x f32 pair "
                      "weights, f64 accumulation",
             "data": "synthetic make_classification(n_informative=20, n_redundant=100, random_state=42)",
-            "config": {"workload": f"MultiSURF{'*' if args.star else ''} n={args.n} p={args.p} "
-                                   f"(BASELINE configs[3])",
-                       "n_samples": args.n, "n_features": args.p,
-                       "parallelism": f"pair-tile shard x{world}, RCCL all-reduce"},
+            "config": {"workload": f"MultiSURF{'*' if args.star else ''} n={args.samples} "
+                                   f"p={args.features} (BASELINE configs[3])",
+                       "n_samples": args.samples, "n_features": args.features,
+                       "parallelism": f"pair-tile shard x{world}, "
+                                      f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend}"
+                                      f" all-reduce"},
             "roofline": {
                 "bound": "valu", "kernel": dom, "achieved": achieved,
                 "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / VALU_PEAK_TFLOPS,

@@ -372,3 +372,37 @@ def test_turf_resident_gpu_equals_refits():
     slow = TuRF(Refit(backend="gpu"), **kw).fit(X, y)
     np.testing.assert_array_equal(fast.top_features_, slow.top_features_)
     np.testing.assert_allclose(fast.feature_importances_, slow.feature_importances_, atol=1e-7)
+
+
+def _two_rank_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fastselect_amd.parallel import multisurf_scores
+    X, y = make_classification(n_samples=900, n_features=400, random_state=7)
+    s = multisurf_scores(X, y, use_star=False, backend="gpu", device=0)
+    np.save(f"{out_path}.{rank}.npy", s)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_share_one_gpu(tmp_path):
+    """The multi-process path with GPU plans: two ranks (both on cuda:0,
+    gloo collectives on device tensors) each compute half the pair tiles;
+    every rank ends with the single-process scores."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from fastselect_amd import MultiSURF
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out = str(tmp_path / "scores")
+    mp.spawn(_two_rank_worker, args=(2, port, out), nprocs=2, join=True)
+    a, b = np.load(out + ".0.npy"), np.load(out + ".1.npy")
+    np.testing.assert_array_equal(a, b)
+    X, y = make_classification(n_samples=900, n_features=400, random_state=7)
+    ref = MultiSURF(backend="gpu").fit(X, y).feature_importances_
+    assert scale_rel_err(a, ref) < 1e-6
