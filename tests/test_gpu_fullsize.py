@@ -1,0 +1,110 @@
+"""Full-size GPU checks at BASELINE.json's configurations, where the oracle
+would take hours: size-independent properties of the exact algorithm.
+
+* determinism: two fits give bit-identical scores;
+* feature-permutation equivariance: permuting X's columns permutes the scores
+  bit for bit (pass-1 distances are exact integers, pass 2 is per feature);
+* class relabelling invariance: hits and misses do not depend on the label
+  values;
+* tile sharding: world-N partials sum to the single-plan scores.
+
+Every test needs the MI355X and runs at cfg3 / cfg4 / cfg5 sizes.
+"""
+import numpy as np
+import pytest
+from conftest import scale_rel_err
+from sklearn.datasets import make_classification
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cfg4():
+    X, y = make_classification(n_samples=20000, n_features=20000, n_informative=20,
+                               n_redundant=100, random_state=42)
+    return X.astype(np.float32), y
+
+
+def _ms(X, y, **kw):
+    from fastselect_amd import MultiSURF
+    est = MultiSURF(backend="gpu", n_features_to_select=10, **kw).fit(X, y)
+    assert est.effective_backend_ == "gpu"
+    return est
+
+
+def test_cfg4_determinism_and_feature_permutation(cfg4):
+    X, y = cfg4
+    a = _ms(X, y)
+    b = _ms(X, y)
+    np.testing.assert_array_equal(a.feature_importances_, b.feature_importances_)
+    perm = np.random.default_rng(0).permutation(X.shape[1])
+    c = _ms(np.ascontiguousarray(X[:, perm]), y)
+    np.testing.assert_array_equal(c.feature_importances_, a.feature_importances_[perm])
+    # the informative block dominates the ranking
+    assert len(set(a.top_features_.tolist())) == 10
+
+
+def test_cfg4_class_relabelling(cfg4):
+    X, y = cfg4
+    a = _ms(X, y)
+    b = _ms(X, np.where(y == 0, 7.5, -3.0))
+    np.testing.assert_array_equal(a.feature_importances_, b.feature_importances_)
+
+
+def test_cfg4_sharded_world4_equals_single(cfg4):
+    import torch
+
+    from fastselect_amd import _lib
+    X, y = cfg4
+    n, p = X.shape
+    r = (X.max(0) - X.min(0)).astype(np.float32)
+    recip = (1 / r).astype(np.float32)
+    isd = np.zeros(p, bool)
+    single = _ms(X, y).feature_importances_
+    world = 4
+    rs_sum = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
+    plans = []
+    for rk in range(world):
+        pl = _lib.Plan("gpu", X, y, recip, isd, rank=rk, world=world)
+        b = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
+        pl.pass1(b.data_ptr())
+        rs_sum += b
+        plans.append(pl)
+    cn_sum = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
+    for pl in plans:
+        b = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
+        pl.select(rs_sum.data_ptr(), b.data_ptr())
+        cn_sum += b
+    sc_sum = torch.zeros(p, dtype=torch.float64, device="cuda")
+    for pl in plans:
+        b = torch.zeros(p, dtype=torch.float64, device="cuda")
+        pl.pass2(cn_sum.data_ptr(), b.data_ptr())
+        sc_sum += b
+        pl.close()
+    torch.cuda.synchronize()
+    sharded = (sc_sum / n).float().cpu().numpy()
+    assert scale_rel_err(sharded, single) < 1e-6
+    assert set(np.argsort(sharded)[::-1][:10]) == set(np.argsort(single)[::-1][:10])
+
+
+def test_cfg3_relieff_determinism_and_relabelling():
+    from fastselect_amd import ReliefF
+    X, y = make_classification(n_samples=20000, n_features=2000, n_informative=20,
+                               n_redundant=50, random_state=42)
+    a = ReliefF(backend="gpu", n_neighbors=10).fit(X, y).feature_importances_
+    b = ReliefF(backend="gpu", n_neighbors=10).fit(X, y).feature_importances_
+    np.testing.assert_array_equal(a, b)
+    # relabelling swaps the class codes (and so the order in which per-class
+    # sums are added): equal up to float64 rounding
+    c = ReliefF(backend="gpu", n_neighbors=10).fit(X, 1 - y).feature_importances_
+    assert scale_rel_err(c, a) < 1e-7
+
+
+def test_cfg5_surf_star_determinism():
+    from fastselect_amd import SURF
+    X, y = make_classification(n_samples=10000, n_features=50000, n_informative=20,
+                               n_redundant=100, random_state=42)
+    a = SURF(backend="gpu", use_star=True).fit(X, y).feature_importances_
+    b = SURF(backend="gpu", use_star=True).fit(X, y).feature_importances_
+    np.testing.assert_array_equal(a, b)
+    assert np.isfinite(a).all() and np.abs(a).max() > 0
