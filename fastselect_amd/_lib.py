@@ -208,7 +208,7 @@ def surf_score(backend, x, y, recip, use_star, is_discrete, n_jobs=-1, device=0)
 class Plan:
     """A sharded MultiSURF plan (``fs_plan_*``) for one rank.
 
-    Exchange buffers (rowstats[2n], counts[2n], scores[n_kept], float64) are
+    Exchange buffers (rowstats[3n], counts[2n], scores[n_kept], float64) are
     passed by address: device pointers for the GPU backend, host pointers for
     the CPU backend (see ``fastselect_amd.parallel``).
     """

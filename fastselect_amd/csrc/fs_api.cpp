@@ -102,7 +102,7 @@ int fs_multisurf_score(int backend, int device, const float* x, int64_t n, int64
   P.use_star = use_star ? 1 : 0;
   if (backend == FS_BACKEND_GPU) return gpu::multisurf_run(P, x, device, scores_out);
   cpu::CpuState st;
-  std::vector<double> rs(2 * n), cnt(2 * n), S(P.n_kept);
+  std::vector<double> rs(3 * n), cnt(2 * n), S(P.n_kept);
   cpu::multisurf_pass1(P, x, 0, 1, n_jobs, st, rs.data());
   cpu::multisurf_select(P, x, 0, 1, rs.data(), n_jobs, st, cnt.data());
   cpu::multisurf_pass2(P, st, cnt.data(), 0, 1, n_jobs, S.data());

@@ -110,14 +110,18 @@ static void distances(const Prepared& P, const std::vector<uint32_t>& xq, int ra
 
 // Mean correction of k_colrank / k_rowcorr: per continuous column a
 // 4096-bin histogram of q gives midranks, corr[i] = sum_c eps*(2 rank-(n-1)).
+// The correction of the continuous columns [c_lo, c_hi) (a rank's share;
+// the shares are summed across ranks with the row moments).
 static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
-                            const std::vector<float>& eps, int n_jobs, std::vector<double>& corr) {
+                            const std::vector<float>& eps, int64_t c_lo, int64_t c_hi,
+                            int n_jobs, std::vector<double>& corr) {
   const int64_t n = P.n;
   constexpr int kBins = 4096;
   int shift = 0;
   while (P.qmax / std::ldexp(1.0, shift) >= (double)kBins) shift++;
   std::vector<float> term((size_t)n * std::max<int64_t>(P.pc, 1), 0.0f);
-  parallel_for(P.pc, n_jobs, [&](int64_t c) {
+  parallel_for(c_hi - c_lo, n_jobs, [&](int64_t cc) {
+    const int64_t c = c_lo + cc;
     std::vector<uint32_t> cum(kBins + 1, 0);
     for (int64_t i = 0; i < n; i++)
       cum[std::min<int64_t>(xq[(size_t)i * P.PW + c] >> shift, kBins - 1) + 1]++;
@@ -132,7 +136,7 @@ static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
   corr.assign(n, 0.0);
   for (int64_t i = 0; i < n; i++) {
     double s = 0.0;
-    for (int64_t c = 0; c < P.pc; c++) s += (double)term[(size_t)i * P.pc + c];
+    for (int64_t c = c_lo; c < c_hi; c++) s += (double)term[(size_t)i * P.pc + c];
     corr[i] = s;
   }
 }
@@ -192,7 +196,7 @@ int multisurf_pass1(const Prepared& P, const void* x, int rank, int world, int n
   std::vector<uint32_t> xq;
   std::vector<float> eps;
   quantize(P, x, 0, n_jobs, xq, S.xs, &eps);
-  mean_correction(P, xq, eps, n_jobs, S.corr);
+  mean_correction(P, xq, eps, P.pc * rank / world, P.pc * (rank + 1) / world, n_jobs, S.corr);
   distances(P, xq, rank, world, n_jobs, S.D);
   const int64_t n = P.n, nb = P.n_pad / kTile;
   parallel_for(n, n_jobs, [&](int64_t i) {
@@ -203,8 +207,9 @@ int multisurf_pass1(const Prepared& P, const void* x, int rank, int world, int n
       s1 += d;
       s2 += d * d;
     }
-    rowstats[2 * i] = s1;
-    rowstats[2 * i + 1] = s2;
+    rowstats[3 * i] = s1;
+    rowstats[3 * i + 1] = s2;
+    rowstats[3 * i + 2] = S.corr[i];
   });
   return FS_OK;
 }
@@ -215,10 +220,10 @@ int multisurf_select(const Prepared& P, const void* x, int rank, int world,
   S.thr.assign(n, 0.0);
   const double nm1 = (double)(n - 1);
   for (int64_t i = 0; i < n; i++) {  // k_thr_ms
-    const double mu = rowstats[2 * i] / nm1;
-    double var = rowstats[2 * i + 1] / nm1 - mu * mu;
+    const double mu = rowstats[3 * i] / nm1;
+    double var = rowstats[3 * i + 1] / nm1 - mu * mu;
     if (var < 0.0) var = 0.0;
-    S.thr[i] = (mu - S.corr[i] / nm1) - 0.5 * std::sqrt(var);
+    S.thr[i] = (mu - rowstats[3 * i + 2] / nm1) - 0.5 * std::sqrt(var);
   }
   const double dq = P.amb_delta * P.SC;
   S.refined = refine_pairs(P, x, 0, rank, world, n_jobs, S.D, [&](int64_t i, int64_t j, double d) {

@@ -8,7 +8,7 @@
 //                   workgroup, 8x8 pairs per lane, v_sad_u32 over LDS
 //                   panels staged with global_load_lds (double-buffered),
 //                   exact integer distances.                         VALU-bound
-//   k_rowstats      per-row sum D, sum D^2 over owned tiles.         HBM-bound
+//   k_tile_rowstats per-row sum D, sum D^2 over owned tiles (+ reduce). HBM-bound
 //   k_select_ms     MultiSURF thresholds + near hit / miss counts.   HBM-bound
 //   k_surf_avg      SURF float32 sequential row mean (SURF.py:162).  HBM-bound
 //   k_weights       symmetric pair weights w_ij = W_ij + W_ji per tile.
@@ -74,13 +74,6 @@ __device__ __forceinline__ uint32_t mismatch_u32(uint32_t a, uint32_t b, uint32_
   return d;
 }
 
-__device__ __forceinline__ bool tile_owned(int64_t nb, int64_t bi, int64_t bj, int rank,
-                                           int world) {
-  if (world == 1) return true;
-  const int64_t a = bi < bj ? bi : bj, b = bi < bj ? bj : bi;
-  return tile_linear(nb, a, b) % world == rank;
-}
-
 // Fixed-shape block reduction of doubles (256 threads), deterministic.
 __device__ __forceinline__ double block_sum_256(double v, double* red) {
   const int tid = threadIdx.x;
@@ -104,7 +97,8 @@ __global__ __launch_bounds__(256) void k_quantize(
     const int64_t* __restrict__ src_col, const double* __restrict__ off,
     const double* __restrict__ qs, const double* __restrict__ scl,
     const int64_t* __restrict__ dtab_off, const double* __restrict__ dtab, int disc_bits,
-    uint32_t* __restrict__ xqT, float* __restrict__ xs, float* __restrict__ epsT) {
+    int64_t eps_lo, int64_t eps_hi, uint32_t* __restrict__ xqT, float* __restrict__ xs,
+    float* __restrict__ epsT) {
   __shared__ uint32_t tile[64][65];
   __shared__ float etile[64][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -149,7 +143,8 @@ __global__ __launch_bounds__(256) void k_quantize(
   __syncthreads();
   for (int r = ty; r < 64; r += 4) {
     xqT[(c0 + r) * n_pad + i0 + tx] = tile[tx][r];
-    epsT[(c0 + r) * n_pad + i0 + tx] = etile[tx][r];
+    // quantisation errors only for this rank's share of the correction
+    if (c0 + r >= eps_lo && c0 + r < eps_hi) epsT[(c0 + r) * n_pad + i0 + tx] = etile[tx][r];
   }
 }
 
@@ -162,11 +157,11 @@ __global__ __launch_bounds__(256) void k_quantize(
 // float32 rounding.  In place: epsT[c][i] <- eps * (2 rank - (n-1)).
 constexpr int kRankBins = 4096;
 __global__ __launch_bounds__(256) void k_colrank(const uint32_t* __restrict__ xqT, int64_t n,
-                                                 int64_t n_pad, int shift,
+                                                 int64_t n_pad, int shift, int64_t c_lo,
                                                  float* __restrict__ epsT) {
   __shared__ uint32_t hist[kRankBins];
   __shared__ uint32_t wsum[4];
-  const int64_t c = blockIdx.x;
+  const int64_t c = c_lo + blockIdx.x;
   const uint32_t* q = xqT + c * n_pad;
   float* e = epsT + c * n_pad;
   for (int b = threadIdx.x; b < kRankBins; b += 256) hist[b] = 0;
@@ -207,18 +202,19 @@ __global__ __launch_bounds__(256) void k_colrank(const uint32_t* __restrict__ xq
   }
 }
 
-// corr[i] = sum over continuous columns of the per-feature bias terms.
+// corr[i] = sum over continuous columns [c_lo, c_hi) (this rank's share) of
+// the per-feature bias terms.
 // Workgroup = 64 rows x 16 waves; wave w sums columns w, w+16, ... (one
 // coalesced 256-byte read per column), then the 16 partials are added in a
 // fixed order (deterministic).
 __global__ __launch_bounds__(1024) void k_rowcorr(const float* __restrict__ epsT, int64_t n,
-                                                  int64_t n_pad, int64_t pc,
+                                                  int64_t n_pad, int64_t c_lo, int64_t c_hi,
                                                   double* __restrict__ corr) {
   __shared__ double part[16][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + lane;  // < n_pad
   double s = 0.0;
-  for (int64_t c = wave; c < pc; c += 16) s += (double)epsT[c * n_pad + i];
+  for (int64_t c = c_lo + wave; c < c_hi; c += 16) s += (double)epsT[c * n_pad + i];
   part[wave][lane] = s;
   __syncthreads();
   if (wave == 0 && i < n) {
@@ -263,10 +259,15 @@ __device__ __forceinline__ void dist_chunk(const uint32_t* __restrict__ A,
   }
 }
 
+// K-split: with splits > 1 workgroup b computes tile b / splits over the
+// chunk range of part b % splits; part 0 writes D, part s the partial buffer
+// Dpart[s - 1] (k_dist_merge adds them).  A rank that owns few tiles (N-GPU
+// runs) thus fills the chip's 2 x CU workgroup slots in more even rounds.
 __global__ __launch_bounds__(256, 2) void k_dist(const uint32_t* __restrict__ xqT, int64_t n_pad,
                                                  int nck_cont, int nck_disc, uint32_t sc_disc,
-                                                 const int2* __restrict__ tiles,
-                                                 double* __restrict__ D) {
+                                                 const int2* __restrict__ tiles, int splits,
+                                                 double* __restrict__ D,
+                                                 double* __restrict__ Dpart) {
   // Two distinct LDS objects (not one indexed array) so the compiler can
   // prove a pending global_load_lds into one buffer does not alias the
   // ds_reads of the other and keeps the copy in flight across the compute.
@@ -275,9 +276,11 @@ __global__ __launch_bounds__(256, 2) void k_dist(const uint32_t* __restrict__ xq
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int2 tl = tiles[blockIdx.x];
+  const int part = (int)(blockIdx.x % (unsigned)splits);
+  const int2 tl = tiles[blockIdx.x / (unsigned)splits];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
   const int tx = tid & 15, ty = tid >> 4;
+  if (part > 0) D = Dpart + (int64_t)(part - 1) * n_pad * n_pad;
 
   uint32_t acc[8][8];
   uint32_t hi[8][4];
@@ -330,10 +333,14 @@ __global__ __launch_bounds__(256, 2) void k_dist(const uint32_t* __restrict__ xq
     __syncthreads();
   };
 
-  const int nck = nck_cont + nck_disc;
-  stage(ldsA0, ldsB0, 0);
-  __syncthreads();
-  for (int ck = 0; ck < nck; ck += 2) {
+  const int nck_all = nck_cont + nck_disc;
+  const int c_begin = (int)((int64_t)nck_all * part / splits);
+  const int nck = (int)((int64_t)nck_all * (part + 1) / splits);  // end of this part
+  if (c_begin < nck) {
+    stage(ldsA0, ldsB0, c_begin);
+    __syncthreads();
+  }
+  for (int ck = c_begin; ck < nck; ck += 2) {
     step(ldsA0, ldsB0, ldsA1, ldsB1, ck, nck);
     if (ck + 1 < nck) step(ldsA1, ldsB1, ldsA0, ldsB0, ck + 1, nck);
   }
@@ -386,6 +393,24 @@ __global__ __launch_bounds__(256, 2) void k_dist(const uint32_t* __restrict__ xq
 // 16-feature panel is 16 KB (one k-row = one 1 KB global_load_lds_dwordx4).
 // 512 lanes per tile: lane (tx, ty) = (tid % 32, tid / 32) owns rows
 // {ty*4 + r, 64 + ty*4 + r} x cols {tx*4 + c} (8 x 4 float64 accumulators).
+// D += sum of the K-split partials over the owned tiles, both halves
+// (integer-valued doubles: exact in any order).
+__global__ __launch_bounds__(256) void k_dist_merge(double* __restrict__ D,
+                                                   const double* __restrict__ Dpart, int nparts,
+                                                   const int2* __restrict__ tiles, int64_t n_pad) {
+  const int2 tl = tiles[blockIdx.x];
+  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  const int64_t plane = n_pad * n_pad;
+  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
+    const int64_t r = e / kTile, c = e % kTile;
+    const int64_t a = (i0 + r) * n_pad + j0 + c, b = (j0 + c) * n_pad + i0 + r;
+    double v = D[a];
+    for (int s = 0; s < nparts; s++) v += Dpart[s * plane + a];
+    D[a] = v;
+    if (tl.x != tl.y) D[b] = v;
+  }
+}
+
 template <bool DISC>
 __device__ __forceinline__ void dist_chunk_f64(const double* __restrict__ A,
                                                const double* __restrict__ B, int tx, int ty,
@@ -515,39 +540,73 @@ __global__ __launch_bounds__(256) void k_quantize_f64(
 // ---------------------------------------------------------------------------
 // MultiSURF row statistics, thresholds and neighbour counts
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_rowstats(const double* __restrict__ D, int64_t n,
-                                                  int64_t n_pad, int rank, int world,
-                                                  double* __restrict__ rowstats) {
-  __shared__ double red[256];
-  const int64_t i = blockIdx.x;
-  const int64_t nb = n_pad / kTile, bi = i / kTile;
-  const double* row = D + i * n_pad;
+// Per-row distance moments from the owned tiles only.  k_tile_rowstats:
+// one workgroup per owned tile; lanes 0..127 sum row i0 + r over the tile's
+// 128 columns (reading the symmetric mirror D[j][i], coalesced), lanes
+// 128..255 sum row j0 + c over its 128 rows (off-diagonal tiles only) ->
+// part[t][256][2].  k_rowstats_reduce adds a row's tile partials in tile
+// order (deterministic) and appends this rank's mean correction:
+// rowstats[3i] = sum D, [3i+1] = sum D^2, [3i+2] = corr share.
+__global__ __launch_bounds__(256) void k_tile_rowstats(const double* __restrict__ D, int64_t n,
+                                                       int64_t n_pad,
+                                                       const int2* __restrict__ tiles,
+                                                       double2* __restrict__ part) {
+  const int2 tl = tiles[blockIdx.x];
+  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  const int tid = threadIdx.x;
+  const bool rows = tid < kTile;
+  const int r = tid & (kTile - 1);
   double s1 = 0.0, s2 = 0.0;
-  for (int64_t j = threadIdx.x; j < n; j += 256) {
-    if (j == i || !tile_owned(nb, bi, j / kTile, rank, world)) continue;
-    const double d = row[j];
-    s1 += d;
-    s2 += d * d;
+  if (rows || tl.x != tl.y) {
+    // rows: row i = i0 + r over columns j0 + c (read D[j][i]);
+    // cols: row j = j0 + r over rows i0 + c (read D[i][j])
+    const int64_t self = rows ? i0 + r : j0 + r;
+    const int64_t other0 = rows ? j0 : i0;
+    if (self < n) {
+      for (int c = 0; c < kTile; c++) {
+        const int64_t o = other0 + c;
+        if (o >= n || o == self) continue;
+        const double d = D[o * n_pad + self];
+        s1 += d;
+        s2 += d * d;
+      }
+    }
   }
-  s1 = block_sum_256(s1, red);
-  s2 = block_sum_256(s2, red);
-  if (threadIdx.x == 0) {
-    rowstats[2 * i] = s1;
-    rowstats[2 * i + 1] = s2;
+  part[(int64_t)blockIdx.x * 256 + tid] = make_double2(s1, s2);
+}
+
+__global__ void k_rowstats_reduce(const double2* __restrict__ part, int64_t n, int64_t nb,
+                                  int rank, int world, const double* __restrict__ corr,
+                                  double* __restrict__ rowstats) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t b = i / kTile, r = i % kTile;
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t a = 0; a < nb; a++) {
+    const int64_t lo = a < b ? a : b, hi = a < b ? b : a;
+    const int64_t t = tile_linear(nb, lo, hi);
+    if (t % world != rank) continue;
+    // tile (b, a >= b): row block b are its rows; tile (a < b, b): its columns
+    const double2 v = part[(t / world) * 256 + (a >= b ? r : kTile + r)];
+    s1 += v.x;
+    s2 += v.y;
   }
+  rowstats[3 * i] = s1;
+  rowstats[3 * i + 1] = s2;
+  rowstats[3 * i + 2] = corr[i];
 }
 
 // MultiSURF threshold (integer units): the quantised mean corrected by
 // corr[i]/(n-1), minus half the quantised spread (MultiSURF.py:193-196).
-__global__ void k_thr_ms(const double* __restrict__ rowstats, const double* __restrict__ corr,
-                         int64_t n, double* __restrict__ thr) {
+__global__ void k_thr_ms(const double* __restrict__ rowstats, int64_t n,
+                         double* __restrict__ thr) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const double nm1 = (double)(n - 1);
-  const double mu = rowstats[2 * i] / nm1;
-  double var = rowstats[2 * i + 1] / nm1 - mu * mu;
+  const double mu = rowstats[3 * i] / nm1;
+  double var = rowstats[3 * i + 1] / nm1 - mu * mu;
   if (var < 0.0) var = 0.0;
-  thr[i] = (mu - corr[i] / nm1) - 0.5 * __builtin_sqrt(var);
+  thr[i] = (mu - rowstats[3 * i + 2] / nm1) - 0.5 * __builtin_sqrt(var);
 }
 
 // SURF: avg_i = float32 sequential sum over j (self included, D_ii = 0) of
@@ -659,31 +718,37 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
 
 // Near hit / miss counts over the owned tiles (D now exact for ambiguous
 // pairs): counts[2i], counts[2i+1].
-__global__ __launch_bounds__(256) void k_count_ms(const double* __restrict__ D, int64_t n,
-                                                  int64_t n_pad, int rank, int world,
-                                                  const int32_t* __restrict__ lab,
-                                                  const double* __restrict__ thr,
-                                                  double* __restrict__ counts) {
-  __shared__ double red[256];
-  const int64_t i = blockIdx.x;
-  const int64_t nb = n_pad / kTile, bi = i / kTile;
-  const double t = thr[i];
-  const int32_t li = lab[i];
-  const double* row = D + i * n_pad;
+__global__ __launch_bounds__(256) void k_tile_counts(const double* __restrict__ D, int64_t n,
+                                                     int64_t n_pad,
+                                                     const int2* __restrict__ tiles,
+                                                     const int32_t* __restrict__ lab,
+                                                     const double* __restrict__ thr,
+                                                     double* __restrict__ counts) {
+  // Near hits / misses over the owned tiles (D exact for ambiguous pairs by
+  // now), same lane layout as k_tile_rowstats; counts are integers, so the
+  // atomic adds are exact in any order (counts zeroed by the caller).
+  const int2 tl = tiles[blockIdx.x];
+  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  const int tid = threadIdx.x;
+  const bool rows = tid < kTile;
+  if (!rows && tl.x == tl.y) return;
+  const int r = tid & (kTile - 1);
+  const int64_t self = rows ? i0 + r : j0 + r;
+  const int64_t other0 = rows ? j0 : i0;
+  if (self >= n) return;
+  const double t = thr[self];
+  const int32_t ls = lab[self];
   double h = 0.0, m = 0.0;
-  for (int64_t j = threadIdx.x; j < n; j += 256) {
-    if (j == i || !tile_owned(nb, bi, j / kTile, rank, world)) continue;
-    if (row[j] < t) {
-      if (lab[j] == li) h += 1.0;
+  for (int c = 0; c < kTile; c++) {
+    const int64_t o = other0 + c;
+    if (o >= n || o == self) continue;
+    if (D[o * n_pad + self] < t) {
+      if (lab[o] == ls) h += 1.0;
       else m += 1.0;
     }
   }
-  h = block_sum_256(h, red);
-  m = block_sum_256(m, red);
-  if (threadIdx.x == 0) {
-    counts[2 * i] = h;
-    counts[2 * i + 1] = m;
-  }
+  if (h != 0.0) atomicAdd(&counts[2 * self], h);
+  if (m != 0.0) atomicAdd(&counts[2 * self + 1], m);
 }
 
 // ---------------------------------------------------------------------------
@@ -1403,6 +1468,10 @@ struct Plan {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   int64_t nb = 0, n_tiles = 0, seg_len = 1, nseg = 1;
+  int ksplit = 1;               // pass-1 K-split parts (k_dist)
+  int64_t c_lo = 0, c_hi = 0;   // this rank's continuous columns of the mean correction
+  double2* rspart = nullptr;    // per owned tile row-moment partials [tiles][256]
+  double* Dpart = nullptr;      // (ksplit - 1) partial distance planes
   int rank_shift = 0;
   // device buffers
   void* x = nullptr;
@@ -1486,6 +1555,34 @@ void plan_destroy(Plan* g) {
   trace_mark("plan: free");
 }
 
+// Pass-1 K-split: k_dist runs 2 workgroups per CU, so T tiles take
+// ceil(T / slots) rounds; splitting every tile's feature range into S parts
+// evens out the last round when a rank owns few tiles (N-GPU runs).  The
+// merge streams (S + 2) tile planes (~66.5 / p of the tile's compute time
+// each); S > 1 only when it gains at least 3%.
+static int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats) {
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      cus <= 0) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  const double slots = 2.0 * cus;
+  auto eff = [&](int sp) {
+    const double rounds = (double)tiles * sp / slots;
+    const double merge = sp > 1 ? (sp + 2) * 66.5 / (double)(feats > 0 ? feats : 1) : 0.0;
+    return rounds / std::ceil(rounds) - merge;
+  };
+  int best = 1;
+  double best_eff = eff(1) + 0.03;
+  for (int sp = 2; sp <= 4 && sp <= nchunks; sp++)
+    if (eff(sp) > best_eff) {
+      best_eff = eff(sp);
+      best = sp;
+    }
+  return best;
+}
+
 // Feature-layout part of a plan: everything sized by the kept features
 // (permutation tables, quantised operands, pass-2 partials), rebuilt when
 // the plan is re-targeted to another feature subset (fs_plan_set_features).
@@ -1518,6 +1615,8 @@ static int plan_layout(Plan* g) {
     }
     if (finalize_scale(Q, cmin.data(), cmax.data())) return FS_EINVAL;
   }
+  g->c_lo = Q.pc * g->rank / g->world;
+  g->c_hi = Q.pc * (g->rank + 1) / g->world;
   const int64_t nfb = (Q.PW + 127) / 128;
   // ~64k pass-2 workgroups: enough to fill 256 CUs and bound tail imbalance.
   g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + 65535) / 65536);
@@ -1600,6 +1699,8 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   std::vector<int2> tl(g->n_tiles);
   for (int64_t t = 0; t < g->n_tiles; t++) tl[t] = make_int2(bi[t], bj[t]);
   g->list_cap = std::max<int64_t>(1 << 16, Q.n * 64);
+  g->ksplit = choose_ksplit(g->n_tiles, device, (int)((Q.PC + Q.PD) / kBK), Q.pc + Q.pd);
+  if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
   const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
   int rc;
   trace_mark("plan: host setup");
@@ -1612,6 +1713,10 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   if (Q.algo != ALGO_RELIEFF &&
       (rc = dalloc(g, &g->Wt, (size_t)(g->n_tiles + 1) * kTile * kTile)))
     return fail(rc);
+  if (g->ksplit > 1 &&
+      (rc = dalloc(g, &g->Dpart, (size_t)(g->ksplit - 1) * Q.n_pad * Q.n_pad)))
+    return fail(rc);
+  if ((rc = dalloc(g, &g->rspart, (size_t)std::max<int64_t>(g->n_tiles, 1) * 256))) return fail(rc);
   trace_mark("plan: hipMalloc");
   std::vector<int32_t> lab(Q.n_pad, -1);
   std::copy(Q.labels.begin(), Q.labels.end(), lab.begin());
@@ -1653,28 +1758,35 @@ static int run_quantize_dist(Plan* g) {
   if (g->x_is_f64)
     k_quantize<double><<<gq, 256, 0, g->stream>>>(
         (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, g->src_col, g->off, g->qs, g->scl,
-        g->dtab_off, g->dtab, Q.disc_bits, g->xqT, g->xs, g->epsT);
+        g->dtab_off, g->dtab, Q.disc_bits, g->c_lo, g->c_hi, g->xqT, g->xs, g->epsT);
   else
     k_quantize<float><<<gq, 256, 0, g->stream>>>(
         (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, g->src_col, g->off, g->qs, g->scl,
-        g->dtab_off, g->dtab, Q.disc_bits, g->xqT, g->xs, g->epsT);
+        g->dtab_off, g->dtab, Q.disc_bits, g->c_lo, g->c_hi, g->xqT, g->xs, g->epsT);
   FS_TRY(launch_check("k_quantize"));
   if (Q.algo == ALGO_MULTISURF) {
-    if (Q.pc > 0) {
-      k_colrank<<<(unsigned)Q.pc, 256, 0, g->stream>>>(g->xqT, Q.n, Q.n_pad, g->rank_shift,
-                                                       g->epsT);
+    // mean correction of this rank's feature share (summed across ranks
+    // with the row moments)
+    if (g->c_hi > g->c_lo) {
+      k_colrank<<<(unsigned)(g->c_hi - g->c_lo), 256, 0, g->stream>>>(
+          g->xqT, Q.n, Q.n_pad, g->rank_shift, g->c_lo, g->epsT);
       FS_TRY(launch_check("k_colrank"));
     }
-    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, g->stream>>>(g->epsT, Q.n, Q.n_pad, Q.pc,
-                                                                 g->corr);
+    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, g->stream>>>(g->epsT, Q.n, Q.n_pad, g->c_lo,
+                                                                 g->c_hi, g->corr);
     FS_TRY(launch_check("k_rowcorr"));
   }
   if (g->n_tiles > 0) {
     FS_HIP(hipEventRecord(g->ev[0], g->stream));
-    k_dist<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->xqT, Q.n_pad, (int)(Q.PC / kBK),
-                                                          (int)(Q.PD / kBK), Q.SCu, g->tiles,
-                                                          g->D);
+    k_dist<<<(unsigned)(g->n_tiles * g->ksplit), 256, 0, g->stream>>>(
+        g->xqT, Q.n_pad, (int)(Q.PC / kBK), (int)(Q.PD / kBK), Q.SCu, g->tiles, g->ksplit, g->D,
+        g->Dpart);
     FS_TRY(launch_check("k_dist"));
+    if (g->ksplit > 1) {
+      k_dist_merge<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, g->Dpart, g->ksplit - 1,
+                                                                g->tiles, Q.n_pad);
+      FS_TRY(launch_check("k_dist_merge"));
+    }
     FS_HIP(hipEventRecord(g->ev[1], g->stream));
   }
   return FS_OK;
@@ -1733,9 +1845,14 @@ static int run_pass2(Plan* g, double* scores_dev) {
 int plan_pass1(Plan* g, double* rowstats) {
   const Prepared& Q = g->P;
   FS_TRY(run_quantize_dist(g));
-  k_rowstats<<<(unsigned)Q.n, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->rank, g->world,
-                                                   rowstats);
-  FS_TRY(launch_check("k_rowstats"));
+  if (g->n_tiles > 0) {
+    k_tile_rowstats<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
+                                                                 g->rspart);
+    FS_TRY(launch_check("k_tile_rowstats"));
+  }
+  k_rowstats_reduce<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(
+      g->rspart, Q.n, g->nb, g->rank, g->world, g->corr, rowstats);
+  FS_TRY(launch_check("k_rowstats_reduce"));
   if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
   return FS_OK;
 }
@@ -1743,13 +1860,15 @@ int plan_pass1(Plan* g, double* rowstats) {
 int plan_select(Plan* g, const double* rowstats, double* counts) {
   const Prepared& Q = g->P;
   FS_HIP(hipSetDevice(g->device));
-  k_thr_ms<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(rowstats, g->corr, Q.n,
-                                                                 g->thr);
+  k_thr_ms<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(rowstats, Q.n, g->thr);
   FS_TRY(launch_check("k_thr_ms"));
   FS_TRY(refine_pairs(g, ALGO_MULTISURF, Q.amb_delta * Q.SC));
-  k_count_ms<<<(unsigned)Q.n, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->rank, g->world,
-                                                   g->lab, g->thr, counts);
-  FS_TRY(launch_check("k_count_ms"));
+  FS_HIP(hipMemsetAsync(counts, 0, sizeof(double) * 2 * Q.n, g->stream));
+  if (g->n_tiles > 0) {
+    k_tile_counts<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
+                                                               g->lab, g->thr, counts);
+    FS_TRY(launch_check("k_tile_counts"));
+  }
   if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
   return FS_OK;
 }
@@ -1808,7 +1927,7 @@ int multisurf_run(const Prepared& P, const void* x, int device, float* scores_ou
   FS_TRY(plan_create(&g, P, x, 0, device, 0, 1, 0));
   double *rs = nullptr, *cnt = nullptr, *sc = nullptr;
   int rc;
-  if ((rc = dalloc(g, &rs, 2 * P.n)) || (rc = dalloc(g, &cnt, 2 * P.n)) ||
+  if ((rc = dalloc(g, &rs, 3 * P.n)) || (rc = dalloc(g, &cnt, 2 * P.n)) ||
       (rc = dalloc(g, &sc, P.n_kept)) || (rc = plan_pass1(g, rs)) ||
       (rc = plan_select(g, rs, cnt)) || (rc = plan_pass2(g, cnt, sc)) ||
       (rc = finish_scores(g, sc, scores_out))) {

@@ -6,7 +6,7 @@ the ranks (tile t -> rank t % world), every rank holds all of X, and the path
 has exactly three exchange points, each a SUM all-reduce of a small float64
 vector (RCCL over xGMI with the 'nccl' backend, gloo on CPU):
 
-    pass1  -> rowstats[2n]  (sum D, sum D^2 per sample)
+    pass1  -> rowstats[3n]  (sum D, sum D^2, mean-correction share per sample)
     select -> counts[2n]    (near hits, near misses)
     pass2  -> scores[p]     (per-feature score sums)
 
@@ -62,7 +62,7 @@ class ShardedMultiSURF:
         self.plan = _lib.Plan(backend, x, y, recip, is_discrete, use_star=use_star,
                               rank=self.rank, world=self.world, device=device, stream=stream)
         f64 = torch.float64
-        self.rowstats = torch.zeros(2 * self.n, dtype=f64, device=self.tdev)
+        self.rowstats = torch.zeros(3 * self.n, dtype=f64, device=self.tdev)
         self.counts = torch.zeros(2 * self.n, dtype=f64, device=self.tdev)
         self.scores = torch.zeros(self.p, dtype=f64, device=self.tdev)
 

@@ -161,13 +161,13 @@ FS_API int fs_plan_set_features(fs_plan* plan, const int64_t* feat_idx, int64_t 
 
 /*
  * Stage 1: quantise the resident X, compute this rank's distance tiles and
- * write this rank's partial per-row moments to rowstats[2n] (sum D, sum D^2;
- * D in the plan's integer distance unit).  Pointers live in the plan's memory
+ * write this rank's partials to rowstats[3n]: per row sum D, sum D^2 (D in the
+ * plan's integer distance unit) and this rank's share of the mean correction
+ * (its slice of the continuous features).  Pointers live in the plan's memory
  * space: device memory for the GPU backend, host memory for the CPU backend.
  */
 FS_API int fs_plan_pass1(fs_plan* plan, double* rowstats);
-/* Stage 2: thresholds from the all-reduced rowstats (plus the rank-local mean
- * correction), exact recomputation of this rank's ambiguous pairs (pairs whose
+/* Stage 2: thresholds from the all-reduced rowstats[3n], exact recomputation of this rank's ambiguous pairs (pairs whose
  * quantised distance lies so close to a threshold that the near/far decision
  * is not certain), then partial per-row (near hits, near misses) -> counts[2n]. */
 FS_API int fs_plan_select(fs_plan* plan, const double* rowstats, double* counts);

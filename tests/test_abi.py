@@ -76,7 +76,7 @@ def test_plan_lifecycle_cpu():
     recip = (1 / r).astype(np.float32)
     isd = np.zeros(9, bool)
     pl = _lib.Plan("cpu", x, y, recip, isd)
-    rs, cn, sc = np.zeros(300), np.zeros(300), np.zeros(9)
+    rs, cn, sc = np.zeros(450), np.zeros(300), np.zeros(9)
     pl.pass1(rs.ctypes.data)
     pl.select(rs.ctypes.data, cn.ctypes.data)
     pl.pass2(cn.ctypes.data, sc.ctypes.data)

@@ -285,7 +285,7 @@ def test_sharded_plans_sum_to_single():
     def run(world):
         plans = [_lib.Plan("gpu", x, y, recip, isd, use_star=True, rank=rk, world=world)
                  for rk in range(world)]
-        rs = [torch.zeros(2 * n, dtype=torch.float64, device="cuda") for _ in plans]
+        rs = [torch.zeros(3 * n, dtype=torch.float64, device="cuda") for _ in plans]
         for pl, b in zip(plans, rs):
             pl.pass1(b.data_ptr())
         rsum = sum(rs)
@@ -346,7 +346,7 @@ def test_plan_set_features_matches_fresh_scoring(oracle):
     for size in (300, 250, 130, 64, 3):
         fidx = np.sort(rng.choice(300, size, replace=False)) if size < 300 else None
         plan.set_features(fidx)
-        rs = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
+        rs = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
         cn = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
         sc = torch.zeros(plan.n_kept, dtype=torch.float64, device="cuda")
         plan.pass1(rs.data_ptr())

@@ -62,11 +62,11 @@ def test_cfg4_sharded_world4_equals_single(cfg4):
     isd = np.zeros(p, bool)
     single = _ms(X, y).feature_importances_
     world = 4
-    rs_sum = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
+    rs_sum = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
     plans = []
     for rk in range(world):
         pl = _lib.Plan("gpu", X, y, recip, isd, rank=rk, world=world)
-        b = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
+        b = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
         pl.pass1(b.data_ptr())
         rs_sum += b
         plans.append(pl)

@@ -71,7 +71,7 @@ def _sharded_cpu(x, y, recip, isd, world, use_star):
     n, p = x.shape
     plans = [_lib.Plan("cpu", x, y, recip, isd, use_star=use_star, rank=r, world=world)
              for r in range(world)]
-    rs = [np.zeros(2 * n) for _ in plans]
+    rs = [np.zeros(3 * n) for _ in plans]
     for pl, b in zip(plans, rs):
         pl.pass1(b.ctypes.data)
     rsum = np.sum(rs, axis=0)

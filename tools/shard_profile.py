@@ -36,7 +36,7 @@ def main():
     n = args.samples
     stream = torch.cuda.current_stream().cuda_stream
     plan = _lib.Plan("gpu", x, y, recip, isd, rank=args.rank, world=args.world, stream=stream)
-    rs = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
+    rs = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
     cn = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
     sc = torch.zeros(args.features, dtype=torch.float64, device="cuda")
 
