@@ -9,7 +9,8 @@ def main(d):
     vals = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(f"{d}/*/run_counter_collection.csv"):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("fs::gpu::", "")
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
+            k = k.split("(")[0].replace("fs::gpu::", "")
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, c in vals.items():
         if not k.startswith("k_"):

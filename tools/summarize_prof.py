@@ -17,7 +17,8 @@ import sys
 
 
 def short(name):
-    return name.split("(")[0].replace("void ", "").replace("fs::gpu::", "")
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    return name.split("(")[0].replace("fs::gpu::", "")
 
 
 def main(src, out):
