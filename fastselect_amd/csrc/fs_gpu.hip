@@ -230,20 +230,20 @@ __global__ __launch_bounds__(1024) void k_rowcorr(const float* __restrict__ epsT
 // ---------------------------------------------------------------------------
 // Workgroup = 256 lanes = one 128x128 tile (bi <= bj).  Lane (tx, ty) owns
 // rows {ty*4 + r, 64 + ty*4 + r} x cols {tx*4 + c, 64 + tx*4 + c} (8x8).
-// Per 16-feature chunk the A panel (rows) and B panel (cols) of xqT, each
-// 16 x 128 u32 = 8 KB, are copied global -> LDS by global_load_lds_dwordx4
+// Per 32-feature chunk the A panel (rows) and B panel (cols) of xqT, each
+// 32 x 128 u32 = 16 KB, are copied global -> LDS by global_load_lds_dwordx4
 // (each wave moves 2 x 1 KB of A and of B), double-buffered: chunk c+1 is in
 // flight while chunk c is consumed.  u32 accumulators absorb 256 features,
 // then their bits >= 24 move into 16-bit halves of a packed high word, so the
 // final distance D = hi * 2^24 + lo is exact below 2^40.
-// One 16-feature chunk of SADs (continuous) or mismatch counts (discrete)
+// One 32-feature chunk of SADs (continuous) or mismatch counts (discrete)
 // from an LDS panel pair.
 template <bool DISC>
 __device__ __forceinline__ void dist_chunk(const uint32_t* __restrict__ A,
                                            const uint32_t* __restrict__ B, int tx, int ty,
                                            uint32_t sc_disc, uint32_t (&acc)[8][8]) {
 #pragma unroll 2
-  for (int k = 0; k < kBK; k++) {
+  for (int k = 0; k < kBKQ; k++) {
     const uint4 a0 = *(const uint4*)&A[k * kTile + ty * 4];
     const uint4 a1 = *(const uint4*)&A[k * kTile + 64 + ty * 4];
     const uint4 b0 = *(const uint4*)&B[k * kTile + tx * 4];
@@ -271,8 +271,8 @@ __global__ __launch_bounds__(256, 2) void k_dist(const uint32_t* __restrict__ xq
   // Two distinct LDS objects (not one indexed array) so the compiler can
   // prove a pending global_load_lds into one buffer does not alias the
   // ds_reads of the other and keeps the copy in flight across the compute.
-  __shared__ __attribute__((aligned(16))) uint32_t ldsA0[kBK * kTile], ldsB0[kBK * kTile];
-  __shared__ __attribute__((aligned(16))) uint32_t ldsA1[kBK * kTile], ldsB1[kBK * kTile];
+  __shared__ __attribute__((aligned(16))) uint32_t ldsA0[kBKQ * kTile], ldsB0[kBKQ * kTile];
+  __shared__ __attribute__((aligned(16))) uint32_t ldsA1[kBKQ * kTile], ldsB1[kBKQ * kTile];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -292,14 +292,15 @@ __global__ __launch_bounds__(256, 2) void k_dist(const uint32_t* __restrict__ xq
     for (int c = 0; c < 4; c++) hi[r][c] = 0;
   }
 
-  // glds lane mapping: instruction s of wave w moves k-rows 2*(2w+s) and
-  // 2*(2w+s)+1; lane l -> k-row offset l/32, 4 u32 at column (l%32)*4.
+  // glds lane mapping: instruction s of wave w moves k-rows 2*(4w+s) and
+  // 2*(4w+s)+1; lane l -> k-row offset l/32, 4 u32 at column (l%32)*4.
+  constexpr int kIns = kBKQ / 8;  // glds instructions per wave and panel
   const int krow_l = lane >> 5, col_l = (lane & 31) * 4;
   auto stage = [&](uint32_t* la_base, uint32_t* lb_base, int ck) {
-    const int64_t k0 = (int64_t)ck * kBK;
+    const int64_t k0 = (int64_t)ck * kBKQ;
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
-      const int ins = wave * 2 + s;
+    for (int s = 0; s < kIns; s++) {
+      const int ins = wave * kIns + s;
       const int64_t krow = k0 + ins * 2 + krow_l;
       const uint32_t* ga = xqT + krow * n_pad + i0 + col_l;
       const uint32_t* gb = xqT + krow * n_pad + j0 + col_l;
@@ -1699,7 +1700,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   std::vector<int2> tl(g->n_tiles);
   for (int64_t t = 0; t < g->n_tiles; t++) tl[t] = make_int2(bi[t], bj[t]);
   g->list_cap = std::max<int64_t>(1 << 16, Q.n * 64);
-  g->ksplit = choose_ksplit(g->n_tiles, device, (int)((Q.PC + Q.PD) / kBK), Q.pc + Q.pd);
+  g->ksplit = choose_ksplit(g->n_tiles, device, (int)((Q.PC + Q.PD) / kBKQ), Q.pc + Q.pd);
   if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
   const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
   int rc;
@@ -1779,7 +1780,7 @@ static int run_quantize_dist(Plan* g) {
   if (g->n_tiles > 0) {
     FS_HIP(hipEventRecord(g->ev[0], g->stream));
     k_dist<<<(unsigned)(g->n_tiles * g->ksplit), 256, 0, g->stream>>>(
-        g->xqT, Q.n_pad, (int)(Q.PC / kBK), (int)(Q.PD / kBK), Q.SCu, g->tiles, g->ksplit, g->D,
+        g->xqT, Q.n_pad, (int)(Q.PC / kBKQ), (int)(Q.PD / kBKQ), Q.SCu, g->tiles, g->ksplit, g->D,
         g->Dpart);
     FS_TRY(launch_check("k_dist"));
     if (g->ksplit > 1) {
