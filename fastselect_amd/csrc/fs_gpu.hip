@@ -232,7 +232,7 @@ __global__ __launch_bounds__(1024) void k_rowcorr(const float* __restrict__ epsT
 // rows {ty*4 + r, 64 + ty*4 + r} x cols {tx*4 + c, 64 + tx*4 + c} (8x8).
 // Per 32-feature chunk the A panel (rows) and B panel (cols) of xqT, each
 // 32 x 128 u32 = 16 KB, are copied global -> LDS by global_load_lds_dwordx4
-// (each wave moves 2 x 1 KB of A and of B), double-buffered: chunk c+1 is in
+// (each wave moves 4 x 1 KB of A and of B), double-buffered: chunk c+1 is in
 // flight while chunk c is consumed.  u32 accumulators absorb 256 features,
 // then their bits >= 24 move into 16-bit halves of a packed high word, so the
 // final distance D = hi * 2^24 + lo is exact below 2^40.
