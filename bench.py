@@ -73,7 +73,7 @@ def make_data(n, p, seed):
     return X.astype(np.float32), y
 
 
-def cpu_baseline(x, y, budget_s=15.0):
+def cpu_baseline(x, y, budget_s=25.0):
     """Oracle MultiSURF on the first m focal samples, extrapolated to n: a
     small untimed run (page-in, thread start), a short run to measure the
     per-sample rate, then a ~budget_s sample whose time is reported."""
