@@ -888,16 +888,29 @@ __device__ __forceinline__ void score_tiles(const float* __restrict__ xs, int64_
   out1 = s1;
 }
 
+// XCD-aware grid: workgroup w normally runs on XCD w % 8, so XCD x is given
+// the segments s = x, x + 8, ... with all nfb feature blocks of a segment in
+// consecutive slots.  The ~160 workgroups an XCD holds at a time then share
+// one segment's pair weights (30 tiles x 64 KB) in that XCD's L2 instead of
+// ~8 segments thrashing it; the 1-D grid has 8 * max_x(segments of x) * nfb
+// slots, the few beyond nseg exit at once.
+constexpr int kXcds = 8;
+
 __global__ __launch_bounds__(256) void k_score(const float* __restrict__ xs, int64_t PW,
                                                int64_t PC, const int2* __restrict__ tiles,
                                                const float* __restrict__ Wt, int64_t n_tiles,
-                                               int64_t seg_len, double* __restrict__ spart) {
+                                               int64_t seg_len, int64_t nseg, int64_t nfb,
+                                               double* __restrict__ spart) {
   __shared__ double red[2][4][64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t f0 = (int64_t)blockIdx.x * 128;
+  const int64_t w = blockIdx.x;
+  const int64_t xcd = w % kXcds, k = w / kXcds;
+  const int64_t seg = xcd + kXcds * (k / nfb), fb = k % nfb;
+  if (seg >= nseg) return;
+  const int64_t f0 = fb * 128;
   const int64_t c0 = f0 + lane;
-  const int64_t t_begin = (int64_t)blockIdx.y * seg_len;
+  const int64_t t_begin = seg * seg_len;
   const int64_t t_end = t_begin + seg_len < n_tiles ? t_begin + seg_len : n_tiles;
   const bool two = f0 + 64 < PW;
   const bool d0 = f0 >= PC, d1 = f0 + 64 >= PC;
@@ -915,7 +928,7 @@ __global__ __launch_bounds__(256) void k_score(const float* __restrict__ xs, int
   __syncthreads();
   if (wave < 2 && (wave == 0 || two)) {
     const double v = (red[wave][0][lane] + red[wave][1][lane]) + (red[wave][2][lane] + red[wave][3][lane]);
-    spart[(int64_t)blockIdx.y * PW + c0 + wave * 64] = v;
+    spart[seg * PW + c0 + wave * 64] = v;
   }
 }
 
@@ -1834,8 +1847,9 @@ static int run_pass2(Plan* g, double* scores_dev) {
   FS_HIP(hipMemsetAsync(scores_dev, 0, sizeof(double) * Q.n_kept, g->stream));
   if (g->n_tiles == 0) return FS_OK;
   FS_HIP(hipEventRecord(g->ev[2], g->stream));
-  k_score<<<dim3((unsigned)nfb, (unsigned)g->nseg), 256, 0, g->stream>>>(
-      g->xs, Q.PW, Q.PC, g->tiles, g->Wt, g->n_tiles, g->seg_len, g->spart);
+  const int64_t seg_per_xcd = (g->nseg + kXcds - 1) / kXcds;
+  k_score<<<(unsigned)(kXcds * seg_per_xcd * nfb), 256, 0, g->stream>>>(
+      g->xs, Q.PW, Q.PC, g->tiles, g->Wt, g->n_tiles, g->seg_len, g->nseg, nfb, g->spart);
   FS_TRY(launch_check("k_score"));
   FS_HIP(hipEventRecord(g->ev[3], g->stream));
   k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(g->spart, g->nseg, Q.PW,
