@@ -28,6 +28,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/fastselect_amd.h"
@@ -230,13 +231,13 @@ __global__ __launch_bounds__(1024) void k_rowcorr(const float* __restrict__ epsT
 // ---------------------------------------------------------------------------
 // Workgroup = 256 lanes = one 128x128 tile (bi <= bj).  Lane (tx, ty) owns
 // rows {ty*4 + r, 64 + ty*4 + r} x cols {tx*4 + c, 64 + tx*4 + c} (8x8).
-// Per 32-feature chunk the A panel (rows) and B panel (cols) of xqT, each
-// 32 x 128 u32 = 16 KB, are copied global -> LDS by global_load_lds_dwordx4
-// (each wave moves 4 x 1 KB of A and of B), double-buffered: chunk c+1 is in
+// Per 16-feature chunk the A panel (rows) and B panel (cols) of xqT, each
+// 16 x 128 u32 = 8 KB, are copied global -> LDS by global_load_lds_dwordx4
+// (each wave moves 2 x 1 KB of A and of B), double-buffered: chunk c+1 is in
 // flight while chunk c is consumed.  u32 accumulators absorb 256 features,
 // then their bits >= 24 move into 16-bit halves of a packed high word, so the
 // final distance D = hi * 2^24 + lo is exact below 2^40.
-// One 32-feature chunk of SADs (continuous) or mismatch counts (discrete)
+// One 16-feature chunk of SADs (continuous) or mismatch counts (discrete)
 // from an LDS panel pair.
 template <bool DISC>
 __device__ __forceinline__ void dist_chunk(const uint32_t* __restrict__ A,
@@ -263,7 +264,7 @@ __device__ __forceinline__ void dist_chunk(const uint32_t* __restrict__ A,
 // chunk range of part b % splits; part 0 writes D, part s the partial buffer
 // Dpart[s - 1] (k_dist_merge adds them).  A rank that owns few tiles (N-GPU
 // runs) thus fills the chip's 2 x CU workgroup slots in more even rounds.
-__global__ __launch_bounds__(256, 2) void k_dist(const uint32_t* __restrict__ xqT, int64_t n_pad,
+__global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xqT, int64_t n_pad,
                                                  int nck_cont, int nck_disc, uint32_t sc_disc,
                                                  const int2* __restrict__ tiles, int splits,
                                                  double* __restrict__ D,
@@ -324,27 +325,34 @@ __global__ __launch_bounds__(256, 2) void k_dist(const uint32_t* __restrict__ xq
       }
   };
 
-  // chunk ck lives in buffer ck & 1; chunk ck+1 is copied while ck is consumed
-  auto step = [&](const uint32_t* A, const uint32_t* B, uint32_t* nA, uint32_t* nB, int ck,
-                  int nck) {
-    if (ck + 1 < nck) stage(nA, nB, ck + 1);
-    if (ck < nck_cont) dist_chunk<false>(A, B, tx, ty, sc_disc, acc);
-    else dist_chunk<true>(A, B, tx, ty, sc_disc, acc);
-    if ((ck % kFlushChunks) == kFlushChunks - 1) flush();
+  // Chunks [c0, c1) of one kind: chunk ck lives in buffer (ck - c0) & 1 and
+  // chunk ck+1 is copied while ck is consumed.  Continuous and discrete
+  // chunks run in separate loops (one dist_chunk instantiation each), which
+  // keeps the register allocation of either loop to itself.
+  auto run = [&](auto disc_tag, int c0, int c1) {
+    constexpr bool DISC = decltype(disc_tag)::value;
+    if (c0 >= c1) return;
+    stage(ldsA0, ldsB0, c0);
     __syncthreads();
+    for (int ck = c0; ck < c1; ck += 2) {
+      if (ck + 1 < c1) stage(ldsA1, ldsB1, ck + 1);
+      dist_chunk<DISC>(ldsA0, ldsB0, tx, ty, sc_disc, acc);
+      if ((ck % kFlushChunks) == kFlushChunks - 1) flush();
+      __syncthreads();
+      if (ck + 1 < c1) {
+        if (ck + 2 < c1) stage(ldsA0, ldsB0, ck + 2);
+        dist_chunk<DISC>(ldsA1, ldsB1, tx, ty, sc_disc, acc);
+        if (((ck + 1) % kFlushChunks) == kFlushChunks - 1) flush();
+        __syncthreads();
+      }
+    }
   };
 
   const int nck_all = nck_cont + nck_disc;
   const int c_begin = (int)((int64_t)nck_all * part / splits);
-  const int nck = (int)((int64_t)nck_all * (part + 1) / splits);  // end of this part
-  if (c_begin < nck) {
-    stage(ldsA0, ldsB0, c_begin);
-    __syncthreads();
-  }
-  for (int ck = c_begin; ck < nck; ck += 2) {
-    step(ldsA0, ldsB0, ldsA1, ldsB1, ck, nck);
-    if (ck + 1 < nck) step(ldsA1, ldsB1, ldsA0, ldsB0, ck + 1, nck);
-  }
+  const int c_end = (int)((int64_t)nck_all * (part + 1) / splits);  // this part's chunks
+  run(std::false_type{}, c_begin, c_end < nck_cont ? c_end : nck_cont);
+  run(std::true_type{}, c_begin > nck_cont ? c_begin : nck_cont, c_end);
   flush();
 
   // Epilogue: D[i][j] for the tile and, off the diagonal, the mirror D[j][i].
@@ -415,25 +423,30 @@ __global__ __launch_bounds__(256) void k_dist_merge(double* __restrict__ D,
 template <bool DISC>
 __device__ __forceinline__ void dist_chunk_f64(const double* __restrict__ A,
                                                const double* __restrict__ B, int tx, int ty,
-                                               double (&acc)[8][4]) {
+                                               double (&acc)[8][8]) {
 #pragma unroll 2
   for (int k = 0; k < kBK; k++) {
     const double4 a0 = *(const double4*)&A[k * kTile + ty * 4];
     const double4 a1 = *(const double4*)&A[k * kTile + 64 + ty * 4];
     const double4 b0 = *(const double4*)&B[k * kTile + tx * 4];
+    const double4 b1 = *(const double4*)&B[k * kTile + 64 + tx * 4];
     const double av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    const double bv[4] = {b0.x, b0.y, b0.z, b0.w};
+    const double bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
     for (int r = 0; r < 8; r++)
 #pragma unroll
-      for (int c = 0; c < 4; c++)
+      for (int c = 0; c < 8; c++)
         // codes are small integers: [a != b] == min(|a - b|, 1) without lane masks
         acc[r][c] += DISC ? __builtin_fmin(__builtin_fabs(av[r] - bv[c]), 1.0)
                           : __builtin_fabs(av[r] - bv[c]);
   }
 }
 
-__global__ __launch_bounds__(512, 2) void k_dist_f64(const double* __restrict__ xT, int64_t n_pad,
+// SURF pass 1 in float64 (SURF.py:153-156 arithmetic): one 128x128 tile per
+// 256-thread workgroup, 8x8 pairs per lane (the lane layout of k_dist), so a
+// k-step reads 128 B of LDS per lane for 64 pair-feature evaluations (8 x 4
+// per lane read 96 B for 32 and left the LDS near its bandwidth).
+__global__ __launch_bounds__(256, 2) void k_dist_f64(const double* __restrict__ xT, int64_t n_pad,
                                                      int nck_cont, int nck_disc,
                                                      const int2* __restrict__ tiles,
                                                      double* __restrict__ D) {
@@ -444,19 +457,19 @@ __global__ __launch_bounds__(512, 2) void k_dist_f64(const double* __restrict__ 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int2 tl = tiles[blockIdx.x];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
-  const int tx = tid & 31, ty = tid >> 5;
-  double acc[8][4];
+  const int tx = tid & 15, ty = tid >> 4;
+  double acc[8][8];
 #pragma unroll
   for (int r = 0; r < 8; r++)
 #pragma unroll
-    for (int c = 0; c < 4; c++) acc[r][c] = 0.0;
-  // 8 waves; instruction s of wave w moves k-row 2w+s (1 KB): lane l ->
+    for (int c = 0; c < 8; c++) acc[r][c] = 0.0;
+  // 4 waves; instruction s of wave w moves k-row 4w+s (1 KB): lane l ->
   // doubles 2l, 2l+1 of that row
   auto stage = [&](double* la, double* lb, int ck) {
     const int64_t k0 = (int64_t)ck * kBK;
 #pragma unroll
-    for (int s = 0; s < 2; s++) {
-      const int krow = wave * 2 + s;
+    for (int s = 0; s < 4; s++) {
+      const int krow = wave * 4 + s;
       const double* ga = xT + (k0 + krow) * n_pad + i0 + 2 * lane;
       const double* gb = xT + (k0 + krow) * n_pad + j0 + 2 * lane;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ga,
@@ -467,32 +480,38 @@ __global__ __launch_bounds__(512, 2) void k_dist_f64(const double* __restrict__ 
                                        16, 0, 0);
     }
   };
-  const int nck = nck_cont + nck_disc;
-  stage(ldsA0, ldsB0, 0);
-  __syncthreads();
-  for (int ck = 0; ck < nck; ck += 2) {
-    if (ck + 1 < nck) stage(ldsA1, ldsB1, ck + 1);
-    if (ck < nck_cont) dist_chunk_f64<false>(ldsA0, ldsB0, tx, ty, acc);
-    else dist_chunk_f64<true>(ldsA0, ldsB0, tx, ty, acc);
+  // continuous then discrete chunks, one instantiation per loop (see k_dist)
+  auto run = [&](auto disc_tag, int c0, int c1) {
+    constexpr bool DISC = decltype(disc_tag)::value;
+    if (c0 >= c1) return;
+    stage(ldsA0, ldsB0, c0);
     __syncthreads();
-    if (ck + 1 < nck) {
-      if (ck + 2 < nck) stage(ldsA0, ldsB0, ck + 2);
-      if (ck + 1 < nck_cont) dist_chunk_f64<false>(ldsA1, ldsB1, tx, ty, acc);
-      else dist_chunk_f64<true>(ldsA1, ldsB1, tx, ty, acc);
+    for (int ck = c0; ck < c1; ck += 2) {
+      if (ck + 1 < c1) stage(ldsA1, ldsB1, ck + 1);
+      dist_chunk_f64<DISC>(ldsA0, ldsB0, tx, ty, acc);
       __syncthreads();
+      if (ck + 1 < c1) {
+        if (ck + 2 < c1) stage(ldsA0, ldsB0, ck + 2);
+        dist_chunk_f64<DISC>(ldsA1, ldsB1, tx, ty, acc);
+        __syncthreads();
+      }
     }
-  }
+  };
+  run(std::false_type{}, 0, nck_cont);
+  run(std::true_type{}, nck_cont, nck_cont + nck_disc);
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     const int64_t i = i0 + ty * 4 + (r & 3) + (r >> 2) * 64;
     double* row = D + i * n_pad + j0 + tx * 4;
     *(double2*)(row + 0) = make_double2(acc[r][0], acc[r][1]);
     *(double2*)(row + 2) = make_double2(acc[r][2], acc[r][3]);
+    *(double2*)(row + 64) = make_double2(acc[r][4], acc[r][5]);
+    *(double2*)(row + 66) = make_double2(acc[r][6], acc[r][7]);
   }
   if (tl.x != tl.y) {
 #pragma unroll
-    for (int c = 0; c < 4; c++) {
-      const int64_t j = j0 + tx * 4 + c;
+    for (int c = 0; c < 8; c++) {
+      const int64_t j = j0 + tx * 4 + (c & 3) + (c >> 2) * 64;
       double* row = D + j * n_pad + i0 + ty * 4;
       *(double2*)(row + 0) = make_double2(acc[0][c], acc[1][c]);
       *(double2*)(row + 2) = make_double2(acc[2][c], acc[3][c]);
@@ -1762,7 +1781,7 @@ static int run_quantize_dist(Plan* g) {
     FS_TRY(launch_check("k_quantize_f64"));
     if (g->n_tiles > 0) {
       FS_HIP(hipEventRecord(g->ev[0], g->stream));
-      k_dist_f64<<<(unsigned)g->n_tiles, 512, 0, g->stream>>>(
+      k_dist_f64<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(
           g->xT64, Q.n_pad, (int)(Q.PC / kBK), (int)(Q.PD / kBK), g->tiles, g->D);
       FS_TRY(launch_check("k_dist_f64"));
       FS_HIP(hipEventRecord(g->ev[1], g->stream));
