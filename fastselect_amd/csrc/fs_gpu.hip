@@ -425,7 +425,7 @@ __device__ __forceinline__ void dist_chunk_f64(const double* __restrict__ A,
                                                const double* __restrict__ B, int tx, int ty,
                                                double (&acc)[8][8]) {
 #pragma unroll 2
-  for (int k = 0; k < kBK; k++) {
+  for (int k = 0; k < kBK64; k++) {
     const double4 a0 = *(const double4*)&A[k * kTile + ty * 4];
     const double4 a1 = *(const double4*)&A[k * kTile + 64 + ty * 4];
     const double4 b0 = *(const double4*)&B[k * kTile + tx * 4];
@@ -450,8 +450,8 @@ __global__ __launch_bounds__(256, 2) void k_dist_f64(const double* __restrict__ 
                                                      int nck_cont, int nck_disc,
                                                      const int2* __restrict__ tiles,
                                                      double* __restrict__ D) {
-  __shared__ __attribute__((aligned(16))) double ldsA0[kBK * kTile], ldsB0[kBK * kTile];
-  __shared__ __attribute__((aligned(16))) double ldsA1[kBK * kTile], ldsB1[kBK * kTile];
+  __shared__ __attribute__((aligned(16))) double ldsA0[kBK64 * kTile], ldsB0[kBK64 * kTile];
+  __shared__ __attribute__((aligned(16))) double ldsA1[kBK64 * kTile], ldsB1[kBK64 * kTile];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -463,13 +463,14 @@ __global__ __launch_bounds__(256, 2) void k_dist_f64(const double* __restrict__ 
   for (int r = 0; r < 8; r++)
 #pragma unroll
     for (int c = 0; c < 8; c++) acc[r][c] = 0.0;
-  // 4 waves; instruction s of wave w moves k-row 4w+s (1 KB): lane l ->
-  // doubles 2l, 2l+1 of that row
+  // 4 waves; instruction s of wave w moves k-row (kBK64/4)w+s (1 KB): lane
+  // l -> doubles 2l, 2l+1 of that row
+  constexpr int kRows = kBK64 / 4;
   auto stage = [&](double* la, double* lb, int ck) {
-    const int64_t k0 = (int64_t)ck * kBK;
+    const int64_t k0 = (int64_t)ck * kBK64;
 #pragma unroll
-    for (int s = 0; s < 4; s++) {
-      const int krow = wave * 4 + s;
+    for (int s = 0; s < kRows; s++) {
+      const int krow = wave * kRows + s;
       const double* ga = xT + (k0 + krow) * n_pad + i0 + 2 * lane;
       const double* gb = xT + (k0 + krow) * n_pad + j0 + 2 * lane;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ga,
@@ -1782,7 +1783,7 @@ static int run_quantize_dist(Plan* g) {
     if (g->n_tiles > 0) {
       FS_HIP(hipEventRecord(g->ev[0], g->stream));
       k_dist_f64<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(
-          g->xT64, Q.n_pad, (int)(Q.PC / kBK), (int)(Q.PD / kBK), g->tiles, g->D);
+          g->xT64, Q.n_pad, (int)(Q.PC / kBK64), (int)(Q.PD / kBK64), g->tiles, g->D);
       FS_TRY(launch_check("k_dist_f64"));
       FS_HIP(hipEventRecord(g->ev[1], g->stream));
     }

@@ -33,7 +33,7 @@ namespace fs {
 enum Algo : int { ALGO_MULTISURF = 0, ALGO_RELIEFF = 1, ALGO_SURF = 2 };
 
 constexpr int kTile = 128;          // pair tile edge (pass 1 / pass 2 / weights)
-constexpr int kBK = 16;             // features per LDS stage, float64 pass 1 (SURF)
+constexpr int kBK64 = 16;           // features per LDS stage, float64 pass 1 (SURF)
 constexpr int kBKQ = 16;            // features per LDS stage, integer pass 1
 constexpr int kFlushChunks = 256 / kBKQ;  // pass-1 u32 window = 256 features
 constexpr int kHiShift = 24;        // pass-1 high part = D >> 24 (16-bit packed)
