@@ -87,7 +87,7 @@ def test_cfg1_multisurf(oracle, star):
 
 
 @pytest.mark.parametrize("n,p,ncls,seed", [(129, 70, 2, 0), (257, 300, 3, 1), (1000, 2000, 2, 2),
-                                          (384, 5000, 2, 3)])
+                                          (384, 5000, 2, 3), (2500, 3000, 2, 4)])
 def test_multisurf_sizes(oracle, n, p, ncls, seed):
     from fastselect_amd import MultiSURF
     X, y = make_classification(n_samples=n, n_features=p, n_informative=20,
