@@ -1589,27 +1589,42 @@ void plan_destroy(Plan* g) {
   trace_mark("plan: free");
 }
 
-// Pass-1 K-split: k_dist runs 2 workgroups per CU, so T tiles take
-// ceil(T / slots) rounds; splitting every tile's feature range into S parts
+// Pass-1 K-split: k_dist holds `slots` workgroups on the chip at a time, so
+// T tiles take ceil(T / slots) rounds; splitting every tile's feature range into S parts
 // evens out the last round when a rank owns few tiles (N-GPU runs).  The
 // merge streams (S + 2) tile planes (~66.5 / p of the tile's compute time
 // each); S > 1 only when it gains at least 3%.
-static int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats) {
+static int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats,
+                         size_t plane_bytes) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
       cus <= 0) {
     (void)hipGetLastError();
     return 1;
   }
-  const double slots = 2.0 * cus;
+  // workgroups of k_dist resident per CU (3 at 163 VGPRs / 32 KB LDS)
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dist, 256, 0) != hipSuccess ||
+      per_cu <= 0) {
+    (void)hipGetLastError();
+    per_cu = 2;
+  }
+  const double slots = (double)per_cu * cus;
   auto eff = [&](int sp) {
     const double rounds = (double)tiles * sp / slots;
     const double merge = sp > 1 ? (sp + 2) * 66.5 / (double)(feats > 0 ? feats : 1) : 0.0;
     return rounds / std::ceil(rounds) - merge;
   };
+  // the S - 1 partial planes may take at most a quarter of the free memory
+  size_t free_b = 0, total_b = 0;
+  int max_sp = 8;
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && plane_bytes > 0)
+    max_sp = (int)std::min<size_t>(8, 1 + free_b / 4 / plane_bytes);
+  else
+    (void)hipGetLastError();
   int best = 1;
   double best_eff = eff(1) + 0.03;
-  for (int sp = 2; sp <= 4 && sp <= nchunks; sp++)
+  for (int sp = 2; sp <= max_sp && sp <= nchunks; sp++)
     if (eff(sp) > best_eff) {
       best_eff = eff(sp);
       best = sp;
@@ -1733,7 +1748,8 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   std::vector<int2> tl(g->n_tiles);
   for (int64_t t = 0; t < g->n_tiles; t++) tl[t] = make_int2(bi[t], bj[t]);
   g->list_cap = std::max<int64_t>(1 << 16, Q.n * 64);
-  g->ksplit = choose_ksplit(g->n_tiles, device, (int)((Q.PC + Q.PD) / kBKQ), Q.pc + Q.pd);
+  g->ksplit = choose_ksplit(g->n_tiles, device, (int)((Q.PC + Q.PD) / kBKQ), Q.pc + Q.pd,
+                            (size_t)Q.n_pad * Q.n_pad * sizeof(double));
   if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
   const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
   int rc;
