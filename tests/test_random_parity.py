@@ -1,0 +1,108 @@
+"""Randomised parity sweep: many small seeded datasets mixing the column kinds
+the reference distinguishes (continuous at any scale/offset, discrete with few
+levels, constant, heavily duplicated, integer-valued above the discrete
+limit), 2-4 imbalanced classes, float32 and float64 inputs, random
+``discrete_limit`` / ``n_neighbors`` -- every estimator on the product path
+against the oracle.
+
+Bar: 1e-5 scale-relative, and identical top-k wherever the
+oracle's own k-th and (k+1)-th scores are separated by more than the
+tolerance (an exact tie is ordered by argsort on bit-identical values, which
+a 1e-5 criterion does not pin).  When every score cancels to ~0 the scale
+itself is rounding noise, so the error may also sit under an absolute floor
+of 2^-22: the reference stores each sample's update (|update| <= 2) as
+float32 and sums the rows in float32, which is already that coarse.
+
+The CPU sweep exercises the native CPU backend (same pipeline as the HIP
+path); the ``gpu`` sweep runs the same cases through the HIP kernels.
+"""
+import numpy as np
+import pytest
+from conftest import scale_rel_err
+
+from fastselect_amd import SURF, MultiSURF, ReliefF
+
+TOL = 1e-5
+N_CASES = 40
+
+
+def make_case(seed):
+    rng = np.random.default_rng(1000 + seed)
+    n = int(rng.integers(2, 161))
+    p = int(rng.integers(1, 61))
+    cols = []
+    for _ in range(p):
+        kind = rng.choice(["cont", "cont", "disc", "const", "dup", "intwide"])
+        if kind == "cont":
+            scale = 10.0 ** rng.uniform(-3, 3)
+            c = rng.standard_normal(n) * scale + rng.uniform(-100, 100)
+        elif kind == "disc":
+            levels = rng.uniform(-5, 5, size=int(rng.integers(2, 9)))
+            c = rng.choice(levels, size=n)
+        elif kind == "const":
+            c = np.full(n, rng.uniform(-3, 3))
+        elif kind == "dup":
+            c = np.round(rng.standard_normal(n), 1)
+        else:
+            c = rng.integers(0, 40, size=n).astype(np.float64)
+        cols.append(c)
+    X = np.stack(cols, axis=1)
+    if rng.random() < 0.5:
+        X = X.astype(np.float32)
+    n_cls = int(rng.integers(2, 5))
+    w = rng.dirichlet(np.ones(n_cls) * 0.8)
+    y = rng.choice(n_cls, size=n, p=w)
+    y[0], y[-1] = 0, 1                     # at least two classes
+    # make the labels informative for a few features
+    for f in rng.choice(p, size=min(p, 3), replace=False):
+        if np.ptp(X[:, f]) > 0:
+            X[:, f] = X[:, f] + y * np.ptp(X[:, f]) * rng.uniform(0.2, 1.0)
+    dl = int(rng.choice([2, 5, 10]))
+    k = int(rng.integers(1, min(10, n - 1) + 1))
+    return X, y, dl, k
+
+
+ABS_FLOOR = 2.0 ** -22
+
+
+def check(a, ref, k=5):
+    err = scale_rel_err(a, ref)
+    ref = np.asarray(ref, dtype=np.float64)
+    if err > TOL:
+        aerr = np.abs(np.asarray(a, dtype=np.float64) - ref).max()
+        assert aerr <= ABS_FLOOR, f"scale-relative error {err:.3e} (abs {aerr:.3e})"
+    if ref.size <= k:
+        return
+    o = np.sort(ref)[::-1]
+    if o[k - 1] - o[k] > 2 * TOL * max(np.abs(ref).max(), 1e-30):
+        ta = set(np.argsort(np.asarray(a))[::-1][:k].tolist())
+        tr = set(np.argsort(ref)[::-1][:k].tolist())
+        assert ta == tr
+
+
+def run_case(oracle, seed, backend):
+    import warnings
+    X, y, dl, k = make_case(seed)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", UserWarning)
+        for star in (False, True):
+            check(MultiSURF(backend=backend, use_star=star, discrete_limit=dl)
+                  .fit(X, y).feature_importances_,
+                  oracle.multisurf_scores(X, y, use_star=star, discrete_limit=dl))
+            check(SURF(backend=backend, use_star=star, discrete_limit=dl)
+                  .fit(X, y).feature_importances_,
+                  oracle.surf_scores(X, y, use_star=star, discrete_limit=dl))
+        check(ReliefF(backend=backend, n_neighbors=k, discrete_limit=dl)
+              .fit(X, y).feature_importances_,
+              oracle.relieff_scores(X, y, n_neighbors=k, discrete_limit=dl))
+
+
+@pytest.mark.parametrize("seed", range(N_CASES))
+def test_random_parity_cpu(oracle, seed):
+    run_case(oracle, seed, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(N_CASES))
+def test_random_parity_gpu(oracle, seed):
+    run_case(oracle, seed, "gpu")
