@@ -16,6 +16,23 @@ from sklearn.utils.validation import check_is_fitted, validate_data
 from . import _base, _lib
 
 
+def relieff_inputs(x, y, discrete_limit, where):
+    """ReliefF.fit's preprocessing after validation (ReliefF.py:366-380, 400):
+    discrete detection and column ranges (computed on ``where``), class priors,
+    class codes, reciprocal ranges (discrete and constant columns -> 1) and the
+    float32 cast.  Returns (x32, y_enc int32, recip f32, is_discrete, priors f32)."""
+    is_discrete, col_min, col_max = _base.column_preprocess(x, discrete_limit, where)
+    class_labels, class_counts = np.unique(y, return_counts=True)
+    class_probs = class_counts / len(y)
+    y_enc = np.searchsorted(class_labels, y)
+    feature_ranges = col_max - col_min
+    feature_ranges[is_discrete] = 1.0
+    feature_ranges[feature_ranges == 0] = 1.0
+    recip = (1.0 / feature_ranges).astype(np.float32)
+    return (np.ascontiguousarray(x, dtype=np.float32), y_enc.astype(np.int32), recip, is_discrete,
+            class_probs.astype(np.float32))
+
+
 class ReliefF(TransformerMixin, BaseEstimator):
     """MI355X-accelerated feature selection with the ReliefF algorithm.
 
@@ -88,24 +105,16 @@ class ReliefF(TransformerMixin, BaseEstimator):
         # preprocessing runs where the scoring will (the backend itself is
         # resolved below, after these steps, as in the reference)
         where = "gpu" if self.backend != "cpu" and _lib.gpu_available() else "cpu"
-        is_discrete, col_min, col_max = _base.column_preprocess(x, self.discrete_limit, where)
+        x32, y_enc, recip_full, is_discrete, class_probs = relieff_inputs(
+            x, y, self.discrete_limit, where)
         self.is_discrete_ = is_discrete
-        class_labels, class_counts = np.unique(y, return_counts=True)
-        class_probs = class_counts / len(y)
-        y_enc = np.searchsorted(class_labels, y)
-        feature_ranges = col_max - col_min
-        feature_ranges[is_discrete] = 1.0
-        feature_ranges[feature_ranges == 0] = 1.0
-        recip_full = (1.0 / feature_ranges).astype(np.float32)
 
         self.effective_backend_ = _base.effective_backend(self.backend)
         if self.verbose:
             where = "GPU" if self.effective_backend_ == "gpu" else "CPU"
             print(f"Running ReliefF on the {where} now...")
-        scores = _lib.relieff_score(self.effective_backend_, x.astype(np.float32),
-                                    y_enc.astype(np.int32), recip_full, is_discrete,
-                                    self.n_neighbors, class_probs.astype(np.float32),
-                                    self.n_jobs)
+        scores = _lib.relieff_score(self.effective_backend_, x32, y_enc, recip_full, is_discrete,
+                                    self.n_neighbors, class_probs, self.n_jobs)
         self.feature_importances_ = scores
         self.top_features_ = _base.top_features(scores, n_select)
         return self

@@ -16,6 +16,17 @@ SURF_GPU_MISSING = ("backend='gpu', but no HIP-enabled GPU is available "
                     "(this build targets AMD MI355X / gfx950).")
 
 
+def surf_inputs(X, discrete_limit, where):
+    """SURF.fit's preprocessing after validation (SURF.py:347-355): discrete
+    detection and reciprocal ranges (discrete and constant columns -> 1),
+    computed on ``where``.  Returns (is_discrete, recip f32)."""
+    is_discrete, col_min, col_max = _base.column_preprocess(X, discrete_limit, where)
+    feature_ranges = col_max - col_min
+    feature_ranges[is_discrete] = 1.0
+    feature_ranges[feature_ranges == 0] = 1.0
+    return is_discrete, (1.0 / feature_ranges).astype(np.float32)
+
+
 class SURF(TransformerMixin, BaseEstimator):
     """MI355X-accelerated feature selection with SURF / SURF*.
 
@@ -69,12 +80,8 @@ class SURF(TransformerMixin, BaseEstimator):
         else:
             self.effective_backend_ = self.backend
 
-        self.is_discrete_, col_min, col_max = _base.column_preprocess(
-            X, self.discrete_limit, self.effective_backend_)
-        feature_ranges = col_max - col_min
-        feature_ranges[self.is_discrete_] = 1.0
-        feature_ranges[feature_ranges == 0] = 1.0
-        recip_full = (1.0 / feature_ranges).astype(np.float32)
+        self.is_discrete_, recip_full = surf_inputs(X, self.discrete_limit,
+                                                    self.effective_backend_)
 
         algo_name = "SURF*" if self.use_star else "SURF"
         if self.verbose:

@@ -36,7 +36,8 @@ _vp = ctypes.c_void_p
 # every symbol include/fastselect_amd.h declares (checked by tests/test_abi.py)
 EXPORTED = (
     "fs_version", "fs_last_error", "fs_device_count", "fs_column_stats", "fs_multisurf_score",
-    "fs_relieff_score", "fs_surf_score", "fs_plan_create", "fs_plan_set_features",
+    "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
+    "fs_plan_create", "fs_plan_set_features",
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2",
     "fs_plan_info", "fs_plan_kernel_ms", "fs_plan_destroy",
 )
@@ -75,6 +76,10 @@ def _load() -> ctypes.CDLL:
                                      _f32p, _i64, _int, _f32p]
     lib.fs_surf_score.argtypes = [_int, _int, _f64p, _i64, _i64, _i32p, _f32p, _int, _u8p, _int,
                                   _f32p]
+    lib.fs_relieff_score_rows.argtypes = [_int, _int, _f32p, _i64, _i64, _i32p, _f32p, _u8p,
+                                          _i64, _f32p, _i64, _int, _i64, _i64, _f64p]
+    lib.fs_surf_score_rows.argtypes = [_int, _int, _f64p, _i64, _i64, _i32p, _f32p, _int, _u8p,
+                                       _int, _i64, _i64, _f64p]
     lib.fs_plan_create.argtypes = [ctypes.POINTER(_vp), _int, _int, _f32p, _i64, _i64, _f64p,
                                    _f32p, _i64p, _i64, _int, _u8p, _int, _int, _int,
                                    ctypes.c_uint64]
@@ -87,7 +92,7 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_kernel_ms.restype = ctypes.c_double
     lib.fs_plan_destroy.argtypes = [_vp]
     for name in ("fs_column_stats", "fs_multisurf_score", "fs_relieff_score", "fs_surf_score",
-                 "fs_plan_create", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
+                 "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
                  "fs_plan_pass2", "fs_plan_info", "fs_plan_destroy"):
         getattr(lib, name).restype = _int
     return lib
@@ -176,32 +181,49 @@ def multisurf_score(backend, x, y, recip, feat_idx, use_star, is_discrete, n_job
     return out
 
 
-def relieff_score(backend, x, y_enc, recip, is_discrete, k, class_probs, n_jobs=-1, device=0):
-    """Drop-in for ``_relieff_{cpu,gpu}_host_caller`` (ReliefF.py:127-134, 222-236)."""
+def relieff_score(backend, x, y_enc, recip, is_discrete, k, class_probs, n_jobs=-1, device=0,
+                  rows=None):
+    """Drop-in for ``_relieff_{cpu,gpu}_host_caller`` (ReliefF.py:127-134, 222-236).
+
+    rows=(begin, end): float64 score sums of those focal samples only
+    (``fs_relieff_score_rows``, row sharding) instead of float32 scores / n.
+    """
     x = np.ascontiguousarray(x, dtype=np.float32)
     n, p = x.shape
     ye = np.ascontiguousarray(y_enc, dtype=np.int32)
     rc_ = np.ascontiguousarray(recip, dtype=np.float32)
     isd = np.ascontiguousarray(is_discrete, dtype=np.uint8)
     cp = np.ascontiguousarray(class_probs, dtype=np.float32)
+    args = (_backend_code(backend), int(device), _p(x, _f32p), n, p, _p(ye, _i32p),
+            _p(rc_, _f32p), _p(isd, _u8p), int(k), _p(cp, _f32p), cp.size, int(n_jobs))
+    if rows is not None:
+        out = np.zeros(p, dtype=np.float64)
+        check(_lib.fs_relieff_score_rows(*args, int(rows[0]), int(rows[1]), _p(out, _f64p)))
+        return out
     out = np.zeros(p, dtype=np.float32)
-    check(_lib.fs_relieff_score(_backend_code(backend), int(device), _p(x, _f32p), n, p,
-                                _p(ye, _i32p), _p(rc_, _f32p), _p(isd, _u8p), int(k),
-                                _p(cp, _f32p), cp.size, int(n_jobs), _p(out, _f32p)))
+    check(_lib.fs_relieff_score(*args, _p(out, _f32p)))
     return out
 
 
-def surf_score(backend, x, y, recip, use_star, is_discrete, n_jobs=-1, device=0):
-    """Drop-in for ``_surf_{cpu,gpu}_host_caller`` (SURF.py:117-128, 198-218)."""
+def surf_score(backend, x, y, recip, use_star, is_discrete, n_jobs=-1, device=0, rows=None):
+    """Drop-in for ``_surf_{cpu,gpu}_host_caller`` (SURF.py:117-128, 198-218).
+
+    rows=(begin, end): float64 score sums of those focal samples only
+    (``fs_surf_score_rows``, row sharding) instead of float32 scores / n.
+    """
     x = np.ascontiguousarray(x, dtype=np.float64)
     n, p = x.shape
     yi = np.ascontiguousarray(y, dtype=np.int32)
     rc_ = np.ascontiguousarray(recip, dtype=np.float32)
     isd = np.ascontiguousarray(is_discrete, dtype=np.uint8)
+    args = (_backend_code(backend), int(device), _p(x, _f64p), n, p, _p(yi, _i32p),
+            _p(rc_, _f32p), int(bool(use_star)), _p(isd, _u8p), int(n_jobs))
+    if rows is not None:
+        out = np.zeros(p, dtype=np.float64)
+        check(_lib.fs_surf_score_rows(*args, int(rows[0]), int(rows[1]), _p(out, _f64p)))
+        return out
     out = np.zeros(p, dtype=np.float32)
-    check(_lib.fs_surf_score(_backend_code(backend), int(device), _p(x, _f64p), n, p,
-                             _p(yi, _i32p), _p(rc_, _f32p), int(bool(use_star)), _p(isd, _u8p),
-                             int(n_jobs), _p(out, _f32p)))
+    check(_lib.fs_surf_score(*args, _p(out, _f32p)))
     return out
 
 

@@ -110,12 +110,18 @@ int fs_multisurf_score(int backend, int device, const float* x, int64_t n, int64
   return FS_OK;
 }
 
-int fs_relieff_score(int backend, int device, const float* x, int64_t n, int64_t p,
-                     const int32_t* y_enc, const float* recip, const uint8_t* is_discrete,
-                     int64_t k, const float* class_probs, int64_t n_classes, int n_jobs,
-                     float* scores_out) {
-  if (!scores_out || !y_enc || !class_probs || n_classes < 1 || k < 0) {
-    set_error("invalid ReliefF arguments (scores_out, y_enc, class_probs, n_classes, k)");
+// Shared by the one-shot and the row-range entry points: validate, prepare,
+// score the focal samples [r_lo, r_hi) -> float64 sums (not divided by n).
+static int relieff_sums(int backend, int device, const float* x, int64_t n, int64_t p,
+                        const int32_t* y_enc, const float* recip, const uint8_t* is_discrete,
+                        int64_t k, const float* class_probs, int64_t n_classes, int n_jobs,
+                        int64_t r_lo, int64_t r_hi, double* sums) {
+  if (!y_enc || !class_probs || n_classes < 1 || k < 0) {
+    set_error("invalid ReliefF arguments (y_enc, class_probs, n_classes, k)");
+    return FS_EINVAL;
+  }
+  if (!(0 <= r_lo && r_lo <= r_hi && r_hi <= n)) {
+    set_error("row range must satisfy 0 <= row_begin <= row_end <= n");
     return FS_EINVAL;
   }
   int rc = check_backend(backend, device);
@@ -136,18 +142,16 @@ int fs_relieff_score(int backend, int device, const float* x, int64_t n, int64_t
   P.class_prior.assign(n_classes, 0.0);
   for (int64_t c = 0; c < n_classes; c++) P.class_prior[c] = (double)class_probs[c];
   P.k_neighbors = k;
-  if (backend == FS_BACKEND_GPU) return gpu::relieff_run(P, x, device, scores_out);
-  std::vector<double> S(P.n_kept);
-  cpu::relieff_run(P, x, n_jobs, S.data());
-  for (int64_t f = 0; f < P.n_kept; f++) scores_out[f] = (float)(S[f] / (double)n);
-  return FS_OK;
+  if (backend == FS_BACKEND_GPU) return gpu::relieff_run(P, x, device, r_lo, r_hi, sums);
+  return cpu::relieff_run(P, x, n_jobs, r_lo, r_hi, sums);
 }
 
-int fs_surf_score(int backend, int device, const double* x, int64_t n, int64_t p,
-                  const int32_t* y, const float* recip, int use_star,
-                  const uint8_t* is_discrete, int n_jobs, float* scores_out) {
-  if (!scores_out) {
-    set_error("scores_out is NULL");
+static int surf_sums(int backend, int device, const double* x, int64_t n, int64_t p,
+                     const int32_t* y, const float* recip, int use_star,
+                     const uint8_t* is_discrete, int n_jobs, int64_t r_lo, int64_t r_hi,
+                     double* sums) {
+  if (!(0 <= r_lo && r_lo <= r_hi && r_hi <= n)) {
+    set_error("row range must satisfy 0 <= row_begin <= row_end <= n");
     return FS_EINVAL;
   }
   int rc = check_backend(backend, device);
@@ -160,11 +164,63 @@ int fs_surf_score(int backend, int device, const double* x, int64_t n, int64_t p
   if (rc) return map_prep_rc(rc);
   if (encode_labels_i32(P, y)) return FS_EINVAL;
   P.use_star = use_star ? 1 : 0;
-  if (backend == FS_BACKEND_GPU) return gpu::surf_run(P, x, device, scores_out);
-  std::vector<double> S(P.n_kept);
-  cpu::surf_run(P, x, n_jobs, S.data());
-  for (int64_t f = 0; f < P.n_kept; f++) scores_out[f] = (float)(S[f] / (double)n);
+  if (backend == FS_BACKEND_GPU) return gpu::surf_run(P, x, device, r_lo, r_hi, sums);
+  return cpu::surf_run(P, x, n_jobs, r_lo, r_hi, sums);
+}
+
+int fs_relieff_score(int backend, int device, const float* x, int64_t n, int64_t p,
+                     const int32_t* y_enc, const float* recip, const uint8_t* is_discrete,
+                     int64_t k, const float* class_probs, int64_t n_classes, int n_jobs,
+                     float* scores_out) {
+  if (!scores_out) {
+    set_error("scores_out is NULL");
+    return FS_EINVAL;
+  }
+  std::vector<double> S(p > 0 ? p : 1);
+  const int rc = relieff_sums(backend, device, x, n, p, y_enc, recip, is_discrete, k,
+                              class_probs, n_classes, n_jobs, 0, n, S.data());
+  if (rc != FS_OK) return rc;
+  for (int64_t f = 0; f < p; f++) scores_out[f] = (float)(S[f] / (double)n);
   return FS_OK;
+}
+
+int fs_relieff_score_rows(int backend, int device, const float* x, int64_t n, int64_t p,
+                          const int32_t* y_enc, const float* recip, const uint8_t* is_discrete,
+                          int64_t k, const float* class_probs, int64_t n_classes, int n_jobs,
+                          int64_t row_begin, int64_t row_end, double* sums_out) {
+  if (!sums_out) {
+    set_error("sums_out is NULL");
+    return FS_EINVAL;
+  }
+  return relieff_sums(backend, device, x, n, p, y_enc, recip, is_discrete, k, class_probs,
+                      n_classes, n_jobs, row_begin, row_end, sums_out);
+}
+
+int fs_surf_score(int backend, int device, const double* x, int64_t n, int64_t p,
+                  const int32_t* y, const float* recip, int use_star,
+                  const uint8_t* is_discrete, int n_jobs, float* scores_out) {
+  if (!scores_out) {
+    set_error("scores_out is NULL");
+    return FS_EINVAL;
+  }
+  std::vector<double> S(p > 0 ? p : 1);
+  const int rc = surf_sums(backend, device, x, n, p, y, recip, use_star, is_discrete, n_jobs, 0,
+                           n, S.data());
+  if (rc != FS_OK) return rc;
+  for (int64_t f = 0; f < p; f++) scores_out[f] = (float)(S[f] / (double)n);
+  return FS_OK;
+}
+
+int fs_surf_score_rows(int backend, int device, const double* x, int64_t n, int64_t p,
+                       const int32_t* y, const float* recip, int use_star,
+                       const uint8_t* is_discrete, int n_jobs, int64_t row_begin,
+                       int64_t row_end, double* sums_out) {
+  if (!sums_out) {
+    set_error("sums_out is NULL");
+    return FS_EINVAL;
+  }
+  return surf_sums(backend, device, x, n, p, y, recip, use_star, is_discrete, n_jobs, row_begin,
+                   row_end, sums_out);
 }
 
 }  // extern "C"

@@ -298,7 +298,8 @@ int multisurf_pass2(const Prepared& P, const CpuState& S, const double* counts, 
   return FS_OK;
 }
 
-int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
+int surf_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int64_t r_hi,
+             double* scores) {
   // SURF compares float32-rounded distances with a float32 sequential mean,
   // so distances are accumulated in float64 from float64 diffs (as
   // k_dist_f64 does; exact to ~1e-16, SURF.py:146-160) rather than quantised.
@@ -317,6 +318,7 @@ int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
   // float32 sequential mean (SURF.py:162-163)
   std::vector<double> avg(n);
   parallel_for(n, n_jobs, [&](int64_t i) {
+    if (i < r_lo || i >= r_hi) return;  // not a focal sample of this call
     float s = 0.0f;
     for (int64_t j = 0; j < n; j++) s += Df[(size_t)i * n + j];
     avg[i] = (double)s / (double)(n - 1);
@@ -326,8 +328,10 @@ int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
     for (int64_t j = i + 1; j < n; j++) {
       const double df = (double)Df[(size_t)i * n + j];
       const bool hit = P.labels[i] == P.labels[j];
-      const float w = (float)(surf_weight(df < avg[i], hit, P.use_star) +
-                              surf_weight(df < avg[j], hit, P.use_star));
+      // each side counts only for the focal samples [r_lo, r_hi)
+      const double wi = (i >= r_lo && i < r_hi) ? surf_weight(df < avg[i], hit, P.use_star) : 0.0;
+      const double wj = (j >= r_lo && j < r_hi) ? surf_weight(df < avg[j], hit, P.use_star) : 0.0;
+      const float w = (float)(wi + wj);
       if (w != 0.0f) pairs.push_back({(int32_t)i, (int32_t)j, w});
     }
   std::vector<double> S(P.PW, 0.0);
@@ -437,7 +441,8 @@ static void relieff_select_row(const Prepared& P, const float* x, const std::vec
   (void)li;
 }
 
-int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
+int relieff_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int64_t r_hi,
+                double* scores) {
   std::vector<uint32_t> xq;
   std::vector<float> xs;
   std::vector<double> D;
@@ -448,6 +453,7 @@ int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores) {
   // per-row partial sums, folded in row order for determinism
   std::vector<double> part((size_t)n * P.PW, 0.0);
   parallel_for(n, n_jobs, [&](int64_t i) {
+    if (i < r_lo || i >= r_hi) return;  // not a focal sample of this call
     std::vector<std::vector<int32_t>> nbr(C);
     relieff_select_row(P, (const float*)x, D, i, nbr);
     const int32_t li = P.labels[i];

@@ -637,10 +637,10 @@ __global__ void k_thr_ms(const double* __restrict__ rowstats, int64_t n,
 // across lanes).  The float32 sum stays strictly sequential in j (the
 // reference's order); 16 loads are issued ahead of the adds that use them.
 __global__ __launch_bounds__(64) void k_surf_avg(const double* __restrict__ D, int64_t n,
-                                                 int64_t n_pad, double inv_sc,
-                                                 double* __restrict__ avg) {
-  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (i >= n) return;
+                                                 int64_t n_pad, double inv_sc, int64_t r_lo,
+                                                 int64_t r_hi, double* __restrict__ avg) {
+  const int64_t i = r_lo + (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= r_hi) return;
   constexpr int kU = 16;
   float s = 0.0f;
   int64_t j = 0;
@@ -780,8 +780,10 @@ __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, i
                                                  const double* __restrict__ thr,
                                                  const int32_t* __restrict__ lab,
                                                  const double* __restrict__ counts, int algo,
-                                                 int use_star, double inv_sc,
-                                                 float* __restrict__ Wt) {
+                                                 int use_star, double inv_sc, int64_t r_lo,
+                                                 int64_t r_hi, float* __restrict__ Wt) {
+  // Only focal samples in [r_lo, r_hi) contribute their side of a pair (row
+  // sharding: another rank scores the other side); MultiSURF passes [0, n).
   const int2 tl = tiles[blockIdx.x];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
   float* out = Wt + (int64_t)blockIdx.x * kTile * kTile;
@@ -801,6 +803,8 @@ __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, i
         wi = surf_weight(df < thr[i], hit, use_star);
         wj = surf_weight(df < thr[j], hit, use_star);
       }
+      if (i < r_lo || i >= r_hi) wi = 0.0;
+      if (j < r_lo || j >= r_hi) wj = 0.0;
       w = (float)(wi + wj);
     }
     out[jj * kTile + ii] = w;
@@ -989,7 +993,7 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
                                                    const int32_t* __restrict__ lab,
                                                    const int64_t* __restrict__ class_count,
                                                    int n_classes, int64_t k, int collect,
-                                                   uint32_t* __restrict__ tkey,
+                                                   int64_t row0, uint32_t* __restrict__ tkey,
                                                    int32_t* __restrict__ tneed,
                                                    int32_t* __restrict__ teq,
                                                    int32_t* __restrict__ nbr,
@@ -1001,7 +1005,7 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
   uint32_t* need = prefix + n_classes;
   uint32_t* keys = need + n_classes;
   uint8_t* labs = (uint8_t*)(keys + n);  // STAGE: class codes (< 64)
-  const int64_t i = blockIdx.x;
+  const int64_t i = row0 + blockIdx.x;
   const int tid = threadIdx.x;
   const int nt = blockDim.x, nwaves = nt >> 6;
   const int32_t li = lab[i];
@@ -1167,10 +1171,10 @@ __global__ __launch_bounds__(256) void k_rf_flag(const double* __restrict__ D, i
                                                  int n_classes,
                                                  const uint32_t* __restrict__ tkey,
                                                  const int32_t* __restrict__ tneed,
-                                                 double band_abs, double band_rel,
+                                                 double band_abs, double band_rel, int64_t row0,
                                                  int2* __restrict__ list, int64_t cap,
                                                  unsigned long long* __restrict__ count) {
-  const int64_t i = blockIdx.x;
+  const int64_t i = row0 + blockIdx.x;
   const double* row = D + i * n_pad;
   for (int64_t j = threadIdx.x; j < n; j += 256) {
     if (j == i) continue;
@@ -1446,9 +1450,11 @@ __global__ __launch_bounds__(64) void k_rf_ties(const int32_t* __restrict__ rows
 }
 
 // acc_f(i) = -sum_hits d / h_found + sum_{c != y_i} (P_c / (1 - P_yi)) sum_misses_c d / k
-// (ReliefF.py:177-216).  Grid (PW/64, row blocks of 16); 4 waves per
-// workgroup, wave w handles rows w, w+4, ... of the block.
-__global__ __launch_bounds__(256) void k_rf_update(const float* __restrict__ xs, int64_t n,
+// (ReliefF.py:177-216) for the focal rows [r_lo, r_hi).  Grid (PW/64, row
+// blocks of 16); 4 waves per workgroup, wave w handles rows w, w+4, ... of
+// the block.
+__global__ __launch_bounds__(256) void k_rf_update(const float* __restrict__ xs, int64_t r_lo,
+                                                   int64_t r_hi,
                                                    int64_t PW, int64_t PC,
                                                    const int32_t* __restrict__ lab,
                                                    const double* __restrict__ prior,
@@ -1462,8 +1468,8 @@ __global__ __launch_bounds__(256) void k_rf_update(const float* __restrict__ xs,
   const int64_t c = (int64_t)blockIdx.x * 64 + lane;
   const bool disc = (int64_t)blockIdx.x * 64 >= PC;
   double acc = 0.0;
-  for (int64_t i = (int64_t)blockIdx.y * 16 + wave; i < n && i < (int64_t)blockIdx.y * 16 + 16;
-       i += 4) {
+  const int64_t b0 = r_lo + (int64_t)blockIdx.y * 16;
+  for (int64_t i = b0 + wave; i < r_hi && i < b0 + 16; i += 4) {
     const int32_t li = lab[i];
     const float a = xs[i * PW + c];
     double denom = 1.0 - prior[li];
@@ -1504,6 +1510,7 @@ struct Plan {
   int64_t nb = 0, n_tiles = 0, seg_len = 1, nseg = 1;
   int ksplit = 1;               // pass-1 K-split parts (k_dist)
   int64_t c_lo = 0, c_hi = 0;   // this rank's continuous columns of the mean correction
+  int64_t r_lo = 0, r_hi = 0;   // focal rows scored by this plan (row sharding)
   double2* rspart = nullptr;    // per owned tile row-moment partials [tiles][256]
   double* Dpart = nullptr;      // (ksplit - 1) partial distance planes
   int rank_shift = 0;
@@ -1702,7 +1709,7 @@ static int plan_layout(Plan* g) {
 }
 
 int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int device,
-                int rank, int world, uint64_t stream) {
+                int rank, int world, uint64_t stream, int64_t r_lo, int64_t r_hi) {
   *out = nullptr;
   const int ndev = device_count();
   if (ndev <= 0) {
@@ -1715,6 +1722,11 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   }
   if (world < 1 || rank < 0 || rank >= world) {
     set_error("invalid rank/world");
+    return FS_EINVAL;
+  }
+  const bool row_mode = r_hi >= 0;
+  if (row_mode && !(0 <= r_lo && r_lo <= r_hi && r_hi <= P.n)) {
+    set_error("row range outside [0, n)");
     return FS_EINVAL;
   }
   FS_HIP(hipSetDevice(device));
@@ -1743,7 +1755,15 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   const Prepared& Q = g->P;
   g->nb = Q.n_pad / kTile;
   std::vector<int32_t> bi, bj;
-  owned_tiles(g->nb, rank, world, bi, bj);
+  if (row_mode) {
+    g->r_lo = r_lo;
+    g->r_hi = r_hi;
+    if (r_hi > r_lo) row_tiles(g->nb, r_lo / kTile, (r_hi + kTile - 1) / kTile, bi, bj);
+  } else {
+    g->r_lo = 0;
+    g->r_hi = Q.n;
+    owned_tiles(g->nb, rank, world, bi, bj);
+  }
   g->n_tiles = (int64_t)bi.size();
   std::vector<int2> tl(g->n_tiles);
   for (int64_t t = 0; t < g->n_tiles; t++) tl[t] = make_int2(bi[t], bj[t]);
@@ -1931,7 +1951,7 @@ int plan_pass2(Plan* g, const double* counts, double* scores) {
     k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
                                                            g->thr, g->lab, counts,
                                                            ALGO_MULTISURF, Q.use_star,
-                                                           1.0 / Q.SC, g->Wt);
+                                                           1.0 / Q.SC, (int64_t)0, Q.n, g->Wt);
     FS_TRY(launch_check("k_weights"));
   }
   FS_TRY(run_pass2(g, scores));
@@ -1989,26 +2009,35 @@ int multisurf_run(const Prepared& P, const void* x, int device, float* scores_ou
   return FS_OK;
 }
 
-int surf_run(const Prepared& P, const void* x, int device, float* scores_out) {
+static int copy_sums(Plan* g, const double* sums_dev, double* sums_out) {
+  FS_HIP(hipMemcpyAsync(sums_out, sums_dev, sizeof(double) * g->P.n_kept, hipMemcpyDeviceToHost,
+                        g->stream));
+  FS_HIP(hipStreamSynchronize(g->stream));
+  return FS_OK;
+}
+
+int surf_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
+             double* sums_out) {
   Plan* g = nullptr;
-  FS_TRY(plan_create(&g, P, x, 1, device, 0, 1, 0));
+  FS_TRY(plan_create(&g, P, x, 1, device, 0, 1, 0, r_lo, r_hi));
   const Prepared& Q = g->P;
   double* sc = nullptr;
   int rc = dalloc(g, &sc, Q.n_kept);
   if (rc == FS_OK) rc = run_quantize_dist(g);  // float64 distances, real units
-  if (rc == FS_OK) {
-    k_surf_avg<<<(unsigned)((Q.n + 63) / 64), 64, 0, g->stream>>>(g->D, Q.n, Q.n_pad, 1.0,
-                                                                  g->thr);
+  if (rc == FS_OK && g->r_hi > g->r_lo) {
+    k_surf_avg<<<(unsigned)((g->r_hi - g->r_lo + 63) / 64), 64, 0, g->stream>>>(
+        g->D, Q.n, Q.n_pad, 1.0, g->r_lo, g->r_hi, g->thr);
     rc = launch_check("k_surf_avg");
   }
-  if (rc == FS_OK) {
+  if (rc == FS_OK && g->n_tiles > 0) {
     k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
                                                            g->thr, g->lab, nullptr, ALGO_SURF,
-                                                           Q.use_star, 1.0, g->Wt);
+                                                           Q.use_star, 1.0, g->r_lo, g->r_hi,
+                                                           g->Wt);
     rc = launch_check("k_weights");
   }
   if (rc == FS_OK) rc = run_pass2(g, sc);
-  if (rc == FS_OK) rc = finish_scores(g, sc, scores_out);
+  if (rc == FS_OK) rc = copy_sums(g, sc, sums_out);
   plan_destroy(g);
   return rc;
 }
@@ -2020,7 +2049,9 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   const Prepared& Q = g->P;
   const int C = Q.n_classes;
   const int64_t k = Q.k_neighbors, n = Q.n;
+  const int64_t r_lo = g->r_lo, nr_own = g->r_hi - g->r_lo;  // focal rows of this plan
   const double inv_sc = 1.0 / Q.SC;
+  if (nr_own <= 0) return FS_OK;
   uint32_t* tkey = nullptr;
   int32_t *tneed = nullptr, *teq = nullptr;
   FS_TRY(dalloc(g, &tkey, (size_t)n * C));
@@ -2034,11 +2065,13 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shstage));
   auto select = [&](int collect) {
     if (stage)
-      k_rf_select<true><<<(unsigned)n, 1024, shstage, g->stream>>>(
-          g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, tkey, tneed, teq, nbr, nfound);
+      k_rf_select<true><<<(unsigned)nr_own, 1024, shstage, g->stream>>>(
+          g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, r_lo, tkey, tneed, teq, nbr,
+          nfound);
     else
-      k_rf_select<false><<<(unsigned)n, 256, shbytes, g->stream>>>(
-          g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, tkey, tneed, teq, nbr, nfound);
+      k_rf_select<false><<<(unsigned)nr_own, 256, shbytes, g->stream>>>(
+          g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, r_lo, tkey, tneed, teq, nbr,
+          nfound);
     return launch_check("k_rf_select");
   };
   // 1. k-th keys from the quantised distances
@@ -2048,9 +2081,9 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   g->n_refined = 0;
   for (int attempt = 0; attempt < 2; attempt++) {
     FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
-    k_rf_flag<<<(unsigned)n, 256, 0, g->stream>>>(g->D, n, Q.n_pad, inv_sc, g->lab, C, tkey,
-                                                  tneed, band_abs, band_rel, g->list,
-                                                  g->list_cap, g->list_count);
+    k_rf_flag<<<(unsigned)nr_own, 256, 0, g->stream>>>(g->D, n, Q.n_pad, inv_sc, g->lab, C,
+                                                       tkey, tneed, band_abs, band_rel, r_lo,
+                                                       g->list, g->list_cap, g->list_count);
     FS_TRY(launch_check("k_rf_flag"));
     unsigned long long cnt = 0;
     FS_HIP(hipMemcpyAsync(&cnt, g->list_count, sizeof(cnt), hipMemcpyDeviceToHost, g->stream));
@@ -2072,15 +2105,17 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   // 3. exact selection
   FS_TRY(select(1));
   // 4. rows with more neighbours at the k-th key than needed
-  std::vector<int32_t> hneed((size_t)n * C), heq((size_t)n * C);
-  FS_HIP(hipMemcpyAsync(hneed.data(), tneed, hneed.size() * 4, hipMemcpyDeviceToHost, g->stream));
-  FS_HIP(hipMemcpyAsync(heq.data(), teq, heq.size() * 4, hipMemcpyDeviceToHost, g->stream));
+  std::vector<int32_t> hneed((size_t)nr_own * C), heq((size_t)nr_own * C);
+  FS_HIP(hipMemcpyAsync(hneed.data(), tneed + r_lo * C, hneed.size() * 4, hipMemcpyDeviceToHost,
+                        g->stream));
+  FS_HIP(hipMemcpyAsync(heq.data(), teq + r_lo * C, heq.size() * 4, hipMemcpyDeviceToHost,
+                        g->stream));
   FS_HIP(hipStreamSynchronize(g->stream));
   std::vector<int32_t> tie_rows;
-  for (int64_t i = 0; i < n; i++)
+  for (int64_t r = 0; r < nr_own; r++)
     for (int c = 0; c < C; c++)
-      if (hneed[i * C + c] > 0 && heq[i * C + c] > hneed[i * C + c]) {
-        tie_rows.push_back((int32_t)i);
+      if (hneed[r * C + c] > 0 && heq[r * C + c] > hneed[r * C + c]) {
+        tie_rows.push_back((int32_t)(r_lo + r));
         break;
       }
   g->n_tie_rows = (int64_t)tie_rows.size();
@@ -2124,13 +2159,14 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   return FS_OK;
 }
 
-int relieff_run(const Prepared& P, const void* x, int device, float* scores_out) {
+int relieff_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
+                double* sums_out) {
   if (P.n_classes > 64) {
     set_error("GPU ReliefF supports at most 64 classes");
     return FS_ENOTSUP;
   }
   Plan* g = nullptr;
-  FS_TRY(plan_create(&g, P, x, 0, device, 0, 1, 0));
+  FS_TRY(plan_create(&g, P, x, 0, device, 0, 1, 0, r_lo, r_hi));
   const Prepared& Q = g->P;
   const int C = Q.n_classes;
   const int64_t k = Q.k_neighbors;
@@ -2140,7 +2176,7 @@ int relieff_run(const Prepared& P, const void* x, int device, float* scores_out)
   double *sc = nullptr, *dprior = nullptr, *part = nullptr;
   int64_t* dcc = nullptr;
   int32_t *nbr = nullptr, *nfound = nullptr;
-  const int64_t nrb = (Q.n + 15) / 16;
+  const int64_t nrb = std::max<int64_t>(1, (g->r_hi - g->r_lo + 15) / 16);
   int rc;
   if ((rc = dalloc(g, &sc, Q.n_kept)) || (rc = dalloc(g, &dprior, C)) ||
       (rc = dalloc(g, &part, (size_t)nrb * Q.PW)) || (rc = dalloc(g, &dcc, C)) ||
@@ -2157,14 +2193,14 @@ int relieff_run(const Prepared& P, const void* x, int device, float* scores_out)
                  (long long)g->n_refined, (long long)g->n_tie_rows);
   }
   k_rf_update<<<dim3((unsigned)(Q.PW / 64), (unsigned)nrb), 256, 0, g->stream>>>(
-      g->xs, Q.n, Q.PW, Q.PC, g->lab, dprior, C, k, nbr, nfound, part);
+      g->xs, g->r_lo, g->r_hi, Q.PW, Q.PC, g->lab, dprior, C, k, nbr, nfound, part);
   rc = launch_check("k_rf_update");
   if (rc == FS_OK) {
     k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(part, nrb, Q.PW,
                                                                      g->out_pos, sc);
     rc = launch_check("k_reduce");
   }
-  if (rc == FS_OK) rc = finish_scores(g, sc, scores_out);
+  if (rc == FS_OK) rc = copy_sums(g, sc, sums_out);
   plan_destroy(g);
   return rc;
 }

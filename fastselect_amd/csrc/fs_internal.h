@@ -104,6 +104,11 @@ int encode_labels_i32(Prepared& P, const int32_t* y);
 // the triangle.  Tile t is owned by rank t % world.
 void owned_tiles(int64_t nb, int rank, int world, std::vector<int32_t>& bi,
                  std::vector<int32_t>& bj);
+// Row sharding (ReliefF / SURF): every upper-triangle tile that touches a
+// row block in [b_lo, b_hi), so that the distance rows of those blocks are
+// complete (each pair's tile writes both halves of D).
+void row_tiles(int64_t nb, int64_t b_lo, int64_t b_hi, std::vector<int32_t>& bi,
+               std::vector<int32_t>& bj);
 FS_HD inline int64_t tile_linear(int64_t nb, int64_t bi, int64_t bj) {
   // number of tiles in rows < bi is bi*nb - bi*(bi-1)/2
   return bi * nb - bi * (bi - 1) / 2 + (bj - bi);
@@ -233,8 +238,11 @@ int multisurf_select(const Prepared& P, const void* x, int rank, int world,
                      const double* rowstats, int n_jobs, CpuState& S, double* counts);
 int multisurf_pass2(const Prepared& P, const CpuState& S, const double* counts, int rank,
                     int world, int n_jobs, double* scores);
-int surf_run(const Prepared& P, const void* x, int n_jobs, double* scores);
-int relieff_run(const Prepared& P, const void* x, int n_jobs, double* scores);
+// Score sums (not divided by n) of the focal samples [r_lo, r_hi).
+int surf_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int64_t r_hi,
+             double* scores);
+int relieff_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int64_t r_hi,
+                double* scores);
 int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap, int n_jobs,
                  void* colmin, void* colmax, int64_t* ndistinct);
 }  // namespace cpu
@@ -249,8 +257,10 @@ int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap,
 int column_minmax(const void* dx, int x_is_f64, int64_t n, int64_t p, void* hmin, void* hmax,
                   void* stream);
 struct Plan;
+// Tile sharding (MultiSURF): tile t belongs to rank t % world.  Row
+// sharding (r_hi >= 0): the tiles touching the 128-row blocks of [r_lo, r_hi).
 int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int device,
-                int rank, int world, uint64_t stream);
+                int rank, int world, uint64_t stream, int64_t r_lo = 0, int64_t r_hi = -1);
 // Re-target a plan (resident X, distances storage) to another feature
 // subset: P is the new layout (same samples, labels and algorithm).
 int plan_set_features(Plan* g, const Prepared& P);
@@ -260,10 +270,14 @@ int plan_pass2(Plan* g, const double* counts_dev, double* scores_dev);
 int plan_info(const Plan* g, int64_t* tiles, double* pfe, int64_t* refined);
 double plan_kernel_ms(const Plan* g, int which);
 void plan_destroy(Plan* g);
-// Single-GPU one-shot runs (host in/out, scores already divided by n).
+// Single-GPU one-shot runs (host in/out).  MultiSURF: scores already divided
+// by n.  SURF / ReliefF: float64 score sums of the focal samples [r_lo, r_hi)
+// (row sharding; the full range gives the single-GPU result times n).
 int multisurf_run(const Prepared& P, const void* x, int device, float* scores_out);
-int surf_run(const Prepared& P, const void* x, int device, float* scores_out);
-int relieff_run(const Prepared& P, const void* x, int device, float* scores_out);
+int surf_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
+             double* sums_out);
+int relieff_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
+                double* sums_out);
 }  // namespace gpu
 
 }  // namespace fs

@@ -40,6 +40,18 @@ void owned_tiles(int64_t nb, int rank, int world, std::vector<int32_t>& bi,
       }
 }
 
+void row_tiles(int64_t nb, int64_t b_lo, int64_t b_hi, std::vector<int32_t>& bi,
+               std::vector<int32_t>& bj) {
+  bi.clear();
+  bj.clear();
+  for (int64_t a = 0; a < nb; a++)
+    for (int64_t b = a; b < nb; b++)
+      if ((a >= b_lo && a < b_hi) || (b >= b_lo && b < b_hi)) {
+        bi.push_back((int32_t)a);
+        bj.push_back((int32_t)b);
+      }
+}
+
 int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64_t p_in,
             const int64_t* feat_idx, int64_t n_kept, const float* recip,
             const uint8_t* is_discrete, int n_jobs, int device_ranges) {

@@ -1,4 +1,4 @@
-"""Sharded MultiSURF over one process per GPU (torch.distributed).
+"""Multi-GPU Relief scoring over one process per GPU (torch.distributed).
 
 The reference is single-device; this is the MI355X-native
 multi-GPU path of §8e: the upper-triangle pair tiles are dealt round-robin to
@@ -12,6 +12,13 @@ vector (RCCL over xGMI with the 'nccl' backend, gloo on CPU):
 
 With world == 1 no collective is issued and the result equals
 ``MultiSURF.fit`` on one device.
+
+ReliefF and SURF shard the focal samples instead (§8e "same row sharding"):
+their neighbour selection is row-local (ReliefF's k nearest per class, SURF's
+float32 sequential per-sample mean, which needs whole distance rows), so each
+rank scores a slice of the samples (``shard_rows``) and one SUM all-reduce of
+the p per-feature sums combines them (``relieff_scores`` / ``surf_scores``).
+A rank computes every distance tile touching its 128-sample blocks.
 """
 from __future__ import annotations
 
@@ -109,3 +116,66 @@ def multisurf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", dev
         return s.cpu().numpy()
     finally:
         job.close()
+
+
+# ---- row-sharded ReliefF / SURF ------------------------------------------
+
+ROW_BLOCK = 128   # the distance tile edge of the GPU plan
+
+
+def shard_rows(n: int, rank: int, world: int):
+    """Focal samples [begin, end) of ``rank``: whole 128-sample blocks dealt
+    contiguously, so every rank touches the same number of distance tiles
+    (up to one block)."""
+    nb = (n + ROW_BLOCK - 1) // ROW_BLOCK
+    b0, b1 = nb * rank // world, nb * (rank + 1) // world
+    return min(n, b0 * ROW_BLOCK), min(n, b1 * ROW_BLOCK)
+
+
+def _allreduce_sums(sums, backend, device):
+    """SUM all-reduce of a float64 host vector across the ranks (RCCL on the
+    GPU with the 'nccl' backend, gloo on the CPU); unchanged when world == 1."""
+    dist, _, world = _dist()
+    if dist is None or world == 1:
+        return sums
+    import torch
+    on_gpu = dist.get_backend() == "nccl"
+    t = torch.from_numpy(np.ascontiguousarray(sums))
+    if on_gpu:
+        t = t.to(torch.device("cuda", device))
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t.cpu().numpy()
+
+
+def relieff_scores(X, y, n_neighbors=3, discrete_limit=10, backend="gpu", device=0, n_jobs=-1):
+    """ReliefF feature scores with the focal samples sharded over the ranks:
+    this rank scores ``shard_rows(n, rank, world)``, one all-reduce sums the
+    slices.  Returns the full float32 score vector (identical on every rank)
+    -- ``ReliefF(n_neighbors=...).fit(X, y).feature_importances_`` up to
+    float64 summation order."""
+    from .ReliefF import relieff_inputs
+    x = np.ascontiguousarray(X, dtype=np.float64)
+    yv = np.asarray(y)
+    n, p = x.shape
+    if np.unique(yv).size < 2:
+        return np.zeros(p, dtype=np.float32)
+    backend = _base.effective_backend(backend)
+    x32, y_enc, recip, isd, priors = relieff_inputs(x, yv, discrete_limit, backend)
+    _, rank, world = _dist()
+    sums = _lib.relieff_score(backend, x32, y_enc, recip, isd, n_neighbors, priors, n_jobs,
+                              device=device, rows=shard_rows(n, rank, world))
+    return (_allreduce_sums(sums, backend, device) / n).astype(np.float32)
+
+
+def surf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", device=0, n_jobs=-1):
+    """SURF / SURF* feature scores with the focal samples sharded over the
+    ranks (see ``relieff_scores``)."""
+    from .SURF import surf_inputs
+    x = np.ascontiguousarray(X, dtype=np.float64)
+    n, p = x.shape
+    backend = _base.effective_backend(backend)
+    isd, recip = surf_inputs(x, discrete_limit, backend)
+    _, rank, world = _dist()
+    sums = _lib.surf_score(backend, x, np.asarray(y).astype(np.int32), recip, use_star, isd,
+                           n_jobs, device=device, rows=shard_rows(n, rank, world))
+    return (_allreduce_sums(sums, backend, device) / n).astype(np.float32)

@@ -95,8 +95,8 @@ FS_API int fs_multisurf_score(int backend, int device, const float* x, int64_t n
  *   k            n_neighbors (>= 1)
  *   class_probs  [n_classes] float32 class priors (ReliefF.py:373-374)
  *   scores_out   [p] float32, scores / n
- * Neighbour ties at the k-th distance are broken by sample index (the
- * reference breaks them in numba-quicksort order).
+ * Neighbours are chosen as the reference chooses them: by its float32
+ * distance key, ties at the k-th key in numba's quicksort order.
  */
 FS_API int fs_relieff_score(int backend, int device, const float* x, int64_t n, int64_t p,
                      const int32_t* y_enc, const float* recip, const uint8_t* is_discrete,
@@ -114,6 +114,29 @@ FS_API int fs_relieff_score(int backend, int device, const float* x, int64_t n, 
 FS_API int fs_surf_score(int backend, int device, const double* x, int64_t n, int64_t p,
                   const int32_t* y, const float* recip, int use_star,
                   const uint8_t* is_discrete, int n_jobs, float* scores_out);
+
+/*
+ * Row-sharded ReliefF / SURF: the float64 score SUMS (not
+ * divided by n) of the focal samples [row_begin, row_end) only, written to
+ * sums_out[p] (host memory).  Other arguments as fs_relieff_score /
+ * fs_surf_score.  Neighbour selection is row-local in both algorithms
+ * (ReliefF's k nearest per class, ReliefF.py:144-175; SURF's per-sample mean
+ * threshold, SURF.py:146-163), so one process per GPU scores a slice of the
+ * samples and a single SUM all-reduce of p doubles combines the slices:
+ * summing the vectors of a partition of [0, n) and dividing by n gives the
+ * one-shot scores up to float64 summation order.  The GPU computes every
+ * distance tile that touches the slice's 128-sample blocks, so slices on
+ * 128-sample boundaries (fastselect_amd.parallel.shard_rows) balance best.
+ */
+FS_API int fs_relieff_score_rows(int backend, int device, const float* x, int64_t n, int64_t p,
+                                 const int32_t* y_enc, const float* recip,
+                                 const uint8_t* is_discrete, int64_t k, const float* class_probs,
+                                 int64_t n_classes, int n_jobs, int64_t row_begin,
+                                 int64_t row_end, double* sums_out);
+FS_API int fs_surf_score_rows(int backend, int device, const double* x, int64_t n, int64_t p,
+                              const int32_t* y, const float* recip, int use_star,
+                              const uint8_t* is_discrete, int n_jobs, int64_t row_begin,
+                              int64_t row_end, double* sums_out);
 
 /*
  * Per-column statistics of X: the preprocessing each reference fit() runs on
