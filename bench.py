@@ -198,8 +198,9 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "fp32",
-            "arith": "pass 1: u32 integer L1 distances (exact); pass 2: f32 diffs x f32 pair "
-                     "weights, f64 accumulation",
+            "arith": "pass 1: integer L1 distances (v_sad_u16 on 16-bit operands for n >= 16384, "
+                     "else v_sad_u32), pairs near a threshold recomputed in the reference's "
+                     "float32 arithmetic; pass 2: f32 diffs x f32 pair weights, f64 accumulation",
             "data": "synthetic make_classification(n_informative=20, n_redundant=100, random_state=42)",
             "config": {"workload": f"MultiSURF{'*' if args.star else ''} n={args.samples} "
                                    f"p={args.features} (BASELINE configs[3])",

@@ -109,7 +109,8 @@ static void distances(const Prepared& P, const std::vector<uint32_t>& xq, int ra
 }
 
 // Mean correction of k_colrank / k_rowcorr: per continuous column a
-// 4096-bin histogram of q gives midranks, corr[i] = sum_c eps*(2 rank-(n-1)).
+// 4096-bin histogram of q (counts and fixed-point eps sums) gives
+// corr[i] = sum_c eps_i (2 rank_i - (n-1)) - (sum_{below} eps - sum_{above} eps).
 // The correction of the continuous columns [c_lo, c_hi) (a rank's share;
 // the shares are summed across ranks with the row moments).
 static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
@@ -122,15 +123,24 @@ static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
   std::vector<float> term((size_t)n * std::max<int64_t>(P.pc, 1), 0.0f);
   parallel_for(c_hi - c_lo, n_jobs, [&](int64_t cc) {
     const int64_t c = c_lo + cc;
+    constexpr double kFx = 16777216.0;  // eps fixed point 2^24, as k_colrank
     std::vector<uint32_t> cum(kBins + 1, 0);
-    for (int64_t i = 0; i < n; i++)
-      cum[std::min<int64_t>(xq[(size_t)i * P.PW + c] >> shift, kBins - 1) + 1]++;
-    for (int b = 0; b < kBins; b++) cum[b + 1] += cum[b];
+    std::vector<int64_t> ecum(kBins + 1, 0);
+    for (int64_t i = 0; i < n; i++) {
+      const int64_t b = std::min<int64_t>(xq[(size_t)i * P.PW + c] >> shift, kBins - 1);
+      cum[b + 1]++;
+      ecum[b + 1] += (int64_t)std::llrint((double)eps[(size_t)i * P.PW + c] * kFx);
+    }
+    for (int b = 0; b < kBins; b++) {
+      cum[b + 1] += cum[b];
+      ecum[b + 1] += ecum[b];
+    }
     for (int64_t i = 0; i < n; i++) {
       const int64_t b = std::min<int64_t>(xq[(size_t)i * P.PW + c] >> shift, kBins - 1);
       const double rank = (double)cum[b] + 0.5 * (double)(cum[b + 1] - cum[b] - 1u);
+      const double B = (double)(ecum[b] - (ecum[kBins] - ecum[b + 1])) / kFx;
       term[(size_t)i * P.pc + c] =
-          (float)((double)eps[(size_t)i * P.PW + c] * (2.0 * rank - (double)(n - 1)));
+          (float)((double)eps[(size_t)i * P.PW + c] * (2.0 * rank - (double)(n - 1)) - B);
     }
   });
   corr.assign(n, 0.0);

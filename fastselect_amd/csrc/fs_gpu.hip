@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <type_traits>
@@ -65,6 +66,14 @@ __device__ __forceinline__ uint32_t sad_u32(uint32_t a, uint32_t b, uint32_t c) 
   return d;
 }
 
+// c + |a.lo - b.lo| + |a.hi - b.hi| over unsigned 16-bit halves (two
+// features per word; checked on gfx950 by tools/ubench/sad16_check.hip)
+__device__ __forceinline__ uint32_t sad_u16(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm("v_sad_u16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
 // c + sc * [a != b] for small category codes, without lane masks (a
 // compare would burn an SGPR pair per pair-accumulator).
 __device__ __forceinline__ uint32_t mismatch_u32(uint32_t a, uint32_t b, uint32_t sc, uint32_t c) {
@@ -92,9 +101,13 @@ __device__ __forceinline__ double block_sum_256(double v, double* red) {
 // ---------------------------------------------------------------------------
 // Quantize: X -> xqT (u32, [PW][n_pad]) and xs (f32, [n_pad][PW])
 // ---------------------------------------------------------------------------
+// With q16 the continuous rows of xqT are packed: word row c/2 holds features
+// c (low half) and c + 1 (high half), and the discrete rows follow at PC/2:
+// [PC/2 + PD][n_pad] words in all (pass 1 then walks one contiguous range).
 template <typename T>
 __global__ __launch_bounds__(256) void k_quantize(
-    const T* __restrict__ x, int64_t n, int64_t n_pad, int64_t p_in, int64_t PW, int64_t pc,
+    const T* __restrict__ x, int64_t n, int64_t n_pad, int64_t p_in, int64_t PW, int64_t PC,
+    int q16, int64_t pc,
     const int64_t* __restrict__ src_col, const double* __restrict__ off,
     const double* __restrict__ qs, const double* __restrict__ scl,
     const int64_t* __restrict__ dtab_off, const double* __restrict__ dtab, int disc_bits,
@@ -142,64 +155,108 @@ __global__ __launch_bounds__(256) void k_quantize(
     etile[r][tx] = e;
   }
   __syncthreads();
-  for (int r = ty; r < 64; r += 4) {
-    xqT[(c0 + r) * n_pad + i0 + tx] = tile[tx][r];
-    // quantisation errors only for this rank's share of the correction
-    if (c0 + r >= eps_lo && c0 + r < eps_hi) epsT[(c0 + r) * n_pad + i0 + tx] = etile[tx][r];
+  if (q16 && c0 < PC) {
+    for (int r = ty; r < 32; r += 4)
+      xqT[(c0 / 2 + r) * n_pad + i0 + tx] = tile[tx][2 * r] | (tile[tx][2 * r + 1] << 16);
+  } else {
+    const int64_t row0 = q16 ? c0 - PC / 2 : c0;  // discrete rows follow the packed ones
+    for (int r = ty; r < 64; r += 4) xqT[(row0 + r) * n_pad + i0 + tx] = tile[tx][r];
   }
+  // quantisation errors only for this rank's share of the correction
+  for (int r = ty; r < 64; r += 4)
+    if (c0 + r >= eps_lo && c0 + r < eps_hi) epsT[(c0 + r) * n_pad + i0 + tx] = etile[tx][r];
 }
 
-// Mean-distance correction.  With q = round(t), t = (x - min) * recip * SC,
-// the quantised row mean is biased by (1/(n-1)) sum_f eps_if (2 rank_if -
-// (n-1)) where eps = q - t and rank_if is the rank of sample i in column f
-// (sum_j sign(t_if - t_jf)); the other error terms are random and ~sqrt(n)
-// smaller.  Ranks come from a 4096-bin histogram of q (midrank
-// inside a bin); the rank error it leaves is far below the reference's own
-// float32 rounding.  In place: epsT[c][i] <- eps * (2 rank - (n-1)).
+// Mean-distance correction.  With q = round(t), t = (x - min) * recip * SC
+// and eps = q - t (|eps| <= 1/2), q_j < q_i implies t_j <= t_i, so for every
+// pair |q_i - q_j| - |t_i - t_j| = sign(t_i - t_j) (eps_i - eps_j) exactly
+// (equal q included).  Summed over j, the quantised row sum of column f is
+// off by
+//   A_i - B_i,  A_i = eps_i (2 rank_i - (n-1)),
+//               B_i = sum_{t_j < t_i} eps_j - sum_{t_j > t_i} eps_j
+// (rank_i = #{t_j < t_i} + #ties / 2).  Both come from one 4096-bin
+// histogram of q whose u64 counters pack the count (bits 44..63) and the sum
+// of eps * 2^24 + 2^23 (bits 0..43; exact for n < 2^20), so one LDS atomic
+// and one scan serve both: samples in other bins
+// are ordered exactly, those sharing i's bin are taken as midrank / zero --
+// the residual is a few samples' eps per feature, far below the reference's
+// own float32 rounding for 32-bit operands and ~1e-7 of a scaled-diff unit
+// per row for 16-bit ones.
+// In place: epsT[c][i] <- A_i - B_i (integer units).
 constexpr int kRankBins = 4096;
-__global__ __launch_bounds__(256) void k_colrank(const uint32_t* __restrict__ xqT, int64_t n,
-                                                 int64_t n_pad, int shift, int64_t c_lo,
-                                                 float* __restrict__ epsT) {
-  __shared__ uint32_t hist[kRankBins];
-  __shared__ uint32_t wsum[4];
-  const int64_t c = c_lo + blockIdx.x;
-  const uint32_t* q = xqT + c * n_pad;
-  float* e = epsT + c * n_pad;
-  for (int b = threadIdx.x; b < kRankBins; b += 256) hist[b] = 0;
-  __syncthreads();
-  for (int64_t i = threadIdx.x; i < n; i += 256) atomicAdd(&hist[min((int)(q[i] >> shift), kRankBins - 1)], 1u);
-  __syncthreads();
-  // exclusive scan of 4096 bins: 256 threads x 16 bins
-  uint32_t loc[16], run = 0;
+__device__ __forceinline__ uint32_t col_q(const uint32_t* __restrict__ xqT, int64_t c, int64_t i,
+                                          int64_t n_pad, int q16) {
+  return q16 ? (xqT[(c >> 1) * n_pad + i] >> ((c & 1) * 16)) & 0xFFFFu : xqT[c * n_pad + i];
+}
+
+// Block-wide (256 threads) in-place exclusive scan of 4096 counters,
+// 16 consecutive bins per thread; returns the grand total.
+template <typename U>
+__device__ U scan_bins_4096(U* bins, U* wsum) {
+  U loc[16], run = 0;
   const int base = threadIdx.x * 16;
 #pragma unroll
   for (int k = 0; k < 16; k++) {
     loc[k] = run;
-    run += hist[base + k];
+    run += bins[base + k];
   }
-  // block scan of the per-thread totals
-  uint32_t v = run;
+  U v = run;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t t = __shfl_up(v, o);
+    const U t = __shfl_up(v, o);
     if (lane >= o) v += t;
   }
   if (lane == 63) wsum[wave] = v;
   __syncthreads();
-  uint32_t wpre = 0;
+  U wpre = 0;
   for (int w = 0; w < wave; w++) wpre += wsum[w];
-  const uint32_t excl = wpre + v - run;
+  const U total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+  const U excl = wpre + v - run;
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < 16; k++) hist[base + k] = excl + loc[k];  // exclusive cumulative count
+  for (int k = 0; k < 16; k++) bins[base + k] = excl + loc[k];
   __syncthreads();
-  // midrank needs the bin count too: cum[b+1] - cum[b]
+  return total;
+}
+
+constexpr int kColHistShift = 44;
+constexpr double kColEpsScale = 16777216.0;  // eps fixed point 2^24
+__device__ __forceinline__ unsigned long long col_hist_code(float e) {
+  const long long fx = __double2ll_rn((double)e * kColEpsScale);  // |fx| <= 2^23
+  return (1ull << kColHistShift) + (unsigned long long)(fx + (1ll << 23));
+}
+__device__ __forceinline__ void col_hist_decode(unsigned long long v, double& cnt, double& esum) {
+  const unsigned long long c = v >> kColHistShift;
+  const long long s = (long long)(v & ((1ull << kColHistShift) - 1ull)) - (long long)(c << 23);
+  cnt = (double)c;
+  esum = (double)s / kColEpsScale;
+}
+
+__global__ __launch_bounds__(256) void k_colrank(const uint32_t* __restrict__ xqT, int64_t n,
+                                                 int64_t n_pad, int shift, int q16, int64_t c_lo,
+                                                 float* __restrict__ epsT) {
+  __shared__ unsigned long long hist[kRankBins];
+  __shared__ unsigned long long wsum[4];
+  const int64_t c = c_lo + blockIdx.x;
+  float* e = epsT + c * n_pad;
+  for (int b = threadIdx.x; b < kRankBins; b += 256) hist[b] = 0ull;
+  __syncthreads();
   for (int64_t i = threadIdx.x; i < n; i += 256) {
-    const int b = min((int)(q[i] >> shift), kRankBins - 1);
-    const uint32_t lo = hist[b];
-    const uint32_t hi = b + 1 < kRankBins ? hist[b + 1] : (uint32_t)n;
-    const double rank = (double)lo + 0.5 * (double)(hi - lo - 1u);
-    e[i] = (float)((double)e[i] * (2.0 * rank - (double)(n - 1)));
+    const int b = min((int)(col_q(xqT, c, i, n_pad, q16) >> shift), kRankBins - 1);
+    atomicAdd(&hist[b], col_hist_code(e[i]));
+  }
+  __syncthreads();
+  const unsigned long long tot = scan_bins_4096(hist, wsum);  // exclusive prefix
+  double n_all, e_all;
+  col_hist_decode(tot, n_all, e_all);
+  for (int64_t i = threadIdx.x; i < n; i += 256) {
+    const int b = min((int)(col_q(xqT, c, i, n_pad, q16) >> shift), kRankBins - 1);
+    double c_lo_, e_lo, c_hi_, e_hi;
+    col_hist_decode(hist[b], c_lo_, e_lo);
+    col_hist_decode(b + 1 < kRankBins ? hist[b + 1] : tot, c_hi_, e_hi);
+    const double rank = c_lo_ + 0.5 * (c_hi_ - c_lo_ - 1.0);
+    const double B = e_lo - (e_all - e_hi);
+    e[i] = (float)((double)e[i] * (2.0 * rank - (double)(n - 1)) - B);
   }
 }
 
@@ -237,9 +294,11 @@ __global__ __launch_bounds__(1024) void k_rowcorr(const float* __restrict__ epsT
 // flight while chunk c is consumed.  u32 accumulators absorb 256 features,
 // then their bits >= 24 move into 16-bit halves of a packed high word, so the
 // final distance D = hi * 2^24 + lo is exact below 2^40.
-// One 16-feature chunk of SADs (continuous) or mismatch counts (discrete)
-// from an LDS panel pair.
-template <bool DISC>
+// One 16-row chunk from an LDS panel pair: SADs of 32-bit operands
+// (kModeU32), of packed 16-bit pairs (kModeU16: 32 features) or mismatch
+// counts (kModeDisc).
+constexpr int kModeU32 = 0, kModeU16 = 1, kModeDisc = 2;
+template <int MODE>
 __device__ __forceinline__ void dist_chunk(const uint32_t* __restrict__ A,
                                            const uint32_t* __restrict__ B, int tx, int ty,
                                            uint32_t sc_disc, uint32_t (&acc)[8][8]) {
@@ -255,8 +314,9 @@ __device__ __forceinline__ void dist_chunk(const uint32_t* __restrict__ A,
     for (int r = 0; r < 8; r++)
 #pragma unroll
       for (int c = 0; c < 8; c++)
-        acc[r][c] = DISC ? mismatch_u32(av[r], bv[c], sc_disc, acc[r][c])
-                         : sad_u32(av[r], bv[c], acc[r][c]);
+        acc[r][c] = MODE == kModeDisc  ? mismatch_u32(av[r], bv[c], sc_disc, acc[r][c])
+                    : MODE == kModeU16 ? sad_u16(av[r], bv[c], acc[r][c])
+                                       : sad_u32(av[r], bv[c], acc[r][c]);
   }
 }
 
@@ -266,6 +326,7 @@ __device__ __forceinline__ void dist_chunk(const uint32_t* __restrict__ A,
 // runs) thus fills the chip's 2 x CU workgroup slots in more even rounds.
 __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xqT, int64_t n_pad,
                                                  int nck_cont, int nck_disc, uint32_t sc_disc,
+                                                 int q16,
                                                  const int2* __restrict__ tiles, int splits,
                                                  double* __restrict__ D,
                                                  double* __restrict__ Dpart) {
@@ -329,19 +390,19 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
   // chunk ck+1 is copied while ck is consumed.  Continuous and discrete
   // chunks run in separate loops (one dist_chunk instantiation each), which
   // keeps the register allocation of either loop to itself.
-  auto run = [&](auto disc_tag, int c0, int c1) {
-    constexpr bool DISC = decltype(disc_tag)::value;
+  auto run = [&](auto mode_tag, int c0, int c1) {
+    constexpr int MODE = decltype(mode_tag)::value;
     if (c0 >= c1) return;
     stage(ldsA0, ldsB0, c0);
     __syncthreads();
     for (int ck = c0; ck < c1; ck += 2) {
       if (ck + 1 < c1) stage(ldsA1, ldsB1, ck + 1);
-      dist_chunk<DISC>(ldsA0, ldsB0, tx, ty, sc_disc, acc);
+      dist_chunk<MODE>(ldsA0, ldsB0, tx, ty, sc_disc, acc);
       if ((ck % kFlushChunks) == kFlushChunks - 1) flush();
       __syncthreads();
       if (ck + 1 < c1) {
         if (ck + 2 < c1) stage(ldsA0, ldsB0, ck + 2);
-        dist_chunk<DISC>(ldsA1, ldsB1, tx, ty, sc_disc, acc);
+        dist_chunk<MODE>(ldsA1, ldsB1, tx, ty, sc_disc, acc);
         if (((ck + 1) % kFlushChunks) == kFlushChunks - 1) flush();
         __syncthreads();
       }
@@ -351,8 +412,12 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
   const int nck_all = nck_cont + nck_disc;
   const int c_begin = (int)((int64_t)nck_all * part / splits);
   const int c_end = (int)((int64_t)nck_all * (part + 1) / splits);  // this part's chunks
-  run(std::false_type{}, c_begin, c_end < nck_cont ? c_end : nck_cont);
-  run(std::true_type{}, c_begin > nck_cont ? c_begin : nck_cont, c_end);
+  // continuous chunks (16-bit pairs or 32-bit values), then discrete ones
+  if (q16)
+    run(std::integral_constant<int, kModeU16>{}, c_begin, c_end < nck_cont ? c_end : nck_cont);
+  else
+    run(std::integral_constant<int, kModeU32>{}, c_begin, c_end < nck_cont ? c_end : nck_cont);
+  run(std::integral_constant<int, kModeDisc>{}, c_begin > nck_cont ? c_begin : nck_cont, c_end);
   flush();
 
   // Epilogue: D[i][j] for the tile and, off the diagonal, the mirror D[j][i].
@@ -655,6 +720,44 @@ __global__ __launch_bounds__(64) void k_surf_avg(const double* __restrict__ D, i
   avg[i] = (double)s / (double)(n - 1);
 }
 
+// Flagged pairs are collected per workgroup in LDS and appended to the
+// global list with one atomic per workgroup (a single global counter hit by
+// every wave that flags a pair serialises in L2).  Overflow of the LDS
+// buffer falls back to direct appends.
+constexpr int kPairBuf = 1024;
+struct PairBuf {
+  int2 v[kPairBuf];
+  unsigned int n;
+  unsigned long long base;
+};
+__device__ __forceinline__ void pairbuf_init(PairBuf& pb) {
+  if (threadIdx.x == 0) pb.n = 0u;
+  __syncthreads();
+}
+__device__ __forceinline__ void pairbuf_add(PairBuf& pb, int64_t i, int64_t j,
+                                            int2* __restrict__ list, int64_t cap,
+                                            unsigned long long* __restrict__ count) {
+  const unsigned int s = atomicAdd(&pb.n, 1u);
+  if (s < (unsigned)kPairBuf) {
+    pb.v[s] = make_int2((int)i, (int)j);
+  } else {
+    const unsigned long long k = atomicAdd(count, 1ull);
+    if ((int64_t)k < cap) list[k] = make_int2((int)i, (int)j);
+  }
+}
+__device__ __forceinline__ void pairbuf_flush(PairBuf& pb, int2* __restrict__ list, int64_t cap,
+                                              unsigned long long* __restrict__ count) {
+  __syncthreads();
+  const unsigned int m = pb.n < (unsigned)kPairBuf ? pb.n : (unsigned)kPairBuf;
+  if (m == 0u) return;
+  if (threadIdx.x == 0) pb.base = atomicAdd(count, (unsigned long long)m);
+  __syncthreads();
+  for (unsigned int t = threadIdx.x; t < m; t += blockDim.x) {
+    const unsigned long long k = pb.base + t;
+    if ((int64_t)k < cap) list[k] = pb.v[t];
+  }
+}
+
 // Ambiguous pairs of the owned tiles: the quantised distance lies within the
 // error band of either endpoint's threshold, so the near/far decision could
 // differ from the reference's.  They are appended to `list` (capacity cap,
@@ -668,28 +771,28 @@ __global__ __launch_bounds__(256) void k_flag_pairs(const double* __restrict__ D
                                                     double inv_sc, double delta,
                                                     int2* __restrict__ list, int64_t cap,
                                                     unsigned long long* __restrict__ count) {
+  __shared__ PairBuf pb;
+  pairbuf_init(pb);
   const int2 tl = tiles[blockIdx.x];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
   for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
     const int jj = e / kTile, ii = e % kTile;
     const int64_t i = i0 + ii, j = j0 + jj;
-    if (!(i < n && j < n && (tl.x < tl.y || ii < jj))) continue;
-    const double d = D[j * n_pad + i];
-    bool amb;
-    if (algo == ALGO_MULTISURF) {
+    bool amb = false;
+    if (!(i < n && j < n && (tl.x < tl.y || ii < jj))) {
+    } else if (algo == ALGO_MULTISURF) {
+      const double d = D[j * n_pad + i];
       amb = __builtin_fabs(d - thr[i]) < delta || __builtin_fabs(d - thr[j]) < delta;
     } else {
-      const double df = d * inv_sc;
+      const double df = D[j * n_pad + i] * inv_sc;
       const float ai = (float)thr[i], aj = (float)thr[j];
       const double bi = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(ai) + 1u) - (double)ai);
       const double bj = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(aj) + 1u) - (double)aj);
       amb = __builtin_fabs(df - thr[i]) < bi || __builtin_fabs(df - thr[j]) < bj;
     }
-    if (amb) {
-      const unsigned long long k = atomicAdd(count, 1ull);
-      if ((int64_t)k < cap) list[k] = make_int2((int)i, (int)j);
-    }
+    if (amb) pairbuf_add(pb, i, j, list, cap, count);
   }
+  pairbuf_flush(pb, list, cap, count);
 }
 
 // Reference-exact distance of each listed pair: sum_f diff_f(i, j) in
@@ -712,13 +815,29 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
     const T* xi = x + (int64_t)pr.x * p_in;
     const T* xj = x + (int64_t)pr.y * p_in;
     double acc = 0.0;
-    for (int64_t c = lane; c < pc; c += 64) {
-      const int64_t col = src_col[c];
-      if (sizeof(T) == 4) {
-        const float dv = __builtin_fabsf((float)xi[col] - (float)xj[col]) * (float)scl[c];
-        acc += (double)dv;
-      } else {
-        acc += __builtin_fabs((double)xi[col] - (double)xj[col]) * scl[c];
+    // 4 features per lane per step: the column indices, then all 8 values,
+    // are requested before any is used (the row reads are latency-bound)
+    constexpr int kU = 4;
+    for (int64_t c0 = lane; c0 < pc; c0 += 64 * kU) {
+      int64_t col[kU];
+      T a[kU], b[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) col[u] = c0 + 64 * u < pc ? src_col[c0 + 64 * u] : -1;
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        a[u] = col[u] >= 0 ? xi[col[u]] : (T)0;
+        b[u] = col[u] >= 0 ? xj[col[u]] : (T)0;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        if (col[u] < 0) break;
+        const int64_t c = c0 + 64 * u;
+        if (sizeof(T) == 4) {
+          const float dv = __builtin_fabsf((float)a[u] - (float)b[u]) * (float)scl[c];
+          acc += (double)dv;
+        } else {
+          acc += __builtin_fabs((double)a[u] - (double)b[u]) * scl[c];
+        }
       }
     }
     for (int64_t c = PC + lane; c < PC + pd; c += 64) {
@@ -1174,19 +1293,24 @@ __global__ __launch_bounds__(256) void k_rf_flag(const double* __restrict__ D, i
                                                  double band_abs, double band_rel, int64_t row0,
                                                  int2* __restrict__ list, int64_t cap,
                                                  unsigned long long* __restrict__ count) {
+  __shared__ PairBuf pb;
+  pairbuf_init(pb);
   const int64_t i = row0 + blockIdx.x;
   const double* row = D + i * n_pad;
-  for (int64_t j = threadIdx.x; j < n; j += 256) {
-    if (j == i) continue;
-    const int32_t c = lab[j];
-    if (tneed[i * n_classes + c] == 0) continue;  // class taken whole
-    const double T = (double)__uint_as_float(tkey[i * n_classes + c]);
-    const double kv = (double)__uint_as_float(rf_key(row[j], inv_sc));
-    if (fabs(kv - T) <= band_abs + band_rel * T) {
-      const unsigned long long slot = atomicAdd(count, 1ull);
-      if ((int64_t)slot < cap) list[slot] = make_int2((int)i, (int)j);
+  for (int64_t j0 = 0; j0 < n; j0 += 256) {
+    const int64_t j = j0 + threadIdx.x;
+    bool flag = false;
+    if (j < n && j != i) {
+      const int32_t c = lab[j];
+      if (tneed[i * n_classes + c] != 0) {  // 0: class taken whole
+        const double T = (double)__uint_as_float(tkey[i * n_classes + c]);
+        const double kv = (double)__uint_as_float(rf_key(row[j], inv_sc));
+        flag = fabs(kv - T) <= band_abs + band_rel * T;
+      }
     }
+    if (flag) pairbuf_add(pb, i, j, list, cap, count);
   }
+  pairbuf_flush(pb, list, cap, count);
 }
 
 // Exact reference keys of whole rows (tie rows of a problem with continuous
@@ -1509,6 +1633,7 @@ struct Plan {
   bool own_stream = false;
   int64_t nb = 0, n_tiles = 0, seg_len = 1, nseg = 1;
   int ksplit = 1;               // pass-1 K-split parts (k_dist)
+  int use_q16 = 0;              // pass 1 on packed 16-bit continuous operands
   int64_t c_lo = 0, c_hi = 0;   // this rank's continuous columns of the mean correction
   int64_t r_lo = 0, r_hi = 0;   // focal rows scored by this plan (row sharding)
   double2* rspart = nullptr;    // per owned tile row-moment partials [tiles][256]
@@ -1639,6 +1764,24 @@ static int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats,
   return best;
 }
 
+// 16-bit pass-1 operands (Prepared::q16) halve k_dist.  ReliefF stays exact
+// with them (every candidate near a k-th key gets its reference key), so it
+// uses them from kQ16MinRowsRF samples on.  MultiSURF's threshold mu - sigma/2
+// comes from the quantised row moments: the sigma error grows as 1/SC and the
+// score error it causes (pairs decided on the wrong side of a threshold, each
+// worth ~1/n^2) falls as ~n^-1.25 -- measured against the 32-bit path: 8.8e-6
+// scale-relative at n=5000, 3.9e-6 at 8192, 1.9e-6 at 20000 --
+// so MultiSURF takes them only from kQ16MinRowsMS samples on.  FS_Q16=0/1 in
+// the environment forces the choice (tests).  SURF has its own float64 pass.
+constexpr int64_t kQ16MinRowsRF = 4096, kQ16MinRowsMS = 16384;
+static int choose_q16(const Prepared& P) {
+  if (P.algo == ALGO_SURF) return 0;
+  const char* env = std::getenv("FS_Q16");
+  if (env && *env) return std::atoi(env) != 0 ? 1 : 0;
+  const int64_t min_rows = P.algo == ALGO_RELIEFF ? kQ16MinRowsRF : kQ16MinRowsMS;
+  return (P.n >= min_rows && P.pc >= kFeatPad) ? 1 : 0;
+}
+
 // Feature-layout part of a plan: everything sized by the kept features
 // (permutation tables, quantised operands, pass-2 partials), rebuilt when
 // the plan is re-targeted to another feature subset (fs_plan_set_features).
@@ -1648,6 +1791,7 @@ static int plan_layout(Plan* g) {
   for (void* q : g->owned_layout) (void)hipFree(q);
   g->owned_layout.clear();
   int rc;
+  Q.q16 = g->use_q16;
   if (!Q.ranges_ready) {
     // continuous column ranges, measured on the device once per plan
     const size_t esz = g->x_is_f64 ? 8 : 4;
@@ -1724,6 +1868,10 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     set_error("invalid rank/world");
     return FS_EINVAL;
   }
+  if (P.n >= (1 << 20)) {  // k_colrank's packed histogram; D alone would be 8 TB
+    set_error("the GPU backend supports fewer than 2^20 samples");
+    return FS_ENOTSUP;
+  }
   const bool row_mode = r_hi >= 0;
   if (row_mode && !(0 <= r_lo && r_lo <= r_hi && r_hi <= P.n)) {
     set_error("row range outside [0, n)");
@@ -1768,7 +1916,11 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   std::vector<int2> tl(g->n_tiles);
   for (int64_t t = 0; t < g->n_tiles; t++) tl[t] = make_int2(bi[t], bj[t]);
   g->list_cap = std::max<int64_t>(1 << 16, Q.n * 64);
-  g->ksplit = choose_ksplit(g->n_tiles, device, (int)((Q.PC + Q.PD) / kBKQ), Q.pc + Q.pd,
+  g->use_q16 = choose_q16(Q);
+  // pass-1 chunk count and the per-tile work in feature units of 32-bit SAD
+  const int64_t rows_q = (g->use_q16 ? Q.PC / 2 : Q.PC) + Q.PD;
+  g->ksplit = choose_ksplit(g->n_tiles, device, (int)(rows_q / kBKQ),
+                            (g->use_q16 ? Q.pc / 2 : Q.pc) + Q.pd,
                             (size_t)Q.n_pad * Q.n_pad * sizeof(double));
   if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
   const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
@@ -1827,19 +1979,21 @@ static int run_quantize_dist(Plan* g) {
   }
   if (g->x_is_f64)
     k_quantize<double><<<gq, 256, 0, g->stream>>>(
-        (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, g->src_col, g->off, g->qs, g->scl,
-        g->dtab_off, g->dtab, Q.disc_bits, g->c_lo, g->c_hi, g->xqT, g->xs, g->epsT);
+        (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
+        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, g->c_lo, g->c_hi, g->xqT, g->xs,
+        g->epsT);
   else
     k_quantize<float><<<gq, 256, 0, g->stream>>>(
-        (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.pc, g->src_col, g->off, g->qs, g->scl,
-        g->dtab_off, g->dtab, Q.disc_bits, g->c_lo, g->c_hi, g->xqT, g->xs, g->epsT);
+        (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
+        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, g->c_lo, g->c_hi, g->xqT, g->xs,
+        g->epsT);
   FS_TRY(launch_check("k_quantize"));
   if (Q.algo == ALGO_MULTISURF) {
     // mean correction of this rank's feature share (summed across ranks
     // with the row moments)
     if (g->c_hi > g->c_lo) {
       k_colrank<<<(unsigned)(g->c_hi - g->c_lo), 256, 0, g->stream>>>(
-          g->xqT, Q.n, Q.n_pad, g->rank_shift, g->c_lo, g->epsT);
+          g->xqT, Q.n, Q.n_pad, g->rank_shift, Q.q16, g->c_lo, g->epsT);
       FS_TRY(launch_check("k_colrank"));
     }
     k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, g->stream>>>(g->epsT, Q.n, Q.n_pad, g->c_lo,
@@ -1849,8 +2003,8 @@ static int run_quantize_dist(Plan* g) {
   if (g->n_tiles > 0) {
     FS_HIP(hipEventRecord(g->ev[0], g->stream));
     k_dist<<<(unsigned)(g->n_tiles * g->ksplit), 256, 0, g->stream>>>(
-        g->xqT, Q.n_pad, (int)(Q.PC / kBKQ), (int)(Q.PD / kBKQ), Q.SCu, g->tiles, g->ksplit, g->D,
-        g->Dpart);
+        g->xqT, Q.n_pad, (int)((Q.q16 ? Q.PC / 2 : Q.PC) / kBKQ), (int)(Q.PD / kBKQ), Q.SCu,
+        Q.q16, g->tiles, g->ksplit, g->D, g->Dpart);
     FS_TRY(launch_check("k_dist"));
     if (g->ksplit > 1) {
       k_dist_merge<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, g->Dpart, g->ksplit - 1,

@@ -85,6 +85,12 @@ struct Prepared {
   // discrete columns of a float32 X are coded by their value bits (equality
   // is all the kernels use), so no value tables are built on the host
   int disc_bits = 0;
+  // GPU pass 1 on 16-bit continuous operands: q <= 65535 (SC ~ 2^16), two
+  // features packed per u32 word and compared by one v_sad_u16 (twice the
+  // pair-feature rate of v_sad_u32).  finalize_scale picks SC accordingly;
+  // the wider quantisation error is absorbed by amb_delta (more pairs are
+  // recomputed exactly) and the mean correction (k_colrank).
+  int q16 = 0;
 };
 
 // Build the permutation, label codes, discrete tables and integer scale.

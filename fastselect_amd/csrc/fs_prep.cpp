@@ -170,7 +170,9 @@ int finalize_scale(Prepared& P, const double* cmin, const double* cmax) {
   const double feats = (double)(P.pc + P.pd);
   const double lim_a = ((4294967295.0 - 16777216.0) / 256.0 - 1.0) / Rm;
   const double lim_b = (1099511627775.0 / feats - 1.0) / Rm;
-  const double sc = std::floor(std::min(lim_a, lim_b));
+  // 16-bit operands: q = round(t) <= Rm * SC + 0.5 must stay <= 65535
+  const double lim_16 = P.q16 ? 65534.0 / Rm : lim_a;
+  const double sc = std::floor(std::min(std::min(lim_a, lim_16), lim_b));
   if (!(sc >= 1.0)) {
     set_error("too many features for the 40-bit integer distance");
     return -1;
@@ -181,10 +183,12 @@ int finalize_scale(Prepared& P, const double* cmin, const double* cmax) {
   // Error model of a quantised distance vs the reference's (float64 sum of
   // float32-rounded diffs): per continuous feature a rounding error of at
   // most 1/SC (std ~ 1/sqrt(6)/SC) plus the reference's own float32
-  // rounding (< 1.2e-7 relative).  16 standard deviations of the sum bound
-  // both the distance and the threshold error with a wide margin.
+  // rounding (< 1.2e-7 relative).  12 standard deviations of the sum (a
+  // tail of 4e-33 per pair; the sum of bounded terms has lighter tails than
+  // a Gaussian, and for pc <= 23 the band exceeds the worst case pc / SC)
+  // bound the distance error; the threshold error is far smaller.
   const double pcd = (double)P.pc;
-  P.amb_delta = 16.0 * std::sqrt(pcd / 6.0 + 1.0) / sc + 4.0e-7 * std::sqrt(pcd);
+  P.amb_delta = 12.0 * std::sqrt(pcd / 6.0 + 1.0) / sc + 4.0e-7 * std::sqrt(pcd);
   P.ranges_ready = 1;
   return 0;
 }

@@ -1,0 +1,68 @@
+"""Pass 1 on packed 16-bit operands (Prepared::q16, v_sad_u16): the default
+for ReliefF from n = 4096 and for MultiSURF from n = 16384 samples.  Same bar
+as every parity test: 1e-5 scale-relative and identical top-k.
+
+ReliefF is exact with them (the band of exactly recomputed keys widens), so
+it is forced on (FS_Q16=1) at sizes the oracle runs in seconds.  MultiSURF's
+thresholds carry a quantisation error whose score effect falls as ~n^-1.25
+(DESIGN.md §2): it is checked against the oracle at n = 16384 (its default
+size) and against the 32-bit path at n = 20000.
+"""
+import numpy as np
+import pytest
+from conftest import assert_parity, scale_rel_err
+from sklearn.datasets import make_classification
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def _fit(cls, X, y, **kw):
+    est = cls(backend="gpu", n_features_to_select=1, **kw).fit(X, y)
+    assert est.effective_backend_ == "gpu"
+    return est.feature_importances_
+
+
+def test_q16_mixed_blocks_relieff(oracle, monkeypatch):
+    from fastselect_amd import ReliefF
+    monkeypatch.setenv("FS_Q16", "1")
+    rng = np.random.default_rng(5)
+    n = 2000
+    Xc = rng.standard_normal((n, 300)) * rng.uniform(0.1, 10, 300)
+    Xd = rng.integers(0, 4, size=(n, 70)).astype(np.float64)
+    X = np.concatenate([Xc, Xd], axis=1)[:, rng.permutation(370)]
+    y = (X[:, 0] + X[:, 5] > 0).astype(int)
+    assert_parity(_fit(ReliefF, X, y, n_neighbors=5), oracle.relieff_scores(X, y, n_neighbors=5),
+                  TOL, k=10)
+
+
+@pytest.mark.parametrize("k,ncls", [(10, 2), (3, 3)])
+def test_q16_relieff_parity(oracle, monkeypatch, k, ncls):
+    from fastselect_amd import ReliefF
+    monkeypatch.setenv("FS_Q16", "1")
+    X, y = make_classification(n_samples=3000, n_features=500, n_informative=20,
+                               n_redundant=20, n_classes=ncls, random_state=k)
+    assert_parity(_fit(ReliefF, X, y, n_neighbors=k),
+                  oracle.relieff_scores(X, y, n_neighbors=k), TOL, k=10)
+
+
+@pytest.mark.slow
+def test_q16_multisurf_default_at_16384(oracle):
+    """n = 16384 takes the 16-bit path by default (oracle: ~2e10 PFE)."""
+    from fastselect_amd import MultiSURF
+    X, y = make_classification(n_samples=16384, n_features=128, n_informative=20,
+                               n_redundant=30, random_state=42)
+    assert_parity(_fit(MultiSURF, X, y), oracle.multisurf_scores(X, y), TOL, k=10)
+
+
+def test_q16_agrees_with_u32_path(monkeypatch):
+    from fastselect_amd import MultiSURF, ReliefF
+    X, y = make_classification(n_samples=20000, n_features=2000, n_informative=20,
+                               n_redundant=50, random_state=42)
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("FS_Q16", flag)
+        out[flag] = (_fit(MultiSURF, X, y), _fit(ReliefF, X, y, n_neighbors=10))
+    for a, b in zip(out["0"], out["1"]):
+        assert scale_rel_err(b, a) < 5e-6
+        assert set(np.argsort(a)[::-1][:10]) == set(np.argsort(b)[::-1][:10])

@@ -18,6 +18,12 @@ constexpr int ITERS = 1 << 15;
     : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4), "+v"(c5), "+v"(c6), "+v"(c7) \
     : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5), "v"(a6), "v"(a7), "v"(b))
 
+#define SADX(op, b) \
+  asm volatile(op " %0, %8, %16, %0\n " op " %1, %9, %16, %1\n " op " %2, %10, %16, %2\n " op " %3, %11, %16, %3\n" \
+               op " %4, %12, %16, %4\n " op " %5, %13, %16, %5\n " op " %6, %14, %16, %6\n " op " %7, %15, %16, %7\n" \
+    : "+v"(c0), "+v"(c1), "+v"(c2), "+v"(c3), "+v"(c4), "+v"(c5), "+v"(c6), "+v"(c7) \
+    : "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5), "v"(a6), "v"(a7), "v"(b))
+
 #define ADD8(op, b) \
   asm volatile(op " %0, %8, %16\n " op " %1, %9, %16\n " op " %2, %10, %16\n " op " %3, %11, %16\n " \
                op " %4, %12, %16\n " op " %5, %13, %16\n " op " %6, %14, %16\n " op " %7, %15, %16\n" \
@@ -53,6 +59,14 @@ __global__ void __launch_bounds__(256) kern(const uint32_t* in, uint32_t* out) {
         "v_pk_add_f32 %4, %4, %8\n v_pk_add_f32 %5, %5, %8\n v_pk_add_f32 %6, %6, %8\n v_pk_add_f32 %7, %7, %8\n"
         : "+v"(p0), "+v"(p1), "+v"(p2), "+v"(p3), "+v"(p4), "+v"(p5), "+v"(p6), "+v"(p7) : "v"(pb));
     }
+    if (MIX == 6) { SADX("v_sad_u16", b); SADX("v_sad_u16", b); SADX("v_sad_u16", b); SADX("v_sad_u16", b); }
+    if (MIX == 7) { SADX("v_sad_u8", b); SADX("v_sad_u8", b); SADX("v_sad_u8", b); SADX("v_sad_u8", b); }
+    if (MIX == 8) { ADD8("v_pk_sub_u16", b); ADD8("v_pk_sub_u16", b); ADD8("v_pk_sub_u16", b); ADD8("v_pk_sub_u16", b); }
+    if (MIX == 9) { SADX("v_dot2_u32_u16", b); SADX("v_dot2_u32_u16", b); SADX("v_dot2_u32_u16", b); SADX("v_dot2_u32_u16", b); }
+    if (MIX == 10) { SADX("v_sad_hi_u8", b); SADX("v_sad_hi_u8", b); SADX("v_sad_hi_u8", b); SADX("v_sad_hi_u8", b); }
+    if (MIX == 11) { SADX("v_mad_u32_u24", b); SADX("v_mad_u32_u24", b); SADX("v_mad_u32_u24", b); SADX("v_mad_u32_u24", b); }
+    if (MIX == 12) { ADD8("v_sub_u32", b); ADD8("v_sub_u32", b); ADD8("v_sub_u32", b); ADD8("v_sub_u32", b); }
+    if (MIX == 13) { SADX("v_fma_f32", b); SADX("v_fma_f32", b); SADX("v_fma_f32", b); SADX("v_fma_f32", b); }
     b += 1;
   }
   out[blockIdx.x * blockDim.x + threadIdx.x] = c0 + c1 + c2 + c3 + c4 + c5 + c6 + c7 + t0 + t1 + t2 + t3 + (uint32_t)(p0 + p1 + p2 + p3 + p4 + p5 + p6 + p7);
@@ -79,14 +93,22 @@ int main() {
   CHK(hipMemset(in, 1, 4096 * 4));
   // instructions per lane in the timed loop (asm body); loop overhead ~3 scalar/vector instrs per iter
   const double lanes = (double)blocks * 256;
-  struct { const char* nm; float ms; double instr_per_iter; } r[6];
+  struct { const char* nm; float ms; double instr_per_iter; } r[14];
   r[0] = {"v_sad_u32", run<0>(blocks, in, out), 32};
   r[1] = {"v_add_f32", run<1>(blocks, in, out), 32};
   r[2] = {"v_add_u32", run<2>(blocks, in, out), 32};
   r[3] = {"v_max_f32", run<3>(blocks, in, out), 32};
   r[4] = {"v_sub_f32 + v_add_f32|abs|", run<4>(blocks, in, out), 16};
   r[5] = {"v_pk_add_f32", run<5>(blocks, in, out), 8};
-  for (int m = 0; m < 6; m++) {
+  r[6] = {"v_sad_u16", run<6>(blocks, in, out), 32};
+  r[7] = {"v_sad_u8", run<7>(blocks, in, out), 32};
+  r[8] = {"v_pk_sub_u16", run<8>(blocks, in, out), 32};
+  r[9] = {"v_dot2_u32_u16", run<9>(blocks, in, out), 32};
+  r[10] = {"v_sad_hi_u8", run<10>(blocks, in, out), 32};
+  r[11] = {"v_mad_u32_u24", run<11>(blocks, in, out), 32};
+  r[12] = {"v_sub_u32", run<12>(blocks, in, out), 32};
+  r[13] = {"v_fma_f32", run<13>(blocks, in, out), 32};
+  for (int m = 0; m < 14; m++) {
     double winstr = lanes / 64.0 * ITERS * r[m].instr_per_iter;   // wave-instructions
     double per_simd = winstr / 1024.0;
     printf("%-30s %8.3f ms  %8.3f Twave-instr/s  -> %.3f G wave-instr/s/SIMD (cycles/instr at 2.4GHz: %.2f)\n",
