@@ -120,12 +120,22 @@ __global__ __launch_bounds__(256) void k_quantize(
   const int64_t c = c0 + tx;
   const int64_t col = src_col[c];
   const bool is_cont = c < pc;
-  for (int r = ty; r < 64; r += 4) {
+  // all 16 of this thread's loads are issued before any value is used
+  constexpr int kR = 16;
+  T xr[kR];
+#pragma unroll
+  for (int k = 0; k < kR; k++) {
+    const int64_t i = i0 + ty + 4 * k;
+    xr[k] = (i < n && col >= 0) ? x[i * p_in + col] : (T)0;
+  }
+#pragma unroll
+  for (int k = 0; k < kR; k++) {
+    const int r = ty + 4 * k;
     const int64_t i = i0 + r;
     uint32_t q = 0;
     float v = 0.0f, e = 0.0f;
     if (i < n && col >= 0) {
-      const double xv = (double)x[i * p_in + col];
+      const double xv = (double)xr[k];
       if (is_cont) {
         const double u = __dadd_rn(xv, -off[c]);
         const double t = __dmul_rn(u, qs[c]);
@@ -1663,6 +1673,8 @@ struct Plan {
   unsigned long long* list_count = nullptr;
   int64_t n_refined = 0;
   int64_t n_tie_rows = 0;      // ReliefF rows re-ordered by k_rf_ties
+  void* sort_scratch = nullptr;  // pair-list sort (fs_sort.hip)
+  size_t sort_scratch_bytes = 0;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<void*> owned;         // buffers sized by n (live as long as the plan)
   std::vector<void*> owned_layout;  // buffers sized by the feature layout (PW)
@@ -2016,6 +2028,25 @@ static int run_quantize_dist(Plan* g) {
   return FS_OK;
 }
 
+// Order the first `count` pairs of g->list by (i, j) (see fs_sort.hip).
+static int sort_pair_list(Plan* g, int64_t count) {
+  if (count < 2) return FS_OK;
+  const size_t need = pair_sort_scratch_bytes(count);
+  if (need == 0) {
+    set_error("pair list sort: temporary storage query failed");
+    return FS_EHIP;
+  }
+  if (need > g->sort_scratch_bytes) {
+    char* p = nullptr;
+    FS_TRY(dalloc(g, &p, need + need / 4));
+    g->sort_scratch = p;
+    g->sort_scratch_bytes = need + need / 4;
+  }
+  return sort_pairs(g->list, count, g->sort_scratch, g->sort_scratch_bytes, g->stream) == 0
+             ? FS_OK
+             : FS_EHIP;
+}
+
 // Flag the ambiguous pairs of the owned tiles and recompute them exactly.
 // One host round trip reads the pair count (to grow the list if needed).
 static int refine_pairs(Plan* g, int algo, double delta) {
@@ -2039,6 +2070,7 @@ static int refine_pairs(Plan* g, int algo, double delta) {
     FS_TRY(dalloc(g, &g->list, g->list_cap));
   }
   if (g->n_refined == 0) return FS_OK;
+  FS_TRY(sort_pair_list(g, g->n_refined));
   const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
   if (g->x_is_f64)
     k_exact_pairs<double><<<grid, 256, 0, g->stream>>>(
@@ -2250,6 +2282,7 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
     FS_TRY(dalloc(g, &g->list, g->list_cap));
   }
   if (g->n_refined > 0) {
+    FS_TRY(sort_pair_list(g, g->n_refined));
     const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
     k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
         (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,

@@ -262,6 +262,11 @@ int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap,
 // x's dtype; runs on `stream` (a hipStream_t) and synchronises it.
 int column_minmax(const void* dx, int x_is_f64, int64_t n, int64_t p, void* hmin, void* hmax,
                   void* stream);
+// Sort a pair list (int2 (i, j) entries) by (i, j) in place (fs_sort.hip);
+// scratch of pair_sort_scratch_bytes(count) bytes of device memory, `stream`
+// a hipStream_t.
+size_t pair_sort_scratch_bytes(int64_t count);
+int sort_pairs(void* list, int64_t count, void* scratch, size_t scratch_bytes, void* stream);
 struct Plan;
 // Tile sharding (MultiSURF): tile t belongs to rank t % world.  Row
 // sharding (r_hi >= 0): the tiles touching the 128-row blocks of [r_lo, r_hi).
