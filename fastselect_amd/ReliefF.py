@@ -119,6 +119,37 @@ class ReliefF(TransformerMixin, BaseEstimator):
         self.top_features_ = _base.top_features(scores, n_select)
         return self
 
+    def _resident_scorer(self, x, y):
+        """A scorer for TuRF that keeps X resident and re-scores column
+        subsets (``ResidentRows``); None when there is nothing to score
+        (a single class: TuRF then refits, which yields zeros)."""
+        from ._resident import ResidentRows
+        x, y = validate_data(self, x, y, dtype=np.float64, ensure_2d=True, y_numeric=True)
+        n = x.shape[0]
+        self._validate_parameters(n, x.shape[1])
+        classes, y_encoded = np.unique(y, return_inverse=True)
+        if len(classes) < 2:
+            return None
+        self.classes_ = classes
+        min_class_size = np.min(np.bincount(y_encoded))
+
+        def warn_small_class():
+            if self.n_neighbors >= min_class_size:
+                warnings.warn(
+                    f"n_neighbors ({self.n_neighbors}) is greater than or equal to the "
+                    f"smallest class size ({min_class_size}).",
+                    UserWarning,
+                )
+
+        where = "gpu" if self.backend != "cpu" and _lib.gpu_available() else "cpu"
+        x32, y_enc, recip, is_discrete, class_probs = relieff_inputs(
+            x, y, self.discrete_limit, where)
+        self.effective_backend_ = _base.effective_backend(self.backend)
+        plan = _lib.RowsPlan(self.effective_backend_, "relieff", x32, y_enc, recip, is_discrete,
+                             k=self.n_neighbors, class_probs=class_probs, n_jobs=self.n_jobs)
+        return ResidentRows(self, "ReliefF", plan, n, is_discrete, self.effective_backend_,
+                            before_score=warn_small_class)
+
     def transform(self, x: np.ndarray) -> np.ndarray:
         """Reduce x to the selected features."""
         check_is_fitted(self)

@@ -94,6 +94,25 @@ class SURF(TransformerMixin, BaseEstimator):
             print("Feature scoring completed.")
         return self
 
+    def _resident_scorer(self, X, y):
+        """A scorer for TuRF that keeps X resident and re-scores column
+        subsets (``ResidentRows``)."""
+        from ._resident import ResidentRows
+        X, y = validate_data(self, X, y, y_numeric=True, dtype=np.float64, ensure_2d=True)
+        n = X.shape[0]
+        self._validate_parameters(n, X.shape[1])
+        if self.backend == "auto":
+            self.effective_backend_ = "gpu" if _lib.gpu_available() else "cpu"
+        elif self.backend == "gpu" and not _lib.gpu_available():
+            raise RuntimeError(SURF_GPU_MISSING)
+        else:
+            self.effective_backend_ = self.backend
+        is_discrete, recip = surf_inputs(X, self.discrete_limit, self.effective_backend_)
+        plan = _lib.RowsPlan(self.effective_backend_, "surf", X, y.astype(np.int32), recip,
+                             is_discrete, use_star=self.use_star, n_jobs=self.n_jobs)
+        return ResidentRows(self, "SURF*" if self.use_star else "SURF", plan, n, is_discrete,
+                            self.effective_backend_)
+
     def transform(self, x: np.ndarray) -> np.ndarray:
         """Reduce x to the selected features."""
         check_is_fitted(self)

@@ -3,8 +3,8 @@
 Iterative Relief: score with a base estimator, drop the lowest-scoring
 ``pct_remove`` fraction of the remaining features (at least one, never going
 below ``n_features_to_select``), re-score on the survivors, repeat.  It works
-with any estimator exposing ``feature_importances_``, in particular the
-MI355X ``ReliefF`` / ``SURF`` / ``MultiSURF`` of this package.
+with any estimator exposing ``feature_importances_``; the MI355X ``ReliefF``
+/ ``SURF`` / ``MultiSURF`` of this package keep X resident across rounds.
 """
 from __future__ import annotations
 
@@ -49,8 +49,10 @@ class TuRF(TransformerMixin, BaseEstimator):
         scorer = clone(self.estimator)
         active = np.arange(self.n_features_in_)
         # Estimators that can keep X resident re-score column subsets in place
-        # (MultiSURF: feat_idx on a device-resident plan);
-        # any other estimator is refit on X[:, active] as the reference does.
+        # (MultiSURF, ReliefF, SURF: a device-resident plan re-targeted with
+        # fs_plan_set_features); any other estimator --
+        # or one that declines (None) -- is refit on X[:, active] as the
+        # reference does.
         resident = getattr(scorer, "_resident_scorer", None)
         runner = resident(X, y) if resident is not None else None
         try:

@@ -37,7 +37,7 @@ _vp = ctypes.c_void_p
 EXPORTED = (
     "fs_version", "fs_last_error", "fs_device_count", "fs_column_stats", "fs_multisurf_score",
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
-    "fs_plan_create", "fs_plan_set_features",
+    "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2",
     "fs_plan_info", "fs_plan_kernel_ms", "fs_plan_destroy",
 )
@@ -83,6 +83,13 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_create.argtypes = [ctypes.POINTER(_vp), _int, _int, _f32p, _i64, _i64, _f64p,
                                    _f32p, _i64p, _i64, _int, _u8p, _int, _int, _int,
                                    ctypes.c_uint64]
+    lib.fs_plan_create_relieff.argtypes = [ctypes.POINTER(_vp), _int, _int, _f32p, _i64, _i64,
+                                           _i32p, _f32p, _u8p, _i64, _f32p, _i64, _i64, _i64,
+                                           _int, ctypes.c_uint64]
+    lib.fs_plan_create_surf.argtypes = [ctypes.POINTER(_vp), _int, _int, _f64p, _i64, _i64,
+                                        _i32p, _f32p, _int, _u8p, _i64, _i64, _int,
+                                        ctypes.c_uint64]
+    lib.fs_plan_score.argtypes = [_vp, _vp]
     lib.fs_plan_set_features.argtypes = [_vp, _i64p, _i64]
     lib.fs_plan_pass1.argtypes = [_vp, _vp]
     lib.fs_plan_select.argtypes = [_vp, _vp, _vp]
@@ -92,7 +99,8 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_kernel_ms.restype = ctypes.c_double
     lib.fs_plan_destroy.argtypes = [_vp]
     for name in ("fs_column_stats", "fs_multisurf_score", "fs_relieff_score", "fs_surf_score",
-                 "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
+                 "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create",
+                 "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
                  "fs_plan_pass2", "fs_plan_info", "fs_plan_destroy"):
         getattr(lib, name).restype = _int
     return lib
@@ -236,7 +244,9 @@ class Plan:
     """
 
     def __init__(self, backend, x, y, recip, is_discrete, use_star=False, feat_idx=None,
-                 rank=0, world=1, n_jobs=-1, device=0, stream=0):
+                 rank=0, world=1, n_jobs=-1, device=0, stream=0, _handle=None):
+        if _handle is not None:  # built by RowsPlan
+            return
         x = np.ascontiguousarray(x, dtype=np.float32)
         self.n, self.p = x.shape
         yv = np.ascontiguousarray(y, dtype=np.float64)
@@ -291,3 +301,41 @@ class Plan:
             self.close()
         except Exception:
             pass
+
+
+class RowsPlan(Plan):
+    """A ReliefF or SURF plan (``fs_plan_create_relieff`` / ``_surf``): X
+    resident, focal samples ``rows``; ``score(ptr)`` writes the float64 score
+    sums of those samples for the current feature subset (``set_features``)."""
+
+    def __init__(self, backend, algo, x, y, recip, is_discrete, k=3, class_probs=None,
+                 use_star=False, rows=None, n_jobs=-1, device=0, stream=0):
+        super().__init__(None, None, None, None, None, _handle=True)
+        self.backend = backend
+        self._h = _vp()
+        rc_ = np.ascontiguousarray(recip, dtype=np.float32)
+        isd = np.ascontiguousarray(is_discrete, dtype=np.uint8)
+        yi = np.ascontiguousarray(y, dtype=np.int32)
+        if algo == "relieff":
+            x = np.ascontiguousarray(x, dtype=np.float32)
+            self.n, self.p = x.shape
+            lo, hi = (0, self.n) if rows is None else rows
+            cp = np.ascontiguousarray(class_probs, dtype=np.float32)
+            check(_lib.fs_plan_create_relieff(
+                ctypes.byref(self._h), _backend_code(backend), int(device), _p(x, _f32p), self.n,
+                self.p, _p(yi, _i32p), _p(rc_, _f32p), _p(isd, _u8p), int(k), _p(cp, _f32p),
+                cp.size, int(lo), int(hi), int(n_jobs), ctypes.c_uint64(int(stream))))
+        elif algo == "surf":
+            x = np.ascontiguousarray(x, dtype=np.float64)
+            self.n, self.p = x.shape
+            lo, hi = (0, self.n) if rows is None else rows
+            check(_lib.fs_plan_create_surf(
+                ctypes.byref(self._h), _backend_code(backend), int(device), _p(x, _f64p), self.n,
+                self.p, _p(yi, _i32p), _p(rc_, _f32p), int(bool(use_star)), _p(isd, _u8p),
+                int(lo), int(hi), int(n_jobs), ctypes.c_uint64(int(stream))))
+        else:
+            raise ValueError(f"unknown algorithm {algo!r}")
+        self.n_kept = self.p
+
+    def score(self, sums_ptr: int) -> None:
+        check(_lib.fs_plan_score(self._h, _vp(sums_ptr)))

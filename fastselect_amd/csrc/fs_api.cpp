@@ -230,12 +230,22 @@ int fs_surf_score_rows(int backend, int device, const double* x, int64_t n, int6
 struct fs_plan {
   int backend = FS_BACKEND_CPU;
   int rank = 0, world = 1, n_jobs = -1;
+  int x_is_f64 = 0;
+  int64_t r_lo = 0, r_hi = 0;   // ReliefF / SURF plans: focal rows
   Prepared P;
+  Prepared P0;                  // as created (all columns): discrete tables for re-targeting
   gpu::Plan* g = nullptr;
   // CPU state
-  std::vector<float> x;
+  std::vector<char> x;          // the CPU plan's copy of X (x_is_f64 ? double : float)
   cpu::CpuState st;
+  const void* xp() const { return (const void*)x.data(); }
 };
+
+static bool is_multisurf_plan(const fs_plan* pl) {
+  if (pl->P.algo == ALGO_MULTISURF) return true;
+  set_error("pass1 / select / pass2 are the MultiSURF plan stages (use fs_plan_score)");
+  return false;
+}
 
 extern "C" {
 
@@ -273,10 +283,123 @@ int fs_plan_create(fs_plan** plan_out, int backend, int device, const float* x, 
       return rc;
     }
   } else {
-    pl->x.assign(x, x + (size_t)n * p);
+    const char* xb = (const char*)x;
+    pl->x.assign(xb, xb + (size_t)n * p * sizeof(float));
   }
   *plan_out = pl;
   return FS_OK;
+}
+
+// ReliefF / SURF plans: prepared problem in pl->P, X uploaded (GPU) or copied
+// (CPU), focal rows [r_lo, r_hi).
+static int finish_rows_plan(fs_plan* pl, int device, const void* x, int64_t r_lo, int64_t r_hi,
+                            uint64_t stream) {
+  const Prepared& P = pl->P;
+  if (pl->backend == FS_BACKEND_GPU && pl->x_is_f64) pl->P0 = P;  // value tables
+  pl->r_lo = r_lo;
+  pl->r_hi = r_hi;
+  if (pl->backend == FS_BACKEND_GPU)
+    return gpu::plan_create(&pl->g, P, x, pl->x_is_f64, device, 0, 1, stream, r_lo, r_hi);
+  const char* xb = (const char*)x;
+  pl->x.assign(xb, xb + (size_t)P.n * P.p_in * (pl->x_is_f64 ? 8 : 4));
+  return FS_OK;
+}
+
+int fs_plan_create_relieff(fs_plan** plan_out, int backend, int device, const float* x,
+                           int64_t n, int64_t p, const int32_t* y_enc, const float* recip,
+                           const uint8_t* is_discrete, int64_t k, const float* class_probs,
+                           int64_t n_classes, int64_t row_begin, int64_t row_end, int n_jobs,
+                           uint64_t stream) {
+  if (!plan_out || !y_enc || !class_probs || n_classes < 1 || k < 0) {
+    set_error("invalid ReliefF plan arguments");
+    return FS_EINVAL;
+  }
+  *plan_out = nullptr;
+  if (!(0 <= row_begin && row_begin <= row_end && row_end <= n)) {
+    set_error("row range must satisfy 0 <= row_begin <= row_end <= n");
+    return FS_EINVAL;
+  }
+  int rc = check_backend(backend, device);
+  if (rc != FS_OK) return rc;
+  if (backend == FS_BACKEND_GPU && n_classes > 64) {
+    set_error("GPU ReliefF supports at most 64 classes");
+    return FS_ENOTSUP;
+  }
+  fs_plan* pl = new fs_plan();
+  pl->backend = backend;
+  pl->n_jobs = n_jobs;
+  rc = prepare(pl->P, ALGO_RELIEFF, x, 0, n, p, nullptr, p, recip, is_discrete, n_jobs,
+               backend == FS_BACKEND_GPU);
+  if (rc) {
+    delete pl;
+    return map_prep_rc(rc);
+  }
+  pl->P.labels.assign(y_enc, y_enc + n);
+  for (int64_t i = 0; i < n; i++)
+    if (pl->P.labels[i] < 0 || pl->P.labels[i] >= n_classes) {
+      delete pl;
+      set_error("y_enc entry outside [0, n_classes)");
+      return FS_EINVAL;
+    }
+  pl->P.n_classes = (int32_t)n_classes;
+  pl->P.class_prior.assign(n_classes, 0.0);
+  for (int64_t c = 0; c < n_classes; c++) pl->P.class_prior[c] = (double)class_probs[c];
+  pl->P.k_neighbors = k;
+  if ((rc = finish_rows_plan(pl, device, x, row_begin, row_end, stream)) != FS_OK) {
+    delete pl;
+    return rc;
+  }
+  *plan_out = pl;
+  return FS_OK;
+}
+
+int fs_plan_create_surf(fs_plan** plan_out, int backend, int device, const double* x, int64_t n,
+                        int64_t p, const int32_t* y, const float* recip, int use_star,
+                        const uint8_t* is_discrete, int64_t row_begin, int64_t row_end,
+                        int n_jobs, uint64_t stream) {
+  if (!plan_out) {
+    set_error("plan_out is NULL");
+    return FS_EINVAL;
+  }
+  *plan_out = nullptr;
+  if (!(0 <= row_begin && row_begin <= row_end && row_end <= n)) {
+    set_error("row range must satisfy 0 <= row_begin <= row_end <= n");
+    return FS_EINVAL;
+  }
+  int rc = check_backend(backend, device);
+  if (rc != FS_OK) return rc;
+  fs_plan* pl = new fs_plan();
+  pl->backend = backend;
+  pl->n_jobs = n_jobs;
+  pl->x_is_f64 = 1;
+  rc = prepare(pl->P, ALGO_SURF, x, 1, n, p, nullptr, p, recip, is_discrete, n_jobs,
+               backend == FS_BACKEND_GPU);
+  if (rc || encode_labels_i32(pl->P, y)) {
+    delete pl;
+    return FS_EINVAL;
+  }
+  pl->P.use_star = use_star ? 1 : 0;
+  if ((rc = finish_rows_plan(pl, device, x, row_begin, row_end, stream)) != FS_OK) {
+    delete pl;
+    return rc;
+  }
+  *plan_out = pl;
+  return FS_OK;
+}
+
+int fs_plan_score(fs_plan* pl, double* sums) {
+  if (!pl || !sums) {
+    set_error("NULL plan or buffer");
+    return FS_EINVAL;
+  }
+  if (pl->P.algo == ALGO_MULTISURF) {
+    set_error("fs_plan_score is for ReliefF / SURF plans (MultiSURF: pass1 / select / pass2)");
+    return FS_EINVAL;
+  }
+  if (pl->g) return gpu::plan_score(pl->g, sums);
+  if (pl->P.algo == ALGO_RELIEFF)
+    return cpu::relieff_run(pl->P, pl->xp(), pl->n_jobs, pl->r_lo, pl->r_hi, sums);
+  return cpu::surf_run(pl->P, pl->xp(), pl->n_jobs, pl->r_lo, pl->r_hi, sums);
 }
 
 int fs_plan_set_features(fs_plan* pl, const int64_t* feat_idx, int64_t n_kept) {
@@ -288,10 +411,10 @@ int fs_plan_set_features(fs_plan* pl, const int64_t* feat_idx, int64_t n_kept) {
   const bool gpu = pl->backend == FS_BACKEND_GPU;
   // the GPU plan keeps X and its column ranges on the device; the CPU plan
   // keeps its own copy of X
-  const void* x = gpu ? nullptr : (const void*)pl->x.data();
+  const void* x = gpu ? nullptr : pl->xp();
   Prepared P;
-  int rc = prepare(P, O.algo, x, 0, O.n, O.p_in, feat_idx, n_kept, O.recip_in.data(),
-                   O.disc_in.data(), pl->n_jobs, gpu);
+  int rc = prepare(P, O.algo, x, pl->x_is_f64, O.n, O.p_in, feat_idx, n_kept, O.recip_in.data(),
+                   O.disc_in.data(), pl->n_jobs, gpu, gpu ? &pl->P0 : nullptr);
   if (rc) return map_prep_rc(rc);
   P.labels = O.labels;
   P.n_classes = O.n_classes;
@@ -311,8 +434,9 @@ int fs_plan_pass1(fs_plan* pl, double* rowstats) {
     set_error("NULL plan or buffer");
     return FS_EINVAL;
   }
+  if (!is_multisurf_plan(pl)) return FS_EINVAL;
   if (pl->g) return gpu::plan_pass1(pl->g, rowstats);
-  return cpu::multisurf_pass1(pl->P, pl->x.data(), pl->rank, pl->world, pl->n_jobs, pl->st,
+  return cpu::multisurf_pass1(pl->P, pl->xp(), pl->rank, pl->world, pl->n_jobs, pl->st,
                               rowstats);
 }
 
@@ -321,8 +445,9 @@ int fs_plan_select(fs_plan* pl, const double* rowstats, double* counts) {
     set_error("NULL plan or buffer");
     return FS_EINVAL;
   }
+  if (!is_multisurf_plan(pl)) return FS_EINVAL;
   if (pl->g) return gpu::plan_select(pl->g, rowstats, counts);
-  return cpu::multisurf_select(pl->P, pl->x.data(), pl->rank, pl->world, rowstats, pl->n_jobs,
+  return cpu::multisurf_select(pl->P, pl->xp(), pl->rank, pl->world, rowstats, pl->n_jobs,
                                pl->st, counts);
 }
 
@@ -331,6 +456,7 @@ int fs_plan_pass2(fs_plan* pl, const double* counts, double* scores) {
     set_error("NULL plan or buffer");
     return FS_EINVAL;
   }
+  if (!is_multisurf_plan(pl)) return FS_EINVAL;
   if (pl->g) return gpu::plan_pass2(pl->g, counts, scores);
   return cpu::multisurf_pass2(pl->P, pl->st, counts, pl->rank, pl->world, pl->n_jobs, scores);
 }

@@ -356,7 +356,7 @@ static float relieff_exact_key(const Prepared& P, const float* x, int64_t i, int
   const float* xi = x + i * P.p_in;
   const float* xj = x + j * P.p_in;
   double d = 0.0;
-  for (int64_t f = 0; f < P.p_in; f++) {
+  for (int64_t f : P.kept_col) {  // the scored features, in their order
     if (P.disc_in[f]) d += xi[f] != xj[f] ? 1.0 : 0.0;
     else d += (double)(std::fabs(xi[f] - xj[f]) * P.recip_in[f]);
   }

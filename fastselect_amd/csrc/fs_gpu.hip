@@ -1678,7 +1678,8 @@ struct Plan {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<void*> owned;         // buffers sized by n (live as long as the plan)
   std::vector<void*> owned_layout;  // buffers sized by the feature layout (PW)
-  bool layout_alloc = false;        // dalloc target: owned_layout
+  std::vector<void*> scratch;       // buffers of one plan_score call
+  int alloc_target = 0;             // dalloc target: 0 owned, 1 owned_layout, 2 scratch
   std::vector<char> colmin, colmax; // per input column, x's dtype (device-measured)
 };
 
@@ -1693,7 +1694,8 @@ static int dalloc(Plan* g, T** p, size_t count) {
               " bytes failed: " + hipGetErrorString(e));
     return FS_EOOM;
   }
-  (g->layout_alloc ? g->owned_layout : g->owned).push_back(q);
+  (g->alloc_target == 1 ? g->owned_layout : g->alloc_target == 2 ? g->scratch : g->owned)
+      .push_back(q);
   *p = (T*)q;
   return FS_OK;
 }
@@ -1726,6 +1728,7 @@ void plan_destroy(Plan* g) {
   trace_mark("kernels (to sync)");
   for (void* q : g->owned) (void)hipFree(q);
   for (void* q : g->owned_layout) (void)hipFree(q);
+  for (void* q : g->scratch) (void)hipFree(q);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
   if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
@@ -1836,7 +1839,7 @@ static int plan_layout(Plan* g) {
   // histogram shift so that the largest quantised value lands in bin < 4096
   g->rank_shift = 0;
   while ((Q.qmax / std::ldexp(1.0, g->rank_shift)) >= (double)kRankBins) g->rank_shift++;
-  g->layout_alloc = true;
+  g->alloc_target = 1;
   rc = FS_OK;
   if ((rc = dalloc(g, &g->src_col, Q.PW)) || (rc = dalloc(g, &g->out_pos, Q.PW)) ||
       (rc = dalloc(g, &g->off, Q.PW)) || (rc = dalloc(g, &g->qs, Q.PW)) ||
@@ -1849,7 +1852,7 @@ static int plan_layout(Plan* g) {
     rc = dalloc(g, &g->epsT, (size_t)Q.PW * Q.n_pad);
   }
   if (rc == FS_OK && Q.algo != ALGO_RELIEFF) rc = dalloc(g, &g->spart, (size_t)g->nseg * Q.PW);
-  g->layout_alloc = false;
+  g->alloc_target = 0;
   if (rc) return rc;
   std::vector<double> qs(Q.PW, 0.0);
   for (int64_t c = 0; c < Q.PW; c++) qs[c] = Q.scale[c] * Q.SC;
@@ -2202,14 +2205,10 @@ static int copy_sums(Plan* g, const double* sums_dev, double* sums_out) {
   return FS_OK;
 }
 
-int surf_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
-             double* sums_out) {
-  Plan* g = nullptr;
-  FS_TRY(plan_create(&g, P, x, 1, device, 0, 1, 0, r_lo, r_hi));
+// SURF score sums of the plan's focal rows into sums_dev[n_kept].
+static int plan_score_surf(Plan* g, double* sums_dev) {
   const Prepared& Q = g->P;
-  double* sc = nullptr;
-  int rc = dalloc(g, &sc, Q.n_kept);
-  if (rc == FS_OK) rc = run_quantize_dist(g);  // float64 distances, real units
+  int rc = run_quantize_dist(g);  // float64 distances, real units
   if (rc == FS_OK && g->r_hi > g->r_lo) {
     k_surf_avg<<<(unsigned)((g->r_hi - g->r_lo + 63) / 64), 64, 0, g->stream>>>(
         g->D, Q.n, Q.n_pad, 1.0, g->r_lo, g->r_hi, g->thr);
@@ -2222,7 +2221,17 @@ int surf_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t
                                                            g->Wt);
     rc = launch_check("k_weights");
   }
-  if (rc == FS_OK) rc = run_pass2(g, sc);
+  if (rc == FS_OK) rc = run_pass2(g, sums_dev);
+  return rc;
+}
+
+int surf_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
+             double* sums_out) {
+  Plan* g = nullptr;
+  FS_TRY(plan_create(&g, P, x, 1, device, 0, 1, 0, r_lo, r_hi));
+  double* sc = nullptr;
+  int rc = dalloc(g, &sc, g->P.n_kept);
+  if (rc == FS_OK) rc = plan_score_surf(g, sc);
   if (rc == FS_OK) rc = copy_sums(g, sc, sums_out);
   plan_destroy(g);
   return rc;
@@ -2240,9 +2249,11 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   if (nr_own <= 0) return FS_OK;
   uint32_t* tkey = nullptr;
   int32_t *tneed = nullptr, *teq = nullptr;
+  g->alloc_target = 2;  // per-call temporaries
   FS_TRY(dalloc(g, &tkey, (size_t)n * C));
   FS_TRY(dalloc(g, &tneed, (size_t)n * C));
   FS_TRY(dalloc(g, &teq, (size_t)n * C));
+  g->alloc_target = 0;
   const size_t shbytes = (size_t)C * 256 * 4 + 2 * (size_t)C * 4;
   const size_t shstage = shbytes + (size_t)n * 5;
   const bool stage = shstage <= 160 * 1024;
@@ -2279,7 +2290,7 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
       break;
     }
     g->list_cap = (int64_t)cnt + cnt / 4;
-    FS_TRY(dalloc(g, &g->list, g->list_cap));
+    FS_TRY(dalloc(g, &g->list, g->list_cap));  // persistent (alloc_target 0 here)
   }
   if (g->n_refined > 0) {
     FS_TRY(sort_pair_list(g, g->n_refined));
@@ -2313,10 +2324,12 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   int32_t *drows = nullptr, *R = nullptr;
   float* keys = nullptr;
   int* status = nullptr;
+  g->alloc_target = 2;
   FS_TRY(dalloc(g, &drows, (size_t)batch));
   FS_TRY(dalloc(g, &R, (size_t)batch * n));
   FS_TRY(dalloc(g, &keys, (size_t)batch * n));
   FS_TRY(dalloc(g, &status, 1));
+  g->alloc_target = 0;
   FS_HIP(hipMemsetAsync(status, 0, sizeof(int), g->stream));
   if (n <= kTieLdsMaxN)
     FS_HIP(hipFuncSetAttribute((const void*)k_rf_ties<true>,
@@ -2346,6 +2359,44 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   return FS_OK;
 }
 
+// ReliefF score sums of the plan's focal rows into sums_dev[n_kept]:
+// pass 1, neighbour selection, then the neighbour-gather update.
+static int plan_score_relieff(Plan* g, double* sums_dev) {
+  const Prepared& Q = g->P;
+  const int C = Q.n_classes;
+  const int64_t k = Q.k_neighbors;
+  std::vector<int64_t> cc(C, 0);
+  for (int64_t i = 0; i < Q.n; i++) cc[Q.labels[i]]++;
+  std::vector<double> prior(Q.class_prior);
+  double *dprior = nullptr, *part = nullptr;
+  int64_t* dcc = nullptr;
+  int32_t *nbr = nullptr, *nfound = nullptr;
+  const int64_t nrb = std::max<int64_t>(1, (g->r_hi - g->r_lo + 15) / 16);
+  int rc;
+  g->alloc_target = 2;  // per-call buffers
+  rc = dalloc(g, &dprior, C);
+  if (rc == FS_OK) rc = dalloc(g, &part, (size_t)nrb * Q.PW);
+  if (rc == FS_OK) rc = dalloc(g, &dcc, C);
+  if (rc == FS_OK) rc = dalloc(g, &nbr, (size_t)Q.n * C * std::max<int64_t>(k, 1));
+  if (rc == FS_OK) rc = dalloc(g, &nfound, (size_t)Q.n * C);
+  g->alloc_target = 0;
+  if (rc || (rc = h2d(g, dcc, cc.data(), C)) || (rc = h2d(g, dprior, prior.data(), C)) ||
+      (rc = run_quantize_dist(g)) || (rc = relieff_select(g, dcc, nbr, nfound)))
+    return rc;
+  if (trace_on()) {
+    (void)hipStreamSynchronize(g->stream);
+    std::fprintf(stderr, "[fs_trace] relieff: %lld exact pairs, %lld tie rows\n",
+                 (long long)g->n_refined, (long long)g->n_tie_rows);
+  }
+  k_rf_update<<<dim3((unsigned)(Q.PW / 64), (unsigned)nrb), 256, 0, g->stream>>>(
+      g->xs, g->r_lo, g->r_hi, Q.PW, Q.PC, g->lab, dprior, C, k, nbr, nfound, part);
+  FS_TRY(launch_check("k_rf_update"));
+  FS_HIP(hipMemsetAsync(sums_dev, 0, sizeof(double) * Q.n_kept, g->stream));
+  k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(part, nrb, Q.PW, g->out_pos,
+                                                                   sums_dev);
+  return launch_check("k_reduce");
+}
+
 int relieff_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
                 double* sums_out) {
   if (P.n_classes > 64) {
@@ -2354,41 +2405,35 @@ int relieff_run(const Prepared& P, const void* x, int device, int64_t r_lo, int6
   }
   Plan* g = nullptr;
   FS_TRY(plan_create(&g, P, x, 0, device, 0, 1, 0, r_lo, r_hi));
-  const Prepared& Q = g->P;
-  const int C = Q.n_classes;
-  const int64_t k = Q.k_neighbors;
-  std::vector<int64_t> cc(C, 0);
-  for (int64_t i = 0; i < Q.n; i++) cc[Q.labels[i]]++;
-  std::vector<double> prior(Q.class_prior);
-  double *sc = nullptr, *dprior = nullptr, *part = nullptr;
-  int64_t* dcc = nullptr;
-  int32_t *nbr = nullptr, *nfound = nullptr;
-  const int64_t nrb = std::max<int64_t>(1, (g->r_hi - g->r_lo + 15) / 16);
-  int rc;
-  if ((rc = dalloc(g, &sc, Q.n_kept)) || (rc = dalloc(g, &dprior, C)) ||
-      (rc = dalloc(g, &part, (size_t)nrb * Q.PW)) || (rc = dalloc(g, &dcc, C)) ||
-      (rc = dalloc(g, &nbr, (size_t)Q.n * C * std::max<int64_t>(k, 1))) ||
-      (rc = dalloc(g, &nfound, (size_t)Q.n * C)) || (rc = h2d(g, dcc, cc.data(), C)) ||
-      (rc = h2d(g, dprior, prior.data(), C)) || (rc = run_quantize_dist(g)) ||
-      (rc = relieff_select(g, dcc, nbr, nfound))) {
-    plan_destroy(g);
-    return rc;
-  }
-  if (trace_on()) {
-    (void)hipStreamSynchronize(g->stream);
-    std::fprintf(stderr, "[fs_trace] relieff: %lld exact pairs, %lld tie rows\n",
-                 (long long)g->n_refined, (long long)g->n_tie_rows);
-  }
-  k_rf_update<<<dim3((unsigned)(Q.PW / 64), (unsigned)nrb), 256, 0, g->stream>>>(
-      g->xs, g->r_lo, g->r_hi, Q.PW, Q.PC, g->lab, dprior, C, k, nbr, nfound, part);
-  rc = launch_check("k_rf_update");
-  if (rc == FS_OK) {
-    k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(part, nrb, Q.PW,
-                                                                     g->out_pos, sc);
-    rc = launch_check("k_reduce");
-  }
+  double* sc = nullptr;
+  int rc = dalloc(g, &sc, g->P.n_kept);
+  if (rc == FS_OK) rc = plan_score_relieff(g, sc);
   if (rc == FS_OK) rc = copy_sums(g, sc, sums_out);
   plan_destroy(g);
+  return rc;
+}
+
+// ReliefF / SURF plans (resident scoring, fs_plan_score): float64 score sums
+// of the plan's focal rows into device memory; per-call buffers are freed
+// before returning.
+int plan_score(Plan* g, double* sums_dev) {
+  FS_HIP(hipSetDevice(g->device));
+  int rc;
+  if (g->P.algo == ALGO_RELIEFF) {
+    if (g->P.n_classes > 64) {
+      set_error("GPU ReliefF supports at most 64 classes");
+      return FS_ENOTSUP;
+    }
+    rc = plan_score_relieff(g, sums_dev);
+  } else if (g->P.algo == ALGO_SURF) {
+    rc = plan_score_surf(g, sums_dev);
+  } else {
+    set_error("fs_plan_score: MultiSURF plans score through pass1 / select / pass2");
+    return FS_EINVAL;
+  }
+  if (hipStreamSynchronize(g->stream) != hipSuccess && rc == FS_OK) rc = FS_EHIP;
+  for (void* q : g->scratch) (void)hipFree(q);
+  g->scratch.clear();
   return rc;
 }
 

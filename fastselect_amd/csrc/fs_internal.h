@@ -64,6 +64,7 @@ struct Prepared {
   // feature order, used where its arithmetic is replayed exactly)
   std::vector<float> recip_in;
   std::vector<uint8_t> disc_in;
+  std::vector<int64_t> kept_col;   // input column of each kept feature, kept order
   std::vector<double> scale;       // continuous: (double)recip
   // discrete: per permuted column, [dtab_off[c], dtab_off[c+1]) slice of the
   // sorted distinct values (kernel dtype widened to double)
@@ -97,9 +98,13 @@ struct Prepared {
 // x is row-major [n][p_in], float32 (x_is_f64 == 0) or float64.
 // With device_ranges != 0 the continuous column minima/maxima (and, for a
 // float32 X, the discrete value tables) are left to the GPU backend.
+// With dtab_src (a Prepared of the same X) the discrete value tables are
+// taken from it instead of being built from x (re-targeting a GPU plan whose
+// X lives on the device).
 int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64_t p_in,
             const int64_t* feat_idx, int64_t n_kept, const float* recip,
-            const uint8_t* is_discrete, int n_jobs, int device_ranges = 0);
+            const uint8_t* is_discrete, int n_jobs, int device_ranges = 0,
+            const Prepared* dtab_src = nullptr);
 // Offsets, integer scale and error band from the per-permuted-column minima
 // and maxima of the continuous columns (c in [0, pc)).
 int finalize_scale(Prepared& P, const double* cmin, const double* cmax);
@@ -278,6 +283,9 @@ int plan_set_features(Plan* g, const Prepared& P);
 int plan_pass1(Plan* g, double* rowstats_dev);
 int plan_select(Plan* g, const double* rowstats_dev, double* counts_dev);
 int plan_pass2(Plan* g, const double* counts_dev, double* scores_dev);
+// ReliefF / SURF plans: float64 score sums of the plan's focal rows
+// (sums_dev[n_kept], device memory), for the plan's current feature subset.
+int plan_score(Plan* g, double* sums_dev);
 int plan_info(const Plan* g, int64_t* tiles, double* pfe, int64_t* refined);
 double plan_kernel_ms(const Plan* g, int which);
 void plan_destroy(Plan* g);

@@ -54,10 +54,12 @@ void row_tiles(int64_t nb, int64_t b_lo, int64_t b_hi, std::vector<int32_t>& bi,
 
 int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64_t p_in,
             const int64_t* feat_idx, int64_t n_kept, const float* recip,
-            const uint8_t* is_discrete, int n_jobs, int device_ranges) {
+            const uint8_t* is_discrete, int n_jobs, int device_ranges,
+            const Prepared* dtab_src) {
   // x may be NULL only when nothing here reads it: ranges left to the
-  // device and a float32 X (discrete columns coded by their bits)
-  const bool x_needed = !(device_ranges && !x_is_f64);
+  // device and discrete columns coded by their bits (float32 X) or tables
+  // taken from dtab_src
+  const bool x_needed = !(device_ranges && (!x_is_f64 || dtab_src));
   if ((!x && x_needed) || !recip || !is_discrete || n < 2 || p_in < 1) {
     set_error("invalid problem: need x, recip, is_discrete, n >= 2 and p >= 1");
     return -1;
@@ -104,12 +106,28 @@ int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64
   for (int64_t c = 0; c < P.pc; c++) P.scale[c] = (double)recip[P.src_col[c]];
   P.recip_in.assign(recip, recip + p_in);
   P.disc_in.assign(is_discrete, is_discrete + p_in);
+  P.kept_col.resize((size_t)n_kept);
+  for (int64_t k = 0; k < n_kept; k++) P.kept_col[k] = feat_idx ? feat_idx[k] : k;
   P.disc_bits = (device_ranges && !x_is_f64) ? 1 : 0;
   const int nthreads = hardware_threads(n_jobs);
 
   // Discrete value tables (sorted distinct values, float equality
   // semantics), one column per task.
-  if (!P.disc_bits && P.pd > 0) {
+  if (!P.disc_bits && P.pd > 0 && dtab_src) {
+    // slices of the source's tables, looked up by input column
+    std::vector<int64_t> perm_of((size_t)p_in, -1);
+    const Prepared& S = *dtab_src;
+    for (int64_t c = S.PC; c < S.PC + S.pd; c++) perm_of[(size_t)S.src_col[c]] = c;
+    for (int64_t k = 0; k < P.pd; k++) {
+      const int64_t c = perm_of[(size_t)P.src_col[P.PC + k]];
+      if (c < 0) {
+        set_error("discrete column without a value table in the source plan");
+        return -1;
+      }
+      P.dtab_off[P.PC + k] = (int64_t)P.dtab.size();
+      P.dtab.insert(P.dtab.end(), S.dtab.begin() + S.dtab_off[c], S.dtab.begin() + S.dtab_off[c + 1]);
+    }
+  } else if (!P.disc_bits && P.pd > 0) {
     std::vector<std::vector<double>> tabs((size_t)P.pd);
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(nthreads, P.pd));
     std::vector<std::thread> th;

@@ -197,6 +197,27 @@ FS_API int fs_plan_select(fs_plan* plan, const double* rowstats, double* counts)
 /* Stage 3: pair weights from the all-reduced counts[2n]; partial per-feature
  * score sums (NOT divided by n) -> scores[n_kept], in feat_idx order. */
 FS_API int fs_plan_pass2(fs_plan* plan, const double* counts, double* scores);
+/*
+ * ReliefF / SURF plans (resident scoring): X uploaded once (GPU) or copied
+ * (CPU), arguments as fs_relieff_score / fs_surf_score, focal samples
+ * [row_begin, row_end) as fs_*_score_rows.  fs_plan_score writes the float64
+ * score sums of those samples for the plan's current feature subset to
+ * sums[n_kept] (device memory for the GPU backend, host memory for the CPU
+ * backend); fs_plan_set_features re-targets the plan to another column subset
+ * without re-uploading X, which is how TuRF re-scores its shrinking feature
+ * sets (TuRF.py:93-115).  pass1 / select / pass2 are MultiSURF-only, and
+ * fs_plan_score is ReliefF / SURF-only (FS_EINVAL otherwise).
+ */
+FS_API int fs_plan_create_relieff(fs_plan** plan_out, int backend, int device, const float* x,
+                                  int64_t n, int64_t p, const int32_t* y_enc, const float* recip,
+                                  const uint8_t* is_discrete, int64_t k, const float* class_probs,
+                                  int64_t n_classes, int64_t row_begin, int64_t row_end,
+                                  int n_jobs, uint64_t stream);
+FS_API int fs_plan_create_surf(fs_plan** plan_out, int backend, int device, const double* x,
+                               int64_t n, int64_t p, const int32_t* y, const float* recip,
+                               int use_star, const uint8_t* is_discrete, int64_t row_begin,
+                               int64_t row_end, int n_jobs, uint64_t stream);
+FS_API int fs_plan_score(fs_plan* plan, double* sums);
 /* Number of pair tiles this plan owns, the pair-feature evaluations one full
  * pass1+pass2 performs on this rank (throughput accounting) and the number of
  * ambiguous pairs the last stage 2 recomputed exactly.  NULL outputs are

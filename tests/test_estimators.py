@@ -354,3 +354,46 @@ def test_turf_resident_plan_validates_like_refit():
                 _RefitMultiSURF(backend="cpu", n_features_to_select=25)):
         with pytest.raises(ValueError, match="n_features"):
             TuRF(est, n_features_to_select=5, pct_remove=0.3).fit(X, y)
+
+
+# ---- TuRF over resident ReliefF / SURF plans (fs_plan_create_relieff/_surf) --
+
+class _RefitReliefF(ReliefF):
+    _resident_scorer = None
+
+
+class _RefitSURF(SURF):
+    _resident_scorer = None
+
+
+@pytest.mark.parametrize("make", [
+    lambda cls: cls(backend="cpu", n_neighbors=5, discrete_limit=12),
+    lambda cls: cls(backend="cpu", n_neighbors=2, discrete_limit=3),
+])
+def test_turf_resident_relieff_equals_refits(make):
+    X, y = make_classification(n_samples=140, n_features=50, n_informative=6, n_classes=3,
+                               random_state=4)
+    X[:, 7] = np.round(X[:, 7])
+    kw = dict(n_features_to_select=8, pct_remove=0.2)
+    fast = TuRF(make(ReliefF), **kw).fit(X, y)
+    slow = TuRF(make(_RefitReliefF), **kw).fit(X, y)
+    assert_array_equal(fast.top_features_, slow.top_features_)
+    assert_allclose(fast.feature_importances_, slow.feature_importances_, rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("star", [False, True])
+def test_turf_resident_surf_equals_refits(star):
+    X, y = make_classification(n_samples=130, n_features=45, n_informative=6, random_state=5)
+    X[:, 2] = np.round(X[:, 2])
+    kw = dict(n_features_to_select=7, pct_remove=0.25)
+    fast = TuRF(SURF(backend="cpu", use_star=star, discrete_limit=12), **kw).fit(X, y)
+    slow = TuRF(_RefitSURF(backend="cpu", use_star=star, discrete_limit=12), **kw).fit(X, y)
+    assert_array_equal(fast.top_features_, slow.top_features_)
+    assert_allclose(fast.feature_importances_, slow.feature_importances_, rtol=0, atol=1e-7)
+
+
+def test_turf_resident_relieff_single_class_falls_back():
+    X, _ = make_classification(n_samples=40, n_features=12, random_state=0)
+    y = np.zeros(40, dtype=int)
+    t = TuRF(ReliefF(backend="cpu"), n_features_to_select=3).fit(X, y)
+    assert t.top_features_.size == 3

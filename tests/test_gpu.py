@@ -374,6 +374,27 @@ def test_turf_resident_gpu_equals_refits():
     np.testing.assert_allclose(fast.feature_importances_, slow.feature_importances_, atol=1e-7)
 
 
+@pytest.mark.parametrize("name", ["ReliefF", "SURF", "SURFstar"])
+def test_turf_resident_rows_gpu_equals_refits(name):
+    """TuRF over resident ReliefF / SURF plans (fs_plan_set_features +
+    fs_plan_score on the device) equals refitting on X[:, active]."""
+    import fastselect_amd as fa
+    cls = {"ReliefF": fa.ReliefF, "SURF": fa.SURF, "SURFstar": fa.SURFstar}[name]
+    kw_est = {"n_neighbors": 6} if name == "ReliefF" else {}
+
+    class Refit(cls):
+        _resident_scorer = None
+
+    X, y = make_classification(n_samples=700, n_features=300, n_informative=10, n_classes=3,
+                               random_state=8)
+    X[:, 4] = np.round(X[:, 4])
+    kw = dict(n_features_to_select=10, pct_remove=0.3)
+    fast = fa.TuRF(cls(backend="gpu", **kw_est), **kw).fit(X, y)
+    slow = fa.TuRF(Refit(backend="gpu", **kw_est), **kw).fit(X, y)
+    np.testing.assert_array_equal(fast.top_features_, slow.top_features_)
+    np.testing.assert_allclose(fast.feature_importances_, slow.feature_importances_, atol=1e-7)
+
+
 def _two_rank_worker(rank, world, port, out_path):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))

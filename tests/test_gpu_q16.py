@@ -66,3 +66,20 @@ def test_q16_agrees_with_u32_path(monkeypatch):
     for a, b in zip(out["0"], out["1"]):
         assert scale_rel_err(b, a) < 5e-6
         assert set(np.argsort(a)[::-1][:10]) == set(np.argsort(b)[::-1][:10])
+
+
+@pytest.mark.slow
+def test_q16_multisurf_mixed_default_at_16384(oracle):
+    """The default 16-bit MultiSURF path with discrete and constant columns
+    mixed in (u32 discrete rows after the packed continuous ones)."""
+    from fastselect_amd import MultiSURF
+    rng = np.random.default_rng(11)
+    n = 16384
+    Xc, y = make_classification(n_samples=n, n_features=70, n_informative=10, n_redundant=10,
+                                random_state=3)
+    Xd = rng.integers(0, 3, size=(n, 20)).astype(np.float64)
+    Xk = np.full((n, 2), 4.0)
+    X = np.concatenate([Xc, Xd, Xk], axis=1)[:, rng.permutation(92)]
+    for star in (False, True):
+        assert_parity(_fit(MultiSURF, X, y, use_star=star),
+                      oracle.multisurf_scores(X, y, use_star=star), TOL, k=10)

@@ -29,6 +29,8 @@ CONFIGS = {
     "cfg5m": dict(algo="multisurf", n=10000, p=50000, R=100, star=True),
     # TuRF over MultiSURF on cfg2's data: device-resident re-targeting vs refits
     "turf2": dict(algo="turf", n=5000, p=5000, R=100),
+    # TuRF over ReliefF (k=10) on cfg3's data
+    "turf3": dict(algo="turf", base="ReliefF", n=20000, p=2000, R=50, k=10),
 }
 
 
@@ -57,13 +59,17 @@ def main():
         if c["algo"] == "turf":
             import fastselect_amd as F
 
-            class Refit(F.MultiSURF):
+            cls = getattr(F, c.get("base", "MultiSURF"))
+            ekw = {"n_neighbors": c["k"]} if "k" in c else {}
+
+            class Refit(cls):
                 _resident_scorer = None
 
             out = {"config": name, **c, "data_s": t_data}
-            for label, base in (("resident", F.MultiSURF), ("refit", Refit)):
+            for label, base in (("resident", cls), ("refit", Refit)):
                 t0 = time.perf_counter()
-                tf = F.TuRF(base(backend="gpu"), n_features_to_select=10, pct_remove=0.1).fit(X, y)
+                tf = F.TuRF(base(backend="gpu", **ekw), n_features_to_select=10,
+                            pct_remove=0.1).fit(X, y)
                 out[f"{label}_s"] = time.perf_counter() - t0
                 out[f"{label}_top"] = tf.top_features_.tolist()
             print(json.dumps(out), flush=True)
