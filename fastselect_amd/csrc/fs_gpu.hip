@@ -34,6 +34,7 @@
 
 #include "../../include/fastselect_amd.h"
 #include "fs_internal.h"
+#include "fs_sparse_asm.inc"
 
 namespace fs {
 namespace gpu {
@@ -904,6 +905,33 @@ __global__ __launch_bounds__(256) void k_tile_counts(const double* __restrict__ 
 // ---------------------------------------------------------------------------
 // Pair weights per owned tile: Wt[t][jj][ii] = W_ij + W_ji for i < j
 // ---------------------------------------------------------------------------
+// Symmetric pair weight W_ij + W_ji of one pair (i, j) of an owned tile.
+__device__ __forceinline__ float pair_weight(const double* __restrict__ D, int64_t n, int64_t n_pad,
+                                             int64_t i, int64_t j, bool upper,
+                                             const double* __restrict__ thr,
+                                             const int32_t* __restrict__ lab,
+                                             const double* __restrict__ counts, int algo,
+                                             int use_star, double inv_sc, int64_t r_lo,
+                                             int64_t r_hi) {
+  if (!(i < n && j < n && upper)) return 0.0f;
+  const double d = D[j * n_pad + i];  // == D[i][j]
+  const bool hit = lab[i] == lab[j];
+  double wi, wj;
+  if (algo == ALGO_MULTISURF) {
+    wi = multisurf_weight(d < thr[i], hit, use_star, counts[2 * i], counts[2 * i + 1]);
+    wj = multisurf_weight(d < thr[j], hit, use_star, counts[2 * j], counts[2 * j + 1]);
+  } else {  // SURF: float32 distance against the float64 mean
+    const double df = (double)(float)(d * inv_sc);
+    wi = surf_weight(df < thr[i], hit, use_star);
+    wj = surf_weight(df < thr[j], hit, use_star);
+  }
+  // Only focal samples in [r_lo, r_hi) contribute their side of a pair (row
+  // sharding: another rank scores the other side); MultiSURF passes [0, n).
+  if (i < r_lo || i >= r_hi) wi = 0.0;
+  if (j < r_lo || j >= r_hi) wj = 0.0;
+  return (float)(wi + wj);
+}
+
 __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, int64_t n,
                                                  int64_t n_pad, const int2* __restrict__ tiles,
                                                  const double* __restrict__ thr,
@@ -911,32 +939,61 @@ __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, i
                                                  const double* __restrict__ counts, int algo,
                                                  int use_star, double inv_sc, int64_t r_lo,
                                                  int64_t r_hi, float* __restrict__ Wt) {
-  // Only focal samples in [r_lo, r_hi) contribute their side of a pair (row
-  // sharding: another rank scores the other side); MultiSURF passes [0, n).
   const int2 tl = tiles[blockIdx.x];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
   float* out = Wt + (int64_t)blockIdx.x * kTile * kTile;
   for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
     const int jj = e / kTile, ii = e % kTile;
-    const int64_t i = i0 + ii, j = j0 + jj;
-    float w = 0.0f;
-    if (i < n && j < n && (tl.x < tl.y || ii < jj)) {
-      const double d = D[j * n_pad + i];  // == D[i][j]
-      const bool hit = lab[i] == lab[j];
-      double wi, wj;
-      if (algo == ALGO_MULTISURF) {
-        wi = multisurf_weight(d < thr[i], hit, use_star, counts[2 * i], counts[2 * i + 1]);
-        wj = multisurf_weight(d < thr[j], hit, use_star, counts[2 * j], counts[2 * j + 1]);
-      } else {  // SURF: float32 distance against the float64 mean
-        const double df = (double)(float)(d * inv_sc);
-        wi = surf_weight(df < thr[i], hit, use_star);
-        wj = surf_weight(df < thr[j], hit, use_star);
-      }
-      if (i < r_lo || i >= r_hi) wi = 0.0;
-      if (j < r_lo || j >= r_hi) wj = 0.0;
-      w = (float)(wi + wj);
-    }
-    out[jj * kTile + ii] = w;
+    out[jj * kTile + ii] = pair_weight(D, n, n_pad, i0 + ii, j0 + jj, tl.x < tl.y || ii < jj, thr,
+                                       lab, counts, algo, use_star, inv_sc, r_lo, r_hi);
+  }
+}
+
+// Sparse pair weights (pass 2 skips zero weights; MultiSURF: ~42% of the
+// pairs are near one of their two samples).  The 128 columns of owned tile t
+// are dealt to kSWaves = 16 streams, stream w taking jj = w, w + 16, ... (8
+// columns); a stream holds its columns' non-zero weights of rows ii in
+// ascending ii as entries (ii * 1024, w) -- 1024 = the byte stride of a row
+// in k_score_sparse's LDS block -- each column padded with (0, 0) to whole
+// groups of kGroup entries (at least one), columns back to back.  The lowest
+// mantissa bit of the first weight of a column's last group is set and that
+// of every other weight cleared (a <= 1-ulp change, far below the 1e-5 bar).
+// Stream (t, w) starts at ent + (t * 16 + w) * kStreamEntries.
+constexpr int kGroup = 8;
+constexpr int kSWaves = 16;                                // waves of k_score_sparse
+constexpr int kStreamEntries = (kTile / kSWaves) * kTile;  // 8 columns x 128 rows
+
+__device__ __forceinline__ uint32_t weight_bits(float w, bool last) {
+  return (__float_as_uint(w) & ~1u) | (last ? 1u : 0u);
+}
+
+__global__ __launch_bounds__(1024) void k_weights_sparse(
+    const double* __restrict__ D, int64_t n, int64_t n_pad, const int2* __restrict__ tiles,
+    const double* __restrict__ thr, const int32_t* __restrict__ lab,
+    const double* __restrict__ counts, int algo, int use_star, double inv_sc, int64_t r_lo,
+    int64_t r_hi, uint2* __restrict__ ent) {
+  const int2 tl = tiles[blockIdx.x];
+  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint2* out = ent + ((int64_t)blockIdx.x * kSWaves + wave) * kStreamEntries;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  int off = 0;
+  for (int jj = wave; jj < kTile; jj += kSWaves) {
+    const float w0 = pair_weight(D, n, n_pad, i0 + lane, j0 + jj, tl.x < tl.y || lane < jj, thr,
+                                 lab, counts, algo, use_star, inv_sc, r_lo, r_hi);
+    const float w1 = pair_weight(D, n, n_pad, i0 + lane + 64, j0 + jj,
+                                 tl.x < tl.y || lane + 64 < jj, thr, lab, counts, algo, use_star,
+                                 inv_sc, r_lo, r_hi);
+    const uint64_t m0 = __ballot(w0 != 0.0f), m1 = __ballot(w1 != 0.0f);
+    const int n0 = __popcll(m0), total = n0 + __popcll(m1);
+    const int padded = total == 0 ? kGroup : (total + kGroup - 1) / kGroup * kGroup;
+    const int last = padded - kGroup;  // first entry of the column's last group
+    const int e0 = __popcll(m0 & below), e1 = n0 + __popcll(m1 & below), ep = total + lane;
+    if (w0 != 0.0f) out[off + e0] = make_uint2((uint32_t)lane * 1024u, weight_bits(w0, e0 == last));
+    if (w1 != 0.0f)
+      out[off + e1] = make_uint2((uint32_t)(lane + 64) * 1024u, weight_bits(w1, e1 == last));
+    if (ep < padded) out[off + ep] = make_uint2(0u, ep == last ? 1u : 0u);
+    off += padded;
   }
 }
 
@@ -1082,6 +1139,121 @@ __global__ __launch_bounds__(256) void k_score(const float* __restrict__ xs, int
   if (wave < 2 && (wave == 0 || two)) {
     const double v = (red[wave][0][lane] + red[wave][1][lane]) + (red[wave][2][lane] + red[wave][3][lane]);
     spart[seg * PW + c0 + wave * 64] = v;
+  }
+}
+
+// Pass 2 over the sparse weights.  Grid as k_score (XCD-aware, segments of
+// consecutive tiles) but with 256-feature blocks and 16 waves per workgroup
+// (one workgroup per CU).  The 128 rows of the current row block sit in LDS
+// (128 KB: row r, lane l = features f0 + l + 64k, k = 0..3, as one float4),
+// staged when the segment reaches a new row block.  Wave w walks its stream
+// of each tile (k_weights_sparse): per column the four B values are VGPRs and
+// every entry is one ds_read_b128 of its row and 4 x (sub, fma |.|) with the
+// weight in an SGPR -- the hand-pipelined loop of fs_sparse_asm.inc for
+// continuous blocks, plain HIP below for blocks holding discrete features.
+template <bool DISC>
+__device__ __forceinline__ float pair_term_d(float a, float b, float w, float acc) {
+  return pair_term<DISC>(a, b, w, acc);
+}
+
+__device__ __forceinline__ void sparse_stream_generic(const float4* __restrict__ As,
+                                                      const uint2* __restrict__ e,
+                                                      const float* __restrict__ xb, int64_t PW,
+                                                      int lane, const bool (&disc)[4],
+                                                      float (&acc)[8]) {
+  int col = 0;
+  float4 b = make_float4(xb[0], xb[64], xb[128], xb[192]);
+  for (int g = 0; col < kTile / kSWaves && g < kStreamEntries; g += kGroup) {
+    uint2 E[kGroup];
+#pragma unroll
+    for (int q = 0; q < kGroup; q++) E[q] = e[g + q];
+#pragma unroll
+    for (int q = 0; q < kGroup; q++) {
+      const float4 a = As[(E[q].x >> 4) + lane];
+      const float w = __uint_as_float(E[q].y);
+      const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        float& c = acc[2 * k + (q & 1)];
+        c = disc[k] ? pair_term_d<true>(av[k], bv[k], w, c) : pair_term_d<false>(av[k], bv[k], w, c);
+      }
+    }
+    if (E[0].y & 1u) {  // end of the column
+      col++;
+      if (col < kTile / kSWaves) {
+        const float* __restrict__ xn = xb + (int64_t)col * kSWaves * PW;
+        b = make_float4(xn[0], xn[64], xn[128], xn[192]);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_score_sparse(
+    const float* __restrict__ xs, int64_t PW, int64_t PC, const int2* __restrict__ tiles,
+    const uint2* __restrict__ ent, int64_t n_tiles, int64_t seg_len, int64_t nseg, int64_t nfb,
+    double* __restrict__ spart) {
+  __shared__ float4 As[kTile * 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t wg = blockIdx.x;
+  const int64_t xcd = wg % kXcds, k = wg / kXcds;
+  const int64_t seg = xcd + kXcds * (k / nfb), fb = k % nfb;
+  if (seg >= nseg) return;
+  const int64_t f0 = fb * 256;
+  const int64_t t_begin = seg * seg_len;
+  const int64_t t_end = t_begin + seg_len < n_tiles ? t_begin + seg_len : n_tiles;
+  // chunk c (features f0 + 64c ..) is real if below PW, discrete from PC on
+  bool disc[4], real[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) {
+    real[c] = f0 + 64 * c < PW;
+    disc[c] = f0 + 64 * c >= PC;
+  }
+  const bool fast = f0 + 256 <= PC;  // four continuous chunks: the asm loop
+  const uint32_t lane16 = (uint32_t)(uintptr_t)As + (uint32_t)lane * 16u;
+  const uint32_t lane4 = (uint32_t)lane * 4u;
+  const uint32_t bstride = (uint32_t)(kSWaves * PW * sizeof(float));
+  const uint32_t ncols = kTile / kSWaves;
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  int cur_bi = -1;
+  for (int64_t t = t_begin; t < t_end; t++) {
+    const int2 tl = tiles[t];
+    if (tl.x != cur_bi) {
+      __syncthreads();
+      const float* __restrict__ xa = xs + (int64_t)tl.x * kTile * PW + f0 + lane;
+      for (int r = wave; r < kTile; r += kSWaves) {
+        const float* __restrict__ xr = xa + (int64_t)r * PW;
+        As[r * 64 + lane] = make_float4(xr[0], real[1] ? xr[64] : 0.0f, real[2] ? xr[128] : 0.0f,
+                                        real[3] ? xr[192] : 0.0f);
+      }
+      __syncthreads();
+      cur_bi = tl.x;
+    }
+    float acc[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    const uint2* __restrict__ e = ent + (t * kSWaves + wave) * kStreamEntries;
+    const float* __restrict__ xb = xs + ((int64_t)tl.y * kTile + wave) * PW + f0;
+    if (fast) {
+      const uint64_t eb = (uint64_t)(uintptr_t)e, bp = (uint64_t)(uintptr_t)xb;
+      FS_SPARSE_STREAM_ASM(acc, lane16, lane4, eb, bp, bstride, ncols);
+    } else {
+      sparse_stream_generic(As, e, xb + lane, PW, lane, disc, acc);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; c++) s[c] += (double)acc[2 * c] + (double)acc[2 * c + 1];
+  }
+  // fixed-order reduction of the 16 waves' partials through the LDS block
+  __syncthreads();
+  double* red = (double*)As;  // [4 chunks][kSWaves][64]
+#pragma unroll
+  for (int c = 0; c < 4; c++) red[(c * kSWaves + wave) * 64 + lane] = s[c];
+  __syncthreads();
+  if (wave < 4 && real[wave]) {
+    const double* r = red + wave * kSWaves * 64 + lane;
+    double v = 0.0;
+#pragma unroll
+    for (int q = 0; q < kSWaves; q += 4)
+      v += (r[q * 64] + r[(q + 1) * 64]) + (r[(q + 2) * 64] + r[(q + 3) * 64]);
+    spart[seg * PW + f0 + 64 * wave + lane] = v;
   }
 }
 
@@ -1665,7 +1837,9 @@ struct Plan {
   double* D = nullptr;
   int2* tiles = nullptr;
   double* thr = nullptr;
-  float* Wt = nullptr;
+  float* Wt = nullptr;          // dense pair weights (sparse == 0)
+  uint2* ent = nullptr;         // sparse pair-weight streams (sparse == 1)
+  int sparse = 0;               // pass 2 over non-zero weights only
   double* spart = nullptr;
   // ambiguous-pair refinement
   int2* list = nullptr;
@@ -1795,6 +1969,18 @@ static int choose_q16(const Prepared& P) {
   if (env && *env) return std::atoi(env) != 0 ? 1 : 0;
   const int64_t min_rows = P.algo == ALGO_RELIEFF ? kQ16MinRowsRF : kQ16MinRowsMS;
   return (P.n >= min_rows && P.pc >= kFeatPad) ? 1 : 0;
+}
+
+// Pass 2 on the non-zero pair weights only (k_weights_sparse +
+// k_score_sparse) unless nearly every pair carries a weight: SURF* weighs
+// every pair (near or far), so it keeps the dense kernel.  MultiSURF weighs
+// the ~42% of pairs near one of their samples, MultiSURF* ~62%, SURF ~60%;
+// row-sharded plans zero the non-owned sides.  FS_SPARSE=0/1 forces it.
+static int choose_sparse(const Prepared& P) {
+  if (P.algo == ALGO_RELIEFF) return 0;
+  const char* env = std::getenv("FS_SPARSE");
+  if (env && *env) return std::atoi(env) != 0 ? 1 : 0;
+  return (P.algo == ALGO_SURF && P.use_star) ? 0 : 1;
 }
 
 // Feature-layout part of a plan: everything sized by the kept features
@@ -1947,9 +2133,19 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       (rc = dalloc(g, &g->tiles, g->n_tiles)) || (rc = dalloc(g, &g->thr, Q.n_pad)) ||
       (rc = dalloc(g, &g->list, g->list_cap)) || (rc = dalloc(g, &g->list_count, 1)))
     return fail(rc);
-  if (Q.algo != ALGO_RELIEFF &&
+  g->sparse = choose_sparse(Q);
+  if (Q.algo != ALGO_RELIEFF && !g->sparse &&
       (rc = dalloc(g, &g->Wt, (size_t)(g->n_tiles + 1) * kTile * kTile)))
     return fail(rc);
+  if (g->sparse) {
+    // One spare tile: k_score_sparse prefetches two groups past the end of a
+    // stream.  Zeroed once, so such reads (and stream tails never written)
+    // hold in-range row offsets.
+    const size_t count = (size_t)(g->n_tiles + 1) * kSWaves * kStreamEntries;
+    if ((rc = dalloc(g, &g->ent, count))) return fail(rc);
+    if (hipMemsetAsync(g->ent, 0, sizeof(uint2) * count, g->stream) != hipSuccess)
+      return fail(FS_EHIP);
+  }
   if (g->ksplit > 1 &&
       (rc = dalloc(g, &g->Dpart, (size_t)(g->ksplit - 1) * Q.n_pad * Q.n_pad)))
     return fail(rc);
@@ -2086,6 +2282,22 @@ static int refine_pairs(Plan* g, int algo, double delta) {
   return launch_check("k_exact_pairs");
 }
 
+// Pair weights of the owned tiles in the form pass 2 reads (dense or sparse).
+static int run_weights(Plan* g, const double* counts, int algo, double inv_sc) {
+  const Prepared& Q = g->P;
+  if (g->n_tiles == 0) return FS_OK;
+  if (g->sparse) {
+    k_weights_sparse<<<(unsigned)g->n_tiles, 64 * kSWaves, 0, g->stream>>>(
+        g->D, Q.n, Q.n_pad, g->tiles, g->thr, g->lab, counts, algo, Q.use_star, inv_sc, g->r_lo,
+        g->r_hi, g->ent);
+    return launch_check("k_weights_sparse");
+  }
+  k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles, g->thr,
+                                                         g->lab, counts, algo, Q.use_star, inv_sc,
+                                                         g->r_lo, g->r_hi, g->Wt);
+  return launch_check("k_weights");
+}
+
 static int run_pass2(Plan* g, double* scores_dev) {
   const Prepared& Q = g->P;
   const int64_t nfb = (Q.PW + 127) / 128;
@@ -2093,9 +2305,16 @@ static int run_pass2(Plan* g, double* scores_dev) {
   if (g->n_tiles == 0) return FS_OK;
   FS_HIP(hipEventRecord(g->ev[2], g->stream));
   const int64_t seg_per_xcd = (g->nseg + kXcds - 1) / kXcds;
-  k_score<<<(unsigned)(kXcds * seg_per_xcd * nfb), 256, 0, g->stream>>>(
-      g->xs, Q.PW, Q.PC, g->tiles, g->Wt, g->n_tiles, g->seg_len, g->nseg, nfb, g->spart);
-  FS_TRY(launch_check("k_score"));
+  if (g->sparse) {
+    const int64_t nfb4 = (Q.PW + 255) / 256;
+    k_score_sparse<<<(unsigned)(kXcds * seg_per_xcd * nfb4), 64 * kSWaves, 0, g->stream>>>(
+        g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->n_tiles, g->seg_len, g->nseg, nfb4, g->spart);
+    FS_TRY(launch_check("k_score_sparse"));
+  } else {
+    k_score<<<(unsigned)(kXcds * seg_per_xcd * nfb), 256, 0, g->stream>>>(
+        g->xs, Q.PW, Q.PC, g->tiles, g->Wt, g->n_tiles, g->seg_len, g->nseg, nfb, g->spart);
+    FS_TRY(launch_check("k_score"));
+  }
   FS_HIP(hipEventRecord(g->ev[3], g->stream));
   k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(g->spart, g->nseg, Q.PW,
                                                                    g->out_pos, scores_dev);
@@ -2136,13 +2355,7 @@ int plan_select(Plan* g, const double* rowstats, double* counts) {
 int plan_pass2(Plan* g, const double* counts, double* scores) {
   const Prepared& Q = g->P;
   FS_HIP(hipSetDevice(g->device));
-  if (g->n_tiles > 0) {
-    k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
-                                                           g->thr, g->lab, counts,
-                                                           ALGO_MULTISURF, Q.use_star,
-                                                           1.0 / Q.SC, (int64_t)0, Q.n, g->Wt);
-    FS_TRY(launch_check("k_weights"));
-  }
+  FS_TRY(run_weights(g, counts, ALGO_MULTISURF, 1.0 / Q.SC));
   FS_TRY(run_pass2(g, scores));
   if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
   return FS_OK;
@@ -2214,13 +2427,7 @@ static int plan_score_surf(Plan* g, double* sums_dev) {
         g->D, Q.n, Q.n_pad, 1.0, g->r_lo, g->r_hi, g->thr);
     rc = launch_check("k_surf_avg");
   }
-  if (rc == FS_OK && g->n_tiles > 0) {
-    k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
-                                                           g->thr, g->lab, nullptr, ALGO_SURF,
-                                                           Q.use_star, 1.0, g->r_lo, g->r_hi,
-                                                           g->Wt);
-    rc = launch_check("k_weights");
-  }
+  if (rc == FS_OK) rc = run_weights(g, nullptr, ALGO_SURF, 1.0);
   if (rc == FS_OK) rc = run_pass2(g, sums_dev);
   return rc;
 }

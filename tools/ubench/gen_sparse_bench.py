@@ -1,0 +1,90 @@
+"""Microbenchmark of k_score_sparse's inner loop (tools/gen_sparse_asm.py)
+on synthetic entry streams.  Writes sparse_bench.hip; build:
+  hipcc --offload-arch=gfx950 -O3 sparse_bench.hip -o sparse_bench
+Variants: 0 as shipped, 1 scalar-cache hits (same group re-read), 2 no LDS reads."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from gen_sparse_asm import gen  # noqa: E402
+
+VARIANTS = [dict(), dict(same_stream=True), dict(no_ds=True)]
+src = ["#include <hip/hip_runtime.h>", "#include <cstdio>", "#include <cstdlib>", "#include <cstdint>",
+       "#include <cstring>", "#include <vector>", "#include <random>", "#include <algorithm>",
+       '#define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)']
+for v, o in enumerate(VARIANTS):
+    src.append(gen(name=f"STREAM{v}", **o))
+src.append(r'''
+constexpr int kTile = 128, kSWaves = 16, kStreamGroups = 128;
+template <int V>
+__global__ __launch_bounds__(1024) void kern(const uint2* ent, const float* xs, int PW, int ntiles,
+                                             int tiles_per_wg, float* out) {
+  __shared__ float4 As[kTile * 64];
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (int r = wave; r < kTile; r += kSWaves) As[r * 64 + lane] = make_float4(r * 0.01f + lane, r * 0.02f, 1.0f, 2.0f);
+  __syncthreads();
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint32_t lane16 = (uint32_t)(uintptr_t)As + lane * 16u, lane4 = lane * 4u;
+  const uint32_t bstride = kSWaves * PW * 4, ncols = kTile / kSWaves;
+  for (int k = 0; k < tiles_per_wg; k++) {
+    const int t = __builtin_amdgcn_readfirstlane((int)((blockIdx.x / 32 * tiles_per_wg + k) % ntiles));
+    const uint64_t eb = (uint64_t)(uintptr_t)(ent + ((int64_t)t * kSWaves + wave) * kStreamGroups * 8);
+    const uint64_t bp = (uint64_t)(uintptr_t)(xs + (int64_t)wave * PW);
+    if (V == 0) STREAM0(acc, lane16, lane4, eb, bp, bstride, ncols);
+    if (V == 1) STREAM1(acc, lane16, lane4, eb, bp, bstride, ncols);
+    if (V == 2) STREAM2(acc, lane16, lane4, eb, bp, bstride, ncols);
+  }
+  out[blockIdx.x * 1024 + threadIdx.x] = acc[0] + acc[1] + acc[2] + acc[3] + acc[4] + acc[5] + acc[6] + acc[7];
+}
+
+int main() {
+  const int ntiles = 2048, PW = 1024;
+  const double dens = 0.42;
+  std::mt19937 rng(1);
+  std::vector<uint2> ent((size_t)(ntiles + 1) * kTile * kTile, make_uint2(0, 0));
+  std::vector<int64_t> tile_groups(ntiles, 0);
+  for (int t = 0; t < ntiles; t++)
+    for (int w = 0; w < kSWaves; w++) {
+      uint2* o = &ent[((size_t)t * kSWaves + w) * kStreamGroups * 8];
+      int off = 0;
+      for (int m = 0; m < kTile / kSWaves; m++) {
+        int c = 0;
+        for (int ii = 0; ii < kTile; ii++)
+          if (std::uniform_real_distribution<double>(0, 1)(rng) < dens) o[off + c++] = make_uint2(ii * 1024u, 0x3c000000u);
+        int pad = c == 0 ? 8 : (c + 7) / 8 * 8;
+        for (int e = c; e < pad; e++) o[off + e] = make_uint2(0, 0);
+        o[off + pad - 8].y |= 1u;
+        off += pad;
+        tile_groups[t] += pad / 8;
+      }
+    }
+  uint2* dent; float *dxs, *dout;
+  CHK(hipMalloc(&dent, ent.size() * 8)); CHK(hipMemcpy(dent, ent.data(), ent.size() * 8, hipMemcpyHostToDevice));
+  CHK(hipMalloc(&dxs, (size_t)(kTile + 2) * PW * 4)); CHK(hipMemset(dxs, 0, (size_t)(kTile + 2) * PW * 4));
+  const int wgs = 4096, tpw = 4;
+  CHK(hipMalloc(&dout, (size_t)wgs * 1024 * 4));
+  double g_total = 0;
+  for (int b = 0; b < wgs; b++) for (int k = 0; k < tpw; k++) g_total += tile_groups[(b / 32 * tpw + k) % ntiles];
+  const char* nm[3] = {"as shipped", "scalar-cache hits", "no LDS reads"};
+  for (int v = 0; v < 3; v++) {
+    auto K = v == 0 ? kern<0> : v == 1 ? kern<1> : kern<2>;
+    hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
+    float best = 1e30f;
+    for (int rep = 0; rep < 4; rep++) {
+      CHK(hipEventRecord(e0));
+      K<<<wgs, 1024>>>(dent, dxs, PW, ntiles, tpw, dout);
+      CHK(hipEventRecord(e1)); CHK(hipEventSynchronize(e1));
+      float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
+      if (rep && ms < best) best = ms;
+    }
+    CHK(hipGetLastError());
+    const double gt = v == 1 ? (double)wgs * tpw * kSWaves * 130 : g_total;  // same_stream: ~130 groups per stream
+    const double valu_ms = gt * 72 * 2 / 1024.0 / 2.4e9 * 1e3;
+    printf("%-20s %8.3f ms   groups %.3g  cycles/group/SIMD %.1f  (VALU floor %.3f ms = %.0f%%)\n", nm[v], best,
+           gt, best * 1e-3 * 2.4e9 * 1024 / gt, valu_ms, 100 * valu_ms / best);
+    fflush(stdout);
+  }
+  return 0;
+}
+''')
+open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "sparse_bench.hip"), "w").write("\n".join(src))
