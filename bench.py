@@ -165,24 +165,33 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t_start
     _, _, refined = job.info()
+    weighted = job.weighted_pairs()  # non-zero pass-2 weights (sparse pass 2), -1 if dense
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
 
-    # dominant kernel roofline (rank-local launch).  Algorithmic count: unique
-    # pairs x features / world (padding and the duplicated half of diagonal
-    # tiles are executed but not counted).
+    # dominant kernel roofline (rank-local launch).  Algorithmic count of
+    # pass 1: unique pairs x features / world (padding and the duplicated half
+    # of diagonal tiles are executed but not counted); of pass 2: the pairs
+    # with a non-zero weight x features when pass 2 is sparse (the work the
+    # reference's near/far accumulation needs), else every unique pair.
     d_ms, s_ms = float(np.mean(dist_ms)), float(np.mean(score_ms))
-    pfe_launch = args.samples * (args.samples - 1) / 2.0 * args.features / world
-    kern = {"k_dist": d_ms, "k_score": s_ms}
+    pairs_dense = args.samples * (args.samples - 1) / 2.0 / world
+    pairs_score = weighted if weighted >= 0 else pairs_dense
+    score_name = "k_score_sparse" if weighted >= 0 else "k_score"
+    pfe = {"k_dist": pairs_dense * args.features, score_name: pairs_score * args.features}
+    kern = {"k_dist": d_ms, score_name: s_ms}
     dom = max(kern, key=kern.get)
+    pfe_launch = pfe[dom]
     achieved = FLOP_PER_PFE * pfe_launch / (kern[dom] * 1e-3) / 1e12
     # algorithmic bytes one launch moves from HBM/L2 into the CUs: both row
-    # panels of every owned tile once (+ D write for k_dist, Wt read for k_score)
+    # panels of every owned tile once (+ D write for k_dist; the pair weights
+    # for k_score: 8-byte entries when sparse, the dense 128x128 f32 tiles else)
+    w_bytes = weighted * 8 if weighted >= 0 else tiles * 128 * 128 * 4
     alg_bytes = {"k_dist": tiles * (2 * 128 * args.features * 4 + 2 * 128 * 128 * 8),
-                 "k_score": tiles * (2 * 128 * args.features * 4 + 128 * 128 * 4)}
+                 score_name: tiles * 2 * 128 * args.features * 4 + w_bytes}
     traffic, traffic_src = pmc_traffic(dom, args.samples, args.features, world)
 
     if rank == 0:
@@ -200,7 +209,8 @@ def main():
             "dtype": "fp32",
             "arith": "pass 1: integer L1 distances (v_sad_u16 on 16-bit operands for n >= 16384, "
                      "else v_sad_u32), pairs near a threshold recomputed in the reference's "
-                     "float32 arithmetic; pass 2: f32 diffs x f32 pair weights, f64 accumulation",
+                     "float32 arithmetic; pass 2 over the pairs with a non-zero weight: f32 diffs x "
+                     "f32 pair weights, f64 accumulation",
             "data": "synthetic make_classification(n_informative=20, n_redundant=100, random_state=42)",
             "config": {"workload": f"MultiSURF{'*' if args.star else ''} n={args.samples} "
                                    f"p={args.features} (BASELINE configs[3])",
@@ -217,6 +227,8 @@ def main():
                 "pfe_per_s": pfe_launch / (kern[dom] * 1e-3),
                 "kernel_ms": kern,
                 "pfe_per_launch": pfe_launch,
+                "pass2_weighted_pairs": weighted,
+                "pass2_pair_density": (pairs_score / pairs_dense) if pairs_dense else None,
                 "hbm_alg_GBps": {k: alg_bytes[k] / (kern[k] * 1e-3) / 1e9 for k in kern},
                 "hbm_peak_GBps": HBM_PEAK_GBPS,
             },

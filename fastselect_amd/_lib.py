@@ -39,7 +39,7 @@ EXPORTED = (
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2",
-    "fs_plan_info", "fs_plan_kernel_ms", "fs_plan_destroy",
+    "fs_plan_info", "fs_plan_weighted_pairs", "fs_plan_kernel_ms", "fs_plan_destroy",
 )
 
 
@@ -95,13 +95,14 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_select.argtypes = [_vp, _vp, _vp]
     lib.fs_plan_pass2.argtypes = [_vp, _vp, _vp]
     lib.fs_plan_info.argtypes = [_vp, _i64p, _f64p, _i64p]
+    lib.fs_plan_weighted_pairs.argtypes = [_vp, _i64p]
     lib.fs_plan_kernel_ms.argtypes = [_vp, _int]
     lib.fs_plan_kernel_ms.restype = ctypes.c_double
     lib.fs_plan_destroy.argtypes = [_vp]
     for name in ("fs_column_stats", "fs_multisurf_score", "fs_relieff_score", "fs_surf_score",
                  "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create",
                  "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
-                 "fs_plan_pass2", "fs_plan_info", "fs_plan_destroy"):
+                 "fs_plan_pass2", "fs_plan_info", "fs_plan_weighted_pairs", "fs_plan_destroy"):
         getattr(lib, name).restype = _int
     return lib
 
@@ -287,6 +288,12 @@ class Plan:
         check(_lib.fs_plan_info(self._h, ctypes.byref(tiles), ctypes.byref(pfe),
                                 ctypes.byref(ref)))
         return int(tiles.value), float(pfe.value), int(ref.value)
+
+    def weighted_pairs(self) -> int:
+        """Owned pairs with a non-zero weight in the last pass 2 (-1: not counted)."""
+        v = ctypes.c_int64(-1)
+        check(_lib.fs_plan_weighted_pairs(self._h, ctypes.byref(v)))
+        return int(v.value)
 
     def kernel_ms(self, which: int) -> float:
         return float(_lib.fs_plan_kernel_ms(self._h, int(which)))

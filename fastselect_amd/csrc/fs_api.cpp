@@ -476,6 +476,16 @@ int fs_plan_info(const fs_plan* pl, int64_t* owned_tiles_out, double* pfe,
   return FS_OK;
 }
 
+int fs_plan_weighted_pairs(const fs_plan* pl, int64_t* pairs) {
+  if (!pl || !pairs) {
+    set_error("NULL plan or output");
+    return FS_EINVAL;
+  }
+  *pairs = -1;
+  if (pl->g) return gpu::plan_weighted_pairs(pl->g, pairs);
+  return FS_OK;
+}
+
 double fs_plan_kernel_ms(const fs_plan* pl, int which) {
   if (!pl || !pl->g) return -1.0;
   return gpu::plan_kernel_ms(pl->g, which);

@@ -971,13 +971,14 @@ __global__ __launch_bounds__(1024) void k_weights_sparse(
     const double* __restrict__ D, int64_t n, int64_t n_pad, const int2* __restrict__ tiles,
     const double* __restrict__ thr, const int32_t* __restrict__ lab,
     const double* __restrict__ counts, int algo, int use_star, double inv_sc, int64_t r_lo,
-    int64_t r_hi, uint2* __restrict__ ent) {
+    int64_t r_hi, uint2* __restrict__ ent, unsigned long long* __restrict__ nnz) {
+  __shared__ int wave_nnz[kSWaves];
   const int2 tl = tiles[blockIdx.x];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint2* out = ent + ((int64_t)blockIdx.x * kSWaves + wave) * kStreamEntries;
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  int off = 0;
+  int off = 0, nz = 0;
   for (int jj = wave; jj < kTile; jj += kSWaves) {
     const float w0 = pair_weight(D, n, n_pad, i0 + lane, j0 + jj, tl.x < tl.y || lane < jj, thr,
                                  lab, counts, algo, use_star, inv_sc, r_lo, r_hi);
@@ -994,6 +995,15 @@ __global__ __launch_bounds__(1024) void k_weights_sparse(
       out[off + e1] = make_uint2((uint32_t)(lane + 64) * 1024u, weight_bits(w1, e1 == last));
     if (ep < padded) out[off + ep] = make_uint2(0u, ep == last ? 1u : 0u);
     off += padded;
+    nz += total;
+  }
+  // non-zero pairs of the tile (throughput accounting)
+  if (lane == 0) wave_nnz[wave] = nz;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kSWaves; w++) t += (unsigned long long)wave_nnz[w];
+    atomicAdd(nnz, t);
   }
 }
 
@@ -1839,6 +1849,8 @@ struct Plan {
   double* thr = nullptr;
   float* Wt = nullptr;          // dense pair weights (sparse == 0)
   uint2* ent = nullptr;         // sparse pair-weight streams (sparse == 1)
+  unsigned long long* nnz = nullptr;  // non-zero weights of the last pass 2
+  bool nnz_valid = false;
   int sparse = 0;               // pass 2 over non-zero weights only
   double* spart = nullptr;
   // ambiguous-pair refinement
@@ -2142,7 +2154,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     // stream.  Zeroed once, so such reads (and stream tails never written)
     // hold in-range row offsets.
     const size_t count = (size_t)(g->n_tiles + 1) * kSWaves * kStreamEntries;
-    if ((rc = dalloc(g, &g->ent, count))) return fail(rc);
+    if ((rc = dalloc(g, &g->ent, count)) || (rc = dalloc(g, &g->nnz, 1))) return fail(rc);
     if (hipMemsetAsync(g->ent, 0, sizeof(uint2) * count, g->stream) != hipSuccess)
       return fail(FS_EHIP);
   }
@@ -2287,9 +2299,11 @@ static int run_weights(Plan* g, const double* counts, int algo, double inv_sc) {
   const Prepared& Q = g->P;
   if (g->n_tiles == 0) return FS_OK;
   if (g->sparse) {
+    FS_HIP(hipMemsetAsync(g->nnz, 0, sizeof(unsigned long long), g->stream));
+    g->nnz_valid = true;
     k_weights_sparse<<<(unsigned)g->n_tiles, 64 * kSWaves, 0, g->stream>>>(
         g->D, Q.n, Q.n_pad, g->tiles, g->thr, g->lab, counts, algo, Q.use_star, inv_sc, g->r_lo,
-        g->r_hi, g->ent);
+        g->r_hi, g->ent, g->nnz);
     return launch_check("k_weights_sparse");
   }
   k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles, g->thr,
@@ -2369,6 +2383,17 @@ int plan_info(const Plan* g, int64_t* tiles, double* pfe, int64_t* refined) {
     *pfe = 2.0 * (double)g->n_tiles * kTile * kTile * (double)(g->P.pc + g->P.pd);
   }
   if (refined) *refined = g->n_refined;
+  return FS_OK;
+}
+
+int plan_weighted_pairs(Plan* g, int64_t* pairs) {
+  *pairs = -1;
+  if (!g->sparse || !g->nnz_valid) return FS_OK;
+  FS_HIP(hipSetDevice(g->device));
+  unsigned long long v = 0;
+  FS_HIP(hipMemcpyAsync(&v, g->nnz, sizeof(v), hipMemcpyDeviceToHost, g->stream));
+  FS_HIP(hipStreamSynchronize(g->stream));
+  *pairs = (int64_t)v;
   return FS_OK;
 }
 

@@ -288,6 +288,7 @@ int plan_pass2(Plan* g, const double* counts_dev, double* scores_dev);
 int plan_score(Plan* g, double* sums_dev);
 int plan_info(const Plan* g, int64_t* tiles, double* pfe, int64_t* refined);
 double plan_kernel_ms(const Plan* g, int which);
+int plan_weighted_pairs(Plan* g, int64_t* pairs);
 void plan_destroy(Plan* g);
 // Single-GPU one-shot runs (host in/out).  MultiSURF: scores already divided
 // by n.  SURF / ReliefF: float64 score sums of the focal samples [r_lo, r_hi)

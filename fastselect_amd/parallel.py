@@ -99,6 +99,9 @@ class ShardedMultiSURF:
     def info(self):
         return self.plan.info()
 
+    def weighted_pairs(self) -> int:
+        return self.plan.weighted_pairs()
+
     def kernel_ms(self, which: int) -> float:
         return self.plan.kernel_ms(which)
 

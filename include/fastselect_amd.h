@@ -224,6 +224,10 @@ FS_API int fs_plan_score(fs_plan* plan, double* sums);
  * skipped. */
 FS_API int fs_plan_info(const fs_plan* plan, int64_t* owned_tiles, double* pair_feature_evals,
                         int64_t* refined_pairs);
+/* Owned pairs that carried a non-zero pass-2 weight in the last pass 2 (the
+ * pairs the sparse GPU pass 2 evaluates; -1 when the plan does not count
+ * them: CPU backend, dense pass 2, or before the first pass 2). */
+FS_API int fs_plan_weighted_pairs(const fs_plan* plan, int64_t* pairs);
 /* Average duration in milliseconds of the last pass1 / pass2 distance and
  * score kernels, measured with HIP events on the plan's stream (GPU only;
  * -1 when unavailable).  which: 0 = distance kernel, 1 = score kernel. */

@@ -427,3 +427,51 @@ def test_two_ranks_share_one_gpu(tmp_path):
     X, y = make_classification(n_samples=900, n_features=400, random_state=7)
     ref = MultiSURF(backend="gpu").fit(X, y).feature_importances_
     assert scale_rel_err(a, ref) < 1e-6
+
+
+@pytest.mark.parametrize("algo,star", [("multisurf", False), ("multisurf", True), ("surf", False),
+                                       ("surf", True)])
+def test_sparse_pass2_matches_dense(monkeypatch, algo, star):
+    """k_weights_sparse + k_score_sparse (non-zero pair weights only) against
+    the dense k_weights + k_score on the same data (FS_SPARSE forces either),
+    with mixed continuous/discrete blocks so both the asm loop and the generic
+    loop run; and both against the oracle."""
+    from fastselect_amd import SURF, MultiSURF
+    from oracle import oracle as O
+    rng = np.random.default_rng(7)
+    X, y = make_classification(n_samples=700, n_features=600, n_informative=15,
+                               n_redundant=30, random_state=3)
+    X[:, 500:] = rng.integers(0, 3, size=(700, 100))  # discrete tail: a mixed 256-block
+    est = MultiSURF if algo == "multisurf" else SURF
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("FS_SPARSE", mode)
+        out[mode] = _fit(est, X, y, use_star=star)
+    ref = (O.multisurf_scores if algo == "multisurf" else O.surf_scores)(X, y, use_star=star)
+    assert scale_rel_err(out["1"], out["0"]) <= 1e-6
+    assert_parity(out["1"], ref, TOL, k=10)
+
+
+def test_sparse_weighted_pairs_count():
+    """fs_plan_weighted_pairs: MultiSURF weighs the pairs near one of their two
+    samples (~40% here); the count is exact against a numpy restatement."""
+    from fastselect_amd.parallel import ShardedMultiSURF
+    X, y = make_classification(n_samples=600, n_features=300, n_informative=10,
+                               n_redundant=20, random_state=5)
+    X = X.astype(np.float32)
+    recip = (1 / (X.max(0) - X.min(0))).astype(np.float32)
+    job = ShardedMultiSURF(X, y, recip, np.zeros(300, bool), use_star=False, backend="gpu",
+                           device=0)
+    job.step()
+    nz = job.weighted_pairs()
+    job.close()
+    Xs = (X - X.min(0)) * recip
+    D = np.abs(Xs[:, None, :].astype(np.float64) - Xs[None, :, :]).sum(-1)
+    n = len(X)
+    off = ~np.eye(n, dtype=bool)
+    mu = D.sum(1) / (n - 1)
+    sd = np.sqrt(np.maximum((D ** 2).sum(1) / (n - 1) - mu ** 2, 0))
+    near = (D < (mu - sd / 2)[:, None]) & off
+    want = int(np.triu(near | near.T, 1).sum())
+    assert 0.2 * n * (n - 1) / 2 < nz < 0.7 * n * (n - 1) / 2
+    assert abs(nz - want) <= max(3, want // 2000)

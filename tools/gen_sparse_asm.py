@@ -31,32 +31,44 @@ Fixed registers (clobbered; the compiler keeps its own values elsewhere):
 import os
 
 SETS = [40, 56, 72]
-ASETS = [64, 96]
 
 
-def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False):
-    """Macro text.  no_ds / same_stream: microbenchmark variants that skip the
-    LDS reads / keep re-reading the stream's first group (scalar-cache hits)."""
+def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4):
+    """Macro text.  feats: features per lane (4: 128 KB LDS block, float4 rows;
+    2: 64 KB, float2 rows, 64-VGPR budget).  no_ds / same_stream:
+    microbenchmark variants that skip the LDS reads / keep re-reading the
+    stream's first groups (scalar-cache hits)."""
+    F = feats
+    if F == 4:
+        ASETS, BCUR, BNXT, TMP, VLO = [64, 96], 56, 60, [48, 52], 48
+        rd = "ds_read_b128"
+    else:
+        ASETS, BCUR, BNXT, TMP, VLO = [32, 48], 26, 28, [22, 24], 22
+        rd = "ds_read_b64"
 
     def issue_rows(k, a):
         s, A = SETS[k], ASETS[a]
-        L = [f"v_add_u32 v{A + 4 * q}, s{s + 2 * q}, %[lane16]" for q in range(8)]
+        L = [f"v_add_u32 v{A + F * q}, s{s + 2 * q}, %[lane16]" for q in range(8)]
         if not no_ds:
-            L += [f"ds_read_b128 v[{A + 4 * q}:{A + 4 * q + 3}], v{A + 4 * q}" for q in range(8)]
+            L += [f"{rd} v[{A + F * q}:{A + F * q + F - 1}], v{A + F * q}" for q in range(8)]
         return L
 
     def compute(k, a):
         s, A = SETS[k], ASETS[a]
         L = []
         for q in range(8):
-            t = 48 if q % 2 == 0 else 52
+            t = TMP[q % 2]
             w = f"s{s + 2 * q + 1}"
-            for f in range(4):
-                L.append(f"v_sub_f32 v{t + f}, v{A + 4 * q + f}, v{56 + f}")
-            for f in range(4):
+            for f in range(F):
+                L.append(f"v_sub_f32 v{t + f}, v{A + F * q + f}, v{BCUR + f}")
+            for f in range(F):
                 acc = f"%[acc{2 * f + (q & 1)}]"
                 L.append(f"v_fma_f32 {acc}, {w}, |v{t + f}|, {acc}")
         return L
+
+    def bload(dst):
+        return [f"global_load_dword v{dst + f}, %[lane4], s[90:91]" + (f" offset:{256 * f}" if f else "")
+                for f in range(F)]
 
     def step(x):
         c, n, nn = x % 3, (x + 1) % 3, (x + 2) % 3
@@ -80,31 +92,22 @@ def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False):
                 "s_cmp_ge_u32 s88, %[ncols]",
                 "s_cbranch_scc1 8f",
                 "s_waitcnt vmcnt(0)",
-                "v_mov_b32 v56, v60", "v_mov_b32 v57, v61", "v_mov_b32 v58, v62", "v_mov_b32 v59, v63",
+                *[f"v_mov_b32 v{BCUR + f}, v{BNXT + f}" for f in range(F)],
                 "s_add_u32 s35, s88, 1",
                 "s_cmp_ge_u32 s35, %[ncols]",
                 f"s_cbranch_scc1 {20 + x}b",
                 "s_add_u32 s90, s90, %[bstride]",
                 "s_addc_u32 s91, s91, 0",
-                "global_load_dword v60, %[lane4], s[90:91]",
-                "global_load_dword v61, %[lane4], s[90:91] offset:256",
-                "global_load_dword v62, %[lane4], s[90:91] offset:512",
-                "global_load_dword v63, %[lane4], s[90:91] offset:768",
+                *bload(BNXT),
                 f"s_branch {20 + x}b"]
 
     lines = [
         "s_mov_b32 s88, 0",
         "s_mov_b64 s[90:91], %[bp]",
-        "global_load_dword v56, %[lane4], s[90:91]",
-        "global_load_dword v57, %[lane4], s[90:91] offset:256",
-        "global_load_dword v58, %[lane4], s[90:91] offset:512",
-        "global_load_dword v59, %[lane4], s[90:91] offset:768",
+        *bload(BCUR),
         "s_add_u32 s90, s90, %[bstride]",
         "s_addc_u32 s91, s91, 0",
-        "global_load_dword v60, %[lane4], s[90:91]",
-        "global_load_dword v61, %[lane4], s[90:91] offset:256",
-        "global_load_dword v62, %[lane4], s[90:91] offset:512",
-        "global_load_dword v63, %[lane4], s[90:91] offset:768",
+        *bload(BNXT),
         "s_mov_b64 s[36:37], %[eb]",
         "s_mov_b32 s34, 0",
         "s_load_dwordx16 s[40:55], s[36:37], s34",
@@ -113,7 +116,7 @@ def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False):
     lines += issue_rows(0, 0)
     lines.append("s_add_u32 s34, s34, 64")
     lines.append("s_load_dwordx16 s[56:71], s[36:37], s34")
-    lines.append("s_waitcnt vmcnt(4)")
+    lines.append(f"s_waitcnt vmcnt({F})")
     lines.append("7:")
     for x in range(6):
         lines += step(x)
@@ -129,13 +132,13 @@ def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False):
     lines.append("s_waitcnt vmcnt(0) lgkmcnt(0)")
 
     body = "\n".join(f'      "{l}\\n"  \\' for l in lines)
-    vclob = ", ".join(f'"v{i}"' for i in range(48, 128))
+    vclob = ", ".join(f'"v{i}"' for i in range(VLO, ASETS[1] + 8 * F))
+    nacc = 2 * F
     sclob = ", ".join(f'"s{i}"' for i in range(34, 92))
     return f'''#define {name}(acc, lane16, lane4, eb, bp, bstride, ncols)  \\
   asm volatile(  \\
 {body}
-      : [acc0] "+v"(acc[0]), [acc1] "+v"(acc[1]), [acc2] "+v"(acc[2]), [acc3] "+v"(acc[3]),  \\
-        [acc4] "+v"(acc[4]), [acc5] "+v"(acc[5]), [acc6] "+v"(acc[6]), [acc7] "+v"(acc[7])   \\
+      : {", ".join(f'[acc{i}] "+v"(acc[{i}])' for i in range(nacc))}  \\
       : [lane16] "v"(lane16), [lane4] "v"(lane4), [eb] "s"(eb), [bp] "s"(bp),  \\
         [bstride] "s"(bstride), [ncols] "s"(ncols)  \\
       : {vclob},  \\
@@ -153,3 +156,176 @@ if __name__ == "__main__":
                         "fs_sparse_asm.inc")
     open(path, "w").write(HEADER + gen())
     print("wrote", os.path.normpath(path))
+
+
+# ---------------------------------------------------------------------------
+# v2 stream: entries through vector memory + DPP broadcast (no scalar loads)
+# ---------------------------------------------------------------------------
+DPP_DOC = """
+Entries through vector memory (no scalar loads in the loop).  A stream (one
+wave, one tile) is its groups back to back (64 B = 8 entries (roff, w)); the
+group counts of its 8 columns come once per stream (s_load_dwordx4 of
+{counts 0-3, counts 4-7, total, 0}).  Lane l loads entry (l & 15) of a group
+pair (global_load_dwordx2, every 16-lane row holds the same 16 entries), and
+entry q of group g is broadcast by DPP row_newbcast:(q + 8 (g & 1)) straight
+into the instruction that uses it:
+  v_add_u32_dpp    addr = roff + lane16           (LDS address of the row)
+  v_fmac_f32_dpp   acc += w * |a - b|
+so the pipeline waits are in-order counters only (vmcnt for entries and B,
+lgkmcnt for the LDS rows) and can run several groups ahead:
+  step g:  [g even] load entry pair g/2 + 3
+           wait entries of g+1; 8 x (v_add_u32_dpp, ds_read_b128) rows of g+1
+           wait B of g and rows of g (lgkmcnt(8))
+           8 x (4 v_sub_f32, 4 v_fmac_f32_dpp)        group g
+           4 x global_load_dword B of group g+4 (its column's row)
+Fixed registers: v64..v127 two A sets, v48..v63 four B sets, v40..v47 four
+entry pairs, v32..v39 |diff| temporaries; s36..s47 stream state.
+"""
+
+
+def gen_dpp(name="FS_SPARSE_STREAM_ASM", plain_fma=False, no_b=False, no_ds=False, plain_add=False):
+    ASET = [64, 96]
+    BSET = [48, 52, 56, 60]
+    ESET = [40, 42, 44, 46]
+    TMP = [32, 36]
+    # s[36:37] entry pointer (next pair load), s[38:39] B row of the prefetch column,
+    # s40 groups left in that column, s41 groups left to compute, s[42:43] counts of
+    # the columns after it, s44 / s45 temporaries, s[46:47] {.., ..} of the count load
+    vm = []      # issue log of vector-memory ops (labels), for the vmcnt values
+
+    def eload(p):
+        vm.append(("E", p))
+        e = ESET[p % 4]
+        return [f"global_load_dwordx2 v[{e}:{e + 1}], %[laneoff], s[36:37]",
+                "s_add_u32 s36, s36, 0x80", "s_addc_u32 s37, s37, 0"]
+
+    def bload(h):
+        b = BSET[h % 4]
+        L = []
+        if no_b and h >= 4:
+            return L
+        for f in range(4):
+            vm.append(("B", h))
+            L.append(f"global_load_dword v{b + f}, %[lane4], s[38:39]" + (f" offset:{256 * f}" if f else ""))
+        # advance the prefetch cursor: next group's column
+        L += ["s_sub_u32 s40, s40, 1", "s_cmp_eq_u32 s40, 0", f"s_cbranch_scc0 {60 + h % 8}f",
+              "s_and_b32 s40, s42, 0xff", "s_lshr_b64 s[42:43], s[42:43], 8",
+              "s_cmp_eq_u32 s40, 0",
+              "s_cselect_b32 s40, 0x7fffffff, s40",      # past the last column: stay
+              "s_cselect_b32 s44, 0, %[bstride]",
+              "s_add_u32 s38, s38, s44", "s_addc_u32 s39, s39, 0",
+              f"{60 + h % 8}:"]
+        return L
+
+    def count_after(kind, idx):
+        # VMEM ops issued after the newest op of (kind, idx)
+        hits = [i for i, v in enumerate(vm) if v == (kind, idx)]
+        return min(63, len(vm) - 1 - max(hits)) if hits else 63
+
+    def rows(g):
+        a = ASET[(g + 0) % 2]
+        e = ESET[(g // 2) % 4]
+        L = []
+        for q in range(8):
+            ln = q + 8 * (g % 2)
+            L.append(f"v_add_u32_dpp v{a + 4 * q}, v{e}, %[lane16] row_newbcast:{ln} row_mask:0xf bank_mask:0xf")
+        for q in range(8):
+            L.append(f"ds_read_b128 v[{a + 4 * q}:{a + 4 * q + 3}], v{a + 4 * q}")
+        return L
+
+    def rows_into(g):
+        a, e = ASET[g % 2], ESET[(g // 2) % 4]
+        L = []
+        for q in range(8):
+            ln = q + 8 * (g % 2)
+            if plain_add:
+                L.append(f"v_add_u32 v{a + 4 * q}, v{e}, %[lane16]")
+            else:
+                L.append(f"v_add_u32_dpp v{a + 4 * q}, v{e}, %[lane16] row_newbcast:{ln} row_mask:0xf bank_mask:0xf")
+        if not no_ds:
+            for q in range(8):
+                L.append(f"ds_read_b128 v[{a + 4 * q}:{a + 4 * q + 3}], v{a + 4 * q}")
+        return L
+
+    def compute(g):
+        a, e, b = ASET[g % 2], ESET[(g // 2) % 4], BSET[g % 4]
+        L = []
+        for q in range(8):
+            ln = q + 8 * (g % 2)
+            t = TMP[q % 2]
+            for f in range(4):
+                L.append(f"v_sub_f32 v{t + f}, v{a + 4 * q + f}, v{b + f}")
+            for f in range(4):
+                acc = f"%[acc{2 * f + (q & 1)}]"
+                if plain_fma:
+                    L.append(f"v_fma_f32 {acc}, v{e + 1}, |v{t + f}|, {acc}")
+                else:
+                    L.append(f"v_fmac_f32_dpp {acc}, v{e + 1}, |v{t + f}| row_newbcast:{ln} row_mask:0xf bank_mask:0xf")
+        return L
+
+    head = ["s_load_dwordx4 s[40:43], %[cb], 0x0",   # s40 c0..3, s41 c4..7, s42 total
+            "s_mov_b64 s[36:37], %[eb]", "s_mov_b64 s[38:39], %[bp]",
+            "s_waitcnt lgkmcnt(0)",
+            "s_mov_b32 s44, s42",                      # total groups
+            "s_mov_b32 s42, s40", "s_mov_b32 s43, s41",   # counts word
+            "s_mov_b32 s41, s44",
+            "s_and_b32 s40, s42, 0xff", "s_lshr_b64 s[42:43], s[42:43], 8",
+            "s_cmp_eq_u32 s41, 0", "s_cbranch_scc1 9f"]
+    head += eload(0) + eload(1) + eload(2)
+    for h in range(4):
+        head += bload(h)
+    head.append(f"s_waitcnt vmcnt({count_after('E', 0)})")
+    head += rows(0)
+
+    # Loop body: 8 steps.  vmcnt(N) is safe when N <= the number of vector
+    # memory ops issued after the awaited one; the body is simulated for
+    # several passes (pass 0 follows the prologue) and each wait takes the
+    # minimum over the passes.
+    waits = {}
+
+    def body(pas, emit):
+        out = []
+        for g in range(8):
+            G = 8 * pas + g                  # global group index in the simulation
+            if g % 2 == 0:
+                out += eload(G // 2 + 3)
+            k = ("E", g)
+            if not emit:
+                waits[k] = min(waits.get(k, 99), count_after("E", (G + 1) // 2))
+            out.append(f"s_waitcnt vmcnt({waits[k] if emit else 0})")
+            out += rows_into(G + 1)
+            k = ("B", g)
+            if not emit:
+                waits[k] = min(waits.get(k, 99), count_after("B", G))
+            out.append(f"s_waitcnt vmcnt({waits[k] if emit else 0}) lgkmcnt(8)")
+            out += compute(G)
+            out += bload(G + 4)
+            out += ["s_sub_u32 s41, s41, 1", "s_cmp_eq_u32 s41, 0", "s_cbranch_scc1 8f"]
+        return out
+
+    for pas in range(4):
+        body(pas, False)
+    lines = head
+    lines.append("7:")
+    lines += body(0, True)
+    lines.append("s_branch 7b")
+    lines.append("8:")
+    lines.append("9:")
+    lines.append("s_waitcnt vmcnt(0) lgkmcnt(0)")
+    return lines, waits
+
+
+def gen_dpp_macro(name="FS_SPARSE_STREAM_ASM", **opts):
+    lines, _ = gen_dpp(name, **opts)
+    body = "\n".join(f'      "{l}\\n"  \\' for l in lines)
+    vclob = ", ".join(f'"v{i}"' for i in range(32, 128))
+    sclob = ", ".join(f'"s{i}"' for i in range(36, 48))
+    return f'''#define {name}(acc, lane16, lane4, laneoff, eb, cb, bp, bstride)  \\
+  asm volatile(  \\
+{body}
+      : {", ".join(f'[acc{i}] "+v"(acc[{i}])' for i in range(8))}  \\
+      : [lane16] "v"(lane16), [lane4] "v"(lane4), [laneoff] "v"(laneoff), [eb] "s"(eb),  \\
+        [cb] "s"(cb), [bp] "s"(bp), [bstride] "s"(bstride)  \\
+      : {vclob},  \\
+        {sclob}, "scc", "memory")
+'''

@@ -8,7 +8,7 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from gen_sparse_asm import gen  # noqa: E402
 
-VARIANTS = [dict(), dict(same_stream=True), dict(no_ds=True)]
+VARIANTS = [dict(), dict(feats=2), dict(feats=2, same_stream=True), dict(feats=2, no_ds=True)]
 src = ["#include <hip/hip_runtime.h>", "#include <cstdio>", "#include <cstdlib>", "#include <cstdint>",
        "#include <cstring>", "#include <vector>", "#include <random>", "#include <algorithm>",
        '#define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)']
@@ -16,15 +16,16 @@ for v, o in enumerate(VARIANTS):
     src.append(gen(name=f"STREAM{v}", **o))
 src.append(r'''
 constexpr int kTile = 128, kSWaves = 16, kStreamGroups = 128;
-template <int V>
-__global__ __launch_bounds__(1024) void kern(const uint2* ent, const float* xs, int PW, int ntiles,
-                                             int tiles_per_wg, float* out) {
-  __shared__ float4 As[kTile * 64];
+template <int V, int F>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(F == 4 ? 4 : 8, F == 4 ? 4 : 8)))
+void kern(const uint2* ent, const float* xs, int PW, int ntiles, int tiles_per_wg, float* out) {
+  __shared__ float As[kTile * 64 * F];
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  for (int r = wave; r < kTile; r += kSWaves) As[r * 64 + lane] = make_float4(r * 0.01f + lane, r * 0.02f, 1.0f, 2.0f);
+  for (int r = wave; r < kTile; r += kSWaves)
+    for (int f = 0; f < F; f++) As[(r * 64 + lane) * F + f] = r * 0.01f + lane + f;
   __syncthreads();
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  const uint32_t lane16 = (uint32_t)(uintptr_t)As + lane * 16u, lane4 = lane * 4u;
+  const uint32_t lane16 = (uint32_t)(uintptr_t)As + lane * 4u * F, lane4 = lane * 4u;
   const uint32_t bstride = kSWaves * PW * 4, ncols = kTile / kSWaves;
   for (int k = 0; k < tiles_per_wg; k++) {
     const int t = __builtin_amdgcn_readfirstlane((int)((blockIdx.x / 32 * tiles_per_wg + k) % ntiles));
@@ -33,6 +34,7 @@ __global__ __launch_bounds__(1024) void kern(const uint2* ent, const float* xs, 
     if (V == 0) STREAM0(acc, lane16, lane4, eb, bp, bstride, ncols);
     if (V == 1) STREAM1(acc, lane16, lane4, eb, bp, bstride, ncols);
     if (V == 2) STREAM2(acc, lane16, lane4, eb, bp, bstride, ncols);
+    if (V == 3) STREAM3(acc, lane16, lane4, eb, bp, bstride, ncols);
   }
   out[blockIdx.x * 1024 + threadIdx.x] = acc[0] + acc[1] + acc[2] + acc[3] + acc[4] + acc[5] + acc[6] + acc[7];
 }
@@ -41,7 +43,7 @@ int main() {
   const int ntiles = 2048, PW = 1024;
   const double dens = 0.42;
   std::mt19937 rng(1);
-  std::vector<uint2> ent((size_t)(ntiles + 1) * kTile * kTile, make_uint2(0, 0));
+  std::vector<uint2> ent((size_t)(ntiles + 1) * kTile * kTile, make_uint2(0, 0)), ent2;
   std::vector<int64_t> tile_groups(ntiles, 0);
   for (int t = 0; t < ntiles; t++)
     for (int w = 0; w < kSWaves; w++) {
@@ -58,30 +60,35 @@ int main() {
         tile_groups[t] += pad / 8;
       }
     }
-  uint2* dent; float *dxs, *dout;
+  ent2 = ent;
+  for (auto& e : ent2) e.x /= 2;   // float2 rows: 512-byte stride
+  uint2 *dent, *dent2; float *dxs, *dout;
   CHK(hipMalloc(&dent, ent.size() * 8)); CHK(hipMemcpy(dent, ent.data(), ent.size() * 8, hipMemcpyHostToDevice));
+  CHK(hipMalloc(&dent2, ent.size() * 8)); CHK(hipMemcpy(dent2, ent2.data(), ent.size() * 8, hipMemcpyHostToDevice));
   CHK(hipMalloc(&dxs, (size_t)(kTile + 2) * PW * 4)); CHK(hipMemset(dxs, 0, (size_t)(kTile + 2) * PW * 4));
   const int wgs = 4096, tpw = 4;
   CHK(hipMalloc(&dout, (size_t)wgs * 1024 * 4));
   double g_total = 0;
   for (int b = 0; b < wgs; b++) for (int k = 0; k < tpw; k++) g_total += tile_groups[(b / 32 * tpw + k) % ntiles];
-  const char* nm[3] = {"as shipped", "scalar-cache hits", "no LDS reads"};
-  for (int v = 0; v < 3; v++) {
-    auto K = v == 0 ? kern<0> : v == 1 ? kern<1> : kern<2>;
+  const char* nm[4] = {"F4 as shipped", "F2 8 waves/SIMD", "F2 scalar-cache hits", "F2 no LDS reads"};
+  for (int v = 0; v < 4; v++) {
+    auto K = v == 0 ? kern<0, 4> : v == 1 ? kern<1, 2> : v == 2 ? kern<2, 2> : kern<3, 2>;
+    const int F = v == 0 ? 4 : 2;
     hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
     float best = 1e30f;
     for (int rep = 0; rep < 4; rep++) {
       CHK(hipEventRecord(e0));
-      K<<<wgs, 1024>>>(dent, dxs, PW, ntiles, tpw, dout);
+      K<<<wgs, 1024>>>(F == 4 ? dent : dent2, dxs, PW, ntiles, tpw, dout);
       CHK(hipEventRecord(e1)); CHK(hipEventSynchronize(e1));
       float ms; CHK(hipEventElapsedTime(&ms, e0, e1));
       if (rep && ms < best) best = ms;
     }
     CHK(hipGetLastError());
-    const double gt = v == 1 ? (double)wgs * tpw * kSWaves * 130 : g_total;  // same_stream: ~130 groups per stream
-    const double valu_ms = gt * 72 * 2 / 1024.0 / 2.4e9 * 1e3;
-    printf("%-20s %8.3f ms   groups %.3g  cycles/group/SIMD %.1f  (VALU floor %.3f ms = %.0f%%)\n", nm[v], best,
-           gt, best * 1e-3 * 2.4e9 * 1024 / gt, valu_ms, 100 * valu_ms / best);
+    const double gt = v == 2 ? (double)wgs * tpw * kSWaves * 130 : g_total;  // same_stream: ~130 groups per stream
+    const double valu_ms = gt * (F == 4 ? 80 : 40) * 2 / 1024.0 / 2.4e9 * 1e3;
+    // per-feature normalisation: cycles per entry-feature
+    printf("%-22s %8.3f ms   groups %.3g  cycles/group/SIMD %.1f  per entry-feature %.2f  (VALU floor %.3f ms = %.0f%%)\n", nm[v], best,
+           gt, best * 1e-3 * 2.4e9 * 1024 / gt, best * 1e-3 * 2.4e9 * 1024 / gt / (8 * F), valu_ms, 100 * valu_ms / best);
     fflush(stdout);
   }
   return 0;
