@@ -8,7 +8,7 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from gen_sparse_asm import gen  # noqa: E402
 
-VARIANTS = [dict(), dict(feats=2), dict(feats=2, same_stream=True), dict(feats=2, no_ds=True)]
+VARIANTS = [dict(), dict(spread=True), dict(same_stream=True), dict(no_ds=True)]
 src = ["#include <hip/hip_runtime.h>", "#include <cstdio>", "#include <cstdlib>", "#include <cstdint>",
        "#include <cstring>", "#include <vector>", "#include <random>", "#include <algorithm>",
        '#define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)']
@@ -70,10 +70,10 @@ int main() {
   CHK(hipMalloc(&dout, (size_t)wgs * 1024 * 4));
   double g_total = 0;
   for (int b = 0; b < wgs; b++) for (int k = 0; k < tpw; k++) g_total += tile_groups[(b / 32 * tpw + k) % ntiles];
-  const char* nm[4] = {"F4 as shipped", "F2 8 waves/SIMD", "F2 scalar-cache hits", "F2 no LDS reads"};
+  const char* nm[4] = {"F4 as shipped", "F4 spread LDS issue", "F4 scalar-cache hits", "F4 no LDS reads"};
   for (int v = 0; v < 4; v++) {
-    auto K = v == 0 ? kern<0, 4> : v == 1 ? kern<1, 2> : v == 2 ? kern<2, 2> : kern<3, 2>;
-    const int F = v == 0 ? 4 : 2;
+    auto K = v == 0 ? kern<0, 4> : v == 1 ? kern<1, 4> : v == 2 ? kern<2, 4> : kern<3, 4>;
+    const int F = 4;
     hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
     float best = 1e30f;
     for (int rep = 0; rep < 4; rep++) {

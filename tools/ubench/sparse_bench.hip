@@ -690,357 +690,553 @@
   asm volatile(  \
       "s_mov_b32 s88, 0\n"  \
       "s_mov_b64 s[90:91], %[bp]\n"  \
-      "global_load_dword v26, %[lane4], s[90:91]\n"  \
-      "global_load_dword v27, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v56, %[lane4], s[90:91]\n"  \
+      "global_load_dword v57, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v58, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v59, %[lane4], s[90:91] offset:768\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_mov_b64 s[36:37], %[eb]\n"  \
       "s_mov_b32 s34, 0\n"  \
       "s_load_dwordx16 s[40:55], s[36:37], s34\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v32, s40, %[lane16]\n"  \
-      "v_add_u32 v34, s42, %[lane16]\n"  \
-      "v_add_u32 v36, s44, %[lane16]\n"  \
-      "v_add_u32 v38, s46, %[lane16]\n"  \
-      "v_add_u32 v40, s48, %[lane16]\n"  \
-      "v_add_u32 v42, s50, %[lane16]\n"  \
-      "v_add_u32 v44, s52, %[lane16]\n"  \
-      "v_add_u32 v46, s54, %[lane16]\n"  \
-      "ds_read_b64 v[32:33], v32\n"  \
-      "ds_read_b64 v[34:35], v34\n"  \
-      "ds_read_b64 v[36:37], v36\n"  \
-      "ds_read_b64 v[38:39], v38\n"  \
-      "ds_read_b64 v[40:41], v40\n"  \
-      "ds_read_b64 v[42:43], v42\n"  \
-      "ds_read_b64 v[44:45], v44\n"  \
-      "ds_read_b64 v[46:47], v46\n"  \
+      "v_add_u32 v64, s40, %[lane16]\n"  \
+      "v_add_u32 v68, s42, %[lane16]\n"  \
+      "v_add_u32 v72, s44, %[lane16]\n"  \
+      "v_add_u32 v76, s46, %[lane16]\n"  \
+      "v_add_u32 v80, s48, %[lane16]\n"  \
+      "v_add_u32 v84, s50, %[lane16]\n"  \
+      "v_add_u32 v88, s52, %[lane16]\n"  \
+      "v_add_u32 v92, s54, %[lane16]\n"  \
+      "ds_read_b128 v[64:67], v64\n"  \
+      "ds_read_b128 v[68:71], v68\n"  \
+      "ds_read_b128 v[72:75], v72\n"  \
+      "ds_read_b128 v[76:79], v76\n"  \
+      "ds_read_b128 v[80:83], v80\n"  \
+      "ds_read_b128 v[84:87], v84\n"  \
+      "ds_read_b128 v[88:91], v88\n"  \
+      "ds_read_b128 v[92:95], v92\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[56:71], s[36:37], s34\n"  \
-      "s_waitcnt vmcnt(2)\n"  \
+      "s_waitcnt vmcnt(4)\n"  \
       "7:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v48, s56, %[lane16]\n"  \
-      "v_add_u32 v50, s58, %[lane16]\n"  \
-      "v_add_u32 v52, s60, %[lane16]\n"  \
-      "v_add_u32 v54, s62, %[lane16]\n"  \
-      "v_add_u32 v56, s64, %[lane16]\n"  \
-      "v_add_u32 v58, s66, %[lane16]\n"  \
-      "v_add_u32 v60, s68, %[lane16]\n"  \
-      "v_add_u32 v62, s70, %[lane16]\n"  \
-      "ds_read_b64 v[48:49], v48\n"  \
-      "ds_read_b64 v[50:51], v50\n"  \
-      "ds_read_b64 v[52:53], v52\n"  \
-      "ds_read_b64 v[54:55], v54\n"  \
-      "ds_read_b64 v[56:57], v56\n"  \
-      "ds_read_b64 v[58:59], v58\n"  \
-      "ds_read_b64 v[60:61], v60\n"  \
-      "ds_read_b64 v[62:63], v62\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[72:87], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v32, v26\n"  \
-      "v_sub_f32 v23, v33, v27\n"  \
-      "v_fma_f32 %[acc0], s41, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s41, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v34, v26\n"  \
-      "v_sub_f32 v25, v35, v27\n"  \
-      "v_fma_f32 %[acc1], s43, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s43, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v36, v26\n"  \
-      "v_sub_f32 v23, v37, v27\n"  \
-      "v_fma_f32 %[acc0], s45, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s45, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v38, v26\n"  \
-      "v_sub_f32 v25, v39, v27\n"  \
-      "v_fma_f32 %[acc1], s47, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s47, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v40, v26\n"  \
-      "v_sub_f32 v23, v41, v27\n"  \
-      "v_fma_f32 %[acc0], s49, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s49, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v42, v26\n"  \
-      "v_sub_f32 v25, v43, v27\n"  \
-      "v_fma_f32 %[acc1], s51, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s51, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v44, v26\n"  \
-      "v_sub_f32 v23, v45, v27\n"  \
-      "v_fma_f32 %[acc0], s53, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s53, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v46, v26\n"  \
-      "v_sub_f32 v25, v47, v27\n"  \
-      "v_fma_f32 %[acc1], s55, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s55, |v25|, %[acc3]\n"  \
+      "v_add_u32 v96, s56, %[lane16]\n"  \
+      "ds_read_b128 v[96:99], v96\n"  \
+      "v_add_u32 v100, s58, %[lane16]\n"  \
+      "ds_read_b128 v[100:103], v100\n"  \
+      "v_sub_f32 v48, v64, v56\n"  \
+      "v_sub_f32 v49, v65, v57\n"  \
+      "v_sub_f32 v50, v66, v58\n"  \
+      "v_sub_f32 v51, v67, v59\n"  \
+      "v_fma_f32 %[acc0], s41, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s41, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s41, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s41, |v51|, %[acc6]\n"  \
+      "v_add_u32 v104, s60, %[lane16]\n"  \
+      "ds_read_b128 v[104:107], v104\n"  \
+      "v_sub_f32 v52, v68, v56\n"  \
+      "v_sub_f32 v53, v69, v57\n"  \
+      "v_sub_f32 v54, v70, v58\n"  \
+      "v_sub_f32 v55, v71, v59\n"  \
+      "v_fma_f32 %[acc1], s43, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s43, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s43, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s43, |v55|, %[acc7]\n"  \
+      "v_add_u32 v108, s62, %[lane16]\n"  \
+      "ds_read_b128 v[108:111], v108\n"  \
+      "v_sub_f32 v48, v72, v56\n"  \
+      "v_sub_f32 v49, v73, v57\n"  \
+      "v_sub_f32 v50, v74, v58\n"  \
+      "v_sub_f32 v51, v75, v59\n"  \
+      "v_fma_f32 %[acc0], s45, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s45, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s45, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s45, |v51|, %[acc6]\n"  \
+      "v_add_u32 v112, s64, %[lane16]\n"  \
+      "ds_read_b128 v[112:115], v112\n"  \
+      "v_sub_f32 v52, v76, v56\n"  \
+      "v_sub_f32 v53, v77, v57\n"  \
+      "v_sub_f32 v54, v78, v58\n"  \
+      "v_sub_f32 v55, v79, v59\n"  \
+      "v_fma_f32 %[acc1], s47, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s47, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s47, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s47, |v55|, %[acc7]\n"  \
+      "v_add_u32 v116, s66, %[lane16]\n"  \
+      "ds_read_b128 v[116:119], v116\n"  \
+      "v_sub_f32 v48, v80, v56\n"  \
+      "v_sub_f32 v49, v81, v57\n"  \
+      "v_sub_f32 v50, v82, v58\n"  \
+      "v_sub_f32 v51, v83, v59\n"  \
+      "v_fma_f32 %[acc0], s49, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s49, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s49, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s49, |v51|, %[acc6]\n"  \
+      "v_add_u32 v120, s68, %[lane16]\n"  \
+      "ds_read_b128 v[120:123], v120\n"  \
+      "v_sub_f32 v52, v84, v56\n"  \
+      "v_sub_f32 v53, v85, v57\n"  \
+      "v_sub_f32 v54, v86, v58\n"  \
+      "v_sub_f32 v55, v87, v59\n"  \
+      "v_fma_f32 %[acc1], s51, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s51, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s51, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s51, |v55|, %[acc7]\n"  \
+      "v_add_u32 v124, s70, %[lane16]\n"  \
+      "ds_read_b128 v[124:127], v124\n"  \
+      "v_sub_f32 v48, v88, v56\n"  \
+      "v_sub_f32 v49, v89, v57\n"  \
+      "v_sub_f32 v50, v90, v58\n"  \
+      "v_sub_f32 v51, v91, v59\n"  \
+      "v_fma_f32 %[acc0], s53, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s53, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s53, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s53, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v92, v56\n"  \
+      "v_sub_f32 v53, v93, v57\n"  \
+      "v_sub_f32 v54, v94, v58\n"  \
+      "v_sub_f32 v55, v95, v59\n"  \
+      "v_fma_f32 %[acc1], s55, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s55, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s55, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s55, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s41, 0\n"  \
       "s_cbranch_scc1 10f\n"  \
       "20:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v32, s72, %[lane16]\n"  \
-      "v_add_u32 v34, s74, %[lane16]\n"  \
-      "v_add_u32 v36, s76, %[lane16]\n"  \
-      "v_add_u32 v38, s78, %[lane16]\n"  \
-      "v_add_u32 v40, s80, %[lane16]\n"  \
-      "v_add_u32 v42, s82, %[lane16]\n"  \
-      "v_add_u32 v44, s84, %[lane16]\n"  \
-      "v_add_u32 v46, s86, %[lane16]\n"  \
-      "ds_read_b64 v[32:33], v32\n"  \
-      "ds_read_b64 v[34:35], v34\n"  \
-      "ds_read_b64 v[36:37], v36\n"  \
-      "ds_read_b64 v[38:39], v38\n"  \
-      "ds_read_b64 v[40:41], v40\n"  \
-      "ds_read_b64 v[42:43], v42\n"  \
-      "ds_read_b64 v[44:45], v44\n"  \
-      "ds_read_b64 v[46:47], v46\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[40:55], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v48, v26\n"  \
-      "v_sub_f32 v23, v49, v27\n"  \
-      "v_fma_f32 %[acc0], s57, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s57, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v50, v26\n"  \
-      "v_sub_f32 v25, v51, v27\n"  \
-      "v_fma_f32 %[acc1], s59, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s59, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v52, v26\n"  \
-      "v_sub_f32 v23, v53, v27\n"  \
-      "v_fma_f32 %[acc0], s61, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s61, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v54, v26\n"  \
-      "v_sub_f32 v25, v55, v27\n"  \
-      "v_fma_f32 %[acc1], s63, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s63, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v56, v26\n"  \
-      "v_sub_f32 v23, v57, v27\n"  \
-      "v_fma_f32 %[acc0], s65, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s65, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v58, v26\n"  \
-      "v_sub_f32 v25, v59, v27\n"  \
-      "v_fma_f32 %[acc1], s67, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s67, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v60, v26\n"  \
-      "v_sub_f32 v23, v61, v27\n"  \
-      "v_fma_f32 %[acc0], s69, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s69, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v62, v26\n"  \
-      "v_sub_f32 v25, v63, v27\n"  \
-      "v_fma_f32 %[acc1], s71, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s71, |v25|, %[acc3]\n"  \
+      "v_add_u32 v64, s72, %[lane16]\n"  \
+      "ds_read_b128 v[64:67], v64\n"  \
+      "v_add_u32 v68, s74, %[lane16]\n"  \
+      "ds_read_b128 v[68:71], v68\n"  \
+      "v_sub_f32 v48, v96, v56\n"  \
+      "v_sub_f32 v49, v97, v57\n"  \
+      "v_sub_f32 v50, v98, v58\n"  \
+      "v_sub_f32 v51, v99, v59\n"  \
+      "v_fma_f32 %[acc0], s57, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s57, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s57, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s57, |v51|, %[acc6]\n"  \
+      "v_add_u32 v72, s76, %[lane16]\n"  \
+      "ds_read_b128 v[72:75], v72\n"  \
+      "v_sub_f32 v52, v100, v56\n"  \
+      "v_sub_f32 v53, v101, v57\n"  \
+      "v_sub_f32 v54, v102, v58\n"  \
+      "v_sub_f32 v55, v103, v59\n"  \
+      "v_fma_f32 %[acc1], s59, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s59, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s59, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s59, |v55|, %[acc7]\n"  \
+      "v_add_u32 v76, s78, %[lane16]\n"  \
+      "ds_read_b128 v[76:79], v76\n"  \
+      "v_sub_f32 v48, v104, v56\n"  \
+      "v_sub_f32 v49, v105, v57\n"  \
+      "v_sub_f32 v50, v106, v58\n"  \
+      "v_sub_f32 v51, v107, v59\n"  \
+      "v_fma_f32 %[acc0], s61, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s61, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s61, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s61, |v51|, %[acc6]\n"  \
+      "v_add_u32 v80, s80, %[lane16]\n"  \
+      "ds_read_b128 v[80:83], v80\n"  \
+      "v_sub_f32 v52, v108, v56\n"  \
+      "v_sub_f32 v53, v109, v57\n"  \
+      "v_sub_f32 v54, v110, v58\n"  \
+      "v_sub_f32 v55, v111, v59\n"  \
+      "v_fma_f32 %[acc1], s63, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s63, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s63, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s63, |v55|, %[acc7]\n"  \
+      "v_add_u32 v84, s82, %[lane16]\n"  \
+      "ds_read_b128 v[84:87], v84\n"  \
+      "v_sub_f32 v48, v112, v56\n"  \
+      "v_sub_f32 v49, v113, v57\n"  \
+      "v_sub_f32 v50, v114, v58\n"  \
+      "v_sub_f32 v51, v115, v59\n"  \
+      "v_fma_f32 %[acc0], s65, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s65, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s65, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s65, |v51|, %[acc6]\n"  \
+      "v_add_u32 v88, s84, %[lane16]\n"  \
+      "ds_read_b128 v[88:91], v88\n"  \
+      "v_sub_f32 v52, v116, v56\n"  \
+      "v_sub_f32 v53, v117, v57\n"  \
+      "v_sub_f32 v54, v118, v58\n"  \
+      "v_sub_f32 v55, v119, v59\n"  \
+      "v_fma_f32 %[acc1], s67, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s67, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s67, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s67, |v55|, %[acc7]\n"  \
+      "v_add_u32 v92, s86, %[lane16]\n"  \
+      "ds_read_b128 v[92:95], v92\n"  \
+      "v_sub_f32 v48, v120, v56\n"  \
+      "v_sub_f32 v49, v121, v57\n"  \
+      "v_sub_f32 v50, v122, v58\n"  \
+      "v_sub_f32 v51, v123, v59\n"  \
+      "v_fma_f32 %[acc0], s69, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s69, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s69, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s69, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v124, v56\n"  \
+      "v_sub_f32 v53, v125, v57\n"  \
+      "v_sub_f32 v54, v126, v58\n"  \
+      "v_sub_f32 v55, v127, v59\n"  \
+      "v_fma_f32 %[acc1], s71, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s71, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s71, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s71, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s57, 0\n"  \
       "s_cbranch_scc1 11f\n"  \
       "21:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v48, s40, %[lane16]\n"  \
-      "v_add_u32 v50, s42, %[lane16]\n"  \
-      "v_add_u32 v52, s44, %[lane16]\n"  \
-      "v_add_u32 v54, s46, %[lane16]\n"  \
-      "v_add_u32 v56, s48, %[lane16]\n"  \
-      "v_add_u32 v58, s50, %[lane16]\n"  \
-      "v_add_u32 v60, s52, %[lane16]\n"  \
-      "v_add_u32 v62, s54, %[lane16]\n"  \
-      "ds_read_b64 v[48:49], v48\n"  \
-      "ds_read_b64 v[50:51], v50\n"  \
-      "ds_read_b64 v[52:53], v52\n"  \
-      "ds_read_b64 v[54:55], v54\n"  \
-      "ds_read_b64 v[56:57], v56\n"  \
-      "ds_read_b64 v[58:59], v58\n"  \
-      "ds_read_b64 v[60:61], v60\n"  \
-      "ds_read_b64 v[62:63], v62\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[56:71], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v32, v26\n"  \
-      "v_sub_f32 v23, v33, v27\n"  \
-      "v_fma_f32 %[acc0], s73, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s73, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v34, v26\n"  \
-      "v_sub_f32 v25, v35, v27\n"  \
-      "v_fma_f32 %[acc1], s75, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s75, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v36, v26\n"  \
-      "v_sub_f32 v23, v37, v27\n"  \
-      "v_fma_f32 %[acc0], s77, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s77, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v38, v26\n"  \
-      "v_sub_f32 v25, v39, v27\n"  \
-      "v_fma_f32 %[acc1], s79, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s79, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v40, v26\n"  \
-      "v_sub_f32 v23, v41, v27\n"  \
-      "v_fma_f32 %[acc0], s81, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s81, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v42, v26\n"  \
-      "v_sub_f32 v25, v43, v27\n"  \
-      "v_fma_f32 %[acc1], s83, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s83, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v44, v26\n"  \
-      "v_sub_f32 v23, v45, v27\n"  \
-      "v_fma_f32 %[acc0], s85, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s85, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v46, v26\n"  \
-      "v_sub_f32 v25, v47, v27\n"  \
-      "v_fma_f32 %[acc1], s87, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s87, |v25|, %[acc3]\n"  \
+      "v_add_u32 v96, s40, %[lane16]\n"  \
+      "ds_read_b128 v[96:99], v96\n"  \
+      "v_add_u32 v100, s42, %[lane16]\n"  \
+      "ds_read_b128 v[100:103], v100\n"  \
+      "v_sub_f32 v48, v64, v56\n"  \
+      "v_sub_f32 v49, v65, v57\n"  \
+      "v_sub_f32 v50, v66, v58\n"  \
+      "v_sub_f32 v51, v67, v59\n"  \
+      "v_fma_f32 %[acc0], s73, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s73, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s73, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s73, |v51|, %[acc6]\n"  \
+      "v_add_u32 v104, s44, %[lane16]\n"  \
+      "ds_read_b128 v[104:107], v104\n"  \
+      "v_sub_f32 v52, v68, v56\n"  \
+      "v_sub_f32 v53, v69, v57\n"  \
+      "v_sub_f32 v54, v70, v58\n"  \
+      "v_sub_f32 v55, v71, v59\n"  \
+      "v_fma_f32 %[acc1], s75, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s75, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s75, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s75, |v55|, %[acc7]\n"  \
+      "v_add_u32 v108, s46, %[lane16]\n"  \
+      "ds_read_b128 v[108:111], v108\n"  \
+      "v_sub_f32 v48, v72, v56\n"  \
+      "v_sub_f32 v49, v73, v57\n"  \
+      "v_sub_f32 v50, v74, v58\n"  \
+      "v_sub_f32 v51, v75, v59\n"  \
+      "v_fma_f32 %[acc0], s77, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s77, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s77, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s77, |v51|, %[acc6]\n"  \
+      "v_add_u32 v112, s48, %[lane16]\n"  \
+      "ds_read_b128 v[112:115], v112\n"  \
+      "v_sub_f32 v52, v76, v56\n"  \
+      "v_sub_f32 v53, v77, v57\n"  \
+      "v_sub_f32 v54, v78, v58\n"  \
+      "v_sub_f32 v55, v79, v59\n"  \
+      "v_fma_f32 %[acc1], s79, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s79, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s79, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s79, |v55|, %[acc7]\n"  \
+      "v_add_u32 v116, s50, %[lane16]\n"  \
+      "ds_read_b128 v[116:119], v116\n"  \
+      "v_sub_f32 v48, v80, v56\n"  \
+      "v_sub_f32 v49, v81, v57\n"  \
+      "v_sub_f32 v50, v82, v58\n"  \
+      "v_sub_f32 v51, v83, v59\n"  \
+      "v_fma_f32 %[acc0], s81, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s81, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s81, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s81, |v51|, %[acc6]\n"  \
+      "v_add_u32 v120, s52, %[lane16]\n"  \
+      "ds_read_b128 v[120:123], v120\n"  \
+      "v_sub_f32 v52, v84, v56\n"  \
+      "v_sub_f32 v53, v85, v57\n"  \
+      "v_sub_f32 v54, v86, v58\n"  \
+      "v_sub_f32 v55, v87, v59\n"  \
+      "v_fma_f32 %[acc1], s83, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s83, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s83, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s83, |v55|, %[acc7]\n"  \
+      "v_add_u32 v124, s54, %[lane16]\n"  \
+      "ds_read_b128 v[124:127], v124\n"  \
+      "v_sub_f32 v48, v88, v56\n"  \
+      "v_sub_f32 v49, v89, v57\n"  \
+      "v_sub_f32 v50, v90, v58\n"  \
+      "v_sub_f32 v51, v91, v59\n"  \
+      "v_fma_f32 %[acc0], s85, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s85, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s85, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s85, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v92, v56\n"  \
+      "v_sub_f32 v53, v93, v57\n"  \
+      "v_sub_f32 v54, v94, v58\n"  \
+      "v_sub_f32 v55, v95, v59\n"  \
+      "v_fma_f32 %[acc1], s87, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s87, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s87, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s87, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s73, 0\n"  \
       "s_cbranch_scc1 12f\n"  \
       "22:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v32, s56, %[lane16]\n"  \
-      "v_add_u32 v34, s58, %[lane16]\n"  \
-      "v_add_u32 v36, s60, %[lane16]\n"  \
-      "v_add_u32 v38, s62, %[lane16]\n"  \
-      "v_add_u32 v40, s64, %[lane16]\n"  \
-      "v_add_u32 v42, s66, %[lane16]\n"  \
-      "v_add_u32 v44, s68, %[lane16]\n"  \
-      "v_add_u32 v46, s70, %[lane16]\n"  \
-      "ds_read_b64 v[32:33], v32\n"  \
-      "ds_read_b64 v[34:35], v34\n"  \
-      "ds_read_b64 v[36:37], v36\n"  \
-      "ds_read_b64 v[38:39], v38\n"  \
-      "ds_read_b64 v[40:41], v40\n"  \
-      "ds_read_b64 v[42:43], v42\n"  \
-      "ds_read_b64 v[44:45], v44\n"  \
-      "ds_read_b64 v[46:47], v46\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[72:87], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v48, v26\n"  \
-      "v_sub_f32 v23, v49, v27\n"  \
-      "v_fma_f32 %[acc0], s41, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s41, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v50, v26\n"  \
-      "v_sub_f32 v25, v51, v27\n"  \
-      "v_fma_f32 %[acc1], s43, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s43, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v52, v26\n"  \
-      "v_sub_f32 v23, v53, v27\n"  \
-      "v_fma_f32 %[acc0], s45, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s45, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v54, v26\n"  \
-      "v_sub_f32 v25, v55, v27\n"  \
-      "v_fma_f32 %[acc1], s47, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s47, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v56, v26\n"  \
-      "v_sub_f32 v23, v57, v27\n"  \
-      "v_fma_f32 %[acc0], s49, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s49, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v58, v26\n"  \
-      "v_sub_f32 v25, v59, v27\n"  \
-      "v_fma_f32 %[acc1], s51, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s51, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v60, v26\n"  \
-      "v_sub_f32 v23, v61, v27\n"  \
-      "v_fma_f32 %[acc0], s53, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s53, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v62, v26\n"  \
-      "v_sub_f32 v25, v63, v27\n"  \
-      "v_fma_f32 %[acc1], s55, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s55, |v25|, %[acc3]\n"  \
+      "v_add_u32 v64, s56, %[lane16]\n"  \
+      "ds_read_b128 v[64:67], v64\n"  \
+      "v_add_u32 v68, s58, %[lane16]\n"  \
+      "ds_read_b128 v[68:71], v68\n"  \
+      "v_sub_f32 v48, v96, v56\n"  \
+      "v_sub_f32 v49, v97, v57\n"  \
+      "v_sub_f32 v50, v98, v58\n"  \
+      "v_sub_f32 v51, v99, v59\n"  \
+      "v_fma_f32 %[acc0], s41, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s41, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s41, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s41, |v51|, %[acc6]\n"  \
+      "v_add_u32 v72, s60, %[lane16]\n"  \
+      "ds_read_b128 v[72:75], v72\n"  \
+      "v_sub_f32 v52, v100, v56\n"  \
+      "v_sub_f32 v53, v101, v57\n"  \
+      "v_sub_f32 v54, v102, v58\n"  \
+      "v_sub_f32 v55, v103, v59\n"  \
+      "v_fma_f32 %[acc1], s43, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s43, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s43, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s43, |v55|, %[acc7]\n"  \
+      "v_add_u32 v76, s62, %[lane16]\n"  \
+      "ds_read_b128 v[76:79], v76\n"  \
+      "v_sub_f32 v48, v104, v56\n"  \
+      "v_sub_f32 v49, v105, v57\n"  \
+      "v_sub_f32 v50, v106, v58\n"  \
+      "v_sub_f32 v51, v107, v59\n"  \
+      "v_fma_f32 %[acc0], s45, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s45, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s45, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s45, |v51|, %[acc6]\n"  \
+      "v_add_u32 v80, s64, %[lane16]\n"  \
+      "ds_read_b128 v[80:83], v80\n"  \
+      "v_sub_f32 v52, v108, v56\n"  \
+      "v_sub_f32 v53, v109, v57\n"  \
+      "v_sub_f32 v54, v110, v58\n"  \
+      "v_sub_f32 v55, v111, v59\n"  \
+      "v_fma_f32 %[acc1], s47, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s47, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s47, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s47, |v55|, %[acc7]\n"  \
+      "v_add_u32 v84, s66, %[lane16]\n"  \
+      "ds_read_b128 v[84:87], v84\n"  \
+      "v_sub_f32 v48, v112, v56\n"  \
+      "v_sub_f32 v49, v113, v57\n"  \
+      "v_sub_f32 v50, v114, v58\n"  \
+      "v_sub_f32 v51, v115, v59\n"  \
+      "v_fma_f32 %[acc0], s49, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s49, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s49, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s49, |v51|, %[acc6]\n"  \
+      "v_add_u32 v88, s68, %[lane16]\n"  \
+      "ds_read_b128 v[88:91], v88\n"  \
+      "v_sub_f32 v52, v116, v56\n"  \
+      "v_sub_f32 v53, v117, v57\n"  \
+      "v_sub_f32 v54, v118, v58\n"  \
+      "v_sub_f32 v55, v119, v59\n"  \
+      "v_fma_f32 %[acc1], s51, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s51, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s51, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s51, |v55|, %[acc7]\n"  \
+      "v_add_u32 v92, s70, %[lane16]\n"  \
+      "ds_read_b128 v[92:95], v92\n"  \
+      "v_sub_f32 v48, v120, v56\n"  \
+      "v_sub_f32 v49, v121, v57\n"  \
+      "v_sub_f32 v50, v122, v58\n"  \
+      "v_sub_f32 v51, v123, v59\n"  \
+      "v_fma_f32 %[acc0], s53, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s53, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s53, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s53, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v124, v56\n"  \
+      "v_sub_f32 v53, v125, v57\n"  \
+      "v_sub_f32 v54, v126, v58\n"  \
+      "v_sub_f32 v55, v127, v59\n"  \
+      "v_fma_f32 %[acc1], s55, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s55, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s55, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s55, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s41, 0\n"  \
       "s_cbranch_scc1 13f\n"  \
       "23:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v48, s72, %[lane16]\n"  \
-      "v_add_u32 v50, s74, %[lane16]\n"  \
-      "v_add_u32 v52, s76, %[lane16]\n"  \
-      "v_add_u32 v54, s78, %[lane16]\n"  \
-      "v_add_u32 v56, s80, %[lane16]\n"  \
-      "v_add_u32 v58, s82, %[lane16]\n"  \
-      "v_add_u32 v60, s84, %[lane16]\n"  \
-      "v_add_u32 v62, s86, %[lane16]\n"  \
-      "ds_read_b64 v[48:49], v48\n"  \
-      "ds_read_b64 v[50:51], v50\n"  \
-      "ds_read_b64 v[52:53], v52\n"  \
-      "ds_read_b64 v[54:55], v54\n"  \
-      "ds_read_b64 v[56:57], v56\n"  \
-      "ds_read_b64 v[58:59], v58\n"  \
-      "ds_read_b64 v[60:61], v60\n"  \
-      "ds_read_b64 v[62:63], v62\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[40:55], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v32, v26\n"  \
-      "v_sub_f32 v23, v33, v27\n"  \
-      "v_fma_f32 %[acc0], s57, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s57, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v34, v26\n"  \
-      "v_sub_f32 v25, v35, v27\n"  \
-      "v_fma_f32 %[acc1], s59, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s59, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v36, v26\n"  \
-      "v_sub_f32 v23, v37, v27\n"  \
-      "v_fma_f32 %[acc0], s61, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s61, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v38, v26\n"  \
-      "v_sub_f32 v25, v39, v27\n"  \
-      "v_fma_f32 %[acc1], s63, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s63, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v40, v26\n"  \
-      "v_sub_f32 v23, v41, v27\n"  \
-      "v_fma_f32 %[acc0], s65, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s65, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v42, v26\n"  \
-      "v_sub_f32 v25, v43, v27\n"  \
-      "v_fma_f32 %[acc1], s67, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s67, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v44, v26\n"  \
-      "v_sub_f32 v23, v45, v27\n"  \
-      "v_fma_f32 %[acc0], s69, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s69, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v46, v26\n"  \
-      "v_sub_f32 v25, v47, v27\n"  \
-      "v_fma_f32 %[acc1], s71, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s71, |v25|, %[acc3]\n"  \
+      "v_add_u32 v96, s72, %[lane16]\n"  \
+      "ds_read_b128 v[96:99], v96\n"  \
+      "v_add_u32 v100, s74, %[lane16]\n"  \
+      "ds_read_b128 v[100:103], v100\n"  \
+      "v_sub_f32 v48, v64, v56\n"  \
+      "v_sub_f32 v49, v65, v57\n"  \
+      "v_sub_f32 v50, v66, v58\n"  \
+      "v_sub_f32 v51, v67, v59\n"  \
+      "v_fma_f32 %[acc0], s57, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s57, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s57, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s57, |v51|, %[acc6]\n"  \
+      "v_add_u32 v104, s76, %[lane16]\n"  \
+      "ds_read_b128 v[104:107], v104\n"  \
+      "v_sub_f32 v52, v68, v56\n"  \
+      "v_sub_f32 v53, v69, v57\n"  \
+      "v_sub_f32 v54, v70, v58\n"  \
+      "v_sub_f32 v55, v71, v59\n"  \
+      "v_fma_f32 %[acc1], s59, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s59, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s59, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s59, |v55|, %[acc7]\n"  \
+      "v_add_u32 v108, s78, %[lane16]\n"  \
+      "ds_read_b128 v[108:111], v108\n"  \
+      "v_sub_f32 v48, v72, v56\n"  \
+      "v_sub_f32 v49, v73, v57\n"  \
+      "v_sub_f32 v50, v74, v58\n"  \
+      "v_sub_f32 v51, v75, v59\n"  \
+      "v_fma_f32 %[acc0], s61, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s61, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s61, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s61, |v51|, %[acc6]\n"  \
+      "v_add_u32 v112, s80, %[lane16]\n"  \
+      "ds_read_b128 v[112:115], v112\n"  \
+      "v_sub_f32 v52, v76, v56\n"  \
+      "v_sub_f32 v53, v77, v57\n"  \
+      "v_sub_f32 v54, v78, v58\n"  \
+      "v_sub_f32 v55, v79, v59\n"  \
+      "v_fma_f32 %[acc1], s63, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s63, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s63, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s63, |v55|, %[acc7]\n"  \
+      "v_add_u32 v116, s82, %[lane16]\n"  \
+      "ds_read_b128 v[116:119], v116\n"  \
+      "v_sub_f32 v48, v80, v56\n"  \
+      "v_sub_f32 v49, v81, v57\n"  \
+      "v_sub_f32 v50, v82, v58\n"  \
+      "v_sub_f32 v51, v83, v59\n"  \
+      "v_fma_f32 %[acc0], s65, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s65, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s65, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s65, |v51|, %[acc6]\n"  \
+      "v_add_u32 v120, s84, %[lane16]\n"  \
+      "ds_read_b128 v[120:123], v120\n"  \
+      "v_sub_f32 v52, v84, v56\n"  \
+      "v_sub_f32 v53, v85, v57\n"  \
+      "v_sub_f32 v54, v86, v58\n"  \
+      "v_sub_f32 v55, v87, v59\n"  \
+      "v_fma_f32 %[acc1], s67, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s67, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s67, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s67, |v55|, %[acc7]\n"  \
+      "v_add_u32 v124, s86, %[lane16]\n"  \
+      "ds_read_b128 v[124:127], v124\n"  \
+      "v_sub_f32 v48, v88, v56\n"  \
+      "v_sub_f32 v49, v89, v57\n"  \
+      "v_sub_f32 v50, v90, v58\n"  \
+      "v_sub_f32 v51, v91, v59\n"  \
+      "v_fma_f32 %[acc0], s69, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s69, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s69, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s69, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v92, v56\n"  \
+      "v_sub_f32 v53, v93, v57\n"  \
+      "v_sub_f32 v54, v94, v58\n"  \
+      "v_sub_f32 v55, v95, v59\n"  \
+      "v_fma_f32 %[acc1], s71, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s71, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s71, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s71, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s57, 0\n"  \
       "s_cbranch_scc1 14f\n"  \
       "24:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v32, s40, %[lane16]\n"  \
-      "v_add_u32 v34, s42, %[lane16]\n"  \
-      "v_add_u32 v36, s44, %[lane16]\n"  \
-      "v_add_u32 v38, s46, %[lane16]\n"  \
-      "v_add_u32 v40, s48, %[lane16]\n"  \
-      "v_add_u32 v42, s50, %[lane16]\n"  \
-      "v_add_u32 v44, s52, %[lane16]\n"  \
-      "v_add_u32 v46, s54, %[lane16]\n"  \
-      "ds_read_b64 v[32:33], v32\n"  \
-      "ds_read_b64 v[34:35], v34\n"  \
-      "ds_read_b64 v[36:37], v36\n"  \
-      "ds_read_b64 v[38:39], v38\n"  \
-      "ds_read_b64 v[40:41], v40\n"  \
-      "ds_read_b64 v[42:43], v42\n"  \
-      "ds_read_b64 v[44:45], v44\n"  \
-      "ds_read_b64 v[46:47], v46\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[56:71], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v48, v26\n"  \
-      "v_sub_f32 v23, v49, v27\n"  \
-      "v_fma_f32 %[acc0], s73, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s73, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v50, v26\n"  \
-      "v_sub_f32 v25, v51, v27\n"  \
-      "v_fma_f32 %[acc1], s75, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s75, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v52, v26\n"  \
-      "v_sub_f32 v23, v53, v27\n"  \
-      "v_fma_f32 %[acc0], s77, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s77, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v54, v26\n"  \
-      "v_sub_f32 v25, v55, v27\n"  \
-      "v_fma_f32 %[acc1], s79, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s79, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v56, v26\n"  \
-      "v_sub_f32 v23, v57, v27\n"  \
-      "v_fma_f32 %[acc0], s81, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s81, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v58, v26\n"  \
-      "v_sub_f32 v25, v59, v27\n"  \
-      "v_fma_f32 %[acc1], s83, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s83, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v60, v26\n"  \
-      "v_sub_f32 v23, v61, v27\n"  \
-      "v_fma_f32 %[acc0], s85, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s85, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v62, v26\n"  \
-      "v_sub_f32 v25, v63, v27\n"  \
-      "v_fma_f32 %[acc1], s87, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s87, |v25|, %[acc3]\n"  \
+      "v_add_u32 v64, s40, %[lane16]\n"  \
+      "ds_read_b128 v[64:67], v64\n"  \
+      "v_add_u32 v68, s42, %[lane16]\n"  \
+      "ds_read_b128 v[68:71], v68\n"  \
+      "v_sub_f32 v48, v96, v56\n"  \
+      "v_sub_f32 v49, v97, v57\n"  \
+      "v_sub_f32 v50, v98, v58\n"  \
+      "v_sub_f32 v51, v99, v59\n"  \
+      "v_fma_f32 %[acc0], s73, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s73, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s73, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s73, |v51|, %[acc6]\n"  \
+      "v_add_u32 v72, s44, %[lane16]\n"  \
+      "ds_read_b128 v[72:75], v72\n"  \
+      "v_sub_f32 v52, v100, v56\n"  \
+      "v_sub_f32 v53, v101, v57\n"  \
+      "v_sub_f32 v54, v102, v58\n"  \
+      "v_sub_f32 v55, v103, v59\n"  \
+      "v_fma_f32 %[acc1], s75, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s75, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s75, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s75, |v55|, %[acc7]\n"  \
+      "v_add_u32 v76, s46, %[lane16]\n"  \
+      "ds_read_b128 v[76:79], v76\n"  \
+      "v_sub_f32 v48, v104, v56\n"  \
+      "v_sub_f32 v49, v105, v57\n"  \
+      "v_sub_f32 v50, v106, v58\n"  \
+      "v_sub_f32 v51, v107, v59\n"  \
+      "v_fma_f32 %[acc0], s77, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s77, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s77, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s77, |v51|, %[acc6]\n"  \
+      "v_add_u32 v80, s48, %[lane16]\n"  \
+      "ds_read_b128 v[80:83], v80\n"  \
+      "v_sub_f32 v52, v108, v56\n"  \
+      "v_sub_f32 v53, v109, v57\n"  \
+      "v_sub_f32 v54, v110, v58\n"  \
+      "v_sub_f32 v55, v111, v59\n"  \
+      "v_fma_f32 %[acc1], s79, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s79, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s79, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s79, |v55|, %[acc7]\n"  \
+      "v_add_u32 v84, s50, %[lane16]\n"  \
+      "ds_read_b128 v[84:87], v84\n"  \
+      "v_sub_f32 v48, v112, v56\n"  \
+      "v_sub_f32 v49, v113, v57\n"  \
+      "v_sub_f32 v50, v114, v58\n"  \
+      "v_sub_f32 v51, v115, v59\n"  \
+      "v_fma_f32 %[acc0], s81, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s81, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s81, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s81, |v51|, %[acc6]\n"  \
+      "v_add_u32 v88, s52, %[lane16]\n"  \
+      "ds_read_b128 v[88:91], v88\n"  \
+      "v_sub_f32 v52, v116, v56\n"  \
+      "v_sub_f32 v53, v117, v57\n"  \
+      "v_sub_f32 v54, v118, v58\n"  \
+      "v_sub_f32 v55, v119, v59\n"  \
+      "v_fma_f32 %[acc1], s83, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s83, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s83, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s83, |v55|, %[acc7]\n"  \
+      "v_add_u32 v92, s54, %[lane16]\n"  \
+      "ds_read_b128 v[92:95], v92\n"  \
+      "v_sub_f32 v48, v120, v56\n"  \
+      "v_sub_f32 v49, v121, v57\n"  \
+      "v_sub_f32 v50, v122, v58\n"  \
+      "v_sub_f32 v51, v123, v59\n"  \
+      "v_fma_f32 %[acc0], s85, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s85, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s85, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s85, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v124, v56\n"  \
+      "v_sub_f32 v53, v125, v57\n"  \
+      "v_sub_f32 v54, v126, v58\n"  \
+      "v_sub_f32 v55, v127, v59\n"  \
+      "v_fma_f32 %[acc1], s87, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s87, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s87, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s87, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s73, 0\n"  \
       "s_cbranch_scc1 15f\n"  \
       "25:\n"  \
@@ -1052,97 +1248,121 @@
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 20b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 20b\n"  \
       "11:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 21b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 21b\n"  \
       "12:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 22b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 22b\n"  \
       "13:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 23b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 23b\n"  \
       "14:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 24b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 24b\n"  \
       "15:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 25b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 25b\n"  \
       "8:\n"  \
       "s_waitcnt vmcnt(0) lgkmcnt(0)\n"  \
-      : [acc0] "+v"(acc[0]), [acc1] "+v"(acc[1]), [acc2] "+v"(acc[2]), [acc3] "+v"(acc[3])  \
+      : [acc0] "+v"(acc[0]), [acc1] "+v"(acc[1]), [acc2] "+v"(acc[2]), [acc3] "+v"(acc[3]), [acc4] "+v"(acc[4]), [acc5] "+v"(acc[5]), [acc6] "+v"(acc[6]), [acc7] "+v"(acc[7])  \
       : [lane16] "v"(lane16), [lane4] "v"(lane4), [eb] "s"(eb), [bp] "s"(bp),  \
         [bstride] "s"(bstride), [ncols] "s"(ncols)  \
-      : "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63",  \
+      : "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127",  \
         "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "scc", "memory")
 
 #define STREAM2(acc, lane16, lane4, eb, bp, bstride, ncols)  \
@@ -1150,369 +1370,565 @@
       "s_mov_b32 s89, 0\n"  \
       "s_mov_b32 s88, 0\n"  \
       "s_mov_b64 s[90:91], %[bp]\n"  \
-      "global_load_dword v26, %[lane4], s[90:91]\n"  \
-      "global_load_dword v27, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v56, %[lane4], s[90:91]\n"  \
+      "global_load_dword v57, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v58, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v59, %[lane4], s[90:91] offset:768\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_mov_b64 s[36:37], %[eb]\n"  \
       "s_mov_b32 s34, 0\n"  \
       "s_load_dwordx16 s[40:55], s[36:37], s34\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v32, s40, %[lane16]\n"  \
-      "v_add_u32 v34, s42, %[lane16]\n"  \
-      "v_add_u32 v36, s44, %[lane16]\n"  \
-      "v_add_u32 v38, s46, %[lane16]\n"  \
-      "v_add_u32 v40, s48, %[lane16]\n"  \
-      "v_add_u32 v42, s50, %[lane16]\n"  \
-      "v_add_u32 v44, s52, %[lane16]\n"  \
-      "v_add_u32 v46, s54, %[lane16]\n"  \
-      "ds_read_b64 v[32:33], v32\n"  \
-      "ds_read_b64 v[34:35], v34\n"  \
-      "ds_read_b64 v[36:37], v36\n"  \
-      "ds_read_b64 v[38:39], v38\n"  \
-      "ds_read_b64 v[40:41], v40\n"  \
-      "ds_read_b64 v[42:43], v42\n"  \
-      "ds_read_b64 v[44:45], v44\n"  \
-      "ds_read_b64 v[46:47], v46\n"  \
+      "v_add_u32 v64, s40, %[lane16]\n"  \
+      "v_add_u32 v68, s42, %[lane16]\n"  \
+      "v_add_u32 v72, s44, %[lane16]\n"  \
+      "v_add_u32 v76, s46, %[lane16]\n"  \
+      "v_add_u32 v80, s48, %[lane16]\n"  \
+      "v_add_u32 v84, s50, %[lane16]\n"  \
+      "v_add_u32 v88, s52, %[lane16]\n"  \
+      "v_add_u32 v92, s54, %[lane16]\n"  \
+      "ds_read_b128 v[64:67], v64\n"  \
+      "ds_read_b128 v[68:71], v68\n"  \
+      "ds_read_b128 v[72:75], v72\n"  \
+      "ds_read_b128 v[76:79], v76\n"  \
+      "ds_read_b128 v[80:83], v80\n"  \
+      "ds_read_b128 v[84:87], v84\n"  \
+      "ds_read_b128 v[88:91], v88\n"  \
+      "ds_read_b128 v[92:95], v92\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[56:71], s[36:37], s34\n"  \
-      "s_waitcnt vmcnt(2)\n"  \
+      "s_waitcnt vmcnt(4)\n"  \
       "7:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v48, s56, %[lane16]\n"  \
-      "v_add_u32 v50, s58, %[lane16]\n"  \
-      "v_add_u32 v52, s60, %[lane16]\n"  \
-      "v_add_u32 v54, s62, %[lane16]\n"  \
-      "v_add_u32 v56, s64, %[lane16]\n"  \
-      "v_add_u32 v58, s66, %[lane16]\n"  \
-      "v_add_u32 v60, s68, %[lane16]\n"  \
-      "v_add_u32 v62, s70, %[lane16]\n"  \
-      "ds_read_b64 v[48:49], v48\n"  \
-      "ds_read_b64 v[50:51], v50\n"  \
-      "ds_read_b64 v[52:53], v52\n"  \
-      "ds_read_b64 v[54:55], v54\n"  \
-      "ds_read_b64 v[56:57], v56\n"  \
-      "ds_read_b64 v[58:59], v58\n"  \
-      "ds_read_b64 v[60:61], v60\n"  \
-      "ds_read_b64 v[62:63], v62\n"  \
+      "v_add_u32 v96, s56, %[lane16]\n"  \
+      "v_add_u32 v100, s58, %[lane16]\n"  \
+      "v_add_u32 v104, s60, %[lane16]\n"  \
+      "v_add_u32 v108, s62, %[lane16]\n"  \
+      "v_add_u32 v112, s64, %[lane16]\n"  \
+      "v_add_u32 v116, s66, %[lane16]\n"  \
+      "v_add_u32 v120, s68, %[lane16]\n"  \
+      "v_add_u32 v124, s70, %[lane16]\n"  \
+      "ds_read_b128 v[96:99], v96\n"  \
+      "ds_read_b128 v[100:103], v100\n"  \
+      "ds_read_b128 v[104:107], v104\n"  \
+      "ds_read_b128 v[108:111], v108\n"  \
+      "ds_read_b128 v[112:115], v112\n"  \
+      "ds_read_b128 v[116:119], v116\n"  \
+      "ds_read_b128 v[120:123], v120\n"  \
+      "ds_read_b128 v[124:127], v124\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_and_b32 s34, s34, 0x40\n"  \
       "s_add_u32 s89, s89, 1\n"  \
       "s_load_dwordx16 s[72:87], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v32, v26\n"  \
-      "v_sub_f32 v23, v33, v27\n"  \
-      "v_fma_f32 %[acc0], s41, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s41, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v34, v26\n"  \
-      "v_sub_f32 v25, v35, v27\n"  \
-      "v_fma_f32 %[acc1], s43, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s43, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v36, v26\n"  \
-      "v_sub_f32 v23, v37, v27\n"  \
-      "v_fma_f32 %[acc0], s45, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s45, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v38, v26\n"  \
-      "v_sub_f32 v25, v39, v27\n"  \
-      "v_fma_f32 %[acc1], s47, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s47, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v40, v26\n"  \
-      "v_sub_f32 v23, v41, v27\n"  \
-      "v_fma_f32 %[acc0], s49, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s49, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v42, v26\n"  \
-      "v_sub_f32 v25, v43, v27\n"  \
-      "v_fma_f32 %[acc1], s51, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s51, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v44, v26\n"  \
-      "v_sub_f32 v23, v45, v27\n"  \
-      "v_fma_f32 %[acc0], s53, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s53, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v46, v26\n"  \
-      "v_sub_f32 v25, v47, v27\n"  \
-      "v_fma_f32 %[acc1], s55, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s55, |v25|, %[acc3]\n"  \
+      "v_sub_f32 v48, v64, v56\n"  \
+      "v_sub_f32 v49, v65, v57\n"  \
+      "v_sub_f32 v50, v66, v58\n"  \
+      "v_sub_f32 v51, v67, v59\n"  \
+      "v_fma_f32 %[acc0], s41, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s41, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s41, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s41, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v68, v56\n"  \
+      "v_sub_f32 v53, v69, v57\n"  \
+      "v_sub_f32 v54, v70, v58\n"  \
+      "v_sub_f32 v55, v71, v59\n"  \
+      "v_fma_f32 %[acc1], s43, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s43, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s43, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s43, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v72, v56\n"  \
+      "v_sub_f32 v49, v73, v57\n"  \
+      "v_sub_f32 v50, v74, v58\n"  \
+      "v_sub_f32 v51, v75, v59\n"  \
+      "v_fma_f32 %[acc0], s45, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s45, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s45, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s45, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v76, v56\n"  \
+      "v_sub_f32 v53, v77, v57\n"  \
+      "v_sub_f32 v54, v78, v58\n"  \
+      "v_sub_f32 v55, v79, v59\n"  \
+      "v_fma_f32 %[acc1], s47, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s47, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s47, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s47, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v80, v56\n"  \
+      "v_sub_f32 v49, v81, v57\n"  \
+      "v_sub_f32 v50, v82, v58\n"  \
+      "v_sub_f32 v51, v83, v59\n"  \
+      "v_fma_f32 %[acc0], s49, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s49, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s49, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s49, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v84, v56\n"  \
+      "v_sub_f32 v53, v85, v57\n"  \
+      "v_sub_f32 v54, v86, v58\n"  \
+      "v_sub_f32 v55, v87, v59\n"  \
+      "v_fma_f32 %[acc1], s51, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s51, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s51, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s51, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v88, v56\n"  \
+      "v_sub_f32 v49, v89, v57\n"  \
+      "v_sub_f32 v50, v90, v58\n"  \
+      "v_sub_f32 v51, v91, v59\n"  \
+      "v_fma_f32 %[acc0], s53, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s53, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s53, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s53, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v92, v56\n"  \
+      "v_sub_f32 v53, v93, v57\n"  \
+      "v_sub_f32 v54, v94, v58\n"  \
+      "v_sub_f32 v55, v95, v59\n"  \
+      "v_fma_f32 %[acc1], s55, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s55, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s55, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s55, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s41, 0\n"  \
       "s_cbranch_scc1 10f\n"  \
       "20:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v32, s72, %[lane16]\n"  \
-      "v_add_u32 v34, s74, %[lane16]\n"  \
-      "v_add_u32 v36, s76, %[lane16]\n"  \
-      "v_add_u32 v38, s78, %[lane16]\n"  \
-      "v_add_u32 v40, s80, %[lane16]\n"  \
-      "v_add_u32 v42, s82, %[lane16]\n"  \
-      "v_add_u32 v44, s84, %[lane16]\n"  \
-      "v_add_u32 v46, s86, %[lane16]\n"  \
-      "ds_read_b64 v[32:33], v32\n"  \
-      "ds_read_b64 v[34:35], v34\n"  \
-      "ds_read_b64 v[36:37], v36\n"  \
-      "ds_read_b64 v[38:39], v38\n"  \
-      "ds_read_b64 v[40:41], v40\n"  \
-      "ds_read_b64 v[42:43], v42\n"  \
-      "ds_read_b64 v[44:45], v44\n"  \
-      "ds_read_b64 v[46:47], v46\n"  \
+      "v_add_u32 v64, s72, %[lane16]\n"  \
+      "v_add_u32 v68, s74, %[lane16]\n"  \
+      "v_add_u32 v72, s76, %[lane16]\n"  \
+      "v_add_u32 v76, s78, %[lane16]\n"  \
+      "v_add_u32 v80, s80, %[lane16]\n"  \
+      "v_add_u32 v84, s82, %[lane16]\n"  \
+      "v_add_u32 v88, s84, %[lane16]\n"  \
+      "v_add_u32 v92, s86, %[lane16]\n"  \
+      "ds_read_b128 v[64:67], v64\n"  \
+      "ds_read_b128 v[68:71], v68\n"  \
+      "ds_read_b128 v[72:75], v72\n"  \
+      "ds_read_b128 v[76:79], v76\n"  \
+      "ds_read_b128 v[80:83], v80\n"  \
+      "ds_read_b128 v[84:87], v84\n"  \
+      "ds_read_b128 v[88:91], v88\n"  \
+      "ds_read_b128 v[92:95], v92\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_and_b32 s34, s34, 0x40\n"  \
       "s_add_u32 s89, s89, 1\n"  \
       "s_load_dwordx16 s[40:55], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v48, v26\n"  \
-      "v_sub_f32 v23, v49, v27\n"  \
-      "v_fma_f32 %[acc0], s57, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s57, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v50, v26\n"  \
-      "v_sub_f32 v25, v51, v27\n"  \
-      "v_fma_f32 %[acc1], s59, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s59, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v52, v26\n"  \
-      "v_sub_f32 v23, v53, v27\n"  \
-      "v_fma_f32 %[acc0], s61, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s61, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v54, v26\n"  \
-      "v_sub_f32 v25, v55, v27\n"  \
-      "v_fma_f32 %[acc1], s63, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s63, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v56, v26\n"  \
-      "v_sub_f32 v23, v57, v27\n"  \
-      "v_fma_f32 %[acc0], s65, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s65, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v58, v26\n"  \
-      "v_sub_f32 v25, v59, v27\n"  \
-      "v_fma_f32 %[acc1], s67, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s67, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v60, v26\n"  \
-      "v_sub_f32 v23, v61, v27\n"  \
-      "v_fma_f32 %[acc0], s69, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s69, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v62, v26\n"  \
-      "v_sub_f32 v25, v63, v27\n"  \
-      "v_fma_f32 %[acc1], s71, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s71, |v25|, %[acc3]\n"  \
+      "v_sub_f32 v48, v96, v56\n"  \
+      "v_sub_f32 v49, v97, v57\n"  \
+      "v_sub_f32 v50, v98, v58\n"  \
+      "v_sub_f32 v51, v99, v59\n"  \
+      "v_fma_f32 %[acc0], s57, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s57, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s57, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s57, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v100, v56\n"  \
+      "v_sub_f32 v53, v101, v57\n"  \
+      "v_sub_f32 v54, v102, v58\n"  \
+      "v_sub_f32 v55, v103, v59\n"  \
+      "v_fma_f32 %[acc1], s59, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s59, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s59, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s59, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v104, v56\n"  \
+      "v_sub_f32 v49, v105, v57\n"  \
+      "v_sub_f32 v50, v106, v58\n"  \
+      "v_sub_f32 v51, v107, v59\n"  \
+      "v_fma_f32 %[acc0], s61, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s61, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s61, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s61, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v108, v56\n"  \
+      "v_sub_f32 v53, v109, v57\n"  \
+      "v_sub_f32 v54, v110, v58\n"  \
+      "v_sub_f32 v55, v111, v59\n"  \
+      "v_fma_f32 %[acc1], s63, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s63, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s63, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s63, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v112, v56\n"  \
+      "v_sub_f32 v49, v113, v57\n"  \
+      "v_sub_f32 v50, v114, v58\n"  \
+      "v_sub_f32 v51, v115, v59\n"  \
+      "v_fma_f32 %[acc0], s65, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s65, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s65, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s65, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v116, v56\n"  \
+      "v_sub_f32 v53, v117, v57\n"  \
+      "v_sub_f32 v54, v118, v58\n"  \
+      "v_sub_f32 v55, v119, v59\n"  \
+      "v_fma_f32 %[acc1], s67, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s67, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s67, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s67, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v120, v56\n"  \
+      "v_sub_f32 v49, v121, v57\n"  \
+      "v_sub_f32 v50, v122, v58\n"  \
+      "v_sub_f32 v51, v123, v59\n"  \
+      "v_fma_f32 %[acc0], s69, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s69, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s69, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s69, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v124, v56\n"  \
+      "v_sub_f32 v53, v125, v57\n"  \
+      "v_sub_f32 v54, v126, v58\n"  \
+      "v_sub_f32 v55, v127, v59\n"  \
+      "v_fma_f32 %[acc1], s71, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s71, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s71, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s71, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s57, 0\n"  \
       "s_cbranch_scc1 11f\n"  \
       "21:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v48, s40, %[lane16]\n"  \
-      "v_add_u32 v50, s42, %[lane16]\n"  \
-      "v_add_u32 v52, s44, %[lane16]\n"  \
-      "v_add_u32 v54, s46, %[lane16]\n"  \
-      "v_add_u32 v56, s48, %[lane16]\n"  \
-      "v_add_u32 v58, s50, %[lane16]\n"  \
-      "v_add_u32 v60, s52, %[lane16]\n"  \
-      "v_add_u32 v62, s54, %[lane16]\n"  \
-      "ds_read_b64 v[48:49], v48\n"  \
-      "ds_read_b64 v[50:51], v50\n"  \
-      "ds_read_b64 v[52:53], v52\n"  \
-      "ds_read_b64 v[54:55], v54\n"  \
-      "ds_read_b64 v[56:57], v56\n"  \
-      "ds_read_b64 v[58:59], v58\n"  \
-      "ds_read_b64 v[60:61], v60\n"  \
-      "ds_read_b64 v[62:63], v62\n"  \
+      "v_add_u32 v96, s40, %[lane16]\n"  \
+      "v_add_u32 v100, s42, %[lane16]\n"  \
+      "v_add_u32 v104, s44, %[lane16]\n"  \
+      "v_add_u32 v108, s46, %[lane16]\n"  \
+      "v_add_u32 v112, s48, %[lane16]\n"  \
+      "v_add_u32 v116, s50, %[lane16]\n"  \
+      "v_add_u32 v120, s52, %[lane16]\n"  \
+      "v_add_u32 v124, s54, %[lane16]\n"  \
+      "ds_read_b128 v[96:99], v96\n"  \
+      "ds_read_b128 v[100:103], v100\n"  \
+      "ds_read_b128 v[104:107], v104\n"  \
+      "ds_read_b128 v[108:111], v108\n"  \
+      "ds_read_b128 v[112:115], v112\n"  \
+      "ds_read_b128 v[116:119], v116\n"  \
+      "ds_read_b128 v[120:123], v120\n"  \
+      "ds_read_b128 v[124:127], v124\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_and_b32 s34, s34, 0x40\n"  \
       "s_add_u32 s89, s89, 1\n"  \
       "s_load_dwordx16 s[56:71], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v32, v26\n"  \
-      "v_sub_f32 v23, v33, v27\n"  \
-      "v_fma_f32 %[acc0], s73, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s73, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v34, v26\n"  \
-      "v_sub_f32 v25, v35, v27\n"  \
-      "v_fma_f32 %[acc1], s75, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s75, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v36, v26\n"  \
-      "v_sub_f32 v23, v37, v27\n"  \
-      "v_fma_f32 %[acc0], s77, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s77, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v38, v26\n"  \
-      "v_sub_f32 v25, v39, v27\n"  \
-      "v_fma_f32 %[acc1], s79, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s79, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v40, v26\n"  \
-      "v_sub_f32 v23, v41, v27\n"  \
-      "v_fma_f32 %[acc0], s81, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s81, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v42, v26\n"  \
-      "v_sub_f32 v25, v43, v27\n"  \
-      "v_fma_f32 %[acc1], s83, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s83, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v44, v26\n"  \
-      "v_sub_f32 v23, v45, v27\n"  \
-      "v_fma_f32 %[acc0], s85, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s85, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v46, v26\n"  \
-      "v_sub_f32 v25, v47, v27\n"  \
-      "v_fma_f32 %[acc1], s87, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s87, |v25|, %[acc3]\n"  \
+      "v_sub_f32 v48, v64, v56\n"  \
+      "v_sub_f32 v49, v65, v57\n"  \
+      "v_sub_f32 v50, v66, v58\n"  \
+      "v_sub_f32 v51, v67, v59\n"  \
+      "v_fma_f32 %[acc0], s73, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s73, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s73, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s73, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v68, v56\n"  \
+      "v_sub_f32 v53, v69, v57\n"  \
+      "v_sub_f32 v54, v70, v58\n"  \
+      "v_sub_f32 v55, v71, v59\n"  \
+      "v_fma_f32 %[acc1], s75, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s75, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s75, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s75, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v72, v56\n"  \
+      "v_sub_f32 v49, v73, v57\n"  \
+      "v_sub_f32 v50, v74, v58\n"  \
+      "v_sub_f32 v51, v75, v59\n"  \
+      "v_fma_f32 %[acc0], s77, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s77, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s77, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s77, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v76, v56\n"  \
+      "v_sub_f32 v53, v77, v57\n"  \
+      "v_sub_f32 v54, v78, v58\n"  \
+      "v_sub_f32 v55, v79, v59\n"  \
+      "v_fma_f32 %[acc1], s79, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s79, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s79, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s79, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v80, v56\n"  \
+      "v_sub_f32 v49, v81, v57\n"  \
+      "v_sub_f32 v50, v82, v58\n"  \
+      "v_sub_f32 v51, v83, v59\n"  \
+      "v_fma_f32 %[acc0], s81, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s81, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s81, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s81, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v84, v56\n"  \
+      "v_sub_f32 v53, v85, v57\n"  \
+      "v_sub_f32 v54, v86, v58\n"  \
+      "v_sub_f32 v55, v87, v59\n"  \
+      "v_fma_f32 %[acc1], s83, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s83, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s83, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s83, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v88, v56\n"  \
+      "v_sub_f32 v49, v89, v57\n"  \
+      "v_sub_f32 v50, v90, v58\n"  \
+      "v_sub_f32 v51, v91, v59\n"  \
+      "v_fma_f32 %[acc0], s85, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s85, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s85, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s85, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v92, v56\n"  \
+      "v_sub_f32 v53, v93, v57\n"  \
+      "v_sub_f32 v54, v94, v58\n"  \
+      "v_sub_f32 v55, v95, v59\n"  \
+      "v_fma_f32 %[acc1], s87, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s87, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s87, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s87, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s73, 0\n"  \
       "s_cbranch_scc1 12f\n"  \
       "22:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v32, s56, %[lane16]\n"  \
-      "v_add_u32 v34, s58, %[lane16]\n"  \
-      "v_add_u32 v36, s60, %[lane16]\n"  \
-      "v_add_u32 v38, s62, %[lane16]\n"  \
-      "v_add_u32 v40, s64, %[lane16]\n"  \
-      "v_add_u32 v42, s66, %[lane16]\n"  \
-      "v_add_u32 v44, s68, %[lane16]\n"  \
-      "v_add_u32 v46, s70, %[lane16]\n"  \
-      "ds_read_b64 v[32:33], v32\n"  \
-      "ds_read_b64 v[34:35], v34\n"  \
-      "ds_read_b64 v[36:37], v36\n"  \
-      "ds_read_b64 v[38:39], v38\n"  \
-      "ds_read_b64 v[40:41], v40\n"  \
-      "ds_read_b64 v[42:43], v42\n"  \
-      "ds_read_b64 v[44:45], v44\n"  \
-      "ds_read_b64 v[46:47], v46\n"  \
+      "v_add_u32 v64, s56, %[lane16]\n"  \
+      "v_add_u32 v68, s58, %[lane16]\n"  \
+      "v_add_u32 v72, s60, %[lane16]\n"  \
+      "v_add_u32 v76, s62, %[lane16]\n"  \
+      "v_add_u32 v80, s64, %[lane16]\n"  \
+      "v_add_u32 v84, s66, %[lane16]\n"  \
+      "v_add_u32 v88, s68, %[lane16]\n"  \
+      "v_add_u32 v92, s70, %[lane16]\n"  \
+      "ds_read_b128 v[64:67], v64\n"  \
+      "ds_read_b128 v[68:71], v68\n"  \
+      "ds_read_b128 v[72:75], v72\n"  \
+      "ds_read_b128 v[76:79], v76\n"  \
+      "ds_read_b128 v[80:83], v80\n"  \
+      "ds_read_b128 v[84:87], v84\n"  \
+      "ds_read_b128 v[88:91], v88\n"  \
+      "ds_read_b128 v[92:95], v92\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_and_b32 s34, s34, 0x40\n"  \
       "s_add_u32 s89, s89, 1\n"  \
       "s_load_dwordx16 s[72:87], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v48, v26\n"  \
-      "v_sub_f32 v23, v49, v27\n"  \
-      "v_fma_f32 %[acc0], s41, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s41, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v50, v26\n"  \
-      "v_sub_f32 v25, v51, v27\n"  \
-      "v_fma_f32 %[acc1], s43, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s43, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v52, v26\n"  \
-      "v_sub_f32 v23, v53, v27\n"  \
-      "v_fma_f32 %[acc0], s45, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s45, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v54, v26\n"  \
-      "v_sub_f32 v25, v55, v27\n"  \
-      "v_fma_f32 %[acc1], s47, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s47, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v56, v26\n"  \
-      "v_sub_f32 v23, v57, v27\n"  \
-      "v_fma_f32 %[acc0], s49, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s49, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v58, v26\n"  \
-      "v_sub_f32 v25, v59, v27\n"  \
-      "v_fma_f32 %[acc1], s51, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s51, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v60, v26\n"  \
-      "v_sub_f32 v23, v61, v27\n"  \
-      "v_fma_f32 %[acc0], s53, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s53, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v62, v26\n"  \
-      "v_sub_f32 v25, v63, v27\n"  \
-      "v_fma_f32 %[acc1], s55, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s55, |v25|, %[acc3]\n"  \
+      "v_sub_f32 v48, v96, v56\n"  \
+      "v_sub_f32 v49, v97, v57\n"  \
+      "v_sub_f32 v50, v98, v58\n"  \
+      "v_sub_f32 v51, v99, v59\n"  \
+      "v_fma_f32 %[acc0], s41, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s41, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s41, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s41, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v100, v56\n"  \
+      "v_sub_f32 v53, v101, v57\n"  \
+      "v_sub_f32 v54, v102, v58\n"  \
+      "v_sub_f32 v55, v103, v59\n"  \
+      "v_fma_f32 %[acc1], s43, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s43, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s43, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s43, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v104, v56\n"  \
+      "v_sub_f32 v49, v105, v57\n"  \
+      "v_sub_f32 v50, v106, v58\n"  \
+      "v_sub_f32 v51, v107, v59\n"  \
+      "v_fma_f32 %[acc0], s45, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s45, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s45, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s45, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v108, v56\n"  \
+      "v_sub_f32 v53, v109, v57\n"  \
+      "v_sub_f32 v54, v110, v58\n"  \
+      "v_sub_f32 v55, v111, v59\n"  \
+      "v_fma_f32 %[acc1], s47, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s47, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s47, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s47, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v112, v56\n"  \
+      "v_sub_f32 v49, v113, v57\n"  \
+      "v_sub_f32 v50, v114, v58\n"  \
+      "v_sub_f32 v51, v115, v59\n"  \
+      "v_fma_f32 %[acc0], s49, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s49, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s49, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s49, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v116, v56\n"  \
+      "v_sub_f32 v53, v117, v57\n"  \
+      "v_sub_f32 v54, v118, v58\n"  \
+      "v_sub_f32 v55, v119, v59\n"  \
+      "v_fma_f32 %[acc1], s51, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s51, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s51, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s51, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v120, v56\n"  \
+      "v_sub_f32 v49, v121, v57\n"  \
+      "v_sub_f32 v50, v122, v58\n"  \
+      "v_sub_f32 v51, v123, v59\n"  \
+      "v_fma_f32 %[acc0], s53, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s53, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s53, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s53, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v124, v56\n"  \
+      "v_sub_f32 v53, v125, v57\n"  \
+      "v_sub_f32 v54, v126, v58\n"  \
+      "v_sub_f32 v55, v127, v59\n"  \
+      "v_fma_f32 %[acc1], s55, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s55, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s55, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s55, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s41, 0\n"  \
       "s_cbranch_scc1 13f\n"  \
       "23:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v48, s72, %[lane16]\n"  \
-      "v_add_u32 v50, s74, %[lane16]\n"  \
-      "v_add_u32 v52, s76, %[lane16]\n"  \
-      "v_add_u32 v54, s78, %[lane16]\n"  \
-      "v_add_u32 v56, s80, %[lane16]\n"  \
-      "v_add_u32 v58, s82, %[lane16]\n"  \
-      "v_add_u32 v60, s84, %[lane16]\n"  \
-      "v_add_u32 v62, s86, %[lane16]\n"  \
-      "ds_read_b64 v[48:49], v48\n"  \
-      "ds_read_b64 v[50:51], v50\n"  \
-      "ds_read_b64 v[52:53], v52\n"  \
-      "ds_read_b64 v[54:55], v54\n"  \
-      "ds_read_b64 v[56:57], v56\n"  \
-      "ds_read_b64 v[58:59], v58\n"  \
-      "ds_read_b64 v[60:61], v60\n"  \
-      "ds_read_b64 v[62:63], v62\n"  \
+      "v_add_u32 v96, s72, %[lane16]\n"  \
+      "v_add_u32 v100, s74, %[lane16]\n"  \
+      "v_add_u32 v104, s76, %[lane16]\n"  \
+      "v_add_u32 v108, s78, %[lane16]\n"  \
+      "v_add_u32 v112, s80, %[lane16]\n"  \
+      "v_add_u32 v116, s82, %[lane16]\n"  \
+      "v_add_u32 v120, s84, %[lane16]\n"  \
+      "v_add_u32 v124, s86, %[lane16]\n"  \
+      "ds_read_b128 v[96:99], v96\n"  \
+      "ds_read_b128 v[100:103], v100\n"  \
+      "ds_read_b128 v[104:107], v104\n"  \
+      "ds_read_b128 v[108:111], v108\n"  \
+      "ds_read_b128 v[112:115], v112\n"  \
+      "ds_read_b128 v[116:119], v116\n"  \
+      "ds_read_b128 v[120:123], v120\n"  \
+      "ds_read_b128 v[124:127], v124\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_and_b32 s34, s34, 0x40\n"  \
       "s_add_u32 s89, s89, 1\n"  \
       "s_load_dwordx16 s[40:55], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v32, v26\n"  \
-      "v_sub_f32 v23, v33, v27\n"  \
-      "v_fma_f32 %[acc0], s57, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s57, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v34, v26\n"  \
-      "v_sub_f32 v25, v35, v27\n"  \
-      "v_fma_f32 %[acc1], s59, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s59, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v36, v26\n"  \
-      "v_sub_f32 v23, v37, v27\n"  \
-      "v_fma_f32 %[acc0], s61, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s61, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v38, v26\n"  \
-      "v_sub_f32 v25, v39, v27\n"  \
-      "v_fma_f32 %[acc1], s63, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s63, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v40, v26\n"  \
-      "v_sub_f32 v23, v41, v27\n"  \
-      "v_fma_f32 %[acc0], s65, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s65, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v42, v26\n"  \
-      "v_sub_f32 v25, v43, v27\n"  \
-      "v_fma_f32 %[acc1], s67, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s67, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v44, v26\n"  \
-      "v_sub_f32 v23, v45, v27\n"  \
-      "v_fma_f32 %[acc0], s69, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s69, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v46, v26\n"  \
-      "v_sub_f32 v25, v47, v27\n"  \
-      "v_fma_f32 %[acc1], s71, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s71, |v25|, %[acc3]\n"  \
+      "v_sub_f32 v48, v64, v56\n"  \
+      "v_sub_f32 v49, v65, v57\n"  \
+      "v_sub_f32 v50, v66, v58\n"  \
+      "v_sub_f32 v51, v67, v59\n"  \
+      "v_fma_f32 %[acc0], s57, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s57, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s57, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s57, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v68, v56\n"  \
+      "v_sub_f32 v53, v69, v57\n"  \
+      "v_sub_f32 v54, v70, v58\n"  \
+      "v_sub_f32 v55, v71, v59\n"  \
+      "v_fma_f32 %[acc1], s59, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s59, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s59, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s59, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v72, v56\n"  \
+      "v_sub_f32 v49, v73, v57\n"  \
+      "v_sub_f32 v50, v74, v58\n"  \
+      "v_sub_f32 v51, v75, v59\n"  \
+      "v_fma_f32 %[acc0], s61, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s61, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s61, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s61, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v76, v56\n"  \
+      "v_sub_f32 v53, v77, v57\n"  \
+      "v_sub_f32 v54, v78, v58\n"  \
+      "v_sub_f32 v55, v79, v59\n"  \
+      "v_fma_f32 %[acc1], s63, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s63, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s63, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s63, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v80, v56\n"  \
+      "v_sub_f32 v49, v81, v57\n"  \
+      "v_sub_f32 v50, v82, v58\n"  \
+      "v_sub_f32 v51, v83, v59\n"  \
+      "v_fma_f32 %[acc0], s65, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s65, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s65, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s65, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v84, v56\n"  \
+      "v_sub_f32 v53, v85, v57\n"  \
+      "v_sub_f32 v54, v86, v58\n"  \
+      "v_sub_f32 v55, v87, v59\n"  \
+      "v_fma_f32 %[acc1], s67, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s67, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s67, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s67, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v88, v56\n"  \
+      "v_sub_f32 v49, v89, v57\n"  \
+      "v_sub_f32 v50, v90, v58\n"  \
+      "v_sub_f32 v51, v91, v59\n"  \
+      "v_fma_f32 %[acc0], s69, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s69, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s69, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s69, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v92, v56\n"  \
+      "v_sub_f32 v53, v93, v57\n"  \
+      "v_sub_f32 v54, v94, v58\n"  \
+      "v_sub_f32 v55, v95, v59\n"  \
+      "v_fma_f32 %[acc1], s71, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s71, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s71, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s71, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s57, 0\n"  \
       "s_cbranch_scc1 14f\n"  \
       "24:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v32, s40, %[lane16]\n"  \
-      "v_add_u32 v34, s42, %[lane16]\n"  \
-      "v_add_u32 v36, s44, %[lane16]\n"  \
-      "v_add_u32 v38, s46, %[lane16]\n"  \
-      "v_add_u32 v40, s48, %[lane16]\n"  \
-      "v_add_u32 v42, s50, %[lane16]\n"  \
-      "v_add_u32 v44, s52, %[lane16]\n"  \
-      "v_add_u32 v46, s54, %[lane16]\n"  \
-      "ds_read_b64 v[32:33], v32\n"  \
-      "ds_read_b64 v[34:35], v34\n"  \
-      "ds_read_b64 v[36:37], v36\n"  \
-      "ds_read_b64 v[38:39], v38\n"  \
-      "ds_read_b64 v[40:41], v40\n"  \
-      "ds_read_b64 v[42:43], v42\n"  \
-      "ds_read_b64 v[44:45], v44\n"  \
-      "ds_read_b64 v[46:47], v46\n"  \
+      "v_add_u32 v64, s40, %[lane16]\n"  \
+      "v_add_u32 v68, s42, %[lane16]\n"  \
+      "v_add_u32 v72, s44, %[lane16]\n"  \
+      "v_add_u32 v76, s46, %[lane16]\n"  \
+      "v_add_u32 v80, s48, %[lane16]\n"  \
+      "v_add_u32 v84, s50, %[lane16]\n"  \
+      "v_add_u32 v88, s52, %[lane16]\n"  \
+      "v_add_u32 v92, s54, %[lane16]\n"  \
+      "ds_read_b128 v[64:67], v64\n"  \
+      "ds_read_b128 v[68:71], v68\n"  \
+      "ds_read_b128 v[72:75], v72\n"  \
+      "ds_read_b128 v[76:79], v76\n"  \
+      "ds_read_b128 v[80:83], v80\n"  \
+      "ds_read_b128 v[84:87], v84\n"  \
+      "ds_read_b128 v[88:91], v88\n"  \
+      "ds_read_b128 v[92:95], v92\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_and_b32 s34, s34, 0x40\n"  \
       "s_add_u32 s89, s89, 1\n"  \
       "s_load_dwordx16 s[56:71], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v48, v26\n"  \
-      "v_sub_f32 v23, v49, v27\n"  \
-      "v_fma_f32 %[acc0], s73, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s73, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v50, v26\n"  \
-      "v_sub_f32 v25, v51, v27\n"  \
-      "v_fma_f32 %[acc1], s75, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s75, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v52, v26\n"  \
-      "v_sub_f32 v23, v53, v27\n"  \
-      "v_fma_f32 %[acc0], s77, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s77, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v54, v26\n"  \
-      "v_sub_f32 v25, v55, v27\n"  \
-      "v_fma_f32 %[acc1], s79, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s79, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v56, v26\n"  \
-      "v_sub_f32 v23, v57, v27\n"  \
-      "v_fma_f32 %[acc0], s81, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s81, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v58, v26\n"  \
-      "v_sub_f32 v25, v59, v27\n"  \
-      "v_fma_f32 %[acc1], s83, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s83, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v60, v26\n"  \
-      "v_sub_f32 v23, v61, v27\n"  \
-      "v_fma_f32 %[acc0], s85, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s85, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v62, v26\n"  \
-      "v_sub_f32 v25, v63, v27\n"  \
-      "v_fma_f32 %[acc1], s87, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s87, |v25|, %[acc3]\n"  \
+      "v_sub_f32 v48, v96, v56\n"  \
+      "v_sub_f32 v49, v97, v57\n"  \
+      "v_sub_f32 v50, v98, v58\n"  \
+      "v_sub_f32 v51, v99, v59\n"  \
+      "v_fma_f32 %[acc0], s73, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s73, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s73, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s73, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v100, v56\n"  \
+      "v_sub_f32 v53, v101, v57\n"  \
+      "v_sub_f32 v54, v102, v58\n"  \
+      "v_sub_f32 v55, v103, v59\n"  \
+      "v_fma_f32 %[acc1], s75, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s75, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s75, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s75, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v104, v56\n"  \
+      "v_sub_f32 v49, v105, v57\n"  \
+      "v_sub_f32 v50, v106, v58\n"  \
+      "v_sub_f32 v51, v107, v59\n"  \
+      "v_fma_f32 %[acc0], s77, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s77, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s77, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s77, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v108, v56\n"  \
+      "v_sub_f32 v53, v109, v57\n"  \
+      "v_sub_f32 v54, v110, v58\n"  \
+      "v_sub_f32 v55, v111, v59\n"  \
+      "v_fma_f32 %[acc1], s79, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s79, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s79, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s79, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v112, v56\n"  \
+      "v_sub_f32 v49, v113, v57\n"  \
+      "v_sub_f32 v50, v114, v58\n"  \
+      "v_sub_f32 v51, v115, v59\n"  \
+      "v_fma_f32 %[acc0], s81, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s81, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s81, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s81, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v116, v56\n"  \
+      "v_sub_f32 v53, v117, v57\n"  \
+      "v_sub_f32 v54, v118, v58\n"  \
+      "v_sub_f32 v55, v119, v59\n"  \
+      "v_fma_f32 %[acc1], s83, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s83, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s83, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s83, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v120, v56\n"  \
+      "v_sub_f32 v49, v121, v57\n"  \
+      "v_sub_f32 v50, v122, v58\n"  \
+      "v_sub_f32 v51, v123, v59\n"  \
+      "v_fma_f32 %[acc0], s85, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s85, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s85, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s85, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v124, v56\n"  \
+      "v_sub_f32 v53, v125, v57\n"  \
+      "v_sub_f32 v54, v126, v58\n"  \
+      "v_sub_f32 v55, v127, v59\n"  \
+      "v_fma_f32 %[acc1], s87, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s87, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s87, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s87, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s73, 0\n"  \
       "s_cbranch_scc1 15f\n"  \
       "25:\n"  \
@@ -1524,398 +1940,618 @@
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 20b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 20b\n"  \
       "11:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 21b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 21b\n"  \
       "12:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 22b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 22b\n"  \
       "13:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 23b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 23b\n"  \
       "14:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 24b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 24b\n"  \
       "15:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 25b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 25b\n"  \
       "8:\n"  \
       "s_waitcnt vmcnt(0) lgkmcnt(0)\n"  \
-      : [acc0] "+v"(acc[0]), [acc1] "+v"(acc[1]), [acc2] "+v"(acc[2]), [acc3] "+v"(acc[3])  \
+      : [acc0] "+v"(acc[0]), [acc1] "+v"(acc[1]), [acc2] "+v"(acc[2]), [acc3] "+v"(acc[3]), [acc4] "+v"(acc[4]), [acc5] "+v"(acc[5]), [acc6] "+v"(acc[6]), [acc7] "+v"(acc[7])  \
       : [lane16] "v"(lane16), [lane4] "v"(lane4), [eb] "s"(eb), [bp] "s"(bp),  \
         [bstride] "s"(bstride), [ncols] "s"(ncols)  \
-      : "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63",  \
+      : "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127",  \
         "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "scc", "memory")
 
 #define STREAM3(acc, lane16, lane4, eb, bp, bstride, ncols)  \
   asm volatile(  \
       "s_mov_b32 s88, 0\n"  \
       "s_mov_b64 s[90:91], %[bp]\n"  \
-      "global_load_dword v26, %[lane4], s[90:91]\n"  \
-      "global_load_dword v27, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v56, %[lane4], s[90:91]\n"  \
+      "global_load_dword v57, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v58, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v59, %[lane4], s[90:91] offset:768\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_mov_b64 s[36:37], %[eb]\n"  \
       "s_mov_b32 s34, 0\n"  \
       "s_load_dwordx16 s[40:55], s[36:37], s34\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v32, s40, %[lane16]\n"  \
-      "v_add_u32 v34, s42, %[lane16]\n"  \
-      "v_add_u32 v36, s44, %[lane16]\n"  \
-      "v_add_u32 v38, s46, %[lane16]\n"  \
-      "v_add_u32 v40, s48, %[lane16]\n"  \
-      "v_add_u32 v42, s50, %[lane16]\n"  \
-      "v_add_u32 v44, s52, %[lane16]\n"  \
-      "v_add_u32 v46, s54, %[lane16]\n"  \
+      "v_add_u32 v64, s40, %[lane16]\n"  \
+      "v_add_u32 v68, s42, %[lane16]\n"  \
+      "v_add_u32 v72, s44, %[lane16]\n"  \
+      "v_add_u32 v76, s46, %[lane16]\n"  \
+      "v_add_u32 v80, s48, %[lane16]\n"  \
+      "v_add_u32 v84, s50, %[lane16]\n"  \
+      "v_add_u32 v88, s52, %[lane16]\n"  \
+      "v_add_u32 v92, s54, %[lane16]\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[56:71], s[36:37], s34\n"  \
-      "s_waitcnt vmcnt(2)\n"  \
+      "s_waitcnt vmcnt(4)\n"  \
       "7:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v48, s56, %[lane16]\n"  \
-      "v_add_u32 v50, s58, %[lane16]\n"  \
-      "v_add_u32 v52, s60, %[lane16]\n"  \
-      "v_add_u32 v54, s62, %[lane16]\n"  \
-      "v_add_u32 v56, s64, %[lane16]\n"  \
-      "v_add_u32 v58, s66, %[lane16]\n"  \
-      "v_add_u32 v60, s68, %[lane16]\n"  \
-      "v_add_u32 v62, s70, %[lane16]\n"  \
+      "v_add_u32 v96, s56, %[lane16]\n"  \
+      "v_add_u32 v100, s58, %[lane16]\n"  \
+      "v_add_u32 v104, s60, %[lane16]\n"  \
+      "v_add_u32 v108, s62, %[lane16]\n"  \
+      "v_add_u32 v112, s64, %[lane16]\n"  \
+      "v_add_u32 v116, s66, %[lane16]\n"  \
+      "v_add_u32 v120, s68, %[lane16]\n"  \
+      "v_add_u32 v124, s70, %[lane16]\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[72:87], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v32, v26\n"  \
-      "v_sub_f32 v23, v33, v27\n"  \
-      "v_fma_f32 %[acc0], s41, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s41, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v34, v26\n"  \
-      "v_sub_f32 v25, v35, v27\n"  \
-      "v_fma_f32 %[acc1], s43, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s43, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v36, v26\n"  \
-      "v_sub_f32 v23, v37, v27\n"  \
-      "v_fma_f32 %[acc0], s45, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s45, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v38, v26\n"  \
-      "v_sub_f32 v25, v39, v27\n"  \
-      "v_fma_f32 %[acc1], s47, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s47, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v40, v26\n"  \
-      "v_sub_f32 v23, v41, v27\n"  \
-      "v_fma_f32 %[acc0], s49, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s49, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v42, v26\n"  \
-      "v_sub_f32 v25, v43, v27\n"  \
-      "v_fma_f32 %[acc1], s51, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s51, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v44, v26\n"  \
-      "v_sub_f32 v23, v45, v27\n"  \
-      "v_fma_f32 %[acc0], s53, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s53, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v46, v26\n"  \
-      "v_sub_f32 v25, v47, v27\n"  \
-      "v_fma_f32 %[acc1], s55, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s55, |v25|, %[acc3]\n"  \
+      "v_sub_f32 v48, v64, v56\n"  \
+      "v_sub_f32 v49, v65, v57\n"  \
+      "v_sub_f32 v50, v66, v58\n"  \
+      "v_sub_f32 v51, v67, v59\n"  \
+      "v_fma_f32 %[acc0], s41, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s41, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s41, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s41, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v68, v56\n"  \
+      "v_sub_f32 v53, v69, v57\n"  \
+      "v_sub_f32 v54, v70, v58\n"  \
+      "v_sub_f32 v55, v71, v59\n"  \
+      "v_fma_f32 %[acc1], s43, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s43, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s43, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s43, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v72, v56\n"  \
+      "v_sub_f32 v49, v73, v57\n"  \
+      "v_sub_f32 v50, v74, v58\n"  \
+      "v_sub_f32 v51, v75, v59\n"  \
+      "v_fma_f32 %[acc0], s45, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s45, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s45, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s45, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v76, v56\n"  \
+      "v_sub_f32 v53, v77, v57\n"  \
+      "v_sub_f32 v54, v78, v58\n"  \
+      "v_sub_f32 v55, v79, v59\n"  \
+      "v_fma_f32 %[acc1], s47, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s47, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s47, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s47, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v80, v56\n"  \
+      "v_sub_f32 v49, v81, v57\n"  \
+      "v_sub_f32 v50, v82, v58\n"  \
+      "v_sub_f32 v51, v83, v59\n"  \
+      "v_fma_f32 %[acc0], s49, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s49, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s49, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s49, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v84, v56\n"  \
+      "v_sub_f32 v53, v85, v57\n"  \
+      "v_sub_f32 v54, v86, v58\n"  \
+      "v_sub_f32 v55, v87, v59\n"  \
+      "v_fma_f32 %[acc1], s51, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s51, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s51, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s51, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v88, v56\n"  \
+      "v_sub_f32 v49, v89, v57\n"  \
+      "v_sub_f32 v50, v90, v58\n"  \
+      "v_sub_f32 v51, v91, v59\n"  \
+      "v_fma_f32 %[acc0], s53, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s53, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s53, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s53, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v92, v56\n"  \
+      "v_sub_f32 v53, v93, v57\n"  \
+      "v_sub_f32 v54, v94, v58\n"  \
+      "v_sub_f32 v55, v95, v59\n"  \
+      "v_fma_f32 %[acc1], s55, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s55, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s55, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s55, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s41, 0\n"  \
       "s_cbranch_scc1 10f\n"  \
       "20:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v32, s72, %[lane16]\n"  \
-      "v_add_u32 v34, s74, %[lane16]\n"  \
-      "v_add_u32 v36, s76, %[lane16]\n"  \
-      "v_add_u32 v38, s78, %[lane16]\n"  \
-      "v_add_u32 v40, s80, %[lane16]\n"  \
-      "v_add_u32 v42, s82, %[lane16]\n"  \
-      "v_add_u32 v44, s84, %[lane16]\n"  \
-      "v_add_u32 v46, s86, %[lane16]\n"  \
+      "v_add_u32 v64, s72, %[lane16]\n"  \
+      "v_add_u32 v68, s74, %[lane16]\n"  \
+      "v_add_u32 v72, s76, %[lane16]\n"  \
+      "v_add_u32 v76, s78, %[lane16]\n"  \
+      "v_add_u32 v80, s80, %[lane16]\n"  \
+      "v_add_u32 v84, s82, %[lane16]\n"  \
+      "v_add_u32 v88, s84, %[lane16]\n"  \
+      "v_add_u32 v92, s86, %[lane16]\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[40:55], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v48, v26\n"  \
-      "v_sub_f32 v23, v49, v27\n"  \
-      "v_fma_f32 %[acc0], s57, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s57, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v50, v26\n"  \
-      "v_sub_f32 v25, v51, v27\n"  \
-      "v_fma_f32 %[acc1], s59, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s59, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v52, v26\n"  \
-      "v_sub_f32 v23, v53, v27\n"  \
-      "v_fma_f32 %[acc0], s61, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s61, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v54, v26\n"  \
-      "v_sub_f32 v25, v55, v27\n"  \
-      "v_fma_f32 %[acc1], s63, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s63, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v56, v26\n"  \
-      "v_sub_f32 v23, v57, v27\n"  \
-      "v_fma_f32 %[acc0], s65, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s65, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v58, v26\n"  \
-      "v_sub_f32 v25, v59, v27\n"  \
-      "v_fma_f32 %[acc1], s67, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s67, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v60, v26\n"  \
-      "v_sub_f32 v23, v61, v27\n"  \
-      "v_fma_f32 %[acc0], s69, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s69, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v62, v26\n"  \
-      "v_sub_f32 v25, v63, v27\n"  \
-      "v_fma_f32 %[acc1], s71, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s71, |v25|, %[acc3]\n"  \
+      "v_sub_f32 v48, v96, v56\n"  \
+      "v_sub_f32 v49, v97, v57\n"  \
+      "v_sub_f32 v50, v98, v58\n"  \
+      "v_sub_f32 v51, v99, v59\n"  \
+      "v_fma_f32 %[acc0], s57, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s57, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s57, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s57, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v100, v56\n"  \
+      "v_sub_f32 v53, v101, v57\n"  \
+      "v_sub_f32 v54, v102, v58\n"  \
+      "v_sub_f32 v55, v103, v59\n"  \
+      "v_fma_f32 %[acc1], s59, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s59, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s59, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s59, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v104, v56\n"  \
+      "v_sub_f32 v49, v105, v57\n"  \
+      "v_sub_f32 v50, v106, v58\n"  \
+      "v_sub_f32 v51, v107, v59\n"  \
+      "v_fma_f32 %[acc0], s61, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s61, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s61, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s61, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v108, v56\n"  \
+      "v_sub_f32 v53, v109, v57\n"  \
+      "v_sub_f32 v54, v110, v58\n"  \
+      "v_sub_f32 v55, v111, v59\n"  \
+      "v_fma_f32 %[acc1], s63, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s63, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s63, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s63, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v112, v56\n"  \
+      "v_sub_f32 v49, v113, v57\n"  \
+      "v_sub_f32 v50, v114, v58\n"  \
+      "v_sub_f32 v51, v115, v59\n"  \
+      "v_fma_f32 %[acc0], s65, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s65, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s65, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s65, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v116, v56\n"  \
+      "v_sub_f32 v53, v117, v57\n"  \
+      "v_sub_f32 v54, v118, v58\n"  \
+      "v_sub_f32 v55, v119, v59\n"  \
+      "v_fma_f32 %[acc1], s67, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s67, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s67, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s67, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v120, v56\n"  \
+      "v_sub_f32 v49, v121, v57\n"  \
+      "v_sub_f32 v50, v122, v58\n"  \
+      "v_sub_f32 v51, v123, v59\n"  \
+      "v_fma_f32 %[acc0], s69, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s69, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s69, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s69, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v124, v56\n"  \
+      "v_sub_f32 v53, v125, v57\n"  \
+      "v_sub_f32 v54, v126, v58\n"  \
+      "v_sub_f32 v55, v127, v59\n"  \
+      "v_fma_f32 %[acc1], s71, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s71, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s71, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s71, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s57, 0\n"  \
       "s_cbranch_scc1 11f\n"  \
       "21:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v48, s40, %[lane16]\n"  \
-      "v_add_u32 v50, s42, %[lane16]\n"  \
-      "v_add_u32 v52, s44, %[lane16]\n"  \
-      "v_add_u32 v54, s46, %[lane16]\n"  \
-      "v_add_u32 v56, s48, %[lane16]\n"  \
-      "v_add_u32 v58, s50, %[lane16]\n"  \
-      "v_add_u32 v60, s52, %[lane16]\n"  \
-      "v_add_u32 v62, s54, %[lane16]\n"  \
+      "v_add_u32 v96, s40, %[lane16]\n"  \
+      "v_add_u32 v100, s42, %[lane16]\n"  \
+      "v_add_u32 v104, s44, %[lane16]\n"  \
+      "v_add_u32 v108, s46, %[lane16]\n"  \
+      "v_add_u32 v112, s48, %[lane16]\n"  \
+      "v_add_u32 v116, s50, %[lane16]\n"  \
+      "v_add_u32 v120, s52, %[lane16]\n"  \
+      "v_add_u32 v124, s54, %[lane16]\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[56:71], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v32, v26\n"  \
-      "v_sub_f32 v23, v33, v27\n"  \
-      "v_fma_f32 %[acc0], s73, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s73, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v34, v26\n"  \
-      "v_sub_f32 v25, v35, v27\n"  \
-      "v_fma_f32 %[acc1], s75, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s75, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v36, v26\n"  \
-      "v_sub_f32 v23, v37, v27\n"  \
-      "v_fma_f32 %[acc0], s77, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s77, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v38, v26\n"  \
-      "v_sub_f32 v25, v39, v27\n"  \
-      "v_fma_f32 %[acc1], s79, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s79, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v40, v26\n"  \
-      "v_sub_f32 v23, v41, v27\n"  \
-      "v_fma_f32 %[acc0], s81, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s81, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v42, v26\n"  \
-      "v_sub_f32 v25, v43, v27\n"  \
-      "v_fma_f32 %[acc1], s83, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s83, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v44, v26\n"  \
-      "v_sub_f32 v23, v45, v27\n"  \
-      "v_fma_f32 %[acc0], s85, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s85, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v46, v26\n"  \
-      "v_sub_f32 v25, v47, v27\n"  \
-      "v_fma_f32 %[acc1], s87, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s87, |v25|, %[acc3]\n"  \
+      "v_sub_f32 v48, v64, v56\n"  \
+      "v_sub_f32 v49, v65, v57\n"  \
+      "v_sub_f32 v50, v66, v58\n"  \
+      "v_sub_f32 v51, v67, v59\n"  \
+      "v_fma_f32 %[acc0], s73, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s73, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s73, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s73, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v68, v56\n"  \
+      "v_sub_f32 v53, v69, v57\n"  \
+      "v_sub_f32 v54, v70, v58\n"  \
+      "v_sub_f32 v55, v71, v59\n"  \
+      "v_fma_f32 %[acc1], s75, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s75, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s75, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s75, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v72, v56\n"  \
+      "v_sub_f32 v49, v73, v57\n"  \
+      "v_sub_f32 v50, v74, v58\n"  \
+      "v_sub_f32 v51, v75, v59\n"  \
+      "v_fma_f32 %[acc0], s77, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s77, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s77, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s77, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v76, v56\n"  \
+      "v_sub_f32 v53, v77, v57\n"  \
+      "v_sub_f32 v54, v78, v58\n"  \
+      "v_sub_f32 v55, v79, v59\n"  \
+      "v_fma_f32 %[acc1], s79, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s79, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s79, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s79, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v80, v56\n"  \
+      "v_sub_f32 v49, v81, v57\n"  \
+      "v_sub_f32 v50, v82, v58\n"  \
+      "v_sub_f32 v51, v83, v59\n"  \
+      "v_fma_f32 %[acc0], s81, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s81, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s81, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s81, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v84, v56\n"  \
+      "v_sub_f32 v53, v85, v57\n"  \
+      "v_sub_f32 v54, v86, v58\n"  \
+      "v_sub_f32 v55, v87, v59\n"  \
+      "v_fma_f32 %[acc1], s83, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s83, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s83, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s83, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v88, v56\n"  \
+      "v_sub_f32 v49, v89, v57\n"  \
+      "v_sub_f32 v50, v90, v58\n"  \
+      "v_sub_f32 v51, v91, v59\n"  \
+      "v_fma_f32 %[acc0], s85, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s85, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s85, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s85, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v92, v56\n"  \
+      "v_sub_f32 v53, v93, v57\n"  \
+      "v_sub_f32 v54, v94, v58\n"  \
+      "v_sub_f32 v55, v95, v59\n"  \
+      "v_fma_f32 %[acc1], s87, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s87, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s87, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s87, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s73, 0\n"  \
       "s_cbranch_scc1 12f\n"  \
       "22:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v32, s56, %[lane16]\n"  \
-      "v_add_u32 v34, s58, %[lane16]\n"  \
-      "v_add_u32 v36, s60, %[lane16]\n"  \
-      "v_add_u32 v38, s62, %[lane16]\n"  \
-      "v_add_u32 v40, s64, %[lane16]\n"  \
-      "v_add_u32 v42, s66, %[lane16]\n"  \
-      "v_add_u32 v44, s68, %[lane16]\n"  \
-      "v_add_u32 v46, s70, %[lane16]\n"  \
+      "v_add_u32 v64, s56, %[lane16]\n"  \
+      "v_add_u32 v68, s58, %[lane16]\n"  \
+      "v_add_u32 v72, s60, %[lane16]\n"  \
+      "v_add_u32 v76, s62, %[lane16]\n"  \
+      "v_add_u32 v80, s64, %[lane16]\n"  \
+      "v_add_u32 v84, s66, %[lane16]\n"  \
+      "v_add_u32 v88, s68, %[lane16]\n"  \
+      "v_add_u32 v92, s70, %[lane16]\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[72:87], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v48, v26\n"  \
-      "v_sub_f32 v23, v49, v27\n"  \
-      "v_fma_f32 %[acc0], s41, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s41, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v50, v26\n"  \
-      "v_sub_f32 v25, v51, v27\n"  \
-      "v_fma_f32 %[acc1], s43, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s43, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v52, v26\n"  \
-      "v_sub_f32 v23, v53, v27\n"  \
-      "v_fma_f32 %[acc0], s45, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s45, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v54, v26\n"  \
-      "v_sub_f32 v25, v55, v27\n"  \
-      "v_fma_f32 %[acc1], s47, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s47, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v56, v26\n"  \
-      "v_sub_f32 v23, v57, v27\n"  \
-      "v_fma_f32 %[acc0], s49, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s49, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v58, v26\n"  \
-      "v_sub_f32 v25, v59, v27\n"  \
-      "v_fma_f32 %[acc1], s51, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s51, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v60, v26\n"  \
-      "v_sub_f32 v23, v61, v27\n"  \
-      "v_fma_f32 %[acc0], s53, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s53, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v62, v26\n"  \
-      "v_sub_f32 v25, v63, v27\n"  \
-      "v_fma_f32 %[acc1], s55, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s55, |v25|, %[acc3]\n"  \
+      "v_sub_f32 v48, v96, v56\n"  \
+      "v_sub_f32 v49, v97, v57\n"  \
+      "v_sub_f32 v50, v98, v58\n"  \
+      "v_sub_f32 v51, v99, v59\n"  \
+      "v_fma_f32 %[acc0], s41, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s41, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s41, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s41, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v100, v56\n"  \
+      "v_sub_f32 v53, v101, v57\n"  \
+      "v_sub_f32 v54, v102, v58\n"  \
+      "v_sub_f32 v55, v103, v59\n"  \
+      "v_fma_f32 %[acc1], s43, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s43, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s43, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s43, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v104, v56\n"  \
+      "v_sub_f32 v49, v105, v57\n"  \
+      "v_sub_f32 v50, v106, v58\n"  \
+      "v_sub_f32 v51, v107, v59\n"  \
+      "v_fma_f32 %[acc0], s45, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s45, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s45, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s45, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v108, v56\n"  \
+      "v_sub_f32 v53, v109, v57\n"  \
+      "v_sub_f32 v54, v110, v58\n"  \
+      "v_sub_f32 v55, v111, v59\n"  \
+      "v_fma_f32 %[acc1], s47, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s47, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s47, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s47, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v112, v56\n"  \
+      "v_sub_f32 v49, v113, v57\n"  \
+      "v_sub_f32 v50, v114, v58\n"  \
+      "v_sub_f32 v51, v115, v59\n"  \
+      "v_fma_f32 %[acc0], s49, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s49, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s49, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s49, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v116, v56\n"  \
+      "v_sub_f32 v53, v117, v57\n"  \
+      "v_sub_f32 v54, v118, v58\n"  \
+      "v_sub_f32 v55, v119, v59\n"  \
+      "v_fma_f32 %[acc1], s51, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s51, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s51, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s51, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v120, v56\n"  \
+      "v_sub_f32 v49, v121, v57\n"  \
+      "v_sub_f32 v50, v122, v58\n"  \
+      "v_sub_f32 v51, v123, v59\n"  \
+      "v_fma_f32 %[acc0], s53, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s53, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s53, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s53, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v124, v56\n"  \
+      "v_sub_f32 v53, v125, v57\n"  \
+      "v_sub_f32 v54, v126, v58\n"  \
+      "v_sub_f32 v55, v127, v59\n"  \
+      "v_fma_f32 %[acc1], s55, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s55, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s55, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s55, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s41, 0\n"  \
       "s_cbranch_scc1 13f\n"  \
       "23:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v48, s72, %[lane16]\n"  \
-      "v_add_u32 v50, s74, %[lane16]\n"  \
-      "v_add_u32 v52, s76, %[lane16]\n"  \
-      "v_add_u32 v54, s78, %[lane16]\n"  \
-      "v_add_u32 v56, s80, %[lane16]\n"  \
-      "v_add_u32 v58, s82, %[lane16]\n"  \
-      "v_add_u32 v60, s84, %[lane16]\n"  \
-      "v_add_u32 v62, s86, %[lane16]\n"  \
+      "v_add_u32 v96, s72, %[lane16]\n"  \
+      "v_add_u32 v100, s74, %[lane16]\n"  \
+      "v_add_u32 v104, s76, %[lane16]\n"  \
+      "v_add_u32 v108, s78, %[lane16]\n"  \
+      "v_add_u32 v112, s80, %[lane16]\n"  \
+      "v_add_u32 v116, s82, %[lane16]\n"  \
+      "v_add_u32 v120, s84, %[lane16]\n"  \
+      "v_add_u32 v124, s86, %[lane16]\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[40:55], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v32, v26\n"  \
-      "v_sub_f32 v23, v33, v27\n"  \
-      "v_fma_f32 %[acc0], s57, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s57, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v34, v26\n"  \
-      "v_sub_f32 v25, v35, v27\n"  \
-      "v_fma_f32 %[acc1], s59, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s59, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v36, v26\n"  \
-      "v_sub_f32 v23, v37, v27\n"  \
-      "v_fma_f32 %[acc0], s61, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s61, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v38, v26\n"  \
-      "v_sub_f32 v25, v39, v27\n"  \
-      "v_fma_f32 %[acc1], s63, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s63, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v40, v26\n"  \
-      "v_sub_f32 v23, v41, v27\n"  \
-      "v_fma_f32 %[acc0], s65, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s65, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v42, v26\n"  \
-      "v_sub_f32 v25, v43, v27\n"  \
-      "v_fma_f32 %[acc1], s67, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s67, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v44, v26\n"  \
-      "v_sub_f32 v23, v45, v27\n"  \
-      "v_fma_f32 %[acc0], s69, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s69, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v46, v26\n"  \
-      "v_sub_f32 v25, v47, v27\n"  \
-      "v_fma_f32 %[acc1], s71, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s71, |v25|, %[acc3]\n"  \
+      "v_sub_f32 v48, v64, v56\n"  \
+      "v_sub_f32 v49, v65, v57\n"  \
+      "v_sub_f32 v50, v66, v58\n"  \
+      "v_sub_f32 v51, v67, v59\n"  \
+      "v_fma_f32 %[acc0], s57, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s57, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s57, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s57, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v68, v56\n"  \
+      "v_sub_f32 v53, v69, v57\n"  \
+      "v_sub_f32 v54, v70, v58\n"  \
+      "v_sub_f32 v55, v71, v59\n"  \
+      "v_fma_f32 %[acc1], s59, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s59, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s59, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s59, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v72, v56\n"  \
+      "v_sub_f32 v49, v73, v57\n"  \
+      "v_sub_f32 v50, v74, v58\n"  \
+      "v_sub_f32 v51, v75, v59\n"  \
+      "v_fma_f32 %[acc0], s61, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s61, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s61, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s61, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v76, v56\n"  \
+      "v_sub_f32 v53, v77, v57\n"  \
+      "v_sub_f32 v54, v78, v58\n"  \
+      "v_sub_f32 v55, v79, v59\n"  \
+      "v_fma_f32 %[acc1], s63, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s63, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s63, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s63, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v80, v56\n"  \
+      "v_sub_f32 v49, v81, v57\n"  \
+      "v_sub_f32 v50, v82, v58\n"  \
+      "v_sub_f32 v51, v83, v59\n"  \
+      "v_fma_f32 %[acc0], s65, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s65, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s65, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s65, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v84, v56\n"  \
+      "v_sub_f32 v53, v85, v57\n"  \
+      "v_sub_f32 v54, v86, v58\n"  \
+      "v_sub_f32 v55, v87, v59\n"  \
+      "v_fma_f32 %[acc1], s67, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s67, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s67, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s67, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v88, v56\n"  \
+      "v_sub_f32 v49, v89, v57\n"  \
+      "v_sub_f32 v50, v90, v58\n"  \
+      "v_sub_f32 v51, v91, v59\n"  \
+      "v_fma_f32 %[acc0], s69, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s69, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s69, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s69, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v92, v56\n"  \
+      "v_sub_f32 v53, v93, v57\n"  \
+      "v_sub_f32 v54, v94, v58\n"  \
+      "v_sub_f32 v55, v95, v59\n"  \
+      "v_fma_f32 %[acc1], s71, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s71, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s71, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s71, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s57, 0\n"  \
       "s_cbranch_scc1 14f\n"  \
       "24:\n"  \
       "s_waitcnt lgkmcnt(0)\n"  \
-      "v_add_u32 v32, s40, %[lane16]\n"  \
-      "v_add_u32 v34, s42, %[lane16]\n"  \
-      "v_add_u32 v36, s44, %[lane16]\n"  \
-      "v_add_u32 v38, s46, %[lane16]\n"  \
-      "v_add_u32 v40, s48, %[lane16]\n"  \
-      "v_add_u32 v42, s50, %[lane16]\n"  \
-      "v_add_u32 v44, s52, %[lane16]\n"  \
-      "v_add_u32 v46, s54, %[lane16]\n"  \
+      "v_add_u32 v64, s40, %[lane16]\n"  \
+      "v_add_u32 v68, s42, %[lane16]\n"  \
+      "v_add_u32 v72, s44, %[lane16]\n"  \
+      "v_add_u32 v76, s46, %[lane16]\n"  \
+      "v_add_u32 v80, s48, %[lane16]\n"  \
+      "v_add_u32 v84, s50, %[lane16]\n"  \
+      "v_add_u32 v88, s52, %[lane16]\n"  \
+      "v_add_u32 v92, s54, %[lane16]\n"  \
       "s_add_u32 s34, s34, 64\n"  \
       "s_load_dwordx16 s[56:71], s[36:37], s34\n"  \
-      "v_sub_f32 v22, v48, v26\n"  \
-      "v_sub_f32 v23, v49, v27\n"  \
-      "v_fma_f32 %[acc0], s73, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s73, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v50, v26\n"  \
-      "v_sub_f32 v25, v51, v27\n"  \
-      "v_fma_f32 %[acc1], s75, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s75, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v52, v26\n"  \
-      "v_sub_f32 v23, v53, v27\n"  \
-      "v_fma_f32 %[acc0], s77, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s77, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v54, v26\n"  \
-      "v_sub_f32 v25, v55, v27\n"  \
-      "v_fma_f32 %[acc1], s79, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s79, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v56, v26\n"  \
-      "v_sub_f32 v23, v57, v27\n"  \
-      "v_fma_f32 %[acc0], s81, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s81, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v58, v26\n"  \
-      "v_sub_f32 v25, v59, v27\n"  \
-      "v_fma_f32 %[acc1], s83, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s83, |v25|, %[acc3]\n"  \
-      "v_sub_f32 v22, v60, v26\n"  \
-      "v_sub_f32 v23, v61, v27\n"  \
-      "v_fma_f32 %[acc0], s85, |v22|, %[acc0]\n"  \
-      "v_fma_f32 %[acc2], s85, |v23|, %[acc2]\n"  \
-      "v_sub_f32 v24, v62, v26\n"  \
-      "v_sub_f32 v25, v63, v27\n"  \
-      "v_fma_f32 %[acc1], s87, |v24|, %[acc1]\n"  \
-      "v_fma_f32 %[acc3], s87, |v25|, %[acc3]\n"  \
+      "v_sub_f32 v48, v96, v56\n"  \
+      "v_sub_f32 v49, v97, v57\n"  \
+      "v_sub_f32 v50, v98, v58\n"  \
+      "v_sub_f32 v51, v99, v59\n"  \
+      "v_fma_f32 %[acc0], s73, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s73, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s73, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s73, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v100, v56\n"  \
+      "v_sub_f32 v53, v101, v57\n"  \
+      "v_sub_f32 v54, v102, v58\n"  \
+      "v_sub_f32 v55, v103, v59\n"  \
+      "v_fma_f32 %[acc1], s75, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s75, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s75, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s75, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v104, v56\n"  \
+      "v_sub_f32 v49, v105, v57\n"  \
+      "v_sub_f32 v50, v106, v58\n"  \
+      "v_sub_f32 v51, v107, v59\n"  \
+      "v_fma_f32 %[acc0], s77, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s77, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s77, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s77, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v108, v56\n"  \
+      "v_sub_f32 v53, v109, v57\n"  \
+      "v_sub_f32 v54, v110, v58\n"  \
+      "v_sub_f32 v55, v111, v59\n"  \
+      "v_fma_f32 %[acc1], s79, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s79, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s79, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s79, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v112, v56\n"  \
+      "v_sub_f32 v49, v113, v57\n"  \
+      "v_sub_f32 v50, v114, v58\n"  \
+      "v_sub_f32 v51, v115, v59\n"  \
+      "v_fma_f32 %[acc0], s81, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s81, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s81, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s81, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v116, v56\n"  \
+      "v_sub_f32 v53, v117, v57\n"  \
+      "v_sub_f32 v54, v118, v58\n"  \
+      "v_sub_f32 v55, v119, v59\n"  \
+      "v_fma_f32 %[acc1], s83, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s83, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s83, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s83, |v55|, %[acc7]\n"  \
+      "v_sub_f32 v48, v120, v56\n"  \
+      "v_sub_f32 v49, v121, v57\n"  \
+      "v_sub_f32 v50, v122, v58\n"  \
+      "v_sub_f32 v51, v123, v59\n"  \
+      "v_fma_f32 %[acc0], s85, |v48|, %[acc0]\n"  \
+      "v_fma_f32 %[acc2], s85, |v49|, %[acc2]\n"  \
+      "v_fma_f32 %[acc4], s85, |v50|, %[acc4]\n"  \
+      "v_fma_f32 %[acc6], s85, |v51|, %[acc6]\n"  \
+      "v_sub_f32 v52, v124, v56\n"  \
+      "v_sub_f32 v53, v125, v57\n"  \
+      "v_sub_f32 v54, v126, v58\n"  \
+      "v_sub_f32 v55, v127, v59\n"  \
+      "v_fma_f32 %[acc1], s87, |v52|, %[acc1]\n"  \
+      "v_fma_f32 %[acc3], s87, |v53|, %[acc3]\n"  \
+      "v_fma_f32 %[acc5], s87, |v54|, %[acc5]\n"  \
+      "v_fma_f32 %[acc7], s87, |v55|, %[acc7]\n"  \
       "s_bitcmp1_b32 s73, 0\n"  \
       "s_cbranch_scc1 15f\n"  \
       "25:\n"  \
@@ -1927,97 +2563,121 @@
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 20b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 20b\n"  \
       "11:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 21b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 21b\n"  \
       "12:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 22b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 22b\n"  \
       "13:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 23b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 23b\n"  \
       "14:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 24b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 24b\n"  \
       "15:\n"  \
       "s_add_u32 s88, s88, 1\n"  \
       "s_cmp_ge_u32 s88, %[ncols]\n"  \
       "s_cbranch_scc1 8f\n"  \
       "s_waitcnt vmcnt(0)\n"  \
-      "v_mov_b32 v26, v28\n"  \
-      "v_mov_b32 v27, v29\n"  \
+      "v_mov_b32 v56, v60\n"  \
+      "v_mov_b32 v57, v61\n"  \
+      "v_mov_b32 v58, v62\n"  \
+      "v_mov_b32 v59, v63\n"  \
       "s_add_u32 s35, s88, 1\n"  \
       "s_cmp_ge_u32 s35, %[ncols]\n"  \
       "s_cbranch_scc1 25b\n"  \
       "s_add_u32 s90, s90, %[bstride]\n"  \
       "s_addc_u32 s91, s91, 0\n"  \
-      "global_load_dword v28, %[lane4], s[90:91]\n"  \
-      "global_load_dword v29, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v60, %[lane4], s[90:91]\n"  \
+      "global_load_dword v61, %[lane4], s[90:91] offset:256\n"  \
+      "global_load_dword v62, %[lane4], s[90:91] offset:512\n"  \
+      "global_load_dword v63, %[lane4], s[90:91] offset:768\n"  \
       "s_branch 25b\n"  \
       "8:\n"  \
       "s_waitcnt vmcnt(0) lgkmcnt(0)\n"  \
-      : [acc0] "+v"(acc[0]), [acc1] "+v"(acc[1]), [acc2] "+v"(acc[2]), [acc3] "+v"(acc[3])  \
+      : [acc0] "+v"(acc[0]), [acc1] "+v"(acc[1]), [acc2] "+v"(acc[2]), [acc3] "+v"(acc[3]), [acc4] "+v"(acc[4]), [acc5] "+v"(acc[5]), [acc6] "+v"(acc[6]), [acc7] "+v"(acc[7])  \
       : [lane16] "v"(lane16), [lane4] "v"(lane4), [eb] "s"(eb), [bp] "s"(bp),  \
         [bstride] "s"(bstride), [ncols] "s"(ncols)  \
-      : "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63",  \
+      : "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89", "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121", "v122", "v123", "v124", "v125", "v126", "v127",  \
         "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s65", "s66", "s67", "s68", "s69", "s70", "s71", "s72", "s73", "s74", "s75", "s76", "s77", "s78", "s79", "s80", "s81", "s82", "s83", "s84", "s85", "s86", "s87", "s88", "s89", "s90", "s91", "scc", "memory")
 
 
@@ -2076,10 +2736,10 @@ int main() {
   CHK(hipMalloc(&dout, (size_t)wgs * 1024 * 4));
   double g_total = 0;
   for (int b = 0; b < wgs; b++) for (int k = 0; k < tpw; k++) g_total += tile_groups[(b / 32 * tpw + k) % ntiles];
-  const char* nm[4] = {"F4 as shipped", "F2 8 waves/SIMD", "F2 scalar-cache hits", "F2 no LDS reads"};
+  const char* nm[4] = {"F4 as shipped", "F4 spread LDS issue", "F4 scalar-cache hits", "F4 no LDS reads"};
   for (int v = 0; v < 4; v++) {
-    auto K = v == 0 ? kern<0, 4> : v == 1 ? kern<1, 2> : v == 2 ? kern<2, 2> : kern<3, 2>;
-    const int F = v == 0 ? 4 : 2;
+    auto K = v == 0 ? kern<0, 4> : v == 1 ? kern<1, 4> : v == 2 ? kern<2, 4> : kern<3, 4>;
+    const int F = 4;
     hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
     float best = 1e30f;
     for (int rep = 0; rep < 4; rep++) {
