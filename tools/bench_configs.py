@@ -27,6 +27,8 @@ CONFIGS = {
     "cfg4": dict(algo="multisurf", n=20000, p=20000, R=100),
     "cfg5s": dict(algo="surf", n=10000, p=50000, R=100, star=True),
     "cfg5m": dict(algo="multisurf", n=10000, p=50000, R=100, star=True),
+    # SURF (no star) on cfg5's data: the sparse pass-2 choice for plain SURF
+    "cfg5surf": dict(algo="surf", n=10000, p=50000, R=100, star=False),
     # TuRF over MultiSURF on cfg2's data: device-resident re-targeting vs refits
     "turf2": dict(algo="turf", n=5000, p=5000, R=100),
     # TuRF over ReliefF (k=10) on cfg3's data

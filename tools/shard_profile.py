@@ -35,15 +35,25 @@ def main():
     isd = np.zeros(args.features, bool)
     n = args.samples
     stream = torch.cuda.current_stream().cuda_stream
+    # The exchanged vectors (row moments, neighbour counts) of the whole job,
+    # from a world-1 plan, stand in for the all-reduces: the rank's sparse
+    # pass 2 then sees the real pair weights.
+    rs_all = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
+    cn_all = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
+    sc = torch.zeros(args.features, dtype=torch.float64, device="cuda")
+    full = _lib.Plan("gpu", x, y, recip, isd, stream=stream)
+    full.pass1(rs_all.data_ptr())
+    full.select(rs_all.data_ptr(), cn_all.data_ptr())
+    torch.cuda.synchronize()
+    full.close()
     plan = _lib.Plan("gpu", x, y, recip, isd, rank=args.rank, world=args.world, stream=stream)
     rs = torch.zeros(3 * n, dtype=torch.float64, device="cuda")
     cn = torch.zeros(2 * n, dtype=torch.float64, device="cuda")
-    sc = torch.zeros(args.features, dtype=torch.float64, device="cuda")
 
     def step():
         plan.pass1(rs.data_ptr())
-        plan.select(rs.data_ptr(), cn.data_ptr())
-        plan.pass2(cn.data_ptr(), sc.data_ptr())
+        plan.select(rs_all.data_ptr(), cn.data_ptr())
+        plan.pass2(cn_all.data_ptr(), sc.data_ptr())
 
     step()
     torch.cuda.synchronize()
@@ -55,7 +65,7 @@ def main():
     tiles, _, refined = plan.info()
     print(json.dumps({"world": args.world, "rank": args.rank, "tiles": tiles, "step_ms": dt * 1e3,
                       "k_dist_ms": plan.kernel_ms(0), "k_score_ms": plan.kernel_ms(1),
-                      "refined": refined}))
+                      "refined": refined, "weighted_pairs": plan.weighted_pairs()}))
 
 
 if __name__ == "__main__":
