@@ -1984,15 +1984,20 @@ static int choose_q16(const Prepared& P) {
 }
 
 // Pass 2 on the non-zero pair weights only (k_weights_sparse +
-// k_score_sparse) unless nearly every pair carries a weight: SURF* weighs
-// every pair (near or far), so it keeps the dense kernel.  MultiSURF weighs
-// the ~42% of pairs near one of their samples, MultiSURF* ~62%, SURF ~60%;
-// row-sharded plans zero the non-owned sides.  FS_SPARSE=0/1 forces it.
-static int choose_sparse(const Prepared& P) {
+// k_score_sparse) or on every pair (k_weights + k_score).  The sparse loop
+// costs ~1.7x the dense one per evaluated pair (LDS row gather), so it pays
+// below ~58% density.  Measured (tools/bench_configs.py, one MI355X):
+// MultiSURF weighs the ~42% of pairs near one of their samples (cfg4 pass 2
+// 142 -> 103 ms sparse); MultiSURF* ~62% (cfg5 91 ms dense vs 102 sparse);
+// SURF about break-even (cfg5), SURF* weighs nearly every pair.  A
+// row-sharded SURF plan zeroes the sides of the samples it does not own, so
+// it goes sparse.  FS_SPARSE=0/1 forces either (tests).
+static int choose_sparse(const Plan* g, const Prepared& P) {
   if (P.algo == ALGO_RELIEFF) return 0;
   const char* env = std::getenv("FS_SPARSE");
   if (env && *env) return std::atoi(env) != 0 ? 1 : 0;
-  return (P.algo == ALGO_SURF && P.use_star) ? 0 : 1;
+  if (P.algo == ALGO_MULTISURF) return P.use_star ? 0 : 1;
+  return (g->r_hi - g->r_lo < P.n) ? 1 : 0;  // SURF / SURF*: only when row-sharded
 }
 
 // Feature-layout part of a plan: everything sized by the kept features
@@ -2145,7 +2150,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       (rc = dalloc(g, &g->tiles, g->n_tiles)) || (rc = dalloc(g, &g->thr, Q.n_pad)) ||
       (rc = dalloc(g, &g->list, g->list_cap)) || (rc = dalloc(g, &g->list_count, 1)))
     return fail(rc);
-  g->sparse = choose_sparse(Q);
+  g->sparse = choose_sparse(g, Q);
   if (Q.algo != ALGO_RELIEFF && !g->sparse &&
       (rc = dalloc(g, &g->Wt, (size_t)(g->n_tiles + 1) * kTile * kTile)))
     return fail(rc);

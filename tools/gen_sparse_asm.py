@@ -463,3 +463,147 @@ def gen12(name="FS_SPARSE_STREAM_ASM", spread=True, same_stream=False, no_ds=Fal
       : {vclob},  \\
         {sclob}, "scc", "memory")
 '''
+
+
+# ---------------------------------------------------------------------------
+# v3: entries staged through an LDS ring (LDS-DMA), no scalar loads in the loop
+# ---------------------------------------------------------------------------
+RING_DOC = """
+Stream layout (SoA groups): group = 16 dwords, rows' LDS byte offsets r0..r7
+then weights w0..w7; per stream a uint4 {group counts of columns 0-3 as bytes,
+of columns 4-7, total groups, 0}.  Each wave owns a 2 KB LDS ring (32 groups,
+two 1 KB halves) filled by LDS-DMA (global_load_lds_dwordx4: 16 groups per
+instruction) one half ahead; the entries reach VGPRs by wave-uniform
+ds_read_b128 (every lane the same 16 bytes), so every wait is an in-order
+counter: lgkmcnt for LDS (no scalar loads outstanding in the loop) and vmcnt
+for LDS-DMA and B.  Step g (unrolled x32: static ring offsets):
+  lgkmcnt(2)                  roffs of g+1 landed (weights of g may be in flight)
+  [g+2 starts a ring half: wait for its LDS-DMA]
+  8 x (v_add_u32, ds_read_b128)  rows of g+1
+  2 x ds_read_b128 roffs of g+2, 2 x ds_read_b128 weights of g+1
+  lgkmcnt(12)                 rows and weights of g landed
+  [g+1 starts a ring half: LDS-DMA of the half after next into the free half]
+  8 x 4 x (v_sub_f32 in place, v_fma_f32 w * |d|)   group g
+  column / stream bookkeeping in SALU (group counts from the stream's uint4)
+Fixed registers: v64..v127 two A sets, v48..v63 two roff sets, v32..v47 two
+weight sets, v24..v27 B, v28..v31 next B; s36..s50 (M0 saved in s46).
+"""
+
+
+def gen_ring(name="FS_SPARSE_RING_ASM", spread=False):
+    ASET = [64, 96]
+    RSET = [48, 56]
+    WSET = [32, 40]
+    BCUR, BNXT = 24, 28
+
+    def bload(dst):
+        return [f"global_load_dword v{dst + f}, %[lane4], s[38:39]" + (f" offset:{256 * f}" if f else "")
+                for f in range(4)]
+
+    def rows(g):
+        A, R = ASET[g % 2], RSET[g % 2]
+        adds = [f"v_add_u32 v{A + 4 * q}, v{R + q}, %[lane16]" for q in range(8)]
+        reads = [f"ds_read_b128 v[{A + 4 * q}:{A + 4 * q + 3}], v{A + 4 * q}" for q in range(8)]
+        return adds, reads
+
+    def entry_reads(g):
+        R, W = RSET[(g + 2) % 2], WSET[(g + 1) % 2]
+        ro = ((g + 2) % 32) * 64
+        wo = ((g + 1) % 32) * 64 + 32
+        return [f"ds_read_b128 v[{R}:{R + 3}], %[ringv] offset:{ro}",
+                f"ds_read_b128 v[{R + 4}:{R + 7}], %[ringv] offset:{ro + 16}",
+                f"ds_read_b128 v[{W}:{W + 3}], %[ringv] offset:{wo}",
+                f"ds_read_b128 v[{W + 4}:{W + 7}], %[ringv] offset:{wo + 16}"]
+
+    def compute_entry(g, q):
+        A, W = ASET[g % 2], WSET[g % 2]
+        L = [f"v_sub_f32 v{A + 4 * q + f}, v{A + 4 * q + f}, v{BCUR + f}" for f in range(4)]
+        for f in range(4):
+            acc = f"%[acc{2 * f + (q & 1)}]"
+            L.append(f"v_fma_f32 {acc}, v{W + q}, |v{A + 4 * q + f}|, {acc}")
+        return L
+
+    def dma(half_off):
+        return ([f"s_add_u32 s44, s47, {half_off}"] if half_off else ["s_mov_b32 s44, s47"]) + [
+            "s_mov_b32 m0, s44", "s_nop 0",
+            "global_load_lds_dwordx4 %[laneoff], s[36:37]",
+            "s_add_u32 s36, s36, 0x400", "s_addc_u32 s37, s37, 0"]
+
+    def step(x):
+        g = x
+        L = ["s_waitcnt lgkmcnt(2)"]
+        if (g + 2) % 16 == 0:   # g+2 opens a ring half: its LDS-DMA must have landed
+            L += ["s_cmp_eq_u32 s48, 0", f"s_cbranch_scc1 {100 + x}f", "s_waitcnt vmcnt(4)",
+                  f"s_branch {200 + x}f", f"{100 + x}:", "s_waitcnt vmcnt(0)", f"{200 + x}:"]
+        adds, reads = rows(g + 1)
+        if not spread:
+            for q in range(8):
+                L += [adds[q], reads[q]]
+            L += entry_reads(g)
+            L.append("s_waitcnt lgkmcnt(12)")
+        else:
+            raise NotImplementedError
+        if (g + 1) % 16 == 0:   # the half after next goes into the half g's group left
+            L += dma(0x400 if ((g + 1) // 16) % 2 == 0 else 0)
+            L += ["s_mov_b32 s48, 0", "s_add_u32 s49, s49, 1"]
+        for q in range(8):
+            L += compute_entry(g, q)
+        L += ["s_sub_u32 s40, s40, 1", "s_cmp_eq_u32 s40, 0", f"s_cbranch_scc1 {300 + x}f",
+              f"{400 + x}:",
+              "s_sub_u32 s41, s41, 1", "s_cmp_eq_u32 s41, 0", "s_cbranch_scc1 8f"]
+        return L
+
+    def switch(x):
+        return [f"{300 + x}:",
+                "s_and_b32 s40, s42, 0xff", "s_lshr_b64 s[42:43], s[42:43], 8",
+                "s_cmp_eq_u32 s49, 0", f"s_cbranch_scc1 {500 + x}f", "s_waitcnt vmcnt(1)",
+                f"s_branch {600 + x}f", f"{500 + x}:", "s_waitcnt vmcnt(0)", f"{600 + x}:",
+                *[f"v_mov_b32 v{BCUR + f}, v{BNXT + f}" for f in range(4)],
+                "s_cmp_eq_u32 s45, 0", f"s_cbranch_scc1 {400 + x}b",
+                "s_sub_u32 s45, s45, 1",
+                "s_add_u32 s38, s38, %[bstride]", "s_addc_u32 s39, s39, 0",
+                *bload(BNXT),
+                "s_add_u32 s48, s48, 4", "s_mov_b32 s49, 0",
+                f"s_branch {400 + x}b"]
+
+    lines = ["s_mov_b32 s46, m0",
+             "s_load_dwordx4 s[40:43], %[cb], 0x0",
+             "s_mov_b64 s[36:37], %[eb]", "s_mov_b64 s[38:39], %[bp]", "s_mov_b32 s47, %[ring]",
+             "s_waitcnt lgkmcnt(0)",
+             "s_mov_b32 s44, s42", "s_mov_b32 s42, s40", "s_mov_b32 s43, s41", "s_mov_b32 s41, s44",
+             "s_and_b32 s40, s42, 0xff", "s_lshr_b64 s[42:43], s[42:43], 8",
+             "s_mov_b32 s45, 6",
+             "s_cmp_eq_u32 s41, 0", "s_cbranch_scc1 9f"]
+    lines += dma(0) + dma(0x400)
+    lines += bload(BCUR) + ["s_add_u32 s38, s38, %[bstride]", "s_addc_u32 s39, s39, 0"] + bload(BNXT)
+    lines += ["s_mov_b32 s48, 8", "s_mov_b32 s49, 0", "s_waitcnt vmcnt(4)"]
+    R0 = RSET[0]
+    lines += [f"ds_read_b128 v[{R0}:{R0 + 3}], %[ringv] offset:0",
+              f"ds_read_b128 v[{R0 + 4}:{R0 + 7}], %[ringv] offset:16", "s_waitcnt lgkmcnt(0)"]
+    adds, reads = rows(0)
+    for q in range(8):
+        lines += [adds[q], reads[q]]
+    R1, W0 = RSET[1], WSET[0]
+    lines += [f"ds_read_b128 v[{R1}:{R1 + 3}], %[ringv] offset:64",
+              f"ds_read_b128 v[{R1 + 4}:{R1 + 7}], %[ringv] offset:80",
+              f"ds_read_b128 v[{W0}:{W0 + 3}], %[ringv] offset:32",
+              f"ds_read_b128 v[{W0 + 4}:{W0 + 7}], %[ringv] offset:48"]
+    lines.append("7:")
+    for x in range(32):
+        lines += step(x)
+    lines.append("s_branch 7b")
+    for x in range(32):
+        lines += switch(x)
+    lines += ["8:", "s_waitcnt vmcnt(0) lgkmcnt(0)", "9:", "s_mov_b32 m0, s46"]
+    body = "\n".join(f'      "{l}\\n"  \\' for l in lines)
+    vclob = ", ".join(f'"v{i}"' for i in range(24, 128))
+    sclob = ", ".join(f'"s{i}"' for i in range(36, 51))
+    return f'''#define {name}(acc_, lane16_, lane4_, laneoff_, ringv_, ring_, eb_, cb_, bp_, bstride_)  \\
+  asm volatile(  \\
+{body}
+      : {", ".join(f'[acc{i}] "+v"(acc_[{i}])' for i in range(8))}  \\
+      : [lane16] "v"(lane16_), [lane4] "v"(lane4_), [laneoff] "v"(laneoff_), [ringv] "v"(ringv_),  \\
+        [ring] "s"(ring_), [eb] "s"(eb_), [cb] "s"(cb_), [bp] "s"(bp_), [bstride] "s"(bstride_)  \\
+      : {vclob},  \\
+        {sclob}, "scc", "memory")
+'''
