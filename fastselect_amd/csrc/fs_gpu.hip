@@ -1823,6 +1823,10 @@ struct Plan {
   int x_is_f64 = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
+  // MultiSURF's mean correction (k_colrank, k_rowcorr) runs on `side`,
+  // forked after k_quantize and joined before k_rowstats_reduce, beside k_dist
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t nb = 0, n_tiles = 0, seg_len = 1, nseg = 1;
   int ksplit = 1;               // pass-1 K-split parts (k_dist)
   int use_q16 = 0;              // pass 1 on packed 16-bit continuous operands
@@ -1915,8 +1919,12 @@ void plan_destroy(Plan* g) {
   for (void* q : g->owned) (void)hipFree(q);
   for (void* q : g->owned_layout) (void)hipFree(q);
   for (void* q : g->scratch) (void)hipFree(q);
+  if (g->side) (void)hipStreamSynchronize(g->side);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
+  if (g->ev_fork) (void)hipEventDestroy(g->ev_fork);
+  if (g->ev_join) (void)hipEventDestroy(g->ev_join);
+  if (g->side) (void)hipStreamDestroy(g->side);
   if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
   delete g;
   trace_mark("plan: free");
@@ -1972,14 +1980,19 @@ static int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats,
 // score error it causes (pairs decided on the wrong side of a threshold, each
 // worth ~1/n^2) falls as ~n^-1.25 -- measured against the 32-bit path: 8.8e-6
 // scale-relative at n=5000, 3.9e-6 at 8192, 1.9e-6 at 20000 --
-// so MultiSURF takes them only from kQ16MinRowsMS samples on.  FS_Q16=0/1 in
+// so MultiSURF takes them only from kQ16MinRowsMS samples on.  MultiSURF*
+// is less sensitive (its far misses weigh the pairs between the two
+// thresholds both ways): 5.5e-7 at cfg4, 1.5e-6 at cfg5 (n = 10000,
+// p = 50000), so it takes them from kQ16MinRowsMSStar on.  FS_Q16=0/1 in
 // the environment forces the choice (tests).  SURF has its own float64 pass.
-constexpr int64_t kQ16MinRowsRF = 4096, kQ16MinRowsMS = 16384;
+constexpr int64_t kQ16MinRowsRF = 4096, kQ16MinRowsMS = 16384, kQ16MinRowsMSStar = 10000;
 static int choose_q16(const Prepared& P) {
   if (P.algo == ALGO_SURF) return 0;
   const char* env = std::getenv("FS_Q16");
   if (env && *env) return std::atoi(env) != 0 ? 1 : 0;
-  const int64_t min_rows = P.algo == ALGO_RELIEFF ? kQ16MinRowsRF : kQ16MinRowsMS;
+  const int64_t min_rows = P.algo == ALGO_RELIEFF ? kQ16MinRowsRF
+                           : P.use_star           ? kQ16MinRowsMSStar
+                                                  : kQ16MinRowsMS;
   return (P.n >= min_rows && P.pc >= kFeatPad) ? 1 : 0;
 }
 
@@ -2118,6 +2131,10 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   };
   for (auto& e : g->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(FS_EHIP);
+  if (hipStreamCreateWithFlags(&g->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&g->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&g->ev_join, hipEventDisableTiming) != hipSuccess)
+    return fail(FS_EHIP);
   const Prepared& Q = g->P;
   g->nb = Q.n_pad / kTile;
   std::vector<int32_t> bi, bj;
@@ -2218,15 +2235,20 @@ static int run_quantize_dist(Plan* g) {
   FS_TRY(launch_check("k_quantize"));
   if (Q.algo == ALGO_MULTISURF) {
     // mean correction of this rank's feature share (summed across ranks
-    // with the row moments)
+    // with the row moments), on the side stream beside k_dist: it reads
+    // xqT as k_dist does and writes only epsT / corr, which k_dist leaves
+    // alone; plan_pass1 joins it before k_rowstats_reduce reads corr
+    FS_HIP(hipEventRecord(g->ev_fork, g->stream));
+    FS_HIP(hipStreamWaitEvent(g->side, g->ev_fork, 0));
     if (g->c_hi > g->c_lo) {
-      k_colrank<<<(unsigned)(g->c_hi - g->c_lo), 256, 0, g->stream>>>(
+      k_colrank<<<(unsigned)(g->c_hi - g->c_lo), 256, 0, g->side>>>(
           g->xqT, Q.n, Q.n_pad, g->rank_shift, Q.q16, g->c_lo, g->epsT);
       FS_TRY(launch_check("k_colrank"));
     }
-    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, g->stream>>>(g->epsT, Q.n, Q.n_pad, g->c_lo,
-                                                                 g->c_hi, g->corr);
+    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, g->side>>>(g->epsT, Q.n, Q.n_pad, g->c_lo,
+                                                               g->c_hi, g->corr);
     FS_TRY(launch_check("k_rowcorr"));
+    FS_HIP(hipEventRecord(g->ev_join, g->side));
   }
   if (g->n_tiles > 0) {
     FS_HIP(hipEventRecord(g->ev[0], g->stream));
@@ -2348,6 +2370,7 @@ int plan_pass1(Plan* g, double* rowstats) {
                                                                  g->rspart);
     FS_TRY(launch_check("k_tile_rowstats"));
   }
+  FS_HIP(hipStreamWaitEvent(g->stream, g->ev_join, 0));  // corr (side stream)
   k_rowstats_reduce<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(
       g->rspart, Q.n, g->nb, g->rank, g->world, g->corr, rowstats);
   FS_TRY(launch_check("k_rowstats_reduce"));

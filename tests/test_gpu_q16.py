@@ -1,5 +1,6 @@
 """Pass 1 on packed 16-bit operands (Prepared::q16, v_sad_u16): the default
-for ReliefF from n = 4096 and for MultiSURF from n = 16384 samples.  Same bar
+for ReliefF from n = 4096, for MultiSURF from n = 16384 and for MultiSURF*
+from n = 10000 samples.  Same bar
 as every parity test: 1e-5 scale-relative and identical top-k.
 
 ReliefF is exact with them (the band of exactly recomputed keys widens), so
@@ -83,3 +84,21 @@ def test_q16_multisurf_mixed_default_at_16384(oracle):
     for star in (False, True):
         assert_parity(_fit(MultiSURF, X, y, use_star=star),
                       oracle.multisurf_scores(X, y, use_star=star), TOL, k=10)
+
+
+def test_q16_multisurf_star_default_at_10000(oracle, monkeypatch):
+    """MultiSURF* takes the 16-bit pass from n = 10000: against the oracle
+    (p = 96) and against the 32-bit path (p = 3000)."""
+    from fastselect_amd import MultiSURF
+    X, y = make_classification(n_samples=10000, n_features=96, n_informative=20,
+                               n_redundant=30, random_state=7)
+    assert_parity(_fit(MultiSURF, X, y, use_star=True),
+                  oracle.multisurf_scores(X, y, use_star=True), TOL, k=10)
+    X, y = make_classification(n_samples=10000, n_features=3000, n_informative=20,
+                               n_redundant=100, random_state=42)
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("FS_Q16", flag)
+        out[flag] = _fit(MultiSURF, X, y, use_star=True)
+    assert scale_rel_err(out["1"], out["0"]) < 5e-6
+    assert set(np.argsort(out["0"])[::-1][:10]) == set(np.argsort(out["1"])[::-1][:10])
