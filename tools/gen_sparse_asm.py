@@ -11,6 +11,17 @@ weight of the column's last group is set (every other weight has it clear;
 the 1-ulp change is far below the 1e-5 parity bar).  Lane l scores features
 f0 + l + 64k, k = 0..3, held in LDS as one float4 per row.
 
+feats=2, low=True (measured, not shipped): a 64 KB row block and <= 64
+VGPRs, so two 1024-thread workgroups share a CU (8 waves per SIMD).  On
+synthetic 42%-dense streams (tools/ubench/sparse_bench) it took 7.77 cycles
+per entry-feature against 8.68 for feats=4 at 4 waves per SIMD.  In
+k_score_sparse at cfg4 (profiles/ubench/r01k_*) VALU busy rose from 53.5% to
+64.6%, but the clock fell from 2.26 to 2.04 GHz (power) and the loop issues
+9% more VALU instructions per pair-feature (one address add per 2 features
+instead of per 4): 105.4 ms against 104.6, so feats=4 stays.  The register
+numbers below are those of feats=4; low=True maps the SGPRs as described at
+the remap.
+
 Pipeline per group g (unrolled x6: 3 SGPR sets x 2 A sets):
   s_waitcnt lgkmcnt(0)            A values of g (LDS) and entries of g+1 (SMEM) landed
   s_load_dwordx16                 entries of g+2 (stream offset += 64)
@@ -31,11 +42,12 @@ Fixed registers (clobbered; the compiler keeps its own values elsewhere):
   s88       column counter              s[90:91] B row pointer
 """
 import os
+import re
 
 SETS = [40, 56, 72]
 
 
-def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, spread=True):
+def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, spread=True, low=False):
     """Macro text.  feats: features per lane (4: 128 KB LDS block, float4 rows;
     2: 64 KB, float2 rows, 64-VGPR budget).  no_ds / same_stream:
     microbenchmark variants that skip the LDS reads / keep re-reading the
@@ -150,10 +162,33 @@ def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, sp
     lines.append("8:")
     lines.append("s_waitcnt vmcnt(0) lgkmcnt(0)")
 
+    # low: the fixed SGPRs moved below s72 (reserved at 8 waves/SIMD), around
+    # s32/s33 (the ABI's stack and frame pointers): entry sets at s16, s36,
+    # s52; stream base s[12:13], column counter s14, s15; offset s68,
+    # temporary s69, B row pointer s[70:71].  The compiler keeps s0..s11.
+    remap = {}
+    if low:
+        for k, base in enumerate((16, 36, 52)):
+            for i in range(16):
+                remap[SETS[k] + i] = base + i
+        remap.update({34: 68, 35: 69, 36: 12, 37: 13, 88: 14, 89: 15, 90: 70, 91: 71})
+
+        def sub(m):
+            lo, hi = int(m.group(1)), m.group(2)
+            if lo not in remap:
+                return m.group(0)
+            return f"s[{remap[lo]}:{remap[int(hi)]}]" if hi else f"s{remap[lo]}"
+        lines = [re.sub(r"(?<![a-z_])s\[?(\d+)(?::(\d+)\])?", sub, l) for l in lines]
     body = "\n".join(f'      "{l}\\n"  \\' for l in lines)
     vclob = ", ".join(f'"v{i}"' for i in range(VLO, ASETS[1] + 8 * F))
     nacc = 2 * F
-    sclob = ", ".join(f'"s{i}"' for i in range(34, 92))
+    # low: clobber only the SGPRs the loop names (the compiler has few left)
+    named = set()
+    for l in lines:
+        for lo, hi in re.findall(r"(?<![a-z_])s\[?(\d+)(?::(\d+)\])?", l):
+            named.update(range(int(lo), int(hi or lo) + 1))
+    sregs = sorted(named & set(remap.values())) if low else range(34, 92)
+    sclob = ", ".join(f'"s{i}"' for i in sregs)
     return f'''#define {name}(acc, lane16, lane4, eb, bp, bstride, ncols)  \\
   asm volatile(  \\
 {body}

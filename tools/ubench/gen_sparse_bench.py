@@ -8,7 +8,7 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from gen_sparse_asm import gen  # noqa: E402
 
-VARIANTS = [dict(), dict(spread=True), dict(same_stream=True), dict(no_ds=True)]
+VARIANTS = [dict(), dict(spread=True), dict(same_stream=True), dict(no_ds=True), dict(feats=2, low=True), dict(feats=2, same_stream=True, low=True)]
 src = ["#include <hip/hip_runtime.h>", "#include <cstdio>", "#include <cstdlib>", "#include <cstdint>",
        "#include <cstring>", "#include <vector>", "#include <random>", "#include <algorithm>",
        '#define CHK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)']
@@ -31,10 +31,12 @@ void kern(const uint2* ent, const float* xs, int PW, int ntiles, int tiles_per_w
     const int t = __builtin_amdgcn_readfirstlane((int)((blockIdx.x / 32 * tiles_per_wg + k) % ntiles));
     const uint64_t eb = (uint64_t)(uintptr_t)(ent + ((int64_t)t * kSWaves + wave) * kStreamGroups * 8);
     const uint64_t bp = (uint64_t)(uintptr_t)(xs + (int64_t)wave * PW);
-    if (V == 0) STREAM0(acc, lane16, lane4, eb, bp, bstride, ncols);
-    if (V == 1) STREAM1(acc, lane16, lane4, eb, bp, bstride, ncols);
-    if (V == 2) STREAM2(acc, lane16, lane4, eb, bp, bstride, ncols);
-    if (V == 3) STREAM3(acc, lane16, lane4, eb, bp, bstride, ncols);
+    if constexpr (V == 0) STREAM0(acc, lane16, lane4, eb, bp, bstride, ncols);
+    if constexpr (V == 1) STREAM1(acc, lane16, lane4, eb, bp, bstride, ncols);
+    if constexpr (V == 2) STREAM2(acc, lane16, lane4, eb, bp, bstride, ncols);
+    if constexpr (V == 3) STREAM3(acc, lane16, lane4, eb, bp, bstride, ncols);
+    if constexpr (V == 4) STREAM4(acc, lane16, lane4, eb, bp, bstride, ncols);
+    if constexpr (V == 5) STREAM5(acc, lane16, lane4, eb, bp, bstride, ncols);
   }
   out[blockIdx.x * 1024 + threadIdx.x] = acc[0] + acc[1] + acc[2] + acc[3] + acc[4] + acc[5] + acc[6] + acc[7];
 }
@@ -70,10 +72,10 @@ int main() {
   CHK(hipMalloc(&dout, (size_t)wgs * 1024 * 4));
   double g_total = 0;
   for (int b = 0; b < wgs; b++) for (int k = 0; k < tpw; k++) g_total += tile_groups[(b / 32 * tpw + k) % ntiles];
-  const char* nm[4] = {"F4 as shipped", "F4 spread LDS issue", "F4 scalar-cache hits", "F4 no LDS reads"};
-  for (int v = 0; v < 4; v++) {
-    auto K = v == 0 ? kern<0, 4> : v == 1 ? kern<1, 4> : v == 2 ? kern<2, 4> : kern<3, 4>;
-    const int F = 4;
+  const char* nm[6] = {"F4 as shipped", "F4 spread LDS issue", "F4 scalar-cache hits", "F4 no LDS reads", "F2 8 waves/SIMD", "F2 scalar-cache hits"};
+  for (int v = 0; v < 6; v++) {
+    auto K = v == 0 ? kern<0, 4> : v == 1 ? kern<1, 4> : v == 2 ? kern<2, 4> : v == 3 ? kern<3, 4> : v == 4 ? kern<4, 2> : kern<5, 2>;
+    const int F = v >= 4 ? 2 : 4;
     hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
     float best = 1e30f;
     for (int rep = 0; rep < 4; rep++) {
@@ -84,7 +86,7 @@ int main() {
       if (rep && ms < best) best = ms;
     }
     CHK(hipGetLastError());
-    const double gt = v == 2 ? (double)wgs * tpw * kSWaves * 130 : g_total;  // same_stream: ~130 groups per stream
+    const double gt = (v == 2 || v == 5) ? (double)wgs * tpw * kSWaves * 130 : g_total;  // same_stream: ~130 groups per stream
     const double valu_ms = gt * (F == 4 ? 80 : 40) * 2 / 1024.0 / 2.4e9 * 1e3;
     // per-feature normalisation: cycles per entry-feature
     printf("%-22s %8.3f ms   groups %.3g  cycles/group/SIMD %.1f  per entry-feature %.2f  (VALU floor %.3f ms = %.0f%%)\n", nm[v], best,
