@@ -2048,9 +2048,16 @@ static int plan_layout(Plan* g) {
   }
   g->c_lo = Q.pc * g->rank / g->world;
   g->c_hi = Q.pc * (g->rank + 1) / g->world;
-  const int64_t nfb = (Q.PW + 127) / 128;
-  // ~64k pass-2 workgroups: enough to fill 256 CUs and bound tail imbalance.
-  g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + 65535) / 65536);
+  // ~64k pass-2 workgroups (dense: 128-feature blocks, sparse: 256): enough
+  // to fill 256 CUs and bound tail imbalance.  Measured for the sparse pass
+  // at cfg4 (tools/pass2_wgs.sh, k_score_sparse ms at world 1 / one rank of
+  // 8): 8k 111.8 / 14.7, 16k 105.9 / 14.6, 32k 104.4 / 14.6, 64k 104.0 /
+  // 14.3, 128k 104.4 / 15.1 -- the tail costs more than the per-workgroup
+  // row-block stage.
+  const int64_t nfb = g->sparse ? (Q.PW + 255) / 256 : (Q.PW + 127) / 128;
+  int64_t wgs = 65536;
+  if (const char* e = std::getenv("FS_PASS2_WGS")) wgs = std::max<int64_t>(256, std::atoll(e));
+  g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + wgs - 1) / wgs);
   g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
   // histogram shift so that the largest quantised value lands in bin < 4096
   g->rank_shift = 0;
