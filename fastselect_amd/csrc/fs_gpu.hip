@@ -867,6 +867,56 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
   }
 }
 
+// k_exact_pairs for the common layout -- every kept feature continuous, in
+// input order (src_col = identity), float32 X with a 16-byte row pitch --
+// reading both rows as float4 (16 B per lane, 4 KB per wave per row and
+// step, 8 loads in flight per lane) instead of a column-indexed dword
+// gather.  Same arithmetic per feature: f32 |a - b| * f32 recip, summed in
+// f64.  The list is sorted by (i, j), so consecutive waves share row i
+// through L2; row j is the HBM read.
+__global__ __launch_bounds__(256) void k_exact_pairs_rows(
+    const float* __restrict__ x, int64_t p, const float* __restrict__ scl32, double sc,
+    const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
+    int64_t n_pad, double* __restrict__ D) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
+  const int64_t total = (int64_t)*count < cap ? (int64_t)*count : cap;
+  const int64_t p4 = p / 4;
+  const float4* __restrict__ s4 = (const float4*)scl32;
+  for (int64_t k = wave; k < total; k += nw) {
+    const int2 pr = list[k];
+    const float4* __restrict__ xi = (const float4*)(x + (int64_t)pr.x * p);
+    const float4* __restrict__ xj = (const float4*)(x + (int64_t)pr.y * p);
+    double acc = 0.0;
+    constexpr int kU = 4;
+    for (int64_t c0 = lane; c0 < p4; c0 += 64 * kU) {
+      float4 a[kU], b[kU], w[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const int64_t c = c0 + 64 * u;
+        const bool in = c < p4;
+        a[u] = in ? xi[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        b[u] = in ? xj[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        w[u] = in ? s4[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        acc += (double)(__builtin_fabsf(a[u].x - b[u].x) * w[u].x);
+        acc += (double)(__builtin_fabsf(a[u].y - b[u].y) * w[u].y);
+        acc += (double)(__builtin_fabsf(a[u].z - b[u].z) * w[u].z);
+        acc += (double)(__builtin_fabsf(a[u].w - b[u].w) * w[u].w);
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) {
+      const double v = acc * sc;
+      D[(int64_t)pr.x * n_pad + pr.y] = v;
+      D[(int64_t)pr.y * n_pad + pr.x] = v;
+    }
+  }
+}
+
 // Near hit / miss counts over the owned tiles (D now exact for ambiguous
 // pairs): counts[2i], counts[2i+1].
 __global__ __launch_bounds__(256) void k_tile_counts(const double* __restrict__ D, int64_t n,
@@ -1840,6 +1890,8 @@ struct Plan {
   int64_t* src_col = nullptr;
   int64_t* out_pos = nullptr;
   double *off = nullptr, *qs = nullptr, *scl = nullptr;
+  float* scl32 = nullptr;       // scl as float (k_exact_pairs_rows)
+  bool rows_direct = false;     // kept features = X's columns, all continuous, f32, 16-B pitch
   int64_t* dtab_off = nullptr;
   double* dtab = nullptr;
   int32_t* lab = nullptr;
@@ -2048,14 +2100,16 @@ static int plan_layout(Plan* g) {
   }
   g->c_lo = Q.pc * g->rank / g->world;
   g->c_hi = Q.pc * (g->rank + 1) / g->world;
-  // ~64k pass-2 workgroups (dense: 128-feature blocks, sparse: 256): enough
-  // to fill 256 CUs and bound tail imbalance.  Measured for the sparse pass
-  // at cfg4 (tools/pass2_wgs.sh, k_score_sparse ms at world 1 / one rank of
-  // 8): 8k 111.8 / 14.7, 16k 105.9 / 14.6, 32k 104.4 / 14.6, 64k 104.0 /
-  // 14.3, 128k 104.4 / 15.1 -- the tail costs more than the per-workgroup
-  // row-block stage.
+  // Pass-2 workgroups: ~64k for the dense pass (256 threads, 128-feature
+  // blocks), ~32k for the sparse one (1024 threads, 256-feature blocks):
+  // enough to fill 256 CUs and bound tail imbalance.  Measured for the sparse
+  // pass at cfg4 (tools/pass2_wgs.sh, k_score_sparse ms at world 1 / one rank
+  // of 8; profiles/r01k/pass2_wgs.txt): 8k 111.8 / 14.7, 16k 105.9 / 14.6,
+  // then on one box, alternating, 32k 107.6 / 14.9 and 107.7 / 14.6 against
+  // 64k 108.1 / 15.0 and 108.0 / 14.6 -- the tail costs more than the
+  // per-workgroup row-block stage below 32k.
   const int64_t nfb = g->sparse ? (Q.PW + 255) / 256 : (Q.PW + 127) / 128;
-  int64_t wgs = 65536;
+  int64_t wgs = g->sparse ? 32768 : 65536;
   if (const char* e = std::getenv("FS_PASS2_WGS")) wgs = std::max<int64_t>(256, std::atoll(e));
   g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + wgs - 1) / wgs);
   g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
@@ -2066,7 +2120,8 @@ static int plan_layout(Plan* g) {
   rc = FS_OK;
   if ((rc = dalloc(g, &g->src_col, Q.PW)) || (rc = dalloc(g, &g->out_pos, Q.PW)) ||
       (rc = dalloc(g, &g->off, Q.PW)) || (rc = dalloc(g, &g->qs, Q.PW)) ||
-      (rc = dalloc(g, &g->scl, Q.PW)) || (rc = dalloc(g, &g->dtab_off, Q.PW + 1)) ||
+      (rc = dalloc(g, &g->scl, Q.PW)) || (rc = dalloc(g, &g->scl32, Q.PW)) ||
+      (rc = dalloc(g, &g->dtab_off, Q.PW + 1)) ||
       (rc = dalloc(g, &g->dtab, Q.dtab.size())) ||
       (rc = dalloc(g, &g->xs, (size_t)(Q.n_pad + 2) * Q.PW))) {
   } else if (Q.algo == ALGO_SURF) {
@@ -2079,10 +2134,15 @@ static int plan_layout(Plan* g) {
   if (rc) return rc;
   std::vector<double> qs(Q.PW, 0.0);
   for (int64_t c = 0; c < Q.PW; c++) qs[c] = Q.scale[c] * Q.SC;
+  std::vector<float> scl32(Q.PW, 0.0f);
+  for (int64_t c = 0; c < Q.PW; c++) scl32[c] = (float)Q.scale[c];
+  g->rows_direct = !g->x_is_f64 && Q.pd == 0 && Q.pc == Q.p_in && Q.p_in % 4 == 0;
+  for (int64_t c = 0; g->rows_direct && c < Q.pc; c++) g->rows_direct = Q.src_col[c] == c;
   if ((rc = h2d(g, g->src_col, Q.src_col.data(), Q.PW)) ||
       (rc = h2d(g, g->out_pos, Q.out_pos.data(), Q.PW)) ||
       (rc = h2d(g, g->off, Q.offset.data(), Q.PW)) || (rc = h2d(g, g->qs, qs.data(), Q.PW)) ||
       (rc = h2d(g, g->scl, Q.scale.data(), Q.PW)) ||
+      (rc = h2d(g, g->scl32, scl32.data(), Q.PW)) ||
       (rc = h2d(g, g->dtab_off, Q.dtab_off.data(), Q.PW + 1)) ||
       (rc = h2d(g, g->dtab, Q.dtab.data(), Q.dtab.size())))
     return rc;
@@ -2317,7 +2377,11 @@ static int refine_pairs(Plan* g, int algo, double delta) {
   if (g->n_refined == 0) return FS_OK;
   FS_TRY(sort_pair_list(g, g->n_refined));
   const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
-  if (g->x_is_f64)
+  if (g->rows_direct && !std::getenv("FS_EXACT_GATHER"))
+    k_exact_pairs_rows<<<grid, 256, 0, g->stream>>>((const float*)g->x, Q.p_in, g->scl32, Q.SC,
+                                                    g->list, g->list_count, g->list_cap, Q.n_pad,
+                                                    g->D);
+  else if (g->x_is_f64)
     k_exact_pairs<double><<<grid, 256, 0, g->stream>>>(
         (const double*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
         g->list_count, g->list_cap, Q.n_pad, 0, g->D);

@@ -452,6 +452,30 @@ def test_sparse_pass2_matches_dense(monkeypatch, algo, star):
     assert_parity(out["1"], ref, TOL, k=10)
 
 
+def test_exact_pairs_row_reads_match_gather(monkeypatch):
+    """k_exact_pairs_rows (float4 reads of whole rows, all-continuous
+    float32 data in input order) against the column-indexed gather
+    (FS_EXACT_GATHER forces it): the 16-bit pass 1 (FS_Q16=1) refines
+    hundreds of pairs here; 1500 features is not a multiple of 256.
+    Both refine the same pairs, so the scores agree to f64 summation order."""
+    from fastselect_amd.parallel import ShardedMultiSURF
+    X, y = make_classification(n_samples=1200, n_features=1500, n_informative=20,
+                               n_redundant=40, random_state=11)
+    x = X.astype(np.float32)
+    recip = (1 / (x.max(0) - x.min(0))).astype(np.float32)
+    monkeypatch.setenv("FS_Q16", "1")
+    out = {}
+    for mode in ("rows", "gather"):
+        if mode == "gather":
+            monkeypatch.setenv("FS_EXACT_GATHER", "1")
+        job = ShardedMultiSURF(x, y, recip, np.zeros(x.shape[1], bool), backend="gpu", device=0)
+        out[mode] = job.step().cpu().numpy()
+        refined = job.info()[2]
+        job.close()
+        assert refined > 200
+    assert scale_rel_err(out["rows"], out["gather"]) <= 1e-7
+
+
 def test_sparse_weighted_pairs_count():
     """fs_plan_weighted_pairs: MultiSURF weighs the pairs near one of their two
     samples (~40% here); the count is exact against a numpy restatement."""
