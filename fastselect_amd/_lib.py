@@ -35,7 +35,8 @@ _vp = ctypes.c_void_p
 
 # every symbol include/fastselect_amd.h declares (checked by tests/test_abi.py)
 EXPORTED = (
-    "fs_version", "fs_last_error", "fs_device_count", "fs_column_stats", "fs_multisurf_score",
+    "fs_version", "fs_last_error", "fs_device_count", "fs_device_cache_release",
+    "fs_column_stats", "fs_multisurf_score",
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2",
@@ -69,6 +70,7 @@ def _load() -> ctypes.CDLL:
     lib.fs_version.restype = ctypes.c_char_p
     lib.fs_last_error.restype = ctypes.c_char_p
     lib.fs_device_count.restype = _int
+    lib.fs_device_cache_release.restype = _int
     lib.fs_column_stats.argtypes = [_int, _int, _vp, _int, _i64, _i64, _i64, _vp, _vp, _i64p]
     lib.fs_multisurf_score.argtypes = [_int, _int, _f32p, _i64, _i64, _f64p, _f32p, _i64p, _i64,
                                        _int, _u8p, _int, _f32p]
@@ -116,6 +118,11 @@ def lib() -> ctypes.CDLL:
 
 def version() -> str:
     return _lib.fs_version().decode()
+
+
+def release_device_cache() -> None:
+    """Free the device blocks kept between fits (fs_device_cache_release)."""
+    _lib.fs_device_cache_release()
 
 
 def device_count() -> int:

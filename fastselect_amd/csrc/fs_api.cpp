@@ -63,6 +63,11 @@ const char* fs_last_error(void) { return g_last_error.c_str(); }
 
 int fs_device_count(void) { return gpu::device_count(); }
 
+int fs_device_cache_release(void) {
+  gpu::dev_cache_release();
+  return FS_OK;
+}
+
 int fs_column_stats(int backend, int device, const void* x, int x_is_f64, int64_t n, int64_t p,
                     int64_t count_cap, void* colmin_out, void* colmax_out,
                     int64_t* ndistinct_out) {

@@ -147,12 +147,14 @@ int column_minmax(const void* dx, int x_is_f64, int64_t n, int64_t p, void* hmin
   minmax_grid(n, rows_per_chunk, nchunks);
   void* buf = nullptr;  // [nchunks][p] min, [nchunks][p] max, [p] min, [p] max
   const size_t part = (size_t)nchunks * p * esz;
-  hipError_t e = hipMalloc(&buf, 2 * part + 2 * (size_t)p * esz);
-  if (e != hipSuccess) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
     (void)hipGetLastError();
-    set_error(std::string("hipMalloc (column ranges): ") + hipGetErrorString(e));
-    return FS_EOOM;
+    set_error("column ranges: hipGetDevice failed");
+    return FS_EHIP;
   }
+  if (int rc = dev_alloc(&buf, 2 * part + 2 * (size_t)p * esz, dev)) return rc;
+  hipError_t e;
   char* b = (char*)buf;
   launch_minmax(dx, x_is_f64, n, p, rows_per_chunk, nchunks, b, b + part, b + 2 * part,
                 b + 2 * part + p * esz, s);
@@ -162,7 +164,7 @@ int column_minmax(const void* dx, int x_is_f64, int64_t n, int64_t p, void* hmin
   if (e == hipSuccess)
     e = hipMemcpyAsync(hmax, b + 2 * part + p * esz, (size_t)p * esz, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
-  (void)hipFree(buf);
+  dev_free(buf);
   if (e != hipSuccess) {
     (void)hipGetLastError();
     set_error(std::string("column ranges: ") + hipGetErrorString(e));
@@ -200,14 +202,12 @@ int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap,
   if ((e = hipSetDevice(device)) != hipSuccess) fail("hipSetDevice", e);
   if (rc == FS_OK && (e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess)
     fail("hipStreamCreate", e);
-  if (rc == FS_OK && (e = hipMalloc(&dx, (size_t)n * p * esz)) != hipSuccess) fail("hipMalloc", e);
-  if (rc == FS_OK && (e = hipMalloc(&pmin, (size_t)nchunks * p * esz)) != hipSuccess)
-    fail("hipMalloc", e);
-  if (rc == FS_OK && (e = hipMalloc(&pmax, (size_t)nchunks * p * esz)) != hipSuccess)
-    fail("hipMalloc", e);
-  if (rc == FS_OK && (e = hipMalloc(&dmin, (size_t)p * esz)) != hipSuccess) fail("hipMalloc", e);
-  if (rc == FS_OK && (e = hipMalloc(&dmax, (size_t)p * esz)) != hipSuccess) fail("hipMalloc", e);
-  if (rc == FS_OK && (e = hipMalloc(&dcnt, (size_t)p * 8)) != hipSuccess) fail("hipMalloc", e);
+  if (rc == FS_OK) rc = dev_alloc((void**)&dx, (size_t)n * p * esz, device);
+  if (rc == FS_OK) rc = dev_alloc((void**)&pmin, (size_t)nchunks * p * esz, device);
+  if (rc == FS_OK) rc = dev_alloc((void**)&pmax, (size_t)nchunks * p * esz, device);
+  if (rc == FS_OK) rc = dev_alloc((void**)&dmin, (size_t)p * esz, device);
+  if (rc == FS_OK) rc = dev_alloc((void**)&dmax, (size_t)p * esz, device);
+  if (rc == FS_OK) rc = dev_alloc((void**)&dcnt, (size_t)p * 8, device);
   if (rc == FS_OK &&
       (e = hipMemcpyAsync(dx, x, (size_t)n * p * esz, hipMemcpyHostToDevice, s)) != hipSuccess)
     fail("hipMemcpy H2D", e);
@@ -233,7 +233,7 @@ int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap,
   if (rc == FS_OK && (e = hipStreamSynchronize(s)) != hipSuccess) fail("column statistics", e);
   if (s) (void)hipStreamSynchronize(s);
   for (void* q : {dx, pmin, pmax, dmin, dmax, (void*)dcnt})
-    if (q) (void)hipFree(q);
+    if (q) dev_free(q);
   if (s) (void)hipStreamDestroy(s);
   return rc;
 }

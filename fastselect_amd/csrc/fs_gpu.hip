@@ -29,7 +29,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <map>
+#include <mutex>
 #include <type_traits>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/fastselect_amd.h"
@@ -1925,17 +1928,122 @@ struct Plan {
   std::vector<char> colmin, colmax; // per input column, x's dtype (device-measured)
 };
 
+// ---------------------------------------------------------------------------
+// Device block cache
+// ---------------------------------------------------------------------------
+// hipMalloc of the ~11 GB a cfg4 plan holds took 190-310 ms per fit on the
+// MI355X (fresh pages are mapped on allocation; tools/fit_breakdown.py) --
+// more than the scoring.  Blocks that plans and the column statistics free
+// are kept per device up to a cap (a quarter of the device's memory;
+// FS_DEVICE_CACHE_MB overrides, 0 disables) and handed to the next request
+// they cover within 2x, so repeated fits (TuRF refits, CV folds, benchmarks)
+// skip the mapping.  A failed hipMalloc releases the device's cache and
+// retries; fs_device_cache_release() returns everything.  Callers free a
+// block only after the streams that use it are synchronised, and every
+// consumer writes or clears what it reads (blocks come back with stale data).
+namespace {
+struct Block {
+  size_t bytes;
+  int device;
+  bool cached;
+};
+std::mutex cache_mu;
+std::unordered_map<void*, Block> blocks;             // every block handed out or cached
+std::multimap<std::pair<int, size_t>, void*> cache;  // (device, bytes) -> cached block
+std::map<int, size_t> cache_bytes;
+
+size_t cache_cap(int device) {  // with cache_mu held
+  static long long env_mb = -2;
+  if (env_mb == -2) {
+    const char* e = std::getenv("FS_DEVICE_CACHE_MB");
+    env_mb = (e && *e) ? std::max(0LL, std::atoll(e)) : -1;
+  }
+  if (env_mb >= 0) return (size_t)env_mb << 20;
+  static std::map<int, size_t> total;
+  auto it = total.find(device);
+  if (it == total.end()) {
+    size_t t = 0;
+    if (hipDeviceTotalMem(&t, device) != hipSuccess) {
+      (void)hipGetLastError();
+      t = 0;
+    }
+    it = total.emplace(device, t).first;
+  }
+  return it->second / 4;
+}
+
+void release_device(int device) {  // with cache_mu held; device < 0: all
+  for (auto it = cache.begin(); it != cache.end();) {
+    if (device >= 0 && it->first.first != device) {
+      ++it;
+      continue;
+    }
+    (void)hipFree(it->second);
+    blocks.erase(it->second);
+    cache_bytes[it->first.first] -= it->first.second;
+    it = cache.erase(it);
+  }
+}
+}  // namespace
+
+int dev_alloc(void** out, size_t bytes, int device) {
+  if (bytes == 0) bytes = 1;
+  std::lock_guard<std::mutex> lk(cache_mu);
+  auto it = cache.lower_bound({device, bytes});
+  if (it != cache.end() && it->first.first == device && it->first.second <= 2 * bytes) {
+    *out = it->second;
+    cache_bytes[device] -= it->first.second;
+    blocks[it->second].cached = false;
+    cache.erase(it);
+    return FS_OK;
+  }
+  hipError_t e = hipMalloc(out, bytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    release_device(device);
+    e = hipMalloc(out, bytes);
+  }
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    set_error(std::string("hipMalloc of ") + std::to_string(bytes) +
+              " bytes failed: " + hipGetErrorString(e));
+    return FS_EOOM;
+  }
+  blocks[*out] = Block{bytes, device, false};
+  return FS_OK;
+}
+
+void dev_free(void* p) {
+  if (!p) return;
+  std::lock_guard<std::mutex> lk(cache_mu);
+  auto it = blocks.find(p);
+  if (it == blocks.end()) {
+    (void)hipFree(p);
+    return;
+  }
+  Block& b = it->second;
+  if (!b.cached && cache_bytes[b.device] + b.bytes <= cache_cap(b.device)) {
+    b.cached = true;
+    cache.emplace(std::make_pair(b.device, b.bytes), p);
+    cache_bytes[b.device] += b.bytes;
+    return;
+  }
+  if (!b.cached) {
+    blocks.erase(it);
+    (void)hipFree(p);
+  }
+}
+
+void dev_cache_release() {
+  std::lock_guard<std::mutex> lk(cache_mu);
+  release_device(-1);
+}
+
 template <typename T>
 static int dalloc(Plan* g, T** p, size_t count) {
   void* q = nullptr;
   if (count == 0) count = 1;
-  hipError_t e = hipMalloc(&q, count * sizeof(T));
-  if (e != hipSuccess) {
-    (void)hipGetLastError();
-    set_error(std::string("hipMalloc of ") + std::to_string(count * sizeof(T)) +
-              " bytes failed: " + hipGetErrorString(e));
-    return FS_EOOM;
-  }
+  if (int rc = dev_alloc(&q, count * sizeof(T), g->device)) return rc;
   (g->alloc_target == 1 ? g->owned_layout : g->alloc_target == 2 ? g->scratch : g->owned)
       .push_back(q);
   *p = (T*)q;
@@ -1968,10 +2076,10 @@ void plan_destroy(Plan* g) {
   if (!g) return;
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   trace_mark("kernels (to sync)");
-  for (void* q : g->owned) (void)hipFree(q);
-  for (void* q : g->owned_layout) (void)hipFree(q);
-  for (void* q : g->scratch) (void)hipFree(q);
   if (g->side) (void)hipStreamSynchronize(g->side);
+  for (void* q : g->owned) dev_free(q);
+  for (void* q : g->owned_layout) dev_free(q);
+  for (void* q : g->scratch) dev_free(q);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
   if (g->ev_fork) (void)hipEventDestroy(g->ev_fork);
@@ -2071,7 +2179,8 @@ static int choose_sparse(const Plan* g, const Prepared& P) {
 static int plan_layout(Plan* g) {
   Prepared& Q = g->P;
   FS_HIP(hipStreamSynchronize(g->stream));
-  for (void* q : g->owned_layout) (void)hipFree(q);
+  if (g->side) FS_HIP(hipStreamSynchronize(g->side));
+  for (void* q : g->owned_layout) dev_free(q);
   g->owned_layout.clear();
   int rc;
   Q.q16 = g->use_q16;
@@ -2763,7 +2872,7 @@ int plan_score(Plan* g, double* sums_dev) {
     return FS_EINVAL;
   }
   if (hipStreamSynchronize(g->stream) != hipSuccess && rc == FS_OK) rc = FS_EHIP;
-  for (void* q : g->scratch) (void)hipFree(q);
+  for (void* q : g->scratch) dev_free(q);
   g->scratch.clear();
   return rc;
 }

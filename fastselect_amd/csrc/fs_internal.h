@@ -261,6 +261,13 @@ int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap,
 // ---- GPU backend ---------------------------------------------------------
 namespace gpu {
 int device_count();
+// Device block cache (fs_gpu.hip): dev_alloc hands out a cached block of
+// `device` that covers `bytes` (within 2x) or a fresh hipMalloc; dev_free
+// keeps the block for the next request (up to the cache cap) or frees it.
+// Blocks come back with stale contents.  Returns FS_OK / FS_EOOM.
+int dev_alloc(void** p, size_t bytes, int device);
+void dev_free(void* p);
+void dev_cache_release();
 int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap, int device,
                  void* colmin, void* colmax, int64_t* ndistinct);
 // Column minima / maxima of a device-resident X, copied to host arrays in

@@ -34,6 +34,7 @@ def test_version_and_device_count():
     from fastselect_amd import _lib
     assert "fastselect_amd" in _lib.version()
     assert _lib.device_count() >= 0
+    _lib.release_device_cache()  # nothing cached (or no device): a no-op
 
 
 def test_gpu_backend_without_device_is_an_error():

@@ -476,6 +476,23 @@ def test_exact_pairs_row_reads_match_gather(monkeypatch):
     assert scale_rel_err(out["rows"], out["gather"]) <= 1e-7
 
 
+def test_device_cache_reuse_gives_same_scores(oracle):
+    """Plans take their device buffers from the block cache, with the stale
+    contents of the previous fit: a fit on other data in between must not
+    change a result, and both must match the oracle."""
+    from fastselect_amd import MultiSURF, _lib
+    X1, y1 = make_classification(n_samples=700, n_features=900, random_state=21)
+    X2, y2 = make_classification(n_samples=700, n_features=900, random_state=22)
+    _lib.release_device_cache()
+    a = MultiSURF(backend="gpu").fit(X1, y1).feature_importances_
+    b = MultiSURF(backend="gpu").fit(X2, y2).feature_importances_
+    c = MultiSURF(backend="gpu").fit(X1, y1).feature_importances_
+    np.testing.assert_array_equal(a, c)
+    assert_parity(a, oracle.multisurf_scores(X1, y1), TOL, k=10)
+    assert_parity(b, oracle.multisurf_scores(X2, y2), TOL, k=10)
+    _lib.release_device_cache()
+
+
 def test_sparse_weighted_pairs_count():
     """fs_plan_weighted_pairs: MultiSURF weighs the pairs near one of their two
     samples (~40% here); the count is exact against a numpy restatement."""
