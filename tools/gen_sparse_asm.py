@@ -22,6 +22,12 @@ instead of per 4): 105.4 ms against 104.6, so feats=4 stays.  The register
 numbers below are those of feats=4; low=True maps the SGPRs as described at
 the remap.
 
+pk=True (measured, not shipped): the four differences of an entry as two
+v_pk_add_f32 (7 instead of 9 VALU instructions per entry).  In
+k_score_sparse at cfg4, alternating on one box (tools/pk_ab.sh,
+profiles/ubench/r01k_pk_ab.txt): 124.1 / 124.1 ms against 104.2 / 105.0 for
+the v_sub_f32 loop -- packed f32 costs more issue time than its two halves.
+
 Pipeline per group g (unrolled x6: 3 SGPR sets x 2 A sets):
   s_waitcnt lgkmcnt(0)            A values of g (LDS) and entries of g+1 (SMEM) landed
   s_load_dwordx16                 entries of g+2 (stream offset += 64)
@@ -47,7 +53,8 @@ import re
 SETS = [40, 56, 72]
 
 
-def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, spread=True, low=False):
+def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, spread=True, low=False,
+        pk=False):
     """Macro text.  feats: features per lane (4: 128 KB LDS block, float4 rows;
     2: 64 KB, float2 rows, 64-VGPR budget).  no_ds / same_stream:
     microbenchmark variants that skip the LDS reads / keep re-reading the
@@ -73,8 +80,13 @@ def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, sp
         for q in range(8):
             t = TMP[q % 2]
             w = f"s{s + 2 * q + 1}"
-            for f in range(F):
-                L.append(f"v_sub_f32 v{t + f}, v{A + F * q + f}, v{BCUR + f}")
+            if pk:  # two differences per instruction (b negated in both halves)
+                for f in range(0, F, 2):
+                    L.append(f"v_pk_add_f32 v[{t + f}:{t + f + 1}], v[{A + F * q + f}:{A + F * q + f + 1}], "
+                             f"v[{BCUR + f}:{BCUR + f + 1}] neg_lo:[0,1] neg_hi:[0,1]")
+            else:
+                for f in range(F):
+                    L.append(f"v_sub_f32 v{t + f}, v{A + F * q + f}, v{BCUR + f}")
             for f in range(F):
                 acc = f"%[acc{2 * f + (q & 1)}]"
                 L.append(f"v_fma_f32 {acc}, {w}, |v{t + f}|, {acc}")
