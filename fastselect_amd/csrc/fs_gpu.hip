@@ -663,12 +663,21 @@ __global__ __launch_bounds__(256) void k_tile_rowstats(const double* __restrict_
     const int64_t self = rows ? i0 + r : j0 + r;
     const int64_t other0 = rows ? j0 : i0;
     if (self < n) {
-      for (int c = 0; c < kTile; c++) {
-        const int64_t o = other0 + c;
-        if (o >= n || o == self) continue;
-        const double d = D[o * n_pad + self];
-        s1 += d;
-        s2 += d * d;
+      // 8 loads in flight per step; skipped entries add 0.0, so the sums and
+      // their order are those of the plain loop
+      for (int c0 = 0; c0 < kTile; c0 += 8) {
+        double d[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int64_t o = other0 + c0 + u;
+          const double v = D[o * n_pad + self];  // o < n_pad: always in bounds
+          d[u] = (o < n && o != self) ? v : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          s1 += d[u];
+          s2 += d[u] * d[u];
+        }
       }
     }
   }
@@ -943,12 +952,20 @@ __global__ __launch_bounds__(256) void k_tile_counts(const double* __restrict__ 
   const double t = thr[self];
   const int32_t ls = lab[self];
   double h = 0.0, m = 0.0;
-  for (int c = 0; c < kTile; c++) {
-    const int64_t o = other0 + c;
-    if (o >= n || o == self) continue;
-    if (D[o * n_pad + self] < t) {
-      if (lab[o] == ls) h += 1.0;
-      else m += 1.0;
+  for (int c0 = 0; c0 < kTile; c0 += 8) {
+    bool near[8];  // 8 loads in flight per step
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int64_t o = other0 + c0 + u;
+      const double v = D[o * n_pad + self];  // o < n_pad: always in bounds
+      near[u] = (o < n) & (o != self) & (v < t);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      if (near[u]) {
+        if (lab[other0 + c0 + u] == ls) h += 1.0;
+        else m += 1.0;
+      }
     }
   }
   if (h != 0.0) atomicAdd(&counts[2 * self], h);
