@@ -65,7 +65,14 @@ class MultiSURF(TransformerMixin, BaseEstimator):
         n_samples = x.shape[0]
         n_select = self._validate_parameters(n_samples, self.n_features_in_)
         self.effective_backend_ = _base.effective_backend(self.backend)
+        x = np.ascontiguousarray(x)
+        with _lib.staged_x(self.effective_backend_, x):  # one upload of X for the whole fit
+            scores = self._score(x, y)
+        self.feature_importances_ = scores
+        self.top_features_ = _base.top_features(scores, n_select)
+        return self
 
+    def _score(self, x, y):
         is_discrete, col_min, col_max = _base.column_preprocess(x, self.discrete_limit,
                                                                 self.effective_backend_)
         feature_ranges = (col_max - col_min).astype(np.float32)  # _compute_ranges
@@ -78,12 +85,9 @@ class MultiSURF(TransformerMixin, BaseEstimator):
             name = "MultiSURF*" if self.use_star else "MultiSURF"
             where = "GPU" if self.effective_backend_ == "gpu" else "CPU"
             print(f"Running {name} on the {where} now...")
-        scores = _lib.multisurf_score(self.effective_backend_, x, y, recip_full,
-                                      all_feature_indices, self.use_star, is_discrete,
-                                      self.n_jobs)
-        self.feature_importances_ = scores
-        self.top_features_ = _base.top_features(scores, n_select)
-        return self
+        return _lib.multisurf_score(self.effective_backend_, x, y, recip_full,
+                                    all_feature_indices, self.use_star, is_discrete,
+                                    self.n_jobs)
 
     def _resident_scorer(self, x, y):
         """A scorer for TuRF that keeps X resident (on the GPU for the GPU

@@ -80,14 +80,16 @@ class SURF(TransformerMixin, BaseEstimator):
         else:
             self.effective_backend_ = self.backend
 
-        self.is_discrete_, recip_full = surf_inputs(X, self.discrete_limit,
-                                                    self.effective_backend_)
+        X = np.ascontiguousarray(X)
+        with _lib.staged_x(self.effective_backend_, X):  # one upload of X for the whole fit
+            self.is_discrete_, recip_full = surf_inputs(X, self.discrete_limit,
+                                                        self.effective_backend_)
 
-        algo_name = "SURF*" if self.use_star else "SURF"
-        if self.verbose:
-            print(f"Running {algo_name} on the {self.effective_backend_.upper()} now...")
-        scores = _lib.surf_score(self.effective_backend_, X, y.astype(np.int32), recip_full,
-                                 self.use_star, self.is_discrete_, self.n_jobs)
+            algo_name = "SURF*" if self.use_star else "SURF"
+            if self.verbose:
+                print(f"Running {algo_name} on the {self.effective_backend_.upper()} now...")
+            scores = _lib.surf_score(self.effective_backend_, X, y.astype(np.int32), recip_full,
+                                     self.use_star, self.is_discrete_, self.n_jobs)
         self.feature_importances_ = scores
         self.top_features_ = _base.top_features(scores, n_select)
         if self.verbose:

@@ -13,6 +13,7 @@ in, float32 scores already divided by n out.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 
@@ -36,6 +37,7 @@ _vp = ctypes.c_void_p
 # every symbol include/fastselect_amd.h declares (checked by tests/test_abi.py)
 EXPORTED = (
     "fs_version", "fs_last_error", "fs_device_count", "fs_device_cache_release",
+    "fs_stage_x", "fs_unstage_x",
     "fs_column_stats", "fs_multisurf_score",
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
@@ -71,6 +73,10 @@ def _load() -> ctypes.CDLL:
     lib.fs_last_error.restype = ctypes.c_char_p
     lib.fs_device_count.restype = _int
     lib.fs_device_cache_release.restype = _int
+    lib.fs_stage_x.argtypes = [_int, _vp, _int, _i64, _i64, ctypes.POINTER(ctypes.c_uint64)]
+    lib.fs_stage_x.restype = _int
+    lib.fs_unstage_x.argtypes = [ctypes.c_uint64]
+    lib.fs_unstage_x.restype = _int
     lib.fs_column_stats.argtypes = [_int, _int, _vp, _int, _i64, _i64, _i64, _vp, _vp, _i64p]
     lib.fs_multisurf_score.argtypes = [_int, _int, _f32p, _i64, _i64, _f64p, _f32p, _i64p, _i64,
                                        _int, _u8p, _int, _f32p]
@@ -118,6 +124,25 @@ def lib() -> ctypes.CDLL:
 
 def version() -> str:
     return _lib.fs_version().decode()
+
+
+@contextlib.contextmanager
+def staged_x(backend, x, device=0):
+    """One upload of X for a whole fit on the GPU backend (fs_stage_x): the
+    column statistics and the scoring call that receive this same array read
+    the device copy.  ``x`` must be C-contiguous float32 / float64 and stay
+    unchanged inside the block; other backends pass through."""
+    if backend != "gpu" or x.dtype not in (np.float32, np.float64) or \
+            not x.flags.c_contiguous or x.ndim != 2 or x.size == 0:
+        yield
+        return
+    h = ctypes.c_uint64(0)
+    check(_lib.fs_stage_x(int(device), x.ctypes.data, int(x.dtype == np.float64), x.shape[0],
+                          x.shape[1], ctypes.byref(h)))
+    try:
+        yield
+    finally:
+        _lib.fs_unstage_x(h)
 
 
 def release_device_cache() -> None:

@@ -68,6 +68,20 @@ int fs_device_cache_release(void) {
   return FS_OK;
 }
 
+int fs_stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p, uint64_t* staged) {
+  if (!x || !staged || n < 1 || p < 1) {
+    set_error("fs_stage_x: need x, staged, n >= 1 and p >= 1");
+    return FS_EINVAL;
+  }
+  if (gpu::device_count() <= 0) {
+    set_error("backend='gpu' requested but no HIP device is visible");
+    return FS_ENODEV;
+  }
+  return gpu::stage_x(device, x, x_is_f64, n, p, staged);
+}
+
+int fs_unstage_x(uint64_t staged) { return gpu::unstage_x(staged); }
+
 int fs_column_stats(int backend, int device, const void* x, int x_is_f64, int64_t n, int64_t p,
                     int64_t count_cap, void* colmin_out, void* colmax_out,
                     int64_t* ndistinct_out) {

@@ -202,23 +202,26 @@ int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap,
   if ((e = hipSetDevice(device)) != hipSuccess) fail("hipSetDevice", e);
   if (rc == FS_OK && (e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess)
     fail("hipStreamCreate", e);
-  if (rc == FS_OK) rc = dev_alloc((void**)&dx, (size_t)n * p * esz, device);
+  // a staged copy of x (fs_stage_x) is read in place, else x is uploaded
+  const void* sx = staged_lookup(x, n, p, x_is_f64, device);
+  if (rc == FS_OK && !sx) rc = dev_alloc((void**)&dx, (size_t)n * p * esz, device);
   if (rc == FS_OK) rc = dev_alloc((void**)&pmin, (size_t)nchunks * p * esz, device);
   if (rc == FS_OK) rc = dev_alloc((void**)&pmax, (size_t)nchunks * p * esz, device);
   if (rc == FS_OK) rc = dev_alloc((void**)&dmin, (size_t)p * esz, device);
   if (rc == FS_OK) rc = dev_alloc((void**)&dmax, (size_t)p * esz, device);
   if (rc == FS_OK) rc = dev_alloc((void**)&dcnt, (size_t)p * 8, device);
   if (rc == FS_OK &&
-      (e = hipMemcpyAsync(dx, x, (size_t)n * p * esz, hipMemcpyHostToDevice, s)) != hipSuccess)
+      !sx && (e = hipMemcpyAsync(dx, x, (size_t)n * p * esz, hipMemcpyHostToDevice, s)) != hipSuccess)
     fail("hipMemcpy H2D", e);
+  const void* xd = sx ? sx : dx;
   if (rc == FS_OK) {
     const size_t lds = sizeof(unsigned long long) << tbits;
-    launch_minmax(dx, x_is_f64, n, p, rows_per_chunk, nchunks, pmin, pmax, dmin, dmax, s);
+    launch_minmax(xd, x_is_f64, n, p, rows_per_chunk, nchunks, pmin, pmax, dmin, dmax, s);
     if (x_is_f64)
-      k_coldistinct<double><<<(unsigned)p, 256, lds, s>>>((const double*)dx, n, p, (int)cap,
+      k_coldistinct<double><<<(unsigned)p, 256, lds, s>>>((const double*)xd, n, p, (int)cap,
                                                           tbits, dcnt);
     else
-      k_coldistinct<float><<<(unsigned)p, 256, lds, s>>>((const float*)dx, n, p, (int)cap, tbits,
+      k_coldistinct<float><<<(unsigned)p, 256, lds, s>>>((const float*)xd, n, p, (int)cap, tbits,
                                                          dcnt);
     if ((e = hipGetLastError()) != hipSuccess) fail("column statistics kernels", e);
   }

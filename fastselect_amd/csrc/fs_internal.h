@@ -268,6 +268,13 @@ int device_count();
 int dev_alloc(void** p, size_t bytes, int device);
 void dev_free(void* p);
 void dev_cache_release();
+// Staged X (fs_stage_x): one device copy of a host matrix that the column
+// statistics and the plan of the same fit read instead of uploading it again.
+// staged_lookup returns the device copy of (host, n, p, f64) on `device`, or
+// nullptr.
+int stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p, uint64_t* handle);
+int unstage_x(uint64_t handle);
+const void* staged_lookup(const void* host, int64_t n, int64_t p, int x_is_f64, int device);
 int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap, int device,
                  void* colmin, void* colmax, int64_t* ndistinct);
 // Column minima / maxima of a device-resident X, copied to host arrays in

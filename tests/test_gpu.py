@@ -493,6 +493,30 @@ def test_device_cache_reuse_gives_same_scores(oracle):
     _lib.release_device_cache()
 
 
+def test_staged_x_matches_uploads():
+    """fs_stage_x: column statistics and scoring calls on the same host
+    array read the staged device copy; results are bit-identical to the
+    uploading path (MultiSURF float32 and SURF float64)."""
+    from fastselect_amd import _lib
+    X, y = make_classification(n_samples=500, n_features=700, random_state=31)
+    x32 = np.ascontiguousarray(X, dtype=np.float32)
+    recip = (1 / (x32.max(0) - x32.min(0))).astype(np.float32)
+    isd = np.zeros(700, bool)
+    fidx = np.arange(700, dtype=np.int64)
+    plain_cs = _lib.column_stats("gpu", x32, 10)
+    plain_ms = _lib.multisurf_score("gpu", x32, y, recip, fidx, False, isd)
+    plain_sf = _lib.surf_score("gpu", X, y, recip, True, isd)
+    with _lib.staged_x("gpu", x32):
+        st_cs = _lib.column_stats("gpu", x32, 10)
+        st_ms = _lib.multisurf_score("gpu", x32, y, recip, fidx, False, isd)
+    with _lib.staged_x("gpu", X):
+        st_sf = _lib.surf_score("gpu", X, y, recip, True, isd)
+    for a, b in zip(plain_cs, st_cs):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(plain_ms, st_ms)
+    np.testing.assert_array_equal(plain_sf, st_sf)
+
+
 def test_sparse_weighted_pairs_count():
     """fs_plan_weighted_pairs: MultiSURF weighs the pairs near one of their two
     samples (~40% here); the count is exact against a numpy restatement."""
