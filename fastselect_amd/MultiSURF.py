@@ -60,7 +60,7 @@ class MultiSURF(TransformerMixin, BaseEstimator):
 
     def fit(self, x: np.ndarray, y: np.ndarray):
         """Score every feature with MultiSURF (or MultiSURF*)."""
-        x, y = validate_data(self, x, y, y_numeric=True, dtype=np.float32, ensure_2d=True)
+        x, y = _base.validate_xy(self, x, y, np.float32, self.n_jobs)
         self.n_features_in_ = x.shape[1]
         n_samples = x.shape[0]
         n_select = self._validate_parameters(n_samples, self.n_features_in_)
@@ -114,7 +114,7 @@ class _ResidentMultiSURF:
 
     def __init__(self, est: MultiSURF, x, y):
         self.est = est
-        x, y = validate_data(est, x, y, y_numeric=True, dtype=np.float32, ensure_2d=True)
+        x, y = _base.validate_xy(est, x, y, np.float32, est.n_jobs)
         est.effective_backend_ = _base.effective_backend(est.backend)
         self.n = x.shape[0]
         self.is_discrete, col_min, col_max = _base.column_preprocess(

@@ -82,7 +82,7 @@ class ReliefF(TransformerMixin, BaseEstimator):
 
     def fit(self, x: np.ndarray, y: np.ndarray):
         """Score every feature with ReliefF."""
-        x, y = validate_data(self, x, y, dtype=np.float64, ensure_2d=True, y_numeric=True)
+        x, y = _base.validate_xy(self, x, y, np.float64, self.n_jobs)
         self.n_features_in_ = x.shape[1]
         n_samples = x.shape[0]
         n_select = self._validate_parameters(n_samples, self.n_features_in_)
@@ -124,7 +124,7 @@ class ReliefF(TransformerMixin, BaseEstimator):
         subsets (``ResidentRows``); None when there is nothing to score
         (a single class: TuRF then refits, which yields zeros)."""
         from ._resident import ResidentRows
-        x, y = validate_data(self, x, y, dtype=np.float64, ensure_2d=True, y_numeric=True)
+        x, y = _base.validate_xy(self, x, y, np.float64, self.n_jobs)
         n = x.shape[0]
         self._validate_parameters(n, x.shape[1])
         classes, y_encoded = np.unique(y, return_inverse=True)

@@ -68,7 +68,7 @@ class SURF(TransformerMixin, BaseEstimator):
 
     def fit(self, X: np.ndarray, y: np.ndarray):
         """Score every feature with SURF (or SURF*)."""
-        X, y = validate_data(self, X, y, y_numeric=True, dtype=np.float64, ensure_2d=True)
+        X, y = _base.validate_xy(self, X, y, np.float64, self.n_jobs)
         self.n_features_in_ = X.shape[1]
         n_samples = X.shape[0]
         n_select = self._validate_parameters(n_samples, self.n_features_in_)
@@ -100,7 +100,7 @@ class SURF(TransformerMixin, BaseEstimator):
         """A scorer for TuRF that keeps X resident and re-scores column
         subsets (``ResidentRows``)."""
         from ._resident import ResidentRows
-        X, y = validate_data(self, X, y, y_numeric=True, dtype=np.float64, ensure_2d=True)
+        X, y = _base.validate_xy(self, X, y, np.float64, self.n_jobs)
         n = X.shape[0]
         self._validate_parameters(n, X.shape[1])
         if self.backend == "auto":

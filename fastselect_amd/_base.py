@@ -37,6 +37,22 @@ def n_select_from(n_features_to_select, n_features: int) -> int:
     raise TypeError("n_features_to_select must be an int or a float.")
 
 
+def validate_xy(est, x, y, dtype, n_jobs=-1):
+    """``validate_data(est, x, y, y_numeric=True, dtype=dtype, ensure_2d=True)``
+    as the reference's fit calls it, with scikit-learn's single-threaded
+    element-wise finiteness scan of X (~56 ms at cfg4) replaced by
+    ``fs_all_finite`` on host threads.  When X holds a NaN or an infinity the
+    plain call runs again and raises scikit-learn's own error, so behaviour and
+    messages are unchanged.  Returns C-contiguous X."""
+    from sklearn.utils.validation import validate_data
+    xv, yv = validate_data(est, x, y, y_numeric=True, dtype=dtype, ensure_2d=True,
+                           ensure_all_finite=False)
+    xv = np.ascontiguousarray(xv)
+    if xv.dtype in (np.float32, np.float64) and not _lib.all_finite(xv, n_jobs):
+        validate_data(est, x, y, y_numeric=True, dtype=dtype, ensure_2d=True)
+    return xv, yv
+
+
 def effective_backend(backend: str) -> str:
     """'auto' -> 'gpu' when a HIP device is visible, else 'cpu'.  An explicit
     'gpu' without a device raises instead of falling back."""

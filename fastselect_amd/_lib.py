@@ -37,7 +37,7 @@ _vp = ctypes.c_void_p
 # every symbol include/fastselect_amd.h declares (checked by tests/test_abi.py)
 EXPORTED = (
     "fs_version", "fs_last_error", "fs_device_count", "fs_device_cache_release",
-    "fs_stage_x", "fs_unstage_x",
+    "fs_stage_x", "fs_unstage_x", "fs_all_finite",
     "fs_column_stats", "fs_multisurf_score",
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
@@ -77,6 +77,8 @@ def _load() -> ctypes.CDLL:
     lib.fs_stage_x.restype = _int
     lib.fs_unstage_x.argtypes = [ctypes.c_uint64]
     lib.fs_unstage_x.restype = _int
+    lib.fs_all_finite.argtypes = [_vp, _int, _i64, _i64, _int, ctypes.POINTER(_int)]
+    lib.fs_all_finite.restype = _int
     lib.fs_column_stats.argtypes = [_int, _int, _vp, _int, _i64, _i64, _i64, _vp, _vp, _i64p]
     lib.fs_multisurf_score.argtypes = [_int, _int, _f32p, _i64, _i64, _f64p, _f32p, _i64p, _i64,
                                        _int, _u8p, _int, _f32p]
@@ -143,6 +145,15 @@ def staged_x(backend, x, device=0):
         yield
     finally:
         _lib.fs_unstage_x(h)
+
+
+def all_finite(x, n_jobs=-1) -> bool:
+    """No NaN and no infinity in a C-contiguous float32 / float64 matrix
+    (fs_all_finite, host threads)."""
+    f = _int(0)
+    check(_lib.fs_all_finite(x.ctypes.data, int(x.dtype == np.float64), x.shape[0],
+                             int(np.prod(x.shape[1:])), int(n_jobs), ctypes.byref(f)))
+    return bool(f.value)
 
 
 def release_device_cache() -> None:

@@ -82,6 +82,15 @@ int fs_stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p, ui
 
 int fs_unstage_x(uint64_t staged) { return gpu::unstage_x(staged); }
 
+int fs_all_finite(const void* x, int x_is_f64, int64_t n, int64_t p, int n_jobs, int* finite) {
+  if (!x || !finite || n < 0 || p < 0) {
+    set_error("fs_all_finite: need x, finite, n >= 0 and p >= 0");
+    return FS_EINVAL;
+  }
+  *finite = cpu::all_finite(x, x_is_f64, n * p, n_jobs);
+  return FS_OK;
+}
+
 int fs_column_stats(int backend, int device, const void* x, int x_is_f64, int64_t n, int64_t p,
                     int64_t count_cap, void* colmin_out, void* colmax_out,
                     int64_t* ndistinct_out) {

@@ -38,6 +38,27 @@ static void parallel_for(int64_t count, int n_jobs, F&& body) {
   for (auto& t : th) t.join();
 }
 
+// 1 if every element of x is finite (no NaN, no infinity), else 0: the
+// exponent-all-ones test on the bit patterns, chunks of 1M elements over
+// std::threads.
+int all_finite(const void* x, int x_is_f64, int64_t count, int n_jobs) {
+  constexpr int64_t kChunk = 1 << 20;
+  std::atomic<int> bad{0};
+  parallel_for((count + kChunk - 1) / kChunk, n_jobs, [&](int64_t c) {
+    const int64_t lo = c * kChunk, hi = std::min<int64_t>(count, lo + kChunk);
+    bool b = false;
+    if (x_is_f64) {
+      const uint64_t* u = (const uint64_t*)x;
+      for (int64_t i = lo; i < hi; i++) b |= (u[i] & 0x7ff0000000000000ull) == 0x7ff0000000000000ull;
+    } else {
+      const uint32_t* u = (const uint32_t*)x;
+      for (int64_t i = lo; i < hi; i++) b |= (u[i] & 0x7f800000u) == 0x7f800000u;
+    }
+    if (b) bad.store(1, std::memory_order_relaxed);
+  });
+  return bad.load() ? 0 : 1;
+}
+
 static inline double load_x(const void* x, int x_is_f64, int64_t idx) {
   return x_is_f64 ? ((const double*)x)[idx] : (double)((const float*)x)[idx];
 }

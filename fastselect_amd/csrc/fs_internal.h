@@ -235,6 +235,8 @@ FS_HD inline int numba_argsort_focus(int64_t len, int32_t* R, KeyFn key, RangeFn
 
 // ---- CPU backend ---------------------------------------------------------
 namespace cpu {
+// 1 if all `count` float32 / float64 elements of x are finite, else 0.
+int all_finite(const void* x, int x_is_f64, int64_t count, int n_jobs);
 // CPU state of a MultiSURF plan (the GPU keeps the same arrays in HBM).
 struct CpuState {
   std::vector<double> D;      // n x n distances (integer units; exact for refined pairs)

@@ -81,6 +81,12 @@ FS_API int fs_device_cache_release(void);
 FS_API int fs_stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p,
                       uint64_t* staged);
 FS_API int fs_unstage_x(uint64_t staged);
+/* *finite = 1 if every element of the n x p float32 / float64 matrix is
+ * finite, else 0 (host threads; n_jobs as the scoring calls).  The
+ * estimators call it in place of scikit-learn's single-threaded scan and fall
+ * back to scikit-learn's own validation, and its error, when it reports 0. */
+FS_API int fs_all_finite(const void* x, int x_is_f64, int64_t n, int64_t p, int n_jobs,
+                         int* finite);
 
 /*
  * MultiSURF / MultiSURF* feature scores.

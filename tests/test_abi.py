@@ -126,3 +126,36 @@ def test_column_preprocess_is_reference_discrete_mask():
         isd, _, _ = _base.column_preprocess(x, limit, "cpu")
         ref = np.array([np.unique(x[:, f]).size <= limit for f in range(x.shape[1])])
         np.testing.assert_array_equal(isd, ref)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_all_finite(dtype):
+    """fs_all_finite: the estimators' replacement for scikit-learn's scan."""
+    from fastselect_amd import _lib
+    x = np.random.default_rng(0).normal(size=(3001, 37)).astype(dtype)
+    assert _lib.all_finite(x)
+    for bad in (np.nan, np.inf, -np.inf):
+        y = x.copy()
+        y[2999, 36] = bad
+        assert not _lib.all_finite(y)
+        assert not _lib.all_finite(y, n_jobs=1)
+    assert _lib.all_finite(np.zeros((0, 5), dtype=dtype))
+
+
+def test_estimators_keep_sklearn_finiteness_errors():
+    """Non-finite X raises scikit-learn's own ValueError (message included),
+    also for float64 values that overflow the float32 cast of MultiSURF."""
+    from fastselect_amd import MultiSURF, ReliefF, SURF
+    rng = np.random.default_rng(1)
+    X = rng.normal(size=(40, 6))
+    y = np.arange(40) % 2
+    for est in (MultiSURF(backend="cpu"), ReliefF(backend="cpu"), SURF(backend="cpu")):
+        Xi = X.copy()
+        Xi[3, 2] = np.inf
+        with pytest.raises(ValueError, match="Input X contains infinity"):
+            est.fit(Xi, y)
+    Xo = X.copy()
+    Xo[5, 1] = 1e300
+    with pytest.raises(ValueError, match="Input X contains infinity or a value too large"):
+        MultiSURF(backend="cpu").fit(Xo, y)
+    SURF(backend="cpu").fit(Xo, y)  # float64 estimators accept it, as the reference
