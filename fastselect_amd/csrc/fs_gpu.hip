@@ -2415,6 +2415,8 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   g->ksplit = choose_ksplit(g->n_tiles, device, (int)(rows_q / kBKQ),
                             (g->use_q16 ? Q.pc / 2 : Q.pc) + Q.pd,
                             (size_t)Q.n_pad * Q.n_pad * sizeof(double));
+  if (const char* e = std::getenv("FS_KSPLIT"))  // A/B of the K-split choice
+    if (std::atoi(e) >= 1) g->ksplit = std::min(8, std::atoi(e));
   if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
   const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
   int rc;
