@@ -139,8 +139,12 @@ def staged_x(backend, x, device=0):
         yield
         return
     h = ctypes.c_uint64(0)
-    check(_lib.fs_stage_x(int(device), x.ctypes.data, int(x.dtype == np.float64), x.shape[0],
-                          x.shape[1], ctypes.byref(h)))
+    if _lib.fs_stage_x(int(device), x.ctypes.data, int(x.dtype == np.float64), x.shape[0],
+                       x.shape[1], ctypes.byref(h)) != 0:
+        # staging is only an optimisation: without device room for the extra
+        # copy the calls upload X themselves (and report their own errors)
+        yield
+        return
     try:
         yield
     finally:
