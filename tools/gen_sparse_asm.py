@@ -28,6 +28,12 @@ k_score_sparse at cfg4, alternating on one box (tools/pk_ab.sh,
 profiles/ubench/r01k_pk_ab.txt): 124.1 / 124.1 ms against 104.2 / 105.0 for
 the v_sub_f32 loop -- packed f32 costs more issue time than its two halves.
 
+lead (default 2): rows of g+1 issued before g's first entry; the rest one per
+entry.  Same-box A/B (tools/lead_ab.sh, profiles/ubench/r01l_lead_ab.txt):
+lead 1 / 0 / 2 within run-to-run noise (102.0-105.5 ms), 3 / 4 / 6 slower
+(103.3 / 104.3 / 104.9 against 102.6), -1 (last row after the last entry)
+106.1-106.4.
+
 Pipeline per group g (unrolled x6: 3 SGPR sets x 2 A sets):
   s_waitcnt lgkmcnt(0)            A values of g (LDS) and entries of g+1 (SMEM) landed
   s_load_dwordx16                 entries of g+2 (stream offset += 64)
@@ -54,7 +60,7 @@ SETS = [40, 56, 72]
 
 
 def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, spread=True, low=False,
-        pk=False):
+        pk=False, lead=2):
     """Macro text.  feats: features per lane (4: 128 KB LDS block, float4 rows;
     2: 64 KB, float2 rows, 64-VGPR budget).  no_ds / same_stream:
     microbenchmark variants that skip the LDS reads / keep re-reading the
@@ -116,13 +122,15 @@ def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, sp
             per = len(comp) // 8
             adds, reads = rows[:8], rows[8:] if not no_ds else [""] * 8
             for q in range(8):
-                if q < 2:
+                if q < lead:
                     L += [adds[q]] + ([reads[q]] if reads[q] else [])
             for e in range(8):
                 L += comp[e * per:(e + 1) * per]
-                q = e + 2
-                if q < 8:
+                q = e + lead
+                if 0 <= q < 8:
                     L += [adds[q]] + ([reads[q]] if reads[q] else [])
+            for q in range(max(0, 8 + lead), 8):  # lead < 0: the rest after the last entry
+                L += [adds[q]] + ([reads[q]] if reads[q] else [])
         L.append(f"s_bitcmp1_b32 s{SETS[c] + 1}, 0")
         L.append(f"s_cbranch_scc1 {10 + x}f")
         L.append(f"{20 + x}:")
@@ -220,7 +228,11 @@ HEADER = """// Generated by tools/gen_sparse_asm.py -- do not edit by hand.
 if __name__ == "__main__":
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "fastselect_amd", "csrc",
                         "fs_sparse_asm.inc")
-    open(path, "w").write(HEADER + gen())
+    text = HEADER + gen()
+    if os.environ.get("FS_GEN_LEAD_VARIANTS"):  # A/B build: FS_SPARSE_STREAM_ASM_L<n>
+        for ld in (1, 0, -1):
+            text += "\n" + gen(name=f"FS_SPARSE_STREAM_ASM_L{ld}".replace("-", "M"), lead=ld)
+    open(path, "w").write(text)
     print("wrote", os.path.normpath(path))
 
 
