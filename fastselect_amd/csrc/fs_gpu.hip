@@ -31,6 +31,7 @@
 #include <string>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <type_traits>
 #include <unordered_map>
 #include <vector>
@@ -2069,6 +2070,8 @@ struct Staged {
   int64_t n, p;
   int f64, device;
   void* dev;
+  std::thread::id owner;  // only the staging thread's calls read it (concurrent
+                          // fits of one array stage and free their own copies)
 };
 std::mutex staged_mu;
 std::vector<Staged> staged;
@@ -2091,7 +2094,7 @@ int stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p, uint6
     return FS_EHIP;
   }
   std::lock_guard<std::mutex> lk(staged_mu);
-  staged.push_back(Staged{x, n, p, x_is_f64 ? 1 : 0, device, d});
+  staged.push_back(Staged{x, n, p, x_is_f64 ? 1 : 0, device, d, std::this_thread::get_id()});
   *handle = (uint64_t)(uintptr_t)d;
   return FS_OK;
 }
@@ -2116,7 +2119,7 @@ const void* staged_lookup(const void* host, int64_t n, int64_t p, int x_is_f64, 
   std::lock_guard<std::mutex> lk(staged_mu);
   for (const Staged& e : staged)
     if (e.host == host && e.n == n && e.p == p && e.f64 == (x_is_f64 ? 1 : 0) &&
-        e.device == device)
+        e.device == device && e.owner == std::this_thread::get_id())
       return e.dev;
   return nullptr;
 }

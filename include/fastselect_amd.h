@@ -76,8 +76,9 @@ FS_API int fs_device_cache_release(void);
 /* Stage X for one fit: upload the n x p row-major matrix (float32, or
  * float64 when x_is_f64) to `device` once.  Until fs_unstage_x, the GPU
  * backend's fs_column_stats and scoring calls given the same host pointer,
- * shape and dtype read the staged copy instead of uploading X again; the
- * caller must not modify x in between.  *staged receives the handle. */
+ * shape and dtype, made from the thread that staged it, read the staged copy
+ * instead of uploading X again; the caller must not modify x in between.
+ * *staged receives the handle. */
 FS_API int fs_stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p,
                       uint64_t* staged);
 FS_API int fs_unstage_x(uint64_t staged);

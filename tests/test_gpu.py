@@ -517,6 +517,34 @@ def test_staged_x_matches_uploads():
     np.testing.assert_array_equal(plain_sf, st_sf)
 
 
+def test_concurrent_fits_on_one_array():
+    """Fits of the same host array in several threads each stage and free
+    their own device copy (staged X is per thread): results equal the
+    sequential fits."""
+    import threading
+    from fastselect_amd import MultiSURF, SURF
+    X, y = make_classification(n_samples=600, n_features=800, random_state=41)
+    X = np.ascontiguousarray(X)
+    ref_m = MultiSURF(backend="gpu").fit(X, y).feature_importances_
+    ref_s = SURF(backend="gpu").fit(X, y).feature_importances_
+    out, errs = {}, []
+
+    def work(k):
+        try:
+            est = MultiSURF(backend="gpu") if k % 2 == 0 else SURF(backend="gpu")
+            out[k] = est.fit(X, y).feature_importances_
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    th = [threading.Thread(target=work, args=(k,)) for k in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs
+    for k, v in out.items():
+        np.testing.assert_array_equal(v, ref_m if k % 2 == 0 else ref_s)
+
+
 def test_sparse_weighted_pairs_count():
     """fs_plan_weighted_pairs: MultiSURF weighs the pairs near one of their two
     samples (~40% here); the count is exact against a numpy restatement."""
