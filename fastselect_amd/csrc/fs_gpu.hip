@@ -1952,7 +1952,7 @@ struct Plan {
 // hipMalloc of the ~11 GB a cfg4 plan holds took 190-310 ms per fit on the
 // MI355X (fresh pages are mapped on allocation; tools/fit_breakdown.py) --
 // more than the scoring.  Blocks that plans and the column statistics free
-// are kept per device up to a cap (a quarter of the device's memory;
+// are kept per device up to a cap (an eighth of the device's memory;
 // FS_DEVICE_CACHE_MB overrides, 0 disables) and handed to the next request
 // they cover within 2x, so repeated fits (TuRF refits, CV folds, benchmarks)
 // skip the mapping.  A failed hipMalloc releases the device's cache and
@@ -1987,7 +1987,7 @@ size_t cache_cap(int device) {  // with cache_mu held
     }
     it = total.emplace(device, t).first;
   }
-  return it->second / 4;
+  return it->second / 8;
 }
 
 void release_device(int device) {  // with cache_mu held; device < 0: all

@@ -69,7 +69,7 @@ FS_API const char* fs_last_error(void);
 FS_API int fs_device_count(void);
 /* Free the device blocks the library keeps between calls.  Plans and the
  * column statistics return their device buffers to a per-device cache (up to
- * a quarter of the device's memory, FS_DEVICE_CACHE_MB overrides, 0
+ * an eighth of the device's memory, FS_DEVICE_CACHE_MB overrides, 0
  * disables), so that the next fit skips hipMalloc's page mapping (190-310 ms
  * for a cfg4 plan).  Returns FS_OK. */
 FS_API int fs_device_cache_release(void);
