@@ -34,6 +34,10 @@ lead 1 / 0 / 2 within run-to-run noise (102.0-105.5 ms), 3 / 4 / 6 slower
 (103.3 / 104.3 / 104.9 against 102.6), -1 (last row after the last entry)
 106.1-106.4.
 
+prio (A/B only): s_setprio 1 or 3 from the group's wait to its second entry.
+Same box, alternating (profiles/ubench/r01l_prio_ab.txt, "lead" column = V):
+104.3 / 104.7 ms plain, 103.3 / 104.0 with 1, 104.1 / 103.9 with 3 -- noise.
+
 Pipeline per group g (unrolled x6: 3 SGPR sets x 2 A sets):
   s_waitcnt lgkmcnt(0)            A values of g (LDS) and entries of g+1 (SMEM) landed
   s_load_dwordx16                 entries of g+2 (stream offset += 64)
@@ -60,7 +64,7 @@ SETS = [40, 56, 72]
 
 
 def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, spread=True, low=False,
-        pk=False, lead=2):
+        pk=False, lead=2, prio=0):
     """Macro text.  feats: features per lane (4: 128 KB LDS block, float4 rows;
     2: 64 KB, float2 rows, 64-VGPR budget).  no_ds / same_stream:
     microbenchmark variants that skip the LDS reads / keep re-reading the
@@ -106,6 +110,8 @@ def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, sp
         c, n, nn = x % 3, (x + 1) % 3, (x + 2) % 3
         ac, an = x % 2, (x + 1) % 2
         L = ["s_waitcnt lgkmcnt(0)"]
+        if prio:  # raised while the wave issues the group's loads (A/B)
+            L.append(f"s_setprio {prio}")
         rows = issue_rows(n, an)
         if not spread:
             L += rows
@@ -126,6 +132,8 @@ def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, sp
                     L += [adds[q]] + ([reads[q]] if reads[q] else [])
             for e in range(8):
                 L += comp[e * per:(e + 1) * per]
+                if prio and e == 1:
+                    L.append("s_setprio 0")
                 q = e + lead
                 if 0 <= q < 8:
                     L += [adds[q]] + ([reads[q]] if reads[q] else [])
@@ -230,8 +238,8 @@ if __name__ == "__main__":
                         "fs_sparse_asm.inc")
     text = HEADER + gen()
     if os.environ.get("FS_GEN_LEAD_VARIANTS"):  # A/B build: FS_SPARSE_STREAM_ASM_L<n>
-        for ld in (1, 0, -1):
-            text += "\n" + gen(name=f"FS_SPARSE_STREAM_ASM_L{ld}".replace("-", "M"), lead=ld)
+        for pr in (1, 3):
+            text += "\n" + gen(name=f"FS_SPARSE_STREAM_ASM_P{pr}", prio=pr)
     open(path, "w").write(text)
     print("wrote", os.path.normpath(path))
 
