@@ -2507,14 +2507,17 @@ static int run_quantize_dist(Plan* g) {
     // with the row moments), on the side stream beside k_dist: it reads
     // xqT as k_dist does and writes only epsT / corr, which k_dist leaves
     // alone; plan_pass1 joins it before k_rowstats_reduce reads corr
+    // FS_SIDE=0: on the main stream, before k_dist (A/B of the overlap)
+    const char* se = std::getenv("FS_SIDE");
+    const hipStream_t cs = (se && *se == '0') ? g->stream : g->side;
     FS_HIP(hipEventRecord(g->ev_fork, g->stream));
     FS_HIP(hipStreamWaitEvent(g->side, g->ev_fork, 0));
     if (g->c_hi > g->c_lo) {
-      k_colrank<<<(unsigned)(g->c_hi - g->c_lo), 256, 0, g->side>>>(
+      k_colrank<<<(unsigned)(g->c_hi - g->c_lo), 256, 0, cs>>>(
           g->xqT, Q.n, Q.n_pad, g->rank_shift, Q.q16, g->c_lo, g->epsT);
       FS_TRY(launch_check("k_colrank"));
     }
-    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, g->side>>>(g->epsT, Q.n, Q.n_pad, g->c_lo,
+    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, cs>>>(g->epsT, Q.n, Q.n_pad, g->c_lo,
                                                                g->c_hi, g->corr);
     FS_TRY(launch_check("k_rowcorr"));
     FS_HIP(hipEventRecord(g->ev_join, g->side));
