@@ -1,5 +1,6 @@
 #!/bin/bash
 # Quantisation split (xqT first, xs + eps beside k_dist) against one quantize (FS_QSPLIT=0).
+# (FS_QSPLIT existed only in the A/B build; the split was not kept: DESIGN.md, profiles/r01l_qsplit_ab.txt)
 set -euo pipefail
 mkdir -p gpurun_out
 for q in 1 0 1 0 1 0; do
