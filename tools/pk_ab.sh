@@ -1,5 +1,6 @@
 #!/bin/bash
 # Sparse pass-2 loop variants A/B on one box: FS_SPARSE_PK=0/1, correctness
+# (FS_SPARSE_PK existed only in the A/B build; not kept: tools/gen_sparse_asm.py docstring)
 # (sparse tests with the packed loop) then alternating world-1 cfg4 steps.
 set -euo pipefail
 mkdir -p gpurun_out
