@@ -5,8 +5,11 @@
 // reference fit() hands to its host caller (MultiSURF.py:409-420,
 // ReliefF.py:366-380, SURF.py:347-355); the caller still computes recip and
 // is_discrete exactly as the reference does.
+#include <sched.h>
+
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <unordered_set>
@@ -16,10 +19,21 @@
 
 namespace fs {
 
+// n_jobs > 0: that many threads.  Otherwise the CPUs this process may run on
+// (its affinity mask, not the machine's count: a container or a GPU box's
+// share), capped by OMP_NUM_THREADS when it is set -- the pool a
+// numba / OpenMP program of the reference would get.
 int hardware_threads(int n_jobs) {
-  int hw = (int)std::thread::hardware_concurrency();
-  if (hw <= 0) hw = 1;
   if (n_jobs > 0) return n_jobs;
+  int hw = 0;
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) hw = CPU_COUNT(&set);
+  if (hw <= 0) hw = (int)std::thread::hardware_concurrency();
+  if (hw <= 0) hw = 1;
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) {
+    const int cap = std::atoi(e);
+    if (cap > 0 && cap < hw) hw = cap;
+  }
   return hw;
 }
 
