@@ -29,7 +29,7 @@ def relieff_inputs(x, y, discrete_limit, where):
     feature_ranges[is_discrete] = 1.0
     feature_ranges[feature_ranges == 0] = 1.0
     recip = (1.0 / feature_ranges).astype(np.float32)
-    return (np.ascontiguousarray(x, dtype=np.float32), y_enc.astype(np.int32), recip, is_discrete,
+    return (_base.to_float32(x), y_enc.astype(np.int32), recip, is_discrete,
             class_probs.astype(np.float32))
 
 

@@ -53,6 +53,26 @@ def validate_xy(est, x, y, dtype, n_jobs=-1):
     return xv, yv
 
 
+def to_float32(x: np.ndarray, n_jobs: int = -1) -> np.ndarray:
+    """``np.ascontiguousarray(x, dtype=np.float32)`` (the reference's cast,
+    round to nearest) with the conversion of large arrays split over threads
+    by row blocks (numpy releases the GIL in the copy): 15.8 ms on one thread
+    for ReliefF's cfg3 matrix."""
+    if x.dtype == np.float32 and x.flags.c_contiguous:
+        return x
+    n = x.shape[0] if x.ndim else 0
+    nt = _lib.host_threads(n_jobs)
+    if x.ndim != 2 or x.size < (1 << 22) or nt <= 1:
+        return np.ascontiguousarray(x, dtype=np.float32)
+    from concurrent.futures import ThreadPoolExecutor
+    out = np.empty(x.shape, dtype=np.float32)
+    edges = np.linspace(0, n, min(n, 4 * nt) + 1).astype(np.int64)
+    with ThreadPoolExecutor(max_workers=nt) as ex:
+        list(ex.map(lambda k: np.copyto(out[edges[k]:edges[k + 1]], x[edges[k]:edges[k + 1]],
+                                        casting="same_kind"), range(len(edges) - 1)))
+    return out
+
+
 def effective_backend(backend: str) -> str:
     """'auto' -> 'gpu' when a HIP device is visible, else 'cpu'.  An explicit
     'gpu' without a device raises instead of falling back."""

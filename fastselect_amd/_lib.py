@@ -160,6 +160,22 @@ def all_finite(x, n_jobs=-1) -> bool:
     return bool(f.value)
 
 
+def host_threads(n_jobs=-1) -> int:
+    """The native library's thread count for ``n_jobs`` (fs_prep.cpp
+    hardware_threads): n_jobs > 0 as given, else the CPUs of this process's
+    affinity mask, capped by OMP_NUM_THREADS when set."""
+    if n_jobs is not None and n_jobs > 0:
+        return int(n_jobs)
+    try:
+        hw = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        hw = os.cpu_count() or 1
+    cap = os.environ.get("OMP_NUM_THREADS", "")
+    if cap.isdigit() and 0 < int(cap) < hw:
+        hw = int(cap)
+    return max(1, hw)
+
+
 def release_device_cache() -> None:
     """Free the device blocks kept between fits (fs_device_cache_release)."""
     _lib.fs_device_cache_release()

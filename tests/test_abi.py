@@ -159,3 +159,14 @@ def test_estimators_keep_sklearn_finiteness_errors():
     with pytest.raises(ValueError, match="Input X contains infinity or a value too large"):
         MultiSURF(backend="cpu").fit(Xo, y)
     SURF(backend="cpu").fit(Xo, y)  # float64 estimators accept it, as the reference
+
+
+def test_threaded_float32_cast_equals_numpy():
+    """_base.to_float32 (row blocks over threads) is numpy's float32 cast."""
+    from fastselect_amd import _base
+    rng = np.random.default_rng(3)
+    x = rng.normal(size=(2500, 1800)) * 10.0 ** rng.integers(-30, 30, size=(2500, 1800))
+    for arr in (x, np.asfortranarray(x), x[::2, 1:]):
+        got = _base.to_float32(arr, n_jobs=4)
+        assert got.flags.c_contiguous and got.dtype == np.float32
+        np.testing.assert_array_equal(got, np.ascontiguousarray(arr, dtype=np.float32))
