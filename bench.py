@@ -26,6 +26,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -62,6 +64,58 @@ def pmc_traffic(kernel, n, p, world):
     return k["hbm_bytes_per_launch"], t.get("source")
 
 
+def rank_envs(n, port, base=None):
+    """Environment of each of the n ranks bench.py starts for ``--gpus n``
+    (one process per GPU, torch.distributed env:// rendezvous on 127.0.0.1),
+    as torch.distributed.run would set it."""
+    base = dict(os.environ if base is None else base)
+    envs = []
+    for r in range(n):
+        e = dict(base)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        envs.append(e)
+    return envs
+
+
+def launch_ranks(n, argv):
+    """``python bench.py --gpus n`` without a launcher: start the n ranks as
+    child processes (before this process touches any GPU), wait for all of
+    them and exit with the first failure's status.  A rank that fails ends
+    the others, so none waits forever at a barrier."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    script = os.path.abspath(__file__)
+    procs = [subprocess.Popen([sys.executable, script] + list(argv), env=e)
+             for e in rank_envs(n, port)]
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            r = p.poll()
+            if r is None:
+                continue
+            live.remove(p)
+            if r != 0 and rc == 0:
+                rc = r if r > 0 else 1
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
@@ -70,7 +124,7 @@ def make_data(n, p, seed):
     from sklearn.datasets import make_classification
     X, y = make_classification(n_samples=n, n_features=p, n_informative=20, n_redundant=100,
                                random_state=seed)
-    return X.astype(np.float32), y
+    return X, y
 
 
 def cpu_baseline(x, y, budget_s=25.0):
@@ -92,11 +146,31 @@ def cpu_baseline(x, y, budget_s=25.0):
     O.multisurf_scores(x, y, i_range=(0, m), n_jobs=threads)
     t = time.perf_counter() - t0
     t_full = t * n / m
+    # the reference's loop evaluates every distance row twice plus the near
+    # accumulation: ~(2 + near fraction) * n^2 * p PFE; the
+    # published reference CPU rate is ~5e9 PFE/s
+    pfe = 2.0 * m * (n - 1) * p
     return {"value": n * p / t_full, "unit": "feature-scores/s", "cores": threads,
-            "kind": "port",
+            "kind": "port", "cpu_model": cpu_model(),
+            "pfe_per_s_distance_passes": pfe / t, "reference_published_pfe_per_s": 5e9,
             "sample": f"oracle MultiSURF (C/OpenMP restatement of the reference backend='cpu') "
                       f"on focal samples [0, {m}) of the same {n}x{p} data: {t:.2f} s, "
                       f"extrapolated x{n / m:.1f} to {t_full:.1f} s"}
+
+
+def fit_ms(X, y, star, repeats=5):
+    """End-to-end ``MultiSURF(backend='gpu').fit`` (validation + float32
+    cast, column statistics, H2D of X, scoring, top-k): median of `repeats`
+    after one warm-up fit.  SURVEY.md §8d's end-to-end timing."""
+    import fastselect_amd
+    est = fastselect_amd.MultiSURF(backend="gpu", n_features_to_select=10, use_star=star)
+    est.fit(X, y)
+    ts = []
+    for _ in range(repeats):
+        t0 = time.perf_counter()
+        est.fit(X, y)
+        ts.append((time.perf_counter() - t0) * 1e3)
+    return float(np.median(ts)), ts
 
 
 def main():
@@ -109,95 +183,146 @@ def main():
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--star", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--dist-backend", default="nccl",
-                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI; "
-                         "gloo only to rehearse several ranks on one GPU)")
+    ap.add_argument("--no-fit", action="store_true", help="skip the end-to-end fit() timing")
+    ap.add_argument("--backend", default="gpu", choices=("gpu", "cpu"),
+                    help="cpu: rehearse the multi-rank job on host threads (gloo, tests only)")
+    ap.add_argument("--dist-backend", default=None,
+                    help="torch.distributed backend for N > 1 (default nccl = RCCL over xGMI "
+                         "on the GPU, gloo with --backend cpu)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    dist_backend = args.dist_backend or ("nccl" if args.backend == "gpu" else "gloo")
+
+    # --gpus N without a launcher: start the N ranks here, before any GPU call
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
 
-    from fastselect_amd import _lib
     from fastselect_amd.parallel import ShardedMultiSURF
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    # one GPU per local rank; ranks beyond the visible GPUs share them (only
-    # meaningful for a gloo rehearsal)
-    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local)
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: launch exactly "
+                         f"one rank per GPU")
+    on_gpu = args.backend == "gpu"
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if on_gpu:
+        ndev = torch.cuda.device_count()
+        if dist_backend == "nccl" and ndev < world:
+            raise SystemExit(f"bench.py: {world} ranks need {world} visible GPUs, found {ndev}")
+        # a gloo rehearsal may put several ranks on one GPU
+        local %= max(1, ndev)
+        torch.cuda.set_device(local)
     if world > 1:
-        if args.dist_backend == "nccl":
+        if dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group(dist_backend)
 
-    t0 = time.perf_counter()
-    x, y = make_data(args.samples, args.features, args.seed)
-    ranges = (x.max(axis=0) - x.min(axis=0)).astype(np.float32)
-    ranges[ranges == 0] = 1
-    recip = (1.0 / ranges).astype(np.float32)
-    # make_classification columns are continuous; the estimator's np.unique
-    # discrete detection (host, ~2 s here) is part of fit(), not of a step
-    is_disc = np.zeros(args.features, dtype=bool)
-    log(f"rank {rank}/{world}: data {args.samples}x{args.features} ready in {time.perf_counter() - t0:.1f} s")
-
-    job = ShardedMultiSURF(x, y, recip, is_disc, use_star=args.star, backend="gpu", device=local)
-    tiles, _, _ = job.info()
+    def sync():
+        if on_gpu:
+            torch.cuda.synchronize()
 
     def barrier():
         if world > 1:
             dist.barrier()
 
+    t0 = time.perf_counter()
+    X, y = make_data(args.samples, args.features, args.seed)
+    x = X.astype(np.float32)
+    ranges = (x.max(axis=0) - x.min(axis=0)).astype(np.float32)
+    ranges[ranges == 0] = 1
+    recip = (1.0 / ranges).astype(np.float32)
+    # make_classification columns are continuous; discrete detection is part
+    # of fit() (timed separately in fit_ms), not of a step
+    is_disc = np.zeros(args.features, dtype=bool)
+    log(f"rank {rank}/{world}: data {args.samples}x{args.features} ready in "
+        f"{time.perf_counter() - t0:.1f} s")
+
+    job = ShardedMultiSURF(x, y, recip, is_disc, use_star=args.star, backend=args.backend,
+                           device=local)
+    tiles, _, _ = job.info()
+
     for w in range(args.warmup):
         job.step()
-        torch.cuda.synchronize()
+        sync()
         log(f"warmup {w} done")
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t_start = time.perf_counter()
     dist_ms, score_ms = [], []
     for s in range(args.steps):
-        scores = job.step()
-        dist_ms.append(job.kernel_ms(0))
-        score_ms.append(job.kernel_ms(1))
-    torch.cuda.synchronize()
+        job.step()
+        if on_gpu:
+            dist_ms.append(job.kernel_ms(0))
+            score_ms.append(job.kernel_ms(1))
+    sync()
     barrier()
     elapsed = time.perf_counter() - t_start
     _, _, refined = job.info()
     weighted = job.weighted_pairs()  # non-zero pass-2 weights (sparse pass 2), -1 if dense
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     ms_per_step = elapsed / args.steps * 1e3
+    n, p = args.samples, args.features
 
-    # dominant kernel roofline (rank-local launch).  Algorithmic count of
-    # pass 1: unique pairs x features / world (padding and the duplicated half
-    # of diagonal tiles are executed but not counted); of pass 2: the pairs
-    # with a non-zero weight x features when pass 2 is sparse (the work the
-    # reference's near/far accumulation needs), else every unique pair.
-    d_ms, s_ms = float(np.mean(dist_ms)), float(np.mean(score_ms))
-    pairs_dense = args.samples * (args.samples - 1) / 2.0 / world
-    pairs_score = weighted if weighted >= 0 else pairs_dense
-    score_name = "k_score_sparse" if weighted >= 0 else "k_score"
-    pfe = {"k_dist": pairs_dense * args.features, score_name: pairs_score * args.features}
-    kern = {"k_dist": d_ms, score_name: s_ms}
-    dom = max(kern, key=kern.get)
-    pfe_launch = pfe[dom]
-    achieved = FLOP_PER_PFE * pfe_launch / (kern[dom] * 1e-3) / 1e12
-    # algorithmic bytes one launch moves from HBM/L2 into the CUs: both row
-    # panels of every owned tile once (+ D write for k_dist; the pair weights
-    # for k_score: 8-byte entries when sparse, the dense 128x128 f32 tiles else)
-    w_bytes = weighted * 8 if weighted >= 0 else tiles * 128 * 128 * 4
-    alg_bytes = {"k_dist": tiles * (2 * 128 * args.features * 4 + 2 * 128 * 128 * 8),
-                 score_name: tiles * 2 * 128 * args.features * 4 + w_bytes}
-    traffic, traffic_src = pmc_traffic(dom, args.samples, args.features, world)
+    roofline = None
+    if on_gpu:
+        # dominant kernel roofline (rank-local launch).  Algorithmic count of
+        # pass 1: unique pairs x features / world (padding and the duplicated
+        # half of diagonal tiles are executed but not counted); of pass 2: the
+        # pairs with a non-zero weight x features when pass 2 is sparse (the
+        # work the reference's near/far accumulation needs), else every pair.
+        d_ms, s_ms = float(np.mean(dist_ms)), float(np.mean(score_ms))
+        pairs_dense = n * (n - 1) / 2.0 / world
+        pairs_score = weighted if weighted >= 0 else pairs_dense
+        score_name = "k_score_sparse" if weighted >= 0 else "k_score"
+        pfe = {"k_dist": pairs_dense * p, score_name: pairs_score * p}
+        kern = {"k_dist": d_ms, score_name: s_ms}
+        dom = max(kern, key=kern.get)
+        achieved = FLOP_PER_PFE * pfe[dom] / (kern[dom] * 1e-3) / 1e12
+        # bytes the tiles stream from L2/HBM into the CUs (both row panels of
+        # every owned tile, + the D write / the pair weights): on-chip reuse
+        # traffic, NOT the algorithmic HBM bytes
+        w_bytes = weighted * 8 if weighted >= 0 else tiles * 128 * 128 * 4
+        panel_bytes = {"k_dist": tiles * (2 * 128 * p * 4 + 2 * 128 * 128 * 8),
+                       score_name: tiles * 2 * 128 * p * 4 + w_bytes}
+        # algorithmic HBM bytes: X once per kernel, D written
+        # by pass 1 (8-byte entries, both halves), the pair weights read by pass 2
+        alg_bytes = {"k_dist": n * p * 4 / world + n * n * 8 / world,
+                     score_name: n * p * 4 + w_bytes}
+        traffic = {k: pmc_traffic(k, n, p, world)[0] for k in kern}
+        roofline = {
+            "bound": "valu", "kernel": dom, "achieved": achieved,
+            "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / VALU_PEAK_TFLOPS,
+            "traffic": traffic[dom],
+            "traffic_source": pmc_traffic(dom, n, p, world)[1],
+            "traffic_per_kernel": traffic,
+            "flop_per_pfe": FLOP_PER_PFE,
+            "pfe_per_s": pfe[dom] / (kern[dom] * 1e-3),
+            "kernel_ms": kern,
+            "pfe_per_launch": pfe[dom],
+            "pass2_weighted_pairs": weighted,
+            "pass2_pair_density": (pairs_score / pairs_dense) if pairs_dense else None,
+            "hbm_alg_GBps": {k: alg_bytes[k] / (kern[k] * 1e-3) / 1e9 for k in kern},
+            "hbm_alg_frac": {k: alg_bytes[k] / (kern[k] * 1e-3) / 1e9 / HBM_PEAK_GBPS
+                             for k in kern},
+            "onchip_panel_GBps": {k: panel_bytes[k] / (kern[k] * 1e-3) / 1e9 for k in kern},
+            "hbm_peak_GBps": HBM_PEAK_GBPS,
+        }
+    job.close()
 
+    out = None
     if rank == 0:
         out = {
             "metric": "feature-scores/sec (n*p/s) MultiSURF fp32",
-            "value": args.samples * args.features / (ms_per_step * 1e-3),
+            "value": n * p / (ms_per_step * 1e-3),
             "unit": "feature-scores/s",
             "n_gpus": world,
             "steps": args.steps,
@@ -212,33 +337,26 @@ def main():
                      "float32 arithmetic; pass 2 over the pairs with a non-zero weight: f32 diffs x "
                      "f32 pair weights, f64 accumulation",
             "data": "synthetic make_classification(n_informative=20, n_redundant=100, random_state=42)",
-            "config": {"workload": f"MultiSURF{'*' if args.star else ''} n={args.samples} "
-                                   f"p={args.features} (BASELINE configs[3])",
-                       "n_samples": args.samples, "n_features": args.features,
-                       "parallelism": f"pair-tile shard x{world}, "
-                                      f"{'RCCL' if args.dist_backend == 'nccl' else args.dist_backend}"
-                                      f" all-reduce"},
-            "roofline": {
-                "bound": "valu", "kernel": dom, "achieved": achieved,
-                "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / VALU_PEAK_TFLOPS,
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "flop_per_pfe": FLOP_PER_PFE,
-                "pfe_per_s": pfe_launch / (kern[dom] * 1e-3),
-                "kernel_ms": kern,
-                "pfe_per_launch": pfe_launch,
-                "pass2_weighted_pairs": weighted,
-                "pass2_pair_density": (pairs_score / pairs_dense) if pairs_dense else None,
-                "hbm_alg_GBps": {k: alg_bytes[k] / (kern[k] * 1e-3) / 1e9 for k in kern},
-                "hbm_peak_GBps": HBM_PEAK_GBPS,
-            },
+            "config": {"workload": f"MultiSURF{'*' if args.star else ''} n={n} p={p} "
+                                   f"(BASELINE configs[3])",
+                       "n_samples": n, "n_features": p,
+                       "parallelism": f"pair-tile shard x{world}"
+                                      + (f", {'RCCL' if dist_backend == 'nccl' else dist_backend}"
+                                         f" all-reduce" if world > 1 else "")},
+            "roofline": roofline,
             "refined_pairs": refined,
         }
+    if on_gpu and world == 1 and not args.no_fit:
+        log("timing end-to-end fit() ...")
+        med, ts = fit_ms(X, y, args.star)
+        out["fit_ms"] = med
+        out["fit_ms_runs"] = ts
+        out["fit_feature_scores_per_s"] = n * p / (med * 1e-3)
+    if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline (oracle) ...")
             out["cpu_baseline"] = cpu_baseline(x, y)
         print(json.dumps(out), flush=True)
-    job.close()
     if world > 1:
         dist.destroy_process_group()
 

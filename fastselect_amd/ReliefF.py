@@ -16,12 +16,12 @@ from sklearn.utils.validation import check_is_fitted, validate_data
 from . import _base, _lib
 
 
-def relieff_inputs(x, y, discrete_limit, where):
+def relieff_inputs(x, y, discrete_limit, where, device=0, n_jobs=-1):
     """ReliefF.fit's preprocessing after validation (ReliefF.py:366-380, 400):
     discrete detection and column ranges (computed on ``where``), class priors,
     class codes, reciprocal ranges (discrete and constant columns -> 1) and the
     float32 cast.  Returns (x32, y_enc int32, recip f32, is_discrete, priors f32)."""
-    is_discrete, col_min, col_max = _base.column_preprocess(x, discrete_limit, where)
+    is_discrete, col_min, col_max = _base.column_preprocess(x, discrete_limit, where, device)
     class_labels, class_counts = np.unique(y, return_counts=True)
     class_probs = class_counts / len(y)
     y_enc = np.searchsorted(class_labels, y)
@@ -29,7 +29,7 @@ def relieff_inputs(x, y, discrete_limit, where):
     feature_ranges[is_discrete] = 1.0
     feature_ranges[feature_ranges == 0] = 1.0
     recip = (1.0 / feature_ranges).astype(np.float32)
-    return (_base.to_float32(x), y_enc.astype(np.int32), recip, is_discrete,
+    return (_base.to_float32(x, n_jobs), y_enc.astype(np.int32), recip, is_discrete,
             class_probs.astype(np.float32))
 
 
@@ -106,7 +106,7 @@ class ReliefF(TransformerMixin, BaseEstimator):
         # resolved below, after these steps, as in the reference)
         where = "gpu" if self.backend != "cpu" and _lib.gpu_available() else "cpu"
         x32, y_enc, recip_full, is_discrete, class_probs = relieff_inputs(
-            x, y, self.discrete_limit, where)
+            x, y, self.discrete_limit, where, n_jobs=self.n_jobs)
         self.is_discrete_ = is_discrete
 
         self.effective_backend_ = _base.effective_backend(self.backend)
@@ -143,7 +143,7 @@ class ReliefF(TransformerMixin, BaseEstimator):
 
         where = "gpu" if self.backend != "cpu" and _lib.gpu_available() else "cpu"
         x32, y_enc, recip, is_discrete, class_probs = relieff_inputs(
-            x, y, self.discrete_limit, where)
+            x, y, self.discrete_limit, where, n_jobs=self.n_jobs)
         self.effective_backend_ = _base.effective_backend(self.backend)
         plan = _lib.RowsPlan(self.effective_backend_, "relieff", x32, y_enc, recip, is_discrete,
                              k=self.n_neighbors, class_probs=class_probs, n_jobs=self.n_jobs)

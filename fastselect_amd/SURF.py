@@ -12,15 +12,17 @@ from sklearn.utils.validation import check_is_fitted, validate_data
 
 from . import _base, _lib
 
-SURF_GPU_MISSING = ("backend='gpu', but no HIP-enabled GPU is available "
-                    "(this build targets AMD MI355X / gfx950).")
+# reference wording (SURF.py:342, matched by tests/test_surf.py:130) kept as a
+# substring
+SURF_GPU_MISSING = ("backend='gpu', but no CUDA-enabled GPU is available. In this build: no "
+                    "HIP-enabled GPU is available (it targets AMD MI355X / gfx950).")
 
 
-def surf_inputs(X, discrete_limit, where):
+def surf_inputs(X, discrete_limit, where, device=0):
     """SURF.fit's preprocessing after validation (SURF.py:347-355): discrete
     detection and reciprocal ranges (discrete and constant columns -> 1),
     computed on ``where``.  Returns (is_discrete, recip f32)."""
-    is_discrete, col_min, col_max = _base.column_preprocess(X, discrete_limit, where)
+    is_discrete, col_min, col_max = _base.column_preprocess(X, discrete_limit, where, device)
     feature_ranges = col_max - col_min
     feature_ranges[is_discrete] = 1.0
     feature_ranges[feature_ranges == 0] = 1.0

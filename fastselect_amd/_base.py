@@ -9,8 +9,11 @@ import numpy as np
 
 from . import _lib
 
-GPU_MISSING = ("backend='gpu' was selected, but no compatible GPU was found "
-               "(no HIP device is visible; this build targets AMD MI355X / gfx950).")
+# The reference's wording is kept as a substring (MultiSURF.py:400-403;
+# callers match it, tests/test_multisurf.py:176), followed by what it means here.
+GPU_MISSING = ("backend='gpu' was selected, but no compatible NVIDIA GPU was found or CUDA "
+               "toolkit is not installed -- in this build: no compatible GPU was found (no HIP "
+               "device is visible; it targets AMD MI355X / gfx950).")
 
 
 def resolve_n_select(name: str, backend: str, n_features_to_select, n_samples: int,
@@ -83,18 +86,19 @@ def effective_backend(backend: str) -> str:
     return backend
 
 
-def column_preprocess(x: np.ndarray, discrete_limit, backend: str):
+def column_preprocess(x: np.ndarray, discrete_limit, backend: str, device: int = 0):
     """The per-column preprocessing of the reference's fit(): returns
     (is_discrete, colmin, colmax) with is_discrete[f] =
     ``np.unique(x[:, f]).size <= discrete_limit`` (MultiSURF.py:416-420,
     ReliefF.py:366-368, SURF.py:347-350) and colmin / colmax = x.min(0) /
     x.max(0) in x's dtype.  Computed by ``fs_column_stats`` on the device the
-    estimator scores on ('gpu': HIP kernels; 'cpu': native threads)."""
+    estimator scores on ('gpu': HIP kernels on ``device``; 'cpu': native
+    threads)."""
     cap = max(0, int(np.floor(discrete_limit)))
     where = backend
     if where == "gpu" and cap > _lib.GPU_STATS_MAX_CAP:
         where = "cpu"  # hash set beyond the GPU kernel's LDS table
-    mn, mx, nd = _lib.column_stats(where, x, cap)
+    mn, mx, nd = _lib.column_stats(where, x, cap, device=device)
     return nd <= discrete_limit, mn, mx
 
 

@@ -38,10 +38,10 @@ _vp = ctypes.c_void_p
 EXPORTED = (
     "fs_version", "fs_last_error", "fs_device_count", "fs_device_cache_release",
     "fs_stage_x", "fs_unstage_x", "fs_all_finite",
-    "fs_column_stats", "fs_multisurf_score",
+    "fs_column_stats", "fs_multisurf_score", "fs_multisurf_score_rows",
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
-    "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2",
+    "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_set_rows",
     "fs_plan_info", "fs_plan_weighted_pairs", "fs_plan_kernel_ms", "fs_plan_destroy",
 )
 
@@ -82,6 +82,9 @@ def _load() -> ctypes.CDLL:
     lib.fs_column_stats.argtypes = [_int, _int, _vp, _int, _i64, _i64, _i64, _vp, _vp, _i64p]
     lib.fs_multisurf_score.argtypes = [_int, _int, _f32p, _i64, _i64, _f64p, _f32p, _i64p, _i64,
                                        _int, _u8p, _int, _f32p]
+    lib.fs_multisurf_score_rows.argtypes = [_int, _int, _f32p, _i64, _i64, _f64p, _f32p, _i64p,
+                                            _i64, _int, _u8p, _int, _i64, _i64, _f64p]
+    lib.fs_plan_set_rows.argtypes = [_vp, _i64, _i64]
     lib.fs_relieff_score.argtypes = [_int, _int, _f32p, _i64, _i64, _i32p, _f32p, _u8p, _i64,
                                      _f32p, _i64, _int, _f32p]
     lib.fs_surf_score.argtypes = [_int, _int, _f64p, _i64, _i64, _i32p, _f32p, _int, _u8p, _int,
@@ -109,7 +112,8 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_kernel_ms.argtypes = [_vp, _int]
     lib.fs_plan_kernel_ms.restype = ctypes.c_double
     lib.fs_plan_destroy.argtypes = [_vp]
-    for name in ("fs_column_stats", "fs_multisurf_score", "fs_relieff_score", "fs_surf_score",
+    for name in ("fs_column_stats", "fs_multisurf_score", "fs_multisurf_score_rows",
+                 "fs_plan_set_rows", "fs_relieff_score", "fs_surf_score",
                  "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create",
                  "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
                  "fs_plan_pass2", "fs_plan_info", "fs_plan_weighted_pairs", "fs_plan_destroy"):
@@ -235,8 +239,13 @@ def column_stats(backend, x, count_cap, device=0):
     return mn, mx, nd
 
 
-def multisurf_score(backend, x, y, recip, feat_idx, use_star, is_discrete, n_jobs=-1, device=0):
-    """Drop-in for ``_multisurf_{cpu,gpu}_host_caller`` (MultiSURF.py:147-162, 256-270)."""
+def multisurf_score(backend, x, y, recip, feat_idx, use_star, is_discrete, n_jobs=-1, device=0,
+                    rows=None):
+    """Drop-in for ``_multisurf_{cpu,gpu}_host_caller`` (MultiSURF.py:147-162, 256-270).
+
+    rows=(begin, end): float64 score sums of those focal samples only
+    (``fs_multisurf_score_rows``) instead of float32 scores / n.
+    """
     x = np.ascontiguousarray(x, dtype=np.float32)
     n, p = x.shape
     yv = np.ascontiguousarray(y, dtype=np.float64)
@@ -244,6 +253,14 @@ def multisurf_score(backend, x, y, recip, feat_idx, use_star, is_discrete, n_job
     isd = np.ascontiguousarray(is_discrete, dtype=np.uint8)
     fidx = None if feat_idx is None else np.ascontiguousarray(feat_idx, dtype=np.int64)
     n_kept = p if fidx is None else fidx.size
+    if rows is not None:
+        sums = np.zeros(n_kept, dtype=np.float64)
+        check(_lib.fs_multisurf_score_rows(_backend_code(backend), int(device), _p(x, _f32p), n, p,
+                                           _p(yv, _f64p), _p(rc_, _f32p),
+                                           None if fidx is None else _p(fidx, _i64p), n_kept,
+                                           int(bool(use_star)), _p(isd, _u8p), int(n_jobs),
+                                           int(rows[0]), int(rows[1]), _p(sums, _f64p)))
+        return sums
     out = np.zeros(n_kept, dtype=np.float32)
     check(_lib.fs_multisurf_score(_backend_code(backend), int(device), _p(x, _f32p), n, p,
                                   _p(yv, _f64p), _p(rc_, _f32p),
@@ -342,6 +359,11 @@ class Plan:
 
     def pass2(self, counts_ptr: int, scores_ptr: int) -> None:
         check(_lib.fs_plan_pass2(self._h, _vp(counts_ptr), _vp(scores_ptr)))
+
+    def set_rows(self, begin: int, end: int) -> None:
+        """Score only the focal samples [begin, end) in the next pass2
+        (``fs_plan_set_rows``; MultiSURF plans)."""
+        check(_lib.fs_plan_set_rows(self._h, int(begin), int(end)))
 
     def info(self):
         """(owned tiles, pair-feature evaluations per step, pairs refined last step)."""

@@ -133,9 +133,37 @@ int fs_multisurf_score(int backend, int device, const float* x, int64_t n, int64
   std::vector<double> rs(3 * n), cnt(2 * n), S(P.n_kept);
   cpu::multisurf_pass1(P, x, 0, 1, n_jobs, st, rs.data());
   cpu::multisurf_select(P, x, 0, 1, rs.data(), n_jobs, st, cnt.data());
-  cpu::multisurf_pass2(P, st, cnt.data(), 0, 1, n_jobs, S.data());
+  cpu::multisurf_pass2(P, st, cnt.data(), 0, 1, n_jobs, 0, n, S.data());
   for (int64_t k = 0; k < P.n_kept; k++) scores_out[k] = (float)(S[k] / (double)n);
   return FS_OK;
+}
+
+int fs_multisurf_score_rows(int backend, int device, const float* x, int64_t n, int64_t p,
+                            const double* y, const float* recip, const int64_t* feat_idx,
+                            int64_t n_kept, int use_star, const uint8_t* is_discrete, int n_jobs,
+                            int64_t row_begin, int64_t row_end, double* sums_out) {
+  if (!sums_out) {
+    set_error("sums_out is NULL");
+    return FS_EINVAL;
+  }
+  if (!(0 <= row_begin && row_begin <= row_end && row_end <= n)) {
+    set_error("row range must satisfy 0 <= row_begin <= row_end <= n");
+    return FS_EINVAL;
+  }
+  int rc = check_backend(backend, device);
+  if (rc != FS_OK) return rc;
+  Prepared P;
+  rc = prepare(P, ALGO_MULTISURF, x, 0, n, p, feat_idx, n_kept, recip, is_discrete, n_jobs,
+               backend == FS_BACKEND_GPU);
+  if (rc) return map_prep_rc(rc);
+  if (encode_labels_f64(P, y)) return FS_EINVAL;
+  P.use_star = use_star ? 1 : 0;
+  if (backend == FS_BACKEND_GPU) return gpu::multisurf_rows(P, x, device, row_begin, row_end, sums_out);
+  cpu::CpuState st;
+  std::vector<double> rs(3 * n), cnt(2 * n);
+  cpu::multisurf_pass1(P, x, 0, 1, n_jobs, st, rs.data());
+  cpu::multisurf_select(P, x, 0, 1, rs.data(), n_jobs, st, cnt.data());
+  return cpu::multisurf_pass2(P, st, cnt.data(), 0, 1, n_jobs, row_begin, row_end, sums_out);
 }
 
 // Shared by the one-shot and the row-range entry points: validate, prepare,
@@ -259,7 +287,7 @@ struct fs_plan {
   int backend = FS_BACKEND_CPU;
   int rank = 0, world = 1, n_jobs = -1;
   int x_is_f64 = 0;
-  int64_t r_lo = 0, r_hi = 0;   // ReliefF / SURF plans: focal rows
+  int64_t r_lo = 0, r_hi = 0;   // focal rows (MultiSURF: fs_plan_set_rows, else [0, n))
   Prepared P;
   Prepared P0;                  // as created (all columns): discrete tables for re-targeting
   gpu::Plan* g = nullptr;
@@ -304,6 +332,8 @@ int fs_plan_create(fs_plan** plan_out, int backend, int device, const float* x, 
     return FS_EINVAL;
   }
   pl->P.use_star = use_star ? 1 : 0;
+  pl->r_lo = 0;
+  pl->r_hi = n;
   if (backend == FS_BACKEND_GPU) {
     rc = gpu::plan_create(&pl->g, pl->P, x, 0, device, rank, world, stream);
     if (rc != FS_OK) {
@@ -486,7 +516,27 @@ int fs_plan_pass2(fs_plan* pl, const double* counts, double* scores) {
   }
   if (!is_multisurf_plan(pl)) return FS_EINVAL;
   if (pl->g) return gpu::plan_pass2(pl->g, counts, scores);
-  return cpu::multisurf_pass2(pl->P, pl->st, counts, pl->rank, pl->world, pl->n_jobs, scores);
+  return cpu::multisurf_pass2(pl->P, pl->st, counts, pl->rank, pl->world, pl->n_jobs, pl->r_lo,
+                              pl->r_hi, scores);
+}
+
+int fs_plan_set_rows(fs_plan* pl, int64_t row_begin, int64_t row_end) {
+  if (!pl) {
+    set_error("plan is NULL");
+    return FS_EINVAL;
+  }
+  if (!is_multisurf_plan(pl)) return FS_EINVAL;
+  if (!(0 <= row_begin && row_begin <= row_end && row_end <= pl->P.n)) {
+    set_error("row range must satisfy 0 <= row_begin <= row_end <= n");
+    return FS_EINVAL;
+  }
+  if (pl->g) {
+    const int rc = gpu::plan_set_rows(pl->g, row_begin, row_end);
+    if (rc != FS_OK) return rc;
+  }
+  pl->r_lo = row_begin;
+  pl->r_hi = row_end;
+  return FS_OK;
 }
 
 int fs_plan_info(const fs_plan* pl, int64_t* owned_tiles_out, double* pfe,

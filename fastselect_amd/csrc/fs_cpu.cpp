@@ -308,7 +308,7 @@ static void scatter_scores(const Prepared& P, const std::vector<double>& S_perm,
 }
 
 int multisurf_pass2(const Prepared& P, const CpuState& S, const double* counts, int rank,
-                    int world, int n_jobs, double* scores) {
+                    int world, int n_jobs, int64_t r_lo, int64_t r_hi, double* scores) {
   const int64_t n = P.n, nb = P.n_pad / kTile;
   std::vector<PairW> pairs;
   for (int64_t i = 0; i < n; i++)
@@ -317,9 +317,13 @@ int multisurf_pass2(const Prepared& P, const CpuState& S, const double* counts, 
       const double d = S.D[(size_t)i * n + j];
       const bool hit = P.labels[i] == P.labels[j];
       const double wi =
-          multisurf_weight(d < S.thr[i], hit, P.use_star, counts[2 * i], counts[2 * i + 1]);
+          (i >= r_lo && i < r_hi)
+              ? multisurf_weight(d < S.thr[i], hit, P.use_star, counts[2 * i], counts[2 * i + 1])
+              : 0.0;
       const double wj =
-          multisurf_weight(d < S.thr[j], hit, P.use_star, counts[2 * j], counts[2 * j + 1]);
+          (j >= r_lo && j < r_hi)
+              ? multisurf_weight(d < S.thr[j], hit, P.use_star, counts[2 * j], counts[2 * j + 1])
+              : 0.0;
       const float w = (float)(wi + wj);
       if (w != 0.0f) pairs.push_back({(int32_t)i, (int32_t)j, w});
     }

@@ -2679,6 +2679,16 @@ int plan_pass2(Plan* g, const double* counts, double* scores) {
   return FS_OK;
 }
 
+int plan_set_rows(Plan* g, int64_t r_lo, int64_t r_hi) {
+  if (g->P.algo != ALGO_MULTISURF) {
+    set_error("focal-row slices of a plan are MultiSURF-only (ReliefF / SURF: row plans)");
+    return FS_EINVAL;
+  }
+  g->r_lo = r_lo;
+  g->r_hi = r_hi;
+  return FS_OK;
+}
+
 int plan_info(const Plan* g, int64_t* tiles, double* pfe, int64_t* refined) {
   if (tiles) *tiles = g->n_tiles;
   if (pfe) {
@@ -2744,6 +2754,23 @@ static int copy_sums(Plan* g, const double* sums_dev, double* sums_out) {
   FS_HIP(hipMemcpyAsync(sums_out, sums_dev, sizeof(double) * g->P.n_kept, hipMemcpyDeviceToHost,
                         g->stream));
   FS_HIP(hipStreamSynchronize(g->stream));
+  return FS_OK;
+}
+
+int multisurf_rows(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
+                   double* sums_out) {
+  Plan* g = nullptr;
+  FS_TRY(plan_create(&g, P, x, 0, device, 0, 1, 0));
+  double *rs = nullptr, *cnt = nullptr, *sc = nullptr;
+  int rc;
+  if ((rc = plan_set_rows(g, r_lo, r_hi)) || (rc = dalloc(g, &rs, 3 * P.n)) ||
+      (rc = dalloc(g, &cnt, 2 * P.n)) || (rc = dalloc(g, &sc, P.n_kept)) ||
+      (rc = plan_pass1(g, rs)) || (rc = plan_select(g, rs, cnt)) ||
+      (rc = plan_pass2(g, cnt, sc)) || (rc = copy_sums(g, sc, sums_out))) {
+    plan_destroy(g);
+    return rc;
+  }
+  plan_destroy(g);
   return FS_OK;
 }
 

@@ -249,8 +249,10 @@ int multisurf_pass1(const Prepared& P, const void* x, int rank, int world, int n
                     CpuState& S, double* rowstats);
 int multisurf_select(const Prepared& P, const void* x, int rank, int world,
                      const double* rowstats, int n_jobs, CpuState& S, double* counts);
+// Score sums of the focal samples [r_lo, r_hi) only (each pair side counts
+// for its own focal sample; [0, n) = the whole fit).
 int multisurf_pass2(const Prepared& P, const CpuState& S, const double* counts, int rank,
-                    int world, int n_jobs, double* scores);
+                    int world, int n_jobs, int64_t r_lo, int64_t r_hi, double* scores);
 // Score sums (not divided by n) of the focal samples [r_lo, r_hi).
 int surf_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int64_t r_hi,
              double* scores);
@@ -299,6 +301,9 @@ int plan_set_features(Plan* g, const Prepared& P);
 int plan_pass1(Plan* g, double* rowstats_dev);
 int plan_select(Plan* g, const double* rowstats_dev, double* counts_dev);
 int plan_pass2(Plan* g, const double* counts_dev, double* scores_dev);
+// MultiSURF focal-sample slice: the next pass2 sums the pair sides of the
+// focal samples [r_lo, r_hi) only (thresholds and counts stay global).
+int plan_set_rows(Plan* g, int64_t r_lo, int64_t r_hi);
 // ReliefF / SURF plans: float64 score sums of the plan's focal rows
 // (sums_dev[n_kept], device memory), for the plan's current feature subset.
 int plan_score(Plan* g, double* sums_dev);
@@ -310,6 +315,9 @@ void plan_destroy(Plan* g);
 // by n.  SURF / ReliefF: float64 score sums of the focal samples [r_lo, r_hi)
 // (row sharding; the full range gives the single-GPU result times n).
 int multisurf_run(const Prepared& P, const void* x, int device, float* scores_out);
+// MultiSURF float64 score sums of the focal samples [r_lo, r_hi).
+int multisurf_rows(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
+                   double* sums_out);
 int surf_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
              double* sums_out);
 int relieff_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,

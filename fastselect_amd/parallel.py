@@ -34,11 +34,12 @@ def _dist():
     return None, 0, 1
 
 
-def prepare_inputs(X, y, discrete_limit: int = 10, backend: str = "cpu"):
+def prepare_inputs(X, y, discrete_limit: int = 10, backend: str = "cpu", device: int = 0):
     """The preprocessing of ``MultiSURF.fit`` (MultiSURF.py:384-420), with the
-    column statistics computed on ``backend``."""
+    column statistics computed on ``backend`` (GPU: on ``device``, the rank's
+    own GPU)."""
     x = np.ascontiguousarray(X, dtype=np.float32)
-    isd, mn, mx = _base.column_preprocess(x, discrete_limit, backend)
+    isd, mn, mx = _base.column_preprocess(x, discrete_limit, backend, device)
     ranges = (mx - mn).astype(np.float32)
     ranges[ranges == 0] = 1
     recip = (1.0 / ranges).astype(np.float32)
@@ -54,7 +55,7 @@ class ShardedMultiSURF:
     """
 
     def __init__(self, x, y, recip, is_discrete, use_star=False, backend="gpu", device=0,
-                 shard=True):
+                 shard=True, rows=None):
         import torch
         self.dist, self.rank, self.world = _dist() if shard else (None, 0, 1)
         self.n, self.p = x.shape
@@ -68,6 +69,8 @@ class ShardedMultiSURF:
             stream = 0
         self.plan = _lib.Plan(backend, x, y, recip, is_discrete, use_star=use_star,
                               rank=self.rank, world=self.world, device=device, stream=stream)
+        if rows is not None:  # focal-sample slice: pass 2 sums those samples only
+            self.plan.set_rows(*rows)
         f64 = torch.float64
         self.rowstats = torch.zeros(3 * self.n, dtype=f64, device=self.tdev)
         self.counts = torch.zeros(2 * self.n, dtype=f64, device=self.tdev)
@@ -83,7 +86,9 @@ class ShardedMultiSURF:
             self.scores = torch.zeros(n_kept, dtype=torch.float64, device=self.tdev)
 
     def _allreduce(self, t):
-        if self.dist is not None and self.world > 1:
+        # issued whenever a process group is up, world 1 included (one RCCL
+        # call per exchange point; a plain single-process job has none)
+        if self.dist is not None:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
 
     def step(self):
@@ -106,13 +111,18 @@ class ShardedMultiSURF:
         return self.plan.kernel_ms(which)
 
     def close(self):
+        """Free the plan and hand its device blocks back to the device:
+        torch's caching allocator shares the GPU with this job and cannot
+        reclaim blocks held in the library's cache (fs_device_cache_release)."""
         self.plan.close()
+        if self.backend == "gpu":
+            _lib.release_device_cache()
 
 
 def multisurf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", device=0):
     """Score X on this rank's share of the tiles and return the full float32
     score vector (identical on every rank)."""
-    x, yv, recip, isd = prepare_inputs(X, y, discrete_limit, backend)
+    x, yv, recip, isd = prepare_inputs(X, y, discrete_limit, backend, device)
     job = ShardedMultiSURF(x, yv, recip, isd, use_star=use_star, backend=backend, device=device)
     try:
         s = job.step()
@@ -163,7 +173,7 @@ def relieff_scores(X, y, n_neighbors=3, discrete_limit=10, backend="gpu", device
     if np.unique(yv).size < 2:
         return np.zeros(p, dtype=np.float32)
     backend = _base.effective_backend(backend)
-    x32, y_enc, recip, isd, priors = relieff_inputs(x, yv, discrete_limit, backend)
+    x32, y_enc, recip, isd, priors = relieff_inputs(x, yv, discrete_limit, backend, device, n_jobs)
     _, rank, world = _dist()
     sums = _lib.relieff_score(backend, x32, y_enc, recip, isd, n_neighbors, priors, n_jobs,
                               device=device, rows=shard_rows(n, rank, world))
@@ -177,7 +187,7 @@ def surf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", device=0
     x = np.ascontiguousarray(X, dtype=np.float64)
     n, p = x.shape
     backend = _base.effective_backend(backend)
-    isd, recip = surf_inputs(x, discrete_limit, backend)
+    isd, recip = surf_inputs(x, discrete_limit, backend, device)
     _, rank, world = _dist()
     sums = _lib.surf_score(backend, x, np.asarray(y).astype(np.int32), recip, use_star, isd,
                            n_jobs, device=device, rows=shard_rows(n, rank, world))

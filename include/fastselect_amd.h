@@ -108,6 +108,24 @@ FS_API int fs_multisurf_score(int backend, int device, const float* x, int64_t n
                        float* scores_out);
 
 /*
+ * MultiSURF / MultiSURF* score SUMS (not divided by n) of the focal samples
+ * [row_begin, row_end) only, written to sums_out[n_kept] (host memory).
+ * The reference's kernel is a prange over focal samples whose rows are
+ * independent once each sample's threshold is known (MultiSURF.py:174-251):
+ * thresholds and neighbour counts stay those of the whole fit, and each pair
+ * contributes only the side of its focal sample inside the range.  Summing
+ * the vectors of a partition of [0, n) and dividing by n gives the one-shot
+ * scores up to float64 summation order; [0, 384) of the reference's
+ * per-sample rows is the same as oracle i_range=(0, 384).  Other arguments as
+ * fs_multisurf_score.
+ */
+FS_API int fs_multisurf_score_rows(int backend, int device, const float* x, int64_t n,
+                                   int64_t p, const double* y, const float* recip,
+                                   const int64_t* feat_idx, int64_t n_kept, int use_star,
+                                   const uint8_t* is_discrete, int n_jobs, int64_t row_begin,
+                                   int64_t row_end, double* sums_out);
+
+/*
  * ReliefF feature scores (ReliefF.py:137-236).
  *   x            [n][p] float32 (the float32 cast of the float64-validated X, ReliefF.py:400)
  *   y_enc        [n] int32 class codes in [0, n_classes) (ReliefF.py:375)
@@ -218,6 +236,10 @@ FS_API int fs_plan_select(fs_plan* plan, const double* rowstats, double* counts)
 /* Stage 3: pair weights from the all-reduced counts[2n]; partial per-feature
  * score sums (NOT divided by n) -> scores[n_kept], in feat_idx order. */
 FS_API int fs_plan_pass2(fs_plan* plan, const double* counts, double* scores);
+/* Restrict the next pass2 of a MultiSURF plan to the focal samples
+ * [row_begin, row_end) (as fs_multisurf_score_rows; a new plan scores
+ * [0, n)).  pass1 / select are unchanged: thresholds and counts are global. */
+FS_API int fs_plan_set_rows(fs_plan* plan, int64_t row_begin, int64_t row_end);
 /*
  * ReliefF / SURF plans (resident scoring): X uploaded once (GPU) or copied
  * (CPU), arguments as fs_relieff_score / fs_surf_score, focal samples

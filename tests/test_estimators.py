@@ -107,6 +107,11 @@ def test_gpu_backend_without_gpu(ms_data, rs_data):
         SURF(backend="gpu").fit(*rs_data)
     with pytest.raises(RuntimeError, match="no compatible GPU"):
         ReliefF(backend="gpu", n_neighbors=1).fit(*rs_data)
+    # the reference tests' own patterns still match (drop-in callers)
+    with pytest.raises(RuntimeError, match="no compatible NVIDIA GPU"):
+        MultiSURF(backend="gpu", n_features_to_select=2).fit(*ms_data)
+    with pytest.raises(RuntimeError, match="no CUDA-enabled GPU is available"):
+        SURF(backend="gpu").fit(*rs_data)
 
 
 @pytest.mark.parametrize("est", [MultiSURF, SURF])

@@ -1,0 +1,132 @@
+"""Parity at BASELINE.json's full sizes (north-star target).
+
+Each case regenerates one BASELINE configuration on the GPU box, checks that
+the input is bit-identical to the one the oracle scored (sha256 of X), runs
+the default GPU path through the C ABI and compares with the committed oracle
+scores of ``tests/golden/fullsize_*.npz`` (made in the container by
+``tests/golden/make_fullsize.py`` with the C restatement of the reference's
+backend='cpu' kernels, oracle/relief_oracle.c).
+
+Bar (BASELINE north_star): max_f |s_f - s_ref_f| <= 1e-5 *
+max_f |s_ref_f| and identical top-10 index sets (the reference ranks with
+np.argsort(scores)[::-1][:k], MultiSURF.py:443).  Slices compare the sums of
+the same focal samples (the reference's per-sample rows summed over
+i_range, / n).
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import assert_parity
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+TOL = 1e-5
+TOPK = 10
+
+_DATA = {}
+
+
+def _fixture(name):
+    path = os.path.join(GOLD, f"fullsize_{name}.npz")
+    if not os.path.exists(path):
+        pytest.fail(f"missing fixture {path} (tests/golden/make_fullsize.py)")
+    return np.load(path, allow_pickle=False)
+
+
+def _data(n, p, red):
+    key = (n, p, red)
+    if key not in _DATA:
+        from sklearn.datasets import make_classification
+        _DATA.clear()  # one configuration resident at a time (cfg5 X is 4 GB)
+        _DATA[key] = make_classification(n_samples=n, n_features=p, n_informative=20,
+                                         n_redundant=red, random_state=42)
+    return _DATA[key]
+
+
+def _inputs(fx):
+    n, p, red = int(fx["n"]), int(fx["p"]), int(fx["n_redundant"])
+    X, y = _data(n, p, red)
+    algo = str(fx["algo"])
+    x = X if algo == "surf" else X.astype(np.float32)
+    dig = hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest()
+    assert dig == str(fx["x_sha256"]), "regenerated X differs from the one the oracle scored"
+    assert int(np.asarray(y).sum()) == int(fx["y_sum"])
+    return X, y
+
+
+@pytest.fixture(scope="module")
+def lib():
+    import fastselect_amd
+    from fastselect_amd import _lib
+    if _lib.device_count() < 1:
+        pytest.fail("no HIP device visible")
+    return fastselect_amd
+
+
+def test_cfg2_multisurf_whole_fit(lib):
+    fx = _fixture("cfg2_multisurf")
+    X, y = _inputs(fx)
+    est = lib.MultiSURF(backend="gpu", n_features_to_select=TOPK).fit(X, y)
+    assert est.effective_backend_ == "gpu"
+    assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
+
+
+def test_cfg3_relieff_k10_whole_fit(lib):
+    fx = _fixture("cfg3_relieff_k10")
+    X, y = _inputs(fx)
+    est = lib.ReliefF(backend="gpu", n_neighbors=10, n_features_to_select=TOPK).fit(X, y)
+    assert est.effective_backend_ == "gpu"
+    assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
+
+
+def test_cfg4_multisurf_north_star(lib):
+    """BASELINE north_star: MultiSURF on 20000 x 20000 fp32, default GPU
+    path (16-bit pass-1 operands), scores within 1e-5 and identical top-k."""
+    fx = _fixture("cfg4_multisurf")
+    X, y = _inputs(fx)
+    est = lib.MultiSURF(backend="gpu", n_features_to_select=TOPK).fit(X, y)
+    assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
+    assert set(est.top_features_.tolist()) == set(np.argsort(fx["scores"])[::-1][:TOPK].tolist())
+
+
+def test_cfg4_multisurf_focal_slices_partition(lib):
+    """fs_multisurf_score_rows on a partition of the focal samples sums to
+    the whole fit's scores (the reference's prange rows are independent)."""
+    from fastselect_amd import _lib
+    from fastselect_amd.parallel import prepare_inputs
+    fx = _fixture("cfg4_multisurf")
+    X, y = _inputs(fx)
+    x, yv, recip, isd = prepare_inputs(X, y, backend="gpu")
+    n = x.shape[0]
+    parts = [(0, 6400), (6400, 13001), (13001, n)]
+    sums = sum(_lib.multisurf_score("gpu", x, yv, recip, None, False, isd, rows=r)
+               for r in parts)
+    assert_parity((sums / n).astype(np.float32), fx["scores"], TOL, TOPK)
+
+
+def test_cfg5_multisurfstar_whole_fit(lib):
+    fx = _fixture("cfg5_multisurfstar")
+    X, y = _inputs(fx)
+    est = lib.MultiSURF(backend="gpu", use_star=True, n_features_to_select=TOPK).fit(X, y)
+    assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
+
+
+@pytest.mark.parametrize("name", ["cfg5_surfstar_slice", "cfg5_surf_slice"])
+def test_cfg5_surf_focal_slice(lib, name):
+    """SURF / SURF* at 10000 x 50000: the oracle's focal-sample slice
+    (SURF.py:131-195 over i_range) against fs_surf_score_rows."""
+    from fastselect_amd import _lib
+    from fastselect_amd.SURF import surf_inputs
+    fx = _fixture(name)
+    X, y = _inputs(fx)
+    x = np.ascontiguousarray(X, dtype=np.float64)
+    isd, recip = surf_inputs(x, 10, "gpu")
+    lo, hi = (int(v) for v in fx["i_range"])
+    sums = _lib.surf_score("gpu", x, np.asarray(y).astype(np.int32), recip,
+                           bool(fx["use_star"]), isd, rows=(lo, hi))
+    assert_parity((sums / x.shape[0]).astype(np.float32), fx["scores"], TOL)

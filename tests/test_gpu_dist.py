@@ -1,0 +1,66 @@
+"""RCCL (torch.distributed 'nccl' backend) on the GPU box.
+
+The box has one MI355X, so the collective path runs at world 1: the process
+group is up, every exchange point of ShardedMultiSURF.step() (rowstats,
+counts, scores) goes through dist.all_reduce over RCCL, and the result must
+equal the single-device C-ABI call bit for bit (an all-reduce over one rank
+is the identity).  N > 1 is covered by the gloo tests (tests/test_bench.py,
+test_parity_cpu.py, test_rows.py) and the driver's multi-GPU bench.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_nccl_world1_step_matches_one_shot():
+    import torch
+    import torch.distributed as dist
+    from sklearn.datasets import make_classification
+
+    from fastselect_amd import _lib
+    from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_port())
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        assert dist.get_backend() == "nccl"
+        X, y = make_classification(n_samples=1500, n_features=700, n_informative=20,
+                                   n_redundant=40, random_state=5)
+        x, yv, recip, isd = prepare_inputs(X, y, backend="gpu", device=0)
+        job = ShardedMultiSURF(x, yv, recip, isd, backend="gpu", device=0)
+        assert job.dist is not None and job.world == 1
+        s = job.step().cpu().numpy()
+        job.close()
+        ref = _lib.multisurf_score("gpu", x, yv, recip, None, False, isd)
+        np.testing.assert_array_equal(s, ref)
+        # the one-call RCCL all-reduce helper of the row-sharded algorithms
+        from fastselect_amd import parallel
+        v = np.arange(7, dtype=np.float64)
+        np.testing.assert_array_equal(parallel._allreduce_sums(v, "gpu", 0), v)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_column_stats_run_on_the_ranks_device():
+    """prepare_inputs(device=d) computes the column statistics on GPU d
+    (they used to default to GPU 0 on every rank)."""
+    import torch
+    from fastselect_amd.parallel import prepare_inputs
+    d = torch.cuda.device_count() - 1
+    X = np.random.default_rng(0).normal(size=(300, 50))
+    x, _, recip, isd = prepare_inputs(X, np.arange(300) % 2, backend="gpu", device=d)
+    rng = (x.max(0) - x.min(0)).astype(np.float32)
+    np.testing.assert_array_equal(recip, (1.0 / rng).astype(np.float32))
+    assert not isd.any()
