@@ -46,9 +46,15 @@ def validate_xy(est, x, y, dtype, n_jobs=-1):
     element-wise finiteness scan of X (~56 ms at cfg4) replaced by
     ``fs_all_finite`` on host threads.  When X holds a NaN or an infinity the
     plain call runs again and raises scikit-learn's own error, so behaviour and
-    messages are unchanged.  Returns C-contiguous X."""
+    messages are unchanged.  A float64 ndarray bound for float32 is cast by
+    ``to_float32`` (the same rounding, over host threads: scikit-learn's cast
+    is one thread, ~0.2 s at cfg4).  Returns C-contiguous X."""
     from sklearn.utils.validation import validate_data
-    xv, yv = validate_data(est, x, y, y_numeric=True, dtype=dtype, ensure_2d=True,
+    xc = x
+    if (dtype == np.float32 and isinstance(x, np.ndarray) and type(x) is np.ndarray
+            and x.dtype == np.float64 and x.ndim == 2):
+        xc = to_float32(x, n_jobs)
+    xv, yv = validate_data(est, xc, y, y_numeric=True, dtype=dtype, ensure_2d=True,
                            ensure_all_finite=False)
     xv = np.ascontiguousarray(xv)
     if xv.dtype in (np.float32, np.float64) and not _lib.all_finite(xv, n_jobs):

@@ -42,7 +42,8 @@ EXPORTED = (
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_set_rows",
-    "fs_plan_info", "fs_plan_weighted_pairs", "fs_plan_kernel_ms", "fs_plan_destroy",
+    "fs_plan_info", "fs_plan_calibration", "fs_plan_weighted_pairs", "fs_plan_kernel_ms",
+    "fs_plan_destroy",
 )
 
 
@@ -108,6 +109,7 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_select.argtypes = [_vp, _vp, _vp]
     lib.fs_plan_pass2.argtypes = [_vp, _vp, _vp]
     lib.fs_plan_info.argtypes = [_vp, _i64p, _f64p, _i64p]
+    lib.fs_plan_calibration.argtypes = [_vp, _f64p]
     lib.fs_plan_weighted_pairs.argtypes = [_vp, _i64p]
     lib.fs_plan_kernel_ms.argtypes = [_vp, _int]
     lib.fs_plan_kernel_ms.restype = ctypes.c_double
@@ -116,7 +118,8 @@ def _load() -> ctypes.CDLL:
                  "fs_plan_set_rows", "fs_relieff_score", "fs_surf_score",
                  "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create",
                  "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
-                 "fs_plan_pass2", "fs_plan_info", "fs_plan_weighted_pairs", "fs_plan_destroy"):
+                 "fs_plan_pass2", "fs_plan_info", "fs_plan_calibration", "fs_plan_weighted_pairs",
+                 "fs_plan_destroy"):
         getattr(lib, name).restype = _int
     return lib
 
@@ -373,6 +376,13 @@ class Plan:
         check(_lib.fs_plan_info(self._h, ctypes.byref(tiles), ctypes.byref(pfe),
                                 ctypes.byref(ref)))
         return int(tiles.value), float(pfe.value), int(ref.value)
+
+    def calibration(self) -> dict:
+        """Refinement-band calibration of the current layout (fs_plan_calibration)."""
+        v = (ctypes.c_double * 6)()
+        check(_lib.fs_plan_calibration(self._h, v))
+        return {"q16": bool(v[0]), "rms": v[1], "max": v[2], "model_sigma": v[3],
+                "band_vs_model": v[4], "guard": bool(v[5])}
 
     def weighted_pairs(self) -> int:
         """Owned pairs with a non-zero weight in the last pass 2 (-1: not counted)."""

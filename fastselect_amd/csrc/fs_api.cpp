@@ -1,6 +1,7 @@
 // fs_api.cpp -- the C ABI (include/fastselect_amd.h): argument validation,
 // backend dispatch, error reporting.  See the header for the reference
 // interface each entry point replaces.
+#include <cmath>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -551,6 +552,17 @@ int fs_plan_info(const fs_plan* pl, int64_t* owned_tiles_out, double* pfe,
   owned_tiles(pl->P.n_pad / kTile, pl->rank, pl->world, bi, bj);
   if (owned_tiles_out) *owned_tiles_out = (int64_t)bi.size();
   if (pfe) *pfe = 2.0 * (double)bi.size() * kTile * kTile * (double)(pl->P.pc + pl->P.pd);
+  return FS_OK;
+}
+
+int fs_plan_calibration(const fs_plan* pl, double* out) {
+  if (!pl || !out) {
+    set_error("NULL plan or output");
+    return FS_EINVAL;
+  }
+  if (pl->g) return gpu::plan_calibration(pl->g, out);
+  const double v[6] = {0.0, 0.0, 0.0, std::sqrt((double)pl->P.pc / 6.0 + 1.0), 1.0, 0.0};
+  for (int k = 0; k < 6; k++) out[k] = v[k];
   return FS_OK;
 }
 

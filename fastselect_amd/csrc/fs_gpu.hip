@@ -930,6 +930,44 @@ __global__ __launch_bounds__(256) void k_exact_pairs_rows(
   }
 }
 
+// Band calibration (calibrate_band): for each sampled pair, the quantised
+// distance's error against the reference's arithmetic, err = sum over the
+// continuous kept features of |q_i - q_j| - SC * f32(|x_i - x_j| * recip),
+// for the 16-bit scale (.x) and the 32-bit scale (.y).  q is formed exactly
+// as k_quantize forms it; discrete features contribute no error.  One wave
+// per pair, fixed-order reduction (every rank computes the same values).
+template <typename T>
+__global__ __launch_bounds__(256) void k_calib(
+    const T* __restrict__ x, int64_t p_in, int64_t pc, const int64_t* __restrict__ src_col,
+    const double* __restrict__ off, const double* __restrict__ qs16,
+    const double* __restrict__ qs32, const float* __restrict__ scl32, double sc16, double sc32,
+    const int2* __restrict__ pairs, int64_t npairs, double2* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const int64_t k = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  if (k >= npairs) return;
+  const int2 pr = pairs[k];
+  const T* xi = x + (int64_t)pr.x * p_in;
+  const T* xj = x + (int64_t)pr.y * p_in;
+  double e16 = 0.0, e32 = 0.0;
+  for (int64_t c = lane; c < pc; c += 64) {
+    const int64_t col = src_col[c];
+    const double a = (double)xi[col], b = (double)xj[col];
+    const double ua = __dadd_rn(a, -off[c]), ub = __dadd_rn(b, -off[c]);
+    const uint32_t qa16 = (uint32_t)__dadd_rn(__dmul_rn(ua, qs16[c]), 0.5);
+    const uint32_t qb16 = (uint32_t)__dadd_rn(__dmul_rn(ub, qs16[c]), 0.5);
+    const uint32_t qa32 = (uint32_t)__dadd_rn(__dmul_rn(ua, qs32[c]), 0.5);
+    const uint32_t qb32 = (uint32_t)__dadd_rn(__dmul_rn(ub, qs32[c]), 0.5);
+    const double ref = (double)(__builtin_fabsf((float)a - (float)b) * scl32[c]);
+    e16 += (qa16 > qb16 ? (double)(qa16 - qb16) : (double)(qb16 - qa16)) - sc16 * ref;
+    e32 += (qa32 > qb32 ? (double)(qa32 - qb32) : (double)(qb32 - qa32)) - sc32 * ref;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    e16 += __shfl_xor(e16, o);
+    e32 += __shfl_xor(e32, o);
+  }
+  if (lane == 0) err[k] = make_double2(e16, e32);
+}
+
 // Near hit / miss counts over the owned tiles (D now exact for ambiguous
 // pairs): counts[2i], counts[2i+1].
 __global__ __launch_bounds__(256) void k_tile_counts(const double* __restrict__ D, int64_t n,
@@ -1901,6 +1939,7 @@ struct Plan {
   int64_t nb = 0, n_tiles = 0, seg_len = 1, nseg = 1;
   int ksplit = 1;               // pass-1 K-split parts (k_dist)
   int use_q16 = 0;              // pass 1 on packed 16-bit continuous operands
+  double calib[6] = {0, 0, 0, 0, 1, 0};  // plan_calibration (calibrate_band)
   int64_t c_lo = 0, c_hi = 0;   // this rank's continuous columns of the mean correction
   int64_t r_lo = 0, r_hi = 0;   // focal rows scored by this plan (row sharding)
   double2* rspart = nullptr;    // per owned tile row-moment partials [tiles][256]
@@ -2258,6 +2297,133 @@ static int choose_sparse(const Plan* g, const Prepared& P) {
   return (g->r_hi - g->r_lo < P.n) ? 1 : 0;  // SURF / SURF*: only when row-sharded
 }
 
+// Refinement band from measured pairs.  The model band of finalize_scale
+// (12 standard deviations of sum_f sign(t_i - t_j)(eps_i - eps_j) for
+// independent per-column rounding) does not hold when the rounding errors of
+// different columns are correlated: duplicated or collinear columns, or
+// columns on one value grid, add their errors up coherently (up to pc units
+// instead of ~sqrt(pc/6)).  kCalibPairs sampled pairs (the same on every
+// rank: a fixed generator over [0, n)) get their quantised distance error
+// against the reference's arithmetic for both operand widths (k_calib).
+//  * 16-bit operands are given up (coherence guard) when the measured rms
+//    error exceeds kCoherence x the model's standard deviation: with errors
+//    that large the quantised threshold mu - sigma/2 drifts as well, and the
+//    32-bit operands make every error 256x smaller.  FS_Q16_GUARD=0 keeps them.
+//  * The band becomes max(model, 3 max|err| + rms/2): three times the largest
+//    sampled error covers the distance error (the model's 12 sigma is ~3.3x
+//    the expected maximum of 4096 Gaussian samples), and rms/2 bounds the
+//    spread term of the threshold (|sigma_q - sigma| <= rms_j(err_ij)).
+// For independent rounding this reproduces the model band (3 x ~3.7 sigma +
+// sigma/2 < 12 sigma), so ordinary data keeps its refinement cost.
+constexpr int64_t kCalibPairs = 4096;
+constexpr double kCoherence = 2.0;
+
+static int calibrate_band(Plan* g) {
+  Prepared& Q = g->P;
+  g->calib[0] = Q.q16;
+  g->calib[1] = g->calib[2] = 0.0;
+  g->calib[3] = std::sqrt((double)Q.pc / 6.0 + 1.0);
+  g->calib[4] = 1.0;
+  g->calib[5] = 0.0;
+  if (Q.algo == ALGO_SURF || Q.pc == 0 || Q.n < 2) return FS_OK;
+  const int64_t all_pairs = Q.n * (Q.n - 1) / 2;
+  const int64_t S = std::min<int64_t>(kCalibPairs, all_pairs);
+  std::vector<int2> pr((size_t)S);
+  uint64_t st = 0x9E3779B97F4A7C15ull ^ ((uint64_t)Q.n << 20) ^ (uint64_t)Q.pc;
+  auto next = [&]() {  // splitmix64
+    uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  for (int64_t k = 0; k < S; k++) {
+    const int64_t i = (int64_t)(next() % (uint64_t)Q.n);
+    int64_t j = (int64_t)(next() % (uint64_t)(Q.n - 1));
+    if (j >= i) j++;
+    pr[(size_t)k] = make_int2((int)std::min(i, j), (int)std::max(i, j));
+  }
+  const int q_now = Q.q16;
+  double sc[2];
+  for (int w = 0; w < 2; w++) {
+    if (set_integer_scale(Q, 1 - w)) return FS_EINVAL;
+    sc[w] = Q.SC;
+  }
+  if (set_integer_scale(Q, q_now)) return FS_EINVAL;
+  std::vector<double> qs((size_t)Q.PW * 2, 0.0);
+  for (int64_t c = 0; c < Q.pc; c++) {
+    qs[(size_t)c] = Q.scale[c] * sc[0];
+    qs[(size_t)(Q.PW + c)] = Q.scale[c] * sc[1];
+  }
+  int2* dpr = nullptr;
+  double* dqs = nullptr;
+  double2* derr = nullptr;
+  int rc = dev_alloc((void**)&dpr, sizeof(int2) * S, g->device);
+  if (!rc) rc = dev_alloc((void**)&dqs, sizeof(double) * qs.size(), g->device);
+  if (!rc) rc = dev_alloc((void**)&derr, sizeof(double2) * S, g->device);
+  std::vector<double2> err((size_t)S);
+  if (!rc && (hipMemcpyAsync(dpr, pr.data(), sizeof(int2) * S, hipMemcpyHostToDevice,
+                             g->stream) != hipSuccess ||
+              hipMemcpyAsync(dqs, qs.data(), sizeof(double) * qs.size(), hipMemcpyHostToDevice,
+                             g->stream) != hipSuccess))
+    rc = FS_EHIP;
+  if (!rc) {
+    const unsigned grid = (unsigned)((S + 3) / 4);
+    if (g->x_is_f64)
+      k_calib<double><<<grid, 256, 0, g->stream>>>((const double*)g->x, Q.p_in, Q.pc, g->src_col,
+                                                   g->off, dqs, dqs + Q.PW, g->scl32, sc[0],
+                                                   sc[1], dpr, S, derr);
+    else
+      k_calib<float><<<grid, 256, 0, g->stream>>>((const float*)g->x, Q.p_in, Q.pc, g->src_col,
+                                                  g->off, dqs, dqs + Q.PW, g->scl32, sc[0],
+                                                  sc[1], dpr, S, derr);
+    rc = launch_check("k_calib");
+  }
+  if (!rc && (hipMemcpyAsync(err.data(), derr, sizeof(double2) * S, hipMemcpyDeviceToHost,
+                             g->stream) != hipSuccess ||
+              hipStreamSynchronize(g->stream) != hipSuccess))
+    rc = FS_EHIP;
+  if (dpr) dev_free(dpr);
+  if (dqs) dev_free(dqs);
+  if (derr) dev_free(derr);
+  if (rc) {
+    (void)hipGetLastError();
+    if (rc == FS_EHIP) set_error("band calibration: HIP call failed");
+    return rc;
+  }
+  double ss[2] = {0.0, 0.0}, mx[2] = {0.0, 0.0};
+  for (const double2& e : err) {
+    const double v[2] = {e.x, e.y};
+    for (int w = 0; w < 2; w++) {
+      ss[w] += v[w] * v[w];
+      mx[w] = std::max(mx[w], std::fabs(v[w]));
+    }
+  }
+  const double rms[2] = {std::sqrt(ss[0] / (double)S), std::sqrt(ss[1] / (double)S)};
+  const double sigma = g->calib[3];
+  const char* guard = std::getenv("FS_Q16_GUARD");
+  if (Q.q16 && rms[0] > kCoherence * sigma && !(guard && *guard == '0')) {
+    g->use_q16 = 0;
+    g->calib[5] = 1.0;
+    if (set_integer_scale(Q, 0)) return FS_EINVAL;
+  }
+  const int w = Q.q16 ? 0 : 1;
+  const double band = (3.0 * mx[w] + 0.5 * rms[w]) / Q.SC;
+  Q.amb_delta = std::max(Q.amb_delta_model, band);
+  g->calib[0] = Q.q16;
+  g->calib[1] = rms[w];
+  g->calib[2] = mx[w];
+  g->calib[4] = Q.amb_delta / Q.amb_delta_model;
+  if (trace_on()) {
+    char msg[256];
+    snprintf(msg, sizeof msg,
+             "calibrate: rms16 %.1f max16 %.1f rms32 %.1f max32 %.1f model sigma %.1f -> q16 %d, "
+             "band x%.2f",
+             rms[0], mx[0], rms[1], mx[1], sigma, Q.q16, g->calib[4]);
+    trace_mark(msg);
+  }
+  return FS_OK;
+}
+
 // Feature-layout part of a plan: everything sized by the kept features
 // (permutation tables, quantised operands, pass-2 partials), rebuilt when
 // the plan is re-targeted to another feature subset (fs_plan_set_features).
@@ -2340,6 +2506,14 @@ static int plan_layout(Plan* g) {
       (rc = h2d(g, g->dtab_off, Q.dtab_off.data(), Q.PW + 1)) ||
       (rc = h2d(g, g->dtab, Q.dtab.data(), Q.dtab.size())))
     return rc;
+  if ((rc = calibrate_band(g))) return rc;
+  if (g->calib[5] != 0.0) {
+    // the coherence guard switched to 32-bit operands: new scale, histogram shift
+    for (int64_t c = 0; c < Q.PW; c++) qs[c] = Q.scale[c] * Q.SC;
+    g->rank_shift = 0;
+    while ((Q.qmax / std::ldexp(1.0, g->rank_shift)) >= (double)kRankBins) g->rank_shift++;
+    if ((rc = h2d(g, g->qs, qs.data(), Q.PW))) return rc;
+  }
   FS_HIP(hipStreamSynchronize(g->stream));
   return FS_OK;
 }
@@ -2697,6 +2871,11 @@ int plan_info(const Plan* g, int64_t* tiles, double* pfe, int64_t* refined) {
     *pfe = 2.0 * (double)g->n_tiles * kTile * kTile * (double)(g->P.pc + g->P.pd);
   }
   if (refined) *refined = g->n_refined;
+  return FS_OK;
+}
+
+int plan_calibration(const Plan* g, double* out) {
+  for (int k = 0; k < 6; k++) out[k] = g->calib[k];
   return FS_OK;
 }
 

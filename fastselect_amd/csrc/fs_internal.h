@@ -79,6 +79,8 @@ struct Prepared {
   // inside which a quantised near/far decision is not trusted; rows with a
   // pair in the band are recomputed with reference-exact arithmetic.
   double amb_delta = 0.0;
+  double amb_delta_model = 0.0;    // amb_delta of the independent-rounding model
+  double Rmax = 0.0;               // largest scaled continuous range (finalize_scale)
   double qmax = 0.0;               // largest quantised continuous value
   // 0 while the continuous column ranges are still to be measured (the GPU
   // backend measures them on the device, then calls finalize_scale)
@@ -108,6 +110,9 @@ int prepare(Prepared& P, int algo, const void* x, int x_is_f64, int64_t n, int64
 // Offsets, integer scale and error band from the per-permuted-column minima
 // and maxima of the continuous columns (c in [0, pc)).
 int finalize_scale(Prepared& P, const double* cmin, const double* cmax);
+// Integer scale, qmax and the model band for 16-bit (q16 = 1) or 32-bit
+// operands, from the ranges finalize_scale measured (P.Rmax).
+int set_integer_scale(Prepared& P, int q16);
 int encode_labels_f64(Prepared& P, const double* y);
 int encode_labels_i32(Prepared& P, const int32_t* y);
 
@@ -308,6 +313,12 @@ int plan_set_rows(Plan* g, int64_t r_lo, int64_t r_hi);
 // (sums_dev[n_kept], device memory), for the plan's current feature subset.
 int plan_score(Plan* g, double* sums_dev);
 int plan_info(const Plan* g, int64_t* tiles, double* pfe, int64_t* refined);
+// Band calibration of the plan's current layout: out[0] = 16-bit operands in
+// use, out[1] / out[2] = rms / max |error| of the sampled pairs' quantised
+// distances (integer units, final operand width), out[3] = the model's
+// standard deviation sqrt(pc/6 + 1), out[4] = band / model band, out[5] = 1
+// if the coherence guard turned 16-bit operands off.
+int plan_calibration(const Plan* g, double* out);
 double plan_kernel_ms(const Plan* g, int which);
 int plan_weighted_pairs(Plan* g, int64_t* pairs);
 void plan_destroy(Plan* g);

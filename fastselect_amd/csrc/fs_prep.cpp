@@ -195,6 +195,13 @@ int finalize_scale(Prepared& P, const double* cmin, const double* cmax) {
     }
     R = r > R ? r : R;
   }
+  P.Rmax = R;
+  return set_integer_scale(P, P.q16);
+}
+
+int set_integer_scale(Prepared& P, int q16) {
+  P.q16 = q16;
+  const double R = P.Rmax;
   // Integer distance scale.  Per-feature |q_a - q_b| <= Rm*SC + 1 must keep
   // (a) a 256-feature window on top of a 24-bit remainder inside u32 and
   // (b) the whole distance below 2^40 (16-bit high part above bit 24).
@@ -218,9 +225,13 @@ int finalize_scale(Prepared& P, const double* cmin, const double* cmax) {
   // rounding (< 1.2e-7 relative).  12 standard deviations of the sum (a
   // tail of 4e-33 per pair; the sum of bounded terms has lighter tails than
   // a Gaussian, and for pc <= 23 the band exceeds the worst case pc / SC)
-  // bound the distance error; the threshold error is far smaller.
+  // bound the distance error; the threshold error is far smaller.  The GPU
+  // backend checks this model against measured pairs (calibrate_band in
+  // fs_gpu.hip) and widens the band where the errors of different columns
+  // add up coherently (duplicated, collinear or same-grid columns).
   const double pcd = (double)P.pc;
   P.amb_delta = 12.0 * std::sqrt(pcd / 6.0 + 1.0) / sc + 4.0e-7 * std::sqrt(pcd);
+  P.amb_delta_model = P.amb_delta;
   P.ranges_ready = 1;
   return 0;
 }

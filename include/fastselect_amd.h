@@ -267,6 +267,16 @@ FS_API int fs_plan_score(fs_plan* plan, double* sums);
  * skipped. */
 FS_API int fs_plan_info(const fs_plan* plan, int64_t* owned_tiles, double* pair_feature_evals,
                         int64_t* refined_pairs);
+/* Refinement-band calibration of the plan's current feature layout (GPU
+ * MultiSURF / ReliefF plans; no reference counterpart -- it guards the
+ * integer pass 1 that replaces the reference's float distance loop,
+ * MultiSURF.py:176-188).  out[6]: [0] 1 if pass 1 runs on 16-bit operands,
+ * [1] / [2] rms / max |quantised - reference| distance error over 4096
+ * sampled pairs (integer units), [3] the independent-rounding model's
+ * standard deviation sqrt(pc/6 + 1), [4] band / model band, [5] 1 if the
+ * coherence guard turned 16-bit operands off.  CPU plans: out[0..5] =
+ * {0, 0, 0, model sigma, 1, 0}. */
+FS_API int fs_plan_calibration(const fs_plan* plan, double* out);
 /* Owned pairs that carried a non-zero pass-2 weight in the last pass 2 (the
  * pairs the sparse GPU pass 2 evaluates; -1 when the plan does not count
  * them: CPU backend, dense pass 2, or before the first pass 2). */

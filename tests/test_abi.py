@@ -165,7 +165,9 @@ def test_threaded_float32_cast_equals_numpy():
     """_base.to_float32 (row blocks over threads) is numpy's float32 cast."""
     from fastselect_amd import _base
     rng = np.random.default_rng(3)
-    x = rng.normal(size=(2500, 1800)) * 10.0 ** rng.integers(-30, 30, size=(2500, 1800))
+    x = rng.normal(size=(4800, 1800)) * 10.0 ** rng.integers(-30, 30, size=(4800, 1800))
+    # the strided view holds 2400 x 1799 > 1 << 22 elements: the threaded path
+    assert x[::2, 1:].size > (1 << 22)
     for arr in (x, np.asfortranarray(x), x[::2, 1:]):
         got = _base.to_float32(arr, n_jobs=4)
         assert got.flags.c_contiguous and got.dtype == np.float32
