@@ -173,6 +173,27 @@ def fit_ms(X, y, star, repeats=5):
     return float(np.median(ts)), ts
 
 
+def sharded_fit_ms(X, y, star, local, barrier, sync, dist, repeats=3):
+    """End-to-end multi-GPU scoring (``parallel.multisurf_scores``: cast,
+    X to the GPUs by per-rank rows + all-gather, column statistics, plan,
+    one step, all-reduces), max over ranks, median of `repeats` after one
+    warm-up."""
+    import torch
+
+    from fastselect_amd.parallel import multisurf_scores
+    multisurf_scores(X, y, use_star=star, device=local, release_cache=False)
+    ts = []
+    for _ in range(repeats):
+        barrier()
+        t0 = time.perf_counter()
+        multisurf_scores(X, y, use_star=star, device=local, release_cache=False)
+        sync()
+        t = torch.tensor([(time.perf_counter() - t0) * 1e3], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ts.append(float(t.item()))
+    return float(np.median(ts)), ts
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -201,7 +222,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from fastselect_amd.parallel import ShardedMultiSURF
+    from fastselect_amd.parallel import ShardedMultiSURF, resident_x
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -243,8 +264,17 @@ def main():
     log(f"rank {rank}/{world}: data {args.samples}x{args.features} ready in "
         f"{time.perf_counter() - t0:.1f} s")
 
-    job = ShardedMultiSURF(x, y, recip, is_disc, use_star=args.star, backend=args.backend,
-                           device=local)
+    # X onto the GPUs: at N > 1 each rank uploads its n/N rows and the rest
+    # arrive by an RCCL all-gather (parallel.resident_x); the plan then copies
+    # the gathered X device-to-device
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    with resident_x(x, args.backend, local):
+        job = ShardedMultiSURF(x, y, recip, is_disc, use_star=args.star, backend=args.backend,
+                               device=local)
+    sync()
+    setup_ms = (time.perf_counter() - t0) * 1e3
     tiles, _, _ = job.info()
 
     for w in range(args.warmup):
@@ -317,6 +347,9 @@ def main():
             "hbm_peak_GBps": HBM_PEAK_GBPS,
         }
     job.close()
+    setup = torch.tensor([setup_ms], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
+    if world > 1:
+        dist.all_reduce(setup, op=dist.ReduceOp.MAX)
 
     out = None
     if rank == 0:
@@ -345,6 +378,9 @@ def main():
                                          f" all-reduce" if world > 1 else "")},
             "roofline": roofline,
             "refined_pairs": refined,
+            # X to the GPUs (per-rank rows + all-gather at N > 1) + plan
+            # creation (device ranges, calibration, layout), max over ranks
+            "setup_ms": float(setup.item()),
         }
     if on_gpu and world == 1 and not args.no_fit:
         log("timing end-to-end fit() ...")
@@ -352,6 +388,16 @@ def main():
         out["fit_ms"] = med
         out["fit_ms_runs"] = ts
         out["fit_feature_scores_per_s"] = n * p / (med * 1e-3)
+    elif on_gpu and world > 1 and not args.no_fit:
+        log("timing end-to-end multi-GPU scoring ...")
+        med, ts = sharded_fit_ms(X, y, args.star, local, barrier, sync, dist)
+        if rank == 0:
+            out["fit_ms"] = med
+            out["fit_ms_runs"] = ts
+            out["fit_feature_scores_per_s"] = n * p / (med * 1e-3)
+            out["fit_path"] = ("parallel.multisurf_scores: float32 cast, per-rank rows + RCCL "
+                               "all-gather of X, column statistics, plan, step, all-reduces; "
+                               "max over ranks")
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline (oracle) ...")

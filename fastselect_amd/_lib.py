@@ -37,7 +37,7 @@ _vp = ctypes.c_void_p
 # every symbol include/fastselect_amd.h declares (checked by tests/test_abi.py)
 EXPORTED = (
     "fs_version", "fs_last_error", "fs_device_count", "fs_device_cache_release",
-    "fs_stage_x", "fs_unstage_x", "fs_all_finite",
+    "fs_stage_x", "fs_stage_x_device", "fs_unstage_x", "fs_all_finite",
     "fs_column_stats", "fs_multisurf_score", "fs_multisurf_score_rows",
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
@@ -76,6 +76,9 @@ def _load() -> ctypes.CDLL:
     lib.fs_device_cache_release.restype = _int
     lib.fs_stage_x.argtypes = [_int, _vp, _int, _i64, _i64, ctypes.POINTER(ctypes.c_uint64)]
     lib.fs_stage_x.restype = _int
+    lib.fs_stage_x_device.argtypes = [_int, _vp, _vp, _int, _i64, _i64,
+                                      ctypes.POINTER(ctypes.c_uint64)]
+    lib.fs_stage_x_device.restype = _int
     lib.fs_unstage_x.argtypes = [ctypes.c_uint64]
     lib.fs_unstage_x.restype = _int
     lib.fs_all_finite.argtypes = [_vp, _int, _i64, _i64, _int, ctypes.POINTER(_int)]
@@ -152,6 +155,22 @@ def staged_x(backend, x, device=0):
         # copy the calls upload X themselves (and report their own errors)
         yield
         return
+    try:
+        yield
+    finally:
+        _lib.fs_unstage_x(h)
+
+
+@contextlib.contextmanager
+def staged_device_x(x, x_device_ptr, device=0):
+    """Register a device copy of the host array ``x`` that the caller holds
+    (``x_device_ptr``: n x p, same dtype, row-major) for the calls inside the
+    block (fs_stage_x_device): the column statistics and the plans given
+    ``x`` read it instead of uploading X."""
+    h = ctypes.c_uint64(0)
+    check(_lib.fs_stage_x_device(int(device), x.ctypes.data, _vp(int(x_device_ptr)),
+                                 int(x.dtype == np.float64), x.shape[0], x.shape[1],
+                                 ctypes.byref(h)))
     try:
         yield
     finally:

@@ -81,6 +81,19 @@ int fs_stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p, ui
   return gpu::stage_x(device, x, x_is_f64, n, p, staged);
 }
 
+int fs_stage_x_device(int device, const void* x, const void* x_device, int x_is_f64, int64_t n,
+                      int64_t p, uint64_t* staged) {
+  if (!x || !x_device || !staged || n < 1 || p < 1) {
+    set_error("fs_stage_x_device: need x, x_device, staged, n >= 1 and p >= 1");
+    return FS_EINVAL;
+  }
+  if (gpu::device_count() <= 0) {
+    set_error("backend='gpu' requested but no HIP device is visible");
+    return FS_ENODEV;
+  }
+  return gpu::stage_x_device(device, x, x_device, x_is_f64, n, p, staged);
+}
+
 int fs_unstage_x(uint64_t staged) { return gpu::unstage_x(staged); }
 
 int fs_all_finite(const void* x, int x_is_f64, int64_t n, int64_t p, int n_jobs, int* finite) {

@@ -2111,6 +2111,7 @@ struct Staged {
   void* dev;
   std::thread::id owner;  // only the staging thread's calls read it (concurrent
                           // fits of one array stage and free their own copies)
+  bool borrowed;          // caller-owned device copy (stage_x_device): not freed
 };
 std::mutex staged_mu;
 std::vector<Staged> staged;
@@ -2133,13 +2134,36 @@ int stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p, uint6
     return FS_EHIP;
   }
   std::lock_guard<std::mutex> lk(staged_mu);
-  staged.push_back(Staged{x, n, p, x_is_f64 ? 1 : 0, device, d, std::this_thread::get_id()});
+  staged.push_back(
+      Staged{x, n, p, x_is_f64 ? 1 : 0, device, d, std::this_thread::get_id(), false});
   *handle = (uint64_t)(uintptr_t)d;
+  return FS_OK;
+}
+
+// A device copy the caller already holds (e.g. X assembled on the GPU by an
+// all-gather of each rank's rows) registered under the host array's key.
+int stage_x_device(int device, const void* x, const void* x_dev, int x_is_f64, int64_t n,
+                   int64_t p, uint64_t* handle) {
+  *handle = 0;
+  if (device < 0 || device >= device_count()) {
+    set_error("fs_stage_x_device: device ordinal out of range");
+    return FS_ENODEV;
+  }
+  std::lock_guard<std::mutex> lk(staged_mu);
+  for (const Staged& e : staged)
+    if (e.dev == x_dev) {
+      set_error("fs_stage_x_device: this device buffer is already staged");
+      return FS_EINVAL;
+    }
+  staged.push_back(Staged{x, n, p, x_is_f64 ? 1 : 0, device, const_cast<void*>(x_dev),
+                          std::this_thread::get_id(), true});
+  *handle = (uint64_t)(uintptr_t)x_dev;
   return FS_OK;
 }
 
 int unstage_x(uint64_t handle) {
   void* d = (void*)(uintptr_t)handle;
+  bool borrowed = false;
   {
     std::lock_guard<std::mutex> lk(staged_mu);
     auto it = std::find_if(staged.begin(), staged.end(),
@@ -2148,9 +2172,10 @@ int unstage_x(uint64_t handle) {
       set_error("fs_unstage_x: unknown handle");
       return FS_EINVAL;
     }
+    borrowed = it->borrowed;
     staged.erase(it);
   }
-  dev_free(d);  // every reader synchronised its stream before returning
+  if (!borrowed) dev_free(d);  // every reader synchronised its stream before returning
   return FS_OK;
 }
 
@@ -2468,8 +2493,13 @@ static int plan_layout(Plan* g) {
   // then on one box, alternating, 32k 107.6 / 14.9 and 107.7 / 14.6 against
   // 64k 108.1 / 15.0 and 108.0 / 14.6 -- the tail costs more than the
   // per-workgroup row-block stage below 32k.
+  // Small problems (cfg2: 820 tiles x 20 blocks) take a quarter of their
+  // (tile, block) units as the target, at least 4096: segments of ~4 tiles
+  // amortise each workgroup's row-block stage (tools/cfg2_sweep.sh,
+  // profiles/r02/cfg2_sweep.txt: cfg2 step 6.11 -> 5.83 ms at 4096-8192).
   const int64_t nfb = g->sparse ? (Q.PW + 255) / 256 : (Q.PW + 127) / 128;
-  int64_t wgs = g->sparse ? 32768 : 65536;
+  int64_t wgs = g->sparse ? std::min<int64_t>(32768, std::max<int64_t>(4096, g->n_tiles * nfb / 4))
+                          : 65536;
   if (const char* e = std::getenv("FS_PASS2_WGS")) wgs = std::max<int64_t>(256, std::atoll(e));
   g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + wgs - 1) / wgs);
   g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);

@@ -282,6 +282,8 @@ void dev_cache_release();
 // staged_lookup returns the device copy of (host, n, p, f64) on `device`, or
 // nullptr.
 int stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p, uint64_t* handle);
+int stage_x_device(int device, const void* x, const void* x_dev, int x_is_f64, int64_t n,
+                   int64_t p, uint64_t* handle);
 int unstage_x(uint64_t handle);
 const void* staged_lookup(const void* host, int64_t n, int64_t p, int x_is_f64, int device);
 int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap, int device,

@@ -19,8 +19,16 @@ float32 sequential per-sample mean, which needs whole distance rows), so each
 rank scores a slice of the samples (``shard_rows``) and one SUM all-reduce of
 the p per-feature sums combines them (``relieff_scores`` / ``surf_scores``).
 A rank computes every distance tile touching its 128-sample blocks.
+
+Getting X onto the GPUs (``resident_x``): with RCCL each rank copies only its
+own n/N rows over PCIe and the rows of the other ranks arrive by one
+all-gather over xGMI, instead of N full host-to-device copies; the gathered
+copy is registered for the column statistics and the plan
+(``fs_stage_x_device``), so neither uploads X again.
 """
 from __future__ import annotations
+
+import contextlib
 
 import numpy as np
 
@@ -32,6 +40,66 @@ def _dist():
     if dist.is_available() and dist.is_initialized():
         return dist, dist.get_rank(), dist.get_world_size()
     return None, 0, 1
+
+
+def row_chunk(n: int, rank: int, world: int):
+    """Rows [lo, hi) that ``rank`` uploads for the all-gather of X: equal
+    chunks of ceil(n / world) rows (the last one short or empty)."""
+    rows = -(-n // world)
+    return min(n, rank * rows), min(n, (rank + 1) * rows), rows
+
+
+def gather_rows(x, device=None, force=False):
+    """All of the float32 host matrix ``x`` in one tensor on ``device`` (a
+    CUDA ordinal; None = host tensors, the gloo rehearsal), with this rank
+    copying only its ``row_chunk`` from the host and the rest all-gathered
+    from the other ranks.  Returns a (world * rows, p) tensor whose first n
+    rows are x."""
+    import torch
+    dist, rank, world = _dist()
+    n, p = x.shape
+    if dist is None or (world == 1 and not force):
+        dev = "cpu" if device is None else torch.device("cuda", device)
+        return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+    lo, hi, rows = row_chunk(n, rank, world)
+    dev = torch.device("cpu") if device is None else torch.device("cuda", device)
+    buf = torch.empty((rows * world, p), dtype=torch.float32, device=dev)
+    mine = buf[rank * rows:(rank + 1) * rows]
+    if hi > lo:
+        mine[:hi - lo].copy_(torch.from_numpy(x[lo:hi]))
+    if dev.type == "cuda":
+        dist.all_gather_into_tensor(buf, mine)          # in place, RCCL over xGMI
+    else:
+        parts = list(buf.split(rows))
+        dist.all_gather(parts, mine.clone())
+    return buf
+
+
+@contextlib.contextmanager
+def resident_x(x, backend="gpu", device=0, gather=None):
+    """X on the GPU for the calls inside the block.  Multi-GPU with RCCL:
+    per-rank rows + all-gather (``gather_rows``), registered as the staged
+    copy of ``x`` (fs_stage_x_device).  One GPU (or gloo): one host-to-device
+    copy (fs_stage_x).  ``x`` must be C-contiguous float32.  gather=True
+    takes the all-gather path at any world size with an 'nccl' group (tests)."""
+    dist, _, world = _dist()
+    if backend != "gpu":
+        yield
+        return
+    if gather is None:
+        gather = dist is not None and world > 1
+    if not gather or dist is None or dist.get_backend() != "nccl":
+        with _lib.staged_x(backend, x, device):
+            yield
+        return
+    buf = gather_rows(x, device, force=True)
+    try:
+        with _lib.staged_device_x(x, buf.data_ptr(), device):
+            yield
+    finally:
+        import torch
+        torch.cuda.current_stream(device).synchronize()
+        del buf
 
 
 def prepare_inputs(X, y, discrete_limit: int = 10, backend: str = "cpu", device: int = 0):
@@ -110,25 +178,31 @@ class ShardedMultiSURF:
     def kernel_ms(self, which: int) -> float:
         return self.plan.kernel_ms(which)
 
-    def close(self):
+    def close(self, release_cache=True):
         """Free the plan and hand its device blocks back to the device:
         torch's caching allocator shares the GPU with this job and cannot
-        reclaim blocks held in the library's cache (fs_device_cache_release)."""
+        reclaim blocks held in the library's cache (fs_device_cache_release).
+        release_cache=False keeps them for the next job (repeated fits)."""
         self.plan.close()
-        if self.backend == "gpu":
+        if self.backend == "gpu" and release_cache:
             _lib.release_device_cache()
 
 
-def multisurf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", device=0):
+def multisurf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", device=0,
+                     release_cache=True):
     """Score X on this rank's share of the tiles and return the full float32
-    score vector (identical on every rank)."""
-    x, yv, recip, isd = prepare_inputs(X, y, discrete_limit, backend, device)
-    job = ShardedMultiSURF(x, yv, recip, isd, use_star=use_star, backend=backend, device=device)
-    try:
-        s = job.step()
-        return s.cpu().numpy()
-    finally:
-        job.close()
+    score vector (identical on every rank).  X reaches the GPUs once
+    (``resident_x``: per-rank rows + an RCCL all-gather when sharded)."""
+    x = _base.to_float32(np.asarray(X))
+    with resident_x(x, backend, device):
+        x, yv, recip, isd = prepare_inputs(x, y, discrete_limit, backend, device)
+        job = ShardedMultiSURF(x, yv, recip, isd, use_star=use_star, backend=backend,
+                               device=device)
+        try:
+            s = job.step()
+            return s.cpu().numpy()
+        finally:
+            job.close(release_cache)
 
 
 # ---- row-sharded ReliefF / SURF ------------------------------------------

@@ -81,6 +81,13 @@ FS_API int fs_device_cache_release(void);
  * *staged receives the handle. */
 FS_API int fs_stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p,
                       uint64_t* staged);
+/* As fs_stage_x, but X is already on `device` (x_device: n x p row-major,
+ * caller-owned, valid until fs_unstage_x, which does not free it): the
+ * multi-GPU path uploads each rank's rows and all-gathers the rest over RCCL
+ * (fastselect_amd/parallel.py), then registers the gathered copy under the
+ * host array's key so that the column statistics and the plan read it. */
+FS_API int fs_stage_x_device(int device, const void* x, const void* x_device, int x_is_f64,
+                             int64_t n, int64_t p, uint64_t* staged);
 FS_API int fs_unstage_x(uint64_t staged);
 /* *finite = 1 if every element of the n x p float32 / float64 matrix is
  * finite, else 0 (host threads; n_jobs as the scoring calls).  The

@@ -53,6 +53,37 @@ def test_nccl_world1_step_matches_one_shot():
         dist.destroy_process_group()
 
 
+def test_nccl_gathered_x_matches_uploaded_x():
+    """The multi-GPU data path at world 1: X assembled on the device by the
+    RCCL all-gather (gather_rows) and registered for the column statistics
+    and the plan (fs_stage_x_device) gives bit-identical scores to the plain
+    upload."""
+    import torch
+    import torch.distributed as dist
+    from sklearn.datasets import make_classification
+
+    from fastselect_amd import _lib
+    from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs, resident_x
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_port())
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        X, y = make_classification(n_samples=1000, n_features=300, n_informative=20,
+                                   n_redundant=40, random_state=9)
+        x = np.ascontiguousarray(X, dtype=np.float32)
+        with resident_x(x, "gpu", 0, gather=True):
+            xi, yv, recip, isd = prepare_inputs(x, y, backend="gpu", device=0)
+            job = ShardedMultiSURF(xi, yv, recip, isd, backend="gpu", device=0)
+            s = job.step().cpu().numpy()
+            job.close()
+        ref = _lib.multisurf_score("gpu", x, yv, recip, None, False, isd)
+        np.testing.assert_array_equal(s, ref)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_column_stats_run_on_the_ranks_device():
     """prepare_inputs(device=d) computes the column statistics on GPU d
     (they used to default to GPU 0 on every rank)."""

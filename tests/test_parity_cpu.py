@@ -150,3 +150,39 @@ def test_relieff_boundary_ties_follow_numba_quicksort(oracle, kind, k):
     dl = 3 if kind != "duplicates" else 10
     s = ReliefF(backend="cpu", n_neighbors=k, discrete_limit=dl).fit(X, y).feature_importances_
     assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=k, discrete_limit=dl), TOL)
+
+
+def _gather_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fastselect_amd.parallel import gather_rows
+    x = np.random.default_rng(4).normal(size=(301, 17)).astype(np.float32)
+    buf = gather_rows(x, None)           # host tensors: the gloo rehearsal of the RCCL gather
+    np.save(f"{out_path}.{rank}.npy", buf.numpy()[:301])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_rows_assembles_x(tmp_path, world):
+    """Multi-GPU data path: each rank contributes only its row_chunk and the
+    all-gather assembles all of X on every rank (gloo here, RCCL on GPUs)."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "x")
+    mp.spawn(_gather_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    x = np.random.default_rng(4).normal(size=(301, 17)).astype(np.float32)
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(f"{out}.{r}.npy"), x)
+
+
+def test_row_chunks_cover_every_row_once():
+    from fastselect_amd.parallel import row_chunk
+    for n in (1, 7, 128, 1000, 20000):
+        for world in (1, 2, 3, 8):
+            seen = np.zeros(n, int)
+            for r in range(world):
+                lo, hi, rows = row_chunk(n, r, world)
+                assert 0 <= lo <= hi <= n and hi - lo <= rows
+                seen[lo:hi] += 1
+            assert (seen == 1).all()
