@@ -103,6 +103,19 @@ __device__ __forceinline__ double block_sum_256(double v, double* red) {
   return r;
 }
 
+// Distance storage.  Full layout (ReliefF / SURF, whose neighbour selection
+// reads whole rows): D[i][j] over n_pad x n_pad, both halves.  Tiled layout
+// (MultiSURF, whose kernels only ever read inside an owned tile): one
+// 128 x 128 block per owned tile t, T_t[b][a] = D(i0 + a, j0 + b) -- half the
+// memory of the full matrix for the whole triangle, and a rank of an N-GPU
+// job holds only its 1/N of the tiles.  d_at(..., a, b) addresses element
+// (i0 + a, j0 + b) of owned tile t either way; consecutive a are consecutive
+// doubles in both layouts (the full layout reads it as D[j][i]).
+__device__ __forceinline__ int64_t d_at(int tiled, int64_t n_pad, int64_t t, int64_t i0,
+                                        int64_t j0, int a, int b) {
+  return tiled ? ((t * kTile + b) * kTile + a) : ((j0 + b) * n_pad + i0 + a);
+}
+
 // ---------------------------------------------------------------------------
 // Quantize: X -> xqT (u32, [PW][n_pad]) and xs (f32, [n_pad][PW])
 // ---------------------------------------------------------------------------
@@ -343,6 +356,7 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
                                                  int nck_cont, int nck_disc, uint32_t sc_disc,
                                                  int q16,
                                                  const int2* __restrict__ tiles, int splits,
+                                                 int tiled, int64_t plane,
                                                  double* __restrict__ D,
                                                  double* __restrict__ Dpart) {
   // Two distinct LDS objects (not one indexed array) so the compiler can
@@ -357,7 +371,8 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
   const int2 tl = tiles[blockIdx.x / (unsigned)splits];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
   const int tx = tid & 15, ty = tid >> 4;
-  if (part > 0) D = Dpart + (int64_t)(part - 1) * n_pad * n_pad;
+  const int64_t t = (int64_t)(blockIdx.x / (unsigned)splits);
+  if (part > 0) D = Dpart + (int64_t)(part - 1) * plane;
 
   uint32_t acc[8][8];
   uint32_t hi[8][4];
@@ -435,9 +450,11 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
   run(std::integral_constant<int, kModeDisc>{}, c_begin > nck_cont ? c_begin : nck_cont, c_end);
   flush();
 
-  // Epilogue: D[i][j] for the tile and, off the diagonal, the mirror D[j][i].
+  // Epilogue.  Full layout: D[i][j] for the tile and, off the diagonal, the
+  // mirror D[j][i].  Tiled: T_t[b][a] only (the mirror pattern below), which
+  // for a diagonal tile is the whole symmetric block.
 #pragma unroll
-  for (int r = 0; r < 8; r++) {
+  for (int r = 0; r < 8 && !tiled; r++) {
     const int64_t i = i0 + ty * 4 + (r & 3) + (r >> 2) * 64;
     double v[8];
 #pragma unroll
@@ -451,17 +468,17 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
     *(double2*)(row + 64) = make_double2(v[4], v[5]);
     *(double2*)(row + 66) = make_double2(v[6], v[7]);
   }
-  if (tl.x != tl.y) {
+  if (tl.x != tl.y || tiled) {
 #pragma unroll
     for (int c = 0; c < 8; c++) {
-      const int64_t j = j0 + tx * 4 + (c & 3) + (c >> 2) * 64;
+      const int b = tx * 4 + (c & 3) + (c >> 2) * 64;
       double v[8];
 #pragma unroll
       for (int r = 0; r < 8; r++) {
         const uint64_t h = (hi[r][c >> 1] >> ((c & 1) * 16)) & 0xFFFFu;
         v[r] = (double)((h << kHiShift) + acc[r][c]);
       }
-      double* row = D + j * n_pad + i0 + ty * 4;
+      double* row = D + d_at(tiled, n_pad, t, i0, j0, ty * 4, b);
       *(double2*)(row + 0) = make_double2(v[0], v[1]);
       *(double2*)(row + 2) = make_double2(v[2], v[3]);
       *(double2*)(row + 64) = make_double2(v[4], v[5]);
@@ -486,10 +503,19 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
 // (integer-valued doubles: exact in any order).
 __global__ __launch_bounds__(256) void k_dist_merge(double* __restrict__ D,
                                                    const double* __restrict__ Dpart, int nparts,
-                                                   const int2* __restrict__ tiles, int64_t n_pad) {
+                                                   const int2* __restrict__ tiles, int64_t n_pad,
+                                                   int tiled, int64_t plane) {
   const int2 tl = tiles[blockIdx.x];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
-  const int64_t plane = n_pad * n_pad;
+  if (tiled) {
+    const int64_t base = (int64_t)blockIdx.x * kTile * kTile;
+    for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
+      double v = D[base + e];
+      for (int s = 0; s < nparts; s++) v += Dpart[s * plane + base + e];
+      D[base + e] = v;
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
     const int64_t r = e / kTile, c = e % kTile;
     const int64_t a = (i0 + r) * n_pad + j0 + c, b = (j0 + c) * n_pad + i0 + r;
@@ -641,37 +667,34 @@ __global__ __launch_bounds__(256) void k_quantize_f64(
 // ---------------------------------------------------------------------------
 // MultiSURF row statistics, thresholds and neighbour counts
 // ---------------------------------------------------------------------------
-// Per-row distance moments from the owned tiles only.  k_tile_rowstats:
-// one workgroup per owned tile; lanes 0..127 sum row i0 + r over the tile's
-// 128 columns (reading the symmetric mirror D[j][i], coalesced), lanes
-// 128..255 sum row j0 + c over its 128 rows (off-diagonal tiles only) ->
-// part[t][256][2].  k_rowstats_reduce adds a row's tile partials in tile
-// order (deterministic) and appends this rank's mean correction:
-// rowstats[3i] = sum D, [3i+1] = sum D^2, [3i+2] = corr share.
+// Per-row distance moments from the owned tiles only (tiled D: MultiSURF).
+// One workgroup per owned tile t.  Lanes 0..127 sum row i0 + a over the
+// tile's 128 columns (T_t[b][a], b = 0..127: coalesced over a); off the
+// diagonal, waves 2 and 3 sum row j0 + b over the tile's rows, one column b
+// at a time (T_t[b][0..127], a contiguous read) with a fixed-order wave
+// reduction, lane b % 64 of wave 2 + b / 64 keeping the result -> part[t][256].
+// k_rowstats_reduce adds a row's tile partials in tile order (deterministic)
+// and appends this rank's mean correction: rowstats[3i] = sum D, [3i+1] =
+// sum D^2, [3i+2] = corr share.
 __global__ __launch_bounds__(256) void k_tile_rowstats(const double* __restrict__ D, int64_t n,
-                                                       int64_t n_pad,
                                                        const int2* __restrict__ tiles,
                                                        double2* __restrict__ part) {
   const int2 tl = tiles[blockIdx.x];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  const double* T = D + (int64_t)blockIdx.x * kTile * kTile;
   const int tid = threadIdx.x;
-  const bool rows = tid < kTile;
-  const int r = tid & (kTile - 1);
   double s1 = 0.0, s2 = 0.0;
-  if (rows || tl.x != tl.y) {
-    // rows: row i = i0 + r over columns j0 + c (read D[j][i]);
-    // cols: row j = j0 + r over rows i0 + c (read D[i][j])
-    const int64_t self = rows ? i0 + r : j0 + r;
-    const int64_t other0 = rows ? j0 : i0;
+  if (tid < kTile) {
+    const int a = tid;
+    const int64_t self = i0 + a;
     if (self < n) {
-      // 8 loads in flight per step; skipped entries add 0.0, so the sums and
-      // their order are those of the plain loop
-      for (int c0 = 0; c0 < kTile; c0 += 8) {
+      // 8 loads in flight per step; skipped entries add 0.0
+      for (int b0 = 0; b0 < kTile; b0 += 8) {
         double d[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          const int64_t o = other0 + c0 + u;
-          const double v = D[o * n_pad + self];  // o < n_pad: always in bounds
+          const int64_t o = j0 + b0 + u;
+          const double v = T[(b0 + u) * kTile + a];
           d[u] = (o < n && o != self) ? v : 0.0;
         }
 #pragma unroll
@@ -679,6 +702,25 @@ __global__ __launch_bounds__(256) void k_tile_rowstats(const double* __restrict_
           s1 += d[u];
           s2 += d[u] * d[u];
         }
+      }
+    }
+  } else if (tl.x != tl.y) {
+    const int lane = tid & 63, w2 = (tid >> 6) - 2;
+    // rows i0 + lane and i0 + 64 + lane of the tile, masked once
+    const bool in0 = i0 + lane < n, in1 = i0 + 64 + lane < n;
+    for (int k = 0; k < 64; k++) {
+      const int b = 64 * w2 + k;
+      const double v0 = in0 ? T[b * kTile + lane] : 0.0;
+      const double v1 = in1 ? T[b * kTile + 64 + lane] : 0.0;
+      double t1 = v0 + v1, t2 = v0 * v0 + v1 * v1;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        t1 += __shfl_xor(t1, o);
+        t2 += __shfl_xor(t2, o);
+      }
+      if (lane == k && j0 + b < n) {
+        s1 = t1;
+        s2 = t2;
       }
     }
   }
@@ -789,7 +831,7 @@ __device__ __forceinline__ void pairbuf_flush(PairBuf& pb, int2* __restrict__ li
 // MultiSURF compares D (integer units) with thr; SURF compares the float32
 // distance with the float64 mean, the band widened by 4 float32 ulps of it.
 __global__ __launch_bounds__(256) void k_flag_pairs(const double* __restrict__ D, int64_t n,
-                                                    int64_t n_pad,
+                                                    int64_t n_pad, int tiled,
                                                     const int2* __restrict__ tiles,
                                                     const double* __restrict__ thr, int algo,
                                                     double inv_sc, double delta,
@@ -805,10 +847,10 @@ __global__ __launch_bounds__(256) void k_flag_pairs(const double* __restrict__ D
     bool amb = false;
     if (!(i < n && j < n && (tl.x < tl.y || ii < jj))) {
     } else if (algo == ALGO_MULTISURF) {
-      const double d = D[j * n_pad + i];
+      const double d = D[d_at(tiled, n_pad, blockIdx.x, i0, j0, ii, jj)];
       amb = __builtin_fabs(d - thr[i]) < delta || __builtin_fabs(d - thr[j]) < delta;
     } else {
-      const double df = D[j * n_pad + i] * inv_sc;
+      const double df = D[d_at(tiled, n_pad, blockIdx.x, i0, j0, ii, jj)] * inv_sc;
       const float ai = (float)thr[i], aj = (float)thr[j];
       const double bi = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(ai) + 1u) - (double)ai);
       const double bj = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(aj) + 1u) - (double)aj);
@@ -817,6 +859,26 @@ __global__ __launch_bounds__(256) void k_flag_pairs(const double* __restrict__ D
     if (amb) pairbuf_add(pb, i, j, list, cap, count);
   }
   pairbuf_flush(pb, list, cap, count);
+}
+
+// Where a refined pair's distance goes.  Full layout: D[i][j] and D[j][i].
+// Tiled (tw.x = tile rows nb, tw.y = world): pair i < j lives in the owned
+// tile of blocks (i / 128, j / 128), the (linear / world)-th tile this rank
+// owns (round-robin ownership, owned_tiles); a diagonal tile holds both
+// halves.
+__device__ __forceinline__ void store_pair(double* __restrict__ D, int64_t n_pad, int2 tw, int2 pr,
+                                           double v) {
+  if (tw.x == 0) {
+    D[(int64_t)pr.x * n_pad + pr.y] = v;
+    D[(int64_t)pr.y * n_pad + pr.x] = v;
+    return;
+  }
+  if (pr.x > pr.y) pr = make_int2(pr.y, pr.x);
+  const int64_t I = pr.x / kTile, J = pr.y / kTile;  // I <= J
+  const int64_t t = tile_linear(tw.x, I, J) / tw.y;
+  const int a = pr.x - (int)(I * kTile), b = pr.y - (int)(J * kTile);
+  D[(t * kTile + b) * kTile + a] = v;
+  if (I == J) D[(t * kTile + a) * kTile + b] = v;
 }
 
 // Reference-exact distance of each listed pair: sum_f diff_f(i, j) in
@@ -829,7 +891,7 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
     const T* __restrict__ x, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
     const int64_t* __restrict__ src_col, const double* __restrict__ scl, double sc,
     const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
-    int64_t n_pad, int mark_f32, double* __restrict__ D) {
+    int64_t n_pad, int2 tw, int mark_f32, double* __restrict__ D) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
@@ -874,8 +936,7 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
       // reference's float32 key, stored negated so k_rf_select knows it is
       // exact (a zero key is stored as +0, never -0, whose bits would sort last).
       const double v = mark_f32 ? (acc > 0.0 ? -(double)(float)acc : 0.0) : acc * sc;
-      D[(int64_t)pr.x * n_pad + pr.y] = v;
-      D[(int64_t)pr.y * n_pad + pr.x] = v;
+      store_pair(D, n_pad, tw, pr, v);
     }
   }
 }
@@ -890,7 +951,7 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
 __global__ __launch_bounds__(256) void k_exact_pairs_rows(
     const float* __restrict__ x, int64_t p, const float* __restrict__ scl32, double sc,
     const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
-    int64_t n_pad, double* __restrict__ D) {
+    int64_t n_pad, int2 tw, double* __restrict__ D) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
@@ -923,9 +984,7 @@ __global__ __launch_bounds__(256) void k_exact_pairs_rows(
     }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (lane == 0) {
-      const double v = acc * sc;
-      D[(int64_t)pr.x * n_pad + pr.y] = v;
-      D[(int64_t)pr.y * n_pad + pr.x] = v;
+      store_pair(D, n_pad, tw, pr, acc * sc);
     }
   }
 }
@@ -971,44 +1030,77 @@ __global__ __launch_bounds__(256) void k_calib(
 // Near hit / miss counts over the owned tiles (D now exact for ambiguous
 // pairs): counts[2i], counts[2i+1].
 __global__ __launch_bounds__(256) void k_tile_counts(const double* __restrict__ D, int64_t n,
-                                                     int64_t n_pad,
                                                      const int2* __restrict__ tiles,
                                                      const int32_t* __restrict__ lab,
                                                      const double* __restrict__ thr,
                                                      double* __restrict__ counts) {
-  // Near hits / misses over the owned tiles (D exact for ambiguous pairs by
-  // now), same lane layout as k_tile_rowstats; counts are integers, so the
-  // atomic adds are exact in any order (counts zeroed by the caller).
+  // Near hits / misses over the owned tiles (tiled D, exact for ambiguous
+  // pairs by now), same lane layout as k_tile_rowstats; counts are integers,
+  // so the atomic adds and the wave reductions are exact in any order
+  // (counts zeroed by the caller).
   const int2 tl = tiles[blockIdx.x];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  const double* T = D + (int64_t)blockIdx.x * kTile * kTile;
   const int tid = threadIdx.x;
-  const bool rows = tid < kTile;
-  if (!rows && tl.x == tl.y) return;
-  const int r = tid & (kTile - 1);
-  const int64_t self = rows ? i0 + r : j0 + r;
-  const int64_t other0 = rows ? j0 : i0;
-  if (self >= n) return;
-  const double t = thr[self];
-  const int32_t ls = lab[self];
-  double h = 0.0, m = 0.0;
-  for (int c0 = 0; c0 < kTile; c0 += 8) {
-    bool near[8];  // 8 loads in flight per step
+  if (tid < kTile) {
+    const int a = tid;
+    const int64_t self = i0 + a;
+    if (self >= n) return;
+    const double t = thr[self];
+    const int32_t ls = lab[self];
+    double h = 0.0, m = 0.0;
+    for (int b0 = 0; b0 < kTile; b0 += 8) {
+      bool near[8];  // 8 loads in flight per step
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int64_t o = other0 + c0 + u;
-      const double v = D[o * n_pad + self];  // o < n_pad: always in bounds
-      near[u] = (o < n) & (o != self) & (v < t);
-    }
+      for (int u = 0; u < 8; u++) {
+        const int64_t o = j0 + b0 + u;
+        const double v = T[(b0 + u) * kTile + a];
+        near[u] = (o < n) & (o != self) & (v < t);
+      }
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      if (near[u]) {
-        if (lab[other0 + c0 + u] == ls) h += 1.0;
-        else m += 1.0;
+      for (int u = 0; u < 8; u++) {
+        if (near[u]) {
+          if (lab[j0 + b0 + u] == ls) h += 1.0;
+          else m += 1.0;
+        }
       }
     }
+    if (h != 0.0) atomicAdd(&counts[2 * self], h);
+    if (m != 0.0) atomicAdd(&counts[2 * self + 1], m);
+    return;
   }
-  if (h != 0.0) atomicAdd(&counts[2 * self], h);
-  if (m != 0.0) atomicAdd(&counts[2 * self + 1], m);
+  if (tl.x == tl.y) return;
+  // columns: row j0 + b over the tile's rows, one b per step (contiguous
+  // T_t[b][0..127]), wave-reduced; lane b % 64 keeps column b's counts
+  const int lane = tid & 63, w2 = (tid >> 6) - 2;
+  const bool in0 = i0 + lane < n, in1 = i0 + 64 + lane < n;
+  const int32_t l0 = in0 ? lab[i0 + lane] : -1, l1 = in1 ? lab[i0 + 64 + lane] : -1;
+  double h = 0.0, m = 0.0;
+  for (int k = 0; k < 64; k++) {
+    const int b = 64 * w2 + k;
+    const int64_t self = j0 + b;
+    if (self >= n) break;  // uniform across the wave
+    const double t = thr[self];
+    const int32_t ls = lab[self];
+    const double v0 = T[b * kTile + lane], v1 = T[b * kTile + 64 + lane];
+    const bool n0 = in0 && v0 < t, n1 = in1 && v1 < t;
+    double hh = (n0 && l0 == ls ? 1.0 : 0.0) + (n1 && l1 == ls ? 1.0 : 0.0);
+    double mm = (n0 && l0 != ls ? 1.0 : 0.0) + (n1 && l1 != ls ? 1.0 : 0.0);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      hh += __shfl_xor(hh, o);
+      mm += __shfl_xor(mm, o);
+    }
+    if (lane == k) {
+      h = hh;
+      m = mm;
+    }
+  }
+  const int64_t self = j0 + 64 * w2 + lane;
+  if (self < n) {
+    if (h != 0.0) atomicAdd(&counts[2 * self], h);
+    if (m != 0.0) atomicAdd(&counts[2 * self + 1], m);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1016,14 +1108,16 @@ __global__ __launch_bounds__(256) void k_tile_counts(const double* __restrict__ 
 // ---------------------------------------------------------------------------
 // Symmetric pair weight W_ij + W_ji of one pair (i, j) of an owned tile.
 __device__ __forceinline__ float pair_weight(const double* __restrict__ D, int64_t n, int64_t n_pad,
-                                             int64_t i, int64_t j, bool upper,
+                                             int tiled, int64_t t, int64_t i0, int64_t j0, int ii,
+                                             int jj, bool upper,
                                              const double* __restrict__ thr,
                                              const int32_t* __restrict__ lab,
                                              const double* __restrict__ counts, int algo,
                                              int use_star, double inv_sc, int64_t r_lo,
                                              int64_t r_hi) {
+  const int64_t i = i0 + ii, j = j0 + jj;
   if (!(i < n && j < n && upper)) return 0.0f;
-  const double d = D[j * n_pad + i];  // == D[i][j]
+  const double d = D[d_at(tiled, n_pad, t, i0, j0, ii, jj)];  // == D[i][j]
   const bool hit = lab[i] == lab[j];
   double wi, wj;
   if (algo == ALGO_MULTISURF) {
@@ -1042,7 +1136,8 @@ __device__ __forceinline__ float pair_weight(const double* __restrict__ D, int64
 }
 
 __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, int64_t n,
-                                                 int64_t n_pad, const int2* __restrict__ tiles,
+                                                 int64_t n_pad, int tiled,
+                                                 const int2* __restrict__ tiles,
                                                  const double* __restrict__ thr,
                                                  const int32_t* __restrict__ lab,
                                                  const double* __restrict__ counts, int algo,
@@ -1053,8 +1148,9 @@ __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, i
   float* out = Wt + (int64_t)blockIdx.x * kTile * kTile;
   for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
     const int jj = e / kTile, ii = e % kTile;
-    out[jj * kTile + ii] = pair_weight(D, n, n_pad, i0 + ii, j0 + jj, tl.x < tl.y || ii < jj, thr,
-                                       lab, counts, algo, use_star, inv_sc, r_lo, r_hi);
+    out[jj * kTile + ii] = pair_weight(D, n, n_pad, tiled, blockIdx.x, i0, j0, ii, jj,
+                                       tl.x < tl.y || ii < jj, thr, lab, counts, algo, use_star,
+                                       inv_sc, r_lo, r_hi);
   }
 }
 
@@ -1077,8 +1173,9 @@ __device__ __forceinline__ uint32_t weight_bits(float w, bool last) {
 }
 
 __global__ __launch_bounds__(1024) void k_weights_sparse(
-    const double* __restrict__ D, int64_t n, int64_t n_pad, const int2* __restrict__ tiles,
-    const double* __restrict__ thr, const int32_t* __restrict__ lab,
+    const double* __restrict__ D, int64_t n, int64_t n_pad, int tiled,
+    const int2* __restrict__ tiles, const double* __restrict__ thr,
+    const int32_t* __restrict__ lab,
     const double* __restrict__ counts, int algo, int use_star, double inv_sc, int64_t r_lo,
     int64_t r_hi, uint2* __restrict__ ent, unsigned long long* __restrict__ nnz) {
   __shared__ int wave_nnz[kSWaves];
@@ -1089,9 +1186,10 @@ __global__ __launch_bounds__(1024) void k_weights_sparse(
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   int off = 0, nz = 0;
   for (int jj = wave; jj < kTile; jj += kSWaves) {
-    const float w0 = pair_weight(D, n, n_pad, i0 + lane, j0 + jj, tl.x < tl.y || lane < jj, thr,
-                                 lab, counts, algo, use_star, inv_sc, r_lo, r_hi);
-    const float w1 = pair_weight(D, n, n_pad, i0 + lane + 64, j0 + jj,
+    const float w0 = pair_weight(D, n, n_pad, tiled, blockIdx.x, i0, j0, lane, jj,
+                                 tl.x < tl.y || lane < jj, thr, lab, counts, algo, use_star,
+                                 inv_sc, r_lo, r_hi);
+    const float w1 = pair_weight(D, n, n_pad, tiled, blockIdx.x, i0, j0, lane + 64, jj,
                                  tl.x < tl.y || lane + 64 < jj, thr, lab, counts, algo, use_star,
                                  inv_sc, r_lo, r_hi);
     const uint64_t m0 = __ballot(w0 != 0.0f), m1 = __ballot(w1 != 0.0f);
@@ -1961,6 +2059,9 @@ struct Plan {
   double* corr = nullptr;
   double* xT64 = nullptr;      // SURF: float64 feature-major operands
   double* D = nullptr;
+  int tiled = 0;                // D in the tiled layout (MultiSURF; d_at)
+  int64_t dplane = 0;           // doubles of one distance plane (D, each Dpart)
+  int2 tw = make_int2(0, 0);    // k_exact_pairs' store_pair: (nb, world) when tiled
   int2* tiles = nullptr;
   double* thr = nullptr;
   float* Wt = nullptr;          // dense pair weights (sparse == 0)
@@ -2616,12 +2717,18 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   std::vector<int2> tl(g->n_tiles);
   for (int64_t t = 0; t < g->n_tiles; t++) tl[t] = make_int2(bi[t], bj[t]);
   g->list_cap = std::max<int64_t>(1 << 16, Q.n * 64);
+  // MultiSURF reads distances only inside owned tiles: tiled layout, one
+  // 128 x 128 block per owned tile (half the full matrix at world 1, 1/N of
+  // the tiles per rank).  ReliefF / SURF select neighbours over whole rows.
+  g->tiled = (Q.algo == ALGO_MULTISURF && !row_mode) ? 1 : 0;
+  g->dplane = g->tiled ? std::max<int64_t>(g->n_tiles, 1) * kTile * kTile : Q.n_pad * Q.n_pad;
+  g->tw = g->tiled ? make_int2((int)g->nb, world) : make_int2(0, 0);
   g->use_q16 = choose_q16(Q);
   // pass-1 chunk count and the per-tile work in feature units of 32-bit SAD
   const int64_t rows_q = (g->use_q16 ? Q.PC / 2 : Q.PC) + Q.PD;
   g->ksplit = choose_ksplit(g->n_tiles, device, (int)(rows_q / kBKQ),
                             (g->use_q16 ? Q.pc / 2 : Q.pc) + Q.pd,
-                            (size_t)Q.n_pad * Q.n_pad * sizeof(double));
+                            (size_t)g->dplane * sizeof(double));
   if (const char* e = std::getenv("FS_KSPLIT"))  // A/B of the K-split choice
     if (std::atoi(e) >= 1) g->ksplit = std::min(8, std::atoi(e));
   if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
@@ -2630,7 +2737,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   trace_mark("plan: host setup");
   if ((rc = dalloc(g, (char**)&g->x, xbytes)) || (rc = dalloc(g, &g->lab, Q.n_pad)) ||
       (rc = dalloc(g, &g->corr, Q.n_pad)) ||
-      (rc = dalloc(g, &g->D, (size_t)Q.n_pad * Q.n_pad)) ||
+      (rc = dalloc(g, &g->D, (size_t)g->dplane)) ||
       (rc = dalloc(g, &g->tiles, g->n_tiles)) || (rc = dalloc(g, &g->thr, Q.n_pad)) ||
       (rc = dalloc(g, &g->list, g->list_cap)) || (rc = dalloc(g, &g->list_count, 1)))
     return fail(rc);
@@ -2648,7 +2755,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       return fail(FS_EHIP);
   }
   if (g->ksplit > 1 &&
-      (rc = dalloc(g, &g->Dpart, (size_t)(g->ksplit - 1) * Q.n_pad * Q.n_pad)))
+      (rc = dalloc(g, &g->Dpart, (size_t)(g->ksplit - 1) * g->dplane)))
     return fail(rc);
   if ((rc = dalloc(g, &g->rspart, (size_t)std::max<int64_t>(g->n_tiles, 1) * 256))) return fail(rc);
   trace_mark("plan: hipMalloc");
@@ -2730,11 +2837,12 @@ static int run_quantize_dist(Plan* g) {
     FS_HIP(hipEventRecord(g->ev[0], g->stream));
     k_dist<<<(unsigned)(g->n_tiles * g->ksplit), 256, 0, g->stream>>>(
         g->xqT, Q.n_pad, (int)((Q.q16 ? Q.PC / 2 : Q.PC) / kBKQ), (int)(Q.PD / kBKQ), Q.SCu,
-        Q.q16, g->tiles, g->ksplit, g->D, g->Dpart);
+        Q.q16, g->tiles, g->ksplit, g->tiled, g->dplane, g->D, g->Dpart);
     FS_TRY(launch_check("k_dist"));
     if (g->ksplit > 1) {
       k_dist_merge<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, g->Dpart, g->ksplit - 1,
-                                                                g->tiles, Q.n_pad);
+                                                                g->tiles, Q.n_pad, g->tiled,
+                                                                g->dplane);
       FS_TRY(launch_check("k_dist_merge"));
     }
     FS_HIP(hipEventRecord(g->ev[1], g->stream));
@@ -2770,8 +2878,8 @@ static int refine_pairs(Plan* g, int algo, double delta) {
   for (int attempt = 0; attempt < 2; attempt++) {
     FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
     k_flag_pairs<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(
-        g->D, Q.n, Q.n_pad, g->tiles, g->thr, algo, 1.0 / Q.SC, delta, g->list, g->list_cap,
-        g->list_count);
+        g->D, Q.n, Q.n_pad, g->tiled, g->tiles, g->thr, algo, 1.0 / Q.SC, delta, g->list,
+        g->list_cap, g->list_count);
     FS_TRY(launch_check("k_flag_pairs"));
     unsigned long long cnt = 0;
     FS_HIP(hipMemcpyAsync(&cnt, g->list_count, sizeof(cnt), hipMemcpyDeviceToHost, g->stream));
@@ -2789,15 +2897,15 @@ static int refine_pairs(Plan* g, int algo, double delta) {
   if (g->rows_direct && !std::getenv("FS_EXACT_GATHER"))
     k_exact_pairs_rows<<<grid, 256, 0, g->stream>>>((const float*)g->x, Q.p_in, g->scl32, Q.SC,
                                                     g->list, g->list_count, g->list_cap, Q.n_pad,
-                                                    g->D);
+                                                    g->tw, g->D);
   else if (g->x_is_f64)
     k_exact_pairs<double><<<grid, 256, 0, g->stream>>>(
         (const double*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, 0, g->D);
+        g->list_count, g->list_cap, Q.n_pad, g->tw, 0, g->D);
   else
     k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
         (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, 0, g->D);
+        g->list_count, g->list_cap, Q.n_pad, g->tw, 0, g->D);
   return launch_check("k_exact_pairs");
 }
 
@@ -2809,11 +2917,12 @@ static int run_weights(Plan* g, const double* counts, int algo, double inv_sc) {
     FS_HIP(hipMemsetAsync(g->nnz, 0, sizeof(unsigned long long), g->stream));
     g->nnz_valid = true;
     k_weights_sparse<<<(unsigned)g->n_tiles, 64 * kSWaves, 0, g->stream>>>(
-        g->D, Q.n, Q.n_pad, g->tiles, g->thr, g->lab, counts, algo, Q.use_star, inv_sc, g->r_lo,
-        g->r_hi, g->ent, g->nnz);
+        g->D, Q.n, Q.n_pad, g->tiled, g->tiles, g->thr, g->lab, counts, algo, Q.use_star, inv_sc,
+        g->r_lo, g->r_hi, g->ent, g->nnz);
     return launch_check("k_weights_sparse");
   }
-  k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles, g->thr,
+  k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiled, g->tiles,
+                                                         g->thr,
                                                          g->lab, counts, algo, Q.use_star, inv_sc,
                                                          g->r_lo, g->r_hi, g->Wt);
   return launch_check("k_weights");
@@ -2846,8 +2955,7 @@ int plan_pass1(Plan* g, double* rowstats) {
   const Prepared& Q = g->P;
   FS_TRY(run_quantize_dist(g));
   if (g->n_tiles > 0) {
-    k_tile_rowstats<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
-                                                                 g->rspart);
+    k_tile_rowstats<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, g->tiles, g->rspart);
     FS_TRY(launch_check("k_tile_rowstats"));
   }
   FS_HIP(hipStreamWaitEvent(g->stream, g->ev_join, 0));  // corr (side stream)
@@ -2866,8 +2974,8 @@ int plan_select(Plan* g, const double* rowstats, double* counts) {
   FS_TRY(refine_pairs(g, ALGO_MULTISURF, Q.amb_delta * Q.SC));
   FS_HIP(hipMemsetAsync(counts, 0, sizeof(double) * 2 * Q.n, g->stream));
   if (g->n_tiles > 0) {
-    k_tile_counts<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiles,
-                                                               g->lab, g->thr, counts);
+    k_tile_counts<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, g->tiles, g->lab,
+                                                               g->thr, counts);
     FS_TRY(launch_check("k_tile_counts"));
   }
   if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
@@ -3069,7 +3177,7 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
     const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
     k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
         (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, 1, g->D);
+        g->list_count, g->list_cap, Q.n_pad, make_int2(0, 0), 1, g->D);
     FS_TRY(launch_check("k_exact_pairs"));
   }
   // 3. exact selection
