@@ -42,7 +42,7 @@ EXPORTED = (
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_set_rows",
-    "fs_plan_info", "fs_plan_calibration", "fs_plan_weighted_pairs", "fs_plan_kernel_ms",
+    "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs", "fs_plan_kernel_ms",
     "fs_plan_destroy",
 )
 
@@ -113,6 +113,8 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_pass2.argtypes = [_vp, _vp, _vp]
     lib.fs_plan_info.argtypes = [_vp, _i64p, _f64p, _i64p]
     lib.fs_plan_calibration.argtypes = [_vp, _f64p]
+    lib.fs_plan_set_shard.argtypes = [_vp, _int, _int]
+    lib.fs_multisurf_shards.argtypes = [_int, _i64, _i64, _int, ctypes.POINTER(_int)]
     lib.fs_plan_weighted_pairs.argtypes = [_vp, _i64p]
     lib.fs_plan_kernel_ms.argtypes = [_vp, _int]
     lib.fs_plan_kernel_ms.restype = ctypes.c_double
@@ -121,7 +123,7 @@ def _load() -> ctypes.CDLL:
                  "fs_plan_set_rows", "fs_relieff_score", "fs_surf_score",
                  "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create",
                  "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
-                 "fs_plan_pass2", "fs_plan_info", "fs_plan_calibration", "fs_plan_weighted_pairs",
+                 "fs_plan_pass2", "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs",
                  "fs_plan_destroy"):
         getattr(lib, name).restype = _int
     return lib
@@ -159,6 +161,13 @@ def staged_x(backend, x, device=0):
         yield
     finally:
         _lib.fs_unstage_x(h)
+
+
+def multisurf_shards(n: int, p: int, world: int = 1, device: int = 0) -> int:
+    """Tile shards per device that fit a MultiSURF job (fs_multisurf_shards)."""
+    v = _int(1)
+    check(_lib.fs_multisurf_shards(int(device), int(n), int(p), int(world), ctypes.byref(v)))
+    return int(v.value)
 
 
 @contextlib.contextmanager
@@ -395,6 +404,10 @@ class Plan:
         check(_lib.fs_plan_info(self._h, ctypes.byref(tiles), ctypes.byref(pfe),
                                 ctypes.byref(ref)))
         return int(tiles.value), float(pfe.value), int(ref.value)
+
+    def set_shard(self, rank: int, world: int) -> None:
+        """Re-target to the pair tiles of shard (rank, world) (fs_plan_set_shard)."""
+        check(_lib.fs_plan_set_shard(self._h, int(rank), int(world)))
 
     def calibration(self) -> dict:
         """Refinement-band calibration of the current layout (fs_plan_calibration)."""

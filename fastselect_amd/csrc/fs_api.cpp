@@ -553,6 +553,40 @@ int fs_plan_set_rows(fs_plan* pl, int64_t row_begin, int64_t row_end) {
   return FS_OK;
 }
 
+int fs_plan_set_shard(fs_plan* pl, int rank, int world) {
+  if (!pl) {
+    set_error("plan is NULL");
+    return FS_EINVAL;
+  }
+  if (!is_multisurf_plan(pl)) return FS_EINVAL;
+  if (world < 1 || rank < 0 || rank >= world) {
+    set_error("shard rank/world must satisfy 0 <= rank < world");
+    return FS_EINVAL;
+  }
+  if (pl->g) {
+    const int rc = gpu::plan_set_shard(pl->g, rank, world);
+    if (rc != FS_OK) return rc;
+  }
+  pl->rank = rank;
+  pl->world = world;
+  return FS_OK;
+}
+
+int fs_multisurf_shards(int device, int64_t n, int64_t p, int world, int* shards) {
+  if (!shards || n < 2 || p < 1 || world < 1) {
+    set_error("fs_multisurf_shards: need shards, n >= 2, p >= 1, world >= 1");
+    return FS_EINVAL;
+  }
+  *shards = 1;
+  if (gpu::device_count() <= 0) return FS_OK;
+  Prepared P;
+  P.n = n;
+  P.n_pad = (n + kTile - 1) / kTile * kTile;
+  P.PW = (p + kFeatPad - 1) / kFeatPad * kFeatPad;
+  *shards = gpu::multisurf_shards(P, device, world);
+  return FS_OK;
+}
+
 int fs_plan_info(const fs_plan* pl, int64_t* owned_tiles_out, double* pfe,
                  int64_t* refined_rows) {
   if (!pl) {

@@ -1474,6 +1474,13 @@ __global__ __launch_bounds__(1024) void k_score_sparse(
   }
 }
 
+// dst[k] += src[k] (the tile shards' partial vectors, summed in shard order).
+__global__ void k_accumulate(double* __restrict__ dst, const double* __restrict__ src,
+                             int64_t count) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < count) dst[k] += src[k];
+}
+
 // out[out_pos[c]] = sum over segments of part[seg][c] (fixed order).
 __global__ void k_reduce(const double* __restrict__ part, int64_t nseg, int64_t PW,
                          const int64_t* __restrict__ out_pos, double* __restrict__ out) {
@@ -2082,7 +2089,9 @@ struct Plan {
   std::vector<void*> owned;         // buffers sized by n (live as long as the plan)
   std::vector<void*> owned_layout;  // buffers sized by the feature layout (PW)
   std::vector<void*> scratch;       // buffers of one plan_score call
-  int alloc_target = 0;             // dalloc target: 0 owned, 1 owned_layout, 2 scratch
+  std::vector<void*> owned_shard;   // buffers sized by the owned tiles (plan_set_shard)
+  int alloc_target = 0;             // dalloc target: 0 owned, 1 owned_layout, 2 scratch, 3 shard
+  bool row_mode = false;
   std::vector<char> colmin, colmax; // per input column, x's dtype (device-measured)
 };
 
@@ -2294,7 +2303,10 @@ static int dalloc(Plan* g, T** p, size_t count) {
   void* q = nullptr;
   if (count == 0) count = 1;
   if (int rc = dev_alloc(&q, count * sizeof(T), g->device)) return rc;
-  (g->alloc_target == 1 ? g->owned_layout : g->alloc_target == 2 ? g->scratch : g->owned)
+  (g->alloc_target == 1   ? g->owned_layout
+   : g->alloc_target == 2 ? g->scratch
+   : g->alloc_target == 3 ? g->owned_shard
+                          : g->owned)
       .push_back(q);
   *p = (T*)q;
   return FS_OK;
@@ -2330,6 +2342,7 @@ void plan_destroy(Plan* g) {
   for (void* q : g->owned) dev_free(q);
   for (void* q : g->owned_layout) dev_free(q);
   for (void* q : g->scratch) dev_free(q);
+  for (void* q : g->owned_shard) dev_free(q);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
   if (g->ev_fork) (void)hipEventDestroy(g->ev_fork);
@@ -2649,6 +2662,79 @@ static int plan_layout(Plan* g) {
   return FS_OK;
 }
 
+// Everything sized by the plan's owned tiles: the tile list, the distance
+// planes (tiled for MultiSURF: one 128 x 128 block per tile), the K-split,
+// row-moment partials and the pass-2 weights.  Called by plan_create and
+// again by plan_set_shard, which frees the previous shard's buffers first.
+static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vector<int32_t>& bj) {
+  const Prepared& Q = g->P;
+  g->n_tiles = (int64_t)bi.size();
+  std::vector<int2> tl(g->n_tiles);
+  for (int64_t t = 0; t < g->n_tiles; t++) tl[t] = make_int2(bi[t], bj[t]);
+  // MultiSURF reads distances only inside owned tiles: tiled layout, one
+  // 128 x 128 block per owned tile (half the full matrix at world 1, 1/N of
+  // the tiles per rank).  ReliefF / SURF select neighbours over whole rows.
+  g->tiled = (Q.algo == ALGO_MULTISURF && !g->row_mode) ? 1 : 0;
+  g->dplane = g->tiled ? std::max<int64_t>(g->n_tiles, 1) * kTile * kTile : Q.n_pad * Q.n_pad;
+  g->tw = g->tiled ? make_int2((int)g->nb, g->world) : make_int2(0, 0);
+  // pass-1 chunk count and the per-tile work in feature units of 32-bit SAD
+  const int64_t rows_q = (g->use_q16 ? Q.PC / 2 : Q.PC) + Q.PD;
+  g->ksplit = choose_ksplit(g->n_tiles, g->device, (int)(rows_q / kBKQ),
+                            (g->use_q16 ? Q.pc / 2 : Q.pc) + Q.pd,
+                            (size_t)g->dplane * sizeof(double));
+  if (const char* e = std::getenv("FS_KSPLIT"))  // A/B of the K-split choice
+    if (std::atoi(e) >= 1) g->ksplit = std::min(8, std::atoi(e));
+  if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
+  g->alloc_target = 3;
+  int rc = FS_OK;
+  if ((rc = dalloc(g, &g->D, (size_t)g->dplane)) || (rc = dalloc(g, &g->tiles, g->n_tiles)) ||
+      (rc = dalloc(g, &g->rspart, (size_t)std::max<int64_t>(g->n_tiles, 1) * 256))) {
+  } else if (Q.algo != ALGO_RELIEFF && !g->sparse) {
+    rc = dalloc(g, &g->Wt, (size_t)(g->n_tiles + 1) * kTile * kTile);
+  } else if (g->sparse) {
+    // One spare tile: k_score_sparse prefetches two groups past the end of a
+    // stream.  Zeroed once, so such reads (and stream tails never written)
+    // hold in-range row offsets.
+    const size_t count = (size_t)(g->n_tiles + 1) * kSWaves * kStreamEntries;
+    if (!(rc = dalloc(g, &g->ent, count)) && !(rc = dalloc(g, &g->nnz, 1)) &&
+        hipMemsetAsync(g->ent, 0, sizeof(uint2) * count, g->stream) != hipSuccess)
+      rc = FS_EHIP;
+  }
+  if (!rc && g->ksplit > 1) rc = dalloc(g, &g->Dpart, (size_t)(g->ksplit - 1) * g->dplane);
+  g->alloc_target = 0;
+  if (rc) return rc;
+  g->nnz_valid = false;
+  return h2d(g, g->tiles, tl.data(), g->n_tiles);
+}
+
+int plan_set_shard(Plan* g, int rank, int world) {
+  if (g->P.algo != ALGO_MULTISURF || g->row_mode) {
+    set_error("tile shards of a plan are MultiSURF-only");
+    return FS_EINVAL;
+  }
+  if (world < 1 || rank < 0 || rank >= world) {
+    set_error("invalid shard rank/world");
+    return FS_EINVAL;
+  }
+  FS_HIP(hipSetDevice(g->device));
+  FS_HIP(hipStreamSynchronize(g->stream));
+  if (g->side) FS_HIP(hipStreamSynchronize(g->side));
+  for (void* q : g->owned_shard) dev_free(q);
+  g->owned_shard.clear();
+  g->D = g->Dpart = nullptr;
+  g->Wt = nullptr;
+  g->ent = nullptr;
+  g->tiles = nullptr;
+  g->rspart = nullptr;
+  g->nnz = nullptr;
+  g->rank = rank;
+  g->world = world;
+  std::vector<int32_t> bi, bj;
+  owned_tiles(g->nb, rank, world, bi, bj);
+  FS_TRY(setup_shard(g, bi, bj));
+  return plan_layout(g);  // pass-2 segments and this shard's mean-correction columns
+}
+
 int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int device,
                 int rank, int world, uint64_t stream, int64_t r_lo, int64_t r_hi) {
   *out = nullptr;
@@ -2713,51 +2799,18 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     g->r_hi = Q.n;
     owned_tiles(g->nb, rank, world, bi, bj);
   }
-  g->n_tiles = (int64_t)bi.size();
-  std::vector<int2> tl(g->n_tiles);
-  for (int64_t t = 0; t < g->n_tiles; t++) tl[t] = make_int2(bi[t], bj[t]);
+  g->row_mode = row_mode;
   g->list_cap = std::max<int64_t>(1 << 16, Q.n * 64);
-  // MultiSURF reads distances only inside owned tiles: tiled layout, one
-  // 128 x 128 block per owned tile (half the full matrix at world 1, 1/N of
-  // the tiles per rank).  ReliefF / SURF select neighbours over whole rows.
-  g->tiled = (Q.algo == ALGO_MULTISURF && !row_mode) ? 1 : 0;
-  g->dplane = g->tiled ? std::max<int64_t>(g->n_tiles, 1) * kTile * kTile : Q.n_pad * Q.n_pad;
-  g->tw = g->tiled ? make_int2((int)g->nb, world) : make_int2(0, 0);
   g->use_q16 = choose_q16(Q);
-  // pass-1 chunk count and the per-tile work in feature units of 32-bit SAD
-  const int64_t rows_q = (g->use_q16 ? Q.PC / 2 : Q.PC) + Q.PD;
-  g->ksplit = choose_ksplit(g->n_tiles, device, (int)(rows_q / kBKQ),
-                            (g->use_q16 ? Q.pc / 2 : Q.pc) + Q.pd,
-                            (size_t)g->dplane * sizeof(double));
-  if (const char* e = std::getenv("FS_KSPLIT"))  // A/B of the K-split choice
-    if (std::atoi(e) >= 1) g->ksplit = std::min(8, std::atoi(e));
-  if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
   const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
   int rc;
   trace_mark("plan: host setup");
   if ((rc = dalloc(g, (char**)&g->x, xbytes)) || (rc = dalloc(g, &g->lab, Q.n_pad)) ||
-      (rc = dalloc(g, &g->corr, Q.n_pad)) ||
-      (rc = dalloc(g, &g->D, (size_t)g->dplane)) ||
-      (rc = dalloc(g, &g->tiles, g->n_tiles)) || (rc = dalloc(g, &g->thr, Q.n_pad)) ||
+      (rc = dalloc(g, &g->corr, Q.n_pad)) || (rc = dalloc(g, &g->thr, Q.n_pad)) ||
       (rc = dalloc(g, &g->list, g->list_cap)) || (rc = dalloc(g, &g->list_count, 1)))
     return fail(rc);
   g->sparse = choose_sparse(g, Q);
-  if (Q.algo != ALGO_RELIEFF && !g->sparse &&
-      (rc = dalloc(g, &g->Wt, (size_t)(g->n_tiles + 1) * kTile * kTile)))
-    return fail(rc);
-  if (g->sparse) {
-    // One spare tile: k_score_sparse prefetches two groups past the end of a
-    // stream.  Zeroed once, so such reads (and stream tails never written)
-    // hold in-range row offsets.
-    const size_t count = (size_t)(g->n_tiles + 1) * kSWaves * kStreamEntries;
-    if ((rc = dalloc(g, &g->ent, count)) || (rc = dalloc(g, &g->nnz, 1))) return fail(rc);
-    if (hipMemsetAsync(g->ent, 0, sizeof(uint2) * count, g->stream) != hipSuccess)
-      return fail(FS_EHIP);
-  }
-  if (g->ksplit > 1 &&
-      (rc = dalloc(g, &g->Dpart, (size_t)(g->ksplit - 1) * g->dplane)))
-    return fail(rc);
-  if ((rc = dalloc(g, &g->rspart, (size_t)std::max<int64_t>(g->n_tiles, 1) * 256))) return fail(rc);
+  if ((rc = setup_shard(g, bi, bj))) return fail(rc);
   trace_mark("plan: hipMalloc");
   std::vector<int32_t> lab(Q.n_pad, -1);
   std::copy(Q.labels.begin(), Q.labels.end(), lab.begin());
@@ -2768,8 +2821,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     return fail(FS_EHIP);
   }
   if ((!sx && (rc = h2d(g, (char*)g->x, (const char*)x, xbytes))) ||
-      (rc = h2d(g, g->lab, lab.data(), Q.n_pad)) ||
-      (rc = h2d(g, g->tiles, tl.data(), g->n_tiles)))
+      (rc = h2d(g, g->lab, lab.data(), Q.n_pad)))
     return fail(rc);
   if ((rc = plan_layout(g))) return fail(rc);
   trace_mark("plan: H2D + layout");
@@ -3051,14 +3103,89 @@ static int finish_scores(Plan* g, double* scores_dev, float* scores_out) {
   return FS_OK;
 }
 
+// Tile shards a device needs for a MultiSURF job of `world` ranks: the
+// tile-sized buffers (~260 KB per tile: the tiled distance block, the
+// pass-2 weight streams, partials) of a rank's 1/world of the n_pad^2/2/128^2
+// tiles, against the free device memory left after the per-sample buffers
+// (X, quantised operands, pass-2 operands, correction terms: ~16 n PW
+// bytes) and a 15% reserve.  1 when everything fits; FS_SHARDS forces it.
+int multisurf_shards(const Prepared& P, int device, int world) {
+  if (const char* e = std::getenv("FS_SHARDS"))
+    if (std::atoi(e) >= 1) return std::atoi(e);
+  size_t free_b = 0, total_b = 0;
+  if (hipSetDevice(device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+    (void)hipGetLastError();
+    return 1;
+  }
+  const int64_t nb = P.n_pad / kTile;
+  const double tiles = (double)nb * (nb + 1) / 2.0 / (double)std::max(world, 1);
+  const double per_tile = 2.0 * kTile * kTile * 8.0 + 8.0 * kTile * 256.0 / 2.0;
+  const double fixed = 16.0 * (double)P.n_pad * (double)P.PW + 8.0 * (double)P.n * 64.0;
+  const double avail = 0.85 * (double)free_b - fixed;
+  if (avail <= 0.0) return 1;  // not even the samples fit: let the allocation report it
+  const double v = std::ceil(tiles * per_tile / avail);
+  return (int)std::max(1.0, std::min(v, 4096.0));
+}
+
+// One MultiSURF scoring pass on a single device in V tile shards (V > 1 when
+// the tile buffers of the whole triangle exceed the device: n beyond HBM).
+// The distances of a shard are recomputed in each of the three rounds (row
+// moments; thresholds -> refinement -> neighbour counts; weights -> pass 2),
+// because no shard's distances are kept while another shard runs: 3x the
+// pass-1 work for O(n p + n^2 / V) device memory.  The reference streams
+// each focal sample's distance row the same way (MultiSURF.py:174-214).
+// V == 1 is the plain pass1 / select / pass2 sequence.
+static int run_multisurf_shards(Plan* g, int shards, int rank, int world, double* rs, double* cnt,
+                                double* sc) {
+  const Prepared& Q = g->P;
+  if (shards <= 1) {
+    FS_TRY(plan_pass1(g, rs));
+    FS_TRY(plan_select(g, rs, cnt));
+    return plan_pass2(g, cnt, sc);
+  }
+  double *rs_v = nullptr, *cnt_v = nullptr, *sc_v = nullptr;
+  FS_TRY(dalloc(g, &rs_v, 3 * Q.n));
+  FS_TRY(dalloc(g, &cnt_v, 2 * Q.n));
+  FS_TRY(dalloc(g, &sc_v, Q.n_kept));
+  const int W = world * shards;
+  auto add = [&](double* dst, const double* src, int64_t count, bool first) -> int {
+    if (first)
+      return hipMemcpyAsync(dst, src, sizeof(double) * count, hipMemcpyDeviceToDevice,
+                            g->stream) == hipSuccess
+                 ? FS_OK
+                 : FS_EHIP;
+    k_accumulate<<<(unsigned)((count + 255) / 256), 256, 0, g->stream>>>(dst, src, count);
+    return launch_check("k_accumulate");
+  };
+  for (int v = 0; v < shards; v++) {  // round 1: row moments
+    FS_TRY(plan_set_shard(g, rank + world * v, W));
+    FS_TRY(plan_pass1(g, rs_v));
+    FS_TRY(add(rs, rs_v, 3 * Q.n, v == 0));
+  }
+  for (int v = 0; v < shards; v++) {  // round 2: thresholds, refinement, counts
+    FS_TRY(plan_set_shard(g, rank + world * v, W));
+    FS_TRY(plan_pass1(g, rs_v));
+    FS_TRY(plan_select(g, rs, cnt_v));
+    FS_TRY(add(cnt, cnt_v, 2 * Q.n, v == 0));
+  }
+  for (int v = 0; v < shards; v++) {  // round 3: weights, pass 2
+    FS_TRY(plan_set_shard(g, rank + world * v, W));
+    FS_TRY(plan_pass1(g, rs_v));
+    FS_TRY(plan_select(g, rs, cnt_v));
+    FS_TRY(plan_pass2(g, cnt, sc_v));
+    FS_TRY(add(sc, sc_v, Q.n_kept, v == 0));
+  }
+  return FS_OK;
+}
+
 int multisurf_run(const Prepared& P, const void* x, int device, float* scores_out) {
   Plan* g = nullptr;
-  FS_TRY(plan_create(&g, P, x, 0, device, 0, 1, 0));
+  const int shards = multisurf_shards(P, device, 1);
+  FS_TRY(plan_create(&g, P, x, 0, device, 0, shards, 0));
   double *rs = nullptr, *cnt = nullptr, *sc = nullptr;
   int rc;
   if ((rc = dalloc(g, &rs, 3 * P.n)) || (rc = dalloc(g, &cnt, 2 * P.n)) ||
-      (rc = dalloc(g, &sc, P.n_kept)) || (rc = plan_pass1(g, rs)) ||
-      (rc = plan_select(g, rs, cnt)) || (rc = plan_pass2(g, cnt, sc)) ||
+      (rc = dalloc(g, &sc, P.n_kept)) || (rc = run_multisurf_shards(g, shards, 0, 1, rs, cnt, sc)) ||
       (rc = finish_scores(g, sc, scores_out))) {
     plan_destroy(g);
     return rc;
@@ -3077,13 +3204,14 @@ static int copy_sums(Plan* g, const double* sums_dev, double* sums_out) {
 int multisurf_rows(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
                    double* sums_out) {
   Plan* g = nullptr;
-  FS_TRY(plan_create(&g, P, x, 0, device, 0, 1, 0));
+  const int shards = multisurf_shards(P, device, 1);
+  FS_TRY(plan_create(&g, P, x, 0, device, 0, shards, 0));
   double *rs = nullptr, *cnt = nullptr, *sc = nullptr;
   int rc;
   if ((rc = plan_set_rows(g, r_lo, r_hi)) || (rc = dalloc(g, &rs, 3 * P.n)) ||
       (rc = dalloc(g, &cnt, 2 * P.n)) || (rc = dalloc(g, &sc, P.n_kept)) ||
-      (rc = plan_pass1(g, rs)) || (rc = plan_select(g, rs, cnt)) ||
-      (rc = plan_pass2(g, cnt, sc)) || (rc = copy_sums(g, sc, sums_out))) {
+      (rc = run_multisurf_shards(g, shards, 0, 1, rs, cnt, sc)) ||
+      (rc = copy_sums(g, sc, sums_out))) {
     plan_destroy(g);
     return rc;
   }

@@ -311,6 +311,13 @@ int plan_pass2(Plan* g, const double* counts_dev, double* scores_dev);
 // MultiSURF focal-sample slice: the next pass2 sums the pair sides of the
 // focal samples [r_lo, r_hi) only (thresholds and counts stay global).
 int plan_set_rows(Plan* g, int64_t r_lo, int64_t r_hi);
+// Re-target a MultiSURF plan to the tiles of (rank, world) (tile t belongs to
+// rank t % world): frees the previous shard's tile buffers and lays out the
+// new ones.  X and its quantised operands stay resident.
+int plan_set_shard(Plan* g, int rank, int world);
+// Tile shards per device for a MultiSURF job of `world` ranks so that the
+// tile buffers fit the device (1 = no sharding; FS_SHARDS forces it).
+int multisurf_shards(const Prepared& P, int device, int world);
 // ReliefF / SURF plans: float64 score sums of the plan's focal rows
 // (sums_dev[n_kept], device memory), for the plan's current feature subset.
 int plan_score(Plan* g, double* sums_dev);

@@ -123,11 +123,20 @@ class ShardedMultiSURF:
     """
 
     def __init__(self, x, y, recip, is_discrete, use_star=False, backend="gpu", device=0,
-                 shard=True, rows=None):
+                 shard=True, rows=None, shards=None):
+        import os
+
         import torch
         self.dist, self.rank, self.world = _dist() if shard else (None, 0, 1)
         self.n, self.p = x.shape
         self.backend = backend
+        # tile shards per device (n beyond HBM): the device holds the distance
+        # tiles of one shard at a time (fs_plan_set_shard, three rounds a step)
+        if shards is None:
+            env = os.environ.get("FS_SHARDS")
+            shards = int(env) if env else (
+                _lib.multisurf_shards(self.n, self.p, self.world, device) if backend == "gpu" else 1)
+        self.shards = max(1, int(shards))
         if backend == "gpu":
             torch.cuda.set_device(device)
             self.tdev = torch.device("cuda", device)
@@ -136,7 +145,8 @@ class ShardedMultiSURF:
             self.tdev = torch.device("cpu")
             stream = 0
         self.plan = _lib.Plan(backend, x, y, recip, is_discrete, use_star=use_star,
-                              rank=self.rank, world=self.world, device=device, stream=stream)
+                              rank=self.rank, world=self.world * self.shards, device=device,
+                              stream=stream)
         if rows is not None:  # focal-sample slice: pass 2 sums those samples only
             self.plan.set_rows(*rows)
         f64 = torch.float64
@@ -159,8 +169,46 @@ class ShardedMultiSURF:
         if self.dist is not None:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
 
+    def _shard(self, v):
+        self.plan.set_shard(self.rank + self.world * v, self.world * self.shards)
+
+    def _step_shards(self):
+        """step() with V tile shards per device: three rounds over the shards
+        (row moments; thresholds + counts; weights + pass 2), each shard's
+        distances recomputed per round, the shards' partial vectors summed
+        before each all-reduce."""
+        import torch
+        V = self.shards
+        tmp3 = torch.zeros_like(self.rowstats)
+        tmp2 = torch.zeros_like(self.counts)
+        tmps = torch.zeros_like(self.scores)
+        self.rowstats.zero_()
+        for v in range(V):
+            self._shard(v)
+            self.plan.pass1(tmp3.data_ptr())
+            self.rowstats += tmp3
+        self._allreduce(self.rowstats)
+        self.counts.zero_()
+        for v in range(V):
+            self._shard(v)
+            self.plan.pass1(tmp3.data_ptr())
+            self.plan.select(self.rowstats.data_ptr(), tmp2.data_ptr())
+            self.counts += tmp2
+        self._allreduce(self.counts)
+        self.scores.zero_()
+        for v in range(V):
+            self._shard(v)
+            self.plan.pass1(tmp3.data_ptr())
+            self.plan.select(self.rowstats.data_ptr(), tmp2.data_ptr())
+            self.plan.pass2(self.counts.data_ptr(), tmps.data_ptr())
+            self.scores += tmps
+        self._allreduce(self.scores)
+        return (self.scores / self.n).float()
+
     def step(self):
         """One full scoring pass; returns float32 scores (device tensor)."""
+        if self.shards > 1:
+            return self._step_shards()
         self.plan.pass1(self.rowstats.data_ptr())
         self._allreduce(self.rowstats)
         self.plan.select(self.rowstats.data_ptr(), self.counts.data_ptr())

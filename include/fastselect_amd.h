@@ -247,6 +247,22 @@ FS_API int fs_plan_pass2(fs_plan* plan, const double* counts, double* scores);
  * [row_begin, row_end) (as fs_multisurf_score_rows; a new plan scores
  * [0, n)).  pass1 / select are unchanged: thresholds and counts are global. */
 FS_API int fs_plan_set_rows(fs_plan* plan, int64_t row_begin, int64_t row_end);
+/* Re-target a MultiSURF plan to the pair tiles of shard (rank, world) --
+ * tile t belongs to rank t % world -- keeping X and its quantised operands
+ * resident (the GPU plan frees the previous shard's distance tiles).  With
+ * it one device scores a job whose distance tiles exceed its memory in
+ * shards; the stages then run in three rounds, each over all shards (row
+ * moments -> all-reduce; select -> counts -> all-reduce; select, pass2 ->
+ * scores), every round recomputing the shard's distances
+ * (fastselect_amd/parallel.py ShardedMultiSURF).  An N-GPU job with V
+ * shards per GPU uses rank + N * v of N * V.  No reference counterpart (the
+ * reference streams each focal sample's distance row, MultiSURF.py:174-214). */
+FS_API int fs_plan_set_shard(fs_plan* plan, int rank, int world);
+/* Shards per device that keep a MultiSURF job of n samples, p features and
+ * `world` ranks within the device's free memory (1 when it fits, or without
+ * a GPU; FS_SHARDS overrides).  The one-shot fs_multisurf_score[_rows]
+ * shards by itself. */
+FS_API int fs_multisurf_shards(int device, int64_t n, int64_t p, int world, int* shards);
 /*
  * ReliefF / SURF plans (resident scoring): X uploaded once (GPU) or copied
  * (CPU), arguments as fs_relieff_score / fs_surf_score, focal samples

@@ -186,3 +186,48 @@ def test_row_chunks_cover_every_row_once():
                 assert 0 <= lo <= hi <= n and hi - lo <= rows
                 seen[lo:hi] += 1
             assert (seen == 1).all()
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+def test_tile_shards_match_one_shard_cpu(shards):
+    """fs_plan_set_shard: a job scored in V tile shards (three rounds, each
+    shard's distances recomputed per round; the GPU backend's mode for n
+    beyond HBM) equals the one-shard job."""
+    from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
+    X, y = make_classification(n_samples=700, n_features=60, n_informative=8, n_redundant=10,
+                               random_state=11)
+    x, yv, recip, isd = prepare_inputs(X, y, backend="cpu")
+    out = []
+    for v in (1, shards):
+        job = ShardedMultiSURF(x, yv, recip, isd, backend="cpu", shard=False, shards=v)
+        assert job.shards == v
+        out.append(job.step().numpy())
+        job.close()
+    assert scale_rel_err(out[1], out[0]) < 1e-6
+    assert set(np.argsort(out[1])[::-1][:10]) == set(np.argsort(out[0])[::-1][:10])
+
+
+def _shard_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
+    X, y = make_classification(n_samples=500, n_features=40, random_state=2)
+    x, yv, recip, isd = prepare_inputs(X, y, backend="cpu")
+    job = ShardedMultiSURF(x, yv, recip, isd, backend="cpu", shards=2)
+    np.save(f"{out_path}.{rank}.npy", job.step().numpy())
+    job.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_with_two_tile_shards_each(tmp_path):
+    """Ranks x shards: rank r takes shards r + 2 v of 4; equal to one process."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "s")
+    mp.spawn(_shard_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    a, b = np.load(out + ".0.npy"), np.load(out + ".1.npy")
+    np.testing.assert_array_equal(a, b)
+    X, y = make_classification(n_samples=500, n_features=40, random_state=2)
+    ref = MultiSURF(backend="cpu").fit(X, y).feature_importances_
+    assert scale_rel_err(a, ref) < 1e-6
