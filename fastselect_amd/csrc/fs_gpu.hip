@@ -668,63 +668,74 @@ __global__ __launch_bounds__(256) void k_quantize_f64(
 // MultiSURF row statistics, thresholds and neighbour counts
 // ---------------------------------------------------------------------------
 // Per-row distance moments from the owned tiles only (tiled D: MultiSURF).
-// One workgroup per owned tile t.  Lanes 0..127 sum row i0 + a over the
-// tile's 128 columns (T_t[b][a], b = 0..127: coalesced over a); off the
-// diagonal, waves 2 and 3 sum row j0 + b over the tile's rows, one column b
-// at a time (T_t[b][0..127], a contiguous read) with a fixed-order wave
-// reduction, lane b % 64 of wave 2 + b / 64 keeping the result -> part[t][256].
-// k_rowstats_reduce adds a row's tile partials in tile order (deterministic)
-// and appends this rank's mean correction: rowstats[3i] = sum D, [3i+1] =
-// sum D^2, [3i+2] = corr share.
+// One workgroup per owned tile t, the 128 x 128 block T_t[b][a] = D(i0 + a,
+// j0 + b) read once, coalesced, in 8 chunks of 16 b-rows: thread tid keeps
+// row i0 + (tid % 128)'s sums over its half of the b's (combined in a fixed
+// order at the end); off the diagonal each chunk is also staged in LDS,
+// where 8 lanes per b sum the chunk's 16 columns over a (shuffle-reduced in
+// a fixed order) -> part[t][256]: [0, 128) rows i0 + a, [128, 256) rows
+// j0 + b.  k_rowstats_reduce adds a row's tile partials in tile order
+// (deterministic) and appends this rank's mean correction: rowstats[3i] =
+// sum D, [3i+1] = sum D^2, [3i+2] = corr share.
 __global__ __launch_bounds__(256) void k_tile_rowstats(const double* __restrict__ D, int64_t n,
                                                        const int2* __restrict__ tiles,
                                                        double2* __restrict__ part) {
+  __shared__ double chunk[16][kTile + 1];
+  __shared__ double2 red[kTile];
+  __shared__ double2 cols[kTile];
   const int2 tl = tiles[blockIdx.x];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
   const double* T = D + (int64_t)blockIdx.x * kTile * kTile;
   const int tid = threadIdx.x;
+  const int a = tid & (kTile - 1), h = tid >> 7;
+  const bool diag = tl.x == tl.y;
+  const bool a_in = i0 + a < n;
   double s1 = 0.0, s2 = 0.0;
-  if (tid < kTile) {
-    const int a = tid;
-    const int64_t self = i0 + a;
-    if (self < n) {
-      // 8 loads in flight per step; skipped entries add 0.0
-      for (int b0 = 0; b0 < kTile; b0 += 8) {
-        double d[8];
+  for (int k = 0; k < kTile / 16; k++) {
+    double v[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const int64_t o = j0 + b0 + u;
-          const double v = T[(b0 + u) * kTile + a];
-          d[u] = (o < n && o != self) ? v : 0.0;
-        }
+    for (int u = 0; u < 8; u++) v[u] = T[(16 * k + h + 2 * u) * kTile + a];  // b = 16k + h + 2u
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-          s1 += d[u];
-          s2 += d[u] * d[u];
-        }
-      }
+    for (int u = 0; u < 8; u++) {
+      const int64_t o = j0 + 16 * k + h + 2 * u;
+      const double d = (a_in && o < n && o != i0 + a) ? v[u] : 0.0;
+      s1 += d;
+      s2 += d * d;
     }
-  } else if (tl.x != tl.y) {
-    const int lane = tid & 63, w2 = (tid >> 6) - 2;
-    // rows i0 + lane and i0 + 64 + lane of the tile, masked once
-    const bool in0 = i0 + lane < n, in1 = i0 + 64 + lane < n;
-    for (int k = 0; k < 64; k++) {
-      const int b = 64 * w2 + k;
-      const double v0 = in0 ? T[b * kTile + lane] : 0.0;
-      const double v1 = in1 ? T[b * kTile + 64 + lane] : 0.0;
-      double t1 = v0 + v1, t2 = v0 * v0 + v1 * v1;
+    if (!diag) {
 #pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        t1 += __shfl_xor(t1, o);
-        t2 += __shfl_xor(t2, o);
+      for (int u = 0; u < 8; u++) chunk[h + 2 * u][a] = a_in ? v[u] : 0.0;
+      __syncthreads();
+      if (tid < 128) {
+        const int bl = tid >> 3, q = tid & 7;
+        double c1 = 0.0, c2 = 0.0;
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+          const double d = chunk[bl][16 * q + e];
+          c1 += d;
+          c2 += d * d;
+        }
+#pragma unroll
+        for (int o = 4; o > 0; o >>= 1) {
+          c1 += __shfl_xor(c1, o);
+          c2 += __shfl_xor(c2, o);
+        }
+        if (q == 0) cols[16 * k + bl] = make_double2(c1, c2);
       }
-      if (lane == k && j0 + b < n) {
-        s1 = t1;
-        s2 = t2;
-      }
+      __syncthreads();
     }
   }
-  part[(int64_t)blockIdx.x * 256 + tid] = make_double2(s1, s2);
+  if (h == 1) red[a] = make_double2(s1, s2);
+  __syncthreads();
+  double2 out;
+  if (tid < kTile) {
+    const double2 o = red[a];
+    out = make_double2(s1 + o.x, s2 + o.y);
+  } else {
+    const int b = tid - kTile;
+    out = (!diag && j0 + b < n) ? cols[b] : make_double2(0.0, 0.0);
+  }
+  part[(int64_t)blockIdx.x * 256 + tid] = out;
 }
 
 __global__ void k_rowstats_reduce(const double2* __restrict__ part, int64_t n, int64_t nb,
