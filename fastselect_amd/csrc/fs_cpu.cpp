@@ -63,6 +63,40 @@ static inline double load_x(const void* x, int x_is_f64, int64_t idx) {
   return x_is_f64 ? ((const double*)x)[idx] : (double)((const float*)x)[idx];
 }
 
+// The refinement band from measured pairs, as the GPU backend's
+// calibrate_band (32-bit operands only here): kCalibPairs sampled pairs get
+// their quantised distance error against the reference's arithmetic (f32
+// diffs summed in f64) and the band becomes max(model, 3 max|err| + rms/2).
+static double calibrated_band(const Prepared& P, const void* x, int x_is_f64, int n_jobs) {
+  if (P.pc == 0 || P.n < 2) return P.amb_delta;
+  std::vector<std::pair<int64_t, int64_t>> pr;
+  calib_pairs(P.n, P.pc, std::min<int64_t>(kCalibPairs, P.n * (P.n - 1) / 2), pr);
+  std::vector<double> err(pr.size(), 0.0);
+  std::vector<double> qs(P.pc);
+  for (int64_t c = 0; c < P.pc; c++) qs[c] = P.scale[c] * P.SC;
+  parallel_for((int64_t)pr.size(), n_jobs, [&](int64_t k) {
+    const int64_t i = pr[k].first, j = pr[k].second;
+    double e = 0.0;
+    for (int64_t c = 0; c < P.pc; c++) {
+      const int64_t col = P.src_col[c];
+      const double a = load_x(x, x_is_f64, i * P.p_in + col);
+      const double b = load_x(x, x_is_f64, j * P.p_in + col);
+      const double ta = (a - P.offset[c]) * qs[c], tb = (b - P.offset[c]) * qs[c];
+      const uint32_t qa = (uint32_t)(ta + 0.5), qb = (uint32_t)(tb + 0.5);
+      const double ref = (double)(std::fabs((float)a - (float)b) * P.recip_in[col]);
+      e += (qa > qb ? (double)(qa - qb) : (double)(qb - qa)) - P.SC * ref;
+    }
+    err[k] = e;
+  });
+  double ss = 0.0, mx = 0.0;
+  for (double e : err) {
+    ss += e * e;
+    mx = std::max(mx, std::fabs(e));
+  }
+  return calibrated_delta(P.amb_delta_model > 0.0 ? P.amb_delta_model : P.amb_delta, P.SC,
+                          std::sqrt(ss / (double)err.size()), mx);
+}
+
 // Same arithmetic as k_quantize (fs_gpu.hip): t = (x - off) * qs,
 // q = trunc(t + 0.5), eps = q - t, every double operation rounded separately.
 static void quantize(const Prepared& P, const void* x, int x_is_f64, int n_jobs,
@@ -256,7 +290,7 @@ int multisurf_select(const Prepared& P, const void* x, int rank, int world,
     if (var < 0.0) var = 0.0;
     S.thr[i] = (mu - rowstats[3 * i + 2] / nm1) - 0.5 * std::sqrt(var);
   }
-  const double dq = P.amb_delta * P.SC;
+  const double dq = calibrated_band(P, x, 0, n_jobs) * P.SC;
   S.refined = refine_pairs(P, x, 0, rank, world, n_jobs, S.D, [&](int64_t i, int64_t j, double d) {
     return std::fabs(d - S.thr[i]) < dq || std::fabs(d - S.thr[j]) < dq;
   });
@@ -394,7 +428,7 @@ static float relieff_exact_key(const Prepared& P, const float* x, int64_t i, int
 // k-th distance exactly -- numba's quicksort order over the exact row.
 // nbr[c] receives the chosen neighbours of class c.
 static void relieff_select_row(const Prepared& P, const float* x, const std::vector<double>& D,
-                               int64_t i, std::vector<std::vector<int32_t>>& nbr) {
+                               int64_t i, double amb, std::vector<std::vector<int32_t>>& nbr) {
   const int64_t n = P.n, k = P.k_neighbors;
   const int C = P.n_classes;
   const double inv_sc = 1.0 / P.SC;
@@ -421,7 +455,7 @@ static void relieff_select_row(const Prepared& P, const float* x, const std::vec
     if (kc == 0 || kc == (int64_t)members[c].size()) continue;  // take all
     // exact keys for every candidate within the quantisation band of T
     const float t0 = kth(c, kc);
-    const double band = 2.0 * (P.amb_delta + (double)t0 * 1.2e-7);
+    const double band = 2.0 * (amb + (double)t0 * 1.2e-7);
     for (int32_t j : members[c])
       if (std::fabs((double)key[j] - (double)t0) <= band) {
         key[j] = relieff_exact_key(P, x, i, j);
@@ -485,12 +519,13 @@ int relieff_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int6
   distances(P, xq, 0, 1, n_jobs, D);
   const int64_t n = P.n, k = P.k_neighbors;
   const int C = P.n_classes;
+  const double amb = calibrated_band(P, x, 0, n_jobs);
   // per-row partial sums, folded in row order for determinism
   std::vector<double> part((size_t)n * P.PW, 0.0);
   parallel_for(n, n_jobs, [&](int64_t i) {
     if (i < r_lo || i >= r_hi) return;  // not a focal sample of this call
     std::vector<std::vector<int32_t>> nbr(C);
-    relieff_select_row(P, (const float*)x, D, i, nbr);
+    relieff_select_row(P, (const float*)x, D, i, amb, nbr);
     const int32_t li = P.labels[i];
     double denom = 1.0 - P.class_prior[li];
     if (denom == 0.0) denom = 1.0;

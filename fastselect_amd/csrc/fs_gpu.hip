@@ -2465,7 +2465,6 @@ static int choose_sparse(const Plan* g, const Prepared& P) {
 //    spread term of the threshold (|sigma_q - sigma| <= rms_j(err_ij)).
 // For independent rounding this reproduces the model band (3 x ~3.7 sigma +
 // sigma/2 < 12 sigma), so ordinary data keeps its refinement cost.
-constexpr int64_t kCalibPairs = 4096;
 constexpr double kCoherence = 2.0;
 
 static int calibrate_band(Plan* g) {
@@ -2478,20 +2477,10 @@ static int calibrate_band(Plan* g) {
   if (Q.algo == ALGO_SURF || Q.pc == 0 || Q.n < 2) return FS_OK;
   const int64_t all_pairs = Q.n * (Q.n - 1) / 2;
   const int64_t S = std::min<int64_t>(kCalibPairs, all_pairs);
+  std::vector<std::pair<int64_t, int64_t>> smp;
+  calib_pairs(Q.n, Q.pc, S, smp);
   std::vector<int2> pr((size_t)S);
-  uint64_t st = 0x9E3779B97F4A7C15ull ^ ((uint64_t)Q.n << 20) ^ (uint64_t)Q.pc;
-  auto next = [&]() {  // splitmix64
-    uint64_t z = (st += 0x9E3779B97F4A7C15ull);
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-  };
-  for (int64_t k = 0; k < S; k++) {
-    const int64_t i = (int64_t)(next() % (uint64_t)Q.n);
-    int64_t j = (int64_t)(next() % (uint64_t)(Q.n - 1));
-    if (j >= i) j++;
-    pr[(size_t)k] = make_int2((int)std::min(i, j), (int)std::max(i, j));
-  }
+  for (int64_t k = 0; k < S; k++) pr[(size_t)k] = make_int2((int)smp[k].first, (int)smp[k].second);
   const int q_now = Q.q16;
   double sc[2];
   for (int w = 0; w < 2; w++) {
@@ -2557,8 +2546,7 @@ static int calibrate_band(Plan* g) {
     if (set_integer_scale(Q, 0)) return FS_EINVAL;
   }
   const int w = Q.q16 ? 0 : 1;
-  const double band = (3.0 * mx[w] + 0.5 * rms[w]) / Q.SC;
-  Q.amb_delta = std::max(Q.amb_delta_model, band);
+  Q.amb_delta = calibrated_delta(Q.amb_delta_model, Q.SC, rms[w], mx[w]);
   g->calib[0] = Q.q16;
   g->calib[1] = rms[w];
   g->calib[2] = mx[w];

@@ -20,6 +20,7 @@
 
 #include <cstdint>
 #include <string>
+#include <utility>
 #include <vector>
 
 #if defined(__HIPCC__)
@@ -113,6 +114,14 @@ int finalize_scale(Prepared& P, const double* cmin, const double* cmax);
 // Integer scale, qmax and the model band for 16-bit (q16 = 1) or 32-bit
 // operands, from the ranges finalize_scale measured (P.Rmax).
 int set_integer_scale(Prepared& P, int q16);
+// Refinement-band calibration (fs_gpu.hip calibrate_band, and the CPU
+// backend's): `count` pairs i < j from a fixed generator over [0, n) (the
+// same on every rank and backend), and the band from their measured errors:
+// max(model, (3 max|err| + rms / 2) / SC) in real distance units.
+constexpr int64_t kCalibPairs = 4096;
+void calib_pairs(int64_t n, int64_t pc, int64_t count,
+                 std::vector<std::pair<int64_t, int64_t>>& out);
+double calibrated_delta(double model, double SC, double rms, double max_abs);
 int encode_labels_f64(Prepared& P, const double* y);
 int encode_labels_i32(Prepared& P, const int32_t* y);
 

@@ -236,6 +236,28 @@ int set_integer_scale(Prepared& P, int q16) {
   return 0;
 }
 
+void calib_pairs(int64_t n, int64_t pc, int64_t count, std::vector<std::pair<int64_t, int64_t>>& out) {
+  out.clear();
+  if (n < 2) return;
+  uint64_t st = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n << 20) ^ (uint64_t)pc;
+  auto next = [&]() {  // splitmix64
+    uint64_t z = (st += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  for (int64_t k = 0; k < count; k++) {
+    const int64_t i = (int64_t)(next() % (uint64_t)n);
+    int64_t j = (int64_t)(next() % (uint64_t)(n - 1));
+    if (j >= i) j++;
+    out.emplace_back(std::min(i, j), std::max(i, j));
+  }
+}
+
+double calibrated_delta(double model, double SC, double rms, double max_abs) {
+  return std::max(model, (3.0 * max_abs + 0.5 * rms) / SC);
+}
+
 namespace cpu {
 
 // Host column statistics (the CPU backend of fs_column_stats).  Threads own

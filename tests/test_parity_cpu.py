@@ -231,3 +231,16 @@ def test_gloo_world2_with_two_tile_shards_each(tmp_path):
     X, y = make_classification(n_samples=500, n_features=40, random_state=2)
     ref = MultiSURF(backend="cpu").fit(X, y).feature_importances_
     assert scale_rel_err(a, ref) < 1e-6
+
+
+def test_cpu_backend_duplicated_columns(oracle):
+    """Coherent column rounding (4 base columns x 1000 copies) on the CPU
+    backend, whose refinement band is calibrated on sampled pairs as the
+    GPU's is (fs_cpu.cpp calibrated_band)."""
+    rng = np.random.default_rng(31)
+    base = rng.standard_normal((800, 4)).astype(np.float32)
+    X = np.repeat(base, 1000, axis=1)
+    y = (base[:, 0] - base[:, 2] > 0).astype(int)
+    for star in (False, True):
+        s = MultiSURF(backend="cpu", use_star=star).fit(X, y).feature_importances_
+        assert scale_rel_err(s, oracle.multisurf_scores(X, y, use_star=star)) < 1e-5
