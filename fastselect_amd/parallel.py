@@ -92,7 +92,17 @@ def resident_x(x, backend="gpu", device=0, gather=None):
         with _lib.staged_x(backend, x, device):
             yield
         return
-    buf = gather_rows(x, device, force=True)
+    try:
+        buf = gather_rows(x, device, force=True)
+    except RuntimeError as e:
+        # the all-gather only saves host-to-device copies: without it every
+        # rank uploads X itself (same result), and says so
+        import sys
+        print(f"fastselect_amd: RCCL all-gather of X failed ({e}); uploading X per rank",
+              file=sys.stderr, flush=True)
+        with _lib.staged_x(backend, x, device):
+            yield
+        return
     try:
         with _lib.staged_device_x(x, buf.data_ptr(), device):
             yield

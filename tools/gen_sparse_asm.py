@@ -64,7 +64,7 @@ SETS = [40, 56, 72]
 
 
 def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, spread=True, low=False,
-        pk=False, lead=2, prio=0):
+        pk=False, lead=2, prio=0, warm=0):
     """Macro text.  feats: features per lane (4: 128 KB LDS block, float4 rows;
     2: 64 KB, float2 rows, 64-VGPR budget).  no_ds / same_stream:
     microbenchmark variants that skip the LDS reads / keep re-reading the
@@ -119,6 +119,13 @@ def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, sp
         if same_stream:  # two groups re-read (scalar-cache hits); s89 bounds the loop
             L += ["s_and_b32 s34, s34, 0x40", "s_add_u32 s89, s89, 1"]
         L.append(f"s_load_dwordx16 s[{SETS[nn]}:{SETS[nn] + 15}], s[36:37], s34")
+        if warm:
+            # L2 warm-up of the group `warm` groups beyond the one just
+            # requested: a vector load (vmcnt, not lgkmcnt) whose value is
+            # discarded, so the scalar load of that group ~warm steps later
+            # finds its line in L2 instead of HBM
+            L += ["s_add_u32 s92, s36, s34", "s_addc_u32 s93, s37, 0",
+                  f"global_load_dword v47, v46, s[92:93] offset:{64 * warm}"]
         if not spread:
             L += compute(c, ac)
         else:
@@ -161,6 +168,8 @@ def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, sp
                 f"s_branch {20 + x}b"]
 
     lines = [
+        *(["v_mov_b32 v46, 0"] if warm else []),  # the warm loads' zero offset (own register:
+        # an input operand holding 0 may share the register of an accumulator)
         "s_mov_b32 s88, 0",
         "s_mov_b64 s[90:91], %[bp]",
         *bload(BCUR),
@@ -208,21 +217,23 @@ def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, sp
             return f"s[{remap[lo]}:{remap[int(hi)]}]" if hi else f"s{remap[lo]}"
         lines = [re.sub(r"(?<![a-z_])s\[?(\d+)(?::(\d+)\])?", sub, l) for l in lines]
     body = "\n".join(f'      "{l}\\n"  \\' for l in lines)
-    vclob = ", ".join(f'"v{i}"' for i in range(VLO, ASETS[1] + 8 * F))
+    vlo = VLO - 2 if warm else VLO
+    vclob = ", ".join(f'"v{i}"' for i in range(vlo, ASETS[1] + 8 * F))
     nacc = 2 * F
     # low: clobber only the SGPRs the loop names (the compiler has few left)
     named = set()
     for l in lines:
         for lo, hi in re.findall(r"(?<![a-z_])s\[?(\d+)(?::(\d+)\])?", l):
             named.update(range(int(lo), int(hi or lo) + 1))
-    sregs = sorted(named & set(remap.values())) if low else range(34, 92)
+    sregs = sorted(named & set(remap.values())) if low else range(34, 94 if warm else 92)
     sclob = ", ".join(f'"s{i}"' for i in sregs)
+    vz = ""
     return f'''#define {name}(acc, lane16, lane4, eb, bp, bstride, ncols)  \\
   asm volatile(  \\
 {body}
       : {", ".join(f'[acc{i}] "+v"(acc[{i}])' for i in range(nacc))}  \\
       : [lane16] "v"(lane16), [lane4] "v"(lane4), [eb] "s"(eb), [bp] "s"(bp),  \\
-        [bstride] "s"(bstride), [ncols] "s"(ncols)  \\
+        [bstride] "s"(bstride), [ncols] "s"(ncols){vz}  \\
       : {vclob},  \\
         {sclob}, "scc", "memory")
 '''
@@ -237,6 +248,15 @@ if __name__ == "__main__":
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "fastselect_amd", "csrc",
                         "fs_sparse_asm.inc")
     text = HEADER + gen()
+    # A/B build only (FS_GEN_WARM=<groups>): FS_SPARSE_STREAM_ASM_WARM, an L2
+    # warm-up vector load per group `warm` groups ahead of the scalar load.
+    # Measured at cfg4 (tools/warm_ab.sh, profiles/r02/warm_ab.txt, with a
+    # runtime switch in k_score_sparse): 102.9-103.1 ms against 102.0 without
+    # -- the entry groups already come from L2 (the XCD-aware grid shares a
+    # segment's streams among the workgroups running at once), so the scalar
+    # loads' wait is L2 latency, which this cannot shorten.  Not shipped.
+    if os.environ.get("FS_GEN_WARM"):
+        text += "\n" + gen(name="FS_SPARSE_STREAM_ASM_WARM", warm=int(os.environ["FS_GEN_WARM"]))
     if os.environ.get("FS_GEN_LEAD_VARIANTS"):  # A/B build: FS_SPARSE_STREAM_ASM_L<n>
         for pr in (1, 3):
             text += "\n" + gen(name=f"FS_SPARSE_STREAM_ASM_P{pr}", prio=pr)
