@@ -1419,7 +1419,7 @@ __device__ __forceinline__ void sparse_stream_generic(const float4* __restrict__
 __global__ __launch_bounds__(1024) void k_score_sparse(
     const float* __restrict__ xs, int64_t PW, int64_t PC, const int2* __restrict__ tiles,
     const uint2* __restrict__ ent, int64_t n_tiles, int64_t seg_len, int64_t nseg, int64_t nfb,
-    double* __restrict__ spart) {
+    int jit, double* __restrict__ spart) {
   __shared__ float4 As[kTile * 64];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1462,7 +1462,10 @@ __global__ __launch_bounds__(1024) void k_score_sparse(
     const float* __restrict__ xb = xs + ((int64_t)tl.y * kTile + wave) * PW + f0;
     if (fast) {
       const uint64_t eb = (uint64_t)(uintptr_t)e, bp = (uint64_t)(uintptr_t)xb;
-      FS_SPARSE_STREAM_ASM(acc, lane16, lane4, eb, bp, bstride, ncols);
+      if (jit)
+        FS_SPARSE_STREAM_ASM_JIT(acc, lane16, lane4, eb, bp, bstride, ncols);
+      else
+        FS_SPARSE_STREAM_ASM(acc, lane16, lane4, eb, bp, bstride, ncols);
     } else {
       sparse_stream_generic(As, e, xb + lane, PW, lane, disc, acc);
     }
@@ -2979,6 +2982,21 @@ static int run_weights(Plan* g, const double* counts, int algo, double inv_sc) {
   return launch_check("k_weights");
 }
 
+// Sparse pass-2 loop variant (fs_sparse_asm.inc): 1 (default) = 16-entry
+// steps with rows read just in time 12 entries ahead (FS_SPARSE_STREAM_ASM_JIT:
+// twice the scalar-load cover), 0 = the round-1 loop of 8-entry groups with
+// the next group's rows double-buffered.  Same box, alternating, cfg4
+// (tools/jit_ab.sh, profiles/r02/jit_ab.txt): 102.2-102.4 vs 103.0-103.2 ms.
+// FS_SPARSE_JIT=0/1 overrides.
+static int sparse_jit() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("FS_SPARSE_JIT");
+    v = (e && *e) ? (std::atoi(e) != 0) : 1;
+  }
+  return v;
+}
+
 static int run_pass2(Plan* g, double* scores_dev) {
   const Prepared& Q = g->P;
   const int64_t nfb = (Q.PW + 127) / 128;
@@ -2989,7 +3007,8 @@ static int run_pass2(Plan* g, double* scores_dev) {
   if (g->sparse) {
     const int64_t nfb4 = (Q.PW + 255) / 256;
     k_score_sparse<<<(unsigned)(kXcds * seg_per_xcd * nfb4), 64 * kSWaves, 0, g->stream>>>(
-        g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->n_tiles, g->seg_len, g->nseg, nfb4, g->spart);
+        g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->n_tiles, g->seg_len, g->nseg, nfb4, sparse_jit(),
+        g->spart);
     FS_TRY(launch_check("k_score_sparse"));
   } else {
     k_score<<<(unsigned)(kXcds * seg_per_xcd * nfb), 256, 0, g->stream>>>(

@@ -244,26 +244,6 @@ HEADER = """// Generated by tools/gen_sparse_asm.py -- do not edit by hand.
 // generator's docstring for the layout, the pipeline and the fixed registers).
 """
 
-if __name__ == "__main__":
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "fastselect_amd", "csrc",
-                        "fs_sparse_asm.inc")
-    text = HEADER + gen()
-    # A/B build only (FS_GEN_WARM=<groups>): FS_SPARSE_STREAM_ASM_WARM, an L2
-    # warm-up vector load per group `warm` groups ahead of the scalar load.
-    # Measured at cfg4 (tools/warm_ab.sh, profiles/r02/warm_ab.txt, with a
-    # runtime switch in k_score_sparse): 102.9-103.1 ms against 102.0 without
-    # -- the entry groups already come from L2 (the XCD-aware grid shares a
-    # segment's streams among the workgroups running at once), so the scalar
-    # loads' wait is L2 latency, which this cannot shorten.  Not shipped.
-    if os.environ.get("FS_GEN_WARM"):
-        text += "\n" + gen(name="FS_SPARSE_STREAM_ASM_WARM", warm=int(os.environ["FS_GEN_WARM"]))
-    if os.environ.get("FS_GEN_LEAD_VARIANTS"):  # A/B build: FS_SPARSE_STREAM_ASM_L<n>
-        for pr in (1, 3):
-            text += "\n" + gen(name=f"FS_SPARSE_STREAM_ASM_P{pr}", prio=pr)
-    open(path, "w").write(text)
-    print("wrote", os.path.normpath(path))
-
-
 # ---------------------------------------------------------------------------
 # v2 stream: entries through vector memory + DPP broadcast (no scalar loads)
 # ---------------------------------------------------------------------------
@@ -694,3 +674,157 @@ def gen_ring(name="FS_SPARSE_RING_ASM", spread=False):
       : {vclob},  \\
         {sclob}, "scc", "memory")
 '''
+
+
+# ---------------------------------------------------------------------------
+# v4: 16-entry steps, rows read just in time with counted lgkmcnt
+# ---------------------------------------------------------------------------
+JIT_DOC = """
+Rows read just in time.  A step is 16 entries (two 8-entry groups, two
+s_load_dwordx16) and starts with the only s_waitcnt lgkmcnt(0): the entries of
+this step (loaded one step earlier) landed, and no LDS read is in flight.
+It then requests the next step's 32 entry dwords into the other SGPR set --
+one whole 16-entry step of cover for the scalar loads, twice the 8-entry
+loop's -- and walks its 16 entries with each row read issued L entries ahead
+into a ring of L + 1 four-VGPR slots, waited with a counted lgkmcnt(M), M =
+the reads issued after it.  Counted waits stay correct with the two scalar
+loads outstanding: if read e were pending, reads e..e+M would be too (LDS
+completes in order), so the count could not be <= M; the scalar loads only
+make a wait stricter (effective lead L - 2 while they are in flight).  The
+differences are formed in place (v_sub_f32 into the slot).  A column ending
+in the step's first group switches B between its two groups.
+Registers: v56..v59 B, v60..v63 next B, v64.. the ring; entry sets s36..s67
+and s68..s99; s24 stream offset (next step), s25 temporary, s[26:27] stream
+base, s22 column counter, s23 temporary, s[20:21] B row pointer.
+"""
+
+
+def gen_jit(name="FS_SPARSE_STREAM_ASM", lead=6):
+    L = lead
+    SET = [36, 68]
+    BCUR, BNXT, RING = 56, 60, 64
+    OFF, TMP, BASE, COLS, TMP2, BPTR = 24, 25, 26, 22, 23, 20
+
+    def slot(e):
+        return RING + 4 * (e % (L + 1))
+
+    def entry_sgprs(k, e):
+        g, q = divmod(e, 8)
+        base = SET[k] + 16 * g + 2 * q
+        return base, base + 1     # roff, weight
+
+    def read(k, e):
+        r, _ = entry_sgprs(k, e)
+        a = slot(e)
+        return [f"v_add_u32 v{a}, s{r}, %[lane16]", f"ds_read_b128 v[{a}:{a + 3}], v{a}"]
+
+    def compute(k, e):
+        _, w = entry_sgprs(k, e)
+        a = slot(e)
+        L_ = [f"v_sub_f32 v{a + f}, v{a + f}, v{BCUR + f}" for f in range(4)]
+        for f in range(4):
+            acc = f"%[acc{2 * f + (e & 1)}]"
+            L_.append(f"v_fma_f32 {acc}, s{w}, |v{a + f}|, {acc}")
+        return L_
+
+    def bload(dst):
+        return [f"global_load_dword v{dst + f}, %[lane4], s[{BPTR}:{BPTR + 1}]" + (f" offset:{256 * f}" if f else "")
+                for f in range(4)]
+
+    def switch(lab, ret):
+        return [f"{lab}:",
+                f"s_add_u32 s{COLS}, s{COLS}, 1",
+                f"s_cmp_ge_u32 s{COLS}, %[ncols]",
+                "s_cbranch_scc1 8f",
+                "s_waitcnt vmcnt(0)",
+                *[f"v_mov_b32 v{BCUR + f}, v{BNXT + f}" for f in range(4)],
+                f"s_add_u32 s{TMP2}, s{COLS}, 1",
+                f"s_cmp_ge_u32 s{TMP2}, %[ncols]",
+                f"s_cbranch_scc1 {ret}b",
+                f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
+                f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0",
+                *bload(BNXT),
+                f"s_branch {ret}b"]
+
+    out_of_line = []
+
+    def step(x):
+        k, o = x % 2, 1 - x % 2
+        S = ["s_waitcnt lgkmcnt(0)",
+             f"s_load_dwordx16 s[{SET[o]}:{SET[o] + 15}], s[{BASE}:{BASE + 1}], s{OFF}",
+             f"s_add_u32 s{TMP}, s{OFF}, 64",
+             f"s_load_dwordx16 s[{SET[o] + 16}:{SET[o] + 31}], s[{BASE}:{BASE + 1}], s{TMP}",
+             f"s_add_u32 s{OFF}, s{OFF}, 128"]
+        for e in range(min(L, 16)):
+            S += read(k, e)
+        issued = min(L, 16)
+        for e in range(16):
+            if e == 8:  # group A's column ended: next column's B before group B
+                S += [f"s_bitcmp1_b32 s{SET[k] + 1}, 0", f"s_cbranch_scc1 {10 + 2 * x}f", f"{40 + 2 * x}:"]
+                out_of_line.extend(switch(10 + 2 * x, 40 + 2 * x))
+            if e + L < 16:
+                S += read(k, e + L)
+                issued = e + L + 1
+            after = issued - (e + 1)          # reads issued after entry e's
+            S.append(f"s_waitcnt lgkmcnt({min(after, 15)})")
+            S += compute(k, e)
+        S += [f"s_bitcmp1_b32 s{SET[k] + 17}, 0", f"s_cbranch_scc1 {11 + 2 * x}f", f"{41 + 2 * x}:"]
+        out_of_line.extend(switch(11 + 2 * x, 41 + 2 * x))
+        return S
+
+    lines = [f"s_mov_b32 s{COLS}, 0",
+             f"s_mov_b64 s[{BPTR}:{BPTR + 1}], %[bp]",
+             *bload(BCUR),
+             f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
+             f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0",
+             *bload(BNXT),
+             f"s_mov_b64 s[{BASE}:{BASE + 1}], %[eb]",
+             f"s_load_dwordx16 s[{SET[0]}:{SET[0] + 15}], s[{BASE}:{BASE + 1}], 0x0",
+             f"s_load_dwordx16 s[{SET[0] + 16}:{SET[0] + 31}], s[{BASE}:{BASE + 1}], 0x40",
+             f"s_mov_b32 s{OFF}, 128",
+             "s_waitcnt vmcnt(4)",
+             "7:"]
+    for x in range(2):
+        lines += step(x)
+    # safety bound: a stream holds at most 8 columns x 16 groups (8 KB)
+    lines += [f"s_cmp_gt_u32 s{OFF}, 0x2100", "s_cbranch_scc0 7b", "s_branch 8f"]
+    lines += out_of_line
+    lines += ["8:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    body = "\n".join(f'      "{l}\\n"  \\' for l in lines)
+    vclob = ", ".join(f'"v{i}"' for i in range(BCUR, RING + 4 * (L + 1)))
+    named = set()
+    for l in lines:
+        for lo, hi in re.findall(r"(?<![a-z_])s\[?(\d+)(?::(\d+)\])?", l):
+            named.update(range(int(lo), int(hi or lo) + 1))
+    sclob = ", ".join(f'"s{i}"' for i in sorted(named))
+    return f'''#define {name}(acc, lane16, lane4, eb, bp, bstride, ncols)  \\
+  asm volatile(  \\
+{body}
+      : {", ".join(f'[acc{i}] "+v"(acc[{i}])' for i in range(8))}  \\
+      : [lane16] "v"(lane16), [lane4] "v"(lane4), [eb] "s"(eb), [bp] "s"(bp),  \\
+        [bstride] "s"(bstride), [ncols] "s"(ncols)  \\
+      : {vclob},  \\
+        {sclob}, "scc", "memory")
+'''
+
+
+if __name__ == "__main__":
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "fastselect_amd", "csrc",
+                        "fs_sparse_asm.inc")
+    text = HEADER + gen()
+    text += "\n" + gen_jit(name="FS_SPARSE_STREAM_ASM_JIT",   # A/B: FS_SPARSE_JIT=1
+                            lead=int(os.environ.get("FS_GEN_JIT_LEAD", "12")))
+    # A/B build only (FS_GEN_WARM=<groups>): FS_SPARSE_STREAM_ASM_WARM, an L2
+    # warm-up vector load per group `warm` groups ahead of the scalar load.
+    # Measured at cfg4 (tools/warm_ab.sh, profiles/r02/warm_ab.txt, with a
+    # runtime switch in k_score_sparse): 102.9-103.1 ms against 102.0 without
+    # -- the entry groups already come from L2 (the XCD-aware grid shares a
+    # segment's streams among the workgroups running at once), so the scalar
+    # loads' wait is L2 latency, which this cannot shorten.  Not shipped.
+    if os.environ.get("FS_GEN_WARM"):
+        text += "\n" + gen(name="FS_SPARSE_STREAM_ASM_WARM", warm=int(os.environ["FS_GEN_WARM"]))
+    if os.environ.get("FS_GEN_LEAD_VARIANTS"):  # A/B build: FS_SPARSE_STREAM_ASM_L<n>
+        for pr in (1, 3):
+            text += "\n" + gen(name=f"FS_SPARSE_STREAM_ASM_P{pr}", prio=pr)
+    open(path, "w").write(text)
+    print("wrote", os.path.normpath(path))
