@@ -699,10 +699,15 @@ base, s22 column counter, s23 temporary, s[20:21] B row pointer.
 """
 
 
-def gen_jit(name="FS_SPARSE_STREAM_ASM", lead=6):
+def gen_jit(name="FS_SPARSE_STREAM_ASM", lead=6, bank_shift=False):
     L = lead
     SET = [36, 68]
-    BCUR, BNXT, RING = 56, 60, 64
+    # bank_shift (A/B only): B in v57..v60 so that v_sub_f32's two VGPR
+    # operands (slot + f, B + f) sit in different VGPR banks (v mod 4).
+    # Measured against the round-1 loop on one box (profiles/r02/
+    # jit_bankshift_ab.txt): 103.35-103.4 vs 103.5-103.56 ms -- no better
+    # than the unshifted JIT loop (102.2-102.4 vs 103.0-103.2); not shipped.
+    BCUR, BNXT, RING = (57, 61, 68) if bank_shift else (56, 60, 64)
     OFF, TMP, BASE, COLS, TMP2, BPTR = 24, 25, 26, 22, 23, 20
 
     def slot(e):
@@ -813,7 +818,8 @@ if __name__ == "__main__":
                         "fs_sparse_asm.inc")
     text = HEADER + gen()
     text += "\n" + gen_jit(name="FS_SPARSE_STREAM_ASM_JIT",   # A/B: FS_SPARSE_JIT=1
-                            lead=int(os.environ.get("FS_GEN_JIT_LEAD", "12")))
+                            lead=int(os.environ.get("FS_GEN_JIT_LEAD", "12")),
+                            bank_shift=bool(int(os.environ.get("FS_GEN_BANK_SHIFT", "0"))))
     # A/B build only (FS_GEN_WARM=<groups>): FS_SPARSE_STREAM_ASM_WARM, an L2
     # warm-up vector load per group `warm` groups ahead of the scalar load.
     # Measured at cfg4 (tools/warm_ab.sh, profiles/r02/warm_ab.txt, with a
