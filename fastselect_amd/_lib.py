@@ -37,7 +37,8 @@ _vp = ctypes.c_void_p
 # every symbol include/fastselect_amd.h declares (checked by tests/test_abi.py)
 EXPORTED = (
     "fs_version", "fs_last_error", "fs_device_count", "fs_device_cache_release",
-    "fs_stage_x", "fs_stage_x_device", "fs_unstage_x", "fs_all_finite",
+    "fs_stage_x", "fs_stage_x_device", "fs_unstage_x", "fs_all_finite", "fs_host_alloc",
+    "fs_host_free",
     "fs_column_stats", "fs_multisurf_score", "fs_multisurf_score_rows",
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
@@ -76,6 +77,10 @@ def _load() -> ctypes.CDLL:
     lib.fs_device_cache_release.restype = _int
     lib.fs_stage_x.argtypes = [_int, _vp, _int, _i64, _i64, ctypes.POINTER(ctypes.c_uint64)]
     lib.fs_stage_x.restype = _int
+    lib.fs_host_alloc.argtypes = [ctypes.c_uint64, ctypes.POINTER(_vp)]
+    lib.fs_host_alloc.restype = _int
+    lib.fs_host_free.argtypes = [_vp]
+    lib.fs_host_free.restype = _int
     lib.fs_stage_x_device.argtypes = [_int, _vp, _vp, _int, _i64, _i64,
                                       ctypes.POINTER(ctypes.c_uint64)]
     lib.fs_stage_x_device.restype = _int
@@ -161,6 +166,25 @@ def staged_x(backend, x, device=0):
         yield
     finally:
         _lib.fs_unstage_x(h)
+
+
+def pinned_empty(shape, dtype):
+    """An uninitialised C-contiguous array in pinned host memory from the
+    library's block cache (fs_host_alloc), returned to the cache when the
+    array is collected; None when no GPU is visible or pinning fails."""
+    import weakref
+    dtype = np.dtype(dtype)
+    nbytes = int(np.prod(shape)) * dtype.itemsize
+    if nbytes == 0 or not gpu_available():
+        return None
+    p = _vp()
+    if _lib.fs_host_alloc(ctypes.c_uint64(nbytes), ctypes.byref(p)) != 0 or not p.value:
+        return None
+    buf = (ctypes.c_char * nbytes).from_address(p.value)
+    arr = np.frombuffer(buf, dtype=dtype).reshape(shape)
+    fin = weakref.finalize(buf, _lib.fs_host_free, _vp(p.value))
+    fin.atexit = False  # at exit the block goes with the process (no HIP call then)
+    return arr
 
 
 def multisurf_shards(n: int, p: int, world: int = 1, device: int = 0) -> int:

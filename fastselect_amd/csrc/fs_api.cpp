@@ -69,6 +69,24 @@ int fs_device_cache_release(void) {
   return FS_OK;
 }
 
+int fs_host_alloc(uint64_t bytes, void** out) {
+  if (!out) {
+    set_error("fs_host_alloc: out is NULL");
+    return FS_EINVAL;
+  }
+  *out = nullptr;
+  if (gpu::device_count() <= 0) {
+    set_error("backend='gpu' requested but no HIP device is visible");
+    return FS_ENODEV;
+  }
+  return gpu::host_alloc(out, (size_t)bytes);
+}
+
+int fs_host_free(void* p) {
+  gpu::host_free(p);
+  return FS_OK;
+}
+
 int fs_stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p, uint64_t* staged) {
   if (!x || !staged || n < 1 || p < 1) {
     set_error("fs_stage_x: need x, staged, n >= 1 and p >= 1");

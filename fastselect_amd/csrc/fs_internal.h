@@ -286,6 +286,9 @@ int device_count();
 int dev_alloc(void** p, size_t bytes, int device);
 void dev_free(void* p);
 void dev_cache_release();
+// Pinned host blocks (hipHostMalloc), cached between fits (fs_host_alloc).
+int host_alloc(void** p, size_t bytes);
+void host_free(void* p);
 // Staged X (fs_stage_x): one device copy of a host matrix that the column
 // statistics and the plan of the same fit read instead of uploading it again.
 // staged_lookup returns the device copy of (host, n, p, f64) on `device`, or

@@ -73,6 +73,12 @@ FS_API int fs_device_count(void);
  * disables), so that the next fit skips hipMalloc's page mapping (190-310 ms
  * for a cfg4 plan).  Returns FS_OK. */
 FS_API int fs_device_cache_release(void);
+/* Pinned host memory for the float32 copy of X a fit makes (GPU backend):
+ * the host threads cast into pinned, already-mapped pages and the upload of
+ * X is a DMA from them.  Blocks are cached between calls (two at most;
+ * fs_device_cache_release frees them).  FS_ENODEV without a GPU. */
+FS_API int fs_host_alloc(uint64_t bytes, void** out);
+FS_API int fs_host_free(void* p);
 /* Stage X for one fit: upload the n x p row-major matrix (float32, or
  * float64 when x_is_f64) to `device` once.  Until fs_unstage_x, the GPU
  * backend's fs_column_stats and scoring calls given the same host pointer,

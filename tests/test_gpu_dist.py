@@ -95,3 +95,16 @@ def test_column_stats_run_on_the_ranks_device():
     rng = (x.max(0) - x.min(0)).astype(np.float32)
     np.testing.assert_array_equal(recip, (1.0 / rng).astype(np.float32))
     assert not isd.any()
+
+
+def test_pinned_float32_cast_equals_numpy():
+    """_base.to_float32 with a GPU visible casts into pinned host memory
+    (fs_host_alloc); the values are numpy's cast, and blocks are reused."""
+    from fastselect_amd import _base
+    rng = np.random.default_rng(8)
+    x = rng.normal(size=(3000, 2000)) * 10.0 ** rng.integers(-20, 20, size=(3000, 2000))
+    for _ in range(3):
+        got = _base.to_float32(x)
+        assert got.flags.c_contiguous and got.dtype == np.float32
+        np.testing.assert_array_equal(got, x.astype(np.float32))
+        del got
