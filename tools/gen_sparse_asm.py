@@ -699,7 +699,7 @@ base, s22 column counter, s23 temporary, s[20:21] B row pointer.
 """
 
 
-def gen_jit(name="FS_SPARSE_STREAM_ASM", lead=6, bank_shift=False):
+def gen_jit(name="FS_SPARSE_STREAM_ASM", lead=6, bank_shift=False, half_lds=False):
     L = lead
     SET = [36, 68]
     # bank_shift (A/B only): B in v57..v60 so that v_sub_f32's two VGPR
@@ -721,6 +721,8 @@ def gen_jit(name="FS_SPARSE_STREAM_ASM", lead=6, bank_shift=False):
     def read(k, e):
         r, _ = entry_sgprs(k, e)
         a = slot(e)
+        if half_lds:  # diagnostic only (wrong scores): half the LDS bytes per entry
+            return [f"v_add_u32 v{a}, s{r}, %[lane16]", f"ds_read_b64 v[{a}:{a + 1}], v{a}"]
         return [f"v_add_u32 v{a}, s{r}, %[lane16]", f"ds_read_b128 v[{a}:{a + 3}], v{a}"]
 
     def compute(k, e):
@@ -827,6 +829,8 @@ if __name__ == "__main__":
     # -- the entry groups already come from L2 (the XCD-aware grid shares a
     # segment's streams among the workgroups running at once), so the scalar
     # loads' wait is L2 latency, which this cannot shorten.  Not shipped.
+    if os.environ.get("FS_GEN_HALF_LDS"):  # diagnostic A/B: FS_SPARSE_JIT=2 (wrong scores)
+        text += "\n" + gen_jit(name="FS_SPARSE_STREAM_ASM_HALF", lead=12, half_lds=True)
     if os.environ.get("FS_GEN_WARM"):
         text += "\n" + gen(name="FS_SPARSE_STREAM_ASM_WARM", warm=int(os.environ["FS_GEN_WARM"]))
     if os.environ.get("FS_GEN_LEAD_VARIANTS"):  # A/B build: FS_SPARSE_STREAM_ASM_L<n>
