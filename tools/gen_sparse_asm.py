@@ -699,7 +699,7 @@ base, s22 column counter, s23 temporary, s[20:21] B row pointer.
 """
 
 
-def gen_jit(name="FS_SPARSE_STREAM_ASM", lead=6, bank_shift=False, half_lds=False):
+def gen_jit(name="FS_SPARSE_STREAM_ASM", lead=6, bank_shift=False, half_lds=False, wait_every=1):
     L = lead
     SET = [36, 68]
     # bank_shift (A/B only): B in v57..v60 so that v_sub_f32's two VGPR
@@ -773,7 +773,10 @@ def gen_jit(name="FS_SPARSE_STREAM_ASM", lead=6, bank_shift=False, half_lds=Fals
                 S += read(k, e + L)
                 issued = e + L + 1
             after = issued - (e + 1)          # reads issued after entry e's
-            S.append(f"s_waitcnt lgkmcnt({min(after, 15)})")
+            if e % wait_every == 0:           # wait_every > 1: one wait covers the next entries too
+                last = min(e + wait_every - 1, 15)
+                after_last = issued - (last + 1)
+                S.append(f"s_waitcnt lgkmcnt({min(max(after_last, 0), 15)})")
             S += compute(k, e)
         S += [f"s_bitcmp1_b32 s{SET[k] + 17}, 0", f"s_cbranch_scc1 {11 + 2 * x}f", f"{41 + 2 * x}:"]
         out_of_line.extend(switch(11 + 2 * x, 41 + 2 * x))
@@ -829,6 +832,9 @@ if __name__ == "__main__":
     # -- the entry groups already come from L2 (the XCD-aware grid shares a
     # segment's streams among the workgroups running at once), so the scalar
     # loads' wait is L2 latency, which this cannot shorten.  Not shipped.
+    if os.environ.get("FS_GEN_WAIT_EVERY"):  # A/B: FS_SPARSE_JIT=2
+        text += "\n" + gen_jit(name="FS_SPARSE_STREAM_ASM_HALF", lead=12,
+                                wait_every=int(os.environ["FS_GEN_WAIT_EVERY"]))
     if os.environ.get("FS_GEN_HALF_LDS"):  # diagnostic A/B: FS_SPARSE_JIT=2 (wrong scores)
         text += "\n" + gen_jit(name="FS_SPARSE_STREAM_ASM_HALF", lead=12, half_lds=True)
     if os.environ.get("FS_GEN_WARM"):

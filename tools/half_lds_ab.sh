@@ -1,7 +1,7 @@
 #!/bin/bash
-# Diagnostic: k_score_sparse with half the LDS bytes per entry (ds_read_b64,
-# wrong scores) against the shipped loop, alternating -- is the loop bound by
-# the LDS traffic of the row reads?
+# A/B of two k_score_sparse loop builds: FS_SPARSE_JIT=1 (shipped) vs 2 (the
+# FS_SPARSE_STREAM_ASM_HALF macro of the current generator run: half-LDS
+# diagnostic or FS_GEN_WAIT_EVERY variant).
 set -uo pipefail
 OUT=gpurun_out/half_lds_ab.txt
 : > "$OUT"
