@@ -69,6 +69,9 @@ def gather_rows(x, device=None, force=False):
         mine[:hi - lo].copy_(torch.from_numpy(x[lo:hi]))
     if dev.type == "cuda":
         dist.all_gather_into_tensor(buf, mine)          # in place, RCCL over xGMI
+        # the library reads buf on its own streams (column statistics): the
+        # gather must have landed, not merely be ordered on torch's stream
+        torch.cuda.current_stream(dev).synchronize()
     else:
         parts = list(buf.split(rows))
         dist.all_gather(parts, mine.clone())
