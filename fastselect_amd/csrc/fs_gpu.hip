@@ -1437,7 +1437,11 @@ __global__ __launch_bounds__(1024) void k_score_sparse(
     real[c] = f0 + 64 * c < PW;
     disc[c] = f0 + 64 * c >= PC;
   }
-  const bool fast = f0 + 256 <= PC;  // four continuous chunks: the asm loop
+  // the asm loop when every real chunk is continuous: a last, partial block
+  // of an all-continuous layout (cfg4: 64 real features in block 78) stages
+  // zeros for the chunks past PW and discards their accumulators, whose B
+  // values (read past the row's end, inside xs's spare rows) are not used
+  const bool fast = (f0 + 256 < PW ? f0 + 256 : PW) <= PC;
   const uint32_t lane16 = (uint32_t)(uintptr_t)As + (uint32_t)lane * 16u;
   const uint32_t lane4 = (uint32_t)lane * 4u;
   const uint32_t bstride = (uint32_t)(kSWaves * PW * sizeof(float));
