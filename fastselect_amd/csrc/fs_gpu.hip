@@ -348,15 +348,17 @@ __device__ __forceinline__ void dist_chunk(const uint32_t* __restrict__ A,
   }
 }
 
-// K-split: with splits > 1 workgroup b computes tile b / splits over the
-// chunk range of part b % splits; part 0 writes D, part s the partial buffer
-// Dpart[s - 1] (k_dist_merge adds them).  A rank that owns few tiles (N-GPU
-// runs) thus fills the chip's 2 x CU workgroup slots in more even rounds.
+// K-split: workgroups b < n_full compute whole tiles; the tiles from n_full
+// on are split into `splits` parts of their chunk range, workgroup
+// n_full + q taking part q % splits of tile n_full + q / splits.  Part 0
+// writes D, part s > 0 the compact partial block
+// Dpart[(q / splits) * (splits - 1) + s - 1] (tile-local layout T[b][a]);
+// k_dist_merge adds them.  The plan splits all tiles or none (choose_ksplit).
 __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xqT, int64_t n_pad,
                                                  int nck_cont, int nck_disc, uint32_t sc_disc,
                                                  int q16,
-                                                 const int2* __restrict__ tiles, int splits,
-                                                 int tiled, int64_t plane,
+                                                 const int2* __restrict__ tiles, int64_t n_full,
+                                                 int splits, int tiled,
                                                  double* __restrict__ D,
                                                  double* __restrict__ Dpart) {
   // Two distinct LDS objects (not one indexed array) so the compiler can
@@ -367,12 +369,19 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int part = (int)(blockIdx.x % (unsigned)splits);
-  const int2 tl = tiles[blockIdx.x / (unsigned)splits];
+  const int64_t b_id = blockIdx.x;
+  const int64_t q = b_id - n_full;  // >= 0: a split tile's part
+  const int part = q < 0 ? 0 : (int)(q % splits);
+  const int nparts = q < 0 ? 1 : splits;
+  int64_t t = q < 0 ? b_id : n_full + q / splits;
+  const int2 tl = tiles[t];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
   const int tx = tid & 15, ty = tid >> 4;
-  const int64_t t = (int64_t)(blockIdx.x / (unsigned)splits);
-  if (part > 0) D = Dpart + (int64_t)(part - 1) * plane;
+  if (part > 0) {  // compact partial block, tile-local layout
+    D = Dpart;
+    t = (q / splits) * (splits - 1) + part - 1;
+    tiled = 1;
+  }
 
   uint32_t acc[8][8];
   uint32_t hi[8][4];
@@ -440,8 +449,8 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
   };
 
   const int nck_all = nck_cont + nck_disc;
-  const int c_begin = (int)((int64_t)nck_all * part / splits);
-  const int c_end = (int)((int64_t)nck_all * (part + 1) / splits);  // this part's chunks
+  const int c_begin = (int)((int64_t)nck_all * part / nparts);
+  const int c_end = (int)((int64_t)nck_all * (part + 1) / nparts);  // this part's chunks
   // continuous chunks (16-bit pairs or 32-bit values), then discrete ones
   if (q16)
     run(std::integral_constant<int, kModeU16>{}, c_begin, c_end < nck_cont ? c_end : nck_cont);
@@ -499,30 +508,39 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
 // 16-feature panel is 16 KB (one k-row = one 1 KB global_load_lds_dwordx4).
 // 512 lanes per tile: lane (tx, ty) = (tid % 32, tid / 32) owns rows
 // {ty*4 + r, 64 + ty*4 + r} x cols {tx*4 + c} (8 x 4 float64 accumulators).
-// D += sum of the K-split partials over the owned tiles, both halves
-// (integer-valued doubles: exact in any order).
+// D += the K-split partials of the split tiles n_full + blockIdx.x (compact
+// blocks, tile-local layout T[b][a]), both halves in the full layout
+// (integer-valued doubles: exact in any order).  Workgroup (x, y) adds the
+// 1024 elements [1024 y, 1024 y + 1024) of tile x, four per lane, so the
+// loads of all parts are in flight together.
+constexpr int kMergeSlices = kTile * kTile / 1024;
 __global__ __launch_bounds__(256) void k_dist_merge(double* __restrict__ D,
                                                    const double* __restrict__ Dpart, int nparts,
-                                                   const int2* __restrict__ tiles, int64_t n_pad,
-                                                   int tiled, int64_t plane) {
-  const int2 tl = tiles[blockIdx.x];
+                                                   const int2* __restrict__ tiles, int64_t n_full,
+                                                   int64_t n_pad, int tiled) {
+  const int64_t t = n_full + blockIdx.x;
+  const int2 tl = tiles[t];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
-  if (tiled) {
-    const int64_t base = (int64_t)blockIdx.x * kTile * kTile;
-    for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
-      double v = D[base + e];
-      for (int s = 0; s < nparts; s++) v += Dpart[s * plane + base + e];
-      D[base + e] = v;
-    }
-    return;
+  const double* __restrict__ part = Dpart + (int64_t)blockIdx.x * nparts * kTile * kTile;
+  int64_t at[4];
+  double v[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int e = blockIdx.y * 1024 + k * 256 + threadIdx.x;
+    at[k] = d_at(tiled, n_pad, t, i0, j0, e % kTile, e / kTile);  // (i0 + a, j0 + b)
+    v[k] = D[at[k]];
   }
-  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
-    const int64_t r = e / kTile, c = e % kTile;
-    const int64_t a = (i0 + r) * n_pad + j0 + c, b = (j0 + c) * n_pad + i0 + r;
-    double v = D[a];
-    for (int s = 0; s < nparts; s++) v += Dpart[s * plane + a];
-    D[a] = v;
-    if (tl.x != tl.y) D[b] = v;
+  for (int s = 0; s < nparts; s++) {
+    const double* __restrict__ ps = part + (int64_t)s * kTile * kTile + blockIdx.y * 1024 + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] += ps[k * 256];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int e = blockIdx.y * 1024 + k * 256 + threadIdx.x;
+    D[at[k]] = v[k];
+    // full layout: the other half too (a diagonal tile's `at` covers it)
+    if (!tiled && tl.x != tl.y) D[(i0 + e % kTile) * n_pad + j0 + e / kTile] = v[k];
   }
 }
 
@@ -2060,7 +2078,8 @@ struct Plan {
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t nb = 0, n_tiles = 0, seg_len = 1, nseg = 1;
-  int ksplit = 1;               // pass-1 K-split parts (k_dist)
+  int ksplit = 1;               // pass-1 K-split parts of the tail tiles (k_dist)
+  int64_t kfull = 0;            // tiles k_dist computes whole (the rest are split)
   int use_q16 = 0;              // pass 1 on packed 16-bit continuous operands
   double calib[6] = {0, 0, 0, 0, 1, 0};  // plan_calibration (calibrate_band)
   int64_t c_lo = 0, c_hi = 0;   // this rank's continuous columns of the mean correction
@@ -2436,12 +2455,13 @@ void plan_destroy(Plan* g) {
 }
 
 // Pass-1 K-split: k_dist holds `slots` workgroups on the chip at a time, so
-// T tiles take ceil(T / slots) rounds; splitting every tile's feature range into S parts
-// evens out the last round when a rank owns few tiles (N-GPU runs).  The
-// merge streams (S + 2) tile planes (~66.5 / p of the tile's compute time
-// each); S > 1 only when it gains at least 3%.
-static int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats,
-                         size_t plane_bytes) {
+// T tiles take ceil(T / slots) rounds; splitting every tile's feature range
+// into S parts evens out the last round when there are few tiles (cfg2: 820
+// tiles on 768 slots; one rank of an N-GPU job).  The merge streams (S + 2)
+// tile planes (~66.5 / p of the tile's compute time each); S > 1 only when
+// the model gains at least 3%.  (Splitting only the last round's tiles was
+// measured too: no better than S = 1 at cfg2, profiles/r02/ksplit_sweep.txt.)
+static int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
       cus <= 0) {
@@ -2464,7 +2484,8 @@ static int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats,
   // the S - 1 partial planes may take at most a quarter of the free memory
   size_t free_b = 0, total_b = 0;
   int max_sp = 8;
-  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && plane_bytes > 0)
+  const size_t plane_bytes = (size_t)std::max<int64_t>(tiles, 1) * kTile * kTile * sizeof(double);
+  if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
     max_sp = (int)std::min<size_t>(8, 1 + free_b / 4 / plane_bytes);
   else
     (void)hipGetLastError();
@@ -2750,11 +2771,11 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
   // pass-1 chunk count and the per-tile work in feature units of 32-bit SAD
   const int64_t rows_q = (g->use_q16 ? Q.PC / 2 : Q.PC) + Q.PD;
   g->ksplit = choose_ksplit(g->n_tiles, g->device, (int)(rows_q / kBKQ),
-                            (g->use_q16 ? Q.pc / 2 : Q.pc) + Q.pd,
-                            (size_t)g->dplane * sizeof(double));
-  if (const char* e = std::getenv("FS_KSPLIT"))  // A/B of the K-split choice
-    if (std::atoi(e) >= 1) g->ksplit = std::min(8, std::atoi(e));
+                            (g->use_q16 ? Q.pc / 2 : Q.pc) + Q.pd);
+  if (const char* e = std::getenv("FS_KSPLIT"))  // A/B and tests
+    if (std::atoi(e) >= 1) g->ksplit = std::min(16, std::atoi(e));
   if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
+  g->kfull = g->ksplit > 1 ? 0 : g->n_tiles;  // k_dist can split only a tail; all or none here
   g->alloc_target = 3;
   int rc = FS_OK;
   if ((rc = dalloc(g, &g->D, (size_t)g->dplane)) || (rc = dalloc(g, &g->tiles, g->n_tiles)) ||
@@ -2770,7 +2791,9 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
         hipMemsetAsync(g->ent, 0, sizeof(uint2) * count, g->stream) != hipSuccess)
       rc = FS_EHIP;
   }
-  if (!rc && g->ksplit > 1) rc = dalloc(g, &g->Dpart, (size_t)(g->ksplit - 1) * g->dplane);
+  if (!rc && g->ksplit > 1)
+    rc = dalloc(g, &g->Dpart,
+                (size_t)(g->n_tiles - g->kfull) * (g->ksplit - 1) * kTile * kTile);
   g->alloc_target = 0;
   if (rc) return rc;
   g->nnz_valid = false;
@@ -2940,7 +2963,9 @@ static int run_quantize_dist(Plan* g) {
     // with the row moments), on the side stream beside k_dist: it reads
     // xqT as k_dist does and writes only epsT / corr, which k_dist leaves
     // alone; plan_pass1 joins it before k_rowstats_reduce reads corr
-    // FS_SIDE=0: on the main stream, before k_dist (A/B of the overlap)
+    // FS_SIDE=0: on the main stream, before k_dist (A/B of the overlap:
+    // the side stream wins at cfg4 and, with the K-split, at cfg2 --
+    // profiles/r02/ksplit_sweep2.txt)
     const char* se = std::getenv("FS_SIDE");
     const hipStream_t cs = (se && *se == '0') ? g->stream : g->side;
     FS_HIP(hipEventRecord(g->ev_fork, g->stream));
@@ -2957,14 +2982,15 @@ static int run_quantize_dist(Plan* g) {
   }
   if (g->n_tiles > 0) {
     FS_HIP(hipEventRecord(g->ev[0], g->stream));
-    k_dist<<<(unsigned)(g->n_tiles * g->ksplit), 256, 0, g->stream>>>(
+    const int64_t n_split = g->ksplit > 1 ? g->n_tiles - g->kfull : 0;
+    const int64_t n_full = g->n_tiles - n_split;
+    k_dist<<<(unsigned)(n_full + n_split * g->ksplit), 256, 0, g->stream>>>(
         g->xqT, Q.n_pad, (int)((Q.q16 ? Q.PC / 2 : Q.PC) / kBKQ), (int)(Q.PD / kBKQ), Q.SCu,
-        Q.q16, g->tiles, g->ksplit, g->tiled, g->dplane, g->D, g->Dpart);
+        Q.q16, g->tiles, n_full, g->ksplit, g->tiled, g->D, g->Dpart);
     FS_TRY(launch_check("k_dist"));
-    if (g->ksplit > 1) {
-      k_dist_merge<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, g->Dpart, g->ksplit - 1,
-                                                                g->tiles, Q.n_pad, g->tiled,
-                                                                g->dplane);
+    if (n_split > 0) {
+      k_dist_merge<<<dim3((unsigned)n_split, kMergeSlices), 256, 0, g->stream>>>(
+          g->D, g->Dpart, g->ksplit - 1, g->tiles, n_full, Q.n_pad, g->tiled);
       FS_TRY(launch_check("k_dist_merge"));
     }
     FS_HIP(hipEventRecord(g->ev[1], g->stream));
