@@ -10,6 +10,8 @@ host callers.
 """
 from __future__ import annotations
 
+import contextlib
+
 import numpy as np
 from sklearn.base import BaseEstimator, TransformerMixin
 from sklearn.utils.validation import check_is_fitted, validate_data
@@ -60,14 +62,19 @@ class MultiSURF(TransformerMixin, BaseEstimator):
 
     def fit(self, x: np.ndarray, y: np.ndarray):
         """Score every feature with MultiSURF (or MultiSURF*)."""
-        x, y = _base.validate_xy(self, x, y, np.float32, self.n_jobs)
-        self.n_features_in_ = x.shape[1]
-        n_samples = x.shape[0]
-        n_select = self._validate_parameters(n_samples, self.n_features_in_)
-        self.effective_backend_ = _base.effective_backend(self.backend)
-        x = np.ascontiguousarray(x)
-        with _lib.staged_x(self.effective_backend_, x):  # one upload of X for the whole fit
-            scores = self._score(x, y)
+        # float64 X: cast, finiteness scan and upload in one native pass
+        x, y, staged = _base.validate_xy_staged(self, x, y, np.float32, self.n_jobs,
+                                                _base.stage_device(self.backend))
+        with _lib.unstaged(staged):
+            self.n_features_in_ = x.shape[1]
+            n_samples = x.shape[0]
+            n_select = self._validate_parameters(n_samples, self.n_features_in_)
+            self.effective_backend_ = _base.effective_backend(self.backend)
+            x = np.ascontiguousarray(x)
+            # one upload of X for the whole fit (already done when staged)
+            with contextlib.nullcontext() if staged else _lib.staged_x(
+                    self.effective_backend_, x):
+                scores = self._score(x, y)
         self.feature_importances_ = scores
         self.top_features_ = _base.top_features(scores, n_select)
         return self

@@ -62,6 +62,40 @@ def validate_xy(est, x, y, dtype, n_jobs=-1):
     return xv, yv
 
 
+def stage_device(backend: str, device: int = 0):
+    """The device a fit may stage X on while validating it (the estimators'
+    backend 'auto' or 'gpu' with a HIP device visible), else None.  Raises
+    nothing: backend errors keep their place after validation."""
+    return device if backend in ("auto", "gpu") and _lib.gpu_available() else None
+
+
+def validate_xy_staged(est, x, y, dtype, n_jobs=-1, device=None):
+    """``validate_xy`` that, for a C-contiguous float64 ndarray bound for
+    float32 and a ``device`` (stage_device), casts, scans and uploads X in one
+    native pass (fs_stage_x_cast: the upload of each row block overlaps the
+    casting of later ones).  Returns (x, y, handle): handle != 0 names the
+    device copy of x, to be released with ``_lib.unstaged(handle)``; 0 means
+    x was not staged (other inputs take validate_xy)."""
+    if (device is None or dtype != np.float32 or type(x) is not np.ndarray
+            or x.dtype != np.float64 or x.ndim != 2 or not x.flags.c_contiguous
+            or x.size < (1 << 20)):
+        xv, yv = validate_xy(est, x, y, dtype, n_jobs)
+        return xv, yv, 0
+    from sklearn.utils.validation import validate_data
+    x32, finite, h = _lib.stage_x_cast(x, n_jobs, device)
+    try:
+        xv, yv = validate_data(est, x32, y, y_numeric=True, dtype=dtype, ensure_2d=True,
+                               ensure_all_finite=False)
+        xv = np.ascontiguousarray(xv)
+        if not finite:  # scikit-learn's own error for the NaN / infinity
+            validate_data(est, x, y, y_numeric=True, dtype=dtype, ensure_2d=True)
+    except BaseException:
+        if h:
+            _lib.lib().fs_unstage_x(h)
+        raise
+    return xv, yv, h
+
+
 def to_float32(x: np.ndarray, n_jobs: int = -1) -> np.ndarray:
     """``np.ascontiguousarray(x, dtype=np.float32)`` (the reference's cast,
     round to nearest) with the conversion of large arrays split over threads

@@ -37,8 +37,8 @@ _vp = ctypes.c_void_p
 # every symbol include/fastselect_amd.h declares (checked by tests/test_abi.py)
 EXPORTED = (
     "fs_version", "fs_last_error", "fs_device_count", "fs_device_cache_release",
-    "fs_stage_x", "fs_stage_x_device", "fs_unstage_x", "fs_all_finite", "fs_host_alloc",
-    "fs_host_free",
+    "fs_stage_x", "fs_stage_x_device", "fs_stage_x_cast", "fs_unstage_x", "fs_all_finite",
+    "fs_host_alloc", "fs_host_free",
     "fs_column_stats", "fs_multisurf_score", "fs_multisurf_score_rows",
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
@@ -84,6 +84,9 @@ def _load() -> ctypes.CDLL:
     lib.fs_stage_x_device.argtypes = [_int, _vp, _vp, _int, _i64, _i64,
                                       ctypes.POINTER(ctypes.c_uint64)]
     lib.fs_stage_x_device.restype = _int
+    lib.fs_stage_x_cast.argtypes = [_int, _vp, _i64, _i64, _int, _vp, ctypes.POINTER(_int),
+                                    ctypes.POINTER(ctypes.c_uint64)]
+    lib.fs_stage_x_cast.restype = _int
     lib.fs_unstage_x.argtypes = [ctypes.c_uint64]
     lib.fs_unstage_x.restype = _int
     lib.fs_all_finite.argtypes = [_vp, _int, _i64, _i64, _int, ctypes.POINTER(_int)]
@@ -166,6 +169,32 @@ def staged_x(backend, x, device=0):
         yield
     finally:
         _lib.fs_unstage_x(h)
+
+
+def stage_x_cast(x, n_jobs=-1, device=0):
+    """``x`` (C-contiguous float64 matrix) cast to float32 by fs_stage_x_cast:
+    returns (x32, finite, handle) -- the cast array (pinned host memory when
+    possible), whether every value of it is finite, and the handle of its
+    device copy on ``device`` (0: not staged; release with ``unstaged``)."""
+    out = pinned_empty(x.shape, np.float32)
+    if out is None:
+        out = np.empty(x.shape, dtype=np.float32)
+    fin = _int(0)
+    h = ctypes.c_uint64(0)
+    check(_lib.fs_stage_x_cast(int(device), x.ctypes.data, x.shape[0], x.shape[1], int(n_jobs),
+                               out.ctypes.data, ctypes.byref(fin), ctypes.byref(h)))
+    return out, bool(fin.value), int(h.value)
+
+
+@contextlib.contextmanager
+def unstaged(handle):
+    """Release a device copy staged by stage_x_cast (handle 0: nothing) when
+    the block ends."""
+    try:
+        yield
+    finally:
+        if handle:
+            _lib.fs_unstage_x(ctypes.c_uint64(handle))
 
 
 def pinned_empty(shape, dtype):

@@ -24,7 +24,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -2369,6 +2371,98 @@ int stage_x_device(int device, const void* x, const void* x_dev, int x_is_f64, i
   staged.push_back(Staged{x, n, p, x_is_f64 ? 1 : 0, device, const_cast<void*>(x_dev),
                           std::this_thread::get_id(), true});
   *handle = (uint64_t)(uintptr_t)x_dev;
+  return FS_OK;
+}
+
+// The float64 -> float32 cast of X that validation makes, fused with its
+// finiteness scan and its upload: host threads cast row blocks (32 MB of
+// float32 each) into `out` while this thread copies every finished block to
+// the device (pinned `out`: a DMA beside the casting of later blocks).  The
+// device copy is registered under `out` as fs_stage_x would; without device
+// room for it (or with a non-finite value, which validation will reject) the
+// cast alone is done and *handle stays 0.  cfg4 (3.2 GB of float64): the cast
+// and the 1.6 GB upload overlap instead of following each other.
+int stage_x_cast(int device, const double* x, int64_t n, int64_t p, int n_jobs, float* out,
+                 int* finite, uint64_t* handle) {
+  *handle = 0;
+  *finite = 1;
+  if (device < 0 || device >= device_count()) {
+    set_error("fs_stage_x_cast: device ordinal out of range");
+    return FS_ENODEV;
+  }
+  FS_HIP(hipSetDevice(device));
+  const int64_t total = n * p;
+  void* d = nullptr;
+  hipStream_t st = nullptr;
+  if (dev_alloc(&d, (size_t)total * sizeof(float), device) != FS_OK ||
+      hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    if (d) dev_free(d);
+    d = nullptr;
+    st = nullptr;
+  }
+  const int64_t blk_rows = std::max<int64_t>(1, (int64_t(8) << 20) / p);
+  const int64_t nblk = (n + blk_rows - 1) / blk_rows;
+  std::vector<char> done((size_t)nblk, 0);
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<int64_t> next{0};
+  std::atomic<int> bad{0};
+  auto work = [&]() {
+    for (int64_t b = next++; b < nblk; b = next++) {
+      const int64_t lo = b * blk_rows * p, hi = std::min(n, (b + 1) * blk_rows) * p;
+      uint32_t any = 0;
+      for (int64_t i = lo; i < hi; i++) {
+        const float v = (float)x[i];  // round to nearest, as numpy's astype
+        out[i] = v;
+        uint32_t u;
+        std::memcpy(&u, &v, 4);
+        any |= (uint32_t)((u & 0x7f800000u) == 0x7f800000u);
+      }
+      if (any) bad.store(1, std::memory_order_relaxed);
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        done[(size_t)b] = 1;
+      }
+      cv.notify_all();
+    }
+  };
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(hardware_threads(n_jobs), nblk));
+  std::vector<std::thread> th;
+  th.reserve(nt);
+  for (int w = 0; w < nt; w++) th.emplace_back(work);
+  bool copy_ok = d != nullptr;
+  for (int64_t b = 0; b < nblk; b++) {
+    {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return done[(size_t)b] != 0; });
+    }
+    if (!copy_ok) continue;
+    const int64_t lo = b * blk_rows * p, hi = std::min(n, (b + 1) * blk_rows) * p;
+    if (hipMemcpyAsync((float*)d + lo, out + lo, (size_t)(hi - lo) * sizeof(float),
+                       hipMemcpyHostToDevice, st) != hipSuccess) {
+      (void)hipGetLastError();
+      copy_ok = false;
+    }
+  }
+  for (auto& t : th) t.join();
+  if (st) {
+    if (hipStreamSynchronize(st) != hipSuccess) {
+      (void)hipGetLastError();
+      copy_ok = false;
+    }
+    (void)hipStreamDestroy(st);
+  }
+  *finite = bad.load() ? 0 : 1;
+  if (d && (!copy_ok || !*finite)) {
+    dev_free(d);
+    d = nullptr;
+  }
+  if (d) {
+    std::lock_guard<std::mutex> lk(staged_mu);
+    staged.push_back(Staged{out, n, p, 0, device, d, std::this_thread::get_id(), false});
+    *handle = (uint64_t)(uintptr_t)d;
+  }
   return FS_OK;
 }
 
