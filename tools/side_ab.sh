@@ -1,14 +1,22 @@
 #!/bin/bash
-# Mean correction beside k_dist (side stream) or before it (FS_SIDE=0): cfg4 world 1 and 8, cfg5 MultiSURF*.
-set -euo pipefail
-mkdir -p gpurun_out
-for side in 1 0 1 0; do
-  for w in 1 8; do
-    FS_SIDE=$side timeout -k 10 120 python3 tools/shard_profile.py --world $w > gpurun_out/side.json 2> gpurun_out/side.err
-    echo "side=$side $(cut -c1-150 gpurun_out/side.json)"
-  done
+# Mean correction (k_colrank + k_rowcorr) beside k_dist or before it
+# (FS_SIDE), working tree against abtree/, cfg4 and cfg2, alternating.
+set -uo pipefail
+OUT=gpurun_out/side_ab.txt
+: > "$OUT"
+run() {
+  local label=$1 dir=$2 n=$3 steps=$4; shift 4
+  local line
+  line=$(cd "$dir" && env "$@" timeout -k 10 150 python3 bench.py --samples $n --features $n --steps $steps \
+           --warmup 3 --no-fit --no-cpu-baseline 2>/dev/null) || { echo "$label FAILED" >> "$OUT"; return 1; }
+  python3 -c "import json,sys; d=json.loads(sys.argv[2]); r=d['roofline']; print(sys.argv[1], round(d['ms_per_step'],3), {k: round(v,3) for k,v in r['kernel_ms'].items()})" "$label" "$line" >> "$OUT"
+}
+for rep in 1 2; do
+  run cfg4_new_side1 . 20000 5 FS_NOOP=1 && run cfg4_new_side0 . 20000 5 FS_SIDE=0 \
+    && run cfg4_old_side1 abtree 20000 5 FS_NOOP=1 || exit 1
 done
-for side in 1 0; do
-  FS_SIDE=$side timeout -k 10 200 python3 tools/bench_configs.py --only cfg5m > gpurun_out/side5.json 2> gpurun_out/side5.err
-  echo "side=$side cfg5m $(python3 -c "import json;d=json.loads(open('gpurun_out/side5.json').read().splitlines()[-1]);print(d['step_s']*1e3, d['k_dist_ms'], d['k_score_ms'])")"
+for rep in 1 2; do
+  run cfg2_new_side1 . 5000 20 FS_NOOP=1 && run cfg2_new_side0 . 5000 20 FS_SIDE=0 \
+    && run cfg2_old_side1 abtree 5000 20 FS_NOOP=1 || exit 1
 done
+cat "$OUT"
