@@ -70,14 +70,16 @@ def stage_device(backend: str, device: int = 0):
 
 
 def validate_xy_staged(est, x, y, dtype, n_jobs=-1, device=None):
-    """``validate_xy`` that, for a C-contiguous float64 ndarray bound for
-    float32 and a ``device`` (stage_device), casts, scans and uploads X in one
-    native pass (fs_stage_x_cast: the upload of each row block overlaps the
-    casting of later ones).  Returns (x, y, handle): handle != 0 names the
-    device copy of x, to be released with ``_lib.unstaged(handle)``; 0 means
-    x was not staged (other inputs take validate_xy)."""
+    """``validate_xy`` that, for a C-contiguous float64 or float32 ndarray
+    bound for float32 and a ``device`` (stage_device), casts (or copies into
+    pinned memory), scans and uploads X in one native pass (fs_stage_x_cast:
+    the upload of each row block overlaps the casting of later ones).
+    Returns (x, y, handle): handle != 0 names the device copy of x, to be
+    released with ``_lib.unstaged(handle)``; 0 means x was not staged (other
+    inputs take validate_xy)."""
     if (device is None or dtype != np.float32 or type(x) is not np.ndarray
-            or x.dtype != np.float64 or x.ndim != 2 or not x.flags.c_contiguous
+            or x.dtype not in (np.float64, np.float32) or x.ndim != 2
+            or not x.flags.c_contiguous
             or x.size < (1 << 20)):
         xv, yv = validate_xy(est, x, y, dtype, n_jobs)
         return xv, yv, 0

@@ -84,7 +84,7 @@ def _load() -> ctypes.CDLL:
     lib.fs_stage_x_device.argtypes = [_int, _vp, _vp, _int, _i64, _i64,
                                       ctypes.POINTER(ctypes.c_uint64)]
     lib.fs_stage_x_device.restype = _int
-    lib.fs_stage_x_cast.argtypes = [_int, _vp, _i64, _i64, _int, _vp, ctypes.POINTER(_int),
+    lib.fs_stage_x_cast.argtypes = [_int, _vp, _int, _i64, _i64, _int, _vp, ctypes.POINTER(_int),
                                     ctypes.POINTER(ctypes.c_uint64)]
     lib.fs_stage_x_cast.restype = _int
     lib.fs_unstage_x.argtypes = [ctypes.c_uint64]
@@ -172,17 +172,18 @@ def staged_x(backend, x, device=0):
 
 
 def stage_x_cast(x, n_jobs=-1, device=0):
-    """``x`` (C-contiguous float64 matrix) cast to float32 by fs_stage_x_cast:
-    returns (x32, finite, handle) -- the cast array (pinned host memory when
-    possible), whether every value of it is finite, and the handle of its
+    """``x`` (C-contiguous float64 or float32 matrix) cast / copied to
+    float32 by fs_stage_x_cast: returns (x32, finite, handle) -- the cast
+    array (pinned host memory when possible), whether every value of it is finite, and the handle of its
     device copy on ``device`` (0: not staged; release with ``unstaged``)."""
     out = pinned_empty(x.shape, np.float32)
     if out is None:
         out = np.empty(x.shape, dtype=np.float32)
     fin = _int(0)
     h = ctypes.c_uint64(0)
-    check(_lib.fs_stage_x_cast(int(device), x.ctypes.data, x.shape[0], x.shape[1], int(n_jobs),
-                               out.ctypes.data, ctypes.byref(fin), ctypes.byref(h)))
+    check(_lib.fs_stage_x_cast(int(device), x.ctypes.data, int(x.dtype == np.float64),
+                               x.shape[0], x.shape[1], int(n_jobs), out.ctypes.data,
+                               ctypes.byref(fin), ctypes.byref(h)))
     return out, bool(fin.value), int(h.value)
 
 

@@ -112,8 +112,8 @@ int fs_stage_x_device(int device, const void* x, const void* x_device, int x_is_
   return gpu::stage_x_device(device, x, x_device, x_is_f64, n, p, staged);
 }
 
-int fs_stage_x_cast(int device, const double* x, int64_t n, int64_t p, int n_jobs, float* out,
-                    int* finite, uint64_t* staged) {
+int fs_stage_x_cast(int device, const void* x, int x_is_f64, int64_t n, int64_t p, int n_jobs,
+                    float* out, int* finite, uint64_t* staged) {
   if (!x || !out || !finite || !staged || n < 1 || p < 1) {
     set_error("fs_stage_x_cast: need x, out, finite, staged, n >= 1 and p >= 1");
     return FS_EINVAL;
@@ -122,7 +122,7 @@ int fs_stage_x_cast(int device, const double* x, int64_t n, int64_t p, int n_job
     set_error("backend='gpu' requested but no HIP device is visible");
     return FS_ENODEV;
   }
-  return gpu::stage_x_cast(device, x, n, p, n_jobs, out, finite, staged);
+  return gpu::stage_x_cast(device, x, x_is_f64, n, p, n_jobs, out, finite, staged);
 }
 
 int fs_unstage_x(uint64_t staged) { return gpu::unstage_x(staged); }

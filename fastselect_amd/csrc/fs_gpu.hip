@@ -2374,16 +2374,17 @@ int stage_x_device(int device, const void* x, const void* x_dev, int x_is_f64, i
   return FS_OK;
 }
 
-// The float64 -> float32 cast of X that validation makes, fused with its
-// finiteness scan and its upload: host threads cast row blocks (32 MB of
-// float32 each) into `out` while this thread copies every finished block to
-// the device (pinned `out`: a DMA beside the casting of later blocks).  The
+// The float64 -> float32 cast of X that validation makes (or, for float32
+// X, a copy into pinned memory), fused with its finiteness scan and its
+// upload: host threads cast row blocks (32 MB of float32 each) into `out`
+// while this thread copies every finished block to the device (pinned
+// `out`: a DMA beside the casting of later blocks).  The
 // device copy is registered under `out` as fs_stage_x would; without device
 // room for it (or with a non-finite value, which validation will reject) the
 // cast alone is done and *handle stays 0.  cfg4 (3.2 GB of float64): the cast
 // and the 1.6 GB upload overlap instead of following each other.
-int stage_x_cast(int device, const double* x, int64_t n, int64_t p, int n_jobs, float* out,
-                 int* finite, uint64_t* handle) {
+int stage_x_cast(int device, const void* x, int x_is_f64, int64_t n, int64_t p, int n_jobs,
+                 float* out, int* finite, uint64_t* handle) {
   *handle = 0;
   *finite = 1;
   if (device < 0 || device >= device_count()) {
@@ -2412,12 +2413,23 @@ int stage_x_cast(int device, const double* x, int64_t n, int64_t p, int n_jobs, 
     for (int64_t b = next++; b < nblk; b = next++) {
       const int64_t lo = b * blk_rows * p, hi = std::min(n, (b + 1) * blk_rows) * p;
       uint32_t any = 0;
-      for (int64_t i = lo; i < hi; i++) {
-        const float v = (float)x[i];  // round to nearest, as numpy's astype
-        out[i] = v;
-        uint32_t u;
-        std::memcpy(&u, &v, 4);
-        any |= (uint32_t)((u & 0x7f800000u) == 0x7f800000u);
+      if (x_is_f64) {
+        const double* xd = (const double*)x;
+        for (int64_t i = lo; i < hi; i++) {
+          const float v = (float)xd[i];  // round to nearest, as numpy's astype
+          out[i] = v;
+          uint32_t u;
+          std::memcpy(&u, &v, 4);
+          any |= (uint32_t)((u & 0x7f800000u) == 0x7f800000u);
+        }
+      } else {
+        const uint32_t* xu = (const uint32_t*)x;
+        uint32_t* ou = (uint32_t*)out;
+        for (int64_t i = lo; i < hi; i++) {
+          const uint32_t u = xu[i];
+          ou[i] = u;
+          any |= (uint32_t)((u & 0x7f800000u) == 0x7f800000u);
+        }
       }
       if (any) bad.store(1, std::memory_order_relaxed);
       {

@@ -294,8 +294,8 @@ void host_free(void* p);
 // staged_lookup returns the device copy of (host, n, p, f64) on `device`, or
 // nullptr.
 int stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p, uint64_t* handle);
-int stage_x_cast(int device, const double* x, int64_t n, int64_t p, int n_jobs, float* out,
-                 int* finite, uint64_t* handle);
+int stage_x_cast(int device, const void* x, int x_is_f64, int64_t n, int64_t p, int n_jobs,
+                 float* out, int* finite, uint64_t* handle);
 int stage_x_device(int device, const void* x, const void* x_dev, int x_is_f64, int64_t n,
                    int64_t p, uint64_t* handle);
 int unstage_x(uint64_t handle);

@@ -94,8 +94,9 @@ FS_API int fs_stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_
  * host array's key so that the column statistics and the plan read it. */
 FS_API int fs_stage_x_device(int device, const void* x, const void* x_device, int x_is_f64,
                              int64_t n, int64_t p, uint64_t* staged);
-/* The float64 -> float32 cast of X (round to nearest, as numpy's astype)
- * into the caller's `out` (n x p, row-major; pinned memory from
+/* The float64 -> float32 cast of X (round to nearest, as numpy's astype;
+ * x_is_f64 = 0: a float32 X is copied as is) into the caller's `out`
+ * (n x p, row-major; pinned memory from
  * fs_host_alloc makes the upload a DMA), fused with the finiteness check of
  * the result (*finite as fs_all_finite) and with fs_stage_x of `out`: row
  * blocks are uploaded while later ones are cast.  *staged = 0 when the device
@@ -103,8 +104,8 @@ FS_API int fs_stage_x_device(int device, const void* x, const void* x_device, in
  * way).  Replaces the cast in scikit-learn's validate_data(dtype=np.float32)
  * that MultiSURF.fit starts with (MultiSURF.py:384-386) plus the upload of
  * the cast array. */
-FS_API int fs_stage_x_cast(int device, const double* x, int64_t n, int64_t p, int n_jobs,
-                           float* out, int* finite, uint64_t* staged);
+FS_API int fs_stage_x_cast(int device, const void* x, int x_is_f64, int64_t n, int64_t p,
+                           int n_jobs, float* out, int* finite, uint64_t* staged);
 FS_API int fs_unstage_x(uint64_t staged);
 /* *finite = 1 if every element of the n x p float32 / float64 matrix is
  * finite, else 0 (host threads; n_jobs as the scoring calls).  The

@@ -1,6 +1,6 @@
-"""fs_stage_x_cast: MultiSURF.fit's float64 -> float32 cast fused with the
-finiteness scan and the upload of X (row blocks uploaded while later ones are
-cast).  The cast must equal numpy's astype bit for bit, the scan must flag
+"""fs_stage_x_cast: MultiSURF.fit's float64 -> float32 cast (float32 X: a
+copy into pinned memory) fused with the finiteness scan and the upload of X
+(row blocks uploaded while later ones are cast).  The cast must equal numpy's astype bit for bit, the scan must flag
 exactly what scikit-learn's check would, and a fit through the staged copy
 must score exactly as a fit of the float32 array."""
 import numpy as np
@@ -17,13 +17,15 @@ def _x64(n=3000, p=700, seed=3):
     return x
 
 
-def test_cast_matches_numpy_and_stages():
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_cast_matches_numpy_and_stages(dtype):
     from fastselect_amd import _lib
-    x = _x64()
+    x = _x64().astype(dtype)
     for n_jobs in (1, 3, -1):
         out, finite, h = _lib.stage_x_cast(x, n_jobs)
         try:
             assert finite and h != 0
+            assert out.ctypes.data != x.ctypes.data
             np.testing.assert_array_equal(out.view(np.uint32), x.astype(np.float32).view(np.uint32))
         finally:
             with _lib.unstaged(h):
@@ -49,6 +51,9 @@ def test_fit_from_float64_equals_fit_from_float32():
     assert X.size >= 1 << 20  # takes the staged cast
     a = MultiSURF(n_features_to_select=10, backend="gpu").fit(X, y)
     b = MultiSURF(n_features_to_select=10, backend="gpu").fit(X.astype(np.float32), y)
+    # not staged at fit time (Fortran order takes validate_xy): same scores
+    d = MultiSURF(n_features_to_select=10, backend="gpu").fit(np.asfortranarray(X), y)
+    np.testing.assert_array_equal(a.feature_importances_, d.feature_importances_)
     np.testing.assert_array_equal(a.feature_importances_, b.feature_importances_)
     np.testing.assert_array_equal(a.top_features_, b.top_features_)
     # ... and again with the same array (the staged copy was released)
@@ -56,9 +61,11 @@ def test_fit_from_float64_equals_fit_from_float32():
     np.testing.assert_array_equal(a.feature_importances_, c.feature_importances_)
 
 
-def test_fit_with_nan_raises_scikit_learn_error():
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+def test_fit_with_nan_raises_scikit_learn_error(dtype):
     from fastselect_amd import MultiSURF
     X, y = make_classification(n_samples=1100, n_features=1000, random_state=2)
+    X = X.astype(dtype)
     X[1050, 10] = np.nan
     with pytest.raises(ValueError, match="Input X contains NaN"):
         MultiSURF(backend="gpu").fit(X, y)
