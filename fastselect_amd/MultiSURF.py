@@ -121,7 +121,8 @@ class _ResidentMultiSURF:
 
     def __init__(self, est: MultiSURF, x, y):
         self.est = est
-        x, y = _base.validate_xy(est, x, y, np.float32, est.n_jobs)
+        x, y = _base.validate_xy(est, x, y, np.float32, est.n_jobs,
+                                 pinned=_base.stage_device(est.backend) is not None)
         est.effective_backend_ = _base.effective_backend(est.backend)
         self.n = x.shape[0]
         self.is_discrete, col_min, col_max = _base.column_preprocess(

@@ -29,7 +29,7 @@ def relieff_inputs(x, y, discrete_limit, where, device=0, n_jobs=-1):
     feature_ranges[is_discrete] = 1.0
     feature_ranges[feature_ranges == 0] = 1.0
     recip = (1.0 / feature_ranges).astype(np.float32)
-    return (_base.to_float32(x, n_jobs), y_enc.astype(np.int32), recip, is_discrete,
+    return (_base.to_float32(x, n_jobs, pinned=where == "gpu"), y_enc.astype(np.int32), recip, is_discrete,
             class_probs.astype(np.float32))
 
 

@@ -40,7 +40,7 @@ def n_select_from(n_features_to_select, n_features: int) -> int:
     raise TypeError("n_features_to_select must be an int or a float.")
 
 
-def validate_xy(est, x, y, dtype, n_jobs=-1):
+def validate_xy(est, x, y, dtype, n_jobs=-1, pinned=False):
     """``validate_data(est, x, y, y_numeric=True, dtype=dtype, ensure_2d=True)``
     as the reference's fit calls it, with scikit-learn's single-threaded
     element-wise finiteness scan of X (~56 ms at cfg4) replaced by
@@ -48,12 +48,13 @@ def validate_xy(est, x, y, dtype, n_jobs=-1):
     plain call runs again and raises scikit-learn's own error, so behaviour and
     messages are unchanged.  A float64 ndarray bound for float32 is cast by
     ``to_float32`` (the same rounding, over host threads: scikit-learn's cast
-    is one thread, ~0.2 s at cfg4).  Returns C-contiguous X."""
+    is one thread, ~0.2 s at cfg4); ``pinned`` (a GPU fit) puts the cast in
+    pinned host memory.  Returns C-contiguous X."""
     from sklearn.utils.validation import validate_data
     xc = x
     if (dtype == np.float32 and isinstance(x, np.ndarray) and type(x) is np.ndarray
             and x.dtype == np.float64 and x.ndim == 2):
-        xc = to_float32(x, n_jobs)
+        xc = to_float32(x, n_jobs, pinned)
     xv, yv = validate_data(est, xc, y, y_numeric=True, dtype=dtype, ensure_2d=True,
                            ensure_all_finite=False)
     xv = np.ascontiguousarray(xv)
@@ -81,7 +82,7 @@ def validate_xy_staged(est, x, y, dtype, n_jobs=-1, device=None):
             or x.dtype not in (np.float64, np.float32) or x.ndim != 2
             or not x.flags.c_contiguous
             or x.size < (1 << 20)):
-        xv, yv = validate_xy(est, x, y, dtype, n_jobs)
+        xv, yv = validate_xy(est, x, y, dtype, n_jobs, pinned=device is not None)
         return xv, yv, 0
     from sklearn.utils.validation import validate_data
     x32, finite, h = _lib.stage_x_cast(x, n_jobs, device)
@@ -98,12 +99,13 @@ def validate_xy_staged(est, x, y, dtype, n_jobs=-1, device=None):
     return xv, yv, h
 
 
-def to_float32(x: np.ndarray, n_jobs: int = -1) -> np.ndarray:
+def to_float32(x: np.ndarray, n_jobs: int = -1, pinned: bool = False) -> np.ndarray:
     """``np.ascontiguousarray(x, dtype=np.float32)`` (the reference's cast,
     round to nearest) with the conversion of large arrays split over threads
     by row blocks (numpy releases the GIL in the copy): 15.8 ms on one thread
-    for ReliefF's cfg3 matrix.  With a GPU visible the result lives in pinned
-    host memory (_lib.pinned_empty)."""
+    for ReliefF's cfg3 matrix.  ``pinned`` (only for fits that score on the
+    GPU: it initialises the HIP runtime) puts the result in pinned host
+    memory (_lib.pinned_empty), so that its upload is a DMA."""
     if x.dtype == np.float32 and x.flags.c_contiguous:
         return x
     n = x.shape[0] if x.ndim else 0
@@ -113,7 +115,7 @@ def to_float32(x: np.ndarray, n_jobs: int = -1) -> np.ndarray:
     from concurrent.futures import ThreadPoolExecutor
     # pinned pages (GPU visible): the cast lands in mapped memory and the
     # upload of X is a DMA from it
-    out = _lib.pinned_empty(x.shape, np.float32)
+    out = _lib.pinned_empty(x.shape, np.float32) if pinned else None
     if out is None:
         out = np.empty(x.shape, dtype=np.float32)
     edges = np.linspace(0, n, min(n, 4 * nt) + 1).astype(np.int64)

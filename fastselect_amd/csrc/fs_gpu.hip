@@ -1198,6 +1198,9 @@ __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, i
 constexpr int kGroup = 8;
 constexpr int kSWaves = 16;                                // waves of k_score_sparse
 constexpr int kStreamEntries = (kTile / kSWaves) * kTile;  // 8 columns x 128 rows
+// floats past xs's last spare row that a pass-2 B-row read may touch (the
+// widest feature block of k_score_sparse)
+constexpr int64_t kXsSlack = 512;
 
 __device__ __forceinline__ uint32_t weight_bits(float w, bool last) {
   return (__float_as_uint(w) & ~1u) | (last ? 1u : 0u);
@@ -2115,7 +2118,8 @@ struct Plan {
   unsigned long long* nnz = nullptr;  // non-zero weights of the last pass 2
   bool nnz_valid = false;
   int sparse = 0;               // pass 2 over non-zero weights only
-  double* spart = nullptr;
+  double* spart = nullptr;       // pass-2 segment partials (own block, shard_segments)
+  size_t spart_cap = 0;           // doubles of spart
   // ambiguous-pair refinement
   int2* list = nullptr;
   int64_t list_cap = 0;
@@ -2550,6 +2554,7 @@ void plan_destroy(Plan* g) {
   for (void* q : g->owned_layout) dev_free(q);
   for (void* q : g->scratch) dev_free(q);
   for (void* q : g->owned_shard) dev_free(q);
+  if (g->spart) dev_free(g->spart);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
   if (g->ev_fork) (void)hipEventDestroy(g->ev_fork);
@@ -2760,6 +2765,51 @@ static int calibrate_band(Plan* g) {
   return FS_OK;
 }
 
+// Shard part of a plan's layout: this rank's continuous columns of the mean
+// correction and the pass-2 segments (sized by the owned tiles and the
+// feature blocks), with the segment partials' buffer grown when needed.
+// plan_layout calls it, and plan_set_shard alone: re-targeting a plan to
+// another tile shard keeps the feature layout, its tables and its band
+// calibration (none of them depends on the shard).
+static int shard_segments(Plan* g) {
+  const Prepared& Q = g->P;
+  g->c_lo = Q.pc * g->rank / g->world;
+  g->c_hi = Q.pc * (g->rank + 1) / g->world;
+  // Pass-2 workgroups: ~64k for the dense pass (256 threads, 128-feature
+  // blocks), ~32k for the sparse one (1024 threads, 256-feature blocks):
+  // enough to fill 256 CUs and bound tail imbalance.  Measured for the sparse
+  // pass at cfg4 (tools/pass2_wgs.sh, k_score_sparse ms at world 1 / one rank
+  // of 8; profiles/r01k/pass2_wgs.txt): 8k 111.8 / 14.7, 16k 105.9 / 14.6,
+  // then on one box, alternating, 32k 107.6 / 14.9 and 107.7 / 14.6 against
+  // 64k 108.1 / 15.0 and 108.0 / 14.6 -- the tail costs more than the
+  // per-workgroup row-block stage below 32k.
+  // Small problems (cfg2: 820 tiles x 20 blocks) take a quarter of their
+  // (tile, block) units as the target, at least 4096: segments of ~4 tiles
+  // amortise each workgroup's row-block stage (tools/cfg2_sweep.sh,
+  // profiles/r02/cfg2_sweep.txt: cfg2 step 6.11 -> 5.83 ms at 4096-8192).
+  const int64_t nfb = g->sparse ? (Q.PW + 255) / 256 : (Q.PW + 127) / 128;
+  int64_t wgs = g->sparse ? std::min<int64_t>(32768, std::max<int64_t>(4096, g->n_tiles * nfb / 4))
+                          : 65536;
+  if (const char* e = std::getenv("FS_PASS2_WGS")) wgs = std::max<int64_t>(256, std::atoll(e));
+  g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + wgs - 1) / wgs);
+  g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
+  if (Q.algo == ALGO_RELIEFF) return FS_OK;
+  const size_t need = (size_t)g->nseg * Q.PW;
+  if (need > g->spart_cap) {
+    if (g->spart) {
+      FS_HIP(hipStreamSynchronize(g->stream));
+      dev_free(g->spart);
+      g->spart = nullptr;
+      g->spart_cap = 0;
+    }
+    void* q = nullptr;
+    FS_TRY(dev_alloc(&q, need * sizeof(double), g->device));
+    g->spart = (double*)q;
+    g->spart_cap = need;
+  }
+  return FS_OK;
+}
+
 // Feature-layout part of a plan: everything sized by the kept features
 // (permutation tables, quantised operands, pass-2 partials), rebuilt when
 // the plan is re-targeted to another feature subset (fs_plan_set_features).
@@ -2794,26 +2844,6 @@ static int plan_layout(Plan* g) {
     }
     if (finalize_scale(Q, cmin.data(), cmax.data())) return FS_EINVAL;
   }
-  g->c_lo = Q.pc * g->rank / g->world;
-  g->c_hi = Q.pc * (g->rank + 1) / g->world;
-  // Pass-2 workgroups: ~64k for the dense pass (256 threads, 128-feature
-  // blocks), ~32k for the sparse one (1024 threads, 256-feature blocks):
-  // enough to fill 256 CUs and bound tail imbalance.  Measured for the sparse
-  // pass at cfg4 (tools/pass2_wgs.sh, k_score_sparse ms at world 1 / one rank
-  // of 8; profiles/r01k/pass2_wgs.txt): 8k 111.8 / 14.7, 16k 105.9 / 14.6,
-  // then on one box, alternating, 32k 107.6 / 14.9 and 107.7 / 14.6 against
-  // 64k 108.1 / 15.0 and 108.0 / 14.6 -- the tail costs more than the
-  // per-workgroup row-block stage below 32k.
-  // Small problems (cfg2: 820 tiles x 20 blocks) take a quarter of their
-  // (tile, block) units as the target, at least 4096: segments of ~4 tiles
-  // amortise each workgroup's row-block stage (tools/cfg2_sweep.sh,
-  // profiles/r02/cfg2_sweep.txt: cfg2 step 6.11 -> 5.83 ms at 4096-8192).
-  const int64_t nfb = g->sparse ? (Q.PW + 255) / 256 : (Q.PW + 127) / 128;
-  int64_t wgs = g->sparse ? std::min<int64_t>(32768, std::max<int64_t>(4096, g->n_tiles * nfb / 4))
-                          : 65536;
-  if (const char* e = std::getenv("FS_PASS2_WGS")) wgs = std::max<int64_t>(256, std::atoll(e));
-  g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + wgs - 1) / wgs);
-  g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
   // histogram shift so that the largest quantised value lands in bin < 4096
   g->rank_shift = 0;
   while ((Q.qmax / std::ldexp(1.0, g->rank_shift)) >= (double)kRankBins) g->rank_shift++;
@@ -2824,15 +2854,19 @@ static int plan_layout(Plan* g) {
       (rc = dalloc(g, &g->scl, Q.PW)) || (rc = dalloc(g, &g->scl32, Q.PW)) ||
       (rc = dalloc(g, &g->dtab_off, Q.PW + 1)) ||
       (rc = dalloc(g, &g->dtab, Q.dtab.size())) ||
-      (rc = dalloc(g, &g->xs, (size_t)(Q.n_pad + 2) * Q.PW))) {
+      // xs: two spare rows (the pass-2 B prefetch runs up to two rows past a
+      // tile) plus kXsSlack floats: the asm loop of a last, partial feature
+      // block reads a whole block width of each B row, past the end of the
+      // last row when PW is narrower than the block
+      (rc = dalloc(g, &g->xs, (size_t)(Q.n_pad + 2) * Q.PW + kXsSlack))) {
   } else if (Q.algo == ALGO_SURF) {
     rc = dalloc(g, &g->xT64, (size_t)Q.PW * Q.n_pad);
   } else if ((rc = dalloc(g, &g->xqT, (size_t)Q.PW * Q.n_pad)) == FS_OK) {
     rc = dalloc(g, &g->epsT, (size_t)Q.PW * Q.n_pad);
   }
-  if (rc == FS_OK && Q.algo != ALGO_RELIEFF) rc = dalloc(g, &g->spart, (size_t)g->nseg * Q.PW);
   g->alloc_target = 0;
   if (rc) return rc;
+  if ((rc = shard_segments(g))) return rc;
   std::vector<double> qs(Q.PW, 0.0);
   for (int64_t c = 0; c < Q.PW; c++) qs[c] = Q.scale[c] * Q.SC;
   std::vector<float> scl32(Q.PW, 0.0f);
@@ -2931,7 +2965,7 @@ int plan_set_shard(Plan* g, int rank, int world) {
   std::vector<int32_t> bi, bj;
   owned_tiles(g->nb, rank, world, bi, bj);
   FS_TRY(setup_shard(g, bi, bj));
-  return plan_layout(g);  // pass-2 segments and this shard's mean-correction columns
+  return shard_segments(g);  // pass-2 segments and this shard's mean-correction columns
 }
 
 int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int device,

@@ -49,6 +49,11 @@ def row_chunk(n: int, rank: int, world: int):
     return min(n, rank * rows), min(n, (rank + 1) * rows), rows
 
 
+class GatherFailed(RuntimeError):
+    """Raised on EVERY rank when some rank could not set up the all-gather of
+    X, so that all of them take the per-rank upload together."""
+
+
 def gather_rows(x, device=None, force=False):
     """All of the float32 host matrix ``x`` in one tensor on ``device`` (a
     CUDA ordinal; None = host tensors, the gloo rehearsal), with this rank
@@ -63,10 +68,22 @@ def gather_rows(x, device=None, force=False):
         return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
     lo, hi, rows = row_chunk(n, rank, world)
     dev = torch.device("cpu") if device is None else torch.device("cuda", device)
-    buf = torch.empty((rows * world, p), dtype=torch.float32, device=dev)
-    mine = buf[rank * rows:(rank + 1) * rows]
-    if hi > lo:
-        mine[:hi - lo].copy_(torch.from_numpy(x[lo:hi]))
+    # The buffer and this rank's rows are set up first and every rank learns
+    # whether all of them managed it before anyone enters the all-gather: a
+    # rank that failed alone (out of memory) would otherwise leave its peers
+    # blocked in the collective while it went on to the next one.
+    err = None
+    try:
+        buf = torch.empty((rows * world, p), dtype=torch.float32, device=dev)
+        mine = buf[rank * rows:(rank + 1) * rows]
+        if hi > lo:
+            mine[:hi - lo].copy_(torch.from_numpy(x[lo:hi]))
+    except RuntimeError as e:
+        err = e
+    ok = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if int(ok.item()) == 0:
+        raise GatherFailed(f"rank {rank}: {err}" if err else "another rank could not stage its rows")
     if dev.type == "cuda":
         dist.all_gather_into_tensor(buf, mine)          # in place, RCCL over xGMI
         # the library reads buf on its own streams (column statistics): the
@@ -97,9 +114,11 @@ def resident_x(x, backend="gpu", device=0, gather=None):
         return
     try:
         buf = gather_rows(x, device, force=True)
-    except RuntimeError as e:
+    except GatherFailed as e:
         # the all-gather only saves host-to-device copies: without it every
-        # rank uploads X itself (same result), and says so
+        # rank uploads X itself (same result), and says so.  Only the
+        # collective decision falls back; an error inside the all-gather
+        # itself propagates on the ranks that see it.
         import sys
         print(f"fastselect_amd: RCCL all-gather of X failed ({e}); uploading X per rank",
               file=sys.stderr, flush=True)
@@ -149,7 +168,6 @@ class ShardedMultiSURF:
             env = os.environ.get("FS_SHARDS")
             shards = int(env) if env else (
                 _lib.multisurf_shards(self.n, self.p, self.world, device) if backend == "gpu" else 1)
-        self.shards = max(1, int(shards))
         if backend == "gpu":
             torch.cuda.set_device(device)
             self.tdev = torch.device("cuda", device)
@@ -157,6 +175,11 @@ class ShardedMultiSURF:
         else:
             self.tdev = torch.device("cpu")
             stream = 0
+        # Every rank must use the same shard count: ownership is tile t ->
+        # shard t % (world * V), so ranks with different V would score some
+        # tiles twice and others never.  Each rank sizes V from its own free
+        # memory; the largest V fits on every rank.
+        self.shards = self._agree_max(max(1, int(shards)))
         self.plan = _lib.Plan(backend, x, y, recip, is_discrete, use_star=use_star,
                               rank=self.rank, world=self.world * self.shards, device=device,
                               stream=stream)
@@ -166,6 +189,15 @@ class ShardedMultiSURF:
         self.rowstats = torch.zeros(3 * self.n, dtype=f64, device=self.tdev)
         self.counts = torch.zeros(2 * self.n, dtype=f64, device=self.tdev)
         self.scores = torch.zeros(self.p, dtype=f64, device=self.tdev)
+
+    def _agree_max(self, v: int) -> int:
+        """MAX of an integer over the ranks (no collective without a group)."""
+        if self.dist is None or self.world == 1:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.int64, device=self.tdev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return int(t.item())
 
     def set_features(self, feat_idx):
         """Score another feature subset of the resident samples from the next
@@ -254,7 +286,7 @@ def multisurf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", dev
     """Score X on this rank's share of the tiles and return the full float32
     score vector (identical on every rank).  X reaches the GPUs once
     (``resident_x``: per-rank rows + an RCCL all-gather when sharded)."""
-    x = _base.to_float32(np.asarray(X))
+    x = _base.to_float32(np.asarray(X), pinned=backend == "gpu")
     with resident_x(x, backend, device):
         x, yv, recip, isd = prepare_inputs(x, y, discrete_limit, backend, device)
         job = ShardedMultiSURF(x, yv, recip, isd, use_star=use_star, backend=backend,

@@ -56,9 +56,13 @@ def _load():
                                    _i64, _i64, ctypes.c_int, _f32p]
     lib.oracle_surf.argtypes = [_f64p, _i64, _i64, _i32p, _f32p, ctypes.c_int, _u8p, _i64, _i64,
                                 ctypes.c_int, _f32p]
+    lib.oracle_multisurf_acc.argtypes = lib.oracle_multisurf.argtypes[:-1] + [ctypes.c_int, _f32p]
+    lib.oracle_relieff_acc.argtypes = lib.oracle_relieff.argtypes[:-1] + [ctypes.c_int, _f32p]
+    lib.oracle_surf_acc.argtypes = lib.oracle_surf.argtypes[:-1] + [ctypes.c_int, _f32p]
     lib.numba_argsort_f32.argtypes = [_f32p, _i64, _i64p]
     lib.oracle_max_threads.restype = ctypes.c_int
-    for fn in (lib.oracle_multisurf, lib.oracle_relieff, lib.oracle_surf):
+    for fn in (lib.oracle_multisurf, lib.oracle_relieff, lib.oracle_surf, lib.oracle_multisurf_acc,
+               lib.oracle_relieff_acc, lib.oracle_surf_acc):
         fn.restype = ctypes.c_int
     _lib = lib
     return lib
@@ -66,6 +70,12 @@ def _load():
 
 def _ptr(a, t):
     return a.ctypes.data_as(t)
+
+
+def _acc(accum) -> int:
+    if accum not in ("f32", "f64"):
+        raise ValueError("accum must be 'f32' (the reference) or 'f64'")
+    return 1 if accum == "f64" else 0
 
 
 def max_threads() -> int:
@@ -79,8 +89,11 @@ def is_discrete_mask(x: np.ndarray, discrete_limit: int) -> np.ndarray:
 
 
 def multisurf_scores(X, y, use_star=False, discrete_limit=10, i_range=None, n_jobs=-1,
-                     feat_idx=None):
-    """Reference ``MultiSURF(backend='cpu').fit(X, y).feature_importances_``."""
+                     feat_idx=None, accum="f32"):
+    """Reference ``MultiSURF(backend='cpu').fit(X, y).feature_importances_``.
+    accum='f64' (parity attribution only, not the reference): the same diffs,
+    distances and near/far decisions with every later sum in float64
+    (oracle_multisurf_acc)."""
     x = np.ascontiguousarray(X, dtype=np.float32)           # validate_data dtype=float32 (:384-386)
     yv = np.ascontiguousarray(np.asarray(y), dtype=np.float64)  # y kept numeric; compared by value (:216)
     n, p = x.shape
@@ -91,16 +104,18 @@ def multisurf_scores(X, y, use_star=False, discrete_limit=10, i_range=None, n_jo
     fidx = np.arange(p, dtype=np.int64) if feat_idx is None else np.ascontiguousarray(feat_idx, dtype=np.int64)
     i0, i1 = (0, n) if i_range is None else i_range
     out = np.zeros(fidx.size, dtype=np.float32)
-    rc = _load().oracle_multisurf(_ptr(x, _f32p), n, p, _ptr(yv, _f64p), _ptr(recip, _f32p),
-                                  _ptr(fidx, _i64p), fidx.size, int(bool(use_star)),
-                                  _ptr(is_disc, _u8p), i0, i1, int(n_jobs), _ptr(out, _f32p))
+    rc = _load().oracle_multisurf_acc(_ptr(x, _f32p), n, p, _ptr(yv, _f64p), _ptr(recip, _f32p),
+                                      _ptr(fidx, _i64p), fidx.size, int(bool(use_star)),
+                                      _ptr(is_disc, _u8p), i0, i1, int(n_jobs), _acc(accum),
+                                      _ptr(out, _f32p))
     if rc != 0:
         raise RuntimeError(f"oracle_multisurf failed: {rc}")
     return out
 
 
-def relieff_scores(X, y, n_neighbors=3, discrete_limit=10, i_range=None, n_jobs=-1):
-    """Reference ``ReliefF(backend='cpu').fit(X, y).feature_importances_``."""
+def relieff_scores(X, y, n_neighbors=3, discrete_limit=10, i_range=None, n_jobs=-1, accum="f32"):
+    """Reference ``ReliefF(backend='cpu').fit(X, y).feature_importances_``
+    (accum as ``multisurf_scores``)."""
     x64 = np.ascontiguousarray(X, dtype=np.float64)          # validate_data dtype=float64 (:343-345)
     y = np.asarray(y)
     n, p = x64.shape
@@ -120,16 +135,17 @@ def relieff_scores(X, y, n_neighbors=3, discrete_limit=10, i_range=None, n_jobs=
     isd = np.ascontiguousarray(is_disc.astype(np.uint8))
     i0, i1 = (0, n) if i_range is None else i_range
     out = np.zeros(p, dtype=np.float32)
-    rc = _load().oracle_relieff(_ptr(x32, _f32p), n, p, _ptr(y_enc, _i32p), _ptr(recip, _f32p),
-                                _ptr(isd, _u8p), int(n_neighbors), _ptr(cp, _f32p), cp.size, i0, i1,
-                                int(n_jobs), _ptr(out, _f32p))
+    rc = _load().oracle_relieff_acc(_ptr(x32, _f32p), n, p, _ptr(y_enc, _i32p), _ptr(recip, _f32p),
+                                    _ptr(isd, _u8p), int(n_neighbors), _ptr(cp, _f32p), cp.size, i0,
+                                    i1, int(n_jobs), _acc(accum), _ptr(out, _f32p))
     if rc != 0:
         raise RuntimeError(f"oracle_relieff failed: {rc}")
     return out
 
 
-def surf_scores(X, y, use_star=False, discrete_limit=10, i_range=None, n_jobs=-1):
-    """Reference ``SURF(backend='cpu').fit(X, y).feature_importances_``."""
+def surf_scores(X, y, use_star=False, discrete_limit=10, i_range=None, n_jobs=-1, accum="f32"):
+    """Reference ``SURF(backend='cpu').fit(X, y).feature_importances_``
+    (accum as ``multisurf_scores``)."""
     x = np.ascontiguousarray(X, dtype=np.float64)            # validate_data dtype=float64 (:330-332)
     n, p = x.shape
     is_disc = is_discrete_mask(x, discrete_limit)             # :347-350
@@ -141,9 +157,9 @@ def surf_scores(X, y, use_star=False, discrete_limit=10, i_range=None, n_jobs=-1
     isd = np.ascontiguousarray(is_disc.astype(np.uint8))
     i0, i1 = (0, n) if i_range is None else i_range
     out = np.zeros(p, dtype=np.float32)
-    rc = _load().oracle_surf(_ptr(x, _f64p), n, p, _ptr(yi, _i32p), _ptr(recip, _f32p),
-                             int(bool(use_star)), _ptr(isd, _u8p), i0, i1, int(n_jobs),
-                             _ptr(out, _f32p))
+    rc = _load().oracle_surf_acc(_ptr(x, _f64p), n, p, _ptr(yi, _i32p), _ptr(recip, _f32p),
+                                 int(bool(use_star)), _ptr(isd, _u8p), i0, i1, int(n_jobs),
+                                 _acc(accum), _ptr(out, _f32p))
     if rc != 0:
         raise RuntimeError(f"oracle_surf failed: {rc}")
     return out

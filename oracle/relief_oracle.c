@@ -77,19 +77,45 @@ static inline double ms_diff(const float* xi, const float* xj, const float* reci
   return (double)d;
 }
 
-ORACLE_API int oracle_multisurf(const float* x, int64_t n, int64_t p, const double* y,
-                                const float* recip, const int64_t* feat_idx, int64_t n_kept,
-                                int use_star, const uint8_t* is_discrete, int64_t i_begin,
-                                int64_t i_end, int n_jobs, float* scores_out) {
+/* accum64 = 0: the reference's arithmetic (float32 per-sample sums, float32
+ * rows, float32 sequential column sum).  accum64 = 1 (parity attribution,
+ * not the reference): the same diffs, distances and near/far decisions, but
+ * every sum after them -- per-sample hit/miss sums, the division, the row and
+ * the column sum -- in float64, rounded to float32 once at the end.  The
+ * difference between the two is the reference's own float32 accumulation
+ * error (tests/test_parity_attribution.py). */
+static inline double acc_round(int accum64, double v) { return accum64 ? v : (double)(float)v; }
+
+/* Column sum of the per-sample rows (float32 sequential as the reference's
+ * `.sum()`, or float64 with accum64), then `/ n` (host callers). */
+static void colsum(const double* temp, int64_t m, int64_t p, int64_t n, int accum64, float* out) {
+#pragma omp parallel for schedule(static)
+  for (int64_t k = 0; k < p; k++) {
+    if (accum64) {
+      double s = 0.0;
+      for (int64_t r = 0; r < m; r++) s += temp[r * p + k];
+      out[k] = (float)(s / (double)n);
+    } else {
+      float s = 0.0f;
+      for (int64_t r = 0; r < m; r++) s += (float)temp[r * p + k];
+      out[k] = s / (float)n;
+    }
+  }
+}
+
+ORACLE_API int oracle_multisurf_acc(const float* x, int64_t n, int64_t p, const double* y,
+                                    const float* recip, const int64_t* feat_idx, int64_t n_kept,
+                                    int use_star, const uint8_t* is_discrete, int64_t i_begin,
+                                    int64_t i_end, int n_jobs, int accum64, float* scores_out) {
   if (n < 2 || i_begin < 0 || i_end > n || i_begin > i_end) return -1;
   int64_t m = i_end - i_begin;
-  float* temp = (float*)calloc((size_t)(m > 0 ? m : 1) * (size_t)n_kept, sizeof(float));
+  double* temp = (double*)calloc((size_t)(m > 0 ? m : 1) * (size_t)n_kept, sizeof(double));
   if (!temp) return -2;
   set_threads(n_jobs);
 #pragma omp parallel
   {
-    float* hit_diffs = (float*)malloc(sizeof(float) * (size_t)n_kept);
-    float* miss_diffs = (float*)malloc(sizeof(float) * (size_t)n_kept);
+    double* hit_diffs = (double*)malloc(sizeof(double) * (size_t)n_kept);
+    double* miss_diffs = (double*)malloc(sizeof(double) * (size_t)n_kept);
 #pragma omp for schedule(dynamic, 1)
     for (int64_t i = i_begin; i < i_end; i++) {
       const float* xi = x + i * p;
@@ -108,8 +134,8 @@ ORACLE_API int oracle_multisurf(const float* x, int64_t n, int64_t p, const doub
       if (var < 0.0) var = 0.0;
       double thresh = mu - 0.5 * sqrt(var);
       /* pass 2: near hits / near misses (/ far misses) (MultiSURF.py:198-243) */
-      memset(hit_diffs, 0, sizeof(float) * (size_t)n_kept);
-      memset(miss_diffs, 0, sizeof(float) * (size_t)n_kept);
+      memset(hit_diffs, 0, sizeof(double) * (size_t)n_kept);
+      memset(miss_diffs, 0, sizeof(double) * (size_t)n_kept);
       int64_t n_hits = 0, n_miss = 0;
       for (int64_t j = 0; j < n; j++) {
         if (i == j) continue;
@@ -121,37 +147,42 @@ ORACLE_API int oracle_multisurf(const float* x, int64_t n, int64_t p, const doub
           if (is_hit) {
             n_hits++;
             for (int64_t k = 0; k < n_kept; k++)
-              hit_diffs[k] = (float)((double)hit_diffs[k] + ms_diff(xi, xj, recip, is_discrete, feat_idx[k]));
+              hit_diffs[k] = acc_round(accum64, hit_diffs[k] + ms_diff(xi, xj, recip, is_discrete, feat_idx[k]));
           } else {
             n_miss++;
             for (int64_t k = 0; k < n_kept; k++)
-              miss_diffs[k] = (float)((double)miss_diffs[k] + ms_diff(xi, xj, recip, is_discrete, feat_idx[k]));
+              miss_diffs[k] = acc_round(accum64, miss_diffs[k] + ms_diff(xi, xj, recip, is_discrete, feat_idx[k]));
           }
         } else if (use_star && !is_hit) {
           for (int64_t k = 0; k < n_kept; k++)
-            miss_diffs[k] = (float)((double)miss_diffs[k] - ms_diff(xi, xj, recip, is_discrete, feat_idx[k]));
+            miss_diffs[k] = acc_round(accum64, miss_diffs[k] - ms_diff(xi, xj, recip, is_discrete, feat_idx[k]));
         }
       }
       /* MultiSURF.py:245-251: in-place float32 /= int (computed in float64) */
       if (n_hits > 0)
-        for (int64_t k = 0; k < n_kept; k++) hit_diffs[k] = (float)((double)hit_diffs[k] / (double)n_hits);
+        for (int64_t k = 0; k < n_kept; k++) hit_diffs[k] = acc_round(accum64, hit_diffs[k] / (double)n_hits);
       if (n_miss > 0)
-        for (int64_t k = 0; k < n_kept; k++) miss_diffs[k] = (float)((double)miss_diffs[k] / (double)n_miss);
-      float* row = temp + (i - i_begin) * n_kept;
-      for (int64_t k = 0; k < n_kept; k++) row[k] = miss_diffs[k] - hit_diffs[k];
+        for (int64_t k = 0; k < n_kept; k++) miss_diffs[k] = acc_round(accum64, miss_diffs[k] / (double)n_miss);
+      double* row = temp + (i - i_begin) * n_kept;
+      for (int64_t k = 0; k < n_kept; k++)
+        row[k] = accum64 ? miss_diffs[k] - hit_diffs[k]
+                         : (double)((float)miss_diffs[k] - (float)hit_diffs[k]);
     }
     free(hit_diffs);
     free(miss_diffs);
   }
   /* MultiSURF.py:252-253 column sum (float32, sequential), host caller :270 `/ n` */
-#pragma omp parallel for schedule(static)
-  for (int64_t k = 0; k < n_kept; k++) {
-    float s = 0.0f;
-    for (int64_t r = 0; r < m; r++) s += temp[r * n_kept + k];
-    scores_out[k] = s / (float)n;
-  }
+  colsum(temp, m, n_kept, n, accum64, scores_out);
   free(temp);
   return 0;
+}
+
+ORACLE_API int oracle_multisurf(const float* x, int64_t n, int64_t p, const double* y,
+                                const float* recip, const int64_t* feat_idx, int64_t n_kept,
+                                int use_star, const uint8_t* is_discrete, int64_t i_begin,
+                                int64_t i_end, int n_jobs, float* scores_out) {
+  return oracle_multisurf_acc(x, n, p, y, recip, feat_idx, n_kept, use_star, is_discrete, i_begin,
+                              i_end, n_jobs, 0, scores_out);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -231,13 +262,13 @@ static inline double rf_diff(const float* xi, const float* xj, const float* reci
   return (double)(fabsf(xi[f] - xj[f]) * recip[f]);
 }
 
-ORACLE_API int oracle_relieff(const float* x, int64_t n, int64_t p, const int32_t* y_enc,
-                              const float* recip, const uint8_t* is_discrete, int64_t k,
-                              const float* class_probs, int64_t n_classes, int64_t i_begin,
-                              int64_t i_end, int n_jobs, float* scores_out) {
+ORACLE_API int oracle_relieff_acc(const float* x, int64_t n, int64_t p, const int32_t* y_enc,
+                                  const float* recip, const uint8_t* is_discrete, int64_t k,
+                                  const float* class_probs, int64_t n_classes, int64_t i_begin,
+                                  int64_t i_end, int n_jobs, int accum64, float* scores_out) {
   if (n < 2 || k < 0 || i_begin < 0 || i_end > n || i_begin > i_end) return -1;
   int64_t m = i_end - i_begin;
-  float* temp = (float*)calloc((size_t)(m > 0 ? m : 1) * (size_t)p, sizeof(float));
+  double* temp = (double*)calloc((size_t)(m > 0 ? m : 1) * (size_t)p, sizeof(double));
   if (!temp) return -2;
   set_threads(n_jobs);
 #pragma omp parallel
@@ -276,7 +307,7 @@ ORACLE_API int oracle_relieff(const float* x, int64_t n, int64_t p, const int32_
       /* ReliefF.py:177-179 */
       double denom = 1.0 - (double)class_probs[lbl_i];
       if (denom == 0.0) denom = 1.0;
-      float* row = temp + (i - i_begin) * p;
+      double* row = temp + (i - i_begin) * p;
       /* ReliefF.py:181-216 */
       for (int64_t f = 0; f < p; f++) {
         double hit_sum = 0.0;
@@ -293,7 +324,7 @@ ORACLE_API int oracle_relieff(const float* x, int64_t n, int64_t p, const int32_
         double update = 0.0;
         if (h_found > 0) update -= hit_sum / (double)h_found;
         if (k > 0) update += miss_sum / (double)k;
-        row[f] = (float)update;
+        row[f] = acc_round(accum64, update);
       }
     }
     free(dists);
@@ -303,14 +334,17 @@ ORACLE_API int oracle_relieff(const float* x, int64_t n, int64_t p, const int32_
     free(m_found);
   }
   /* ReliefF.py:219-220 column sum, host caller :236 `/ n` */
-#pragma omp parallel for schedule(static)
-  for (int64_t f = 0; f < p; f++) {
-    float s = 0.0f;
-    for (int64_t r = 0; r < m; r++) s += temp[r * p + f];
-    scores_out[f] = s / (float)n;
-  }
+  colsum(temp, m, p, n, accum64, scores_out);
   free(temp);
   return 0;
+}
+
+ORACLE_API int oracle_relieff(const float* x, int64_t n, int64_t p, const int32_t* y_enc,
+                              const float* recip, const uint8_t* is_discrete, int64_t k,
+                              const float* class_probs, int64_t n_classes, int64_t i_begin,
+                              int64_t i_end, int n_jobs, float* scores_out) {
+  return oracle_relieff_acc(x, n, p, y_enc, recip, is_discrete, k, class_probs, n_classes, i_begin,
+                            i_end, n_jobs, 0, scores_out);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -324,21 +358,22 @@ static inline double sf_diff(const double* xi, const double* xj, const float* re
   return fabs(xi[f] - xj[f]) * (double)recip[f];
 }
 
-ORACLE_API int oracle_surf(const double* x, int64_t n, int64_t p, const int32_t* y,
-                           const float* recip, int use_star, const uint8_t* is_discrete,
-                           int64_t i_begin, int64_t i_end, int n_jobs, float* scores_out) {
+ORACLE_API int oracle_surf_acc(const double* x, int64_t n, int64_t p, const int32_t* y,
+                               const float* recip, int use_star, const uint8_t* is_discrete,
+                               int64_t i_begin, int64_t i_end, int n_jobs, int accum64,
+                               float* scores_out) {
   if (n < 2 || i_begin < 0 || i_end > n || i_begin > i_end) return -1;
   int64_t m = i_end - i_begin;
-  float* temp = (float*)calloc((size_t)(m > 0 ? m : 1) * (size_t)p, sizeof(float));
+  double* temp = (double*)calloc((size_t)(m > 0 ? m : 1) * (size_t)p, sizeof(double));
   if (!temp) return -2;
   set_threads(n_jobs);
 #pragma omp parallel
   {
     float* dists = (float*)malloc(sizeof(float) * (size_t)n);
-    float* nh = (float*)malloc(sizeof(float) * (size_t)p);
-    float* nm = (float*)malloc(sizeof(float) * (size_t)p);
-    float* fh = (float*)malloc(sizeof(float) * (size_t)p);
-    float* fm = (float*)malloc(sizeof(float) * (size_t)p);
+    double* nh = (double*)malloc(sizeof(double) * (size_t)p);
+    double* nm = (double*)malloc(sizeof(double) * (size_t)p);
+    double* fh = (double*)malloc(sizeof(double) * (size_t)p);
+    double* fm = (double*)malloc(sizeof(double) * (size_t)p);
 #pragma omp for schedule(dynamic, 1)
     for (int64_t i = i_begin; i < i_end; i++) {
       const double* xi = x + i * p;
@@ -357,28 +392,37 @@ ORACLE_API int oracle_surf(const double* x, int64_t n, int64_t p, const int32_t*
       float sum_d = 0.0f;
       for (int64_t j = 0; j < n; j++) sum_d += dists[j];
       double avg = (double)sum_d / (double)(n - 1);
-      memset(nh, 0, sizeof(float) * (size_t)p);
-      memset(nm, 0, sizeof(float) * (size_t)p);
-      memset(fh, 0, sizeof(float) * (size_t)p);
-      memset(fm, 0, sizeof(float) * (size_t)p);
+      memset(nh, 0, sizeof(double) * (size_t)p);
+      memset(nm, 0, sizeof(double) * (size_t)p);
+      memset(fh, 0, sizeof(double) * (size_t)p);
+      memset(fm, 0, sizeof(double) * (size_t)p);
       /* SURF.py:170-189 */
       for (int64_t j = 0; j < n; j++) {
         if (i == j) continue;
         int is_hit = y[i] == y[j];
         int is_near = (double)dists[j] < avg;
-        float* acc;
+        double* acc;
         if (is_near) acc = is_hit ? nh : nm;
         else if (use_star) acc = is_hit ? fh : fm;
         else continue;
         const double* xj = x + j * p;
-        for (int64_t f = 0; f < p; f++) acc[f] += (float)sf_diff(xi, xj, recip, is_discrete, f);
+        /* float32 diffs (diffs_from_i), float32 sums (or float64 with accum64) */
+        for (int64_t f = 0; f < p; f++)
+          acc[f] = accum64 ? acc[f] + (double)(float)sf_diff(xi, xj, recip, is_discrete, f)
+                           : (double)((float)acc[f] + (float)sf_diff(xi, xj, recip, is_discrete, f));
       }
       /* SURF.py:191-195 */
-      float* row = temp + (i - i_begin) * p;
+      double* row = temp + (i - i_begin) * p;
       for (int64_t f = 0; f < p; f++) {
-        float u = nm[f] - nh[f];
-        if (use_star) u += fh[f] - fm[f];
-        row[f] = u;
+        if (accum64) {
+          double u = nm[f] - nh[f];
+          if (use_star) u += fh[f] - fm[f];
+          row[f] = u;
+        } else {
+          float u = (float)nm[f] - (float)nh[f];
+          if (use_star) u += (float)fh[f] - (float)fm[f];
+          row[f] = (double)u;
+        }
       }
     }
     free(dists);
@@ -388,12 +432,14 @@ ORACLE_API int oracle_surf(const double* x, int64_t n, int64_t p, const int32_t*
     free(fm);
   }
   /* SURF.py:195/216-218: private_scores accumulation then `/ n` */
-#pragma omp parallel for schedule(static)
-  for (int64_t f = 0; f < p; f++) {
-    float s = 0.0f;
-    for (int64_t r = 0; r < m; r++) s += temp[r * p + f];
-    scores_out[f] = s / (float)n;
-  }
+  colsum(temp, m, p, n, accum64, scores_out);
   free(temp);
   return 0;
+}
+
+ORACLE_API int oracle_surf(const double* x, int64_t n, int64_t p, const int32_t* y,
+                           const float* recip, int use_star, const uint8_t* is_discrete,
+                           int64_t i_begin, int64_t i_end, int n_jobs, float* scores_out) {
+  return oracle_surf_acc(x, n, p, y, recip, use_star, is_discrete, i_begin, i_end, n_jobs, 0,
+                         scores_out);
 }

@@ -13,6 +13,9 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+TESTS = os.path.dirname(os.path.abspath(__file__))
+if TESTS not in sys.path:
+    sys.path.insert(0, TESTS)
 
 
 def pytest_configure(config):
@@ -27,21 +30,15 @@ def oracle():
     return O
 
 
-def scale_rel_err(a, ref):
-    """max_f |a_f - ref_f| / max_f |ref_f| (SURVEY.md §8d parity criterion)."""
-    a = np.asarray(a, dtype=np.float64)
-    ref = np.asarray(ref, dtype=np.float64)
-    den = np.abs(ref).max()
-    if den == 0.0:
-        return np.abs(a).max()
-    return np.abs(a - ref).max() / den
+from parity_metrics import scale_rel_err, summary, topk_same  # noqa: E402  (tests/ on sys.path)
 
 
 def assert_parity(a, ref, tol=1e-5, k=None):
-    """Scores within `tol` scale-relative, and identical top-k index sets."""
+    """Scores within `tol` scale-relative, and identical
+    top-k index sets.  A failure reports the per-element figures of §8d too."""
     err = scale_rel_err(a, ref)
-    assert err <= tol, f"scale-relative error {err:.3e} > {tol:.1e}"
+    assert err <= tol, f"scale-relative error {err:.3e} > {tol:.1e} ({summary(a, ref)})"
     if k is not None:
         ta = set(np.argsort(np.asarray(a))[::-1][:k].tolist())
         tr = set(np.argsort(np.asarray(ref))[::-1][:k].tolist())
-        assert ta == tr, f"top-{k} differ: {sorted(ta ^ tr)}"
+        assert ta == tr, f"top-{k} differ: {sorted(ta ^ tr)} ({summary(a, ref)})"

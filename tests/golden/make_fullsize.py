@@ -12,6 +12,8 @@ size):
     i_range    focal samples the oracle scored ([0, n) = the whole fit; a
                slice gives sum_{i in slice} row_i / n, the reference's column
                sum restricted to those rows)
+    accum      'f32' (the reference's arithmetic) or 'f64' (*_f64 fixtures:
+               the same diffs and decisions, every later sum in float64)
 
 Inputs follow SURVEY.md §8d: make_classification(n, p, n_informative=20,
 n_redundant=R, random_state=42), R = 50 for cfg3 and 100 otherwise.
@@ -38,6 +40,17 @@ CONFIGS = {
     "cfg5_surf_slice": ("surf", 10000, 50000, 100, (4992, 5376), {"use_star": False}),
     "cfg5_multisurfstar": ("multisurf", 10000, 50000, 100, None, {"use_star": True}),
     "cfg4_multisurf": ("multisurf", 20000, 20000, 100, None, {}),
+    # accum='f64': the oracle with every sum after the diffs in float64 (not
+    # the reference; the "exact" side of tests/test_parity_attribution.py)
+    "cfg2_multisurf_f64": ("multisurf", 5000, 5000, 100, None, {"accum": "f64"}),
+    "cfg3_relieff_k10_f64": ("relieff", 20000, 2000, 50, None, {"n_neighbors": 10, "accum": "f64"}),
+    "cfg5_surfstar_slice_f64": ("surf", 10000, 50000, 100, (0, 384),
+                                {"use_star": True, "accum": "f64"}),
+    "cfg5_surf_slice_f64": ("surf", 10000, 50000, 100, (4992, 5376),
+                            {"use_star": False, "accum": "f64"}),
+    "cfg4_multisurf_f64": ("multisurf", 20000, 20000, 100, None, {"accum": "f64"}),
+    "cfg5_multisurfstar_f64": ("multisurf", 10000, 50000, 100, None,
+                               {"use_star": True, "accum": "f64"}),
 }
 
 
@@ -71,7 +84,8 @@ def run(name, n_jobs):
              scores=s.astype(np.float32), i_range=ir, n=np.array(n), p=np.array(p),
              n_redundant=np.array(red), algo=np.array(algo),
              use_star=np.array(bool(extra.get("use_star", False))),
-             n_neighbors=np.array(int(extra.get("n_neighbors", 0))))
+             n_neighbors=np.array(int(extra.get("n_neighbors", 0))),
+             accum=np.array(extra.get("accum", "f32")))
     print(f"{name}: {time.time() - t0:.0f} s -> {out}", flush=True)
 
 

@@ -172,3 +172,27 @@ def test_threaded_float32_cast_equals_numpy():
         got = _base.to_float32(arr, n_jobs=4)
         assert got.flags.c_contiguous and got.dtype == np.float32
         np.testing.assert_array_equal(got, np.ascontiguousarray(arr, dtype=np.float32))
+
+
+def test_cpu_preprocessing_does_not_pin_host_memory(monkeypatch):
+    """a backend='cpu' fit must not touch the HIP runtime
+    -- the threaded float32 cast uses plain host memory unless the fit scores
+    on the GPU (pinned=True)."""
+    from fastselect_amd import _base, _lib
+    from fastselect_amd.ReliefF import relieff_inputs
+
+    def boom(*a, **k):
+        raise AssertionError("pinned host memory requested by a CPU fit")
+
+    monkeypatch.setattr(_lib, "pinned_empty", boom)
+    rng = np.random.default_rng(5)
+    x = rng.normal(size=(2100, 2000))
+    y = np.arange(2100) % 2
+    assert x.size >= (1 << 22)
+    got = _base.to_float32(x, n_jobs=4)
+    np.testing.assert_array_equal(got, x.astype(np.float32))
+    from fastselect_amd import ReliefF
+    xv, _ = _base.validate_xy(ReliefF(backend="cpu"), x, y, np.float32, 4)
+    np.testing.assert_array_equal(xv, x.astype(np.float32))
+    x32 = relieff_inputs(x, y, 10, "cpu", n_jobs=4)[0]
+    np.testing.assert_array_equal(x32, x.astype(np.float32))

@@ -12,6 +12,18 @@ max_f |s_ref_f| and identical top-10 index sets (the reference ranks with
 np.argsort(scores)[::-1][:k], MultiSURF.py:443).  Slices compare the sums of
 the same focal samples (the reference's per-sample rows summed over
 i_range, / n).
+
+Attribution (VERDICT r2 next #1b): where a float64-accumulation fixture
+exists (fullsize_*_f64.npz: the oracle with the same diffs and near/far
+decisions but every later sum in float64), the GPU's scores must be at least
+as close to those float64 sums as the reference arithmetic is -- in the
+maximum and in the rms over all features -- i.e. the residual against the
+reference is the reference's own float32 accumulation.  Where the GPU takes
+every near/far decision as the reference does (32-bit pass 1: cfg2, ReliefF,
+SURF's float64 pass) it must also meet the per-element rtol 1e-5 against
+those sums on every feature with |s| >= 1e-2 max|s|, and miss it on no
+larger a share of the features with |s| >= 1e-3 max|s| than the reference
+arithmetic does.
 """
 import hashlib
 import os
@@ -20,6 +32,7 @@ import numpy as np
 import pytest
 
 from conftest import assert_parity
+from parity_metrics import per_element, summary
 
 pytestmark = pytest.mark.gpu
 
@@ -36,6 +49,24 @@ def _fixture(name):
     if not os.path.exists(path):
         pytest.fail(f"missing fixture {path} (tests/golden/make_fullsize.py)")
     return np.load(path, allow_pickle=False)
+
+
+def _attribute(name, s, ref, per_element_bar):
+    """The attribution check above, when fullsize_{name}_f64.npz exists."""
+    path = os.path.join(GOLD, f"fullsize_{name}_f64.npz")
+    if not os.path.exists(path):
+        return
+    exact = np.load(path, allow_pickle=False)["scores"].astype(np.float64)
+    s, ref = np.asarray(s, np.float64), np.asarray(ref, np.float64)
+    dg, do = np.abs(s - exact), np.abs(ref - exact)
+    msg = (f"GPU vs f64 sums: {summary(s, exact)}; reference arithmetic vs f64 sums: "
+           f"{summary(ref, exact)}")
+    print(msg)
+    assert dg.max() <= do.max(), msg
+    assert np.sqrt((dg ** 2).mean()) <= np.sqrt((do ** 2).mean()), msg
+    if per_element_bar:
+        assert per_element(s, exact, 1e-2, TOL)["over"] == 0.0, msg
+        assert per_element(s, exact, 1e-3, TOL)["over"] <= per_element(ref, exact, 1e-3, TOL)["over"], msg
 
 
 def _data(n, p, red):
@@ -74,6 +105,7 @@ def test_cfg2_multisurf_whole_fit(lib):
     est = lib.MultiSURF(backend="gpu", n_features_to_select=TOPK).fit(X, y)
     assert est.effective_backend_ == "gpu"
     assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
+    _attribute("cfg2_multisurf", est.feature_importances_, fx["scores"], True)
 
 
 def test_cfg3_relieff_k10_whole_fit(lib):
@@ -82,6 +114,7 @@ def test_cfg3_relieff_k10_whole_fit(lib):
     est = lib.ReliefF(backend="gpu", n_neighbors=10, n_features_to_select=TOPK).fit(X, y)
     assert est.effective_backend_ == "gpu"
     assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
+    _attribute("cfg3_relieff_k10", est.feature_importances_, fx["scores"], True)
 
 
 def test_cfg4_multisurf_north_star(lib):
@@ -91,6 +124,9 @@ def test_cfg4_multisurf_north_star(lib):
     X, y = _inputs(fx)
     est = lib.MultiSURF(backend="gpu", n_features_to_select=TOPK).fit(X, y)
     assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
+    # 16-bit pass 1 decides pairs between the quantised and the reference
+    # threshold differently (Numerics): no per-element claim
+    _attribute("cfg4_multisurf", est.feature_importances_, fx["scores"], False)
     assert set(est.top_features_.tolist()) == set(np.argsort(fx["scores"])[::-1][:TOPK].tolist())
 
 
@@ -114,13 +150,21 @@ def test_cfg5_multisurfstar_whole_fit(lib):
     X, y = _inputs(fx)
     est = lib.MultiSURF(backend="gpu", use_star=True, n_features_to_select=TOPK).fit(X, y)
     assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
+    _attribute("cfg5_multisurfstar", est.feature_importances_, fx["scores"], False)
 
 
+@pytest.mark.parametrize("sparse", ["default", "0"])
 @pytest.mark.parametrize("name", ["cfg5_surfstar_slice", "cfg5_surf_slice"])
-def test_cfg5_surf_focal_slice(lib, name):
+def test_cfg5_surf_focal_slice(lib, name, sparse, monkeypatch):
     """SURF / SURF* at 10000 x 50000: the oracle's focal-sample slice
-    (SURF.py:131-195 over i_range) against fs_surf_score_rows."""
+    (SURF.py:131-195 over i_range) against fs_surf_score_rows.  A row slice
+    takes the sparse pass 2; FS_SPARSE=0 forces the dense k_weights ->
+    k_score pass 2 that the whole single-device SURF / SURF* fit
+    (BASELINE configs[4]) takes, so that path is compared with the oracle at
+    size too (VERDICT r2 weak #4)."""
     from fastselect_amd import _lib
+    if sparse != "default":
+        monkeypatch.setenv("FS_SPARSE", sparse)
     from fastselect_amd.SURF import surf_inputs
     fx = _fixture(name)
     X, y = _inputs(fx)
@@ -129,4 +173,6 @@ def test_cfg5_surf_focal_slice(lib, name):
     lo, hi = (int(v) for v in fx["i_range"])
     sums = _lib.surf_score("gpu", x, np.asarray(y).astype(np.int32), recip,
                            bool(fx["use_star"]), isd, rows=(lo, hi))
-    assert_parity((sums / x.shape[0]).astype(np.float32), fx["scores"], TOL)
+    s = (sums / x.shape[0]).astype(np.float32)
+    assert_parity(s, fx["scores"], TOL)
+    _attribute(name, s, fx["scores"], True)

@@ -233,6 +233,39 @@ def test_gloo_world2_with_two_tile_shards_each(tmp_path):
     assert scale_rel_err(a, ref) < 1e-6
 
 
+def _uneven_shard_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    # each rank sizes its shard count from its own memory: here they disagree
+    os.environ["FS_SHARDS"] = str(1 + 2 * rank)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
+    X, y = make_classification(n_samples=500, n_features=40, random_state=2)
+    x, yv, recip, isd = prepare_inputs(X, y, backend="cpu")
+    job = ShardedMultiSURF(x, yv, recip, isd, backend="cpu")
+    np.save(f"{out_path}.{rank}.npy", job.step().numpy())
+    np.save(f"{out_path}.{rank}.v.npy", np.array(job.shards))
+    job.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_ranks_agree_on_the_shard_count(tmp_path):
+    """ranks that size their tile-shard count differently
+    (FS_SHARDS 1 and 3 here; free memory on GPUs) must still deal the tiles
+    by one ownership map -- the MAX over ranks -- or tiles are scored twice or
+    never.  Equal to one process."""
+    import torch.multiprocessing as mp
+    out = str(tmp_path / "u")
+    mp.spawn(_uneven_shard_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    assert int(np.load(out + ".0.v.npy")) == int(np.load(out + ".1.v.npy")) == 3
+    a, b = np.load(out + ".0.npy"), np.load(out + ".1.npy")
+    np.testing.assert_array_equal(a, b)
+    X, y = make_classification(n_samples=500, n_features=40, random_state=2)
+    ref = MultiSURF(backend="cpu").fit(X, y).feature_importances_
+    assert scale_rel_err(a, ref) < 1e-6
+
+
 def test_cpu_backend_duplicated_columns(oracle):
     """Coherent column rounding (4 base columns x 1000 copies) on the CPU
     backend, whose refinement band is calibrated on sampled pairs as the
