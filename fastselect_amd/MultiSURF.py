@@ -38,6 +38,12 @@ class MultiSURF(TransformerMixin, BaseEstimator):
         CPU threads for backend='cpu' (-1 = all).
     verbose : bool, default=False
         Print progress messages.
+    devices : None, int or sequence of int, default=None
+        GPU ordinals the GPU backend scores on, one host thread each (the
+        pair tiles dealt round-robin, the exchange vectors summed on the
+        host).  None: every visible device the job has work for (one per
+        4096 samples).  Not a reference parameter (the reference is
+        single-device); ignored by backend='cpu'.
     """
 
     def __init__(
@@ -48,6 +54,7 @@ class MultiSURF(TransformerMixin, BaseEstimator):
         discrete_limit: int = 10,
         n_jobs: int = -1,
         verbose: bool = False,
+        devices=None,
     ):
         self.n_features_to_select = n_features_to_select
         self.backend = backend
@@ -55,6 +62,7 @@ class MultiSURF(TransformerMixin, BaseEstimator):
         self.discrete_limit = discrete_limit
         self.n_jobs = n_jobs
         self.verbose = verbose
+        self.devices = devices
 
     def _validate_parameters(self, n_samples, n_features):
         return _base.resolve_n_select("MultiSURF", self.backend, self.n_features_to_select,
@@ -63,25 +71,29 @@ class MultiSURF(TransformerMixin, BaseEstimator):
     def fit(self, x: np.ndarray, y: np.ndarray):
         """Score every feature with MultiSURF (or MultiSURF*)."""
         # float64 X: cast, finiteness scan and upload in one native pass
-        x, y, staged = _base.validate_xy_staged(self, x, y, np.float32, self.n_jobs,
-                                                _base.stage_device(self.backend))
+        sd = _base.stage_device(self.backend, self.devices, _base.rows_hint(x))
+        x, y, staged = _base.validate_xy_staged(self, x, y, np.float32, self.n_jobs, sd)
         with _lib.unstaged(staged):
             self.n_features_in_ = x.shape[1]
             n_samples = x.shape[0]
             n_select = self._validate_parameters(n_samples, self.n_features_in_)
             self.effective_backend_ = _base.effective_backend(self.backend)
+            self.devices_ = _base.fit_devices(self.devices, self.effective_backend_, n_samples)
             x = np.ascontiguousarray(x)
-            # one upload of X for the whole fit (already done when staged)
-            with contextlib.nullcontext() if staged else _lib.staged_x(
-                    self.effective_backend_, x):
+            # one upload of X for the whole fit (already done when staged);
+            # a multi-device fit uploads X per device
+            multi = self.devices_ is not None and len(self.devices_) > 1
+            with contextlib.nullcontext() if staged or multi else _lib.staged_x(
+                    self.effective_backend_, x, self.devices_[0] if self.devices_ else 0):
                 scores = self._score(x, y)
         self.feature_importances_ = scores
         self.top_features_ = _base.top_features(scores, n_select)
         return self
 
     def _score(self, x, y):
+        dev0 = self.devices_[0] if self.devices_ else 0
         is_discrete, col_min, col_max = _base.column_preprocess(x, self.discrete_limit,
-                                                                self.effective_backend_)
+                                                                self.effective_backend_, dev0)
         feature_ranges = (col_max - col_min).astype(np.float32)  # _compute_ranges
         feature_ranges[feature_ranges == 0] = 1
         recip_full = (1.0 / feature_ranges).astype(np.float32)
@@ -94,7 +106,7 @@ class MultiSURF(TransformerMixin, BaseEstimator):
             print(f"Running {name} on the {where} now...")
         return _lib.multisurf_score(self.effective_backend_, x, y, recip_full,
                                     all_feature_indices, self.use_star, is_discrete,
-                                    self.n_jobs)
+                                    self.n_jobs, devices=self.devices_)
 
     def _resident_scorer(self, x, y):
         """A scorer for TuRF that keeps X resident (on the GPU for the GPU

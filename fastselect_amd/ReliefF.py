@@ -50,6 +50,12 @@ class ReliefF(TransformerMixin, BaseEstimator):
         Print progress messages.
     n_jobs : int, default=-1
         CPU threads for backend='cpu' (-1 = all).
+    devices : None, int or sequence of int, default=None
+        GPU ordinals the GPU backend scores on, one host thread each (whole
+        128-sample blocks of the focal samples per thread, the score sums
+        added on the host).  None: every visible device the job has work for
+        (one per 4096 samples).  Not a reference parameter; ignored by
+        backend='cpu'.
     """
 
     def __init__(
@@ -60,6 +66,7 @@ class ReliefF(TransformerMixin, BaseEstimator):
         backend: str = "auto",
         verbose: bool = False,
         n_jobs: int = -1,
+        devices=None,
     ):
         self.n_features_to_select = n_features_to_select
         self.discrete_limit = discrete_limit
@@ -67,6 +74,7 @@ class ReliefF(TransformerMixin, BaseEstimator):
         self.backend = backend
         self.verbose = verbose
         self.n_jobs = n_jobs
+        self.devices = devices
 
     def _validate_parameters(self, n_samples, n_features):
         if self.backend not in ["auto", "gpu", "cpu"]:
@@ -105,16 +113,19 @@ class ReliefF(TransformerMixin, BaseEstimator):
         # preprocessing runs where the scoring will (the backend itself is
         # resolved below, after these steps, as in the reference)
         where = "gpu" if self.backend != "cpu" and _lib.gpu_available() else "cpu"
+        sd = _base.stage_device(self.backend, self.devices, n_samples)
         x32, y_enc, recip_full, is_discrete, class_probs = relieff_inputs(
-            x, y, self.discrete_limit, where, n_jobs=self.n_jobs)
+            x, y, self.discrete_limit, where, 0 if sd is None else sd, n_jobs=self.n_jobs)
         self.is_discrete_ = is_discrete
 
         self.effective_backend_ = _base.effective_backend(self.backend)
+        self.devices_ = _base.fit_devices(self.devices, self.effective_backend_, n_samples)
         if self.verbose:
             where = "GPU" if self.effective_backend_ == "gpu" else "CPU"
             print(f"Running ReliefF on the {where} now...")
         scores = _lib.relieff_score(self.effective_backend_, x32, y_enc, recip_full, is_discrete,
-                                    self.n_neighbors, class_probs, self.n_jobs)
+                                    self.n_neighbors, class_probs, self.n_jobs,
+                                    devices=self.devices_)
         self.feature_importances_ = scores
         self.top_features_ = _base.top_features(scores, n_select)
         return self

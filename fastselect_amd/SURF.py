@@ -46,6 +46,12 @@ class SURF(TransformerMixin, BaseEstimator):
         CPU threads for backend='cpu' (-1 = all).
     verbose : bool, default=False
         Print progress messages.
+    devices : None, int or sequence of int, default=None
+        GPU ordinals the GPU backend scores on, one host thread each (whole
+        128-sample blocks of the focal samples per thread, the score sums
+        added on the host).  None: every visible device the job has work for
+        (one per 4096 samples).  Not a reference parameter; ignored by
+        backend='cpu'.
     """
 
     def __init__(
@@ -56,6 +62,7 @@ class SURF(TransformerMixin, BaseEstimator):
         discrete_limit: int = 10,
         n_jobs: int = -1,
         verbose: bool = False,
+        devices=None,
     ):
         self.n_features_to_select = n_features_to_select
         self.backend = backend
@@ -63,6 +70,7 @@ class SURF(TransformerMixin, BaseEstimator):
         self.discrete_limit = discrete_limit
         self.n_jobs = n_jobs
         self.verbose = verbose
+        self.devices = devices
 
     def _validate_parameters(self, n_samples, n_features):
         return _base.resolve_n_select("SURF", self.backend, self.n_features_to_select,
@@ -82,16 +90,21 @@ class SURF(TransformerMixin, BaseEstimator):
         else:
             self.effective_backend_ = self.backend
 
+        self.devices_ = _base.fit_devices(self.devices, self.effective_backend_, n_samples)
+        dev0 = self.devices_[0] if self.devices_ else 0
         X = np.ascontiguousarray(X)
-        with _lib.staged_x(self.effective_backend_, X):  # one upload of X for the whole fit
+        # one upload of X for the whole fit (a multi-device fit uploads per device)
+        multi = self.devices_ is not None and len(self.devices_) > 1
+        with _lib.staged_x("cpu" if multi else self.effective_backend_, X, dev0):
             self.is_discrete_, recip_full = surf_inputs(X, self.discrete_limit,
-                                                        self.effective_backend_)
+                                                        self.effective_backend_, dev0)
 
             algo_name = "SURF*" if self.use_star else "SURF"
             if self.verbose:
                 print(f"Running {algo_name} on the {self.effective_backend_.upper()} now...")
             scores = _lib.surf_score(self.effective_backend_, X, y.astype(np.int32), recip_full,
-                                     self.use_star, self.is_discrete_, self.n_jobs)
+                                     self.use_star, self.is_discrete_, self.n_jobs,
+                                     devices=self.devices_)
         self.feature_importances_ = scores
         self.top_features_ = _base.top_features(scores, n_select)
         if self.verbose:

@@ -63,11 +63,72 @@ def validate_xy(est, x, y, dtype, n_jobs=-1, pinned=False):
     return xv, yv
 
 
-def stage_device(backend: str, device: int = 0):
-    """The device a fit may stage X on while validating it (the estimators'
-    backend 'auto' or 'gpu' with a HIP device visible), else None.  Raises
-    nothing: backend errors keep their place after validation."""
-    return device if backend in ("auto", "gpu") and _lib.gpu_available() else None
+AUTO_ROWS_PER_DEVICE = 4096
+
+
+def _device_list(devices, count: int):
+    """devices as a list of ordinals, or None when it is not a valid value."""
+    if devices is None:
+        return list(range(count))
+    def ordinal(d):
+        return isinstance(d, (int, np.integer)) and not isinstance(d, (bool, np.bool_))
+
+    if ordinal(devices):
+        devs = [int(devices)]
+    elif isinstance(devices, (str, bytes)) or not hasattr(devices, "__iter__"):
+        return None
+    else:
+        devs = list(devices)
+        if not all(ordinal(d) for d in devs):
+            return None
+        devs = [int(d) for d in devs]
+    if not devs or any(d < 0 or d >= count for d in devs):
+        return None
+    return devs
+
+
+def fit_devices(devices, backend: str, n_samples: int):
+    """The GPU ordinals a fit scores on (SURVEY.md §5 "Config / flags", §8(b)
+    "one host thread per device"), or None for backend 'cpu'.
+
+    devices=None: every visible device, as many as the job has work for (one
+    per AUTO_ROWS_PER_DEVICE samples, at least one); an int: that device; a
+    sequence: those ordinals, repeats allowed (several plans share a
+    device).  Raises ValueError for anything else."""
+    if backend != "gpu":
+        return None
+    count = _lib.device_count()
+    devs = _device_list(devices, count)
+    if devs is None:
+        raise ValueError(f"devices must be None, a device ordinal or a non-empty sequence of "
+                         f"ordinals in [0, {count}); got {devices!r}")
+    if devices is None:
+        devs = devs[:max(1, min(len(devs), int(n_samples) // AUTO_ROWS_PER_DEVICE))]
+    return devs
+
+
+def stage_device(backend: str, devices=None, n_samples=None):
+    """The device a fit may stage X on while validating it: the fit's one
+    device when backend is 'auto' or 'gpu', a HIP device is visible and the
+    fit will run on a single device; else None (multi-device fits upload
+    per device).  Raises nothing: backend and device errors keep their place
+    after validation."""
+    if backend not in ("auto", "gpu") or not _lib.gpu_available():
+        return None
+    devs = _device_list(devices, _lib.device_count())
+    if devs is None:
+        return None
+    if devices is None and n_samples is not None:
+        devs = devs[:max(1, min(len(devs), int(n_samples) // AUTO_ROWS_PER_DEVICE))]
+    return devs[0] if len(devs) == 1 else None
+
+
+def rows_hint(x):
+    """Sample count of an array-like before validation (None if unknown)."""
+    try:
+        return int(np.shape(x)[0])
+    except (TypeError, ValueError, IndexError):
+        return None
 
 
 def validate_xy_staged(est, x, y, dtype, n_jobs=-1, device=None):

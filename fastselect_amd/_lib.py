@@ -21,6 +21,11 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfastselect_amd.so")
+# A/B experiments only: FS_LIB_VARIANT=<name> loads a variant build of the
+# same sources (tools/build_variant.sh -> _variants/libfastselect_amd_<name>.so)
+if os.environ.get("FS_LIB_VARIANT"):
+    LIB_PATH = os.path.join(_HERE, "_variants",
+                            f"libfastselect_amd_{os.environ['FS_LIB_VARIANT']}.so")
 
 FS_OK, FS_EINVAL, FS_ENODEV, FS_EOOM, FS_EHIP, FS_ENOTSUP = 0, -1, -2, -3, -4, -5
 BACKEND_CPU, BACKEND_GPU = 0, 1
@@ -44,7 +49,8 @@ EXPORTED = (
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_set_rows",
     "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs", "fs_plan_kernel_ms",
-    "fs_plan_destroy",
+    "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
+    "fs_surf_score_devices",
 )
 
 
@@ -105,6 +111,13 @@ def _load() -> ctypes.CDLL:
                                           _i64, _f32p, _i64, _int, _i64, _i64, _f64p]
     lib.fs_surf_score_rows.argtypes = [_int, _int, _f64p, _i64, _i64, _i32p, _f32p, _int, _u8p,
                                        _int, _i64, _i64, _f64p]
+    _ip = ctypes.POINTER(_int)
+    lib.fs_multisurf_score_devices.argtypes = [_ip, _int, _f32p, _i64, _i64, _f64p, _f32p, _i64p,
+                                               _i64, _int, _u8p, _int, _i64, _i64, _f64p]
+    lib.fs_relieff_score_devices.argtypes = [_ip, _int, _f32p, _i64, _i64, _i32p, _f32p, _u8p,
+                                             _i64, _f32p, _i64, _int, _i64, _i64, _f64p]
+    lib.fs_surf_score_devices.argtypes = [_ip, _int, _f64p, _i64, _i64, _i32p, _f32p, _int, _u8p,
+                                          _int, _i64, _i64, _f64p]
     lib.fs_plan_create.argtypes = [ctypes.POINTER(_vp), _int, _int, _f32p, _i64, _i64, _f64p,
                                    _f32p, _i64p, _i64, _int, _u8p, _int, _int, _int,
                                    ctypes.c_uint64]
@@ -132,7 +145,8 @@ def _load() -> ctypes.CDLL:
                  "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create",
                  "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
                  "fs_plan_pass2", "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs",
-                 "fs_plan_destroy"):
+                 "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
+                 "fs_surf_score_devices"):
         getattr(lib, name).restype = _int
     return lib
 
@@ -324,12 +338,25 @@ def column_stats(backend, x, count_cap, device=0):
     return mn, mx, nd
 
 
+def _devices_arg(devices):
+    d = np.ascontiguousarray(devices, dtype=np.int32)
+    return d, _p(d, ctypes.POINTER(_int)), int(d.size)
+
+
+def _multi(backend, devices):
+    """The *_devices entry point applies: GPU backend and more than one
+    device ordinal (one ordinal is the plain call on that device)."""
+    return backend == "gpu" and devices is not None and len(devices) > 1
+
+
 def multisurf_score(backend, x, y, recip, feat_idx, use_star, is_discrete, n_jobs=-1, device=0,
-                    rows=None):
+                    rows=None, devices=None):
     """Drop-in for ``_multisurf_{cpu,gpu}_host_caller`` (MultiSURF.py:147-162, 256-270).
 
     rows=(begin, end): float64 score sums of those focal samples only
     (``fs_multisurf_score_rows``) instead of float32 scores / n.
+    devices=[d0, d1, ...] (GPU backend): one host thread per entry
+    (``fs_multisurf_score_devices``); one entry = ``device``.
     """
     x = np.ascontiguousarray(x, dtype=np.float32)
     n, p = x.shape
@@ -338,6 +365,18 @@ def multisurf_score(backend, x, y, recip, feat_idx, use_star, is_discrete, n_job
     isd = np.ascontiguousarray(is_discrete, dtype=np.uint8)
     fidx = None if feat_idx is None else np.ascontiguousarray(feat_idx, dtype=np.int64)
     n_kept = p if fidx is None else fidx.size
+    if devices is not None and not _multi(backend, devices):
+        device = int(devices[0])
+    if _multi(backend, devices):
+        _keep, dp, nd = _devices_arg(devices)
+        lo, hi = (0, n) if rows is None else (int(rows[0]), int(rows[1]))
+        sums = np.zeros(n_kept, dtype=np.float64)
+        check(_lib.fs_multisurf_score_devices(dp, nd, _p(x, _f32p), n, p, _p(yv, _f64p),
+                                              _p(rc_, _f32p),
+                                              None if fidx is None else _p(fidx, _i64p), n_kept,
+                                              int(bool(use_star)), _p(isd, _u8p), int(n_jobs),
+                                              lo, hi, _p(sums, _f64p)))
+        return sums if rows is not None else (sums / n).astype(np.float32)
     if rows is not None:
         sums = np.zeros(n_kept, dtype=np.float64)
         check(_lib.fs_multisurf_score_rows(_backend_code(backend), int(device), _p(x, _f32p), n, p,
@@ -356,11 +395,12 @@ def multisurf_score(backend, x, y, recip, feat_idx, use_star, is_discrete, n_job
 
 
 def relieff_score(backend, x, y_enc, recip, is_discrete, k, class_probs, n_jobs=-1, device=0,
-                  rows=None):
+                  rows=None, devices=None):
     """Drop-in for ``_relieff_{cpu,gpu}_host_caller`` (ReliefF.py:127-134, 222-236).
 
     rows=(begin, end): float64 score sums of those focal samples only
     (``fs_relieff_score_rows``, row sharding) instead of float32 scores / n.
+    devices: as ``multisurf_score`` (``fs_relieff_score_devices``).
     """
     x = np.ascontiguousarray(x, dtype=np.float32)
     n, p = x.shape
@@ -368,6 +408,16 @@ def relieff_score(backend, x, y_enc, recip, is_discrete, k, class_probs, n_jobs=
     rc_ = np.ascontiguousarray(recip, dtype=np.float32)
     isd = np.ascontiguousarray(is_discrete, dtype=np.uint8)
     cp = np.ascontiguousarray(class_probs, dtype=np.float32)
+    if devices is not None and not _multi(backend, devices):
+        device = int(devices[0])
+    if _multi(backend, devices):
+        _keep, dp, nd = _devices_arg(devices)
+        lo, hi = (0, n) if rows is None else (int(rows[0]), int(rows[1]))
+        sums = np.zeros(p, dtype=np.float64)
+        check(_lib.fs_relieff_score_devices(dp, nd, _p(x, _f32p), n, p, _p(ye, _i32p),
+                                            _p(rc_, _f32p), _p(isd, _u8p), int(k), _p(cp, _f32p),
+                                            cp.size, int(n_jobs), lo, hi, _p(sums, _f64p)))
+        return sums if rows is not None else (sums / n).astype(np.float32)
     args = (_backend_code(backend), int(device), _p(x, _f32p), n, p, _p(ye, _i32p),
             _p(rc_, _f32p), _p(isd, _u8p), int(k), _p(cp, _f32p), cp.size, int(n_jobs))
     if rows is not None:
@@ -379,17 +429,29 @@ def relieff_score(backend, x, y_enc, recip, is_discrete, k, class_probs, n_jobs=
     return out
 
 
-def surf_score(backend, x, y, recip, use_star, is_discrete, n_jobs=-1, device=0, rows=None):
+def surf_score(backend, x, y, recip, use_star, is_discrete, n_jobs=-1, device=0, rows=None,
+               devices=None):
     """Drop-in for ``_surf_{cpu,gpu}_host_caller`` (SURF.py:117-128, 198-218).
 
     rows=(begin, end): float64 score sums of those focal samples only
     (``fs_surf_score_rows``, row sharding) instead of float32 scores / n.
+    devices: as ``multisurf_score`` (``fs_surf_score_devices``).
     """
     x = np.ascontiguousarray(x, dtype=np.float64)
     n, p = x.shape
     yi = np.ascontiguousarray(y, dtype=np.int32)
     rc_ = np.ascontiguousarray(recip, dtype=np.float32)
     isd = np.ascontiguousarray(is_discrete, dtype=np.uint8)
+    if devices is not None and not _multi(backend, devices):
+        device = int(devices[0])
+    if _multi(backend, devices):
+        _keep, dp, nd = _devices_arg(devices)
+        lo, hi = (0, n) if rows is None else (int(rows[0]), int(rows[1]))
+        sums = np.zeros(p, dtype=np.float64)
+        check(_lib.fs_surf_score_devices(dp, nd, _p(x, _f64p), n, p, _p(yi, _i32p),
+                                         _p(rc_, _f32p), int(bool(use_star)), _p(isd, _u8p),
+                                         int(n_jobs), lo, hi, _p(sums, _f64p)))
+        return sums if rows is not None else (sums / n).astype(np.float32)
     args = (_backend_code(backend), int(device), _p(x, _f64p), n, p, _p(yi, _i32p),
             _p(rc_, _f32p), int(bool(use_star)), _p(isd, _u8p), int(n_jobs))
     if rows is not None:

@@ -56,6 +56,27 @@ static int check_backend(int backend, int device) {
   return FS_OK;
 }
 
+// devices[0..n) for the multi-device entry points: at least one, each a
+// visible HIP ordinal (repeats allowed: several plans share a device).
+static int check_devices(const int* devices, int n) {
+  if (!devices || n < 1) {
+    set_error("devices: need at least one device ordinal");
+    return FS_EINVAL;
+  }
+  const int nd = gpu::device_count();
+  if (nd <= 0) {
+    set_error("backend='gpu' was selected, but no HIP device (MI355X) is visible");
+    return FS_ENODEV;
+  }
+  for (int i = 0; i < n; i++)
+    if (devices[i] < 0 || devices[i] >= nd) {
+      set_error("devices: ordinal " + std::to_string(devices[i]) + " out of range (" +
+                std::to_string(nd) + " visible)");
+      return FS_EINVAL;
+    }
+  return FS_OK;
+}
+
 extern "C" {
 
 const char* fs_version(void) { return "fastselect_amd 0.1.0 (gfx950)"; }
@@ -216,7 +237,8 @@ int fs_multisurf_score_rows(int backend, int device, const float* x, int64_t n, 
 static int relieff_sums(int backend, int device, const float* x, int64_t n, int64_t p,
                         const int32_t* y_enc, const float* recip, const uint8_t* is_discrete,
                         int64_t k, const float* class_probs, int64_t n_classes, int n_jobs,
-                        int64_t r_lo, int64_t r_hi, double* sums) {
+                        int64_t r_lo, int64_t r_hi, double* sums, const int* devices = nullptr,
+                        int n_devices = 0) {
   if (!y_enc || !class_probs || n_classes < 1 || k < 0) {
     set_error("invalid ReliefF arguments (y_enc, class_probs, n_classes, k)");
     return FS_EINVAL;
@@ -243,6 +265,13 @@ static int relieff_sums(int backend, int device, const float* x, int64_t n, int6
   P.class_prior.assign(n_classes, 0.0);
   for (int64_t c = 0; c < n_classes; c++) P.class_prior[c] = (double)class_probs[c];
   P.k_neighbors = k;
+  if (devices) {
+    if (n_classes > 64) {
+      set_error("GPU ReliefF supports at most 64 classes");
+      return FS_ENOTSUP;
+    }
+    return gpu::rows_run_devices(P, x, devices, n_devices, r_lo, r_hi, sums);
+  }
   if (backend == FS_BACKEND_GPU) return gpu::relieff_run(P, x, device, r_lo, r_hi, sums);
   return cpu::relieff_run(P, x, n_jobs, r_lo, r_hi, sums);
 }
@@ -250,7 +279,7 @@ static int relieff_sums(int backend, int device, const float* x, int64_t n, int6
 static int surf_sums(int backend, int device, const double* x, int64_t n, int64_t p,
                      const int32_t* y, const float* recip, int use_star,
                      const uint8_t* is_discrete, int n_jobs, int64_t r_lo, int64_t r_hi,
-                     double* sums) {
+                     double* sums, const int* devices = nullptr, int n_devices = 0) {
   if (!(0 <= r_lo && r_lo <= r_hi && r_hi <= n)) {
     set_error("row range must satisfy 0 <= row_begin <= row_end <= n");
     return FS_EINVAL;
@@ -265,6 +294,7 @@ static int surf_sums(int backend, int device, const double* x, int64_t n, int64_
   if (rc) return map_prep_rc(rc);
   if (encode_labels_i32(P, y)) return FS_EINVAL;
   P.use_star = use_star ? 1 : 0;
+  if (devices) return gpu::rows_run_devices(P, x, devices, n_devices, r_lo, r_hi, sums);
   if (backend == FS_BACKEND_GPU) return gpu::surf_run(P, x, device, r_lo, r_hi, sums);
   return cpu::surf_run(P, x, n_jobs, r_lo, r_hi, sums);
 }
@@ -322,6 +352,59 @@ int fs_surf_score_rows(int backend, int device, const double* x, int64_t n, int6
   }
   return surf_sums(backend, device, x, n, p, y, recip, use_star, is_discrete, n_jobs, row_begin,
                    row_end, sums_out);
+}
+
+int fs_multisurf_score_devices(const int* devices, int n_devices, const float* x, int64_t n,
+                               int64_t p, const double* y, const float* recip,
+                               const int64_t* feat_idx, int64_t n_kept, int use_star,
+                               const uint8_t* is_discrete, int n_jobs, int64_t row_begin,
+                               int64_t row_end, double* sums_out) {
+  if (!sums_out) {
+    set_error("sums_out is NULL");
+    return FS_EINVAL;
+  }
+  if (!(0 <= row_begin && row_begin <= row_end && row_end <= n)) {
+    set_error("row range must satisfy 0 <= row_begin <= row_end <= n");
+    return FS_EINVAL;
+  }
+  int rc = check_devices(devices, n_devices);
+  if (rc != FS_OK) return rc;
+  Prepared P;
+  rc = prepare(P, ALGO_MULTISURF, x, 0, n, p, feat_idx, n_kept, recip, is_discrete, n_jobs, true);
+  if (rc) return map_prep_rc(rc);
+  if (encode_labels_f64(P, y)) return FS_EINVAL;
+  P.use_star = use_star ? 1 : 0;
+  return gpu::multisurf_run_devices(P, x, devices, n_devices, row_begin, row_end, sums_out);
+}
+
+int fs_relieff_score_devices(const int* devices, int n_devices, const float* x, int64_t n,
+                             int64_t p, const int32_t* y_enc, const float* recip,
+                             const uint8_t* is_discrete, int64_t k, const float* class_probs,
+                             int64_t n_classes, int n_jobs, int64_t row_begin, int64_t row_end,
+                             double* sums_out) {
+  if (!sums_out) {
+    set_error("sums_out is NULL");
+    return FS_EINVAL;
+  }
+  const int rc = check_devices(devices, n_devices);
+  if (rc != FS_OK) return rc;
+  return relieff_sums(FS_BACKEND_GPU, devices[0], x, n, p, y_enc, recip, is_discrete, k,
+                      class_probs, n_classes, n_jobs, row_begin, row_end, sums_out, devices,
+                      n_devices);
+}
+
+int fs_surf_score_devices(const int* devices, int n_devices, const double* x, int64_t n,
+                          int64_t p, const int32_t* y, const float* recip, int use_star,
+                          const uint8_t* is_discrete, int n_jobs, int64_t row_begin,
+                          int64_t row_end, double* sums_out) {
+  if (!sums_out) {
+    set_error("sums_out is NULL");
+    return FS_EINVAL;
+  }
+  const int rc = check_devices(devices, n_devices);
+  if (rc != FS_OK) return rc;
+  return surf_sums(FS_BACKEND_GPU, devices[0], x, n, p, y, recip, use_star, is_discrete, n_jobs,
+                   row_begin, row_end, sums_out, devices, n_devices);
 }
 
 }  // extern "C"

@@ -1515,6 +1515,225 @@ __global__ __launch_bounds__(1024) void k_score_sparse(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Pass 2, sparse v2: 64-row half tiles, 8 features per lane
+// ---------------------------------------------------------------------------
+// The v1 streams above hold a whole 128-row tile per wave, so a workgroup
+// keeps 128 rows x 256 features (128 KB) in LDS and every entry feeds 4
+// features per lane: the entry streams are re-read once per 256-feature block
+// (79 times at cfg4) and each scalar load of 8 entries covers 8 x 9 VALU.
+// v2 splits each tile into its two 64-row halves: a workgroup keeps 64 rows x
+// 512 features (the same 128 KB) and every entry feeds 8 features per lane --
+// one v_add_u32 address, two ds_read_b128, 8 x (v_sub_f32, v_fma_f32 |.|): 17
+// VALU per 8 pair-features instead of 18, half the scalar loads and half the
+// entry-stream reads per pair-feature (40 feature blocks at cfg4), and twice
+// the arithmetic behind every scalar load.  The B rows (the tile's columns)
+// are read once per half instead of once per tile; the two halves of a
+// (segment, feature block) sit in adjacent grid slots of one XCD, so the
+// second read is mostly an L2 hit.
+//
+// Stream (t, h, w) (k_weights_sparse2): the columns jj = w, w + 16, ... (8)
+// of owned tile t, each column's non-zero weights of the rows ii in
+// [64h, 64h + 64) as entries ((ii - 64h) * 2048, weight) in ascending ii --
+// 2048 = the byte stride of a row in the LDS block -- with NO padding: the
+// lowest mantissa bit of a weight is set on the last entry of its column and
+// clear elsewhere (a <= 1-ulp change, far below the 1e-5 bar), and an empty
+// column holds one (0, 0x1) entry (a denormal weight, zero for every
+// purpose).  Stream (t, h, w) starts at ent + ((t * 2 + h) * 16 + w) *
+// kStreamEntries2; 8 columns x 64 rows fill it at most.
+constexpr int kHalf = 64;
+constexpr int kRowBytes2 = 2048;                           // 64 lanes x 8 floats
+// Entries of a column padded with zero weights to a multiple of kGroup2
+// (the generated loop then tests the column-end flag once per group; A/B
+// builds set FS_V2_GROUP, tools/build_variant.sh)
+#ifndef FS_V2_GROUP
+#define FS_V2_GROUP 1
+#endif
+constexpr int kGroup2 = FS_V2_GROUP;
+static_assert(kHalf % kGroup2 == 0, "a full column must need no padding");
+constexpr int kStreamEntries2 = (kTile / kSWaves) * kHalf;  // 512
+static_assert(kStreamEntries2 * 2 == kStreamEntries, "v2 streams reuse the v1 buffer size");
+
+__global__ __launch_bounds__(1024) void k_weights_sparse2(
+    const double* __restrict__ D, int64_t n, int64_t n_pad, int tiled,
+    const int2* __restrict__ tiles, const double* __restrict__ thr,
+    const int32_t* __restrict__ lab,
+    const double* __restrict__ counts, int algo, int use_star, double inv_sc, int64_t r_lo,
+    int64_t r_hi, uint2* __restrict__ ent, unsigned long long* __restrict__ nnz) {
+  __shared__ int wave_nnz[kSWaves];
+  const int2 tl = tiles[blockIdx.x];
+  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint2* out0 = ent + (((int64_t)blockIdx.x * 2 + 0) * kSWaves + wave) * kStreamEntries2;
+  uint2* out1 = ent + (((int64_t)blockIdx.x * 2 + 1) * kSWaves + wave) * kStreamEntries2;
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint32_t roff = (uint32_t)lane * (uint32_t)kRowBytes2;
+  int off0 = 0, off1 = 0, nz = 0;
+  for (int jj = wave; jj < kTile; jj += kSWaves) {
+    const float w0 = pair_weight(D, n, n_pad, tiled, blockIdx.x, i0, j0, lane, jj,
+                                 tl.x < tl.y || lane < jj, thr, lab, counts, algo, use_star,
+                                 inv_sc, r_lo, r_hi);
+    const float w1 = pair_weight(D, n, n_pad, tiled, blockIdx.x, i0, j0, lane + 64, jj,
+                                 tl.x < tl.y || lane + 64 < jj, thr, lab, counts, algo, use_star,
+                                 inv_sc, r_lo, r_hi);
+    const uint64_t m0 = __ballot(w0 != 0.0f), m1 = __ballot(w1 != 0.0f);
+    const int n0 = __popcll(m0), n1 = __popcll(m1);
+    // padded lengths (at least one entry: an empty column still ends)
+    const int p0 = n0 == 0 ? kGroup2 : (n0 + kGroup2 - 1) / kGroup2 * kGroup2;
+    const int p1 = n1 == 0 ? kGroup2 : (n1 + kGroup2 - 1) / kGroup2 * kGroup2;
+    const int e0 = __popcll(m0 & below), e1 = __popcll(m1 & below);
+    if (w0 != 0.0f) out0[off0 + e0] = make_uint2(roff, weight_bits(w0, e0 == p0 - 1));
+    if (w1 != 0.0f) out1[off1 + e1] = make_uint2(roff, weight_bits(w1, e1 == p1 - 1));
+    if (n0 + lane < p0) out0[off0 + n0 + lane] = make_uint2(0u, n0 + lane == p0 - 1 ? 1u : 0u);
+    if (n1 + lane < p1) out1[off1 + n1 + lane] = make_uint2(0u, n1 + lane == p1 - 1 ? 1u : 0u);
+    off0 += p0;
+    off1 += p1;
+    nz += n0 + n1;
+  }
+  if (lane == 0) wave_nnz[wave] = nz;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long t = 0;
+    for (int w = 0; w < kSWaves; w++) t += (unsigned long long)wave_nnz[w];
+    atomicAdd(nnz, t);
+  }
+}
+
+// Generic (plain HIP) walk of one v2 stream: F features per lane (8: chunks
+// c = 0, 1 of the row, 4 each; 4: chunk 0 only), per-lane discrete flags.
+// Used for feature blocks holding discrete features; continuous blocks take
+// the generated loop of fs_sparse_asm.inc.
+template <int F>
+__device__ __forceinline__ void sparse2_stream_generic(const float4* __restrict__ As,
+                                                       const uint2* __restrict__ e,
+                                                       const float* __restrict__ xb, int64_t bstride,
+                                                       int lane, const bool (&disc)[F],
+                                                       float (&acc)[F]) {
+  constexpr int C = F / 4;
+  float b[F];
+  int col = 0;
+#pragma unroll
+  for (int c = 0; c < C; c++) {
+    const float4 v = *(const float4*)(xb + 256 * c);
+    b[4 * c] = v.x; b[4 * c + 1] = v.y; b[4 * c + 2] = v.z; b[4 * c + 3] = v.w;
+  }
+  for (int q = 0; q < kStreamEntries2; q++) {
+    const uint2 E = e[q];
+    const float w = __uint_as_float(E.y);
+#pragma unroll
+    for (int c = 0; c < C; c++) {
+      const float4 a = As[(E.x >> 4) + 64 * c + lane];
+      const float av[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const int f = 4 * c + k;
+        acc[f] = disc[f] ? pair_term<true>(av[k], b[f], w, acc[f])
+                         : pair_term<false>(av[k], b[f], w, acc[f]);
+      }
+    }
+    if (E.y & 1u) {  // last entry of the column
+      if (++col == kTile / kSWaves) break;
+      xb += bstride;
+#pragma unroll
+      for (int c = 0; c < C; c++) {
+        const float4 v = *(const float4*)(xb + 256 * c);
+        b[4 * c] = v.x; b[4 * c + 1] = v.y; b[4 * c + 2] = v.z; b[4 * c + 3] = v.w;
+      }
+    }
+  }
+}
+
+// Grid: XCD-aware as k_score_sparse, the slots of a segment ordered
+// (feature block, half) so that the two halves of one block are neighbours.
+// F = 8: 512-feature blocks f_base + 512 fb; F = 4: 256-feature blocks (the
+// tail of a layout whose width is not a multiple of 512).  Lane l scores
+// features f0 + 4l + k and (F = 8) f0 + 256 + 4l + k, k = 0..3; partials go
+// to spart[(seg * 2 + h) * PW + f].
+template <int F>
+__global__ __launch_bounds__(1024) void k_score_sparse2(
+    const float* __restrict__ xs, int64_t PW, int64_t PC, const int2* __restrict__ tiles,
+    const uint2* __restrict__ ent, int64_t n_tiles, int64_t seg_len, int64_t nseg, int64_t nfb,
+    int64_t f_base, int use_asm, double* __restrict__ spart) {
+  constexpr int C = F / 4;
+  __shared__ float4 As[kHalf * 2 * 64];  // 64 rows x 2 chunks x 64 lanes (128 KB)
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t wg = blockIdx.x;
+  const int64_t xcd = wg % kXcds, k = wg / kXcds;
+  const int64_t seg = xcd + kXcds * (k / (2 * nfb)), r2 = k % (2 * nfb);
+  if (seg >= nseg) return;
+  const int64_t fb = r2 >> 1, h = r2 & 1;
+  const int64_t f0 = f_base + fb * (64 * F);
+  const int64_t t_begin = seg * seg_len;
+  const int64_t t_end = t_begin + seg_len < n_tiles ? t_begin + seg_len : n_tiles;
+  bool disc[F];
+#pragma unroll
+  for (int c = 0; c < C; c++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) disc[4 * c + q] = f0 + 256 * c + 4 * lane + q >= PC;
+  // the generated loop when every real feature of the block is continuous;
+  // features past PW stage zeros and their accumulators are discarded (their
+  // B values are read past the row's end: xs has kXsSlack floats of slack)
+  const int64_t f_end = f0 + 64 * F < PW ? f0 + 64 * F : PW;
+  const bool fast = use_asm && f_end <= PC;
+  const uint32_t lds_lane = (uint32_t)(uintptr_t)As + (uint32_t)lane * 16u;
+  const uint32_t glb_lane = (uint32_t)lane * 16u;
+  const int64_t bstride = kSWaves * PW;
+  const uint32_t bstride_b = (uint32_t)(bstride * sizeof(float));
+  const uint32_t ncols = kTile / kSWaves;
+  double s[F];
+#pragma unroll
+  for (int q = 0; q < F; q++) s[q] = 0.0;
+  int cur_bi = -1;
+  for (int64_t t = t_begin; t < t_end; t++) {
+    const int2 tl = tiles[t];
+    if (tl.x != cur_bi) {
+      __syncthreads();
+      const float* __restrict__ xa = xs + ((int64_t)tl.x * kTile + h * kHalf) * PW + f0 + 4 * lane;
+      for (int rc = wave; rc < kHalf * 2; rc += kSWaves) {
+        const int r = rc >> 1, c = rc & 1;
+        float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (c < C && f0 + 256 * c + 4 * lane < PW) v = *(const float4*)(xa + (int64_t)r * PW + 256 * c);
+        As[rc * 64 + lane] = v;
+      }
+      __syncthreads();
+      cur_bi = tl.x;
+    }
+    float acc[F];
+#pragma unroll
+    for (int q = 0; q < F; q++) acc[q] = 0.0f;
+    const uint2* __restrict__ e = ent + ((t * 2 + h) * kSWaves + wave) * kStreamEntries2;
+    const float* __restrict__ xb = xs + ((int64_t)tl.y * kTile + wave) * PW + f0;
+    if (fast) {
+      const uint64_t eb = (uint64_t)(uintptr_t)e, bp = (uint64_t)(uintptr_t)xb;
+      if constexpr (F == 8)
+        FS_SPARSE2_ASM_F8(acc, lds_lane, glb_lane, eb, bp, bstride_b, ncols);
+      else
+        FS_SPARSE2_ASM_F4(acc, lds_lane, glb_lane, eb, bp, bstride_b, ncols);
+    } else {
+      sparse2_stream_generic<F>(As, e, xb + 4 * lane, bstride, lane, disc, acc);
+    }
+#pragma unroll
+    for (int q = 0; q < F; q++) s[q] += (double)acc[q];
+  }
+  // fixed-order reduction of the 16 waves' partials through the LDS block
+  __syncthreads();
+  double* red = (double*)As;  // [F][kSWaves][64] (64 KB at F = 8)
+#pragma unroll
+  for (int q = 0; q < F; q++) red[(q * kSWaves + wave) * 64 + lane] = s[q];
+  __syncthreads();
+  if (wave < F) {
+    const int q = wave;                                  // feature f0 + 256 (q/4) + 4 lane + q%4
+    const int64_t f = f0 + 256 * (q >> 2) + 4 * lane + (q & 3);
+    const double* rr = red + q * kSWaves * 64 + lane;
+    double v = 0.0;
+#pragma unroll
+    for (int w = 0; w < kSWaves; w += 4)
+      v += (rr[w * 64] + rr[(w + 1) * 64]) + (rr[(w + 2) * 64] + rr[(w + 3) * 64]);
+    if (f < PW) spart[(seg * 2 + h) * PW + f] = v;
+  }
+}
+
 // dst[k] += src[k] (the tile shards' partial vectors, summed in shard order).
 __global__ void k_accumulate(double* __restrict__ dst, const double* __restrict__ src,
                              int64_t count) {
@@ -2083,6 +2302,7 @@ struct Plan {
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int64_t nb = 0, n_tiles = 0, seg_len = 1, nseg = 1;
+  int64_t nsegpart = 1;         // rows of spart (nseg, or 2 * nseg for the v2 sparse pass)
   int ksplit = 1;               // pass-1 K-split parts of the tail tiles (k_dist)
   int64_t kfull = 0;            // tiles k_dist computes whole (the rest are split)
   int use_q16 = 0;              // pass 1 on packed 16-bit continuous operands
@@ -2118,6 +2338,7 @@ struct Plan {
   unsigned long long* nnz = nullptr;  // non-zero weights of the last pass 2
   bool nnz_valid = false;
   int sparse = 0;               // pass 2 over non-zero weights only
+  int sparse_v = 2;             // sparse stream layout: 2 = half tiles x 8 features (v1: A/B)
   double* spart = nullptr;       // pass-2 segment partials (own block, shard_segments)
   size_t spart_cap = 0;           // doubles of spart
   // ambiguous-pair refinement
@@ -2787,14 +3008,19 @@ static int shard_segments(Plan* g) {
   // (tile, block) units as the target, at least 4096: segments of ~4 tiles
   // amortise each workgroup's row-block stage (tools/cfg2_sweep.sh,
   // profiles/r02/cfg2_sweep.txt: cfg2 step 6.11 -> 5.83 ms at 4096-8192).
-  const int64_t nfb = g->sparse ? (Q.PW + 255) / 256 : (Q.PW + 127) / 128;
+  // v2 sparse: (512-feature block, half) units, two per 512 features
+  const int64_t nfb = !g->sparse       ? (Q.PW + 127) / 128
+                      : g->sparse_v == 1 ? (Q.PW + 255) / 256
+                                         : 2 * ((Q.PW + 511) / 512);
   int64_t wgs = g->sparse ? std::min<int64_t>(32768, std::max<int64_t>(4096, g->n_tiles * nfb / 4))
                           : 65536;
   if (const char* e = std::getenv("FS_PASS2_WGS")) wgs = std::max<int64_t>(256, std::atoll(e));
   g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + wgs - 1) / wgs);
   g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
+  // partial rows per segment: one per half with the v2 streams
+  g->nsegpart = (g->sparse && g->sparse_v == 2) ? 2 * g->nseg : g->nseg;
   if (Q.algo == ALGO_RELIEFF) return FS_OK;
-  const size_t need = (size_t)g->nseg * Q.PW;
+  const size_t need = (size_t)g->nsegpart * Q.PW;
   if (need > g->spart_cap) {
     if (g->spart) {
       FS_HIP(hipStreamSynchronize(g->stream));
@@ -3043,6 +3269,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       (rc = dalloc(g, &g->list, g->list_cap)) || (rc = dalloc(g, &g->list_count, 1)))
     return fail(rc);
   g->sparse = choose_sparse(g, Q);
+  if (const char* e = std::getenv("FS_SPARSE_V")) g->sparse_v = std::atoi(e) == 1 ? 1 : 2;
   if ((rc = setup_shard(g, bi, bj))) return fail(rc);
   trace_mark("plan: hipMalloc");
   std::vector<int32_t> lab(Q.n_pad, -1);
@@ -3204,6 +3431,12 @@ static int run_weights(Plan* g, const double* counts, int algo, double inv_sc) {
   if (g->sparse) {
     FS_HIP(hipMemsetAsync(g->nnz, 0, sizeof(unsigned long long), g->stream));
     g->nnz_valid = true;
+    if (g->sparse_v == 2) {
+      k_weights_sparse2<<<(unsigned)g->n_tiles, 64 * kSWaves, 0, g->stream>>>(
+          g->D, Q.n, Q.n_pad, g->tiled, g->tiles, g->thr, g->lab, counts, algo, Q.use_star,
+          inv_sc, g->r_lo, g->r_hi, g->ent, g->nnz);
+      return launch_check("k_weights_sparse2");
+    }
     k_weights_sparse<<<(unsigned)g->n_tiles, 64 * kSWaves, 0, g->stream>>>(
         g->D, Q.n, Q.n_pad, g->tiled, g->tiles, g->thr, g->lab, counts, algo, Q.use_star, inv_sc,
         g->r_lo, g->r_hi, g->ent, g->nnz);
@@ -3231,6 +3464,17 @@ static int sparse_jit() {
   return v;
 }
 
+// The generated loop of k_score_sparse2 for continuous feature blocks (1,
+// default) or the plain-HIP walk for every block (0: FS_SPARSE_ASM=0, A/B).
+static int sparse_asm() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = std::getenv("FS_SPARSE_ASM");
+    v = (e && *e) ? (std::atoi(e) != 0) : 1;
+  }
+  return v;
+}
+
 static int run_pass2(Plan* g, double* scores_dev) {
   const Prepared& Q = g->P;
   const int64_t nfb = (Q.PW + 127) / 128;
@@ -3238,7 +3482,24 @@ static int run_pass2(Plan* g, double* scores_dev) {
   if (g->n_tiles == 0) return FS_OK;
   FS_HIP(hipEventRecord(g->ev[2], g->stream));
   const int64_t seg_per_xcd = (g->nseg + kXcds - 1) / kXcds;
-  if (g->sparse) {
+  if (g->sparse && g->sparse_v == 2) {
+    // 512-feature blocks, then the tail of the layout in 256-feature blocks
+    const int64_t nfb8 = Q.PW / 512, f_tail = nfb8 * 512;
+    const int64_t nfb4 = (Q.PW - f_tail + 255) / 256;
+    const int use_asm = sparse_asm();
+    if (nfb8 > 0) {
+      k_score_sparse2<8><<<(unsigned)(kXcds * seg_per_xcd * 2 * nfb8), 64 * kSWaves, 0,
+                           g->stream>>>(g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->n_tiles,
+                                        g->seg_len, g->nseg, nfb8, 0, use_asm, g->spart);
+      FS_TRY(launch_check("k_score_sparse2<8>"));
+    }
+    if (nfb4 > 0) {
+      k_score_sparse2<4><<<(unsigned)(kXcds * seg_per_xcd * 2 * nfb4), 64 * kSWaves, 0,
+                           g->stream>>>(g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->n_tiles,
+                                        g->seg_len, g->nseg, nfb4, f_tail, use_asm, g->spart);
+      FS_TRY(launch_check("k_score_sparse2<4>"));
+    }
+  } else if (g->sparse) {
     const int64_t nfb4 = (Q.PW + 255) / 256;
     k_score_sparse<<<(unsigned)(kXcds * seg_per_xcd * nfb4), 64 * kSWaves, 0, g->stream>>>(
         g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->n_tiles, g->seg_len, g->nseg, nfb4, sparse_jit(),
@@ -3250,7 +3511,7 @@ static int run_pass2(Plan* g, double* scores_dev) {
     FS_TRY(launch_check("k_score"));
   }
   FS_HIP(hipEventRecord(g->ev[3], g->stream));
-  k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(g->spart, g->nseg, Q.PW,
+  k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(g->spart, g->nsegpart, Q.PW,
                                                                    g->out_pos, scores_dev);
   return launch_check("k_reduce");
 }
@@ -3695,6 +3956,191 @@ int plan_score(Plan* g, double* sums_dev) {
   for (void* q : g->scratch) dev_free(q);
   g->scratch.clear();
   return rc;
+}
+
+}  // namespace gpu
+}  // namespace fs
+
+// ---------------------------------------------------------------------------
+// Single-process multi-GPU (the estimators' `devices=`)
+// ---------------------------------------------------------------------------
+namespace fs {
+namespace gpu {
+
+namespace {
+// Barrier of the device threads that also agrees on failure: every thread
+// hands in its status; when one failed, all of them return after the barrier
+// instead of waiting for a peer that will never arrive at the next one.
+class StageBarrier {
+ public:
+  explicit StageBarrier(int n) : n_(n) {}
+  bool arrive(int rc, const std::string& err) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (rc != FS_OK && rc_ == FS_OK) {
+      rc_ = rc;
+      err_ = err;
+    }
+    const uint64_t gen = gen_;
+    if (++count_ == n_) {
+      count_ = 0;
+      gen_++;
+      cv_.notify_all();
+    } else {
+      cv_.wait(lk, [&] { return gen_ != gen; });
+    }
+    return rc_ == FS_OK;
+  }
+  int rc() const { return rc_; }
+  const std::string& err() const { return err_; }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int n_, count_ = 0, rc_ = FS_OK;
+  uint64_t gen_ = 0;
+  std::string err_;
+};
+
+// rank-order sum of the ranks' host vectors (the same order on every
+// thread, so every device gets bit-identical vectors)
+void rank_sum(const std::vector<std::vector<double>>& parts, std::vector<double>& out) {
+  const size_t len = parts[0].size();
+  out.assign(len, 0.0);
+  for (const auto& v : parts)
+    for (size_t k = 0; k < len; k++) out[k] += v[k];
+}
+}  // namespace
+
+// MultiSURF over several devices from one process: thread r (devices[r],
+// repeats allowed) owns the tiles t with t % (N V) == r + N v of the
+// upper triangle -- the partition of parallel.py's one-process-per-GPU path
+// -- and the three exchange vectors (row moments, neighbour counts, score
+// sums) are copied to the host after each stage and summed in rank order,
+// where the multi-process path all-reduces them over RCCL.  V > 1 tile
+// shards per device when the largest share exceeds a device's memory.
+// Focal samples [r_lo, r_hi) as fs_multisurf_score_rows; sums (not / n).
+int multisurf_run_devices(const Prepared& P, const void* x, const int* devices, int ndev,
+                          int64_t r_lo, int64_t r_hi, double* sums_out) {
+  const int N = ndev;
+  int V = 1;
+  for (int r = 0; r < N; r++) V = std::max(V, multisurf_shards(P, devices[r], N));
+  const int W = N * V;
+  const int64_t n = P.n, nk = P.n_kept;
+  StageBarrier bar(N);
+  std::vector<std::vector<double>> h_rs(N, std::vector<double>(3 * n)),
+      h_cnt(N, std::vector<double>(2 * n)), h_sc(N, std::vector<double>(nk));
+  std::vector<double> result;
+  auto worker = [&](int r) {
+    Plan* g = nullptr;
+    double *rs = nullptr, *cnt = nullptr, *sc = nullptr, *tmp = nullptr;
+    std::vector<double> sum;
+    auto fail_out = [&](int rc) {
+      bar.arrive(rc, rc ? std::string(fs_last_error()) : std::string());
+      return rc;
+    };
+    int rc = plan_create(&g, P, x, 0, devices[r], r, W, 0);
+    if (!rc) rc = plan_set_rows(g, r_lo, r_hi);
+    if (!rc && ((rc = dalloc(g, &rs, 3 * n)) || (rc = dalloc(g, &cnt, 2 * n)) ||
+                (rc = dalloc(g, &sc, nk)) || (rc = dalloc(g, &tmp, std::max<int64_t>(3 * n, nk)))))
+      ;
+    // device vector -> host part r; barrier; rank-order sum -> device
+    auto exchange = [&](double* dev, int64_t len, std::vector<std::vector<double>>& parts) -> bool {
+      int e = rc;
+      if (!e && (hipMemcpyAsync(parts[r].data(), dev, sizeof(double) * len, hipMemcpyDeviceToHost,
+                                g->stream) != hipSuccess ||
+                 hipStreamSynchronize(g->stream) != hipSuccess)) {
+        set_error("multi-device exchange: device-to-host copy failed");
+        e = FS_EHIP;
+      }
+      if (!bar.arrive(e, e ? std::string(fs_last_error()) : std::string())) return false;
+      rank_sum(parts, sum);
+      if (hipMemcpyAsync(dev, sum.data(), sizeof(double) * len, hipMemcpyHostToDevice,
+                         g->stream) != hipSuccess) {
+        rc = FS_EHIP;
+        set_error("multi-device exchange: host-to-device copy failed");
+      }
+      return true;
+    };
+    auto acc = [&](double* dst, const double* src, int64_t len, bool first) -> int {
+      if (first)
+        return hipMemcpyAsync(dst, src, sizeof(double) * len, hipMemcpyDeviceToDevice,
+                              g->stream) == hipSuccess ? FS_OK : FS_EHIP;
+      k_accumulate<<<(unsigned)((len + 255) / 256), 256, 0, g->stream>>>(dst, src, len);
+      return launch_check("k_accumulate");
+    };
+    bool ok = true;
+    if (V == 1) {
+      if (!rc) rc = plan_pass1(g, rs);
+      ok = exchange(rs, 3 * n, h_rs);
+      if (ok && !rc) rc = plan_select(g, rs, cnt);
+      ok = ok && exchange(cnt, 2 * n, h_cnt);
+      if (ok && !rc) rc = plan_pass2(g, cnt, sc);
+      ok = ok && exchange(sc, nk, h_sc);
+    } else {
+      for (int round = 0; round < 3 && ok; round++) {
+        for (int v = 0; v < V && !rc; v++) {
+          if ((rc = plan_set_shard(g, r + N * v, W))) break;
+          if ((rc = plan_pass1(g, tmp))) break;
+          if (round == 0) { rc = acc(rs, tmp, 3 * n, v == 0); continue; }
+          if ((rc = plan_select(g, rs, tmp))) break;
+          if (round == 1) { rc = acc(cnt, tmp, 2 * n, v == 0); continue; }
+          if ((rc = plan_pass2(g, cnt, tmp))) break;
+          rc = acc(sc, tmp, nk, v == 0);
+        }
+        ok = exchange(round == 0 ? rs : round == 1 ? cnt : sc, round == 0 ? 3 * n : round == 1 ? 2 * n : nk,
+                      round == 0 ? h_rs : round == 1 ? h_cnt : h_sc);
+      }
+    }
+    if (ok && !rc && r == 0) result = sum;  // every thread holds the same sums
+    if (g) plan_destroy(g);
+    if (ok) fail_out(rc);  // final agreement: a late failure fails the call
+    return rc;
+  };
+  std::vector<std::thread> th;
+  for (int r = 1; r < N; r++) th.emplace_back(worker, r);
+  worker(0);
+  for (auto& t : th) t.join();
+  if (bar.rc() != FS_OK) {
+    set_error(bar.err().empty() ? std::string("multi-device MultiSURF failed") : bar.err());
+    return bar.rc();
+  }
+  std::copy(result.begin(), result.end(), sums_out);
+  return FS_OK;
+}
+
+// ReliefF / SURF over several devices: thread r scores the focal samples of
+// its whole 128-sample blocks of [r_lo, r_hi) (parallel.shard_rows) on
+// devices[r]; the float64 sums are added on the host in rank order.  Their
+// neighbour selection is row-local (ReliefF.py:144-175, SURF.py:146-163),
+// so there is no other exchange.
+int rows_run_devices(const Prepared& P, const void* x, const int* devices, int ndev,
+                     int64_t r_lo, int64_t r_hi, double* sums_out) {
+  const int N = ndev;
+  const int64_t b0 = r_lo / kTile, b1 = (r_hi + kTile - 1) / kTile, nb = b1 - b0;
+  std::vector<std::vector<double>> parts(N, std::vector<double>(P.n_kept, 0.0));
+  std::vector<int> rcs(N, FS_OK);
+  std::vector<std::string> errs(N);
+  auto worker = [&](int r) {
+    const int64_t lo = std::max(r_lo, (b0 + nb * r / N) * kTile);
+    const int64_t hi = std::min(r_hi, (b0 + nb * (r + 1) / N) * kTile);
+    if (hi <= lo) return;
+    rcs[r] = P.algo == ALGO_RELIEFF ? relieff_run(P, x, devices[r], lo, hi, parts[r].data())
+                                    : surf_run(P, x, devices[r], lo, hi, parts[r].data());
+    if (rcs[r] != FS_OK) errs[r] = fs_last_error();
+  };
+  std::vector<std::thread> th;
+  for (int r = 1; r < N; r++) th.emplace_back(worker, r);
+  worker(0);
+  for (auto& t : th) t.join();
+  for (int r = 0; r < N; r++)
+    if (rcs[r] != FS_OK) {
+      set_error(errs[r]);
+      return rcs[r];
+    }
+  std::vector<double> sum;
+  rank_sum(parts, sum);
+  std::copy(sum.begin(), sum.end(), sums_out);
+  return FS_OK;
 }
 
 }  // namespace gpu

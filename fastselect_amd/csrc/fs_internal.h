@@ -349,6 +349,13 @@ void plan_destroy(Plan* g);
 // by n.  SURF / ReliefF: float64 score sums of the focal samples [r_lo, r_hi)
 // (row sharding; the full range gives the single-GPU result times n).
 int multisurf_run(const Prepared& P, const void* x, int device, float* scores_out);
+// One process, several devices (devices[0..ndev), repeats allowed): MultiSURF
+// tile partition / ReliefF and SURF row partition with host-side rank-order
+// sums in place of the all-reduces.  Score sums of [r_lo, r_hi) (not / n).
+int multisurf_run_devices(const Prepared& P, const void* x, const int* devices, int ndev,
+                          int64_t r_lo, int64_t r_hi, double* sums_out);
+int rows_run_devices(const Prepared& P, const void* x, const int* devices, int ndev,
+                     int64_t r_lo, int64_t r_hi, double* sums_out);
 // MultiSURF float64 score sums of the focal samples [r_lo, r_hi).
 int multisurf_rows(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
                    double* sums_out);

@@ -18,12 +18,13 @@ class SURFstar(SURF):
     use_star = True
 
     def __init__(self, n_features_to_select=0.2, backend="auto", discrete_limit=10, n_jobs=-1,
-                 verbose=False):
+                 verbose=False, devices=None):
         self.n_features_to_select = n_features_to_select
         self.backend = backend
         self.discrete_limit = discrete_limit
         self.n_jobs = n_jobs
         self.verbose = verbose
+        self.devices = devices
 
 
 class MultiSURFstar(MultiSURF):
@@ -32,9 +33,10 @@ class MultiSURFstar(MultiSURF):
     use_star = True
 
     def __init__(self, n_features_to_select=0.2, backend="auto", discrete_limit=10, n_jobs=-1,
-                 verbose=False):
+                 verbose=False, devices=None):
         self.n_features_to_select = n_features_to_select
         self.backend = backend
         self.discrete_limit = discrete_limit
         self.n_jobs = n_jobs
         self.verbose = verbose
+        self.devices = devices

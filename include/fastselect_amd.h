@@ -203,6 +203,37 @@ FS_API int fs_surf_score_rows(int backend, int device, const double* x, int64_t 
                               int64_t row_end, double* sums_out);
 
 /*
+ * Single-process multi-GPU scoring (the estimators' `devices=`; SURVEY.md
+ * §5 "Config / flags", §8(b) "Threading: one host thread per device").  One
+ * host thread per entry of devices[0 .. n_devices) -- ordinals may repeat
+ * (several plans share one device) -- with the partitions of the
+ * one-process-per-GPU path (fastselect_amd/parallel.py): MultiSURF deals the
+ * upper-triangle pair tiles round-robin (tile t -> thread t % N) and sums its
+ * three exchange vectors (row moments, neighbour counts, score sums) on the
+ * host in thread order after each stage, where the multi-process path
+ * all-reduces them over RCCL; ReliefF / SURF give each thread whole 128-sample
+ * blocks of the focal range and sum the score vectors once.  Write the
+ * float64 score SUMS of the focal samples [row_begin, row_end) (not divided
+ * by n; [0, n) for a whole fit) to sums_out.  Other arguments as the
+ * one-shot calls; the reference's fit is one call on one device
+ * (MultiSURF.py:393-440, ReliefF.py:382-403, SURF.py:339-372).
+ */
+FS_API int fs_multisurf_score_devices(const int* devices, int n_devices, const float* x, int64_t n,
+                                      int64_t p, const double* y, const float* recip,
+                                      const int64_t* feat_idx, int64_t n_kept, int use_star,
+                                      const uint8_t* is_discrete, int n_jobs, int64_t row_begin,
+                                      int64_t row_end, double* sums_out);
+FS_API int fs_relieff_score_devices(const int* devices, int n_devices, const float* x, int64_t n,
+                                    int64_t p, const int32_t* y_enc, const float* recip,
+                                    const uint8_t* is_discrete, int64_t k, const float* class_probs,
+                                    int64_t n_classes, int n_jobs, int64_t row_begin,
+                                    int64_t row_end, double* sums_out);
+FS_API int fs_surf_score_devices(const int* devices, int n_devices, const double* x, int64_t n,
+                                 int64_t p, const int32_t* y, const float* recip, int use_star,
+                                 const uint8_t* is_discrete, int n_jobs, int64_t row_begin,
+                                 int64_t row_end, double* sums_out);
+
+/*
  * Per-column statistics of X: the preprocessing each reference fit() runs on
  * the host before scoring -- x.min(axis=0), x.max(axis=0) and, per column,
  * np.unique(x[:, f]).size compared with discrete_limit (MultiSURF.py:141-144,

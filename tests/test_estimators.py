@@ -402,3 +402,25 @@ def test_turf_resident_relieff_single_class_falls_back():
     y = np.zeros(40, dtype=int)
     t = TuRF(ReliefF(backend="cpu"), n_features_to_select=3).fit(X, y)
     assert t.top_features_.size == 3
+
+
+def test_devices_parameter_resolution(monkeypatch):
+    """``devices=`` (single-process multi-GPU, SURVEY.md §5 "Config"):
+    resolution rules on a pretend 4-GPU host, and a get_params round trip."""
+    from fastselect_amd import _base, _lib
+    monkeypatch.setattr(_lib, "device_count", lambda: 4)
+    assert _base.fit_devices(None, "cpu", 10 ** 6) is None
+    assert _base.fit_devices([7], "cpu", 10) is None           # ignored by the CPU backend
+    assert _base.fit_devices(None, "gpu", 100) == [0]          # small job: one device
+    assert _base.fit_devices(None, "gpu", 9000) == [0, 1]      # one per 4096 samples
+    assert _base.fit_devices(None, "gpu", 10 ** 6) == [0, 1, 2, 3]
+    assert _base.fit_devices(2, "gpu", 10) == [2]
+    assert _base.fit_devices(np.int64(3), "gpu", 10) == [3]
+    assert _base.fit_devices((0, 0, 1), "gpu", 10) == [0, 0, 1]
+    for bad in ([], [4], [-1], "0", 1.5, True, [0, None]):
+        with pytest.raises(ValueError, match="devices"):
+            _base.fit_devices(bad, "gpu", 10)
+    est = MultiSURF(devices=[0, 1])
+    assert est.get_params()["devices"] == [0, 1]
+    assert ReliefF(devices=2).get_params()["devices"] == 2
+    assert SURF().get_params()["devices"] is None

@@ -818,10 +818,321 @@ def gen_jit(name="FS_SPARSE_STREAM_ASM", lead=6, bank_shift=False, half_lds=Fals
 '''
 
 
+# ---------------------------------------------------------------------------
+# v2 (round 3, shipped): 64-row half tiles, F = 8 (or 4) features per lane,
+# unpadded streams with per-entry column-end flags
+# ---------------------------------------------------------------------------
+V2_DOC = """
+Sparse v2 loop (k_score_sparse2).  Stream = the entries (roff, w) of one
+wave's 8 columns in one 64-row half tile, unpadded: roff = row * 2048 (the
+row's byte offset in the LDS block: 64 lanes x 8 floats), w the pair weight
+with its lowest mantissa bit set on the last entry of a column.  Lane l
+scores features f0 + 4l + k (chunk 0, LDS offset 0) and f0 + 256 + 4l + k
+(chunk 1, LDS offset 1024), k = 0..3.  Per entry: v_add_u32 (address),
+ds_read_b128 x F/4 (chunk 1 first: the chunk-0 read overwrites the address
+register), F x (v_sub_f32 in place, v_fma_f32 acc += w * |d|) -- 2F + 1 VALU
+per F pair-features.
+A step is 16 entries (two s_load_dwordx16, issued at the start of the
+previous step) and starts with the only lgkmcnt(0); the rows of entry e are
+read L entries ahead into a ring of L + 1 F-VGPR slots and waited with a
+counted lgkmcnt(M) (correct with the scalar loads in flight: LDS completes in
+order, so if e's read were pending the M reads after it would be too).  After
+each entry an SCC test of the weight's flag branches out of line to the
+column switch: B <- next B (prefetched one column ahead, two
+global_load_dwordx4), the load of the column after it, or the exit after the
+stream's 8th column.  A safety bound on the stream offset ends the loop on a
+malformed stream.
+Registers: v24.. B (F), then next B (F), then the ring; s20..s27 and
+s36..s99 as the v1 JIT loop.
+"""
+
+
+def gen_v2(name, F=8, lead=4, diag="", grp=1):
+    """diag (A/B diagnostics only, wrong scores): "lds1" skips the chunk-1
+    row read (half the LDS traffic), "nosub" drops the v_sub_f32 (half the
+    VALU), "nolds" skips every row read (the slots keep stale values)."""
+    L = lead
+    R = F // 4                      # ds_read_b128 per entry
+    SET = [36, 68]
+    BCUR, BNXT = 24, 24 + F
+    RING = 24 + 2 * F
+    OFF, TMP, BASE, COLS, TMP2, BPTR = 24, 25, 26, 22, 23, 20
+
+    def slot(e):
+        return RING + F * (e % (L + 1))
+
+    def entry_sgprs(k, e):
+        base = SET[k] + 2 * e
+        return base, base + 1       # roff, weight
+
+    def read(k, e):
+        r, _ = entry_sgprs(k, e)
+        a = slot(e)
+        L_ = [f"v_add_u32 v{a}, s{r}, %[lds_lane]"]
+        if diag == "nolds":
+            return L_
+        if F == 8 and diag != "lds1":  # chunk 1 first: the chunk-0 read overwrites the address
+            L_.append(f"ds_read_b128 v[{a + 4}:{a + 7}], v{a} offset:1024")
+        L_.append(f"ds_read_b128 v[{a}:{a + 3}], v{a}")
+        return L_
+
+    def compute(k, e):
+        _, w = entry_sgprs(k, e)
+        a = slot(e)
+        L_ = [] if diag == "nosub" else [f"v_sub_f32 v{a + f}, v{a + f}, v{BCUR + f}" for f in range(F)]
+        L_ += [f"v_fma_f32 %[acc{f}], s{w}, |v{a + f}|, %[acc{f}]" for f in range(F)]
+        return L_
+
+    def bload(dst):
+        L_ = [f"global_load_dwordx4 v[{dst}:{dst + 3}], %[glb_lane], s[{BPTR}:{BPTR + 1}]"]
+        if F == 8:
+            L_.append(f"global_load_dwordx4 v[{dst + 4}:{dst + 7}], %[glb_lane], "
+                      f"s[{BPTR}:{BPTR + 1}] offset:1024")
+        return L_
+
+    out_of_line = []
+
+    def switch(lab, ret):
+        return [f"{lab}:",
+                f"s_add_u32 s{COLS}, s{COLS}, 1",
+                f"s_cmp_ge_u32 s{COLS}, %[ncols]",
+                "s_cbranch_scc1 8f",
+                "s_waitcnt vmcnt(0)",
+                *[f"v_mov_b32 v{BCUR + f}, v{BNXT + f}" for f in range(F)],
+                f"s_add_u32 s{TMP2}, s{COLS}, 1",
+                f"s_cmp_ge_u32 s{TMP2}, %[ncols]",
+                f"s_cbranch_scc1 {ret}b",
+                f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
+                f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0",
+                *bload(BNXT),
+                f"s_branch {ret}b"]
+
+    if diag in ("lds1", "nolds"):
+        R = 1 if diag == "lds1" else 0
+
+    def step(x):
+        k, o = x % 2, 1 - x % 2
+        S = ["s_waitcnt lgkmcnt(0)",
+             f"s_load_dwordx16 s[{SET[o]}:{SET[o] + 15}], s[{BASE}:{BASE + 1}], s{OFF}",
+             f"s_add_u32 s{TMP}, s{OFF}, 64",
+             f"s_load_dwordx16 s[{SET[o] + 16}:{SET[o] + 31}], s[{BASE}:{BASE + 1}], s{TMP}",
+             f"s_add_u32 s{OFF}, s{OFF}, 128"]
+        for e in range(min(L, 16)):
+            S += read(k, e)
+        issued = min(L, 16)
+        for e in range(16):
+            if e + L < 16:
+                S += read(k, e + L)
+                issued = e + L + 1
+            after = (issued - (e + 1)) * R      # LDS reads issued after entry e's last one
+            S.append(f"s_waitcnt lgkmcnt({min(after, 15)})")
+            S += compute(k, e)
+            if (e + 1) % grp == 0:  # columns are padded to whole groups of grp entries
+                _, w = entry_sgprs(k, e)
+                sw, ret = 100 + 16 * x + e, 200 + 16 * x + e
+                S += [f"s_bitcmp1_b32 s{w}, 0", f"s_cbranch_scc1 {sw}f", f"{ret}:"]
+                out_of_line.extend(switch(sw, ret))
+        return S
+
+    lines = [f"s_mov_b32 s{COLS}, 0",
+             f"s_mov_b64 s[{BPTR}:{BPTR + 1}], %[bp]",
+             *bload(BCUR),
+             f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
+             f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0",
+             *bload(BNXT),
+             f"s_mov_b64 s[{BASE}:{BASE + 1}], %[eb]",
+             f"s_load_dwordx16 s[{SET[0]}:{SET[0] + 15}], s[{BASE}:{BASE + 1}], 0x0",
+             f"s_load_dwordx16 s[{SET[0] + 16}:{SET[0] + 31}], s[{BASE}:{BASE + 1}], 0x40",
+             f"s_mov_b32 s{OFF}, 128",
+             f"s_waitcnt vmcnt({R})",
+             "7:"]
+    for x in range(2):
+        lines += step(x)
+    # safety bound: a stream holds at most 8 columns x 64 rows (4 KB)
+    lines += [f"s_cmp_gt_u32 s{OFF}, 0x1100", "s_cbranch_scc0 7b", "s_branch 8f"]
+    lines += out_of_line
+    lines += ["8:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    body = "\n".join(f'      "{l}\\n"  \\' for l in lines)
+    vclob = ", ".join(f'"v{i}"' for i in range(BCUR, RING + F * (L + 1)))
+    named = set()
+    for l in lines:
+        for lo, hi in re.findall(r"(?<![a-z_])s\[?(\d+)(?::(\d+)\])?", l):
+            named.update(range(int(lo), int(hi or lo) + 1))
+    sclob = ", ".join(f'"s{i}"' for i in sorted(named))
+    return f"""#define {name}(acc_, lds_lane_, glb_lane_, eb_, bp_, bstride_, ncols_)  \\
+  asm volatile(  \\
+{body}
+      : {", ".join(f'[acc{i}] "+v"(acc_[{i}])' for i in range(F))}  \\
+      : [lds_lane] "v"(lds_lane_), [glb_lane] "v"(glb_lane_), [eb] "s"(eb_), [bp] "s"(bp_),  \\
+        [bstride] "s"(bstride_), [ncols] "s"(ncols_)  \\
+      : {vclob},  \\
+        {sclob}, "scc", "memory")
+"""
+
+
+V2X_DOC = """
+Sparse v2 loop with cross-step lookahead (k_score_sparse2; FS_GEN_V2X).
+The plain v2 loop drains the LDS pipeline at every step: the step's lgkmcnt(0)
+(the only safe wait while scalar loads are in flight, since they return out
+of order) comes before the step's first row reads can be issued, because
+their addresses are in the entries that wait is for.  Here the scalar loads
+run two steps ahead through three SGPR sets (steps of S = 8 or 12 entries:
+3 x 2S SGPRs), so at the start of step k the entries of step k + 1 are
+already in SGPRs and the rows of the first L entries of each step are read
+during the previous step: the lgkmcnt(0) at a step's start then waits only
+for scalar loads issued a whole step earlier and row reads issued L entries
+earlier.
+"""
+
+
+def gen_v2x(name, F=8, lead=3, S=8):
+    L = lead
+    assert 1 <= L <= S
+    R = F // 4
+    NS = 3
+    W = 2 * S                        # SGPRs per set
+    SET = [28 + W * i for i in range(NS)]
+    assert SET[-1] + W <= 102
+    BCUR, BNXT = 24, 24 + F
+    RING = 24 + 2 * F
+    OFF, TMP, BASE, COLS, TMP2, BPTR = 24, 25, 26, 22, 23, 20
+    NSTEP = NS                       # unrolled steps (set rotation)
+    TOT = S * NSTEP                  # entries per unrolled body
+    # reads run L entries ahead across the loop's back edge: ring slots must
+    # line up with the next pass of the body
+    assert TOT % (L + 1) == 0, "3 * S must be a multiple of lead + 1"
+
+    def slot(e):
+        return RING + F * (e % (L + 1))
+
+    def entry_sgprs(g):              # g = entry index within the unrolled body
+        st, e = divmod(g % TOT, S)
+        base = SET[st % NS] + 2 * e
+        return base, base + 1
+
+    def read(g):
+        r, _ = entry_sgprs(g)
+        a = slot(g)
+        L_ = [f"v_add_u32 v{a}, s{r}, %[lds_lane]"]
+        if F == 8:
+            L_.append(f"ds_read_b128 v[{a + 4}:{a + 7}], v{a} offset:1024")
+        L_.append(f"ds_read_b128 v[{a}:{a + 3}], v{a}")
+        return L_
+
+    def compute(g):
+        _, w = entry_sgprs(g)
+        a = slot(g)
+        L_ = [f"v_sub_f32 v{a + f}, v{a + f}, v{BCUR + f}" for f in range(F)]
+        L_ += [f"v_fma_f32 %[acc{f}], s{w}, |v{a + f}|, %[acc{f}]" for f in range(F)]
+        return L_
+
+    def bload(dst):
+        L_ = [f"global_load_dwordx4 v[{dst}:{dst + 3}], %[glb_lane], s[{BPTR}:{BPTR + 1}]"]
+        if F == 8:
+            L_.append(f"global_load_dwordx4 v[{dst + 4}:{dst + 7}], %[glb_lane], "
+                      f"s[{BPTR}:{BPTR + 1}] offset:1024")
+        return L_
+
+    def sload(st, off_reg):          # entries of one step into set st
+        b = SET[st % NS]
+        if S == 8:
+            return [f"s_load_dwordx16 s[{b}:{b + 15}], s[{BASE}:{BASE + 1}], s{off_reg}"]
+        return [f"s_load_dwordx16 s[{b}:{b + 15}], s[{BASE}:{BASE + 1}], s{off_reg}",
+                f"s_add_u32 s{TMP}, s{off_reg}, 64",
+                f"s_load_dwordx8 s[{b + 16}:{b + 23}], s[{BASE}:{BASE + 1}], s{TMP}"]
+
+    out_of_line = []
+
+    def switch(lab, ret):
+        return [f"{lab}:",
+                f"s_add_u32 s{COLS}, s{COLS}, 1",
+                f"s_cmp_ge_u32 s{COLS}, %[ncols]",
+                "s_cbranch_scc1 8f",
+                "s_waitcnt vmcnt(0)",
+                *[f"v_mov_b32 v{BCUR + f}, v{BNXT + f}" for f in range(F)],
+                f"s_add_u32 s{TMP2}, s{COLS}, 1",
+                f"s_cmp_ge_u32 s{TMP2}, %[ncols]",
+                f"s_cbranch_scc1 {ret}b",
+                f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
+                f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0",
+                *bload(BNXT),
+                f"s_branch {ret}b"]
+
+    def step(st):
+        # entries st*S .. st*S + S-1 of the body; rows of the first L of them
+        # were read during the previous step (or the prologue)
+        S_ = ["s_waitcnt lgkmcnt(0)"]
+        S_ += sload(st + 2, OFF)
+        S_.append(f"s_add_u32 s{OFF}, s{OFF}, {8 * S}")
+        issued_upto = st * S + L      # entries whose rows were requested (exclusive)
+        for e in range(S):
+            g = st * S + e
+            S_ += read(g + L)
+            issued_upto = g + L + 1
+            after = (issued_upto - (g + 1)) * R
+            S_.append(f"s_waitcnt lgkmcnt({min(after, 15)})")
+            S_ += compute(g)
+            _, w = entry_sgprs(g)
+            sw, ret = 100 + g, 200 + g
+            S_ += [f"s_bitcmp1_b32 s{w}, 0", f"s_cbranch_scc1 {sw}f", f"{ret}:"]
+            out_of_line.extend(switch(sw, ret))
+        return S_
+
+    lines = [f"s_mov_b32 s{COLS}, 0",
+             f"s_mov_b64 s[{BPTR}:{BPTR + 1}], %[bp]",
+             *bload(BCUR),
+             f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
+             f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0",
+             *bload(BNXT),
+             f"s_mov_b64 s[{BASE}:{BASE + 1}], %[eb]",
+             f"s_mov_b32 s{OFF}, 0"]
+    lines += sload(0, OFF)
+    lines.append(f"s_add_u32 s{OFF}, s{OFF}, {8 * S}")
+    lines += sload(1, OFF)
+    lines.append(f"s_add_u32 s{OFF}, s{OFF}, {8 * S}")
+    lines += ["s_waitcnt lgkmcnt(0)", f"s_waitcnt vmcnt({R})"]
+    for g in range(L):
+        lines += read(g)
+    lines.append("7:")
+    for st in range(NSTEP):
+        lines += step(st)
+    # safety bound: a stream holds at most 8 columns x 64 rows (4 KB)
+    lines += [f"s_cmp_gt_u32 s{OFF}, 0x1200", "s_cbranch_scc0 7b", "s_branch 8f"]
+    lines += out_of_line
+    lines += ["8:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    body = "\n".join(f'      "{l}\\n"  \\' for l in lines)
+    vclob = ", ".join(f'"v{i}"' for i in range(BCUR, RING + F * (L + 1)))
+    named = set()
+    for l in lines:
+        for lo, hi in re.findall(r"(?<![a-z_])s\[?(\d+)(?::(\d+)\])?", l):
+            named.update(range(int(lo), int(hi or lo) + 1))
+    sclob = ", ".join(f'"s{i}"' for i in sorted(named))
+    return f"""#define {name}(acc_, lds_lane_, glb_lane_, eb_, bp_, bstride_, ncols_)  \\
+  asm volatile(  \\
+{body}
+      : {", ".join(f'[acc{i}] "+v"(acc_[{i}])' for i in range(F))}  \\
+      : [lds_lane] "v"(lds_lane_), [glb_lane] "v"(glb_lane_), [eb] "s"(eb_), [bp] "s"(bp_),  \\
+        [bstride] "s"(bstride_), [ncols] "s"(ncols_)  \\
+      : {vclob},  \\
+        {sclob}, "scc", "memory")
+"""
+
+
 if __name__ == "__main__":
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "fastselect_amd", "csrc",
                         "fs_sparse_asm.inc")
     text = HEADER + gen()
+    if os.environ.get("FS_GEN_V2X", "0") != "0":   # cross-step lookahead (A/B)
+        text += "\n" + gen_v2x("FS_SPARSE2_ASM_F8", F=8,
+                               lead=int(os.environ.get("FS_GEN_V2_LEAD8", "3")),
+                               S=int(os.environ.get("FS_GEN_V2X", "8")))
+    else:
+        text += "\n" + gen_v2("FS_SPARSE2_ASM_F8", F=8,
+                              lead=int(os.environ.get("FS_GEN_V2_LEAD8", "3")),
+                              diag=os.environ.get("FS_GEN_V2_DIAG", ""),
+                              grp=int(os.environ.get("FS_GEN_V2_GROUP", "1")))
+    text += "\n" + gen_v2("FS_SPARSE2_ASM_F4", F=4,
+                          lead=int(os.environ.get("FS_GEN_V2_LEAD4", "6")))
     text += "\n" + gen_jit(name="FS_SPARSE_STREAM_ASM_JIT",   # A/B: FS_SPARSE_JIT=1
                             lead=int(os.environ.get("FS_GEN_JIT_LEAD", "12")),
                             bank_shift=bool(int(os.environ.get("FS_GEN_BANK_SHIFT", "0"))))
