@@ -118,6 +118,22 @@ __device__ __forceinline__ int64_t d_at(int tiled, int64_t n_pad, int64_t t, int
   return tiled ? ((t * kTile + b) * kTile + a) : ((j0 + b) * n_pad + i0 + a);
 }
 
+// Row window of the full layout (ReliefF / SURF row plans): only the rows
+// [win.x, win.y) -- the plan's focal 128-sample blocks -- are stored, and the
+// plan's D points where row 0 would be, so row r of the full matrix is still
+// D + r * n_pad.  A whole fit stores every row; a row-sharded plan (one rank
+// of N, a row panel) 1/N of them.  Writes skip rows outside the window; a
+// read of (i0 + a, j0 + b) takes row j0 + b when it is stored and row i0 + a
+// otherwise (D is symmetric, and every tile of a row plan has one of its two
+// blocks inside the window).
+__device__ __forceinline__ bool d_row_in(int2 win, int64_t r) { return r >= win.x && r < win.y; }
+__device__ __forceinline__ int64_t d_rd(int tiled, int2 win, int64_t n_pad, int64_t t, int64_t i0,
+                                        int64_t j0, int a, int b) {
+  if (tiled) return (t * kTile + b) * kTile + a;
+  const int64_t j = j0 + b;
+  return d_row_in(win, j) ? j * n_pad + i0 + a : (i0 + a) * n_pad + j;
+}
+
 // ---------------------------------------------------------------------------
 // Quantize: X -> xqT (u32, [PW][n_pad]) and xs (f32, [n_pad][PW])
 // ---------------------------------------------------------------------------
@@ -360,7 +376,7 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
                                                  int nck_cont, int nck_disc, uint32_t sc_disc,
                                                  int q16,
                                                  const int2* __restrict__ tiles, int64_t n_full,
-                                                 int splits, int tiled,
+                                                 int splits, int tiled, int2 win,
                                                  double* __restrict__ D,
                                                  double* __restrict__ Dpart) {
   // Two distinct LDS objects (not one indexed array) so the compiler can
@@ -462,11 +478,13 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
   flush();
 
   // Epilogue.  Full layout: D[i][j] for the tile and, off the diagonal, the
-  // mirror D[j][i].  Tiled: T_t[b][a] only (the mirror pattern below), which
-  // for a diagonal tile is the whole symmetric block.
+  // mirror D[j][i], each only where its row is in the window.  Tiled: T_t[b][a]
+  // only (the mirror pattern below), which for a diagonal tile is the whole
+  // symmetric block.
 #pragma unroll
   for (int r = 0; r < 8 && !tiled; r++) {
     const int64_t i = i0 + ty * 4 + (r & 3) + (r >> 2) * 64;
+    if (!d_row_in(win, i)) continue;
     double v[8];
 #pragma unroll
     for (int c = 0; c < 8; c++) {
@@ -483,6 +501,7 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
 #pragma unroll
     for (int c = 0; c < 8; c++) {
       const int b = tx * 4 + (c & 3) + (c >> 2) * 64;
+      if (!tiled && !d_row_in(win, j0 + b)) continue;
       double v[8];
 #pragma unroll
       for (int r = 0; r < 8; r++) {
@@ -519,7 +538,7 @@ constexpr int kMergeSlices = kTile * kTile / 1024;
 __global__ __launch_bounds__(256) void k_dist_merge(double* __restrict__ D,
                                                    const double* __restrict__ Dpart, int nparts,
                                                    const int2* __restrict__ tiles, int64_t n_full,
-                                                   int64_t n_pad, int tiled) {
+                                                   int64_t n_pad, int tiled, int2 win) {
   const int64_t t = n_full + blockIdx.x;
   const int2 tl = tiles[t];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
@@ -529,7 +548,7 @@ __global__ __launch_bounds__(256) void k_dist_merge(double* __restrict__ D,
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int e = blockIdx.y * 1024 + k * 256 + threadIdx.x;
-    at[k] = d_at(tiled, n_pad, t, i0, j0, e % kTile, e / kTile);  // (i0 + a, j0 + b)
+    at[k] = d_rd(tiled, win, n_pad, t, i0, j0, e % kTile, e / kTile);  // (i0 + a, j0 + b)
     v[k] = D[at[k]];
   }
   for (int s = 0; s < nparts; s++) {
@@ -541,8 +560,10 @@ __global__ __launch_bounds__(256) void k_dist_merge(double* __restrict__ D,
   for (int k = 0; k < 4; k++) {
     const int e = blockIdx.y * 1024 + k * 256 + threadIdx.x;
     D[at[k]] = v[k];
-    // full layout: the other half too (a diagonal tile's `at` covers it)
-    if (!tiled && tl.x != tl.y) D[(i0 + e % kTile) * n_pad + j0 + e / kTile] = v[k];
+    // full layout: the other half too where `at` was row j0 + b and row
+    // i0 + a is stored (a diagonal tile's `at` covers both halves)
+    if (!tiled && tl.x != tl.y && d_row_in(win, j0 + e / kTile) && d_row_in(win, i0 + e % kTile))
+      D[(i0 + e % kTile) * n_pad + j0 + e / kTile] = v[k];
   }
 }
 
@@ -574,7 +595,7 @@ __device__ __forceinline__ void dist_chunk_f64(const double* __restrict__ A,
 // per lane read 96 B for 32 and left the LDS near its bandwidth).
 __global__ __launch_bounds__(256, 2) void k_dist_f64(const double* __restrict__ xT, int64_t n_pad,
                                                      int nck_cont, int nck_disc,
-                                                     const int2* __restrict__ tiles,
+                                                     const int2* __restrict__ tiles, int2 win,
                                                      double* __restrict__ D) {
   __shared__ __attribute__((aligned(16))) double ldsA0[kBK64 * kTile], ldsB0[kBK64 * kTile];
   __shared__ __attribute__((aligned(16))) double ldsA1[kBK64 * kTile], ldsB1[kBK64 * kTile];
@@ -629,6 +650,7 @@ __global__ __launch_bounds__(256, 2) void k_dist_f64(const double* __restrict__ 
 #pragma unroll
   for (int r = 0; r < 8; r++) {
     const int64_t i = i0 + ty * 4 + (r & 3) + (r >> 2) * 64;
+    if (!d_row_in(win, i)) continue;
     double* row = D + i * n_pad + j0 + tx * 4;
     *(double2*)(row + 0) = make_double2(acc[r][0], acc[r][1]);
     *(double2*)(row + 2) = make_double2(acc[r][2], acc[r][3]);
@@ -639,6 +661,7 @@ __global__ __launch_bounds__(256, 2) void k_dist_f64(const double* __restrict__ 
 #pragma unroll
     for (int c = 0; c < 8; c++) {
       const int64_t j = j0 + tx * 4 + (c & 3) + (c >> 2) * 64;
+      if (!d_row_in(win, j)) continue;
       double* row = D + j * n_pad + i0 + ty * 4;
       *(double2*)(row + 0) = make_double2(acc[0][c], acc[1][c]);
       *(double2*)(row + 2) = make_double2(acc[2][c], acc[3][c]);
@@ -793,28 +816,34 @@ __global__ void k_thr_ms(const double* __restrict__ rowstats, int64_t n,
 }
 
 // SURF: avg_i = float32 sequential sum over j (self included, D_ii = 0) of
-// the float32 distance row, / (n - 1) in float64 (SURF.py:146-163).  Thread
-// i walks column i of the symmetric D so a wave's loads are coalesced.
-// One lane per row; D is symmetric, so lane i reads column i (coalesced
-// across lanes).  The float32 sum stays strictly sequential in j (the
-// reference's order); 16 loads are issued ahead of the adds that use them.
+// the float32 distance row, / (n - 1) in float64 (SURF.py:146-163).  One
+// wave per 64 focal rows: 64 x 64 blocks of the rows are staged through LDS
+// with coalesced row-segment loads (a row plan stores only its own rows, so
+// the symmetric column cannot be read instead), then lane r adds its row's 64
+// values in j order -- the float32 sum stays strictly sequential in j, the
+// reference's order.
 __global__ __launch_bounds__(64) void k_surf_avg(const double* __restrict__ D, int64_t n,
                                                  int64_t n_pad, double inv_sc, int64_t r_lo,
                                                  int64_t r_hi, double* __restrict__ avg) {
-  const int64_t i = r_lo + (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (i >= r_hi) return;
-  constexpr int kU = 16;
+  __shared__ float blk[64][65];
+  const int lane = threadIdx.x;
+  const int64_t row0 = r_lo + (int64_t)blockIdx.x * 64;
+  const int64_t nrows = r_hi - row0 < 64 ? r_hi - row0 : 64;
   float s = 0.0f;
-  int64_t j = 0;
-  for (; j + kU <= n; j += kU) {
-    double v[kU];
-#pragma unroll
-    for (int u = 0; u < kU; u++) v[u] = D[(j + u) * n_pad + i];
-#pragma unroll
-    for (int u = 0; u < kU; u++) s += (float)(v[u] * inv_sc);
+  for (int64_t j0 = 0; j0 < n; j0 += 64) {
+    const int64_t j = j0 + lane;
+#pragma unroll 8
+    for (int r = 0; r < 64; r++) {
+      float v = 0.0f;
+      if (r < nrows && j < n) v = (float)(D[(row0 + r) * n_pad + j] * inv_sc);
+      blk[r][lane] = v;
+    }
+    __syncthreads();
+    const int cnt = n - j0 < 64 ? (int)(n - j0) : 64;
+    for (int c = 0; c < cnt; c++) s += blk[lane][c];
+    __syncthreads();
   }
-  for (; j < n; j++) s += (float)(D[j * n_pad + i] * inv_sc);
-  avg[i] = (double)s / (double)(n - 1);
+  if (lane < nrows) avg[row0 + lane] = (double)s / (double)(n - 1);
 }
 
 // Flagged pairs are collected per workgroup in LDS and appended to the
@@ -862,7 +891,7 @@ __device__ __forceinline__ void pairbuf_flush(PairBuf& pb, int2* __restrict__ li
 // MultiSURF compares D (integer units) with thr; SURF compares the float32
 // distance with the float64 mean, the band widened by 4 float32 ulps of it.
 __global__ __launch_bounds__(256) void k_flag_pairs(const double* __restrict__ D, int64_t n,
-                                                    int64_t n_pad, int tiled,
+                                                    int64_t n_pad, int tiled, int2 win,
                                                     const int2* __restrict__ tiles,
                                                     const double* __restrict__ thr, int algo,
                                                     double inv_sc, double delta,
@@ -878,10 +907,10 @@ __global__ __launch_bounds__(256) void k_flag_pairs(const double* __restrict__ D
     bool amb = false;
     if (!(i < n && j < n && (tl.x < tl.y || ii < jj))) {
     } else if (algo == ALGO_MULTISURF) {
-      const double d = D[d_at(tiled, n_pad, blockIdx.x, i0, j0, ii, jj)];
+      const double d = D[d_rd(tiled, win, n_pad, blockIdx.x, i0, j0, ii, jj)];
       amb = __builtin_fabs(d - thr[i]) < delta || __builtin_fabs(d - thr[j]) < delta;
     } else {
-      const double df = D[d_at(tiled, n_pad, blockIdx.x, i0, j0, ii, jj)] * inv_sc;
+      const double df = D[d_rd(tiled, win, n_pad, blockIdx.x, i0, j0, ii, jj)] * inv_sc;
       const float ai = (float)thr[i], aj = (float)thr[j];
       const double bi = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(ai) + 1u) - (double)ai);
       const double bj = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(aj) + 1u) - (double)aj);
@@ -897,11 +926,11 @@ __global__ __launch_bounds__(256) void k_flag_pairs(const double* __restrict__ D
 // tile of blocks (i / 128, j / 128), the (linear / world)-th tile this rank
 // owns (round-robin ownership, owned_tiles); a diagonal tile holds both
 // halves.
-__device__ __forceinline__ void store_pair(double* __restrict__ D, int64_t n_pad, int2 tw, int2 pr,
-                                           double v) {
-  if (tw.x == 0) {
-    D[(int64_t)pr.x * n_pad + pr.y] = v;
-    D[(int64_t)pr.y * n_pad + pr.x] = v;
+__device__ __forceinline__ void store_pair(double* __restrict__ D, int64_t n_pad, int2 tw, int2 win,
+                                           int2 pr, double v) {
+  if (tw.x == 0) {  // full layout: both halves, where their rows are stored
+    if (d_row_in(win, pr.x)) D[(int64_t)pr.x * n_pad + pr.y] = v;
+    if (d_row_in(win, pr.y)) D[(int64_t)pr.y * n_pad + pr.x] = v;
     return;
   }
   if (pr.x > pr.y) pr = make_int2(pr.y, pr.x);
@@ -922,7 +951,7 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
     const T* __restrict__ x, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
     const int64_t* __restrict__ src_col, const double* __restrict__ scl, double sc,
     const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
-    int64_t n_pad, int2 tw, int mark_f32, double* __restrict__ D) {
+    int64_t n_pad, int2 tw, int2 win, int mark_f32, double* __restrict__ D) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
@@ -967,7 +996,7 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
       // reference's float32 key, stored negated so k_rf_select knows it is
       // exact (a zero key is stored as +0, never -0, whose bits would sort last).
       const double v = mark_f32 ? (acc > 0.0 ? -(double)(float)acc : 0.0) : acc * sc;
-      store_pair(D, n_pad, tw, pr, v);
+      store_pair(D, n_pad, tw, win, pr, v);
     }
   }
 }
@@ -982,7 +1011,7 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
 __global__ __launch_bounds__(256) void k_exact_pairs_rows(
     const float* __restrict__ x, int64_t p, const float* __restrict__ scl32, double sc,
     const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
-    int64_t n_pad, int2 tw, double* __restrict__ D) {
+    int64_t n_pad, int2 tw, int2 win, double* __restrict__ D) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
@@ -1015,7 +1044,7 @@ __global__ __launch_bounds__(256) void k_exact_pairs_rows(
     }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (lane == 0) {
-      store_pair(D, n_pad, tw, pr, acc * sc);
+      store_pair(D, n_pad, tw, win, pr, acc * sc);
     }
   }
 }
@@ -1139,7 +1168,7 @@ __global__ __launch_bounds__(256) void k_tile_counts(const double* __restrict__ 
 // ---------------------------------------------------------------------------
 // Symmetric pair weight W_ij + W_ji of one pair (i, j) of an owned tile.
 __device__ __forceinline__ float pair_weight(const double* __restrict__ D, int64_t n, int64_t n_pad,
-                                             int tiled, int64_t t, int64_t i0, int64_t j0, int ii,
+                                             int tiled, int2 win, int64_t t, int64_t i0, int64_t j0, int ii,
                                              int jj, bool upper,
                                              const double* __restrict__ thr,
                                              const int32_t* __restrict__ lab,
@@ -1148,7 +1177,7 @@ __device__ __forceinline__ float pair_weight(const double* __restrict__ D, int64
                                              int64_t r_hi) {
   const int64_t i = i0 + ii, j = j0 + jj;
   if (!(i < n && j < n && upper)) return 0.0f;
-  const double d = D[d_at(tiled, n_pad, t, i0, j0, ii, jj)];  // == D[i][j]
+  const double d = D[d_rd(tiled, win, n_pad, t, i0, j0, ii, jj)];  // == D[i][j]
   const bool hit = lab[i] == lab[j];
   double wi, wj;
   if (algo == ALGO_MULTISURF) {
@@ -1167,7 +1196,7 @@ __device__ __forceinline__ float pair_weight(const double* __restrict__ D, int64
 }
 
 __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, int64_t n,
-                                                 int64_t n_pad, int tiled,
+                                                 int64_t n_pad, int tiled, int2 win,
                                                  const int2* __restrict__ tiles,
                                                  const double* __restrict__ thr,
                                                  const int32_t* __restrict__ lab,
@@ -1179,7 +1208,7 @@ __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, i
   float* out = Wt + (int64_t)blockIdx.x * kTile * kTile;
   for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
     const int jj = e / kTile, ii = e % kTile;
-    out[jj * kTile + ii] = pair_weight(D, n, n_pad, tiled, blockIdx.x, i0, j0, ii, jj,
+    out[jj * kTile + ii] = pair_weight(D, n, n_pad, tiled, win, blockIdx.x, i0, j0, ii, jj,
                                        tl.x < tl.y || ii < jj, thr, lab, counts, algo, use_star,
                                        inv_sc, r_lo, r_hi);
   }
@@ -1207,7 +1236,7 @@ __device__ __forceinline__ uint32_t weight_bits(float w, bool last) {
 }
 
 __global__ __launch_bounds__(1024) void k_weights_sparse(
-    const double* __restrict__ D, int64_t n, int64_t n_pad, int tiled,
+    const double* __restrict__ D, int64_t n, int64_t n_pad, int tiled, int2 win,
     const int2* __restrict__ tiles, const double* __restrict__ thr,
     const int32_t* __restrict__ lab,
     const double* __restrict__ counts, int algo, int use_star, double inv_sc, int64_t r_lo,
@@ -1220,10 +1249,10 @@ __global__ __launch_bounds__(1024) void k_weights_sparse(
   const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
   int off = 0, nz = 0;
   for (int jj = wave; jj < kTile; jj += kSWaves) {
-    const float w0 = pair_weight(D, n, n_pad, tiled, blockIdx.x, i0, j0, lane, jj,
+    const float w0 = pair_weight(D, n, n_pad, tiled, win, blockIdx.x, i0, j0, lane, jj,
                                  tl.x < tl.y || lane < jj, thr, lab, counts, algo, use_star,
                                  inv_sc, r_lo, r_hi);
-    const float w1 = pair_weight(D, n, n_pad, tiled, blockIdx.x, i0, j0, lane + 64, jj,
+    const float w1 = pair_weight(D, n, n_pad, tiled, win, blockIdx.x, i0, j0, lane + 64, jj,
                                  tl.x < tl.y || lane + 64 < jj, thr, lab, counts, algo, use_star,
                                  inv_sc, r_lo, r_hi);
     const uint64_t m0 = __ballot(w0 != 0.0f), m1 = __ballot(w1 != 0.0f);
@@ -1555,7 +1584,7 @@ constexpr int kStreamEntries2 = (kTile / kSWaves) * kHalf;  // 512
 static_assert(kStreamEntries2 * 2 == kStreamEntries, "v2 streams reuse the v1 buffer size");
 
 __global__ __launch_bounds__(1024) void k_weights_sparse2(
-    const double* __restrict__ D, int64_t n, int64_t n_pad, int tiled,
+    const double* __restrict__ D, int64_t n, int64_t n_pad, int tiled, int2 win,
     const int2* __restrict__ tiles, const double* __restrict__ thr,
     const int32_t* __restrict__ lab,
     const double* __restrict__ counts, int algo, int use_star, double inv_sc, int64_t r_lo,
@@ -1570,10 +1599,10 @@ __global__ __launch_bounds__(1024) void k_weights_sparse2(
   const uint32_t roff = (uint32_t)lane * (uint32_t)kRowBytes2;
   int off0 = 0, off1 = 0, nz = 0;
   for (int jj = wave; jj < kTile; jj += kSWaves) {
-    const float w0 = pair_weight(D, n, n_pad, tiled, blockIdx.x, i0, j0, lane, jj,
+    const float w0 = pair_weight(D, n, n_pad, tiled, win, blockIdx.x, i0, j0, lane, jj,
                                  tl.x < tl.y || lane < jj, thr, lab, counts, algo, use_star,
                                  inv_sc, r_lo, r_hi);
-    const float w1 = pair_weight(D, n, n_pad, tiled, blockIdx.x, i0, j0, lane + 64, jj,
+    const float w1 = pair_weight(D, n, n_pad, tiled, win, blockIdx.x, i0, j0, lane + 64, jj,
                                  tl.x < tl.y || lane + 64 < jj, thr, lab, counts, algo, use_star,
                                  inv_sc, r_lo, r_hi);
     const uint64_t m0 = __ballot(w0 != 0.0f), m1 = __ballot(w1 != 0.0f);
@@ -2331,6 +2360,8 @@ struct Plan {
   int tiled = 0;                // D in the tiled layout (MultiSURF; d_at)
   int64_t dplane = 0;           // doubles of one distance plane (D, each Dpart)
   int2 tw = make_int2(0, 0);    // k_exact_pairs' store_pair: (nb, world) when tiled
+  int2 win = make_int2(0, 0);   // full layout: rows [win.x, win.y) stored (d_row_in)
+  void* D_alloc = nullptr;      // allocation behind D (D itself points at row 0)
   int2* tiles = nullptr;
   double* thr = nullptr;
   float* Wt = nullptr;          // dense pair weights (sparse == 0)
@@ -3132,7 +3163,19 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
   // 128 x 128 block per owned tile (half the full matrix at world 1, 1/N of
   // the tiles per rank).  ReliefF / SURF select neighbours over whole rows.
   g->tiled = (Q.algo == ALGO_MULTISURF && !g->row_mode) ? 1 : 0;
-  g->dplane = g->tiled ? std::max<int64_t>(g->n_tiles, 1) * kTile * kTile : Q.n_pad * Q.n_pad;
+  // ReliefF / SURF: the rows of the plan's focal 128-sample blocks only
+  // (d_row_in): a whole fit holds n_pad^2, one rank of an N-way row split or
+  // one row panel (rows_run_panels) its share
+  if (g->tiled) {
+    g->win = make_int2(0, 0);
+  } else {
+    const int64_t w0 = g->row_mode ? g->r_lo / kTile * kTile : 0;
+    const int64_t w1 = g->row_mode ? std::min<int64_t>(Q.n_pad, (g->r_hi + kTile - 1) / kTile * kTile)
+                                   : Q.n_pad;
+    g->win = make_int2((int)w0, (int)std::max(w0, w1));
+  }
+  g->dplane = g->tiled ? std::max<int64_t>(g->n_tiles, 1) * kTile * kTile
+                       : std::max<int64_t>((int64_t)(g->win.y - g->win.x), 1) * Q.n_pad;
   g->tw = g->tiled ? make_int2((int)g->nb, g->world) : make_int2(0, 0);
   // pass-1 chunk count and the per-tile work in feature units of 32-bit SAD
   const int64_t rows_q = (g->use_q16 ? Q.PC / 2 : Q.PC) + Q.PD;
@@ -3144,7 +3187,9 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
   g->kfull = g->ksplit > 1 ? 0 : g->n_tiles;  // k_dist can split only a tail; all or none here
   g->alloc_target = 3;
   int rc = FS_OK;
-  if ((rc = dalloc(g, &g->D, (size_t)g->dplane)) || (rc = dalloc(g, &g->tiles, g->n_tiles)) ||
+  if ((rc = dalloc(g, (double**)&g->D_alloc, (size_t)g->dplane)) ||
+      (g->D = (double*)g->D_alloc - (g->tiled ? 0 : (int64_t)g->win.x * Q.n_pad), false) ||
+      (rc = dalloc(g, &g->tiles, g->n_tiles)) ||
       (rc = dalloc(g, &g->rspart, (size_t)std::max<int64_t>(g->n_tiles, 1) * 256))) {
   } else if (Q.algo != ALGO_RELIEFF && !g->sparse) {
     rc = dalloc(g, &g->Wt, (size_t)(g->n_tiles + 1) * kTile * kTile);
@@ -3181,6 +3226,7 @@ int plan_set_shard(Plan* g, int rank, int world) {
   for (void* q : g->owned_shard) dev_free(q);
   g->owned_shard.clear();
   g->D = g->Dpart = nullptr;
+  g->D_alloc = nullptr;
   g->Wt = nullptr;
   g->ent = nullptr;
   g->tiles = nullptr;
@@ -3308,7 +3354,7 @@ static int run_quantize_dist(Plan* g) {
     if (g->n_tiles > 0) {
       FS_HIP(hipEventRecord(g->ev[0], g->stream));
       k_dist_f64<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(
-          g->xT64, Q.n_pad, (int)(Q.PC / kBK64), (int)(Q.PD / kBK64), g->tiles, g->D);
+          g->xT64, Q.n_pad, (int)(Q.PC / kBK64), (int)(Q.PD / kBK64), g->tiles, g->win, g->D);
       FS_TRY(launch_check("k_dist_f64"));
       FS_HIP(hipEventRecord(g->ev[1], g->stream));
     }
@@ -3353,11 +3399,11 @@ static int run_quantize_dist(Plan* g) {
     const int64_t n_full = g->n_tiles - n_split;
     k_dist<<<(unsigned)(n_full + n_split * g->ksplit), 256, 0, g->stream>>>(
         g->xqT, Q.n_pad, (int)((Q.q16 ? Q.PC / 2 : Q.PC) / kBKQ), (int)(Q.PD / kBKQ), Q.SCu,
-        Q.q16, g->tiles, n_full, g->ksplit, g->tiled, g->D, g->Dpart);
+        Q.q16, g->tiles, n_full, g->ksplit, g->tiled, g->win, g->D, g->Dpart);
     FS_TRY(launch_check("k_dist"));
     if (n_split > 0) {
       k_dist_merge<<<dim3((unsigned)n_split, kMergeSlices), 256, 0, g->stream>>>(
-          g->D, g->Dpart, g->ksplit - 1, g->tiles, n_full, Q.n_pad, g->tiled);
+          g->D, g->Dpart, g->ksplit - 1, g->tiles, n_full, Q.n_pad, g->tiled, g->win);
       FS_TRY(launch_check("k_dist_merge"));
     }
     FS_HIP(hipEventRecord(g->ev[1], g->stream));
@@ -3393,7 +3439,7 @@ static int refine_pairs(Plan* g, int algo, double delta) {
   for (int attempt = 0; attempt < 2; attempt++) {
     FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
     k_flag_pairs<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(
-        g->D, Q.n, Q.n_pad, g->tiled, g->tiles, g->thr, algo, 1.0 / Q.SC, delta, g->list,
+        g->D, Q.n, Q.n_pad, g->tiled, g->win, g->tiles, g->thr, algo, 1.0 / Q.SC, delta, g->list,
         g->list_cap, g->list_count);
     FS_TRY(launch_check("k_flag_pairs"));
     unsigned long long cnt = 0;
@@ -3412,15 +3458,15 @@ static int refine_pairs(Plan* g, int algo, double delta) {
   if (g->rows_direct && !std::getenv("FS_EXACT_GATHER"))
     k_exact_pairs_rows<<<grid, 256, 0, g->stream>>>((const float*)g->x, Q.p_in, g->scl32, Q.SC,
                                                     g->list, g->list_count, g->list_cap, Q.n_pad,
-                                                    g->tw, g->D);
+                                                    g->tw, g->win, g->D);
   else if (g->x_is_f64)
     k_exact_pairs<double><<<grid, 256, 0, g->stream>>>(
         (const double*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, g->tw, 0, g->D);
+        g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D);
   else
     k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
         (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, g->tw, 0, g->D);
+        g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D);
   return launch_check("k_exact_pairs");
 }
 
@@ -3433,16 +3479,17 @@ static int run_weights(Plan* g, const double* counts, int algo, double inv_sc) {
     g->nnz_valid = true;
     if (g->sparse_v == 2) {
       k_weights_sparse2<<<(unsigned)g->n_tiles, 64 * kSWaves, 0, g->stream>>>(
-          g->D, Q.n, Q.n_pad, g->tiled, g->tiles, g->thr, g->lab, counts, algo, Q.use_star,
-          inv_sc, g->r_lo, g->r_hi, g->ent, g->nnz);
+          g->D, Q.n, Q.n_pad, g->tiled, g->win, g->tiles, g->thr, g->lab, counts, algo,
+          Q.use_star, inv_sc, g->r_lo, g->r_hi, g->ent, g->nnz);
       return launch_check("k_weights_sparse2");
     }
     k_weights_sparse<<<(unsigned)g->n_tiles, 64 * kSWaves, 0, g->stream>>>(
-        g->D, Q.n, Q.n_pad, g->tiled, g->tiles, g->thr, g->lab, counts, algo, Q.use_star, inv_sc,
-        g->r_lo, g->r_hi, g->ent, g->nnz);
+        g->D, Q.n, Q.n_pad, g->tiled, g->win, g->tiles, g->thr, g->lab, counts, algo, Q.use_star,
+        inv_sc, g->r_lo, g->r_hi, g->ent, g->nnz);
     return launch_check("k_weights_sparse");
   }
-  k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiled, g->tiles,
+  k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiled, g->win,
+                                                         g->tiles,
                                                          g->thr,
                                                          g->lab, counts, algo, Q.use_star, inv_sc,
                                                          g->r_lo, g->r_hi, g->Wt);
@@ -3746,8 +3793,72 @@ static int plan_score_surf(Plan* g, double* sums_dev) {
   return rc;
 }
 
+// Rows per panel of a ReliefF / SURF one-shot call: a plan stores the
+// distance rows of its focal blocks (d_row_in), ~n_pad * 8 bytes per row plus
+// its share of the pass-2 weights and selection scratch (~n_pad * 16 more),
+// beside the per-sample buffers (X, the quantised and pass-2 operands:
+// ~20 n_pad PW bytes).  Focal ranges whose rows exceed 80% of the free
+// device memory are scored in panels of whole 128-sample blocks, one plan
+// each, and their sums added -- the reference streams each focal sample's
+// distance row the same way (ReliefF.py:143-157, SURF.py:139-163).
+// FS_ROW_PANEL=<rows> forces the panel height (tests).
+static int64_t row_panel_rows(const Prepared& P, int device, int64_t rows) {
+  if (const char* e = std::getenv("FS_ROW_PANEL"))
+    if (std::atoll(e) >= 1) return std::max<int64_t>(kTile, std::atoll(e) / kTile * kTile);
+  size_t free_b = 0, total_b = 0;
+  if (hipSetDevice(device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+    (void)hipGetLastError();
+    return rows;
+  }
+  const double fixed = 20.0 * (double)P.n_pad * (double)P.PW + 8.0 * (double)P.n * (double)P.p_in;
+  const double per_row = 24.0 * (double)P.n_pad;
+  const double avail = 0.8 * (double)free_b - fixed;
+  if (avail <= per_row * kTile) return kTile;  // let the allocation report it
+  const int64_t fit = (int64_t)(avail / per_row) / kTile * kTile;
+  return std::max<int64_t>(kTile, std::min<int64_t>(fit, (rows + kTile - 1) / kTile * kTile));
+}
+
+// Score [r_lo, r_hi) in panels of `panel` rows (block-aligned), summing the
+// panels' float64 sums in panel order.
+template <typename Fn>
+static int run_panels(const Prepared& P, int64_t r_lo, int64_t r_hi, int64_t panel,
+                      double* sums_out, Fn&& one) {
+  std::fill(sums_out, sums_out + P.n_kept, 0.0);
+  std::vector<double> part((size_t)P.n_kept);
+  for (int64_t lo = r_lo; lo < r_hi;) {
+    const int64_t hi = std::min(r_hi, (lo / kTile * kTile) + panel);
+    FS_TRY(one(lo, hi, part.data()));
+    for (int64_t k = 0; k < P.n_kept; k++) sums_out[k] += part[k];
+    lo = hi;
+  }
+  return FS_OK;
+}
+
+static int surf_run_one(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
+                        double* sums_out);
+static int relieff_run_one(const Prepared& P, const void* x, int device, int64_t r_lo,
+                           int64_t r_hi, double* sums_out);
+
 int surf_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
              double* sums_out) {
+  const int64_t panel = row_panel_rows(P, device, r_hi - r_lo);
+  if (r_hi - r_lo <= panel) return surf_run_one(P, x, device, r_lo, r_hi, sums_out);
+  return run_panels(P, r_lo, r_hi, panel, sums_out, [&](int64_t lo, int64_t hi, double* o) {
+    return surf_run_one(P, x, device, lo, hi, o);
+  });
+}
+
+int relieff_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
+                double* sums_out) {
+  const int64_t panel = row_panel_rows(P, device, r_hi - r_lo);
+  if (r_hi - r_lo <= panel) return relieff_run_one(P, x, device, r_lo, r_hi, sums_out);
+  return run_panels(P, r_lo, r_hi, panel, sums_out, [&](int64_t lo, int64_t hi, double* o) {
+    return relieff_run_one(P, x, device, lo, hi, o);
+  });
+}
+
+static int surf_run_one(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
+                        double* sums_out) {
   Plan* g = nullptr;
   FS_TRY(plan_create(&g, P, x, 1, device, 0, 1, 0, r_lo, r_hi));
   double* sc = nullptr;
@@ -3818,7 +3929,7 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
     const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
     k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
         (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, make_int2(0, 0), 1, g->D);
+        g->list_count, g->list_cap, Q.n_pad, make_int2(0, 0), g->win, 1, g->D);
     FS_TRY(launch_check("k_exact_pairs"));
   }
   // 3. exact selection
@@ -3918,8 +4029,8 @@ static int plan_score_relieff(Plan* g, double* sums_dev) {
   return launch_check("k_reduce");
 }
 
-int relieff_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
-                double* sums_out) {
+static int relieff_run_one(const Prepared& P, const void* x, int device, int64_t r_lo,
+                           int64_t r_hi, double* sums_out) {
   if (P.n_classes > 64) {
     set_error("GPU ReliefF supports at most 64 classes");
     return FS_ENOTSUP;

@@ -73,7 +73,7 @@ def test_surf_devices_equal_one_device(F, oracle, star):
 
 def test_devices_bad_ordinal_is_a_value_error(F):
     from fastselect_amd import _lib
-    X, y = _data(300, 40, 5)
+    X, y = _data(300, 80, 5)
     with pytest.raises(ValueError, match="devices"):
         F.MultiSURF(backend="gpu", devices=[0, _lib.device_count()]).fit(X, y)
     with pytest.raises(ValueError, match="devices"):
@@ -84,7 +84,7 @@ def test_devices_default_uses_visible_devices(F):
     """devices=None: every visible device the job has work for (one per
     4096 samples), so a small fit stays on one device."""
     from fastselect_amd import _base, _lib
-    X, y = _data(500, 50, 6)
+    X, y = _data(500, 80, 6)
     est = F.MultiSURF(backend="gpu").fit(X, y)
     assert est.devices_ == [0]
     assert _base.fit_devices(None, "gpu", 10 ** 6) == list(range(_lib.device_count()))
