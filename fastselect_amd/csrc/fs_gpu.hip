@@ -1707,6 +1707,7 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
   const bool fast = use_asm && f_end <= PC;
   const uint32_t lds_lane = (uint32_t)(uintptr_t)As + (uint32_t)lane * 16u;
   const uint32_t glb_lane = (uint32_t)lane * 16u;
+  const uint32_t pf_lane = (uint32_t)lane * 32u;
   const int64_t bstride = kSWaves * PW;
   const uint32_t bstride_b = (uint32_t)(bstride * sizeof(float));
   const uint32_t ncols = kTile / kSWaves;
@@ -1734,11 +1735,22 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
     const uint2* __restrict__ e = ent + ((t * 2 + h) * kSWaves + wave) * kStreamEntries2;
     const float* __restrict__ xb = xs + ((int64_t)tl.y * kTile + wave) * PW + f0;
     if (fast) {
-      const uint64_t eb = (uint64_t)(uintptr_t)e, bp = (uint64_t)(uintptr_t)xb;
+      const uint64_t eb = (uint64_t)(uintptr_t)e;
+#ifdef FS_V2_DIAG_BHOT  // A/B diagnostic only (wrong scores): every B from one hot row
+      const uint64_t bp = (uint64_t)(uintptr_t)(xs + (int64_t)wave * PW + f0);
+#else
+      const uint64_t bp = (uint64_t)(uintptr_t)xb;
+#endif
+      // the next tile's B rows (warmed into L2 by the loop; the last tile
+      // of a segment warms its own again)
+      const int64_t tn = t + 1 < t_end ? t + 1 : t;
+      const uint64_t bpn =
+          (uint64_t)(uintptr_t)(xs + ((int64_t)tiles[tn].y * kTile + wave) * PW + f0);
+      const uint64_t enb = (uint64_t)(uintptr_t)(ent + ((tn * 2 + h) * kSWaves + wave) * kStreamEntries2);
       if constexpr (F == 8)
-        FS_SPARSE2_ASM_F8(acc, lds_lane, glb_lane, eb, bp, bstride_b, ncols);
+        FS_SPARSE2_ASM_F8(acc, lds_lane, glb_lane, eb, bp, bstride_b, ncols, bpn, pf_lane, enb);
       else
-        FS_SPARSE2_ASM_F4(acc, lds_lane, glb_lane, eb, bp, bstride_b, ncols);
+        FS_SPARSE2_ASM_F4(acc, lds_lane, glb_lane, eb, bp, bstride_b, ncols, bpn, pf_lane, enb);
     } else {
       sparse2_stream_generic<F>(As, e, xb + 4 * lane, bstride, lane, disc, acc);
     }

@@ -847,15 +847,19 @@ s36..s99 as the v1 JIT loop.
 """
 
 
-def gen_v2(name, F=8, lead=4, diag="", grp=1):
+def gen_v2(name, F=8, lead=4, diag="", grp=1, pfn=True):
     """diag (A/B diagnostics only, wrong scores): "lds1" skips the chunk-1
     row read (half the LDS traffic), "nosub" drops the v_sub_f32 (half the
     VALU), "nolds" skips every row read (the slots keep stale values)."""
     L = lead
     R = F // 4                      # ds_read_b128 per entry
     SET = [36, 68]
+    # bpre2: B prefetched two columns ahead (a third B set, two moves per switch)
+    NB = 3 if diag == "bpre2" else 2
     BCUR, BNXT = 24, 24 + F
-    RING = 24 + 2 * F
+    BNX2 = 24 + 2 * F
+    RING = 24 + NB * F
+    PF = RING + F * (L + 1)          # two scratch VGPRs of the next-tile prefetch
     OFF, TMP, BASE, COLS, TMP2, BPTR = 24, 25, 26, 22, 23, 20
 
     def slot(e):
@@ -883,16 +887,35 @@ def gen_v2(name, F=8, lead=4, diag="", grp=1):
         L_ += [f"v_fma_f32 %[acc{f}], s{w}, |v{a + f}|, %[acc{f}]" for f in range(F)]
         return L_
 
+    ntm = " nt" if diag == "bnt" else ""   # A/B: B rows as non-temporal loads
+
     def bload(dst):
-        L_ = [f"global_load_dwordx4 v[{dst}:{dst + 3}], %[glb_lane], s[{BPTR}:{BPTR + 1}]"]
+        L_ = [f"global_load_dwordx4 v[{dst}:{dst + 3}], %[glb_lane], s[{BPTR}:{BPTR + 1}]{ntm}"]
         if F == 8:
             L_.append(f"global_load_dwordx4 v[{dst + 4}:{dst + 7}], %[glb_lane], "
-                      f"s[{BPTR}:{BPTR + 1}] offset:1024")
+                      f"s[{BPTR}:{BPTR + 1}] offset:1024{ntm}")
         return L_
 
     out_of_line = []
 
     def switch(lab, ret):
+        if diag == "bpre2":
+            # BNXT was requested two switches ago, BNX2 at the last one
+            return [f"{lab}:",
+                    f"s_add_u32 s{COLS}, s{COLS}, 1",
+                    f"s_cmp_ge_u32 s{COLS}, %[ncols]",
+                    "s_cbranch_scc1 8f",
+                    f"s_waitcnt vmcnt({R})",
+                    *[f"v_mov_b32 v{BCUR + f}, v{BNXT + f}" for f in range(F)],
+                    "s_waitcnt vmcnt(0)",
+                    *[f"v_mov_b32 v{BNXT + f}, v{BNX2 + f}" for f in range(F)],
+                    f"s_add_u32 s{TMP2}, s{COLS}, 2",
+                    f"s_cmp_ge_u32 s{TMP2}, %[ncols]",
+                    f"s_cbranch_scc1 {ret}b",
+                    f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
+                    f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0",
+                    *bload(BNX2),
+                    f"s_branch {ret}b"]
         return [f"{lab}:",
                 f"s_add_u32 s{COLS}, s{COLS}, 1",
                 f"s_cmp_ge_u32 s{COLS}, %[ncols]",
@@ -902,8 +925,8 @@ def gen_v2(name, F=8, lead=4, diag="", grp=1):
                 f"s_add_u32 s{TMP2}, s{COLS}, 1",
                 f"s_cmp_ge_u32 s{TMP2}, %[ncols]",
                 f"s_cbranch_scc1 {ret}b",
-                f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
-                f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0",
+                *([] if diag == "bhot" else [f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
+                                             f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0"]),
                 *bload(BNXT),
                 f"s_branch {ret}b"]
 
@@ -939,13 +962,30 @@ def gen_v2(name, F=8, lead=4, diag="", grp=1):
              *bload(BCUR),
              f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
              f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0",
-             *bload(BNXT),
-             f"s_mov_b64 s[{BASE}:{BASE + 1}], %[eb]",
-             f"s_load_dwordx16 s[{SET[0]}:{SET[0] + 15}], s[{BASE}:{BASE + 1}], 0x0",
-             f"s_load_dwordx16 s[{SET[0] + 16}:{SET[0] + 31}], s[{BASE}:{BASE + 1}], 0x40",
-             f"s_mov_b32 s{OFF}, 128",
-             f"s_waitcnt vmcnt({R})",
-             "7:"]
+             *bload(BNXT)]
+    if diag == "bpre2":
+        lines += [f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
+                  f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0",
+                  *bload(BNX2)]
+    if pfn:
+        # warm L2 with the next tile's first two B rows (this wave's columns
+        # 0 and 1 there: 2 KB each, one 32-byte piece per lane): the stream
+        # start of the next tile would otherwise wait for them from HBM.  The
+        # loaded values are never used; the exit's vmcnt(0) retires them.
+        lines += ["s_mov_b64 s[28:29], %[bpn]",
+                  f"global_load_dword v{PF}, %[pf_lane], s[28:29]",
+                  "s_add_u32 s28, s28, %[bstride]",
+                  "s_addc_u32 s29, s29, 0",
+                  f"global_load_dword v{PF + 1}, %[pf_lane], s[28:29]"]
+    if diag == "spf":
+        # A/B: warm the scalar cache / L2 with the next tile's stream head
+        lines += ["s_load_dword s28, %[enb], 0x0", "s_load_dword s29, %[enb], 0x40"]
+    lines += [f"s_mov_b64 s[{BASE}:{BASE + 1}], %[eb]",
+              f"s_load_dwordx16 s[{SET[0]}:{SET[0] + 15}], s[{BASE}:{BASE + 1}], 0x0",
+              f"s_load_dwordx16 s[{SET[0] + 16}:{SET[0] + 31}], s[{BASE}:{BASE + 1}], 0x40",
+              f"s_mov_b32 s{OFF}, 128",
+              f"s_waitcnt vmcnt({(NB - 1) * R + (2 if pfn else 0)})",
+              "7:"]
     for x in range(2):
         lines += step(x)
     # safety bound: a stream holds at most 8 columns x 64 rows (4 KB)
@@ -953,18 +993,19 @@ def gen_v2(name, F=8, lead=4, diag="", grp=1):
     lines += out_of_line
     lines += ["8:", "s_waitcnt vmcnt(0) lgkmcnt(0)"]
     body = "\n".join(f'      "{l}\\n"  \\' for l in lines)
-    vclob = ", ".join(f'"v{i}"' for i in range(BCUR, RING + F * (L + 1)))
+    vclob = ", ".join(f'"v{i}"' for i in range(BCUR, PF + (2 if pfn else 0)))
     named = set()
     for l in lines:
         for lo, hi in re.findall(r"(?<![a-z_])s\[?(\d+)(?::(\d+)\])?", l):
             named.update(range(int(lo), int(hi or lo) + 1))
     sclob = ", ".join(f'"s{i}"' for i in sorted(named))
-    return f"""#define {name}(acc_, lds_lane_, glb_lane_, eb_, bp_, bstride_, ncols_)  \\
+    return f"""#define {name}(acc_, lds_lane_, glb_lane_, eb_, bp_, bstride_, ncols_, bpn_, pf_lane_, enb_)  \\
   asm volatile(  \\
 {body}
       : {", ".join(f'[acc{i}] "+v"(acc_[{i}])' for i in range(F))}  \\
       : [lds_lane] "v"(lds_lane_), [glb_lane] "v"(glb_lane_), [eb] "s"(eb_), [bp] "s"(bp_),  \\
-        [bstride] "s"(bstride_), [ncols] "s"(ncols_)  \\
+        [bstride] "s"(bstride_), [ncols] "s"(ncols_), [bpn] "s"(bpn_), [pf_lane] "v"(pf_lane_),  \\
+        [enb] "s"(enb_)  \\
       : {vclob},  \\
         {sclob}, "scc", "memory")
 """
@@ -1130,9 +1171,11 @@ if __name__ == "__main__":
         text += "\n" + gen_v2("FS_SPARSE2_ASM_F8", F=8,
                               lead=int(os.environ.get("FS_GEN_V2_LEAD8", "3")),
                               diag=os.environ.get("FS_GEN_V2_DIAG", ""),
-                              grp=int(os.environ.get("FS_GEN_V2_GROUP", "1")))
+                              grp=int(os.environ.get("FS_GEN_V2_GROUP", "1")),
+                              pfn=os.environ.get("FS_GEN_V2_PFN", "0") != "0")
     text += "\n" + gen_v2("FS_SPARSE2_ASM_F4", F=4,
-                          lead=int(os.environ.get("FS_GEN_V2_LEAD4", "6")))
+                          lead=int(os.environ.get("FS_GEN_V2_LEAD4", "6")),
+                          pfn=os.environ.get("FS_GEN_V2_PFN", "0") != "0")
     text += "\n" + gen_jit(name="FS_SPARSE_STREAM_ASM_JIT",   # A/B: FS_SPARSE_JIT=1
                             lead=int(os.environ.get("FS_GEN_JIT_LEAD", "12")),
                             bank_shift=bool(int(os.environ.get("FS_GEN_BANK_SHIFT", "0"))))
