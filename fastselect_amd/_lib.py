@@ -530,7 +530,7 @@ class Plan:
         v = (ctypes.c_double * 6)()
         check(_lib.fs_plan_calibration(self._h, v))
         return {"q16": bool(v[0]), "rms": v[1], "max": v[2], "model_sigma": v[3],
-                "band_vs_model": v[4], "guard": bool(v[5])}
+                "band_vs_model": v[4], "guard": bool(v[5]), "row_guard": v[5] == 2.0}
 
     def weighted_pairs(self) -> int:
         """Owned pairs with a non-zero weight in the last pass 2 (-1: not counted)."""

@@ -2347,7 +2347,8 @@ struct Plan {
   int ksplit = 1;               // pass-1 K-split parts of the tail tiles (k_dist)
   int64_t kfull = 0;            // tiles k_dist computes whole (the rest are split)
   int use_q16 = 0;              // pass 1 on packed 16-bit continuous operands
-  double calib[6] = {0, 0, 0, 0, 1, 0};  // plan_calibration (calibrate_band)
+  double calib[7] = {0, 0, 0, 0, 1, 0, 0};  // plan_calibration (calibrate_band, row_guard)
+  double cal32[2] = {0, 0};     // sampled rms / max error of 32-bit operands (row_guard)
   int64_t c_lo = 0, c_hi = 0;   // this rank's continuous columns of the mean correction
   int64_t r_lo = 0, r_hi = 0;   // focal rows scored by this plan (row sharding)
   double2* rspart = nullptr;    // per owned tile row-moment partials [tiles][256]
@@ -2941,6 +2942,7 @@ static int calibrate_band(Plan* g) {
   g->calib[3] = std::sqrt((double)Q.pc / 6.0 + 1.0);
   g->calib[4] = 1.0;
   g->calib[5] = 0.0;
+  g->calib[6] = 0.0;
   if (Q.algo == ALGO_SURF || Q.pc == 0 || Q.n < 2) return FS_OK;
   const int64_t all_pairs = Q.n * (Q.n - 1) / 2;
   const int64_t S = std::min<int64_t>(kCalibPairs, all_pairs);
@@ -3005,6 +3007,8 @@ static int calibrate_band(Plan* g) {
     }
   }
   const double rms[2] = {std::sqrt(ss[0] / (double)S), std::sqrt(ss[1] / (double)S)};
+  g->cal32[0] = rms[1];
+  g->cal32[1] = mx[1];
   const double sigma = g->calib[3];
   const char* guard = std::getenv("FS_Q16_GUARD");
   if (Q.q16 && rms[0] > kCoherence * sigma && !(guard && *guard == '0')) {
@@ -3075,6 +3079,83 @@ static int shard_segments(Plan* g) {
     FS_TRY(dev_alloc(&q, need * sizeof(double), g->device));
     g->spart = (double*)q;
     g->spart_cap = need;
+  }
+  return FS_OK;
+}
+
+// Per-row coherence guard of the 16-bit pass 1 (VERDICT r2 next #1c).  The
+// sampled calibration above sees a few rows whose every feature rounds the
+// same way only by chance, and even a band that covers their pair errors
+// cannot fix what those errors do to the OTHER rows' thresholds: row j's
+// sigma comes from its quantised second moment, to which a coherent row k
+// adds ~2 b_k (D_jk - mu_j) -- large when k sits far from everyone (at the
+// column minima), so every threshold moves the same way and the score
+// errors add up over rows (tests/test_gpu_rowcoherent.py: 4 such rows of
+// 16384 gave 3.3e-5).  The mean correction (k_colrank / k_rowcorr) measures
+// each row's bias directly: corr_k = sum_j err_kj, and for independent
+// rounding b_k = corr_k / (n - 1) has standard deviation sqrt(pc / 36).  So
+// once per feature layout, before any step, the correction is computed over
+// all continuous columns on the 16-bit operands; a row beyond 12 standard
+// deviations turns the 16-bit operands off (32-bit: 256x smaller errors).
+// Every rank computes the same full correction, so every rank decides alike.
+// ~5 ms per fit at cfg4, none per step; FS_Q16_GUARD=0 disables it.
+static int row_guard(Plan* g) {
+  Prepared& Q = g->P;
+  const char* guard = std::getenv("FS_Q16_GUARD");
+  if (!Q.q16 || Q.pc == 0 || Q.n < 2 || Q.algo == ALGO_SURF || (guard && *guard == '0'))
+    return FS_OK;
+  double* corr = nullptr;
+  FS_TRY(dev_alloc((void**)&corr, sizeof(double) * Q.n_pad, g->device));
+  dim3 gq((unsigned)(Q.PW / 64), (unsigned)(Q.n_pad / 64));
+  int rc = FS_OK;
+  if (g->x_is_f64)
+    k_quantize<double><<<gq, 256, 0, g->stream>>>(
+        (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
+        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, 0, Q.pc, g->xqT, g->xs, g->epsT);
+  else
+    k_quantize<float><<<gq, 256, 0, g->stream>>>(
+        (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
+        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, 0, Q.pc, g->xqT, g->xs, g->epsT);
+  rc = launch_check("k_quantize (row guard)");
+  if (!rc) {
+    k_colrank<<<(unsigned)Q.pc, 256, 0, g->stream>>>(g->xqT, Q.n, Q.n_pad, g->rank_shift, Q.q16, 0,
+                                                     g->epsT);
+    rc = launch_check("k_colrank (row guard)");
+  }
+  if (!rc) {
+    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, g->stream>>>(g->epsT, Q.n, Q.n_pad, 0, Q.pc,
+                                                                corr);
+    rc = launch_check("k_rowcorr (row guard)");
+  }
+  std::vector<double> h((size_t)Q.n);
+  if (!rc && (hipMemcpyAsync(h.data(), corr, sizeof(double) * Q.n, hipMemcpyDeviceToHost,
+                             g->stream) != hipSuccess ||
+              hipStreamSynchronize(g->stream) != hipSuccess)) {
+    (void)hipGetLastError();
+    set_error("row guard: device-to-host copy failed");
+    rc = FS_EHIP;
+  }
+  dev_free(corr);
+  if (rc) return rc;
+  double worst = 0.0;
+  for (double c : h) worst = std::max(worst, std::fabs(c) / (double)(Q.n - 1));
+  const double limit = 12.0 * std::sqrt((double)Q.pc / 36.0 + 1.0);
+  g->calib[6] = worst / limit;
+  if (worst > limit) {
+    g->use_q16 = 0;
+    g->calib[5] = 2.0;
+    if (set_integer_scale(Q, 0)) return FS_EINVAL;
+    Q.amb_delta = calibrated_delta(Q.amb_delta_model, Q.SC, g->cal32[0], g->cal32[1]);
+    g->calib[0] = 0.0;
+    g->calib[1] = g->cal32[0];
+    g->calib[2] = g->cal32[1];
+    g->calib[4] = Q.amb_delta / Q.amb_delta_model;
+  }
+  if (trace_on()) {
+    char msg[160];
+    snprintf(msg, sizeof msg, "row guard: max |row bias| %.1f (limit %.1f) -> q16 %d", worst,
+             limit, Q.q16);
+    trace_mark(msg);
   }
   return FS_OK;
 }
@@ -3151,6 +3232,7 @@ static int plan_layout(Plan* g) {
       (rc = h2d(g, g->dtab, Q.dtab.data(), Q.dtab.size())))
     return rc;
   if ((rc = calibrate_band(g))) return rc;
+  if ((rc = row_guard(g))) return rc;
   if (g->calib[5] != 0.0) {
     // the coherence guard switched to 32-bit operands: new scale, histogram shift
     for (int64_t c = 0; c < Q.PW; c++) qs[c] = Q.scale[c] * Q.SC;

@@ -346,7 +346,9 @@ FS_API int fs_plan_info(const fs_plan* plan, int64_t* owned_tiles, double* pair_
  * [1] / [2] rms / max |quantised - reference| distance error over 4096
  * sampled pairs (integer units), [3] the independent-rounding model's
  * standard deviation sqrt(pc/6 + 1), [4] band / model band, [5] 1 if the
- * coherence guard turned 16-bit operands off.  CPU plans: out[0..5] =
+ * coherence guard turned 16-bit operands off, 2 if the per-row guard did (a
+ * row whose mean pass-1 error, measured by the mean correction, exceeds 12
+ * standard deviations of independent rounding).  CPU plans: out[0..5] =
  * {0, 0, 0, model sigma, 1, 0}. */
 FS_API int fs_plan_calibration(const fs_plan* plan, double* out);
 /* Owned pairs that carried a non-zero pass-2 weight in the last pass 2 (the
