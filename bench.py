@@ -1,6 +1,13 @@
 """Benchmark: MultiSURF feature scoring on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--samples 20000 --features 20000]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg4]
+                    [--samples 20000 --features 20000]
+
+--config picks a BASELINE.json configuration: cfg4 (default, the headline:
+MultiSURF 20000 x 20000), cfg2 (MultiSURF 5000 x 5000), cfg3 (ReliefF k=10,
+20000 x 2000), cfg5s (SURF* 10000 x 50000), cfg5m (MultiSURF* 10000 x
+50000).  Every line carries the dominant kernel's roofline and, at N=1, a CPU
+baseline from the oracle on a bounded sample of the same workload.
 
 For N > 1 launch one process per GPU with torch.distributed.run; the pair
 tiles are sharded round-robin over the ranks and the three small exchange
@@ -43,8 +50,22 @@ sys.path.insert(0, ROOT)
 # slots are the cost of two FMAs, so one PFE is priced at 4 FMA-equivalent
 # FLOPs against that peak ("Kernels").
 VALU_PEAK_TFLOPS = 157.3
+# float64 vector peak (SURF's float64 distance kernel k_dist_f64: v_add_f64
+# sub + v_add_f64 |.| per PFE, each priced as one FMA): AMD's MI355X figure,
+# half the FP32 vector rate (16 f64 lanes per SIMD cycle); not re-measured here
+VALU_F64_PEAK_TFLOPS = 78.6
 FLOP_PER_PFE = 4
 HBM_PEAK_GBPS = 8000.0
+
+# BASELINE.json configs (make_classification n_informative=20, n_redundant=R,
+# random_state=42)
+CONFIGS = {
+    "cfg2": dict(algo="multisurf", n=5000, p=5000, red=100, star=False, idx=1),
+    "cfg3": dict(algo="relieff", n=20000, p=2000, red=50, k=10, star=False, idx=2),
+    "cfg4": dict(algo="multisurf", n=20000, p=20000, red=100, star=False, idx=3),
+    "cfg5s": dict(algo="surf", n=10000, p=50000, red=100, star=True, idx=4),
+    "cfg5m": dict(algo="multisurf", n=10000, p=50000, red=100, star=True, idx=4),
+}
 TRAFFIC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
@@ -120,11 +141,62 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def make_data(n, p, seed):
+def make_data(n, p, seed, red=100):
     from sklearn.datasets import make_classification
-    X, y = make_classification(n_samples=n, n_features=p, n_informative=20, n_redundant=100,
+    X, y = make_classification(n_samples=n, n_features=p, n_informative=20, n_redundant=red,
                                random_state=seed)
     return X, y
+
+
+def oracle_threads():
+    """Threads of the CPU baseline: this job's CPU share (OMP_NUM_THREADS, 16
+    on the GPU box, where nproc counts the whole machine), at most 16."""
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    return min(threads, 16)
+
+
+def full_host_note(value, threads):
+    """The baseline's full-host figure by linear scaling (the oracle is a
+    per-focal-sample parallel loop, SURVEY.md §8d): stated beside the
+    measured one (VERDICT r2 weak #8), labelled as extrapolated."""
+    cores = os.cpu_count() or threads
+    return {"machine_cores": cores,
+            "value_full_host_extrapolated": value * cores / threads,
+            "full_host_note": f"measured on {threads} threads (this job's CPU share); x{cores}/"
+                              f"{threads} linear scaling to all {cores} cores of the host, "
+                              f"not measured"}
+
+
+def cpu_baseline_rows(algo, X, y, k, star, budget_s=25.0):
+    """Oracle ReliefF / SURF on the first m focal samples, extrapolated to n
+    (as cpu_baseline)."""
+    from oracle import oracle as O
+    O.build()
+    threads = oracle_threads()
+    n, p = X.shape
+
+    def run(m):
+        if algo == "relieff":
+            return O.relieff_scores(X, y, n_neighbors=k, i_range=(0, m), n_jobs=threads)
+        return O.surf_scores(X, y, use_star=star, i_range=(0, m), n_jobs=threads)
+    run(threads)  # warm-up
+    m = min(n, 2 * threads)
+    t0 = time.perf_counter()
+    run(m)
+    t = time.perf_counter() - t0
+    m = int(min(n, max(threads, threads * round(budget_s / t * m / threads))))
+    t0 = time.perf_counter()
+    run(m)
+    t = time.perf_counter() - t0
+    t_full = t * n / m
+    name = "ReliefF" if algo == "relieff" else ("SURF*" if star else "SURF")
+    out = {"value": n * p / t_full, "unit": "feature-scores/s", "cores": threads, "kind": "port",
+           "cpu_model": cpu_model(),
+           "sample": f"oracle {name} (C/OpenMP restatement of the reference backend='cpu') on "
+                     f"focal samples [0, {m}) of the same {n}x{p} data: {t:.2f} s, extrapolated "
+                     f"x{n / m:.1f} to {t_full:.1f} s"}
+    out.update(full_host_note(out["value"], threads))
+    return out
 
 
 def cpu_baseline(x, y, budget_s=25.0):
@@ -133,8 +205,7 @@ def cpu_baseline(x, y, budget_s=25.0):
     per-sample rate, then a ~budget_s sample whose time is reported."""
     from oracle import oracle as O
     O.build()
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    threads = min(threads, 16)
+    threads = oracle_threads()
     n, p = x.shape
     O.multisurf_scores(x, y, i_range=(0, threads), n_jobs=threads)  # warm-up
     m = min(n, 2 * threads)
@@ -150,12 +221,14 @@ def cpu_baseline(x, y, budget_s=25.0):
     # accumulation: ~(2 + near fraction) * n^2 * p PFE; the
     # published reference CPU rate is ~5e9 PFE/s
     pfe = 2.0 * m * (n - 1) * p
-    return {"value": n * p / t_full, "unit": "feature-scores/s", "cores": threads,
-            "kind": "port", "cpu_model": cpu_model(),
-            "pfe_per_s_distance_passes": pfe / t, "reference_published_pfe_per_s": 5e9,
-            "sample": f"oracle MultiSURF (C/OpenMP restatement of the reference backend='cpu') "
-                      f"on focal samples [0, {m}) of the same {n}x{p} data: {t:.2f} s, "
-                      f"extrapolated x{n / m:.1f} to {t_full:.1f} s"}
+    out = {"value": n * p / t_full, "unit": "feature-scores/s", "cores": threads,
+           "kind": "port", "cpu_model": cpu_model(),
+           "pfe_per_s_distance_passes": pfe / t, "reference_published_pfe_per_s": 5e9,
+           "sample": f"oracle MultiSURF (C/OpenMP restatement of the reference backend='cpu') "
+                     f"on focal samples [0, {m}) of the same {n}x{p} data: {t:.2f} s, "
+                     f"extrapolated x{n / m:.1f} to {t_full:.1f} s"}
+    out.update(full_host_note(out["value"], threads))
+    return out
 
 
 def fit_ms(X, y, star, repeats=5):
@@ -194,15 +267,136 @@ def sharded_fit_ms(X, y, star, local, barrier, sync, dist, repeats=3):
     return float(np.median(ts)), ts
 
 
+def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_backend):
+    """ReliefF (cfg3) / SURF* (cfg5s): a step is one scoring pass of a
+    resident row plan (fs_plan_score: pass 1, neighbour selection or mean,
+    pass 2 / update) over X in HBM; at N > 1 rank r scores the focal samples
+    parallel.shard_rows(n, r, N) and one all-reduce sums the vectors."""
+    import torch
+
+    from fastselect_amd import _lib
+    from fastselect_amd.parallel import shard_rows
+    algo, n, p = cfg["algo"], args.samples, args.features
+    t0 = time.perf_counter()
+    X, y = make_data(n, p, args.seed, cfg["red"])
+    if algo == "relieff":
+        from fastselect_amd.ReliefF import relieff_inputs
+        xin, ye, recip, isd, pri = relieff_inputs(X, y, 10, "gpu" if on_gpu else "cpu", local)
+        kw = dict(k=cfg["k"], class_probs=pri)
+    else:
+        from fastselect_amd.SURF import surf_inputs
+        xin = np.ascontiguousarray(X, dtype=np.float64)
+        isd, recip = surf_inputs(xin, 10, "gpu" if on_gpu else "cpu", local)
+        ye = np.asarray(y).astype(np.int32)
+        kw = dict(use_star=args.star)
+    log(f"rank {rank}/{world}: data {n}x{p} ready in {time.perf_counter() - t0:.1f} s")
+    rows = shard_rows(n, rank, world)
+    tdev = torch.device("cuda", local) if on_gpu else torch.device("cpu")
+    stream = torch.cuda.current_stream().cuda_stream if on_gpu else 0
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    plan = _lib.RowsPlan(args.backend, algo, xin, ye, recip, isd, rows=rows, device=local,
+                         stream=stream, **kw)
+    sums = torch.zeros(p, dtype=torch.float64, device=tdev)
+    sync()
+    setup_ms = (time.perf_counter() - t0) * 1e3
+
+    def step():
+        plan.score(sums.data_ptr())
+        if world > 1:
+            dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+
+    for w in range(args.warmup):
+        step()
+        sync()
+        log(f"warmup {w} done")
+    barrier()
+    sync()
+    t_start = time.perf_counter()
+    kms = {0: [], 1: [], 2: []}
+    for _ in range(args.steps):
+        step()
+        if on_gpu:
+            for w in kms:
+                kms[w].append(plan.kernel_ms(w))
+    sync()
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    ms_per_step = float(t.item()) / args.steps * 1e3
+    roofline = None
+    if on_gpu:
+        nb = (n + 127) // 128
+        b0, b1 = rows[0] // 128, (rows[1] + 127) // 128
+        # distance pairs this rank computes: every upper-triangle tile that
+        # touches its focal blocks (algorithmic count: unique pairs of them)
+        tiles = sum(1 for a in range(nb) for b in range(a, nb) if b0 <= a < b1 or b0 <= b < b1)
+        pairs = min(tiles * 128.0 * 128.0, n * (n - 1) / 2.0)
+        k_ms = float(np.mean(kms[0]))
+        name = "k_dist" if algo == "relieff" else "k_dist_f64"
+        peak = VALU_PEAK_TFLOPS if algo == "relieff" else VALU_F64_PEAK_TFLOPS
+        achieved = FLOP_PER_PFE * pairs * p / (k_ms * 1e-3) / 1e12
+        roofline = {"bound": "valu", "kernel": name, "achieved": achieved, "peak": peak,
+                    "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
+                    "flop_per_pfe": FLOP_PER_PFE, "pfe_per_launch": pairs * p,
+                    "pfe_per_s": pairs * p / (k_ms * 1e-3),
+                    "kernel_ms": {name: k_ms, "stage2": float(np.mean(kms[1]))}}
+        if algo == "relieff":
+            # k_rf_select: one float64 distance row per focal sample read per launch
+            sel_ms = float(np.mean(kms[2]))
+            rbytes = (rows[1] - rows[0]) * n * 8.0
+            roofline["kernel_ms"]["k_rf_select"] = sel_ms
+            roofline["k_rf_select_hbm"] = {"bytes": rbytes, "GBps": rbytes / (sel_ms * 1e-3) / 1e9,
+                                           "peak": HBM_PEAK_GBPS,
+                                           "frac": rbytes / (sel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+            roofline["peak_note"] = ("k_dist here runs 16-bit operands (v_sad_u16, 2 PFE per "
+                                     "issue slot pair): priced as the fp32 path, as cfg4")
+        else:
+            roofline["peak_note"] = ("float64 vector peak (AMD MI355X figure, half the fp32 rate); "
+                                     "2 v_add_f64 per PFE, each priced as one FMA")
+    plan.close()
+    out = None
+    if rank == 0:
+        name = "ReliefF k=%d" % cfg["k"] if algo == "relieff" else ("SURF*" if args.star else "SURF")
+        out = {
+            "metric": f"feature-scores/sec (n*p/s) {name} fp32",
+            "value": n * p / (ms_per_step * 1e-3), "unit": "feature-scores/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": "fp32" if algo == "relieff" else "fp64 distances",
+            "data": f"synthetic make_classification(n_informative=20, n_redundant={cfg['red']}, "
+                    f"random_state=42)",
+            "config": {"workload": f"{name} n={n} p={p} (BASELINE configs[{cfg['idx']}])",
+                       "name": args.config, "n_samples": n, "n_features": p,
+                       "parallelism": f"focal-row shard x{world}"
+                                      + (f", {'RCCL' if dist_backend == 'nccl' else dist_backend}"
+                                         f" all-reduce" if world > 1 else "")},
+            "roofline": roofline, "setup_ms": setup_ms,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            log("timing CPU baseline (oracle) ...")
+            out["cpu_baseline"] = cpu_baseline_rows(algo, X, y, cfg.get("k", 0), args.star)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--samples", type=int, default=20000)
-    ap.add_argument("--features", type=int, default=20000)
+    ap.add_argument("--config", default="cfg4", choices=sorted(CONFIGS),
+                    help="BASELINE.json configuration (cfg4: the headline MultiSURF 20000x20000)")
+    ap.add_argument("--samples", type=int, default=None)
+    ap.add_argument("--features", type=int, default=None)
     ap.add_argument("--seed", type=int, default=42)
     ap.add_argument("--star", action="store_true")
+    ap.add_argument("--no-q32", action="store_true",
+                    help="skip the 32-bit pass-1 comparison step time (MultiSURF at N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-fit", action="store_true", help="skip the end-to-end fit() timing")
     ap.add_argument("--backend", default="gpu", choices=("gpu", "cpu"),
@@ -213,6 +407,10 @@ def main():
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
+    cfg = CONFIGS[args.config]
+    args.samples = args.samples or cfg["n"]
+    args.features = args.features or cfg["p"]
+    args.star = args.star or cfg["star"]
     dist_backend = args.dist_backend or ("nccl" if args.backend == "gpu" else "gloo")
 
     # --gpus N without a launcher: start the N ranks here, before any GPU call
@@ -252,8 +450,12 @@ def main():
         if world > 1:
             dist.barrier()
 
+    if cfg["algo"] != "multisurf":
+        return bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier,
+                          dist_backend)
+
     t0 = time.perf_counter()
-    X, y = make_data(args.samples, args.features, args.seed)
+    X, y = make_data(args.samples, args.features, args.seed, cfg["red"])
     x = X.astype(np.float32)
     ranges = (x.max(axis=0) - x.min(axis=0)).astype(np.float32)
     ranges[ranges == 0] = 1
@@ -276,6 +478,7 @@ def main():
     sync()
     setup_ms = (time.perf_counter() - t0) * 1e3
     tiles, _, _ = job.info()
+    q16_used = bool(job.plan.calibration()["q16"]) if on_gpu else False
 
     for w in range(args.warmup):
         job.step()
@@ -347,6 +550,28 @@ def main():
             "hbm_peak_GBps": HBM_PEAK_GBPS,
         }
     job.close()
+    # the decision-finer 32-bit pass 1 (FS_Q16=0) beside the default step
+    # (VERDICT r2 next #6): same job, 32-bit operands forced
+    q32 = None
+    if on_gpu and world == 1 and not args.no_q32:
+        os.environ["FS_Q16"] = "0"
+        try:
+            with resident_x(x, args.backend, local):
+                job32 = ShardedMultiSURF(x, y, recip, is_disc, use_star=args.star,
+                                         backend=args.backend, device=local)
+            job32.step()
+            sync()
+            t_q = time.perf_counter()
+            ks = max(1, min(args.steps, 3))
+            for _ in range(ks):
+                job32.step()
+            sync()
+            q32 = {"ms_per_step": (time.perf_counter() - t_q) / ks * 1e3,
+                   "kernel_ms": {"k_dist": job32.kernel_ms(0), "pass2": job32.kernel_ms(1)},
+                   "steps": ks}
+            job32.close()
+        finally:
+            del os.environ["FS_Q16"]
     setup = torch.tensor([setup_ms], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
     if world > 1:
         dist.all_reduce(setup, op=dist.ReduceOp.MAX)
@@ -371,7 +596,8 @@ def main():
                      "f32 pair weights, f64 accumulation",
             "data": "synthetic make_classification(n_informative=20, n_redundant=100, random_state=42)",
             "config": {"workload": f"MultiSURF{'*' if args.star else ''} n={n} p={p} "
-                                   f"(BASELINE configs[3])",
+                                   f"(BASELINE configs[{cfg['idx']}])",
+                       "name": args.config,
                        "n_samples": n, "n_features": p,
                        "parallelism": f"pair-tile shard x{world}"
                                       + (f", {'RCCL' if dist_backend == 'nccl' else dist_backend}"
@@ -381,7 +607,10 @@ def main():
             # X to the GPUs (per-rank rows + all-gather at N > 1) + plan
             # creation (device ranges, calibration, layout), max over ranks
             "setup_ms": float(setup.item()),
+            "pass1_operands": "16-bit" if q16_used else "32-bit",
         }
+        if q32 is not None:
+            out["q32_pass1"] = q32
     if on_gpu and world == 1 and not args.no_fit:
         log("timing end-to-end fit() ...")
         med, ts = fit_ms(X, y, args.star)

@@ -2393,7 +2393,9 @@ struct Plan {
   int64_t n_tie_rows = 0;      // ReliefF rows re-ordered by k_rf_ties
   void* sort_scratch = nullptr;  // pair-list sort (fs_sort.hip)
   size_t sort_scratch_bytes = 0;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // ev[0..1] distance kernel, ev[2..3] score kernel(s) / ReliefF selection +
+  // update, ev[4..5] ReliefF's first k_rf_select launch (plan_kernel_ms)
+  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   std::vector<void*> owned;         // buffers sized by n (live as long as the plan)
   std::vector<void*> owned_layout;  // buffers sized by the feature layout (PW)
   std::vector<void*> scratch;       // buffers of one plan_score call
@@ -3736,8 +3738,8 @@ int plan_weighted_pairs(Plan* g, int64_t* pairs) {
 
 double plan_kernel_ms(const Plan* g, int which) {
   float ms = -1.0f;
-  hipEvent_t a = which == 0 ? g->ev[0] : g->ev[2];
-  hipEvent_t b = which == 0 ? g->ev[1] : g->ev[3];
+  if (which < 0 || which > 2) return -1.0;
+  hipEvent_t a = g->ev[2 * which], b = g->ev[2 * which + 1];
   if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess) {
     (void)hipGetLastError();
     return -1.0;
@@ -3998,7 +4000,9 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
     return launch_check("k_rf_select");
   };
   // 1. k-th keys from the quantised distances
+  FS_HIP(hipEventRecord(g->ev[4], g->stream));
   FS_TRY(select(0));
+  FS_HIP(hipEventRecord(g->ev[5], g->stream));
   // 2. exact keys inside the band (quantisation error + float32 rounding)
   const double band_abs = 2.0 * Q.amb_delta, band_rel = 2.0 * 1.2e-7;
   g->n_refined = 0;
@@ -4107,8 +4111,10 @@ static int plan_score_relieff(Plan* g, double* sums_dev) {
   if (rc == FS_OK) rc = dalloc(g, &nfound, (size_t)Q.n * C);
   g->alloc_target = 0;
   if (rc || (rc = h2d(g, dcc, cc.data(), C)) || (rc = h2d(g, dprior, prior.data(), C)) ||
-      (rc = run_quantize_dist(g)) || (rc = relieff_select(g, dcc, nbr, nfound)))
+      (rc = run_quantize_dist(g)))
     return rc;
+  FS_HIP(hipEventRecord(g->ev[2], g->stream));
+  if ((rc = relieff_select(g, dcc, nbr, nfound))) return rc;
   if (trace_on()) {
     (void)hipStreamSynchronize(g->stream);
     std::fprintf(stderr, "[fs_trace] relieff: %lld exact pairs, %lld tie rows\n",
@@ -4117,6 +4123,7 @@ static int plan_score_relieff(Plan* g, double* sums_dev) {
   k_rf_update<<<dim3((unsigned)(Q.PW / 64), (unsigned)nrb), 256, 0, g->stream>>>(
       g->xs, g->r_lo, g->r_hi, Q.PW, Q.PC, g->lab, dprior, C, k, nbr, nfound, part);
   FS_TRY(launch_check("k_rf_update"));
+  FS_HIP(hipEventRecord(g->ev[3], g->stream));
   FS_HIP(hipMemsetAsync(sums_dev, 0, sizeof(double) * Q.n_kept, g->stream));
   k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(part, nrb, Q.PW, g->out_pos,
                                                                    sums_dev);

@@ -357,7 +357,9 @@ FS_API int fs_plan_calibration(const fs_plan* plan, double* out);
 FS_API int fs_plan_weighted_pairs(const fs_plan* plan, int64_t* pairs);
 /* Average duration in milliseconds of the last pass1 / pass2 distance and
  * score kernels, measured with HIP events on the plan's stream (GPU only;
- * -1 when unavailable).  which: 0 = distance kernel, 1 = score kernel. */
+ * -1 when unavailable).  which: 0 = distance kernel, 1 = score kernel (for
+ * ReliefF plans: neighbour selection, exact refinement and update), 2 =
+ * ReliefF's first k_rf_select launch. */
 FS_API double fs_plan_kernel_ms(const fs_plan* plan, int which);
 FS_API int fs_plan_destroy(fs_plan* plan);
 
