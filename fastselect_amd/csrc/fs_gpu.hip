@@ -1806,13 +1806,14 @@ __device__ __forceinline__ uint32_t rf_key(double d, double inv_sc) {
 }
 
 // One workgroup per focal row.  For each class c the k_c-th smallest key T_c
-// is found digit by digit (4 x 8-bit LDS histograms) -> tkey[i][c], and
-// tneed[i][c] = how many keys equal to T_c belong to the k_c nearest (0 when
-// the class is taken whole).  With `collect`, wave (c % 4) then scans j in
-// ascending order and takes every key < T_c plus the first tneed keys ==
-// T_c (index order; rows where more keys equal T_c than are needed are
-// re-ordered the reference's way by k_rf_ties), and teq[i][c] counts the
-// keys equal to T_c.
+// is found digit by digit (a 10-bit LDS histogram right below the row's
+// common key bits, then a ranked gather of the chosen bucket, or 8-bit
+// passes when the bucket is big) -> tkey[i][c], and tneed[i][c] = how many
+// keys equal to T_c belong to the k_c nearest (0 when the class is taken
+// whole).  With `collect`, every key < T_c (index order) and then the first
+// tneed keys == T_c (index order) go to nbr (rows where more keys equal T_c
+// than are needed are re-ordered the reference's way by k_rf_ties), and
+// teq[i][c] counts the keys equal to T_c.
 template <bool STAGE>
 __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D, int64_t n,
                                                    int64_t n_pad, double inv_sc,
@@ -1823,11 +1824,15 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
                                                    int32_t* __restrict__ tneed,
                                                    int32_t* __restrict__ teq,
                                                    int32_t* __restrict__ nbr,
-                                                   int32_t* __restrict__ nfound) {
-  // hist[n_classes][256], prefix[C], need[C], then (STAGE) the row's keys
+                                                   int32_t* __restrict__ nfound,
+                                                   double band_abs, double band_rel,
+                                                   int2* __restrict__ list, int64_t cap,
+                                                   unsigned long long* __restrict__ count) {
+  // hist[n_classes][1024 (n_classes <= 8) or 256], prefix[C], need[C], then
+  // (STAGE) the row's keys and class codes
   extern __shared__ uint32_t sh[];
   uint32_t* hist = sh;
-  uint32_t* prefix = sh + n_classes * 256;
+  uint32_t* prefix = sh + n_classes * (n_classes <= 8 ? 1024 : 256);
   uint32_t* need = prefix + n_classes;
   uint32_t* keys = need + n_classes;
   uint8_t* labs = (uint8_t*)(keys + n);  // STAGE: class codes (< 64)
@@ -1890,8 +1895,13 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
   }
   const uint32_t diff = kor & ~kand;  // bits that are not common
   const int top = diff ? 31 - __builtin_clz(diff) : 0;
-  const int d_start = top / 8;
-  const uint32_t common = d_start >= 3 ? 0u : (kand & (0xFFFFFFFFu << (8 * (d_start + 1))));
+  // Pass 1 takes the WB bits [lo1, top] right below the common prefix (a
+  // byte-aligned first digit would hold only the few varying exponent bits:
+  // ~20 of 256 bins used, LDS atomics serialising on them); 10-bit digits
+  // when the histograms fit (n_classes <= 8), else 8.
+  const int wb = n_classes <= 8 ? 10 : 8;
+  const int lo1 = top - (wb - 1) > 0 ? top - (wb - 1) : 0;
+  const uint32_t common = top >= 31 ? 0u : (kand & ~(0xFFFFFFFFu >> (31 - top)));
   for (int c = tid; c < n_classes; c += nt) {
     const int64_t members = class_count[c] - (c == li ? 1 : 0);
     const int64_t kc = members < k ? members : k;
@@ -1901,89 +1911,261 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
     need[c] = (uint32_t)kc;
     if (kc == members) prefix[c] = 0xFFFFFFFFu, need[c] = 0;
   }
-  __syncthreads();
-  for (int d = d_start; d >= 0; d--) {
-    for (int e = tid; e < n_classes * 256; e += nt) hist[e] = 0;
+  // One pass: histogram of the digit [lo, hi) of the keys whose bits >= hi
+  // match their class's prefix, then per class (one wave each) the bucket
+  // holding the need-th key, by a wave prefix sum over the bins.
+  __shared__ uint32_t bcount[64];  // keys in the chosen bucket, per class
+  auto radix_pass = [&](int lo, int hi) {
+    const int nbins = 1 << (hi - lo);
+    const uint32_t dmask = (uint32_t)nbins - 1u;
+    for (int e = tid; e < n_classes * nbins; e += nt) hist[e] = 0;
     __syncthreads();
-    const int sh_hi = 8 * (d + 1);
     for (int64_t j = tid; j < n; j += nt) {
       if (j == i) continue;
       const int32_t c = lab_of(j);
       if (need[c] == 0) continue;
       const uint32_t key = key_of(j);
-      if (sh_hi < 32 && (key >> sh_hi) != (prefix[c] >> sh_hi)) continue;
-      atomicAdd(&hist[c * 256 + ((key >> (8 * d)) & 0xFF)], 1u);
+      if (hi < 32 && (key >> hi) != (prefix[c] >> hi)) continue;
+      atomicAdd(&hist[c * nbins + ((key >> lo) & dmask)], 1u);
     }
     __syncthreads();
-    // per class (one wave each): the bucket holding the need-th key, by a
-    // wave prefix sum over 4 bins per lane
-    {
-      const int wv = tid >> 6, ln = tid & 63;
-      for (int c = wv; c < n_classes; c += nwaves) {
-        const uint32_t nd = need[c];
-        if (nd == 0) continue;
-        const uint32_t* hc = hist + c * 256 + 4 * ln;
-        const uint32_t h0 = hc[0], h1 = hc[1], h2 = hc[2], h3 = hc[3];
-        const uint32_t tot = h0 + h1 + h2 + h3;
-        uint32_t incl = tot;
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t t = __shfl_up(incl, o);
-          if (ln >= o) incl += t;
+    const int wv = tid >> 6, ln = tid & 63;
+    const int bpl = (nbins + 63) >> 6;  // bins per lane
+    for (int c = wv; c < n_classes; c += nwaves) {
+      const uint32_t nd = need[c];
+      if (nd == 0) continue;
+      const uint32_t* hc = hist + c * nbins;
+      const int b0 = ln * bpl;
+      uint32_t tot = 0u;
+      for (int q = 0; q < bpl; q++)
+        if (b0 + q < nbins) tot += hc[b0 + q];
+      uint32_t incl = tot;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o);
+        if (ln >= o) incl += t;
+      }
+      // the first lane whose inclusive sum reaches nd owns the bucket
+      const uint64_t m = __ballot(incl >= nd);
+      const int owner = (int)__builtin_ctzll(m);
+      if (ln == owner) {
+        uint32_t cum = incl - tot;
+        int b = b0;
+        for (; b < b0 + bpl - 1; b++) {
+          if (cum + hc[b] >= nd) break;
+          cum += hc[b];
         }
-        const uint32_t excl = incl - tot;
-        // the first lane whose inclusive sum reaches nd owns the bucket
-        const uint64_t m = __ballot(incl >= nd);
-        const int owner = (int)__builtin_ctzll(m);
-        if (ln == owner) {
-          uint32_t cum = excl, b = 4 * ln;
-          const uint32_t hv[4] = {h0, h1, h2, h3};
-          for (int q = 0; q < 4; q++, b++) {
-            if (cum + hv[q] >= nd) break;
-            cum += hv[q];
-          }
-          prefix[c] |= b << (8 * d);
-          need[c] = nd - cum;
-        }
+        prefix[c] |= (uint32_t)b << lo;
+        need[c] = nd - cum;
+        bcount[c] = hc[b];
       }
     }
     __syncthreads();
+  };
+  __syncthreads();
+  radix_pass(lo1, top + 1);
+  if (lo1 > 0) {
+    // Small buckets (<= 64 keys: the common case, the k nearest sit in the
+    // sparse low tail) finish in one gather: the bucket's keys go to a list
+    // (in the histogram space, free now) and the need-th smallest is found by
+    // ranking.  Classes with bigger buckets (ties, discrete data) continue
+    // with 8-bit passes below lo1.
+    __shared__ uint32_t gcnt[64];
+    __shared__ int any_big;
+    uint32_t* list = hist;  // [class][64]
+    if (tid == 0) any_big = 0;
+    for (int c = tid; c < n_classes; c += nt) {
+      gcnt[c] = 0u;
+      if (need[c] != 0 && bcount[c] > 64u) any_big = 1;
+    }
+    __syncthreads();
+    for (int64_t j = tid; j < n; j += nt) {
+      if (j == i) continue;
+      const int32_t c = lab_of(j);
+      if (need[c] == 0 || bcount[c] > 64u) continue;
+      const uint32_t key = key_of(j);
+      if ((key >> lo1) != (prefix[c] >> lo1)) continue;
+      const uint32_t slot = atomicAdd(&gcnt[c], 1u);
+      list[c * 64 + slot] = key;
+    }
+    __syncthreads();
+    const int wv = tid >> 6, ln = tid & 63;
+    for (int c = wv; c < n_classes; c += nwaves) {
+      const uint32_t nd = need[c], m = bcount[c];
+      if (nd == 0 || m > 64u) continue;
+      const uint32_t v = ln < (int)m ? list[c * 64 + ln] : 0xFFFFFFFFu;
+      uint32_t nlt = 0u, nle = 0u;
+      for (uint32_t q = 0; q < m; q++) {
+        const uint32_t w = list[c * 64 + q];
+        nlt += w < v;
+        nle += w <= v;
+      }
+      // the need-th smallest: nlt < nd <= nle (ties: one owner per value,
+      // any lane holding it writes the same result)
+      const bool own = ln < (int)m && nlt < nd && nd <= nle;
+      const uint64_t mo = __ballot(own);
+      if (mo != 0ull && ln == (int)__builtin_ctzll(mo)) {
+        prefix[c] = v;
+        need[c] = nd - nlt;
+      }
+    }
+    __syncthreads();
+    if (any_big)
+      for (int hi = lo1; hi > 0; hi -= 8) radix_pass(hi - 8 > 0 ? hi - 8 : 0, hi);
   }
   for (int c = tid; c < n_classes; c += nt) {
     tkey[i * n_classes + c] = prefix[c];
     tneed[i * n_classes + c] = (int32_t)need[c];
   }
-  if (!collect) return;
-  // Ordered collection, one wave per class.
-  const int wave = tid >> 6, lane = tid & 63;
-  for (int c = wave; c < n_classes; c += nwaves) {
-    const uint32_t T = prefix[c];
-    uint32_t eq_left = need[c];
-    int64_t cnt = 0, n_eq = 0;
-    int32_t* out = nbr + (i * n_classes + c) * k;
-    for (int64_t j0 = 0; j0 < n; j0 += 64) {
-      const int64_t j = j0 + lane;
-      bool lt = false, eq = false;
-      if (j < n && j != i && lab_of(j) == c) {
-        const uint32_t key = key_of(j);
-        lt = key < T;
-        eq = key == T;
+  if (!collect) {
+    // k_rf_flag's sweep on the staged row (list != null): candidates whose
+    // quantised key lies within the band of their class's k-th key go to the
+    // exact-pair list, one global atomic per wave with any
+    if (list == nullptr) return;
+    const int lane = tid & 63;
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (int64_t j0 = 0; j0 < n; j0 += nt) {
+      const int64_t j = j0 + tid;
+      bool flag = false;
+      if (j < n && j != i) {
+        const int32_t c = lab_of(j);
+        if (need[c] != 0) {
+          const double T = (double)__uint_as_float(prefix[c]);
+          const double kv = (double)__uint_as_float(key_of(j));
+          flag = fabs(kv - T) <= band_abs + band_rel * T;
+        }
       }
-      const uint64_t meq = __ballot(eq);
-      const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-      // equal keys: only the first eq_left (in j order) are taken
-      const uint32_t eq_rank = (uint32_t)__popcll(meq & below);
-      const bool take_eq = eq && eq_rank < eq_left;
-      const bool take = lt || take_eq;
-      const uint64_t mt = __ballot(take);
-      if (take) out[cnt + __popcll(mt & below)] = (int32_t)j;
-      cnt += __popcll(mt);
-      const uint32_t eq_taken = (uint32_t)__popcll(meq);
-      n_eq += eq_taken;
-      eq_left = eq_taken >= eq_left ? 0u : eq_left - eq_taken;
+      const uint64_t m = __ballot(flag);
+      if (m == 0ull) continue;
+      const int leader = (int)__builtin_ctzll(m);
+      unsigned long long base = 0ull;
+      if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(m));
+      base = __shfl(base, leader);
+      if (flag) {
+        const unsigned long long kk = base + (unsigned long long)__popcll(m & below);
+        if ((int64_t)kk < cap) list[kk] = make_int2((int)i, (int)j);
+      }
     }
-    if (lane == 0) {
-      nfound[i * n_classes + c] = (int32_t)cnt;
-      teq[i * n_classes + c] = (int32_t)n_eq;
+    return;
+  }
+  // Ordered collection over all waves: wave w takes the contiguous chunk
+  // [j_w, j_w+1) of the row.  Pass 1 counts, per class, the keys below the
+  // k-th key T and the keys equal to it in the chunk; a scan over the waves
+  // turns them into each wave's output offset and the number of equal keys
+  // before its chunk (only the first need[c] equal keys in j order are
+  // taken, as the reference's stable order among ties at this stage).
+  // Pass 2 writes.  (One wave per class swept the whole row before: with
+  // two classes, 2 of 16 waves did all the work.)
+  // per-wave counts and offsets [wave][class] reuse the histogram space
+  // (4 x 16 x C <= 256 x C words)
+  uint32_t* cnt_lt = hist;
+  uint32_t* cnt_eq = hist + 16 * n_classes;
+  uint32_t* off_lt = hist + 32 * n_classes;
+  uint32_t* off_eq = hist + 48 * n_classes;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int64_t chunk = (n + nwaves - 1) / nwaves;
+  const int64_t jb = (int64_t)wave * chunk, je = jb + chunk < n ? jb + chunk : n;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int c = lane; c < n_classes; c += 64) cnt_lt[wave * n_classes + c] = cnt_eq[wave * n_classes + c] = 0u;
+  __syncthreads();
+  // Keys are classified 4 x 64 at a time (the loads of the four go out
+  // together: the chain label -> T[label] -> compare is LDS-latency bound).
+  constexpr int kCU = 4;
+  auto classify = [&](int64_t j0, int32_t (&cv)[kCU], bool (&lt)[kCU], bool (&eq)[kCU]) {
+    uint32_t kv[kCU];
+#pragma unroll
+    for (int u = 0; u < kCU; u++) {
+      const int64_t j = j0 + 64 * u + lane;
+      const bool ok = j < je && j != i;
+      cv[u] = ok ? lab_of(j) : -1;
+      kv[u] = ok ? key_of(j) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kCU; u++) {
+      const uint32_t T = cv[u] >= 0 ? prefix[cv[u]] : 0u;
+      lt[u] = cv[u] >= 0 && kv[u] < T;
+      eq[u] = cv[u] >= 0 && kv[u] == T;
+    }
+  };
+  const bool few = n_classes <= 8;  // lane c keeps class c's counts (ballots)
+  uint32_t my_lt = 0u, my_eq = 0u;
+  for (int64_t j0 = jb; j0 < je; j0 += 64 * kCU) {
+    int32_t cv[kCU];
+    bool lt[kCU], eq[kCU];
+    classify(j0, cv, lt, eq);
+#pragma unroll
+    for (int u = 0; u < kCU; u++) {
+      if (few) {
+        for (int cc = 0; cc < n_classes; cc++) {
+          const uint32_t nl = (uint32_t)__popcll(__ballot(lt[u] && cv[u] == cc));
+          const uint32_t ne = (uint32_t)__popcll(__ballot(eq[u] && cv[u] == cc));
+          if (lane == cc) my_lt += nl, my_eq += ne;
+        }
+      } else {  // many classes: LDS atomics
+        if (lt[u]) atomicAdd(&cnt_lt[wave * n_classes + cv[u]], 1u);
+        else if (eq[u]) atomicAdd(&cnt_eq[wave * n_classes + cv[u]], 1u);
+      }
+    }
+  }
+  if (few && lane < n_classes) {
+    cnt_lt[wave * n_classes + lane] = my_lt;
+    cnt_eq[wave * n_classes + lane] = my_eq;
+  }
+  __syncthreads();
+  // exclusive scans over the waves, per class (one thread per class)
+  for (int c = tid; c < n_classes; c += nt) {
+    uint32_t a = 0u, b = 0u;
+    for (int w = 0; w < nwaves; w++) {
+      off_lt[w * n_classes + c] = a;
+      off_eq[w * n_classes + c] = b;
+      a += cnt_lt[w * n_classes + c];
+      b += cnt_eq[w * n_classes + c];
+    }
+    // every key below T is taken; the first need[c] equal keys follow them
+    const uint32_t take_eq = b < need[c] ? b : need[c];
+    nfound[i * n_classes + c] = (int32_t)(a + take_eq);
+    teq[i * n_classes + c] = (int32_t)b;
+    cnt_lt[c] = a;  // total below T (base of the equal keys' slots)
+  }
+  __syncthreads();
+  // pass 2: write.  Keys below T keep j order among themselves; equal keys
+  // (in j order) follow.  A wave walks its chunk in j order, so a per-wave
+  // running count per class gives each key its slot: lane c holds class c's
+  // (one sweep for all classes), or one sweep per class when there are many.
+  uint32_t run_lt = 0u, run_eq = 0u;
+  if (few && lane < n_classes) {
+    run_lt = off_lt[wave * n_classes + lane];
+    run_eq = off_eq[wave * n_classes + lane];
+  }
+  for (int c1 = 0; c1 < (few ? 1 : n_classes); c1++) {
+    if (!few) {
+      run_lt = off_lt[wave * n_classes + c1];
+      run_eq = off_eq[wave * n_classes + c1];
+    }
+    for (int64_t j0 = jb; j0 < je; j0 += 64 * kCU) {
+      int32_t cv[kCU];
+      bool lt[kCU], eq[kCU];
+      classify(j0, cv, lt, eq);
+#pragma unroll
+      for (int u = 0; u < kCU; u++) {
+        const int64_t j = j0 + 64 * u + lane;
+        for (int cc = few ? 0 : c1; cc < (few ? n_classes : c1 + 1); cc++) {
+          const bool l = lt[u] && cv[u] == cc, e = eq[u] && cv[u] == cc;
+          const uint64_t mlt = __ballot(l), meq = __ballot(e);
+          if ((mlt | meq) == 0ull) continue;
+          const uint32_t rl = few ? (uint32_t)__shfl((int)run_lt, cc) : run_lt;
+          const uint32_t re = few ? (uint32_t)__shfl((int)run_eq, cc) : run_eq;
+          int32_t* out = nbr + (i * n_classes + cc) * k;
+          if (l) out[rl + __popcll(mlt & below)] = (int32_t)j;
+          if (e) {
+            const uint32_t r = re + (uint32_t)__popcll(meq & below);
+            if (r < need[cc]) out[cnt_lt[cc] + r] = (int32_t)j;
+          }
+          if (!few || lane == cc) {
+            run_lt += (uint32_t)__popcll(mlt);
+            run_eq += (uint32_t)__popcll(meq);
+          }
+        }
+      }
     }
   }
 }
@@ -2282,8 +2464,10 @@ __global__ __launch_bounds__(64) void k_rf_ties(const int32_t* __restrict__ rows
 
 // acc_f(i) = -sum_hits d / h_found + sum_{c != y_i} (P_c / (1 - P_yi)) sum_misses_c d / k
 // (ReliefF.py:177-216) for the focal rows [r_lo, r_hi).  Grid (PW/64, row
-// blocks of 16); 4 waves per workgroup, wave w handles rows w, w+4, ... of
-// the block.
+// blocks of kRfRows); 4 waves per workgroup, wave w handles rows w, w+4, ...
+// of the block.  (64-row blocks: the partials k_reduce then folds are 1/4 of
+// 16-row blocks', and the grid still holds ~10^4 workgroups at n = 20000.)
+constexpr int64_t kRfRows = 64;
 __global__ __launch_bounds__(256) void k_rf_update(const float* __restrict__ xs, int64_t r_lo,
                                                    int64_t r_hi,
                                                    int64_t PW, int64_t PC,
@@ -2299,8 +2483,8 @@ __global__ __launch_bounds__(256) void k_rf_update(const float* __restrict__ xs,
   const int64_t c = (int64_t)blockIdx.x * 64 + lane;
   const bool disc = (int64_t)blockIdx.x * 64 >= PC;
   double acc = 0.0;
-  const int64_t b0 = r_lo + (int64_t)blockIdx.y * 16;
-  for (int64_t i = b0 + wave; i < r_hi && i < b0 + 16; i += 4) {
+  const int64_t b0 = r_lo + (int64_t)blockIdx.y * kRfRows;
+  for (int64_t i = b0 + wave; i < r_hi && i < b0 + kRfRows; i += 4) {
     const int32_t li = lab[i];
     const float a = xs[i * PW + c];
     double denom = 1.0 - prior[li];
@@ -3982,42 +4166,53 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   FS_TRY(dalloc(g, &tneed, (size_t)n * C));
   FS_TRY(dalloc(g, &teq, (size_t)n * C));
   g->alloc_target = 0;
-  const size_t shbytes = (size_t)C * 256 * 4 + 2 * (size_t)C * 4;
+  // histograms: 1024 bins per class for n_classes <= 8 (10-bit first digit)
+  const size_t shbytes = (size_t)C * (C <= 8 ? 1024 : 256) * 4 + 2 * (size_t)C * 4;
   const size_t shstage = shbytes + (size_t)n * 5;
   const bool stage = shstage <= 160 * 1024;
   if (stage)
     FS_HIP(hipFuncSetAttribute((const void*)k_rf_select<true>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shstage));
-  auto select = [&](int collect) {
+  // band of the exact-key refinement (quantisation error + float32 rounding)
+  const double band_abs = 2.0 * Q.amb_delta, band_rel = 2.0 * 1.2e-7;
+  auto select = [&](int collect, int2* lst) {
     if (stage)
       k_rf_select<true><<<(unsigned)nr_own, 1024, shstage, g->stream>>>(
           g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, r_lo, tkey, tneed, teq, nbr,
-          nfound);
+          nfound, band_abs, band_rel, lst, g->list_cap, g->list_count);
     else
       k_rf_select<false><<<(unsigned)nr_own, 256, shbytes, g->stream>>>(
           g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, r_lo, tkey, tneed, teq, nbr,
-          nfound);
+          nfound, band_abs, band_rel, lst, g->list_cap, g->list_count);
     return launch_check("k_rf_select");
   };
-  // 1. k-th keys from the quantised distances
+  // 1. k-th keys from the quantised distances, and (same launch, on the
+  // staged row) the candidates inside the band around them
+  FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
   FS_HIP(hipEventRecord(g->ev[4], g->stream));
-  FS_TRY(select(0));
+  FS_TRY(select(0, g->list));
   FS_HIP(hipEventRecord(g->ev[5], g->stream));
-  // 2. exact keys inside the band (quantisation error + float32 rounding)
-  const double band_abs = 2.0 * Q.amb_delta, band_rel = 2.0 * 1.2e-7;
+  // 2. exact keys inside the band; a list that overflowed is grown and the
+  // band re-flagged by k_rf_flag (from the stored keys)
   g->n_refined = 0;
-  for (int attempt = 0; attempt < 2; attempt++) {
-    FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
-    k_rf_flag<<<(unsigned)nr_own, 256, 0, g->stream>>>(g->D, n, Q.n_pad, inv_sc, g->lab, C,
-                                                       tkey, tneed, band_abs, band_rel, r_lo,
-                                                       g->list, g->list_cap, g->list_count);
-    FS_TRY(launch_check("k_rf_flag"));
+  for (int attempt = 0; attempt < 3; attempt++) {
+    if (attempt > 0) {
+      FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
+      k_rf_flag<<<(unsigned)nr_own, 256, 0, g->stream>>>(g->D, n, Q.n_pad, inv_sc, g->lab, C,
+                                                         tkey, tneed, band_abs, band_rel, r_lo,
+                                                         g->list, g->list_cap, g->list_count);
+      FS_TRY(launch_check("k_rf_flag"));
+    }
     unsigned long long cnt = 0;
     FS_HIP(hipMemcpyAsync(&cnt, g->list_count, sizeof(cnt), hipMemcpyDeviceToHost, g->stream));
     FS_HIP(hipStreamSynchronize(g->stream));
     if ((int64_t)cnt <= g->list_cap) {
       g->n_refined = (int64_t)cnt;
       break;
+    }
+    if (attempt == 2) {
+      set_error("ReliefF exact-pair list: overflow after growing");
+      return FS_EHIP;
     }
     g->list_cap = (int64_t)cnt + cnt / 4;
     FS_TRY(dalloc(g, &g->list, g->list_cap));  // persistent (alloc_target 0 here)
@@ -4031,7 +4226,7 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
     FS_TRY(launch_check("k_exact_pairs"));
   }
   // 3. exact selection
-  FS_TRY(select(1));
+  FS_TRY(select(1, nullptr));
   // 4. rows with more neighbours at the k-th key than needed
   std::vector<int32_t> hneed((size_t)nr_own * C), heq((size_t)nr_own * C);
   FS_HIP(hipMemcpyAsync(hneed.data(), tneed + r_lo * C, hneed.size() * 4, hipMemcpyDeviceToHost,
@@ -4101,7 +4296,7 @@ static int plan_score_relieff(Plan* g, double* sums_dev) {
   double *dprior = nullptr, *part = nullptr;
   int64_t* dcc = nullptr;
   int32_t *nbr = nullptr, *nfound = nullptr;
-  const int64_t nrb = std::max<int64_t>(1, (g->r_hi - g->r_lo + 15) / 16);
+  const int64_t nrb = std::max<int64_t>(1, (g->r_hi - g->r_lo + kRfRows - 1) / kRfRows);
   int rc;
   g->alloc_target = 2;  // per-call buffers
   rc = dalloc(g, &dprior, C);

@@ -111,8 +111,9 @@ def test_surf_sizes(oracle, n, p, seed):
 
 
 @pytest.mark.parametrize("n,p,ncls,k,seed", [(500, 300, 2, 10, 0), (600, 200, 5, 3, 1),
-                                            (300, 100, 3, 40, 2)])
+                                            (300, 100, 3, 40, 2), (900, 150, 12, 5, 3)])
 def test_relieff_sizes(oracle, n, p, ncls, k, seed):
+    """12 classes: k_rf_select's 8-bit first digit (10-bit up to 8 classes)."""
     from fastselect_amd import ReliefF
     X, y = make_classification(n_samples=n, n_features=p, n_informative=10, n_redundant=10,
                                n_classes=ncls, n_clusters_per_class=1, random_state=seed)
