@@ -338,10 +338,14 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
         k_ms = float(np.mean(kms[0]))
         name = "k_dist" if algo == "relieff" else "k_dist_f64"
         peak = VALU_PEAK_TFLOPS if algo == "relieff" else VALU_F64_PEAK_TFLOPS
-        achieved = FLOP_PER_PFE * pairs * p / (k_ms * 1e-3) / 1e12
+        # ReliefF's k_dist on 16-bit operands (n >= 4096): one v_sad_u16 per 2
+        # PFE, one issue slot per PFE = 2 FMA-equivalent FLOPs (32-bit: 4)
+        q16 = algo == "relieff" and bool(plan.calibration()["q16"])
+        fpp = FLOP_PER_PFE // 2 if q16 else FLOP_PER_PFE
+        achieved = fpp * pairs * p / (k_ms * 1e-3) / 1e12
         roofline = {"bound": "valu", "kernel": name, "achieved": achieved, "peak": peak,
                     "unit": "TFLOP/s", "frac": achieved / peak, "traffic": None,
-                    "flop_per_pfe": FLOP_PER_PFE, "pfe_per_launch": pairs * p,
+                    "flop_per_pfe": fpp, "pfe_per_launch": pairs * p,
                     "pfe_per_s": pairs * p / (k_ms * 1e-3),
                     "kernel_ms": {name: k_ms, "stage2": float(np.mean(kms[1]))}}
         if algo == "relieff":
@@ -352,8 +356,11 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
             roofline["k_rf_select_hbm"] = {"bytes": rbytes, "GBps": rbytes / (sel_ms * 1e-3) / 1e9,
                                            "peak": HBM_PEAK_GBPS,
                                            "frac": rbytes / (sel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
-            roofline["peak_note"] = ("k_dist here runs 16-bit operands (v_sad_u16, 2 PFE per "
-                                     "issue slot pair): priced as the fp32 path, as cfg4")
+            roofline["peak_note"] = (
+                "k_dist on 16-bit operands: v_sad_u16 takes 2 PFE per issue slot, so 1 slot per "
+                "PFE = 2 FMA-equivalent FLOPs against the fp32 vector peak" if q16 else
+                "k_dist on 32-bit operands: one half-rate v_sad_u32 per PFE = 4 FMA-equivalent "
+                "FLOPs against the fp32 vector peak")
         else:
             roofline["peak_note"] = ("float64 vector peak (AMD MI355X figure, half the fp32 rate); "
                                      "2 v_add_f64 per PFE, each priced as one FMA")
@@ -519,7 +526,10 @@ def main():
         pfe = {"k_dist": pairs_dense * p, score_name: pairs_score * p}
         kern = {"k_dist": d_ms, score_name: s_ms}
         dom = max(kern, key=kern.get)
-        achieved = FLOP_PER_PFE * pfe[dom] / (kern[dom] * 1e-3) / 1e12
+        # FMA-equivalent FLOPs per PFE: k_dist 2 on 16-bit operands (one
+        # v_sad_u16 per 2 PFE), 4 on 32-bit (half-rate v_sad_u32); pass 2 4
+        fpp = {"k_dist": FLOP_PER_PFE // 2 if q16_used else FLOP_PER_PFE, score_name: FLOP_PER_PFE}
+        achieved = fpp[dom] * pfe[dom] / (kern[dom] * 1e-3) / 1e12
         # bytes the tiles stream from L2/HBM into the CUs (both row panels of
         # every owned tile, + the D write / the pair weights): on-chip reuse
         # traffic, NOT the algorithmic HBM bytes
@@ -537,8 +547,10 @@ def main():
             "traffic": traffic[dom],
             "traffic_source": pmc_traffic(dom, n, p, world)[1],
             "traffic_per_kernel": traffic,
-            "flop_per_pfe": FLOP_PER_PFE,
+            "flop_per_pfe": fpp[dom],
             "pfe_per_s": pfe[dom] / (kern[dom] * 1e-3),
+            "valu_frac_per_kernel": {k: fpp[k] * pfe[k] / (kern[k] * 1e-3) / 1e12 / VALU_PEAK_TFLOPS
+                                     for k in kern},
             "kernel_ms": kern,
             "pfe_per_launch": pfe[dom],
             "pass2_weighted_pairs": weighted,

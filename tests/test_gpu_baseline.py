@@ -50,8 +50,11 @@ def _fixture(name):
     return np.load(path, allow_pickle=False)
 
 
-def _attribute(name, s, ref, per_element_bar):
-    """The attribution check above, when fullsize_{name}_f64.npz exists."""
+def _attribute(name, s, ref, per_element_bar, rms=True):
+    """The attribution check above, when fullsize_{name}_f64.npz exists.
+    rms=False (16-bit pass 1): only the max is compared -- pairs between the
+    quantised and the reference threshold are decided differently there, an
+    error of its own beside the accumulation's (Numerics)."""
     path = os.path.join(GOLD, f"fullsize_{name}_f64.npz")
     if not os.path.exists(path):
         return
@@ -62,7 +65,8 @@ def _attribute(name, s, ref, per_element_bar):
            f"{summary(ref, exact)}")
     print(msg)
     assert dg.max() <= do.max(), msg
-    assert np.sqrt((dg ** 2).mean()) <= np.sqrt((do ** 2).mean()), msg
+    if rms:
+        assert np.sqrt((dg ** 2).mean()) <= np.sqrt((do ** 2).mean()), msg
     if per_element_bar:
         # every feature with |s| >= 1e-2 max|s| within rtol 1e-5 of the
         # float64 sums; the 1e-3 band is reported (profiles/r03/
@@ -128,9 +132,24 @@ def test_cfg4_multisurf_north_star(lib):
     est = lib.MultiSURF(backend="gpu", n_features_to_select=TOPK).fit(X, y)
     assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
     # 16-bit pass 1 decides pairs between the quantised and the reference
-    # threshold differently (Numerics): no per-element claim
-    _attribute("cfg4_multisurf", est.feature_importances_, fx["scores"], False)
+    # threshold differently (Numerics): no per-element or rms claim
+    # (measured: max 1.9e-6 vs the reference arithmetic's 2.9e-6 of max|s|,
+    # rms 4.0e-7 vs 7.5e-8; profiles/r03/parity_report.txt)
+    _attribute("cfg4_multisurf", est.feature_importances_, fx["scores"], False, rms=False)
     assert set(est.top_features_.tolist()) == set(np.argsort(fx["scores"])[::-1][:TOPK].tolist())
+
+
+def test_cfg4_multisurf_q32_attribution(lib, monkeypatch):
+    """The north-star data on 32-bit pass-1 operands (FS_Q16=0: every
+    near/far decision the reference's): the whole residual is then
+    accumulation, and the GPU is at least as close to the float64 sums as
+    the reference's float32 arithmetic, max and rms."""
+    monkeypatch.setenv("FS_Q16", "0")
+    fx = _fixture("cfg4_multisurf")
+    X, y = _inputs(fx)
+    est = lib.MultiSURF(backend="gpu", n_features_to_select=TOPK).fit(X, y)
+    assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
+    _attribute("cfg4_multisurf", est.feature_importances_, fx["scores"], False)
 
 
 def test_cfg4_multisurf_focal_slices_partition(lib):

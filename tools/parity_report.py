@@ -72,6 +72,8 @@ def main():
         variants = [("default", {})]
         if str(fx["algo"]) == "surf":  # the whole-fit (dense) pass 2 beside the sparse slice path
             variants.append(("FS_SPARSE=0", {"FS_SPARSE": "0"}))
+        if str(fx["algo"]) == "multisurf" and n >= 16384:  # 32-bit pass 1 beside the 16-bit default
+            variants.append(("FS_Q16=0", {"FS_Q16": "0"}))
         for label, env in variants:
             old = {k: os.environ.get(k) for k in env}
             os.environ.update(env)

@@ -1,5 +1,6 @@
 """Quick GPU check of the sparse pass-2 variants against the oracle (small
-shapes covering: 512-feature blocks, the 256-feature tail, p = 64 (a single
+shapes covering: 512-feature blocks, the 256-feature tail, a tail longer than
+256 features (one more, partial, 512-feature block), p = 64 (a single
 partial block), discrete / mixed blocks, n not a multiple of 128).  Each
 configuration runs with FS_SPARSE_V=1 (round-2 streams) and 2 (half tiles x 8
 features), the latter with the generated loop and with the plain-HIP walk
@@ -17,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 CASES = [  # (n, p, discrete columns, seed)
     (1024, 64, 0, 1), (700, 600, 0, 2), (1500, 1100, 0, 3), (900, 520, 40, 4), (640, 300, 300, 5),
-    (2100, 2048, 0, 6),
+    (2100, 2048, 0, 6), (900, 800, 0, 7), (600, 1400, 30, 8),
 ]
 
 CHILD = r"""

@@ -40,6 +40,17 @@ def main(src, out):
         if "fetch_KiB_per_launch" in s and "write_KiB_per_launch" in s:
             s["hbm_bytes_per_launch"] = (2.0 * s["fetch_KiB_per_launch"] + s["write_KiB_per_launch"]) * 1024
             s["hbm_GBps"] = s["hbm_bytes_per_launch"] / (s["avg_ms"] * 1e-3) / 1e9
+    # pass 2 of the sparse path runs one launch per feature width
+    # (k_score_sparse2<8>, <4> for a tail): bench.py prices them together as
+    # "k_score_sparse" (its HIP events span the pass)
+    parts = [s for k, s in stats.items() if k.startswith("k_score_sparse2<")]
+    if parts and all("hbm_bytes_per_launch" in s for s in parts):
+        stats["k_score_sparse"] = {
+            "calls": parts[0]["calls"], "avg_ms": sum(s["avg_ms"] for s in parts),
+            "hbm_bytes_per_launch": sum(s["hbm_bytes_per_launch"] for s in parts),
+            "parts": [k for k in stats if k.startswith("k_score_sparse2<")]}
+        stats["k_score_sparse"]["hbm_GBps"] = (stats["k_score_sparse"]["hbm_bytes_per_launch"]
+                                               / (stats["k_score_sparse"]["avg_ms"] * 1e-3) / 1e9)
     bench = json.load(open(f"{src}/bench_trace.json"))
     with open(f"{out}_summary.json", "w") as f:
         json.dump({"bench": bench, "kernels": stats}, f, indent=1)
