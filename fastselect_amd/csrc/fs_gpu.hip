@@ -1782,16 +1782,32 @@ __global__ void k_accumulate(double* __restrict__ dst, const double* __restrict_
   if (k < count) dst[k] += src[k];
 }
 
-// out[out_pos[c]] = sum over segments of part[seg][c] (fixed order).
-__global__ void k_reduce(const double* __restrict__ part, int64_t nseg, int64_t PW,
-                         const int64_t* __restrict__ out_pos, double* __restrict__ out) {
-  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (c >= PW) return;
+// out[out_pos[c]] = sum over segments of part[seg][c] (fixed order).  One
+// 1024-thread workgroup per 64 columns: wave w sums the segments w, w + 16,
+// ... (one coalesced 512-byte read per segment), then the 16 partials are
+// added in a fixed tree (deterministic run to run).  A thread per column
+// walking every segment (the round-2 form) left ~80 workgroups on the chip:
+// 0.3 ms for one rank of N = 8 at cfg4.
+constexpr int kReduceWaves = 16;
+__global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part, int64_t nseg,
+                                                 int64_t PW, const int64_t* __restrict__ out_pos,
+                                                 double* __restrict__ out) {
+  __shared__ double red[kReduceWaves][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + lane;
+  double s = 0.0;
+  if (c < PW)
+    for (int64_t g = wave; g < nseg; g += kReduceWaves) s += part[g * PW + c];
+  red[wave][lane] = s;
+  __syncthreads();
+  if (wave != 0 || c >= PW) return;
   const int64_t o = out_pos[c];
   if (o < 0) return;
-  double s = 0.0;
-  for (int64_t g = 0; g < nseg; g++) s += part[g * PW + c];
-  out[o] = s;
+  double q[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    q[k] = (red[4 * k][lane] + red[4 * k + 1][lane]) + (red[4 * k + 2][lane] + red[4 * k + 3][lane]);
+  out[o] = (q[0] + q[1]) + (q[2] + q[3]);
 }
 
 // ---------------------------------------------------------------------------
@@ -3843,7 +3859,7 @@ static int run_pass2(Plan* g, double* scores_dev) {
     FS_TRY(launch_check("k_score"));
   }
   FS_HIP(hipEventRecord(g->ev[3], g->stream));
-  k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(g->spart, g->nsegpart, Q.PW,
+  k_reduce<<<(unsigned)((Q.PW + 63) / 64), 1024, 0, g->stream>>>(g->spart, g->nsegpart, Q.PW,
                                                                    g->out_pos, scores_dev);
   return launch_check("k_reduce");
 }
@@ -4325,7 +4341,7 @@ static int plan_score_relieff(Plan* g, double* sums_dev) {
   FS_TRY(launch_check("k_rf_update"));
   FS_HIP(hipEventRecord(g->ev[3], g->stream));
   FS_HIP(hipMemsetAsync(sums_dev, 0, sizeof(double) * Q.n_kept, g->stream));
-  k_reduce<<<(unsigned)((Q.PW + 255) / 256), 256, 0, g->stream>>>(part, nrb, Q.PW, g->out_pos,
+  k_reduce<<<(unsigned)((Q.PW + 63) / 64), 1024, 0, g->stream>>>(part, nrb, Q.PW, g->out_pos,
                                                                    sums_dev);
   return launch_check("k_reduce");
 }

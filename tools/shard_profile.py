@@ -1,5 +1,12 @@
 """Time one rank's share of a world-N MultiSURF step on one GPU (what each
-rank of an N-GPU run executes, minus the collectives).
+rank of an N-GPU run executes, minus the collectives), and add a model of
+the step's three SUM all-reduces (rowstats 3n, counts 2n, scores p float64)
+so the projected per-rank step covers the whole exchange: ring all-reduce
+2 (N-1) / N * bytes / link_bw + 2 (N-1) * hop_latency, with conservative
+xGMI figures (50 GB/s effective per ring direction -- a third of the
+153 GB/s link -- and 10 us per ring step; measured RCCL small-message
+latency on MI300-class nodes is below that).  Not measured: this box has one
+GPU.
 
     python tools/shard_profile.py --world 8 [--samples 20000 --features 20000]
 """
@@ -14,6 +21,10 @@ import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+LINK_BW = 50e9   # bytes/s per ring direction (conservative xGMI figure)
+HOP_S = 10e-6    # seconds per ring step (conservative RCCL latency)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, default=8)
@@ -21,6 +32,7 @@ def main():
     ap.add_argument("--samples", type=int, default=20000)
     ap.add_argument("--features", type=int, default=20000)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--world1", action="store_true", help="also time the whole job (world 1)")
     args = ap.parse_args()
     import torch
     from sklearn.datasets import make_classification
@@ -63,9 +75,16 @@ def main():
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / args.steps
     tiles, _, refined = plan.info()
+    N = args.world
+    ar_bytes = [3 * n * 8, 2 * n * 8, args.features * 8]
+    ar_ms = sum(2 * (N - 1) / N * b / LINK_BW + 2 * (N - 1) * HOP_S for b in ar_bytes) * 1e3 \
+        if N > 1 else 0.0
     print(json.dumps({"world": args.world, "rank": args.rank, "tiles": tiles, "step_ms": dt * 1e3,
                       "k_dist_ms": plan.kernel_ms(0), "k_score_ms": plan.kernel_ms(1),
-                      "refined": refined, "weighted_pairs": plan.weighted_pairs()}))
+                      "refined": refined, "weighted_pairs": plan.weighted_pairs(),
+                      "allreduce_model_ms": ar_ms, "step_with_allreduce_ms": dt * 1e3 + ar_ms,
+                      "allreduce_model": f"ring, {LINK_BW / 1e9:.0f} GB/s, {HOP_S * 1e6:.0f} us "
+                                         f"per step, bytes {ar_bytes}"}))
 
 
 if __name__ == "__main__":
