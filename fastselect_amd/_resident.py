@@ -32,7 +32,13 @@ class ResidentRows:
         if self.backend == "gpu":
             import torch
             if self._buf is None or self._buf.numel() != n_kept:
-                self._buf = torch.zeros(n_kept, dtype=torch.float64, device="cuda")
+                # no fill kernel: the plan clears the sums on its own stream.
+                # That stream is non-blocking, so nothing torch queued on its
+                # stream is ordered before the plan's kernels -- a torch.zeros
+                # here could land after the plan's k_reduce and wipe the
+                # sums (TuRF over ReliefF varied run to run that way)
+                self._buf = torch.empty(n_kept, dtype=torch.float64, device="cuda")
+            torch.cuda.current_stream().synchronize()
             self.plan.score(self._buf.data_ptr())  # synchronises the plan's stream
             return self._buf.cpu().numpy()
         out = np.zeros(n_kept, dtype=np.float64)

@@ -260,8 +260,14 @@ int multisurf_pass1(const Prepared& P, const void* x, int rank, int world, int n
                     CpuState& S, double* rowstats) {
   std::vector<uint32_t> xq;
   std::vector<float> eps;
-  quantize(P, x, 0, n_jobs, xq, S.xs, &eps);
-  mean_correction(P, xq, eps, P.pc * rank / world, P.pc * (rank + 1) / world, n_jobs, S.corr);
+  // FS_MEANCORR=0 drops the mean correction, as on the GPU (A/B only)
+  const char* mc = std::getenv("FS_MEANCORR");
+  const bool mean_corr = !(mc && *mc && std::atoi(mc) == 0);
+  quantize(P, x, 0, n_jobs, xq, S.xs, mean_corr ? &eps : nullptr);
+  if (mean_corr)
+    mean_correction(P, xq, eps, P.pc * rank / world, P.pc * (rank + 1) / world, n_jobs, S.corr);
+  else
+    S.corr.assign(P.n, 0.0);
   distances(P, xq, rank, world, n_jobs, S.D);
   const int64_t n = P.n, nb = P.n_pad / kTile;
   parallel_for(n, n_jobs, [&](int64_t i) {

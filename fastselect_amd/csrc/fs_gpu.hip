@@ -378,7 +378,8 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
                                                  const int2* __restrict__ tiles, int64_t n_full,
                                                  int splits, int tiled, int2 win,
                                                  double* __restrict__ D,
-                                                 double* __restrict__ Dpart) {
+                                                 double* __restrict__ Dpart, int64_t sk_wgs,
+                                                 int64_t sk_units) {
   // Two distinct LDS objects (not one indexed array) so the compiler can
   // prove a pending global_load_lds into one buffer does not alias the
   // ds_reads of the other and keeps the copy in flight across the compute.
@@ -387,133 +388,194 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int64_t b_id = blockIdx.x;
-  const int64_t q = b_id - n_full;  // >= 0: a split tile's part
-  const int part = q < 0 ? 0 : (int)(q % splits);
-  const int nparts = q < 0 ? 1 : splits;
-  int64_t t = q < 0 ? b_id : n_full + q / splits;
-  const int2 tl = tiles[t];
-  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
   const int tx = tid & 15, ty = tid >> 4;
-  if (part > 0) {  // compact partial block, tile-local layout
-    D = Dpart;
-    t = (q / splits) * (splits - 1) + part - 1;
-    tiled = 1;
-  }
-
-  uint32_t acc[8][8];
-  uint32_t hi[8][4];
-#pragma unroll
-  for (int r = 0; r < 8; r++) {
-#pragma unroll
-    for (int c = 0; c < 8; c++) acc[r][c] = 0;
-#pragma unroll
-    for (int c = 0; c < 4; c++) hi[r][c] = 0;
-  }
-
+  const int nck_all = nck_cont + nck_disc;
   // glds lane mapping: instruction s of wave w moves k-rows 2*(4w+s) and
   // 2*(4w+s)+1; lane l -> k-row offset l/32, 4 u32 at column (l%32)*4.
   constexpr int kIns = kBKQ / 8;  // glds instructions per wave and panel
   const int krow_l = lane >> 5, col_l = (lane & 31) * 4;
-  auto stage = [&](uint32_t* la_base, uint32_t* lb_base, int ck) {
-    const int64_t k0 = (int64_t)ck * kBKQ;
-#pragma unroll
-    for (int s = 0; s < kIns; s++) {
-      const int ins = wave * kIns + s;
-      const int64_t krow = k0 + ins * 2 + krow_l;
-      const uint32_t* ga = xqT + krow * n_pad + i0 + col_l;
-      const uint32_t* gb = xqT + krow * n_pad + j0 + col_l;
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ga,
-                                       (__attribute__((address_space(3))) void*)(la_base + ins * 2 * kTile),
-                                       16, 0, 0);
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gb,
-                                       (__attribute__((address_space(3))) void*)(lb_base + ins * 2 * kTile),
-                                       16, 0, 0);
+
+  // One tile's chunks [c_begin, c_end): accumulate, then write the block to
+  // D (out_part < 0) or to the compact partial block Dpart[out_part]
+  // (tile-local layout T[b][a]).
+  auto segment = [&](int64_t t, int c_begin, int c_end, int64_t out_part) {
+    const int2 tl = tiles[t];
+    const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+    double* Dout = D;
+    int64_t t_out = t;
+    int tiled_out = tiled;
+    if (out_part >= 0) {
+      Dout = Dpart;
+      t_out = out_part;
+      tiled_out = 1;
     }
-  };
-
-  auto flush = [&]() {
+    uint32_t acc[8][8];
+    uint32_t hi[8][4];
 #pragma unroll
-    for (int r = 0; r < 8; r++)
+    for (int r = 0; r < 8; r++) {
 #pragma unroll
-      for (int c = 0; c < 8; c++) {
-        const uint32_t top = acc[r][c] >> kHiShift;
-        acc[r][c] &= (1u << kHiShift) - 1u;
-        hi[r][c >> 1] += (c & 1) ? (top << 16) : top;
+      for (int c = 0; c < 8; c++) acc[r][c] = 0;
+#pragma unroll
+      for (int c = 0; c < 4; c++) hi[r][c] = 0;
+    }
+    auto stage = [&](uint32_t* la_base, uint32_t* lb_base, int ck) {
+      const int64_t k0 = (int64_t)ck * kBKQ;
+#pragma unroll
+      for (int s = 0; s < kIns; s++) {
+        const int ins = wave * kIns + s;
+        const int64_t krow = k0 + ins * 2 + krow_l;
+        const uint32_t* ga = xqT + krow * n_pad + i0 + col_l;
+        const uint32_t* gb = xqT + krow * n_pad + j0 + col_l;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)ga,
+                                         (__attribute__((address_space(3))) void*)(la_base + ins * 2 * kTile),
+                                         16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gb,
+                                         (__attribute__((address_space(3))) void*)(lb_base + ins * 2 * kTile),
+                                         16, 0, 0);
       }
-  };
-
-  // Chunks [c0, c1) of one kind: chunk ck lives in buffer (ck - c0) & 1 and
-  // chunk ck+1 is copied while ck is consumed.  Continuous and discrete
-  // chunks run in separate loops (one dist_chunk instantiation each), which
-  // keeps the register allocation of either loop to itself.
-  auto run = [&](auto mode_tag, int c0, int c1) {
-    constexpr int MODE = decltype(mode_tag)::value;
-    if (c0 >= c1) return;
-    stage(ldsA0, ldsB0, c0);
-    __syncthreads();
-    for (int ck = c0; ck < c1; ck += 2) {
-      if (ck + 1 < c1) stage(ldsA1, ldsB1, ck + 1);
-      dist_chunk<MODE>(ldsA0, ldsB0, tx, ty, sc_disc, acc);
-      if ((ck % kFlushChunks) == kFlushChunks - 1) flush();
+    };
+    auto flush = [&]() {
+#pragma unroll
+      for (int r = 0; r < 8; r++)
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+          const uint32_t top = acc[r][c] >> kHiShift;
+          acc[r][c] &= (1u << kHiShift) - 1u;
+          hi[r][c >> 1] += (c & 1) ? (top << 16) : top;
+        }
+    };
+    // Chunks [c0, c1) of one kind: chunk ck lives in buffer (ck - c0) & 1 and
+    // chunk ck+1 is copied while ck is consumed.  Continuous and discrete
+    // chunks run in separate loops (one dist_chunk instantiation each), which
+    // keeps the register allocation of either loop to itself.
+    auto run = [&](auto mode_tag, int c0, int c1) {
+      constexpr int MODE = decltype(mode_tag)::value;
+      if (c0 >= c1) return;
+      stage(ldsA0, ldsB0, c0);
       __syncthreads();
-      if (ck + 1 < c1) {
-        if (ck + 2 < c1) stage(ldsA0, ldsB0, ck + 2);
-        dist_chunk<MODE>(ldsA1, ldsB1, tx, ty, sc_disc, acc);
-        if (((ck + 1) % kFlushChunks) == kFlushChunks - 1) flush();
+      for (int ck = c0; ck < c1; ck += 2) {
+        if (ck + 1 < c1) stage(ldsA1, ldsB1, ck + 1);
+        dist_chunk<MODE>(ldsA0, ldsB0, tx, ty, sc_disc, acc);
+        if ((ck % kFlushChunks) == kFlushChunks - 1) flush();
         __syncthreads();
+        if (ck + 1 < c1) {
+          if (ck + 2 < c1) stage(ldsA0, ldsB0, ck + 2);
+          dist_chunk<MODE>(ldsA1, ldsB1, tx, ty, sc_disc, acc);
+          if (((ck + 1) % kFlushChunks) == kFlushChunks - 1) flush();
+          __syncthreads();
+        }
       }
-    }
-  };
+    };
+    // continuous chunks (16-bit pairs or 32-bit values), then discrete ones
+    if (q16)
+      run(std::integral_constant<int, kModeU16>{}, c_begin, c_end < nck_cont ? c_end : nck_cont);
+    else
+      run(std::integral_constant<int, kModeU32>{}, c_begin, c_end < nck_cont ? c_end : nck_cont);
+    run(std::integral_constant<int, kModeDisc>{}, c_begin > nck_cont ? c_begin : nck_cont, c_end);
+    flush();
 
-  const int nck_all = nck_cont + nck_disc;
-  const int c_begin = (int)((int64_t)nck_all * part / nparts);
-  const int c_end = (int)((int64_t)nck_all * (part + 1) / nparts);  // this part's chunks
-  // continuous chunks (16-bit pairs or 32-bit values), then discrete ones
-  if (q16)
-    run(std::integral_constant<int, kModeU16>{}, c_begin, c_end < nck_cont ? c_end : nck_cont);
-  else
-    run(std::integral_constant<int, kModeU32>{}, c_begin, c_end < nck_cont ? c_end : nck_cont);
-  run(std::integral_constant<int, kModeDisc>{}, c_begin > nck_cont ? c_begin : nck_cont, c_end);
-  flush();
-
-  // Epilogue.  Full layout: D[i][j] for the tile and, off the diagonal, the
-  // mirror D[j][i], each only where its row is in the window.  Tiled: T_t[b][a]
-  // only (the mirror pattern below), which for a diagonal tile is the whole
-  // symmetric block.
+    // Epilogue.  Full layout: D[i][j] for the tile and, off the diagonal, the
+    // mirror D[j][i], each only where its row is in the window.  Tiled: T_t[b][a]
+    // only (the mirror pattern below), which for a diagonal tile is the whole
+    // symmetric block.
 #pragma unroll
-  for (int r = 0; r < 8 && !tiled; r++) {
-    const int64_t i = i0 + ty * 4 + (r & 3) + (r >> 2) * 64;
-    if (!d_row_in(win, i)) continue;
-    double v[8];
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-      const uint64_t h = (hi[r][c >> 1] >> ((c & 1) * 16)) & 0xFFFFu;
-      v[c] = (double)((h << kHiShift) + acc[r][c]);
-    }
-    double* row = D + i * n_pad + j0 + tx * 4;
-    *(double2*)(row + 0) = make_double2(v[0], v[1]);
-    *(double2*)(row + 2) = make_double2(v[2], v[3]);
-    *(double2*)(row + 64) = make_double2(v[4], v[5]);
-    *(double2*)(row + 66) = make_double2(v[6], v[7]);
-  }
-  if (tl.x != tl.y || tiled) {
-#pragma unroll
-    for (int c = 0; c < 8; c++) {
-      const int b = tx * 4 + (c & 3) + (c >> 2) * 64;
-      if (!tiled && !d_row_in(win, j0 + b)) continue;
+    for (int r = 0; r < 8 && !tiled_out; r++) {
+      const int64_t i = i0 + ty * 4 + (r & 3) + (r >> 2) * 64;
+      if (!d_row_in(win, i)) continue;
       double v[8];
 #pragma unroll
-      for (int r = 0; r < 8; r++) {
+      for (int c = 0; c < 8; c++) {
         const uint64_t h = (hi[r][c >> 1] >> ((c & 1) * 16)) & 0xFFFFu;
-        v[r] = (double)((h << kHiShift) + acc[r][c]);
+        v[c] = (double)((h << kHiShift) + acc[r][c]);
       }
-      double* row = D + d_at(tiled, n_pad, t, i0, j0, ty * 4, b);
+      double* row = Dout + i * n_pad + j0 + tx * 4;
       *(double2*)(row + 0) = make_double2(v[0], v[1]);
       *(double2*)(row + 2) = make_double2(v[2], v[3]);
       *(double2*)(row + 64) = make_double2(v[4], v[5]);
       *(double2*)(row + 66) = make_double2(v[6], v[7]);
     }
+    if (tl.x != tl.y || tiled_out) {
+#pragma unroll
+      for (int c = 0; c < 8; c++) {
+        const int b = tx * 4 + (c & 3) + (c >> 2) * 64;
+        if (!tiled_out && !d_row_in(win, j0 + b)) continue;
+        double v[8];
+#pragma unroll
+        for (int r = 0; r < 8; r++) {
+          const uint64_t h = (hi[r][c >> 1] >> ((c & 1) * 16)) & 0xFFFFu;
+          v[r] = (double)((h << kHiShift) + acc[r][c]);
+        }
+        double* row = Dout + d_at(tiled_out, n_pad, t_out, i0, j0, ty * 4, b);
+        *(double2*)(row + 0) = make_double2(v[0], v[1]);
+        *(double2*)(row + 2) = make_double2(v[2], v[3]);
+        *(double2*)(row + 64) = make_double2(v[4], v[5]);
+        *(double2*)(row + 66) = make_double2(v[6], v[7]);
+      }
+    }
+  };
+
+  const int64_t b_id = blockIdx.x;
+  if (sk_wgs > 0) {
+    // Stream-K: the (tile, chunk) units [b U / W, (b + 1) U / W), U = tiles
+    // x chunks, tile by tile.  A segment that starts a tile writes D; one
+    // that starts inside it (only the workgroup's first) writes the partial
+    // block Dpart[b], added by k_dist_merge_sk.
+    const int64_t u_lo = b_id * sk_units / sk_wgs, u_hi = (b_id + 1) * sk_units / sk_wgs;
+    for (int64_t u = u_lo; u < u_hi;) {
+      const int64_t t = u / nck_all;
+      const int cb = (int)(u - t * nck_all);
+      const int ce = (int)std::min<int64_t>(nck_all, cb + (u_hi - u));
+      segment(t, cb, ce, cb > 0 ? b_id : -1);
+      u += ce - cb;
+    }
+    return;
+  }
+  const int64_t q = b_id - n_full;  // >= 0: a split tile's part
+  const int part = q < 0 ? 0 : (int)(q % splits);
+  const int nparts = q < 0 ? 1 : splits;
+  const int64_t t = q < 0 ? b_id : n_full + q / splits;
+  const int c_begin = (int)((int64_t)nck_all * part / nparts);
+  const int c_end = (int)((int64_t)nck_all * (part + 1) / nparts);  // this part's chunks
+  segment(t, c_begin, c_end, part > 0 ? (q / splits) * (splits - 1) + part - 1 : -1);
+}
+
+// Stream-K merge: tile t (grid.x) adds the partial blocks of the workgroups
+// whose unit range starts strictly inside it (Dpart[b], tile-local T[b][a])
+// to the block its first segment wrote.  Integer-valued doubles: exact, the
+// same D as one workgroup per tile.
+__global__ __launch_bounds__(256) void k_dist_merge_sk(double* __restrict__ D,
+                                                      const double* __restrict__ Dpart,
+                                                      const int2* __restrict__ tiles, int64_t nck,
+                                                      int64_t sk_wgs, int64_t sk_units,
+                                                      int64_t n_pad, int tiled, int2 win) {
+  const int64_t t = blockIdx.x;
+  const int64_t base = t * nck;
+  // first workgroup whose range starts after `base`
+  int64_t b = base * sk_wgs / sk_units;
+  while (b > 0 && (b * sk_units / sk_wgs) > base) b--;
+  while (b * sk_units / sk_wgs <= base) b++;
+  if (b >= sk_wgs || b * sk_units / sk_wgs >= base + nck) return;  // tile computed whole
+  const int2 tl = tiles[t];
+  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  int64_t at[4];
+  double v[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int e = blockIdx.y * 1024 + k * 256 + threadIdx.x;
+    at[k] = d_rd(tiled, win, n_pad, t, i0, j0, e % kTile, e / kTile);  // (i0 + a, j0 + b)
+    v[k] = D[at[k]];
+  }
+  for (; b < sk_wgs && b * sk_units / sk_wgs < base + nck; b++) {
+    const double* __restrict__ ps = Dpart + b * kTile * kTile + blockIdx.y * 1024 + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < 4; k++) v[k] += ps[k * 256];
+  }
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int e = blockIdx.y * 1024 + k * 256 + threadIdx.x;
+    D[at[k]] = v[k];
+    if (!tiled && tl.x != tl.y && d_row_in(win, j0 + e / kTile) && d_row_in(win, i0 + e % kTile))
+      D[(i0 + e % kTile) * n_pad + j0 + e / kTile] = v[k];
   }
 }
 
@@ -1931,6 +1993,11 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
   // match their class's prefix, then per class (one wave each) the bucket
   // holding the need-th key, by a wave prefix sum over the bins.
   __shared__ uint32_t bcount[64];  // keys in the chosen bucket, per class
+  // done[c]: class c's k-th key is final (the small-bucket gather below
+  // leaves need[c] as a rank among the keys EQUAL to it, which a further
+  // radix pass -- counting all keys under the prefix -- must not reuse)
+  __shared__ uint8_t done[64];
+  for (int c = tid; c < n_classes; c += nt) done[c] = 0;
   auto radix_pass = [&](int lo, int hi) {
     const int nbins = 1 << (hi - lo);
     const uint32_t dmask = (uint32_t)nbins - 1u;
@@ -1939,7 +2006,7 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
     for (int64_t j = tid; j < n; j += nt) {
       if (j == i) continue;
       const int32_t c = lab_of(j);
-      if (need[c] == 0) continue;
+      if (need[c] == 0 || done[c]) continue;
       const uint32_t key = key_of(j);
       if (hi < 32 && (key >> hi) != (prefix[c] >> hi)) continue;
       atomicAdd(&hist[c * nbins + ((key >> lo) & dmask)], 1u);
@@ -1949,7 +2016,7 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
     const int bpl = (nbins + 63) >> 6;  // bins per lane
     for (int c = wv; c < n_classes; c += nwaves) {
       const uint32_t nd = need[c];
-      if (nd == 0) continue;
+      if (nd == 0 || done[c]) continue;
       const uint32_t* hc = hist + c * nbins;
       const int b0 = ln * bpl;
       uint32_t tot = 0u;
@@ -2022,6 +2089,7 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
       if (mo != 0ull && ln == (int)__builtin_ctzll(mo)) {
         prefix[c] = v;
         need[c] = nd - nlt;
+        done[c] = 1;
       }
     }
     __syncthreads();
@@ -2545,6 +2613,8 @@ struct Plan {
   int64_t nb = 0, n_tiles = 0, seg_len = 1, nseg = 1;
   int64_t nsegpart = 1;         // rows of spart (nseg, or 2 * nseg for the v2 sparse pass)
   int ksplit = 1;               // pass-1 K-split parts of the tail tiles (k_dist)
+  int64_t sk_wgs = 0;           // pass-1 stream-K workgroups (0: off; choose_streamk)
+  int64_t sk_units = 0;         // stream-K units: tiles x chunks
   int64_t kfull = 0;            // tiles k_dist computes whole (the rest are split)
   int use_q16 = 0;              // pass 1 on packed 16-bit continuous operands
   double calib[7] = {0, 0, 0, 0, 1, 0, 0};  // plan_calibration (calibrate_band, row_guard)
@@ -3039,6 +3109,46 @@ void plan_destroy(Plan* g) {
 // tile planes (~66.5 / p of the tile's compute time each); S > 1 only when
 // the model gains at least 3%.  (Splitting only the last round's tiles was
 // measured too: no better than S = 1 at cfg2, profiles/r02/ksplit_sweep.txt.)
+// k_dist workgroups resident on the device at once (CUs x occupancy), 0 if
+// the runtime cannot say.
+static int64_t kdist_slots(int device) {
+  int cus = 0, per_cu = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+      cus <= 0) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dist, 256, 0) != hipSuccess ||
+      per_cu <= 0) {
+    (void)hipGetLastError();
+    per_cu = 2;
+  }
+  return (int64_t)per_cu * cus;
+}
+
+// Pass-1 stream-K (round 3): instead of splitting every tile's feature range
+// into S parts (S - 1 partial blocks per tile, all merged), the T x C
+// (tile, chunk) units are dealt in equal contiguous ranges to W = R x slots
+// workgroups, R = ceil(T / slots) rounds, so every round is full and only
+// the tiles a range boundary falls into (about one per workgroup) leave a
+// partial block.  Measured against the K-split where the model splits (few
+// tiles per slot): cfg2 k_dist 2.42 vs 2.39 ms (S = 8), one rank of N = 8
+// 8.70 vs 8.56 ms -- the merge was not what the split costs, and the
+// coarser ranges balance worse against k_colrank beside k_dist -- so it is
+// opt-in: FS_STREAMK=1 on R x slots workgroups, FS_STREAMK=w >= 2 on w
+// (tests: ranges spanning many tiles).  Bit-identical to the unsplit pass.
+static int64_t choose_streamk(int64_t tiles, int device, int64_t nchunks, int ksplit) {
+  (void)ksplit;
+  const char* e = std::getenv("FS_STREAMK");
+  const int64_t force = (e && *e) ? std::atoll(e) : 0;
+  if (force <= 0 || tiles <= 0 || nchunks <= 0) return 0;
+  if (force >= 2) return std::min<int64_t>(force, tiles * nchunks);
+  const int64_t slots = kdist_slots(device);
+  if (slots <= 0) return 0;
+  const int64_t rounds = (tiles + slots - 1) / slots;
+  return std::min<int64_t>(rounds * slots, tiles * nchunks);
+}
+
 static int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
@@ -3480,6 +3590,12 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
   if (const char* e = std::getenv("FS_KSPLIT"))  // A/B and tests
     if (std::atoi(e) >= 1) g->ksplit = std::min(16, std::atoi(e));
   if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
+  g->sk_wgs = 0;
+  if (Q.algo != ALGO_SURF && !std::getenv("FS_KSPLIT")) {
+    g->sk_wgs = choose_streamk(g->n_tiles, g->device, rows_q / kBKQ, g->ksplit);
+    if (g->sk_wgs > 0) g->ksplit = 1;
+  }
+  g->sk_units = g->n_tiles * (rows_q / kBKQ);
   g->kfull = g->ksplit > 1 ? 0 : g->n_tiles;  // k_dist can split only a tail; all or none here
   g->alloc_target = 3;
   int rc = FS_OK;
@@ -3501,6 +3617,7 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
   if (!rc && g->ksplit > 1)
     rc = dalloc(g, &g->Dpart,
                 (size_t)(g->n_tiles - g->kfull) * (g->ksplit - 1) * kTile * kTile);
+  if (!rc && g->sk_wgs > 0) rc = dalloc(g, &g->Dpart, (size_t)g->sk_wgs * kTile * kTile);
   g->alloc_target = 0;
   if (rc) return rc;
   g->nnz_valid = false;
@@ -3679,28 +3796,56 @@ static int run_quantize_dist(Plan* g) {
     const hipStream_t cs = (se && *se == '0') ? g->stream : g->side;
     FS_HIP(hipEventRecord(g->ev_fork, g->stream));
     FS_HIP(hipStreamWaitEvent(g->side, g->ev_fork, 0));
-    if (g->c_hi > g->c_lo) {
-      k_colrank<<<(unsigned)(g->c_hi - g->c_lo), 256, 0, cs>>>(
-          g->xqT, Q.n, Q.n_pad, g->rank_shift, Q.q16, g->c_lo, g->epsT);
-      FS_TRY(launch_check("k_colrank"));
+    // The correction runs for both operand widths: with 32-bit operands a
+    // row's mean error is tiny for independent rounding, but columns on a
+    // shared value grid round coherently (every sample of a level alike) and
+    // then move the thresholds enough to matter (intgrid, n = 3000:
+    // 2.2e-5 without it; tests/test_gpu_adversarial.py).  FS_MEANCORR=0
+    // drops it (A/B: cfg2 4.63 -> 4.34 ms, cfg4 163 -> 162 ms per step,
+    // tools/meancorr_ab.sh).
+    static const int mc_env = [] {
+      const char* e = std::getenv("FS_MEANCORR");
+      return (e && *e) ? std::atoi(e) : -1;
+    }();
+    const bool mean_corr = mc_env != 0;
+    if (!mean_corr) {
+      FS_HIP(hipMemsetAsync(g->corr, 0, sizeof(double) * Q.n_pad, cs));
+    } else {
+      if (g->c_hi > g->c_lo) {
+        k_colrank<<<(unsigned)(g->c_hi - g->c_lo), 256, 0, cs>>>(
+            g->xqT, Q.n, Q.n_pad, g->rank_shift, Q.q16, g->c_lo, g->epsT);
+        FS_TRY(launch_check("k_colrank"));
+      }
+      k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, cs>>>(g->epsT, Q.n, Q.n_pad, g->c_lo,
+                                                                 g->c_hi, g->corr);
+      FS_TRY(launch_check("k_rowcorr"));
     }
-    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, cs>>>(g->epsT, Q.n, Q.n_pad, g->c_lo,
-                                                               g->c_hi, g->corr);
-    FS_TRY(launch_check("k_rowcorr"));
     FS_HIP(hipEventRecord(g->ev_join, g->side));
   }
   if (g->n_tiles > 0) {
     FS_HIP(hipEventRecord(g->ev[0], g->stream));
     const int64_t n_split = g->ksplit > 1 ? g->n_tiles - g->kfull : 0;
     const int64_t n_full = g->n_tiles - n_split;
-    k_dist<<<(unsigned)(n_full + n_split * g->ksplit), 256, 0, g->stream>>>(
-        g->xqT, Q.n_pad, (int)((Q.q16 ? Q.PC / 2 : Q.PC) / kBKQ), (int)(Q.PD / kBKQ), Q.SCu,
-        Q.q16, g->tiles, n_full, g->ksplit, g->tiled, g->win, g->D, g->Dpart);
-    FS_TRY(launch_check("k_dist"));
-    if (n_split > 0) {
-      k_dist_merge<<<dim3((unsigned)n_split, kMergeSlices), 256, 0, g->stream>>>(
-          g->D, g->Dpart, g->ksplit - 1, g->tiles, n_full, Q.n_pad, g->tiled, g->win);
-      FS_TRY(launch_check("k_dist_merge"));
+    const int nck = (int)((Q.q16 ? Q.PC / 2 : Q.PC) / kBKQ), nckd = (int)(Q.PD / kBKQ);
+    if (g->sk_wgs > 0) {
+      k_dist<<<(unsigned)g->sk_wgs, 256, 0, g->stream>>>(
+          g->xqT, Q.n_pad, nck, nckd, Q.SCu, Q.q16, g->tiles, g->n_tiles, 1, g->tiled, g->win,
+          g->D, g->Dpart, g->sk_wgs, g->sk_units);
+      FS_TRY(launch_check("k_dist"));
+      k_dist_merge_sk<<<dim3((unsigned)g->n_tiles, kMergeSlices), 256, 0, g->stream>>>(
+          g->D, g->Dpart, g->tiles, (int64_t)(nck + nckd), g->sk_wgs, g->sk_units, Q.n_pad,
+          g->tiled, g->win);
+      FS_TRY(launch_check("k_dist_merge_sk"));
+    } else {
+      k_dist<<<(unsigned)(n_full + n_split * g->ksplit), 256, 0, g->stream>>>(
+          g->xqT, Q.n_pad, nck, nckd, Q.SCu, Q.q16, g->tiles, n_full, g->ksplit, g->tiled,
+          g->win, g->D, g->Dpart, 0, 0);
+      FS_TRY(launch_check("k_dist"));
+      if (n_split > 0) {
+        k_dist_merge<<<dim3((unsigned)n_split, kMergeSlices), 256, 0, g->stream>>>(
+            g->D, g->Dpart, g->ksplit - 1, g->tiles, n_full, Q.n_pad, g->tiled, g->win);
+        FS_TRY(launch_check("k_dist_merge"));
+      }
     }
     FS_HIP(hipEventRecord(g->ev[1], g->stream));
   }

@@ -143,6 +143,27 @@ def test_relieff_boundary_ties_follow_numba_quicksort(oracle, kind, k):
     assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=k, discrete_limit=dl), TOL)
 
 
+def test_relieff_small_and_big_buckets_in_one_row(oracle):
+    """k_rf_select: one class's k-th key settled by the small-bucket gather
+    while another class, whose members all sit at one distance (> 64 keys in
+    the bucket), still needs radix passes; the settled class must keep its
+    key (a further pass once re-bucketed it: TuRF over ReliefF then varied
+    from run to run)."""
+    from fastselect_amd import ReliefF
+    rng = np.random.default_rng(12)
+    n, p = 600, 40
+    X = rng.standard_normal((n, p))
+    y = np.zeros(n, dtype=int)
+    y[200:400] = 1
+    y[400:] = 2
+    X[200:400] = X[200]                     # class 1: 200 identical rows
+    X[400:] = np.round(X[400:], 1)          # class 2: coarse grid (ties)
+    for k in (3, 10):
+        s = _fit(ReliefF, X, y, n_neighbors=k)
+        assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=k), TOL)
+        np.testing.assert_array_equal(_fit(ReliefF, X, y, n_neighbors=k), s)
+
+
 def test_relieff_ties_large_rows(oracle):
     """Tie replay on rows long enough for many 64-wide partition rounds and
     deep recursion (all-discrete data: ties in every row), CPU == GPU == oracle."""
