@@ -349,9 +349,9 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
                     "pfe_per_s": pairs * p / (k_ms * 1e-3),
                     "kernel_ms": {name: k_ms, "stage2": float(np.mean(kms[1]))}}
         if algo == "relieff":
-            # k_rf_select: one float64 distance row per focal sample read per launch
+            # k_rf_select: one float32 key row per focal sample read per launch
             sel_ms = float(np.mean(kms[2]))
-            rbytes = (rows[1] - rows[0]) * n * 8.0
+            rbytes = (rows[1] - rows[0]) * n * 4.0
             roofline["kernel_ms"]["k_rf_select"] = sel_ms
             roofline["k_rf_select_hbm"] = {"bytes": rbytes, "GBps": rbytes / (sel_ms * 1e-3) / 1e9,
                                            "peak": HBM_PEAK_GBPS,

@@ -379,7 +379,8 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
                                                  int splits, int tiled, int2 win,
                                                  double* __restrict__ D,
                                                  double* __restrict__ Dpart, int64_t sk_wgs,
-                                                 int64_t sk_units) {
+                                                 int64_t sk_units, float* __restrict__ Dk,
+                                                 double inv_sc) {
   // Two distinct LDS objects (not one indexed array) so the compiler can
   // prove a pending global_load_lds into one buffer does not alias the
   // ds_reads of the other and keeps the copy in flight across the compute.
@@ -477,7 +478,33 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
     // Epilogue.  Full layout: D[i][j] for the tile and, off the diagonal, the
     // mirror D[j][i], each only where its row is in the window.  Tiled: T_t[b][a]
     // only (the mirror pattern below), which for a diagonal tile is the whole
-    // symmetric block.
+    // symmetric block.  ReliefF (Dk): the float32 keys f32(D / SC) instead, the
+    // value k_rf_select sorts (full layout, whole tiles only).
+    if (Dk != nullptr) {
+      auto keyv = [&](int r, int c) {
+        const uint64_t h = (hi[r][c >> 1] >> ((c & 1) * 16)) & 0xFFFFu;
+        return (float)((double)((h << kHiShift) + acc[r][c]) * inv_sc);
+      };
+#pragma unroll
+      for (int r = 0; r < 8; r++) {
+        const int64_t i = i0 + ty * 4 + (r & 3) + (r >> 2) * 64;
+        if (!d_row_in(win, i)) continue;
+        float* row = Dk + i * n_pad + j0 + tx * 4;
+        *(float4*)(row + 0) = make_float4(keyv(r, 0), keyv(r, 1), keyv(r, 2), keyv(r, 3));
+        *(float4*)(row + 64) = make_float4(keyv(r, 4), keyv(r, 5), keyv(r, 6), keyv(r, 7));
+      }
+      if (tl.x != tl.y) {
+#pragma unroll
+        for (int c = 0; c < 8; c++) {
+          const int b = tx * 4 + (c & 3) + (c >> 2) * 64;
+          if (!d_row_in(win, j0 + b)) continue;
+          float* row = Dk + (j0 + b) * n_pad + i0 + ty * 4;
+          *(float4*)(row + 0) = make_float4(keyv(0, c), keyv(1, c), keyv(2, c), keyv(3, c));
+          *(float4*)(row + 64) = make_float4(keyv(4, c), keyv(5, c), keyv(6, c), keyv(7, c));
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int r = 0; r < 8 && !tiled_out; r++) {
       const int64_t i = i0 + ty * 4 + (r & 3) + (r >> 2) * 64;
@@ -1013,7 +1040,8 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
     const T* __restrict__ x, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
     const int64_t* __restrict__ src_col, const double* __restrict__ scl, double sc,
     const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
-    int64_t n_pad, int2 tw, int2 win, int mark_f32, double* __restrict__ D) {
+    int64_t n_pad, int2 tw, int2 win, int mark_f32, double* __restrict__ D,
+    float* __restrict__ Dk) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
@@ -1057,8 +1085,14 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
       // MultiSURF: exact distance in integer units.  ReliefF (mark_f32): the
       // reference's float32 key, stored negated so k_rf_select knows it is
       // exact (a zero key is stored as +0, never -0, whose bits would sort last).
-      const double v = mark_f32 ? (acc > 0.0 ? -(double)(float)acc : 0.0) : acc * sc;
-      store_pair(D, n_pad, tw, win, pr, v);
+      if (Dk != nullptr) {  // ReliefF float keys (full layout): the key itself
+        const float kf = (float)acc;
+        if (d_row_in(win, pr.x)) Dk[(int64_t)pr.x * n_pad + pr.y] = kf;
+        if (d_row_in(win, pr.y)) Dk[(int64_t)pr.y * n_pad + pr.x] = kf;
+      } else {
+        const double v = mark_f32 ? (acc > 0.0 ? -(double)(float)acc : 0.0) : acc * sc;
+        store_pair(D, n_pad, tw, win, pr, v);
+      }
     }
   }
 }
@@ -1878,7 +1912,10 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part
 // ---------------------------------------------------------------------------
 // The key of j is the reference's float32 distance row (ReliefF.py:149-155):
 // float32(D_ij / SC) from the quantised distance, or the exact reference key
-// where k_exact_pairs stored one (negative D, see k_exact_pairs).
+// where k_exact_pairs stored one.  ReliefF plans store these keys directly
+// (Dk, float32: k_dist's epilogue forms them, k_exact_pairs overwrites the
+// refined ones); rf_key forms them from a float64 D (negative = exact key),
+// the layout of the other plans.
 __device__ __forceinline__ uint32_t rf_key(double d, double inv_sc) {
   return __float_as_uint(d < 0.0 ? (float)(-d) : (float)(d * inv_sc));
 }
@@ -1892,8 +1929,11 @@ __device__ __forceinline__ uint32_t rf_key(double d, double inv_sc) {
 // tneed keys == T_c (index order) go to nbr (rows where more keys equal T_c
 // than are needed are re-ordered the reference's way by k_rf_ties), and
 // teq[i][c] counts the keys equal to T_c.
-template <bool STAGE>
-__global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D, int64_t n,
+// KF: the plan stores ReliefF's distances as the float32 keys themselves
+// (Dk: k_dist's epilogue and k_exact_pairs write them), half the bytes of D.
+template <bool STAGE, bool KF>
+__global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D,
+                                                   const float* __restrict__ Dk, int64_t n,
                                                    int64_t n_pad, double inv_sc,
                                                    const int32_t* __restrict__ lab,
                                                    const int64_t* __restrict__ class_count,
@@ -1918,10 +1958,13 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
   const int tid = threadIdx.x;
   const int nt = blockDim.x, nwaves = nt >> 6;
   const int32_t li = lab[i];
-  const double* row = D + i * n_pad;
+  const double* row = KF ? nullptr : D + i * n_pad;
+  const float* rowk = KF ? Dk + i * n_pad : nullptr;
   // STAGE: the row's float32 keys are read from HBM once into LDS (the five
   // sweeps below then cost no HBM traffic)
-  auto key_of = [&](int64_t j) { return STAGE ? keys[j] : rf_key(row[j], inv_sc); };
+  auto key_of = [&](int64_t j) {
+    return STAGE ? keys[j] : (KF ? __float_as_uint(rowk[j]) : rf_key(row[j], inv_sc));
+  };
   auto lab_of = [&](int64_t j) { return STAGE ? (int32_t)labs[j] : lab[j]; };
   // Key range of the row: bits above the highest bit in which two keys
   // differ are common to all of them, so the radix passes start below it
@@ -1933,19 +1976,21 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
   // staging: the row read is latency-bound otherwise)
   constexpr int kU = 8;
   for (int64_t j0 = tid; j0 < n; j0 += (int64_t)kU * nt) {
-    double dv[kU];
+    uint32_t rv[kU];  // the raw key (KF) ...
+    double dv[kU];    // ... or the distance it is formed from
     int32_t lv[kU];
 #pragma unroll
     for (int u = 0; u < kU; u++) {
       const int64_t j = j0 + (int64_t)u * nt;
-      dv[u] = j < n ? row[j] : 0.0;
+      if (KF) rv[u] = j < n ? __float_as_uint(rowk[j]) : 0u;
+      else dv[u] = j < n ? row[j] : 0.0;
       lv[u] = (STAGE && j < n) ? lab[j] : 0;
     }
 #pragma unroll
     for (int u = 0; u < kU; u++) {
       const int64_t j = j0 + (int64_t)u * nt;
       if (j >= n) continue;
-      const uint32_t kv = rf_key(dv[u], inv_sc);
+      const uint32_t kv = KF ? rv[u] : rf_key(dv[u], inv_sc);
       if (STAGE) {
         keys[j] = kv;
         labs[j] = (uint8_t)lv[u];
@@ -2257,7 +2302,8 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
 // Candidates whose quantised key lies within `band` of their class's k-th
 // key T (tkey from a first k_rf_select) go to the exact-pair list: after
 // k_exact_pairs stores their reference keys, a second selection is exact.
-__global__ __launch_bounds__(256) void k_rf_flag(const double* __restrict__ D, int64_t n,
+__global__ __launch_bounds__(256) void k_rf_flag(const double* __restrict__ D,
+                                                 const float* __restrict__ Dk, int64_t n,
                                                  int64_t n_pad, double inv_sc,
                                                  const int32_t* __restrict__ lab,
                                                  int n_classes,
@@ -2277,7 +2323,8 @@ __global__ __launch_bounds__(256) void k_rf_flag(const double* __restrict__ D, i
       const int32_t c = lab[j];
       if (tneed[i * n_classes + c] != 0) {  // 0: class taken whole
         const double T = (double)__uint_as_float(tkey[i * n_classes + c]);
-        const double kv = (double)__uint_as_float(rf_key(row[j], inv_sc));
+        const double kv = Dk != nullptr ? (double)Dk[i * n_pad + j]
+                                        : (double)__uint_as_float(rf_key(row[j], inv_sc));
         flag = fabs(kv - T) <= band_abs + band_rel * T;
       }
     }
@@ -2293,8 +2340,8 @@ template <typename T>
 __global__ __launch_bounds__(256) void k_rf_exact_rows(
     const T* __restrict__ x, int64_t n, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
     const int64_t* __restrict__ src_col, const double* __restrict__ scl,
-    const int32_t* __restrict__ rows, const double* __restrict__ D, int64_t n_pad, double inv_sc,
-    float* __restrict__ keys) {
+    const int32_t* __restrict__ rows, const double* __restrict__ D,
+    const float* __restrict__ Dk, int64_t n_pad, double inv_sc, float* __restrict__ keys) {
   const int lane = threadIdx.x & 63;
   const int64_t r = blockIdx.x;
   const int64_t i = rows[r];
@@ -2302,7 +2349,7 @@ __global__ __launch_bounds__(256) void k_rf_exact_rows(
   if (j >= n) return;
   float kv;
   if (pc == 0) {
-    kv = __uint_as_float(rf_key(D[i * n_pad + j], inv_sc));
+    kv = Dk != nullptr ? Dk[i * n_pad + j] : __uint_as_float(rf_key(D[i * n_pad + j], inv_sc));
   } else {
     const T* xi = x + i * p_in;
     const T* xj = x + j * p_in;
@@ -2645,6 +2692,7 @@ struct Plan {
   int2 tw = make_int2(0, 0);    // k_exact_pairs' store_pair: (nb, world) when tiled
   int2 win = make_int2(0, 0);   // full layout: rows [win.x, win.y) stored (d_row_in)
   void* D_alloc = nullptr;      // allocation behind D (D itself points at row 0)
+  float* Dk = nullptr;          // ReliefF: the float32 keys instead of D (same layout)
   int2* tiles = nullptr;
   double* thr = nullptr;
   float* Wt = nullptr;          // dense pair weights (sparse == 0)
@@ -3590,8 +3638,12 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
   if (const char* e = std::getenv("FS_KSPLIT"))  // A/B and tests
     if (std::atoi(e) >= 1) g->ksplit = std::min(16, std::atoi(e));
   if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
+  // ReliefF stores float32 keys (Dk), formed in k_dist's epilogue from whole
+  // tiles: no K-split (partial sums cannot be keyed before they are added)
+  const bool dkeys = Q.algo == ALGO_RELIEFF;
+  if (dkeys) g->ksplit = 1;
   g->sk_wgs = 0;
-  if (Q.algo != ALGO_SURF && !std::getenv("FS_KSPLIT")) {
+  if (Q.algo != ALGO_SURF && !dkeys && !std::getenv("FS_KSPLIT")) {
     g->sk_wgs = choose_streamk(g->n_tiles, g->device, rows_q / kBKQ, g->ksplit);
     if (g->sk_wgs > 0) g->ksplit = 1;
   }
@@ -3599,8 +3651,12 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
   g->kfull = g->ksplit > 1 ? 0 : g->n_tiles;  // k_dist can split only a tail; all or none here
   g->alloc_target = 3;
   int rc = FS_OK;
-  if ((rc = dalloc(g, (double**)&g->D_alloc, (size_t)g->dplane)) ||
-      (g->D = (double*)g->D_alloc - (g->tiled ? 0 : (int64_t)g->win.x * Q.n_pad), false) ||
+  g->Dk = nullptr;
+  if ((rc = dkeys ? dalloc(g, (float**)&g->D_alloc, (size_t)g->dplane)
+                  : dalloc(g, (double**)&g->D_alloc, (size_t)g->dplane)) ||
+      (dkeys ? (g->Dk = (float*)g->D_alloc - (int64_t)g->win.x * Q.n_pad, g->D = nullptr)
+             : (g->D = (double*)g->D_alloc - (g->tiled ? 0 : (int64_t)g->win.x * Q.n_pad)),
+       false) ||
       (rc = dalloc(g, &g->tiles, g->n_tiles)) ||
       (rc = dalloc(g, &g->rspart, (size_t)std::max<int64_t>(g->n_tiles, 1) * 256))) {
   } else if (Q.algo != ALGO_RELIEFF && !g->sparse) {
@@ -3830,7 +3886,7 @@ static int run_quantize_dist(Plan* g) {
     if (g->sk_wgs > 0) {
       k_dist<<<(unsigned)g->sk_wgs, 256, 0, g->stream>>>(
           g->xqT, Q.n_pad, nck, nckd, Q.SCu, Q.q16, g->tiles, g->n_tiles, 1, g->tiled, g->win,
-          g->D, g->Dpart, g->sk_wgs, g->sk_units);
+          g->D, g->Dpart, g->sk_wgs, g->sk_units, g->Dk, 1.0 / Q.SC);
       FS_TRY(launch_check("k_dist"));
       k_dist_merge_sk<<<dim3((unsigned)g->n_tiles, kMergeSlices), 256, 0, g->stream>>>(
           g->D, g->Dpart, g->tiles, (int64_t)(nck + nckd), g->sk_wgs, g->sk_units, Q.n_pad,
@@ -3839,7 +3895,7 @@ static int run_quantize_dist(Plan* g) {
     } else {
       k_dist<<<(unsigned)(n_full + n_split * g->ksplit), 256, 0, g->stream>>>(
           g->xqT, Q.n_pad, nck, nckd, Q.SCu, Q.q16, g->tiles, n_full, g->ksplit, g->tiled,
-          g->win, g->D, g->Dpart, 0, 0);
+          g->win, g->D, g->Dpart, 0, 0, g->Dk, 1.0 / Q.SC);
       FS_TRY(launch_check("k_dist"));
       if (n_split > 0) {
         k_dist_merge<<<dim3((unsigned)n_split, kMergeSlices), 256, 0, g->stream>>>(
@@ -3903,11 +3959,11 @@ static int refine_pairs(Plan* g, int algo, double delta) {
   else if (g->x_is_f64)
     k_exact_pairs<double><<<grid, 256, 0, g->stream>>>(
         (const double*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D);
+        g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D, nullptr);
   else
     k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
         (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D);
+        g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D, nullptr);
   return launch_check("k_exact_pairs");
 }
 
@@ -4257,7 +4313,9 @@ static int64_t row_panel_rows(const Prepared& P, int device, int64_t rows) {
     return rows;
   }
   const double fixed = 20.0 * (double)P.n_pad * (double)P.PW + 8.0 * (double)P.n * (double)P.p_in;
-  const double per_row = 24.0 * (double)P.n_pad;
+  // a stored row of D (8 bytes per sample; ReliefF's float32 keys 4) plus
+  // the per-row scratch
+  const double per_row = (P.algo == ALGO_RELIEFF ? 20.0 : 24.0) * (double)P.n_pad;
   const double avail = 0.8 * (double)free_b - fixed;
   if (avail <= per_row * kTile) return kTile;  // let the allocation report it
   const int64_t fit = (int64_t)(avail / per_row) / kTile * kTile;
@@ -4337,18 +4395,18 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   const size_t shstage = shbytes + (size_t)n * 5;
   const bool stage = shstage <= 160 * 1024;
   if (stage)
-    FS_HIP(hipFuncSetAttribute((const void*)k_rf_select<true>,
+    FS_HIP(hipFuncSetAttribute((const void*)k_rf_select<true, true>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)shstage));
   // band of the exact-key refinement (quantisation error + float32 rounding)
   const double band_abs = 2.0 * Q.amb_delta, band_rel = 2.0 * 1.2e-7;
   auto select = [&](int collect, int2* lst) {
     if (stage)
-      k_rf_select<true><<<(unsigned)nr_own, 1024, shstage, g->stream>>>(
-          g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, r_lo, tkey, tneed, teq, nbr,
+      k_rf_select<true, true><<<(unsigned)nr_own, 1024, shstage, g->stream>>>(
+          g->D, g->Dk, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, r_lo, tkey, tneed, teq, nbr,
           nfound, band_abs, band_rel, lst, g->list_cap, g->list_count);
     else
-      k_rf_select<false><<<(unsigned)nr_own, 256, shbytes, g->stream>>>(
-          g->D, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, r_lo, tkey, tneed, teq, nbr,
+      k_rf_select<false, true><<<(unsigned)nr_own, 256, shbytes, g->stream>>>(
+          g->D, g->Dk, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, r_lo, tkey, tneed, teq, nbr,
           nfound, band_abs, band_rel, lst, g->list_cap, g->list_count);
     return launch_check("k_rf_select");
   };
@@ -4364,7 +4422,7 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   for (int attempt = 0; attempt < 3; attempt++) {
     if (attempt > 0) {
       FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
-      k_rf_flag<<<(unsigned)nr_own, 256, 0, g->stream>>>(g->D, n, Q.n_pad, inv_sc, g->lab, C,
+      k_rf_flag<<<(unsigned)nr_own, 256, 0, g->stream>>>(g->D, g->Dk, n, Q.n_pad, inv_sc, g->lab, C,
                                                          tkey, tneed, band_abs, band_rel, r_lo,
                                                          g->list, g->list_cap, g->list_count);
       FS_TRY(launch_check("k_rf_flag"));
@@ -4388,7 +4446,7 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
     const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
     k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
         (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, make_int2(0, 0), g->win, 1, g->D);
+        g->list_count, g->list_cap, Q.n_pad, make_int2(0, 0), g->win, 1, g->D, g->Dk);
     FS_TRY(launch_check("k_exact_pairs"));
   }
   // 3. exact selection
@@ -4429,7 +4487,7 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
     const int64_t nr = std::min<int64_t>(batch, (int64_t)tie_rows.size() - r0);
     FS_TRY(h2d(g, drows, tie_rows.data() + r0, (size_t)nr));
     k_rf_exact_rows<float><<<dim3((unsigned)nr, (unsigned)((n + 3) / 4)), 256, 0, g->stream>>>(
-        (const float*)g->x, n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, drows, g->D,
+        (const float*)g->x, n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, drows, g->D, g->Dk,
         Q.n_pad, inv_sc, keys);
     FS_TRY(launch_check("k_rf_exact_rows"));
     if (n <= kTieLdsMaxN)

@@ -16,7 +16,8 @@ size):
                the same diffs and decisions, every later sum in float64)
 
 Inputs follow SURVEY.md §8d: make_classification(n, p, n_informative=20,
-n_redundant=R, random_state=42), R = 50 for cfg3 and 100 otherwise.
+n_redundant=R, random_state=42), R = 50 for cfg3 and 100 otherwise; the
+3-class cfg3 variant passes n_classes=3 (recorded in the fixture).
 
 Run (container, ~45 min on 8 cores for everything):
     python tests/golden/make_fullsize.py [names...]
@@ -40,6 +41,9 @@ CONFIGS = {
     "cfg5_surf_slice": ("surf", 10000, 50000, 100, (4992, 5376), {"use_star": False}),
     "cfg5_multisurfstar": ("multisurf", 10000, 50000, 100, None, {"use_star": True}),
     "cfg4_multisurf": ("multisurf", 20000, 20000, 100, None, {}),
+    # "add a 3-class cfg3 variant to exercise prior weights"
+    "cfg3_relieff_k10_3class": ("relieff", 20000, 2000, 50, None,
+                                {"n_neighbors": 10, "n_classes": 3}),
     # accum='f64': the oracle with every sum after the diffs in float64 (not
     # the reference; the "exact" side of tests/test_parity_attribution.py)
     "cfg2_multisurf_f64": ("multisurf", 5000, 5000, 100, None, {"accum": "f64"}),
@@ -51,13 +55,15 @@ CONFIGS = {
     "cfg4_multisurf_f64": ("multisurf", 20000, 20000, 100, None, {"accum": "f64"}),
     "cfg5_multisurfstar_f64": ("multisurf", 10000, 50000, 100, None,
                                {"use_star": True, "accum": "f64"}),
+    "cfg3_relieff_k10_3class_f64": ("relieff", 20000, 2000, 50, None,
+                                    {"n_neighbors": 10, "n_classes": 3, "accum": "f64"}),
 }
 
 
-def make_data(n, p, n_redundant, seed=42):
+def make_data(n, p, n_redundant, seed=42, n_classes=2):
     from sklearn.datasets import make_classification
     return make_classification(n_samples=n, n_features=p, n_informative=20,
-                               n_redundant=n_redundant, random_state=seed)
+                               n_redundant=n_redundant, n_classes=n_classes, random_state=seed)
 
 
 def x_digest(x):
@@ -67,8 +73,10 @@ def x_digest(x):
 def run(name, n_jobs):
     from oracle import oracle as O
     algo, n, p, red, i_range, extra = CONFIGS[name]
+    extra = dict(extra)
+    n_classes = extra.pop("n_classes", 2)
     t0 = time.time()
-    X, y = make_data(n, p, red)
+    X, y = make_data(n, p, red, n_classes=n_classes)
     if algo == "multisurf":
         x = X.astype(np.float32)
         s = O.multisurf_scores(x, y, i_range=i_range, n_jobs=n_jobs, **extra)
@@ -85,7 +93,7 @@ def run(name, n_jobs):
              n_redundant=np.array(red), algo=np.array(algo),
              use_star=np.array(bool(extra.get("use_star", False))),
              n_neighbors=np.array(int(extra.get("n_neighbors", 0))),
-             accum=np.array(extra.get("accum", "f32")))
+             accum=np.array(extra.get("accum", "f32")), n_classes=np.array(n_classes))
     print(f"{name}: {time.time() - t0:.0f} s -> {out}", flush=True)
 
 

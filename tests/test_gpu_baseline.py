@@ -76,19 +76,20 @@ def _attribute(name, s, ref, per_element_bar, rms=True):
         assert per_element(s, exact, 1e-2, TOL)["over"] == 0.0, msg
 
 
-def _data(n, p, red):
-    key = (n, p, red)
+def _data(n, p, red, n_classes=2):
+    key = (n, p, red, n_classes)
     if key not in _DATA:
         from sklearn.datasets import make_classification
         _DATA.clear()  # one configuration resident at a time (cfg5 X is 4 GB)
         _DATA[key] = make_classification(n_samples=n, n_features=p, n_informative=20,
-                                         n_redundant=red, random_state=42)
+                                         n_redundant=red, n_classes=n_classes, random_state=42)
     return _DATA[key]
 
 
 def _inputs(fx):
     n, p, red = int(fx["n"]), int(fx["p"]), int(fx["n_redundant"])
-    X, y = _data(n, p, red)
+    ncls = int(fx["n_classes"]) if "n_classes" in fx else 2
+    X, y = _data(n, p, red, ncls)
     algo = str(fx["algo"])
     x = X if algo == "surf" else X.astype(np.float32)
     dig = hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest()
@@ -122,6 +123,17 @@ def test_cfg3_relieff_k10_whole_fit(lib):
     assert est.effective_backend_ == "gpu"
     assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
     _attribute("cfg3_relieff_k10", est.feature_importances_, fx["scores"], True)
+
+
+def test_cfg3_relieff_k10_three_classes(lib):
+    """SURVEY.md §8d's 3-class cfg3 variant: prior-weighted misses of two
+    other classes per focal sample (ReliefF.py:177-216)."""
+    fx = _fixture("cfg3_relieff_k10_3class")
+    X, y = _inputs(fx)
+    est = lib.ReliefF(backend="gpu", n_neighbors=10, n_features_to_select=TOPK).fit(X, y)
+    assert est.effective_backend_ == "gpu"
+    assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
+    _attribute("cfg3_relieff_k10_3class", est.feature_importances_, fx["scores"], True)
 
 
 def test_cfg4_multisurf_north_star(lib):

@@ -63,8 +63,9 @@ def main():
     for path in paths:
         fx = np.load(path, allow_pickle=False)
         n, p, red = int(fx["n"]), int(fx["p"]), int(fx["n_redundant"])
+        ncls = int(fx["n_classes"]) if "n_classes" in fx else 2
         X, y = make_classification(n_samples=n, n_features=p, n_informative=20, n_redundant=red,
-                                   random_state=42)
+                                   n_classes=ncls, random_state=42)
         lo, hi = (int(v) for v in fx["i_range"])
         ref = fx["scores"]
         f64 = path[:-4] + "_f64.npz"
