@@ -98,12 +98,14 @@ def test_multisurf_sizes(oracle, n, p, ncls, seed):
 
 
 @pytest.mark.parametrize("n,p,nd,seed", [(1024, 64, 0, 1), (700, 600, 0, 2), (900, 800, 0, 7),
-                                          (600, 1400, 30, 8), (640, 300, 300, 5)])
+                                          (600, 1400, 30, 8), (640, 300, 300, 5), (800, 576, 0, 9),
+                                          (700, 520, 20, 10)])
 def test_multisurf_sparse_pass2_layouts(oracle, n, p, nd, seed):
     """Layouts of the sparse pass 2 (k_score_sparse2): a single 64-feature
     block with n a multiple of 128 (the last row's B reads run into xs's
     slack), a 256-feature tail, a tail over 256 features (one partial
-    512-feature block), discrete columns in the last block, all discrete."""
+    512-feature block), discrete columns in the last block, all discrete, a
+    64-feature tail (one F = 4 block), continuous and discrete."""
     from fastselect_amd import MultiSURF
     X, y = make_classification(n_samples=n, n_features=p, n_informative=min(10, p // 2),
                                n_redundant=min(20, p // 4), random_state=seed)
