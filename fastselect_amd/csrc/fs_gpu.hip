@@ -16,7 +16,8 @@
 //                   VGPRs, pair weights in SGPRs (scalar loads),
 //                   acc += w * |a - b| (v_sub_f32 + v_fma_f32 |.|). VALU-bound
 //   k_reduce        deterministic segment sum of pass-2 partials.
-//   k_rf_select     ReliefF: per-row radix select of the k nearest per class.
+//   k_rf_select     ReliefF: per-row radix select of the k nearest per class,
+//                   exact keys of the candidates at the k-th key, in one launch.
 //   k_rf_update     ReliefF: neighbour-gather update.
 //
 // No float atomics touch scores: every reduction has a fixed order, so two
@@ -1913,7 +1914,7 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part
 // The key of j is the reference's float32 distance row (ReliefF.py:149-155):
 // float32(D_ij / SC) from the quantised distance, or the exact reference key
 // where k_exact_pairs stored one.  ReliefF plans store these keys directly
-// (Dk, float32: k_dist's epilogue forms them, k_exact_pairs overwrites the
+// (Dk, float32: k_dist's epilogue forms them, k_rf_select overwrites the
 // refined ones); rf_key forms them from a float64 D (negative = exact key),
 // the layout of the other plans.
 __device__ __forceinline__ uint32_t rf_key(double d, double inv_sc) {
@@ -1925,29 +1926,51 @@ __device__ __forceinline__ uint32_t rf_key(double d, double inv_sc) {
 // common key bits, then a ranked gather of the chosen bucket, or 8-bit
 // passes when the bucket is big) -> tkey[i][c], and tneed[i][c] = how many
 // keys equal to T_c belong to the k_c nearest (0 when the class is taken
-// whole).  With `collect`, every key < T_c (index order) and then the first
-// tneed keys == T_c (index order) go to nbr (rows where more keys equal T_c
-// than are needed are re-ordered the reference's way by k_rf_ties), and
-// teq[i][c] counts the keys equal to T_c.
+// whole).  With x (continuous features), the candidates within the band of
+// their class's T_c get the reference's exact keys in the kernel and T_c is
+// re-selected among them (see the refinement below).  Every key < T_c (index
+// order) and then the first tneed keys == T_c (index order) go to nbr (rows
+// where more keys equal T_c than are needed are re-ordered the reference's
+// way by k_rf_ties), and teq[i][c] counts the keys equal to T_c.
 // KF: the plan stores ReliefF's distances as the float32 keys themselves
-// (Dk: k_dist's epilogue and k_exact_pairs write them), half the bytes of D.
+// (Dk: k_dist's epilogue writes them, this kernel the refined ones), half
+// the bytes of D.
+// -DFS_RF_PROF (profiling builds only): per-phase wall-clock stamps of the
+// first 4096 rows of a k_rf_select launch, printed under FS_TRACE
+#ifdef FS_RF_PROF
+__device__ uint64_t fs_rf_prof[4096 * 8];
+#define RF_T(k)                                                  \
+  do {                                                           \
+    if (threadIdx.x == 0 && blockIdx.x < 4096)                   \
+      fs_rf_prof[blockIdx.x * 8 + (k)] = wall_clock64();         \
+  } while (0)
+#else
+#define RF_T(k) \
+  do {          \
+  } while (0)
+#endif
 template <bool STAGE, bool KF>
 __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D,
                                                    const float* __restrict__ Dk, int64_t n,
                                                    int64_t n_pad, double inv_sc,
                                                    const int32_t* __restrict__ lab,
                                                    const int64_t* __restrict__ class_count,
-                                                   int n_classes, int64_t k, int collect,
+                                                   int n_classes, int64_t k,
                                                    int64_t row0, uint32_t* __restrict__ tkey,
                                                    int32_t* __restrict__ tneed,
                                                    int32_t* __restrict__ teq,
                                                    int32_t* __restrict__ nbr,
                                                    int32_t* __restrict__ nfound,
                                                    double band_abs, double band_rel,
-                                                   int2* __restrict__ list, int64_t cap,
-                                                   unsigned long long* __restrict__ count) {
+                                                   int64_t cap,
+                                                   unsigned long long* __restrict__ count,
+                                                   const float* __restrict__ x, int64_t p_in,
+                                                   int64_t pc, int64_t PC, int64_t pd,
+                                                   const int64_t* __restrict__ src_col,
+                                                   const double* __restrict__ scl, int xlds) {
   // hist[n_classes][1024 (n_classes <= 8) or 256], prefix[C], need[C], then
-  // (STAGE) the row's keys and class codes
+  // (STAGE) the row's keys and class codes, then (xlds) the focal sample's
+  // continuous values, their columns and scales for the exact keys
   extern __shared__ uint32_t sh[];
   uint32_t* hist = sh;
   uint32_t* prefix = sh + n_classes * (n_classes <= 8 ? 1024 : 256);
@@ -1966,6 +1989,60 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
     return STAGE ? keys[j] : (KF ? __float_as_uint(rowk[j]) : rf_key(row[j], inv_sc));
   };
   auto lab_of = [&](int64_t j) { return STAGE ? (int32_t)labs[j] : lab[j]; };
+  // xlds > 0: an LDS buffer of xlds floats after the row's keys (the host
+  // sizes it from what is left of the 160 KB) for the listed candidates'
+  // exact keys: all threads gather x_i, the scales and a batch of candidate
+  // rows at their continuous columns, then each wave sums one candidate from
+  // LDS (two dependent loads per row of candidates, not two per 512 columns)
+  float* xbuf = nullptr;
+  if (x != nullptr && xlds > 0) {
+    uintptr_t base = STAGE ? (uintptr_t)(labs + n) : (uintptr_t)keys;
+    xbuf = (float*)((base + 15) & ~(uintptr_t)15);
+  }
+  const int64_t xb_rows = xbuf != nullptr && pc > 0 ? (int64_t)xlds / pc - 2 : 0;
+  const float* __restrict__ xi = x != nullptr ? x + i * p_in : nullptr;
+  // The reference's float32 key of pair (i, jj), wave-wide (every lane gets
+  // it): k_exact_pairs<float>'s sum term by term in its order (lane l sums
+  // columns l, l+64, ... in f64, then the discrete mismatches, then the
+  // xor-shuffle tree); the unroll only batches the loads.
+  auto exact_key = [&](int64_t jj, int ln) -> double {
+    const float* __restrict__ xj = x + jj * p_in;
+    double acc = 0.0;
+    {
+      constexpr int kUe = 8;
+      for (int64_t c0 = ln; c0 < pc; c0 += 64 * kUe) {
+        int64_t col[kUe];
+        float av[kUe], bv[kUe], sv[kUe];
+#pragma unroll
+        for (int u = 0; u < kUe; u++) {
+          col[u] = c0 + 64 * u < pc ? src_col[c0 + 64 * u] : -1;
+          sv[u] = c0 + 64 * u < pc ? (float)scl[c0 + 64 * u] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kUe; u++) {
+          av[u] = col[u] >= 0 ? xi[col[u]] : 0.0f;
+          bv[u] = col[u] >= 0 ? xj[col[u]] : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kUe; u++)
+          if (col[u] >= 0) acc += (double)(__builtin_fabsf(av[u] - bv[u]) * sv[u]);
+      }
+    }
+    for (int64_t c = PC + ln; c < PC + pd; c += 64) {
+      const int64_t cl = src_col[c];
+      acc += (xi[cl] != xj[cl]) ? 1.0 : 0.0;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    return acc;
+  };
+  // stores pair (i, jj)'s exact key into the row (LDS or HBM); its bits
+  auto store_key = [&](int64_t jj, double acc) -> uint32_t {
+    const uint32_t v = __float_as_uint((float)acc);  // acc >= 0: +0 at worst
+    if (STAGE) keys[jj] = v;
+    else if (KF) const_cast<float*>(rowk)[jj] = (float)acc;
+    else const_cast<double*>(row)[jj] = -(double)(float)acc;
+    return v;
+  };
   // Key range of the row: bits above the highest bit in which two keys
   // differ are common to all of them, so the radix passes start below it
   // (a row's distances share their float exponent or nearly: starting at
@@ -1975,6 +2052,7 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
   // 8 independent loads in flight per thread (one workgroup per CU when
   // staging: the row read is latency-bound otherwise)
   constexpr int kU = 8;
+  RF_T(0);
   for (int64_t j0 = tid; j0 < n; j0 += (int64_t)kU * nt) {
     uint32_t rv[kU];  // the raw key (KF) ...
     double dv[kU];    // ... or the distance it is formed from
@@ -2016,6 +2094,26 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
     kor |= red_or[w];
     kand &= red_and[w];
   }
+  // x != null: the exact keys in one launch.  Round 0 selects on the
+  // quantised keys; every candidate whose key lies within the band of its
+  // class's k-th key then gets the reference's key, computed right here by
+  // one wave with k_exact_pairs' arithmetic, and round 1 selects again on
+  // the updated row (no pair list, no second read of the row).  kor / kand
+  // also take the exact keys in (a wider key range is still a valid one).
+  __shared__ uint32_t kor_s, kand_s;
+  __shared__ int n_ex, nflag;
+  __shared__ uint32_t lcnt[64];  // keys of a class below T outside the band
+  __shared__ uint32_t bcount[64];  // keys in the chosen bucket, per class
+  __shared__ uint8_t done[64];
+  __shared__ uint32_t gcnt[64];
+  __shared__ int any_big;
+  RF_T(1);
+  if (tid == 0) kor_s = kor, kand_s = kand, n_ex = 0;
+  const int rounds = x != nullptr ? 2 : 1;
+  for (int round = 0; round < rounds; round++) {
+  __syncthreads();
+  kor = kor_s;
+  kand = kand_s;
   const uint32_t diff = kor & ~kand;  // bits that are not common
   const int top = diff ? 31 - __builtin_clz(diff) : 0;
   // Pass 1 takes the WB bits [lo1, top] right below the common prefix (a
@@ -2037,11 +2135,9 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
   // One pass: histogram of the digit [lo, hi) of the keys whose bits >= hi
   // match their class's prefix, then per class (one wave each) the bucket
   // holding the need-th key, by a wave prefix sum over the bins.
-  __shared__ uint32_t bcount[64];  // keys in the chosen bucket, per class
   // done[c]: class c's k-th key is final (the small-bucket gather below
   // leaves need[c] as a rank among the keys EQUAL to it, which a further
   // radix pass -- counting all keys under the prefix -- must not reuse)
-  __shared__ uint8_t done[64];
   for (int c = tid; c < n_classes; c += nt) done[c] = 0;
   auto radix_pass = [&](int lo, int hi) {
     const int nbins = 1 << (hi - lo);
@@ -2091,14 +2187,13 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
   };
   __syncthreads();
   radix_pass(lo1, top + 1);
+  RF_T(2);
   if (lo1 > 0) {
     // Small buckets (<= 64 keys: the common case, the k nearest sit in the
     // sparse low tail) finish in one gather: the bucket's keys go to a list
     // (in the histogram space, free now) and the need-th smallest is found by
     // ranking.  Classes with bigger buckets (ties, discrete data) continue
     // with 8-bit passes below lo1.
-    __shared__ uint32_t gcnt[64];
-    __shared__ int any_big;
     uint32_t* list = hist;  // [class][64]
     if (tid == 0) any_big = 0;
     for (int c = tid; c < n_classes; c += nt) {
@@ -2141,40 +2236,164 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
     if (any_big)
       for (int hi = lo1; hi > 0; hi -= 8) radix_pass(hi - 8 > 0 ? hi - 8 : 0, hi);
   }
+  RF_T(3);
+  if (round + 1 < rounds) {
+    // Candidates within the band of their class's k-th key T go to a list
+    // (j | class << 26); the other keys of a class below T are counted
+    // (lcnt: all of them stay below the exact T).  The listed keys get the
+    // reference's keys, spread over the waves, and the exact k-th key of
+    // class c is the (kc - lcnt[c])-th smallest listed key of c: no second
+    // pass over the row.  A list over kFCap entries (ties, discrete-heavy
+    // rows) takes the general route: exact keys in chunk order, then a
+    // second selection over the whole row.
+    constexpr int kFCap = 256;
+    uint32_t* fl = hist;  // [kFCap] entries, [kFCap] exact keys
+    const int wave_e = tid >> 6, lane_e = tid & 63;
+    const int64_t chunk_e = (n + nwaves - 1) / nwaves;
+    const int64_t jb_e = (int64_t)wave_e * chunk_e;
+    const int64_t je_e = jb_e + chunk_e < n ? jb_e + chunk_e : n;
+    auto flagged = [&](int64_t j, int32_t c, uint32_t kv) {
+      const double T = (double)__uint_as_float(prefix[c]);
+      return fabs((double)__uint_as_float(kv) - T) <= band_abs + band_rel * T;
+    };
+    for (int c = tid; c < n_classes; c += nt) lcnt[c] = 0u;
+    if (tid == 0) nflag = 0;
+    __syncthreads();
+    for (int64_t j = jb_e + lane_e; j < je_e; j += 64) {
+      if (j == i) continue;
+      const int32_t c = lab_of(j);
+      if (need[c] == 0) continue;
+      const uint32_t kv = key_of(j);
+      if (flagged(j, c, kv)) {
+        const int slot = atomicAdd(&nflag, 1);
+        if (slot < kFCap) fl[slot] = (uint32_t)j | ((uint32_t)c << 26);
+      } else if (kv < prefix[c]) {
+        atomicAdd(&lcnt[c], 1u);
+      }
+    }
+    __syncthreads();
+    RF_T(4);
+    const int F = nflag;
+    if (F == 0) break;  // nothing near any k-th key: round 0's keys are final
+    if (F <= (cap < kFCap ? (int)cap : kFCap)) {  // cap: FS_RF_FCAP (tests)
+      if (xb_rows >= 1) {
+        // batches of xb_rows candidates: xbuf = [x_i | scales | rows...]
+        for (int e0 = 0; e0 < F; e0 += (int)xb_rows) {
+          const int nb = F - e0 < (int)xb_rows ? F - e0 : (int)xb_rows;
+          const int pci = (int)pc, tot = (nb + 2) * pci;  // < xlds
+          for (int t0 = tid; t0 < tot; t0 += 4 * nt) {
+            float v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+              const int t = t0 + u * nt;
+              v[u] = 0.0f;
+              if (t < tot) {
+                const int q = t / pci, c = t - q * pci;
+                if (q == 1) {
+                  v[u] = (float)scl[c];
+                } else {
+                  const int64_t jr = q == 0 ? i : (int64_t)(fl[e0 + q - 2] & ((1u << 26) - 1u));
+                  v[u] = x[jr * p_in + src_col[c]];
+                }
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+              const int t = t0 + u * nt;
+              if (t < tot) xbuf[t] = v[u];
+            }
+          }
+          __syncthreads();
+          for (int q = wave_e; q < nb; q += nwaves) {
+            const int e = e0 + q;
+            const int64_t jj = (int64_t)(fl[e] & ((1u << 26) - 1u));
+            const float* xr = xbuf + (int64_t)(q + 2) * pc;
+            double acc = 0.0;
+            for (int64_t c = lane_e; c < pc; c += 64)
+              acc += (double)(__builtin_fabsf(xbuf[c] - xr[c]) * xbuf[pc + c]);
+            for (int64_t c = PC + lane_e; c < PC + pd; c += 64) {
+              const int64_t cl = src_col[c];
+              acc += (xi[cl] != x[jj * p_in + cl]) ? 1.0 : 0.0;
+            }
+            for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+            if (lane_e == 0) fl[kFCap + e] = store_key(jj, acc);
+          }
+          __syncthreads();
+        }
+      } else {
+        for (int e = wave_e; e < F; e += nwaves) {
+          const int64_t jj = (int64_t)(fl[e] & ((1u << 26) - 1u));
+          const double acc = exact_key(jj, lane_e);
+          if (lane_e == 0) fl[kFCap + e] = store_key(jj, acc);
+        }
+        __syncthreads();
+      }
+      RF_T(5);
+      for (int c = wave_e; c < n_classes; c += nwaves) {
+        if (need[c] == 0) continue;
+        const int64_t members = class_count[c] - (c == li ? 1 : 0);
+        const uint32_t kc = (uint32_t)(members < k ? members : k);
+        const uint32_t r = kc - lcnt[c];  // 1-based rank among c's listed keys
+        for (int e0 = 0; e0 < F; e0 += 64) {
+          const int e = e0 + lane_e;
+          bool own = false;
+          uint32_t v = 0u, nlt = 0u, nle = 0u;
+          if (e < F && (int)(fl[e] >> 26) == c) {
+            v = fl[kFCap + e];
+            for (int q = 0; q < F; q++) {
+              if ((int)(fl[q] >> 26) != c) continue;
+              const uint32_t w = fl[kFCap + q];
+              nlt += w < v;
+              nle += w <= v;
+            }
+            own = nlt < r && r <= nle;
+          }
+          const uint64_t mo = __ballot(own);
+          if (mo != 0ull) {
+            if (lane_e == (int)__builtin_ctzll(mo)) {
+              prefix[c] = v;
+              need[c] = r - nlt;
+            }
+            break;
+          }
+        }
+      }
+      if (tid == 0) n_ex = F;
+      RF_T(6);
+      __syncthreads();
+      break;
+    }
+    // general route: every flagged sample of a wave's chunk, in order
+    int n_local = 0;
+    for (int64_t j0 = jb_e; j0 < je_e; j0 += 64) {
+      const int64_t j = j0 + lane_e;
+      bool flag = false;
+      if (j < je_e && j != i) {
+        const int32_t c = lab_of(j);
+        if (need[c] != 0) flag = flagged(j, c, key_of(j));
+      }
+      uint64_t m = __ballot(flag);
+      while (m != 0ull) {
+        const int64_t jj = j0 + __builtin_ctzll(m);
+        m &= m - 1ull;
+        const double acc = exact_key(jj, lane_e);
+        if (lane_e == 0) {
+          const uint32_t v = store_key(jj, acc);
+          atomicOr(&kor_s, v);
+          atomicAnd(&kand_s, v);
+        }
+        n_local++;
+      }
+    }
+    if (lane_e == 0 && n_local != 0) atomicAdd(&n_ex, n_local);
+    __threadfence_block();
+    __syncthreads();
+  }
+  }  // rounds
+  if (tid == 0 && count != nullptr && n_ex != 0) atomicAdd(count, (unsigned long long)n_ex);
   for (int c = tid; c < n_classes; c += nt) {
     tkey[i * n_classes + c] = prefix[c];
     tneed[i * n_classes + c] = (int32_t)need[c];
-  }
-  if (!collect) {
-    // k_rf_flag's sweep on the staged row (list != null): candidates whose
-    // quantised key lies within the band of their class's k-th key go to the
-    // exact-pair list, one global atomic per wave with any
-    if (list == nullptr) return;
-    const int lane = tid & 63;
-    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    for (int64_t j0 = 0; j0 < n; j0 += nt) {
-      const int64_t j = j0 + tid;
-      bool flag = false;
-      if (j < n && j != i) {
-        const int32_t c = lab_of(j);
-        if (need[c] != 0) {
-          const double T = (double)__uint_as_float(prefix[c]);
-          const double kv = (double)__uint_as_float(key_of(j));
-          flag = fabs(kv - T) <= band_abs + band_rel * T;
-        }
-      }
-      const uint64_t m = __ballot(flag);
-      if (m == 0ull) continue;
-      const int leader = (int)__builtin_ctzll(m);
-      unsigned long long base = 0ull;
-      if (lane == leader) base = atomicAdd(count, (unsigned long long)__popcll(m));
-      base = __shfl(base, leader);
-      if (flag) {
-        const unsigned long long kk = base + (unsigned long long)__popcll(m & below);
-        if ((int64_t)kk < cap) list[kk] = make_int2((int)i, (int)j);
-      }
-    }
-    return;
   }
   // Ordered collection over all waves: wave w takes the contiguous chunk
   // [j_w, j_w+1) of the row.  Pass 1 counts, per class, the keys below the
@@ -2297,40 +2516,7 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
       }
     }
   }
-}
-
-// Candidates whose quantised key lies within `band` of their class's k-th
-// key T (tkey from a first k_rf_select) go to the exact-pair list: after
-// k_exact_pairs stores their reference keys, a second selection is exact.
-__global__ __launch_bounds__(256) void k_rf_flag(const double* __restrict__ D,
-                                                 const float* __restrict__ Dk, int64_t n,
-                                                 int64_t n_pad, double inv_sc,
-                                                 const int32_t* __restrict__ lab,
-                                                 int n_classes,
-                                                 const uint32_t* __restrict__ tkey,
-                                                 const int32_t* __restrict__ tneed,
-                                                 double band_abs, double band_rel, int64_t row0,
-                                                 int2* __restrict__ list, int64_t cap,
-                                                 unsigned long long* __restrict__ count) {
-  __shared__ PairBuf pb;
-  pairbuf_init(pb);
-  const int64_t i = row0 + blockIdx.x;
-  const double* row = D + i * n_pad;
-  for (int64_t j0 = 0; j0 < n; j0 += 256) {
-    const int64_t j = j0 + threadIdx.x;
-    bool flag = false;
-    if (j < n && j != i) {
-      const int32_t c = lab[j];
-      if (tneed[i * n_classes + c] != 0) {  // 0: class taken whole
-        const double T = (double)__uint_as_float(tkey[i * n_classes + c]);
-        const double kv = Dk != nullptr ? (double)Dk[i * n_pad + j]
-                                        : (double)__uint_as_float(rf_key(row[j], inv_sc));
-        flag = fabs(kv - T) <= band_abs + band_rel * T;
-      }
-    }
-    if (flag) pairbuf_add(pb, i, j, list, cap, count);
-  }
-  pairbuf_flush(pb, list, cap, count);
+  RF_T(7);
 }
 
 // Exact reference keys of whole rows (tie rows of a problem with continuous
@@ -3774,7 +3960,8 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     owned_tiles(g->nb, rank, world, bi, bj);
   }
   g->row_mode = row_mode;
-  g->list_cap = std::max<int64_t>(1 << 16, Q.n * 64);
+  // (ReliefF refines in k_rf_select and uses only the counter)
+  g->list_cap = Q.algo == ALGO_RELIEFF ? 1 : std::max<int64_t>(1 << 16, Q.n * 64);
   g->use_q16 = choose_q16(Q);
   const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
   int rc;
@@ -4392,65 +4579,68 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   g->alloc_target = 0;
   // histograms: 1024 bins per class for n_classes <= 8 (10-bit first digit)
   const size_t shbytes = (size_t)C * (C <= 8 ? 1024 : 256) * 4 + 2 * (size_t)C * 4;
-  const size_t shstage = shbytes + (size_t)n * 5;
-  const bool stage = shstage <= 160 * 1024;
-  if (stage)
-    FS_HIP(hipFuncSetAttribute((const void*)k_rf_select<true, true>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)shstage));
+  size_t shstage = shbytes + (size_t)n * 5;
+  // (k_rf_select's static LDS, ~1 KB, comes out of the same 160 KB)
+  constexpr size_t kSelLds = 159 * 1024;
+  const bool stage = shstage <= kSelLds;
+  // the rest of the 160 KB: the exact keys' gather buffer (x_i, the scales
+  // and at least one candidate row at the continuous columns), else none
+  // (the unstaged kernel keeps to 40 KB: four workgroups per CU)
+  size_t shsel = stage ? shstage : shbytes;
+  int xlds = 0;
+  const size_t lds_cap = stage ? kSelLds : 40 * 1024;
+  const size_t lds_left = lds_cap > shsel + 16 ? lds_cap - 16 - shsel : 0;
+  if (Q.pc > 0 && lds_left / 4 >= (size_t)Q.pc * 3) xlds = (int)(lds_left / 4);
+  if (const char* e = std::getenv("FS_RF_XLDS")) {  // A/B, tests: a cap in floats
+    const long v = std::atol(e);
+    if (v < xlds) xlds = v >= 3 * Q.pc ? (int)v : 0;
+  }
+  if (xlds) shsel += 16 + (size_t)xlds * 4;
+  if (shsel > 64 * 1024) {
+    if (stage)
+      FS_HIP(hipFuncSetAttribute((const void*)k_rf_select<true, true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shsel));
+    else
+      FS_HIP(hipFuncSetAttribute((const void*)k_rf_select<false, true>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)shsel));
+  }
   // band of the exact-key refinement (quantisation error + float32 rounding)
   const double band_abs = 2.0 * Q.amb_delta, band_rel = 2.0 * 1.2e-7;
-  auto select = [&](int collect, int2* lst) {
-    if (stage)
-      k_rf_select<true, true><<<(unsigned)nr_own, 1024, shstage, g->stream>>>(
-          g->D, g->Dk, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, r_lo, tkey, tneed, teq, nbr,
-          nfound, band_abs, band_rel, lst, g->list_cap, g->list_count);
-    else
-      k_rf_select<false, true><<<(unsigned)nr_own, 256, shbytes, g->stream>>>(
-          g->D, g->Dk, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, collect, r_lo, tkey, tneed, teq, nbr,
-          nfound, band_abs, band_rel, lst, g->list_cap, g->list_count);
-    return launch_check("k_rf_select");
-  };
-  // 1. k-th keys from the quantised distances, and (same launch, on the
-  // staged row) the candidates inside the band around them
+  // One launch: selection on the quantised keys, the reference's keys for
+  // the candidates inside the band around each k-th key (computed in the
+  // kernel, k_exact_pairs' arithmetic), the exact k-th keys, ordered
+  // collection.
+  // Continuous features only need the exact keys (discrete distances are
+  // exact integers already).
+  const float* xk = Q.pc > 0 ? (const float*)g->x : nullptr;
+  // candidates listed in LDS per row (above: the general route); FS_RF_FCAP
+  // lowers it (0 forces the general route: tests)
+  int64_t fcap = 256;
+  if (const char* e = std::getenv("FS_RF_FCAP")) fcap = std::max<int64_t>(0, std::atoll(e));
   FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
+#ifdef FS_RF_PROF
+  {
+    void* pp = nullptr;
+    FS_HIP(hipGetSymbolAddress(&pp, HIP_SYMBOL(fs_rf_prof)));
+    FS_HIP(hipMemsetAsync(pp, 0, 4096 * 8 * 8, g->stream));
+  }
+#endif
   FS_HIP(hipEventRecord(g->ev[4], g->stream));
-  FS_TRY(select(0, g->list));
+  if (stage)
+    k_rf_select<true, true><<<(unsigned)nr_own, 1024, shsel, g->stream>>>(
+        g->D, g->Dk, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, r_lo, tkey, tneed, teq, nbr,
+        nfound, band_abs, band_rel, fcap, g->list_count, xk, Q.p_in, Q.pc, Q.PC, Q.pd,
+        g->src_col, g->scl, xlds);
+  else
+    k_rf_select<false, true><<<(unsigned)nr_own, 256, shsel, g->stream>>>(
+        g->D, g->Dk, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, r_lo, tkey, tneed, teq, nbr,
+        nfound, band_abs, band_rel, fcap, g->list_count, xk, Q.p_in, Q.pc, Q.PC, Q.pd,
+        g->src_col, g->scl, xlds);
+  FS_TRY(launch_check("k_rf_select"));
   FS_HIP(hipEventRecord(g->ev[5], g->stream));
-  // 2. exact keys inside the band; a list that overflowed is grown and the
-  // band re-flagged by k_rf_flag (from the stored keys)
-  g->n_refined = 0;
-  for (int attempt = 0; attempt < 3; attempt++) {
-    if (attempt > 0) {
-      FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
-      k_rf_flag<<<(unsigned)nr_own, 256, 0, g->stream>>>(g->D, g->Dk, n, Q.n_pad, inv_sc, g->lab, C,
-                                                         tkey, tneed, band_abs, band_rel, r_lo,
-                                                         g->list, g->list_cap, g->list_count);
-      FS_TRY(launch_check("k_rf_flag"));
-    }
-    unsigned long long cnt = 0;
-    FS_HIP(hipMemcpyAsync(&cnt, g->list_count, sizeof(cnt), hipMemcpyDeviceToHost, g->stream));
-    FS_HIP(hipStreamSynchronize(g->stream));
-    if ((int64_t)cnt <= g->list_cap) {
-      g->n_refined = (int64_t)cnt;
-      break;
-    }
-    if (attempt == 2) {
-      set_error("ReliefF exact-pair list: overflow after growing");
-      return FS_EHIP;
-    }
-    g->list_cap = (int64_t)cnt + cnt / 4;
-    FS_TRY(dalloc(g, &g->list, g->list_cap));  // persistent (alloc_target 0 here)
-  }
-  if (g->n_refined > 0) {
-    FS_TRY(sort_pair_list(g, g->n_refined));
-    const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
-    k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
-        (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, make_int2(0, 0), g->win, 1, g->D, g->Dk);
-    FS_TRY(launch_check("k_exact_pairs"));
-  }
-  // 3. exact selection
-  FS_TRY(select(1, nullptr));
+  // exact keys computed (list_count), read with the tie counts below
+  unsigned long long ex_cnt = 0;
+  FS_HIP(hipMemcpyAsync(&ex_cnt, g->list_count, sizeof(ex_cnt), hipMemcpyDeviceToHost, g->stream));
   // 4. rows with more neighbours at the k-th key than needed
   std::vector<int32_t> hneed((size_t)nr_own * C), heq((size_t)nr_own * C);
   FS_HIP(hipMemcpyAsync(hneed.data(), tneed + r_lo * C, hneed.size() * 4, hipMemcpyDeviceToHost,
@@ -4458,6 +4648,27 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   FS_HIP(hipMemcpyAsync(heq.data(), teq + r_lo * C, heq.size() * 4, hipMemcpyDeviceToHost,
                         g->stream));
   FS_HIP(hipStreamSynchronize(g->stream));
+  g->n_refined = (int64_t)ex_cnt;
+#ifdef FS_RF_PROF
+  if (trace_on()) {
+    std::vector<uint64_t> pr(4096 * 8);
+    FS_HIP(hipMemcpyFromSymbol(pr.data(), HIP_SYMBOL(fs_rf_prof), pr.size() * 8));
+    const int64_t nrow = std::min<int64_t>(4096, nr_own);
+    double acc[8] = {0};
+    for (int64_t r = 0; r < nrow; r++) {
+      uint64_t last = pr[r * 8];
+      for (int q = 1; q < 8; q++) {
+        const uint64_t b = pr[r * 8 + q];
+        if (b == 0) continue;  // phase skipped
+        acc[q] += (double)(b - last);
+        last = b;
+      }
+    }
+    std::fprintf(stderr, "[fs_trace] k_rf_select phases (us/row, 100 MHz):");
+    for (int q = 1; q < 8; q++) std::fprintf(stderr, " %d:%.2f", q, acc[q] / nrow / 100.0);
+    std::fprintf(stderr, "\n");
+  }
+#endif
   std::vector<int32_t> tie_rows;
   for (int64_t r = 0; r < nr_own; r++)
     for (int c = 0; c < C; c++)

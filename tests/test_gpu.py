@@ -181,6 +181,48 @@ def test_relieff_small_and_big_buckets_in_one_row(oracle):
         np.testing.assert_array_equal(_fit(ReliefF, X, y, n_neighbors=k), s)
 
 
+def test_relieff_unstaged_rows(oracle):
+    """n past what k_rf_select stages in LDS (5 bytes per sample + the
+    histograms > 160 KB: n > ~31000): the row is read from HBM on every
+    sweep (k_rf_select<false>, 256 threads per row)."""
+    from fastselect_amd import ReliefF
+    X, y = make_classification(n_samples=33000, n_features=24, n_informative=8, n_redundant=4,
+                               random_state=13)
+    s = _fit(ReliefF, X, y, n_neighbors=5)
+    assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=5), TOL, k=5)
+
+
+@pytest.mark.parametrize("n", [2500, 33000])
+def test_relieff_exact_keys_lds_and_global(n, monkeypatch):
+    """k_rf_select's in-kernel exact keys: candidate rows gathered into LDS
+    in batches (default; one row per batch with FS_RF_XLDS=3*pc) or summed
+    straight from HBM (FS_RF_XLDS=0), and the
+    exact k-th key comes from the row's candidate list (default) or from a
+    second selection over the whole row (FS_RF_FCAP=0, the route of rows with
+    over 256 candidates): the keys are the same float32 numbers and the
+    selections agree, so the scores are bit-identical.  Mixed data (a
+    discrete block), 1100 continuous columns (not a multiple of the unrolled
+    column step); n=33000 takes the unstaged kernel."""
+    from fastselect_amd import ReliefF
+    rng = np.random.default_rng(5)
+    p = 1200 if n < 10000 else 80
+    X, y = make_classification(n_samples=n, n_features=p, n_informative=12, n_redundant=20,
+                               n_classes=3, random_state=17)
+    X[:, -100 if n < 10000 else -10:] = rng.integers(0, 4, size=(n, 100 if n < 10000 else 10))
+    out = {}
+    pc = 1100 if n < 10000 else 70
+    for mode, env in (("default", {}), ("hbm", {"FS_RF_XLDS": "0"}),
+                      ("batch1", {"FS_RF_XLDS": str(3 * pc)}),
+                      ("general", {"FS_RF_FCAP": "0"})):
+        for key, val in env.items():
+            monkeypatch.setenv(key, val)
+        out[mode] = _fit(ReliefF, X, y, n_neighbors=7)
+        for key in env:
+            monkeypatch.delenv(key)
+    for mode in ("hbm", "batch1", "general"):
+        assert np.array_equal(out["default"], out[mode]), mode
+
+
 def test_relieff_ties_large_rows(oracle):
     """Tie replay on rows long enough for many 64-wide partition rounds and
     deep recursion (all-discrete data: ties in every row), CPU == GPU == oracle."""
