@@ -1932,9 +1932,10 @@ __device__ __forceinline__ uint32_t rf_key(double d, double inv_sc) {
 // order) and then the first tneed keys == T_c (index order) go to nbr (rows
 // where more keys equal T_c than are needed are re-ordered the reference's
 // way by k_rf_ties), and teq[i][c] counts the keys equal to T_c.
-// KF: the plan stores ReliefF's distances as the float32 keys themselves
-// (Dk: k_dist's epilogue writes them, this kernel the refined ones), half
-// the bytes of D.
+// The keys are ReliefF's float32 distances as the plan stores them (Dk:
+// k_dist's epilogue writes them, this kernel the refined ones).  STAGE: the
+// row and its class codes are staged in LDS (n <= 32768); else read from HBM
+// on every sweep (256 threads per row).
 // -DFS_RF_PROF (profiling builds only): per-phase wall-clock stamps of the
 // first 4096 rows of a k_rf_select launch, printed under FS_TRACE
 #ifdef FS_RF_PROF
@@ -1949,86 +1950,124 @@ __device__ uint64_t fs_rf_prof[4096 * 8];
   do {          \
   } while (0)
 #endif
-template <bool STAGE, bool KF>
-__global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D,
-                                                   const float* __restrict__ Dk, int64_t n,
-                                                   int64_t n_pad, double inv_sc,
-                                                   const int32_t* __restrict__ lab,
-                                                   const int64_t* __restrict__ class_count,
-                                                   int n_classes, int64_t k,
-                                                   int64_t row0, uint32_t* __restrict__ tkey,
-                                                   int32_t* __restrict__ tneed,
-                                                   int32_t* __restrict__ teq,
-                                                   int32_t* __restrict__ nbr,
-                                                   int32_t* __restrict__ nfound,
-                                                   double band_abs, double band_rel,
-                                                   int64_t cap,
-                                                   unsigned long long* __restrict__ count,
-                                                   const float* __restrict__ x, int64_t p_in,
-                                                   int64_t pc, int64_t PC, int64_t pd,
-                                                   const int64_t* __restrict__ src_col,
-                                                   const double* __restrict__ scl, int xlds) {
-  // hist[n_classes][1024 (n_classes <= 8) or 256], prefix[C], need[C], then
-  // (STAGE) the row's keys and class codes, then (xlds) the focal sample's
-  // continuous values, their columns and scales for the exact keys
-  extern __shared__ uint32_t sh[];
+template <bool STAGE>
+__global__ __launch_bounds__(1024) void k_rf_select(
+    const float* __restrict__ Dk, int n, int64_t n_pad, const int32_t* __restrict__ lab,
+    const uint8_t* __restrict__ lab8, const int64_t* __restrict__ class_count, int n_classes,
+    int k, int64_t row0, uint32_t* __restrict__ tkey, int32_t* __restrict__ tneed,
+    int32_t* __restrict__ teq, int32_t* __restrict__ nbr, int32_t* __restrict__ nfound,
+    double band_abs, double band_rel, int fcap, unsigned long long* __restrict__ count,
+    const float* __restrict__ x, int64_t p_in, int pc, int PC, int pd,
+    const int64_t* __restrict__ src_col, const double* __restrict__ scl, int xlds) {
+  // Dynamic LDS: hist[C][1024 (C <= 8) or 256]; STAGE: the row's keys and
+  // class codes by quads of samples (16-byte aligned); xlds floats of exact-
+  // key buffer after them.  Per-class state lives in static LDS.
+  extern __shared__ __align__(16) uint32_t sh[];
+  const int C = n_classes;
+  const int nbins1 = C <= 8 ? 1024 : 256;
+  const int nq = (n + 3) >> 2;
   uint32_t* hist = sh;
-  uint32_t* prefix = sh + n_classes * (n_classes <= 8 ? 1024 : 256);
-  uint32_t* need = prefix + n_classes;
-  uint32_t* keys = need + n_classes;
-  uint8_t* labs = (uint8_t*)(keys + n);  // STAGE: class codes (< 64)
-  const int64_t i = row0 + blockIdx.x;
-  const int tid = threadIdx.x;
-  const int nt = blockDim.x, nwaves = nt >> 6;
-  const int32_t li = lab[i];
-  const double* row = KF ? nullptr : D + i * n_pad;
-  const float* rowk = KF ? Dk + i * n_pad : nullptr;
-  // STAGE: the row's float32 keys are read from HBM once into LDS (the five
-  // sweeps below then cost no HBM traffic)
-  auto key_of = [&](int64_t j) {
-    return STAGE ? keys[j] : (KF ? __float_as_uint(rowk[j]) : rf_key(row[j], inv_sc));
-  };
-  auto lab_of = [&](int64_t j) { return STAGE ? (int32_t)labs[j] : lab[j]; };
-  // xlds > 0: an LDS buffer of xlds floats after the row's keys (the host
-  // sizes it from what is left of the 160 KB) for the listed candidates'
-  // exact keys: all threads gather x_i, the scales and a batch of candidate
-  // rows at their continuous columns, then each wave sums one candidate from
-  // LDS (two dependent loads per row of candidates, not two per 512 columns)
+  uint32_t* keys = sh + C * nbins1;             // STAGE: [4 nq]
+  uint8_t* labs = (uint8_t*)(keys + 4 * nq);    // STAGE: [4 nq]
+  const int i = (int)(row0 + blockIdx.x);
+  const int tid = threadIdx.x, nt = blockDim.x, nwaves = nt >> 6;
+  const int wave = tid >> 6, lane = tid & 63;
+  const int li = lab[i];
+  float* __restrict__ rowk = const_cast<float*>(Dk) + (int64_t)i * n_pad;
+  // the focal sample's own key and the padding after n read as kNone: above
+  // every finite key, and (its bit 31 set) never equal to an active class's
+  // prefix at any digit, so the sweeps need no index test
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  __shared__ uint32_t prefix[64], need[64], pm[64], lcnt[64], bcount[64], gcnt[64];
+  __shared__ uint2 kband[64];  // exact-key band per class: [klo, klo + kn)
+  __shared__ uint8_t done[64];
+  __shared__ uint32_t red_or[16], red_and[16], kor_s, kand_s;
+  __shared__ int n_ex, nflag, any_big;
+
+  // xbuf (exact keys of the listed candidates): [x_i | scales | columns |
+  // candidate rows ...] at the continuous columns, pc floats each
   float* xbuf = nullptr;
   if (x != nullptr && xlds > 0) {
-    uintptr_t base = STAGE ? (uintptr_t)(labs + n) : (uintptr_t)keys;
+    const uintptr_t base = STAGE ? (uintptr_t)(labs + 4 * nq) : (uintptr_t)keys;
     xbuf = (float*)((base + 15) & ~(uintptr_t)15);
   }
-  const int64_t xb_rows = xbuf != nullptr && pc > 0 ? (int64_t)xlds / pc - 2 : 0;
-  const float* __restrict__ xi = x != nullptr ? x + i * p_in : nullptr;
+  const int xb_rows = xbuf != nullptr && pc > 0 ? xlds / pc - 3 : 0;
+  const bool xst = xb_rows >= 1;
+  int* xcol = xst ? (int*)(xbuf + 2 * pc) : nullptr;
+  const float* __restrict__ xi = x != nullptr ? x + (int64_t)i * p_in : nullptr;
+
+  // Quad q (samples 4q..4q+3): keys and class codes
+  auto load_quad = [&](int q, uint32_t (&kv)[4], uint32_t& lb) {
+    if (STAGE) {
+      const uint4 v = ((const uint4*)keys)[q];
+      kv[0] = v.x, kv[1] = v.y, kv[2] = v.z, kv[3] = v.w;
+      lb = ((const uint32_t*)labs)[q];
+    } else {
+      const float4 v = ((const float4*)rowk)[q];
+      kv[0] = __float_as_uint(v.x), kv[1] = __float_as_uint(v.y);
+      kv[2] = __float_as_uint(v.z), kv[3] = __float_as_uint(v.w);
+      lb = ((const uint32_t*)lab8)[q];
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if (4 * q + e >= n || 4 * q + e == i) kv[e] = kNone;
+    }
+  };
+  // Order-free sweep over the row, two quads per thread in flight: the
+  // per-class value arr[c] of every sample is loaded before any test (the
+  // sweeps are latency- and issue-bound: no per-sample branches or waits),
+  // then fn(j, c, key, arr[c]).
+  auto sweep = [&](const auto* arr, auto&& fn) {
+    for (int q0 = tid; q0 < nq; q0 += 2 * nt) {
+      const int q1 = q0 + nt < nq ? q0 + nt : nq - 1;
+      uint32_t kv[2][4], lb[2];
+      load_quad(q0, kv[0], lb[0]);
+      load_quad(q1, kv[1], lb[1]);
+      int cv[2][4];
+      auto av = arr[0];
+      decltype(av) pv[2][4];
+#pragma unroll
+      for (int h = 0; h < 2; h++)
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          cv[h][e] = (int)((lb[h] >> (8 * e)) & 0xFFu);
+          pv[h][e] = arr[cv[h][e]];
+        }
+#pragma unroll
+      for (int e = 0; e < 4; e++) fn(4 * q0 + e, cv[0][e], kv[0][e], pv[0][e]);
+      if (q0 + nt < nq) {
+#pragma unroll
+        for (int e = 0; e < 4; e++) fn(4 * q1 + e, cv[1][e], kv[1][e], pv[1][e]);
+      }
+    }
+  };
+
   // The reference's float32 key of pair (i, jj), wave-wide (every lane gets
   // it): k_exact_pairs<float>'s sum term by term in its order (lane l sums
   // columns l, l+64, ... in f64, then the discrete mismatches, then the
   // xor-shuffle tree); the unroll only batches the loads.
-  auto exact_key = [&](int64_t jj, int ln) -> double {
-    const float* __restrict__ xj = x + jj * p_in;
+  auto exact_key = [&](int jj) -> double {
+    const float* __restrict__ xj = x + (int64_t)jj * p_in;
     double acc = 0.0;
-    {
-      constexpr int kUe = 8;
-      for (int64_t c0 = ln; c0 < pc; c0 += 64 * kUe) {
-        int64_t col[kUe];
-        float av[kUe], bv[kUe], sv[kUe];
+    constexpr int kUe = 8;
+    for (int c0 = lane; c0 < pc; c0 += 64 * kUe) {
+      int64_t col[kUe];
+      float av[kUe], bv[kUe], sv[kUe];
 #pragma unroll
-        for (int u = 0; u < kUe; u++) {
-          col[u] = c0 + 64 * u < pc ? src_col[c0 + 64 * u] : -1;
-          sv[u] = c0 + 64 * u < pc ? (float)scl[c0 + 64 * u] : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < kUe; u++) {
-          av[u] = col[u] >= 0 ? xi[col[u]] : 0.0f;
-          bv[u] = col[u] >= 0 ? xj[col[u]] : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < kUe; u++)
-          if (col[u] >= 0) acc += (double)(__builtin_fabsf(av[u] - bv[u]) * sv[u]);
+      for (int u = 0; u < kUe; u++) {
+        const int c = c0 + 64 * u < pc ? c0 + 64 * u : pc - 1;
+        col[u] = src_col[c];
+        sv[u] = (float)scl[c];
       }
+#pragma unroll
+      for (int u = 0; u < kUe; u++) {
+        av[u] = xi[col[u]];
+        bv[u] = xj[col[u]];
+      }
+#pragma unroll
+      for (int u = 0; u < kUe; u++)
+        if (c0 + 64 * u < pc) acc += (double)(__builtin_fabsf(av[u] - bv[u]) * sv[u]);
     }
-    for (int64_t c = PC + ln; c < PC + pd; c += 64) {
+    for (int c = PC + lane; c < PC + pd; c += 64) {
       const int64_t cl = src_col[c];
       acc += (xi[cl] != xj[cl]) ? 1.0 : 0.0;
     }
@@ -2036,306 +2075,340 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
     return acc;
   };
   // stores pair (i, jj)'s exact key into the row (LDS or HBM); its bits
-  auto store_key = [&](int64_t jj, double acc) -> uint32_t {
+  auto store_key = [&](int jj, double acc) -> uint32_t {
     const uint32_t v = __float_as_uint((float)acc);  // acc >= 0: +0 at worst
     if (STAGE) keys[jj] = v;
-    else if (KF) const_cast<float*>(rowk)[jj] = (float)acc;
-    else const_cast<double*>(row)[jj] = -(double)(float)acc;
+    else rowk[jj] = (float)acc;
     return v;
   };
-  // Key range of the row: bits above the highest bit in which two keys
-  // differ are common to all of them, so the radix passes start below it
-  // (a row's distances share their float exponent or nearly: starting at
-  // bit 31 would pile every key into one or two bins of the first pass).
-  __shared__ uint32_t red_or[16], red_and[16];
+
+  // 1. The row.  Key range: bits above the highest bit in which two keys
+  // differ are common to all of them, so the radix passes start below it (a
+  // row's distances share their float exponent or nearly).  The exact-key
+  // buffer's fixed rows (x_i, scales, columns) load under the row's read:
+  // column indices first, the keys, then x_i at those columns.
   uint32_t kor = 0u, kand = 0xFFFFFFFFu;
-  // 8 independent loads in flight per thread (one workgroup per CU when
-  // staging: the row read is latency-bound otherwise)
-  constexpr int kU = 8;
   RF_T(0);
-  for (int64_t j0 = tid; j0 < n; j0 += (int64_t)kU * nt) {
-    uint32_t rv[kU];  // the raw key (KF) ...
-    double dv[kU];    // ... or the distance it is formed from
-    int32_t lv[kU];
+  if (STAGE) {
+    // one round trip: 8 quads per thread cover n <= 32768 (STAGE's range)
+    constexpr int kQ = 8;
+    int scol[2] = {0, 0};
+    float ssc[2] = {0.0f, 0.0f}, sxi[2] = {0.0f, 0.0f};
+    if (xst) {
 #pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const int64_t j = j0 + (int64_t)u * nt;
-      if (KF) rv[u] = j < n ? __float_as_uint(rowk[j]) : 0u;
-      else dv[u] = j < n ? row[j] : 0.0;
-      lv[u] = (STAGE && j < n) ? lab[j] : 0;
+      for (int s = 0; s < 2; s++) {
+        const int c = tid + s * nt < pc ? tid + s * nt : pc - 1;
+        scol[s] = (int)src_col[c];
+        ssc[s] = (float)scl[c];
+      }
+    }
+    uint4 kq[kQ];
+    uint32_t lq[kQ];
+#pragma unroll
+    for (int u = 0; u < kQ; u++) {
+      const int q = tid + u * nt < nq ? tid + u * nt : nq - 1;
+      kq[u] = ((const uint4*)rowk)[q];
+      lq[u] = ((const uint32_t*)lab8)[q];
+    }
+    if (xst) {
+#pragma unroll
+      for (int s = 0; s < 2; s++) sxi[s] = xi[scol[s]];
     }
 #pragma unroll
-    for (int u = 0; u < kU; u++) {
-      const int64_t j = j0 + (int64_t)u * nt;
-      if (j >= n) continue;
-      const uint32_t kv = KF ? rv[u] : rf_key(dv[u], inv_sc);
-      if (STAGE) {
-        keys[j] = kv;
-        labs[j] = (uint8_t)lv[u];
+    for (int u = 0; u < kQ; u++) {
+      const int q = tid + u * nt;
+      if (q >= nq) continue;
+      uint32_t kv[4] = {kq[u].x, kq[u].y, kq[u].z, kq[u].w};
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int j = 4 * q + e;
+        if (j >= n || j == i) {
+          kv[e] = kNone;
+        } else {
+          kor |= kv[e];
+          kand &= kv[e];
+        }
       }
-      if (j != i) {
-        kor |= kv;
-        kand &= kv;
+      ((uint4*)keys)[q] = make_uint4(kv[0], kv[1], kv[2], kv[3]);
+      ((uint32_t*)labs)[q] = lq[u];
+    }
+    if (xst) {
+#pragma unroll
+      for (int s = 0; s < 2; s++) {
+        const int c = tid + s * nt;
+        if (c < pc) xbuf[c] = sxi[s], xbuf[pc + c] = ssc[s], xcol[c] = scol[s];
       }
+    }
+  } else {
+    for (int q = tid; q < nq; q += nt) {
+      uint32_t kv[4], lb;
+      load_quad(q, kv, lb);
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        if (kv[e] != kNone) kor |= kv[e], kand &= kv[e];
+    }
+  }
+  if (xst) {  // the columns past 2 per thread
+    for (int c = tid + (STAGE ? 2 * nt : 0); c < pc; c += nt) {
+      const int col = (int)src_col[c];
+      xbuf[c] = xi[col];
+      xbuf[pc + c] = (float)scl[c];
+      xcol[c] = col;
     }
   }
   for (int o = 32; o > 0; o >>= 1) {
     kor |= __shfl_xor(kor, o);
     kand &= __shfl_xor(kand, o);
   }
-  if ((tid & 63) == 0) {
-    red_or[tid >> 6] = kor;
-    red_and[tid >> 6] = kand;
-  }
+  if (lane == 0) red_or[wave] = kor, red_and[wave] = kand;
   __syncthreads();
-  kor = 0u;
-  kand = 0xFFFFFFFFu;
-  for (int w = 0; w < nwaves; w++) {
-    kor |= red_or[w];
-    kand &= red_and[w];
-  }
-  // x != null: the exact keys in one launch.  Round 0 selects on the
-  // quantised keys; every candidate whose key lies within the band of its
-  // class's k-th key then gets the reference's key, computed right here by
-  // one wave with k_exact_pairs' arithmetic, and round 1 selects again on
-  // the updated row (no pair list, no second read of the row).  kor / kand
-  // also take the exact keys in (a wider key range is still a valid one).
-  __shared__ uint32_t kor_s, kand_s;
-  __shared__ int n_ex, nflag;
-  __shared__ uint32_t lcnt[64];  // keys of a class below T outside the band
-  __shared__ uint32_t bcount[64];  // keys in the chosen bucket, per class
-  __shared__ uint8_t done[64];
-  __shared__ uint32_t gcnt[64];
-  __shared__ int any_big;
   RF_T(1);
-  if (tid == 0) kor_s = kor, kand_s = kand, n_ex = 0;
+  if (tid == 0) {
+    uint32_t o = 0u, a = 0xFFFFFFFFu;
+    for (int w = 0; w < nwaves; w++) o |= red_or[w], a &= red_and[w];
+    kor_s = o, kand_s = a, n_ex = 0;
+  }
+
+  // 2. Selection.  x != null: round 0 selects on the quantised keys, the
+  // candidates within the band of their class's k-th key get the reference's
+  // keys (3.), and the exact k-th keys follow from them; round 1 (a second
+  // selection over the row) only for rows with over fcap candidates.
   const int rounds = x != nullptr ? 2 : 1;
   for (int round = 0; round < rounds; round++) {
-  __syncthreads();
-  kor = kor_s;
-  kand = kand_s;
-  const uint32_t diff = kor & ~kand;  // bits that are not common
-  const int top = diff ? 31 - __builtin_clz(diff) : 0;
-  // Pass 1 takes the WB bits [lo1, top] right below the common prefix (a
-  // byte-aligned first digit would hold only the few varying exponent bits:
-  // ~20 of 256 bins used, LDS atomics serialising on them); 10-bit digits
-  // when the histograms fit (n_classes <= 8), else 8.
-  const int wb = n_classes <= 8 ? 10 : 8;
-  const int lo1 = top - (wb - 1) > 0 ? top - (wb - 1) : 0;
-  const uint32_t common = top >= 31 ? 0u : (kand & ~(0xFFFFFFFFu >> (31 - top)));
-  for (int c = tid; c < n_classes; c += nt) {
-    const int64_t members = class_count[c] - (c == li ? 1 : 0);
-    const int64_t kc = members < k ? members : k;
-    prefix[c] = common;
-    // need = rank (1-based) of the wanted key inside the current bucket;
-    // kc == members: take everything (T = 0xFFFFFFFF, nothing equal needed)
-    need[c] = (uint32_t)kc;
-    if (kc == members) prefix[c] = 0xFFFFFFFFu, need[c] = 0;
-  }
-  // One pass: histogram of the digit [lo, hi) of the keys whose bits >= hi
-  // match their class's prefix, then per class (one wave each) the bucket
-  // holding the need-th key, by a wave prefix sum over the bins.
-  // done[c]: class c's k-th key is final (the small-bucket gather below
-  // leaves need[c] as a rank among the keys EQUAL to it, which a further
-  // radix pass -- counting all keys under the prefix -- must not reuse)
-  for (int c = tid; c < n_classes; c += nt) done[c] = 0;
-  auto radix_pass = [&](int lo, int hi) {
-    const int nbins = 1 << (hi - lo);
-    const uint32_t dmask = (uint32_t)nbins - 1u;
-    for (int e = tid; e < n_classes * nbins; e += nt) hist[e] = 0;
     __syncthreads();
-    for (int64_t j = tid; j < n; j += nt) {
-      if (j == i) continue;
-      const int32_t c = lab_of(j);
-      if (need[c] == 0 || done[c]) continue;
-      const uint32_t key = key_of(j);
-      if (hi < 32 && (key >> hi) != (prefix[c] >> hi)) continue;
-      atomicAdd(&hist[c * nbins + ((key >> lo) & dmask)], 1u);
+    const uint32_t kor_r = kor_s, kand_r = kand_s;
+    const uint32_t diff = kor_r & ~kand_r;  // bits that are not common
+    const int top = diff ? 31 - __builtin_clz(diff) : 0;  // <= 30: keys are >= 0
+    // pass 1 takes the WB bits [lo1, top] right below the common prefix;
+    // 10-bit digits when the histograms fit (C <= 8), else 8
+    const int wb = C <= 8 ? 10 : 8;
+    const int lo1 = top - (wb - 1) > 0 ? top - (wb - 1) : 0;
+    const uint32_t common = top >= 31 ? 0u : (kand_r & ~(0xFFFFFFFFu >> (31 - top)));
+    for (int c = tid; c < C; c += nt) {
+      const int64_t members = class_count[c] - (c == li ? 1 : 0);
+      const int64_t kc = members < k ? members : k;
+      // need = rank (1-based) of the wanted key inside the current bucket;
+      // kc == members: take everything (T = kNone, nothing equal needed)
+      prefix[c] = kc == members ? kNone : common;
+      need[c] = kc == members ? 0u : (uint32_t)kc;
+      done[c] = 0;
     }
-    __syncthreads();
-    const int wv = tid >> 6, ln = tid & 63;
-    const int bpl = (nbins + 63) >> 6;  // bins per lane
-    for (int c = wv; c < n_classes; c += nwaves) {
-      const uint32_t nd = need[c];
-      if (nd == 0 || done[c]) continue;
-      const uint32_t* hc = hist + c * nbins;
-      const int b0 = ln * bpl;
-      uint32_t tot = 0u;
-      for (int q = 0; q < bpl; q++)
-        if (b0 + q < nbins) tot += hc[b0 + q];
-      uint32_t incl = tot;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o);
-        if (ln >= o) incl += t;
-      }
-      // the first lane whose inclusive sum reaches nd owns the bucket
-      const uint64_t m = __ballot(incl >= nd);
-      const int owner = (int)__builtin_ctzll(m);
-      if (ln == owner) {
-        uint32_t cum = incl - tot;
-        int b = b0;
-        for (; b < b0 + bpl - 1; b++) {
-          if (cum + hc[b] >= nd) break;
-          cum += hc[b];
+    // One pass: histogram of the digit [lo, hi) of the keys whose bits >= hi
+    // match their class's prefix, then per class (one wave each) the bucket
+    // holding the need-th key, by a wave prefix sum over the bins.  done[c]:
+    // class c's k-th key is final (the small-bucket gather leaves need[c] as
+    // a rank among the keys EQUAL to it, which a further pass must not reuse).
+    // pm[c]: the prefix to match, kNone for classes not in the pass.
+    auto radix_pass = [&](int lo, int hi) {
+      const int nbins = 1 << (hi - lo);
+      const uint32_t dmask = (uint32_t)nbins - 1u;
+      __syncthreads();
+      for (int e = tid; e < C * nbins; e += nt) hist[e] = 0;
+      for (int c = tid; c < C; c += nt) pm[c] = (need[c] != 0 && !done[c]) ? prefix[c] : kNone;
+      __syncthreads();
+      sweep(pm, [&](int, int c, uint32_t key, uint32_t P) {
+        if ((key >> hi) == (P >> hi)) atomicAdd(&hist[c * nbins + ((key >> lo) & dmask)], 1u);
+      });
+      __syncthreads();
+      const int bpl = (nbins + 63) >> 6;  // bins per lane
+      for (int c = wave; c < C; c += nwaves) {
+        const uint32_t nd = need[c];
+        if (nd == 0 || done[c]) continue;
+        const uint32_t* hc = hist + c * nbins;
+        const int b0 = lane * bpl;
+        // the lane's bins in registers (bpl <= 16), loaded together
+        uint32_t hv[16], tot = 0u;
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          const int b = b0 + q < nbins ? b0 + q : nbins - 1;
+          hv[q] = hc[b];
         }
-        prefix[c] |= (uint32_t)b << lo;
-        need[c] = nd - cum;
-        bcount[c] = hc[b];
+#pragma unroll
+        for (int q = 0; q < 16; q++) {
+          if (q >= bpl || b0 + q >= nbins) hv[q] = 0u;
+          tot += hv[q];
+        }
+        uint32_t incl = tot;
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t t = __shfl_up(incl, o);
+          if (lane >= o) incl += t;
+        }
+        // the first lane whose inclusive sum reaches nd owns the bucket
+        const uint64_t m = __ballot(incl >= nd);
+        const int owner = (int)__builtin_ctzll(m);
+        if (lane == owner) {
+          uint32_t cum = incl - tot, bsel = (uint32_t)b0, bc = 0u;
+          bool found = false;
+#pragma unroll
+          for (int q = 0; q < 16; q++) {
+            if (!found && q < bpl) {
+              if (q == bpl - 1 || cum + hv[q] >= nd) {
+                found = true;
+                bsel = (uint32_t)(b0 + q);
+                bc = hv[q];
+              } else {
+                cum += hv[q];
+              }
+            }
+          }
+          prefix[c] |= bsel << lo;
+          need[c] = nd - cum;
+          bcount[c] = bc;
+        }
       }
-    }
-    __syncthreads();
-  };
-  __syncthreads();
-  radix_pass(lo1, top + 1);
-  RF_T(2);
-  if (lo1 > 0) {
-    // Small buckets (<= 64 keys: the common case, the k nearest sit in the
-    // sparse low tail) finish in one gather: the bucket's keys go to a list
-    // (in the histogram space, free now) and the need-th smallest is found by
-    // ranking.  Classes with bigger buckets (ties, discrete data) continue
-    // with 8-bit passes below lo1.
-    uint32_t* list = hist;  // [class][64]
-    if (tid == 0) any_big = 0;
-    for (int c = tid; c < n_classes; c += nt) {
-      gcnt[c] = 0u;
-      if (need[c] != 0 && bcount[c] > 64u) any_big = 1;
-    }
-    __syncthreads();
-    for (int64_t j = tid; j < n; j += nt) {
-      if (j == i) continue;
-      const int32_t c = lab_of(j);
-      if (need[c] == 0 || bcount[c] > 64u) continue;
-      const uint32_t key = key_of(j);
-      if ((key >> lo1) != (prefix[c] >> lo1)) continue;
-      const uint32_t slot = atomicAdd(&gcnt[c], 1u);
-      list[c * 64 + slot] = key;
-    }
-    __syncthreads();
-    const int wv = tid >> 6, ln = tid & 63;
-    for (int c = wv; c < n_classes; c += nwaves) {
-      const uint32_t nd = need[c], m = bcount[c];
-      if (nd == 0 || m > 64u) continue;
-      const uint32_t v = ln < (int)m ? list[c * 64 + ln] : 0xFFFFFFFFu;
-      uint32_t nlt = 0u, nle = 0u;
-      for (uint32_t q = 0; q < m; q++) {
-        const uint32_t w = list[c * 64 + q];
-        nlt += w < v;
-        nle += w <= v;
+      __syncthreads();
+    };
+    radix_pass(lo1, top + 1);
+    RF_T(2);
+    if (lo1 > 0) {
+      // Small buckets (<= 64 keys: the common case, the k nearest sit in the
+      // sparse low tail) finish in one gather: the bucket's keys go to a list
+      // (in the histogram space, free now) and the need-th smallest is found
+      // by ranking.  Classes with bigger buckets (ties, discrete data)
+      // continue with 8-bit passes below lo1.
+      uint32_t* list = hist;  // [class][64]
+      if (tid == 0) any_big = 0;
+      __syncthreads();
+      for (int c = tid; c < C; c += nt) {
+        gcnt[c] = 0u;
+        if (need[c] != 0 && bcount[c] > 64u) any_big = 1;
+        pm[c] = (need[c] != 0 && bcount[c] <= 64u) ? prefix[c] : kNone;
       }
-      // the need-th smallest: nlt < nd <= nle (ties: one owner per value,
-      // any lane holding it writes the same result)
-      const bool own = ln < (int)m && nlt < nd && nd <= nle;
-      const uint64_t mo = __ballot(own);
-      if (mo != 0ull && ln == (int)__builtin_ctzll(mo)) {
-        prefix[c] = v;
-        need[c] = nd - nlt;
-        done[c] = 1;
+      __syncthreads();
+      sweep(pm, [&](int, int c, uint32_t key, uint32_t P) {
+        if ((key >> lo1) == (P >> lo1)) {
+          // (a class outside the gather can take the kNone keys: at most 4)
+          const uint32_t slot = atomicAdd(&gcnt[c], 1u);
+          if (slot < 64u) list[c * 64 + slot] = key;
+        }
+      });
+      __syncthreads();
+      for (int c = wave; c < C; c += nwaves) {
+        const uint32_t nd = need[c], m = bcount[c];
+        if (nd == 0 || m > 64u) continue;
+        const uint32_t v = lane < (int)m ? list[c * 64 + lane] : kNone;
+        uint32_t nlt = 0u, nle = 0u;
+        for (uint32_t q = 0; q < m; q++) {
+          const uint32_t w = list[c * 64 + q];
+          nlt += w < v;
+          nle += w <= v;
+        }
+        // the need-th smallest: nlt < nd <= nle (ties: one owner per value)
+        const bool own = lane < (int)m && nlt < nd && nd <= nle;
+        const uint64_t mo = __ballot(own);
+        if (mo != 0ull && lane == (int)__builtin_ctzll(mo)) {
+          prefix[c] = v;
+          need[c] = nd - nlt;
+          done[c] = 1;
+        }
       }
+      __syncthreads();
+      if (any_big)
+        for (int hi = lo1; hi > 0; hi -= 8) radix_pass(hi - 8 > 0 ? hi - 8 : 0, hi);
     }
-    __syncthreads();
-    if (any_big)
-      for (int hi = lo1; hi > 0; hi -= 8) radix_pass(hi - 8 > 0 ? hi - 8 : 0, hi);
-  }
-  RF_T(3);
-  if (round + 1 < rounds) {
-    // Candidates within the band of their class's k-th key T go to a list
-    // (j | class << 26); the other keys of a class below T are counted
-    // (lcnt: all of them stay below the exact T).  The listed keys get the
+    RF_T(3);
+    if (round + 1 >= rounds) break;
+
+    // 3. Exact keys.  The band |key - T| <= band_abs + band_rel * T (in f64)
+    // is, for float keys, an interval of key bits [klo, klo + kn): found per
+    // class from the f64 bounds rounded to float, then stepped to the exact
+    // edges (a step or two), so the sweep tests two integers.  Candidates go
+    // to a list (j | class << 26); the keys of a class below the band are
+    // counted (lcnt: they stay below the exact T).  The listed keys get the
     // reference's keys, spread over the waves, and the exact k-th key of
-    // class c is the (kc - lcnt[c])-th smallest listed key of c: no second
-    // pass over the row.  A list over kFCap entries (ties, discrete-heavy
-    // rows) takes the general route: exact keys in chunk order, then a
-    // second selection over the whole row.
+    // class c is the (kc - lcnt[c])-th smallest listed key of c.  More than
+    // fcap candidates (ties, discrete-heavy rows): the general route, exact
+    // keys in chunk order and a second selection over the row.
     constexpr int kFCap = 256;
     uint32_t* fl = hist;  // [kFCap] entries, [kFCap] exact keys
-    const int wave_e = tid >> 6, lane_e = tid & 63;
-    const int64_t chunk_e = (n + nwaves - 1) / nwaves;
-    const int64_t jb_e = (int64_t)wave_e * chunk_e;
-    const int64_t je_e = jb_e + chunk_e < n ? jb_e + chunk_e : n;
-    auto flagged = [&](int64_t j, int32_t c, uint32_t kv) {
-      const double T = (double)__uint_as_float(prefix[c]);
-      return fabs((double)__uint_as_float(kv) - T) <= band_abs + band_rel * T;
-    };
-    for (int c = tid; c < n_classes; c += nt) lcnt[c] = 0u;
+    for (int c = tid; c < C; c += nt) {
+      lcnt[c] = 0u;
+      uint2 kb = make_uint2(0u, 0u);
+      if (need[c] != 0) {
+        const uint32_t P = prefix[c];
+        const double T = (double)__uint_as_float(P);
+        const double B = band_abs + band_rel * T;
+        auto in_band = [&](uint32_t f) { return fabs((double)__uint_as_float(f) - T) <= B; };
+        const double lo_d = T - B, hi_d = T + B;
+        uint32_t a = lo_d <= 0.0 ? 0u : __float_as_uint((float)lo_d);
+        if (a > P) a = P;
+        while (a > 0u && in_band(a - 1u)) a--;
+        while (!in_band(a)) a++;
+        uint32_t b = __float_as_uint((float)hi_d);
+        if (b < P) b = P;
+        if (b > 0x7F7FFFFFu) b = 0x7F7FFFFFu;
+        while (b < 0x7F7FFFFFu && in_band(b + 1u)) b++;
+        while (!in_band(b)) b--;
+        kb = make_uint2(a, b - a + 1u);
+      }
+      kband[c] = kb;
+    }
     if (tid == 0) nflag = 0;
     __syncthreads();
-    for (int64_t j = jb_e + lane_e; j < je_e; j += 64) {
-      if (j == i) continue;
-      const int32_t c = lab_of(j);
-      if (need[c] == 0) continue;
-      const uint32_t kv = key_of(j);
-      if (flagged(j, c, kv)) {
+    sweep(kband, [&](int j, int c, uint32_t key, uint2 kb) {
+      if (key - kb.x < kb.y) {
         const int slot = atomicAdd(&nflag, 1);
         if (slot < kFCap) fl[slot] = (uint32_t)j | ((uint32_t)c << 26);
-      } else if (kv < prefix[c]) {
+      } else if (key < kb.x) {
         atomicAdd(&lcnt[c], 1u);
       }
-    }
+    });
     __syncthreads();
     RF_T(4);
     const int F = nflag;
     if (F == 0) break;  // nothing near any k-th key: round 0's keys are final
-    if (F <= (cap < kFCap ? (int)cap : kFCap)) {  // cap: FS_RF_FCAP (tests)
-      if (xb_rows >= 1) {
-        // batches of xb_rows candidates: xbuf = [x_i | scales | rows...]
-        for (int e0 = 0; e0 < F; e0 += (int)xb_rows) {
-          const int nb = F - e0 < (int)xb_rows ? F - e0 : (int)xb_rows;
-          const int pci = (int)pc, tot = (nb + 2) * pci;  // < xlds
+    if (F <= (fcap < kFCap ? fcap : kFCap)) {
+      if (xst) {
+        // batches of xb_rows candidates gathered at the staged columns
+        for (int e0 = 0; e0 < F; e0 += xb_rows) {
+          const int nb = F - e0 < xb_rows ? F - e0 : xb_rows;
+          const int tot = nb * pc;
           for (int t0 = tid; t0 < tot; t0 += 4 * nt) {
             float v[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-              const int t = t0 + u * nt;
-              v[u] = 0.0f;
-              if (t < tot) {
-                const int q = t / pci, c = t - q * pci;
-                if (q == 1) {
-                  v[u] = (float)scl[c];
-                } else {
-                  const int64_t jr = q == 0 ? i : (int64_t)(fl[e0 + q - 2] & ((1u << 26) - 1u));
-                  v[u] = x[jr * p_in + src_col[c]];
-                }
-              }
+              const int t = t0 + u * nt < tot ? t0 + u * nt : tot - 1;
+              const int q = t / pc, c = t - q * pc;
+              const int jr = (int)(fl[e0 + q] & ((1u << 26) - 1u));
+              v[u] = x[(int64_t)jr * p_in + xcol[c]];
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-              const int t = t0 + u * nt;
-              if (t < tot) xbuf[t] = v[u];
-            }
+            for (int u = 0; u < 4; u++)
+              if (t0 + u * nt < tot) xbuf[3 * pc + t0 + u * nt] = v[u];
           }
           __syncthreads();
-          for (int q = wave_e; q < nb; q += nwaves) {
+          for (int q = wave; q < nb; q += nwaves) {
             const int e = e0 + q;
-            const int64_t jj = (int64_t)(fl[e] & ((1u << 26) - 1u));
-            const float* xr = xbuf + (int64_t)(q + 2) * pc;
+            const int jj = (int)(fl[e] & ((1u << 26) - 1u));
+            const float* xr = xbuf + (3 + q) * pc;
             double acc = 0.0;
-            for (int64_t c = lane_e; c < pc; c += 64)
+            for (int c = lane; c < pc; c += 64)
               acc += (double)(__builtin_fabsf(xbuf[c] - xr[c]) * xbuf[pc + c]);
-            for (int64_t c = PC + lane_e; c < PC + pd; c += 64) {
+            for (int c = PC + lane; c < PC + pd; c += 64) {
               const int64_t cl = src_col[c];
-              acc += (xi[cl] != x[jj * p_in + cl]) ? 1.0 : 0.0;
+              acc += (xi[cl] != x[(int64_t)jj * p_in + cl]) ? 1.0 : 0.0;
             }
             for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-            if (lane_e == 0) fl[kFCap + e] = store_key(jj, acc);
+            if (lane == 0) fl[kFCap + e] = store_key(jj, acc);
           }
           __syncthreads();
         }
       } else {
-        for (int e = wave_e; e < F; e += nwaves) {
-          const int64_t jj = (int64_t)(fl[e] & ((1u << 26) - 1u));
-          const double acc = exact_key(jj, lane_e);
-          if (lane_e == 0) fl[kFCap + e] = store_key(jj, acc);
+        for (int e = wave; e < F; e += nwaves) {
+          const int jj = (int)(fl[e] & ((1u << 26) - 1u));
+          const double acc = exact_key(jj);
+          if (lane == 0) fl[kFCap + e] = store_key(jj, acc);
         }
         __syncthreads();
       }
       RF_T(5);
-      for (int c = wave_e; c < n_classes; c += nwaves) {
+      for (int c = wave; c < C; c += nwaves) {
         if (need[c] == 0) continue;
         const int64_t members = class_count[c] - (c == li ? 1 : 0);
         const uint32_t kc = (uint32_t)(members < k ? members : k);
         const uint32_t r = kc - lcnt[c];  // 1-based rank among c's listed keys
         for (int e0 = 0; e0 < F; e0 += 64) {
-          const int e = e0 + lane_e;
+          const int e = e0 + lane;
           bool own = false;
           uint32_t v = 0u, nlt = 0u, nle = 0u;
           if (e < F && (int)(fl[e] >> 26) == c) {
@@ -2350,7 +2423,7 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
           }
           const uint64_t mo = __ballot(own);
           if (mo != 0ull) {
-            if (lane_e == (int)__builtin_ctzll(mo)) {
+            if (lane == (int)__builtin_ctzll(mo)) {
               prefix[c] = v;
               need[c] = r - nlt;
             }
@@ -2359,25 +2432,29 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
         }
       }
       if (tid == 0) n_ex = F;
-      RF_T(6);
       __syncthreads();
+      RF_T(6);
       break;
     }
-    // general route: every flagged sample of a wave's chunk, in order
+    // general route: every candidate of a wave's chunk, in ballot order
+    const int chunk_e = (n + nwaves - 1) / nwaves;
+    const int jb_e = wave * chunk_e, je_e = jb_e + chunk_e < n ? jb_e + chunk_e : n;
     int n_local = 0;
-    for (int64_t j0 = jb_e; j0 < je_e; j0 += 64) {
-      const int64_t j = j0 + lane_e;
+    for (int j0 = jb_e; j0 < je_e; j0 += 64) {
+      const int j = j0 + lane;
       bool flag = false;
       if (j < je_e && j != i) {
-        const int32_t c = lab_of(j);
-        if (need[c] != 0) flag = flagged(j, c, key_of(j));
+        const int c = STAGE ? (int)labs[j] : (int)lab8[j];
+        const uint32_t key = STAGE ? keys[j] : __float_as_uint(rowk[j]);
+        const uint2 kb = kband[c];
+        flag = key - kb.x < kb.y;
       }
       uint64_t m = __ballot(flag);
       while (m != 0ull) {
-        const int64_t jj = j0 + __builtin_ctzll(m);
+        const int jj = j0 + __builtin_ctzll(m);
         m &= m - 1ull;
-        const double acc = exact_key(jj, lane_e);
-        if (lane_e == 0) {
+        const double acc = exact_key(jj);
+        if (lane == 0) {
           const uint32_t v = store_key(jj, acc);
           atomicOr(&kor_s, v);
           atomicAnd(&kand_s, v);
@@ -2385,135 +2462,152 @@ __global__ __launch_bounds__(1024) void k_rf_select(const double* __restrict__ D
         n_local++;
       }
     }
-    if (lane_e == 0 && n_local != 0) atomicAdd(&n_ex, n_local);
+    if (lane == 0 && n_local != 0) atomicAdd(&n_ex, n_local);
     __threadfence_block();
-    __syncthreads();
-  }
   }  // rounds
-  if (tid == 0 && count != nullptr && n_ex != 0) atomicAdd(count, (unsigned long long)n_ex);
-  for (int c = tid; c < n_classes; c += nt) {
-    tkey[i * n_classes + c] = prefix[c];
-    tneed[i * n_classes + c] = (int32_t)need[c];
-  }
-  // Ordered collection over all waves: wave w takes the contiguous chunk
-  // [j_w, j_w+1) of the row.  Pass 1 counts, per class, the keys below the
-  // k-th key T and the keys equal to it in the chunk; a scan over the waves
-  // turns them into each wave's output offset and the number of equal keys
-  // before its chunk (only the first need[c] equal keys in j order are
-  // taken, as the reference's stable order among ties at this stage).
-  // Pass 2 writes.  (One wave per class swept the whole row before: with
-  // two classes, 2 of 16 waves did all the work.)
-  // per-wave counts and offsets [wave][class] reuse the histogram space
-  // (4 x 16 x C <= 256 x C words)
-  uint32_t* cnt_lt = hist;
-  uint32_t* cnt_eq = hist + 16 * n_classes;
-  uint32_t* off_lt = hist + 32 * n_classes;
-  uint32_t* off_eq = hist + 48 * n_classes;
-  const int wave = tid >> 6, lane = tid & 63;
-  const int64_t chunk = (n + nwaves - 1) / nwaves;
-  const int64_t jb = (int64_t)wave * chunk, je = jb + chunk < n ? jb + chunk : n;
-  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  for (int c = lane; c < n_classes; c += 64) cnt_lt[wave * n_classes + c] = cnt_eq[wave * n_classes + c] = 0u;
   __syncthreads();
-  // Keys are classified 4 x 64 at a time (the loads of the four go out
-  // together: the chain label -> T[label] -> compare is LDS-latency bound).
+  if (tid == 0 && count != nullptr && n_ex != 0) atomicAdd(count, (unsigned long long)n_ex);
+  for (int c = tid; c < C; c += nt) {
+    tkey[(int64_t)i * C + c] = prefix[c];
+    tneed[(int64_t)i * C + c] = (int32_t)need[c];
+  }
+
+  // 4. Ordered collection over all waves: wave w takes the contiguous chunk
+  // [j_w, j_w+1) of the row.  Pass 1 counts, per class, the keys below the
+  // k-th key T and the keys equal to it in the chunk, and lists them (j
+  // order, by ballot compaction) in the wave's slice of the histogram space;
+  // a scan over the waves turns the counts into each wave's output offsets
+  // and the number of equal keys before its chunk (only the first need[c]
+  // equal keys in j order are taken, as the reference's stable order among
+  // ties at this stage).  Pass 2 writes from the lists, or sweeps the chunk
+  // again when a list overflowed (ties).  Groups of 4 x 64 keys with no key
+  // <= T of its class (nearly all: k per class in a row of n) are skipped
+  // on one ballot.  Per-wave counters [wave][class] and the lists reuse the
+  // histogram space.
+  uint32_t* cnt_lt = hist;
+  uint32_t* cnt_eq = hist + 16 * C;
+  uint32_t* off_lt = hist + 32 * C;
+  uint32_t* off_eq = hist + 48 * C;
+  const int lcap = (C * nbins1 - 64 * C) / 16;  // list entries per wave (>= 60)
+  uint32_t* wl = hist + 64 * C + wave * lcap;
+  __shared__ int ovf;
+  const int chunk = (n + nwaves - 1) / nwaves;
+  const int jb = wave * chunk, je = jb + chunk < n ? jb + chunk : n;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int c = lane; c < C; c += 64) cnt_lt[wave * C + c] = cnt_eq[wave * C + c] = 0u;
+  if (tid == 0) ovf = 0;
+  __syncthreads();
   constexpr int kCU = 4;
-  auto classify = [&](int64_t j0, int32_t (&cv)[kCU], bool (&lt)[kCU], bool (&eq)[kCU]) {
-    uint32_t kv[kCU];
+  auto classify = [&](int j0, int (&cv)[kCU], bool (&lt)[kCU], bool (&eq)[kCU]) -> bool {
+    uint32_t kv[kCU], tv[kCU];
 #pragma unroll
     for (int u = 0; u < kCU; u++) {
-      const int64_t j = j0 + 64 * u + lane;
-      const bool ok = j < je && j != i;
-      cv[u] = ok ? lab_of(j) : -1;
-      kv[u] = ok ? key_of(j) : 0u;
+      const int j = j0 + 64 * u + lane;
+      const int jc = j < je ? j : je - 1;  // unconditional loads
+      cv[u] = STAGE ? (int)labs[jc] : (int)lab8[jc];
+      kv[u] = STAGE ? keys[jc] : __float_as_uint(rowk[jc]);
     }
 #pragma unroll
+    for (int u = 0; u < kCU; u++) tv[u] = prefix[cv[u]];
+    bool any = false;
+#pragma unroll
     for (int u = 0; u < kCU; u++) {
-      const uint32_t T = cv[u] >= 0 ? prefix[cv[u]] : 0u;
-      lt[u] = cv[u] >= 0 && kv[u] < T;
-      eq[u] = cv[u] >= 0 && kv[u] == T;
+      const int j = j0 + 64 * u + lane;
+      const bool ok = j < je && j != i;
+      lt[u] = ok && kv[u] < tv[u];
+      eq[u] = ok && kv[u] == tv[u];
+      any |= lt[u] | eq[u];
+    }
+    return __ballot(any) != 0ull;
+  };
+  // the classes present among the wave's flagged lanes (bit c), wave-wide
+  auto classes_of = [&](bool f, int c) {
+    uint64_t cm = f ? (1ull << c) : 0ull;
+    for (int o = 32; o > 0; o >>= 1) cm |= __shfl_xor(cm, o);
+    return cm;
+  };
+  // pass-1 counts of one batch of 64 keys (lane 0 keeps the wave's counters)
+  auto tally = [&](bool l, bool e, int c) {
+    for (uint64_t cm = classes_of(l || e, c); cm != 0ull; cm &= cm - 1ull) {
+      const int cc = __builtin_ctzll(cm);
+      const uint32_t nl = (uint32_t)__popcll(__ballot(l && c == cc));
+      const uint32_t ne = (uint32_t)__popcll(__ballot(e && c == cc));
+      if (lane == 0) cnt_lt[wave * C + cc] += nl, cnt_eq[wave * C + cc] += ne;
     }
   };
-  const bool few = n_classes <= 8;  // lane c keeps class c's counts (ballots)
-  uint32_t my_lt = 0u, my_eq = 0u;
-  for (int64_t j0 = jb; j0 < je; j0 += 64 * kCU) {
-    int32_t cv[kCU];
-    bool lt[kCU], eq[kCU];
-    classify(j0, cv, lt, eq);
-#pragma unroll
-    for (int u = 0; u < kCU; u++) {
-      if (few) {
-        for (int cc = 0; cc < n_classes; cc++) {
-          const uint32_t nl = (uint32_t)__popcll(__ballot(lt[u] && cv[u] == cc));
-          const uint32_t ne = (uint32_t)__popcll(__ballot(eq[u] && cv[u] == cc));
-          if (lane == cc) my_lt += nl, my_eq += ne;
-        }
-      } else {  // many classes: LDS atomics
-        if (lt[u]) atomicAdd(&cnt_lt[wave * n_classes + cv[u]], 1u);
-        else if (eq[u]) atomicAdd(&cnt_eq[wave * n_classes + cv[u]], 1u);
+  // pass-2 writes of one batch of 64 keys in j order (running slots in
+  // off_lt / off_eq, lane 0 advances them)
+  auto emit = [&](bool l, bool e, int c, int j) {
+    for (uint64_t cm = classes_of(l || e, c); cm != 0ull; cm &= cm - 1ull) {
+      const int cc = __builtin_ctzll(cm);
+      const bool lc = l && c == cc, ec = e && c == cc;
+      const uint64_t mlt = __ballot(lc), meq = __ballot(ec);
+      const uint32_t rl = off_lt[wave * C + cc], re = off_eq[wave * C + cc];
+      int32_t* out = nbr + ((int64_t)i * C + cc) * k;
+      if (lc) out[rl + __popcll(mlt & below)] = j;
+      if (ec) {
+        const uint32_t r = re + (uint32_t)__popcll(meq & below);
+        if (r < need[cc]) out[cnt_lt[cc] + r] = j;
+      }
+      if (lane == 0) {
+        off_lt[wave * C + cc] = rl + (uint32_t)__popcll(mlt);
+        off_eq[wave * C + cc] = re + (uint32_t)__popcll(meq);
       }
     }
+  };
+  int nlist = 0;  // wave-uniform
+  for (int j0 = jb; j0 < je; j0 += 64 * kCU) {
+    int cv[kCU];
+    bool lt[kCU], eq[kCU];
+    if (!classify(j0, cv, lt, eq)) continue;
+#pragma unroll
+    for (int u = 0; u < kCU; u++) {
+      const bool h = lt[u] || eq[u];
+      const uint64_t mh = __ballot(h);
+      if (mh == 0ull) continue;
+      tally(lt[u], eq[u], cv[u]);
+      const int slot = nlist + (int)__popcll(mh & below);
+      if (h && slot < lcap)
+        wl[slot] = (uint32_t)(j0 + 64 * u + lane) | (eq[u] ? 1u << 25 : 0u) |
+                   ((uint32_t)cv[u] << 26);
+      nlist += (int)__popcll(mh);
+    }
   }
-  if (few && lane < n_classes) {
-    cnt_lt[wave * n_classes + lane] = my_lt;
-    cnt_eq[wave * n_classes + lane] = my_eq;
-  }
+  if (lane == 0 && nlist > lcap) ovf = 1;
   __syncthreads();
   // exclusive scans over the waves, per class (one thread per class)
-  for (int c = tid; c < n_classes; c += nt) {
+  for (int c = tid; c < C; c += nt) {
     uint32_t a = 0u, b = 0u;
     for (int w = 0; w < nwaves; w++) {
-      off_lt[w * n_classes + c] = a;
-      off_eq[w * n_classes + c] = b;
-      a += cnt_lt[w * n_classes + c];
-      b += cnt_eq[w * n_classes + c];
+      const uint32_t ca = cnt_lt[w * C + c], cb = cnt_eq[w * C + c];
+      off_lt[w * C + c] = a;
+      off_eq[w * C + c] = b;
+      a += ca;
+      b += cb;
     }
     // every key below T is taken; the first need[c] equal keys follow them
     const uint32_t take_eq = b < need[c] ? b : need[c];
-    nfound[i * n_classes + c] = (int32_t)(a + take_eq);
-    teq[i * n_classes + c] = (int32_t)b;
+    nfound[(int64_t)i * C + c] = (int32_t)(a + take_eq);
+    teq[(int64_t)i * C + c] = (int32_t)b;
     cnt_lt[c] = a;  // total below T (base of the equal keys' slots)
   }
   __syncthreads();
   // pass 2: write.  Keys below T keep j order among themselves; equal keys
-  // (in j order) follow.  A wave walks its chunk in j order, so a per-wave
-  // running count per class gives each key its slot: lane c holds class c's
-  // (one sweep for all classes), or one sweep per class when there are many.
-  uint32_t run_lt = 0u, run_eq = 0u;
-  if (few && lane < n_classes) {
-    run_lt = off_lt[wave * n_classes + lane];
-    run_eq = off_eq[wave * n_classes + lane];
-  }
-  for (int c1 = 0; c1 < (few ? 1 : n_classes); c1++) {
-    if (!few) {
-      run_lt = off_lt[wave * n_classes + c1];
-      run_eq = off_eq[wave * n_classes + c1];
+  // (in j order) follow.
+  if (!ovf) {
+    for (int e0 = 0; e0 < nlist; e0 += 64) {
+      const int e = e0 + lane;
+      const uint32_t ent = e < nlist ? wl[e] : 0u;
+      const bool iseq = (ent >> 25) & 1u;
+      emit(e < nlist && !iseq, e < nlist && iseq, (int)(ent >> 26), (int)(ent & ((1u << 25) - 1u)));
     }
-    for (int64_t j0 = jb; j0 < je; j0 += 64 * kCU) {
-      int32_t cv[kCU];
+  } else {
+    for (int j0 = jb; j0 < je; j0 += 64 * kCU) {
+      int cv[kCU];
       bool lt[kCU], eq[kCU];
-      classify(j0, cv, lt, eq);
+      if (!classify(j0, cv, lt, eq)) continue;
 #pragma unroll
-      for (int u = 0; u < kCU; u++) {
-        const int64_t j = j0 + 64 * u + lane;
-        for (int cc = few ? 0 : c1; cc < (few ? n_classes : c1 + 1); cc++) {
-          const bool l = lt[u] && cv[u] == cc, e = eq[u] && cv[u] == cc;
-          const uint64_t mlt = __ballot(l), meq = __ballot(e);
-          if ((mlt | meq) == 0ull) continue;
-          const uint32_t rl = few ? (uint32_t)__shfl((int)run_lt, cc) : run_lt;
-          const uint32_t re = few ? (uint32_t)__shfl((int)run_eq, cc) : run_eq;
-          int32_t* out = nbr + (i * n_classes + cc) * k;
-          if (l) out[rl + __popcll(mlt & below)] = (int32_t)j;
-          if (e) {
-            const uint32_t r = re + (uint32_t)__popcll(meq & below);
-            if (r < need[cc]) out[cnt_lt[cc] + r] = (int32_t)j;
-          }
-          if (!few || lane == cc) {
-            run_lt += (uint32_t)__popcll(mlt);
-            run_eq += (uint32_t)__popcll(meq);
-          }
-        }
-      }
+      for (int u = 0; u < kCU; u++) emit(lt[u], eq[u], cv[u], j0 + 64 * u + lane);
     }
   }
   RF_T(7);
@@ -2867,6 +2961,7 @@ struct Plan {
   int64_t* dtab_off = nullptr;
   double* dtab = nullptr;
   int32_t* lab = nullptr;
+  uint8_t* lab8 = nullptr;  // ReliefF: class codes as bytes (zero padding)
   uint32_t* xqT = nullptr;
   float* xs = nullptr;
   float* epsT = nullptr;
@@ -3985,6 +4080,12 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   if ((!sx && (rc = h2d(g, (char*)g->x, (const char*)x, xbytes))) ||
       (rc = h2d(g, g->lab, lab.data(), Q.n_pad)))
     return fail(rc);
+  if (Q.algo == ALGO_RELIEFF) {
+    std::vector<uint8_t> lab8((size_t)Q.n_pad + 16, 0);
+    for (int64_t j = 0; j < Q.n; j++) lab8[j] = (uint8_t)Q.labels[j];
+    if ((rc = dalloc(g, &g->lab8, lab8.size())) || (rc = h2d(g, g->lab8, lab8.data(), lab8.size())))
+      return fail(rc);
+  }
   if ((rc = plan_layout(g))) return fail(rc);
   trace_mark("plan: H2D + layout");
   *out = g;
@@ -4577,31 +4678,35 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   FS_TRY(dalloc(g, &tneed, (size_t)n * C));
   FS_TRY(dalloc(g, &teq, (size_t)n * C));
   g->alloc_target = 0;
-  // histograms: 1024 bins per class for n_classes <= 8 (10-bit first digit)
-  const size_t shbytes = (size_t)C * (C <= 8 ? 1024 : 256) * 4 + 2 * (size_t)C * 4;
-  size_t shstage = shbytes + (size_t)n * 5;
-  // (k_rf_select's static LDS, ~1 KB, comes out of the same 160 KB)
-  constexpr size_t kSelLds = 159 * 1024;
-  const bool stage = shstage <= kSelLds;
-  // the rest of the 160 KB: the exact keys' gather buffer (x_i, the scales
-  // and at least one candidate row at the continuous columns), else none
-  // (the unstaged kernel keeps to 40 KB: four workgroups per CU)
+  // histograms: 1024 bins per class for n_classes <= 8 (10-bit first digit);
+  // staged rows: 4 B of key + 1 B of class code per sample (by quads), for
+  // n <= 32768 (one round trip of 8 quads per thread)
+  const size_t shbytes = (size_t)C * (C <= 8 ? 1024 : 256) * 4;
+  const size_t nq = (size_t)(n + 3) / 4;
+  const size_t shstage = shbytes + nq * 20;
+  // (k_rf_select's static LDS, 2.2 KB, comes out of the same 160 KB)
+  constexpr size_t kSelLds = 157 * 1024;
+  const bool stage = n <= 32768 && shstage <= kSelLds;
+  // the rest of the 160 KB: the exact keys' gather buffer (x_i, the scales,
+  // the column indices and at least one candidate row at the continuous
+  // columns), else none (the unstaged kernel keeps to 40 KB: four
+  // workgroups per CU)
   size_t shsel = stage ? shstage : shbytes;
   int xlds = 0;
   const size_t lds_cap = stage ? kSelLds : 40 * 1024;
   const size_t lds_left = lds_cap > shsel + 16 ? lds_cap - 16 - shsel : 0;
-  if (Q.pc > 0 && lds_left / 4 >= (size_t)Q.pc * 3) xlds = (int)(lds_left / 4);
+  if (Q.pc > 0 && lds_left / 4 >= (size_t)Q.pc * 4) xlds = (int)(lds_left / 4);
   if (const char* e = std::getenv("FS_RF_XLDS")) {  // A/B, tests: a cap in floats
     const long v = std::atol(e);
-    if (v < xlds) xlds = v >= 3 * Q.pc ? (int)v : 0;
+    if (v < xlds) xlds = v >= 4 * Q.pc ? (int)v : 0;
   }
   if (xlds) shsel += 16 + (size_t)xlds * 4;
   if (shsel > 64 * 1024) {
     if (stage)
-      FS_HIP(hipFuncSetAttribute((const void*)k_rf_select<true, true>,
+      FS_HIP(hipFuncSetAttribute((const void*)k_rf_select<true>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shsel));
     else
-      FS_HIP(hipFuncSetAttribute((const void*)k_rf_select<false, true>,
+      FS_HIP(hipFuncSetAttribute((const void*)k_rf_select<false>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)shsel));
   }
   // band of the exact-key refinement (quantisation error + float32 rounding)
@@ -4615,8 +4720,8 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   const float* xk = Q.pc > 0 ? (const float*)g->x : nullptr;
   // candidates listed in LDS per row (above: the general route); FS_RF_FCAP
   // lowers it (0 forces the general route: tests)
-  int64_t fcap = 256;
-  if (const char* e = std::getenv("FS_RF_FCAP")) fcap = std::max<int64_t>(0, std::atoll(e));
+  int fcap = 256;
+  if (const char* e = std::getenv("FS_RF_FCAP")) fcap = std::max(0, std::atoi(e));
   FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
 #ifdef FS_RF_PROF
   {
@@ -4627,15 +4732,15 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
 #endif
   FS_HIP(hipEventRecord(g->ev[4], g->stream));
   if (stage)
-    k_rf_select<true, true><<<(unsigned)nr_own, 1024, shsel, g->stream>>>(
-        g->D, g->Dk, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, r_lo, tkey, tneed, teq, nbr,
-        nfound, band_abs, band_rel, fcap, g->list_count, xk, Q.p_in, Q.pc, Q.PC, Q.pd,
-        g->src_col, g->scl, xlds);
+    k_rf_select<true><<<(unsigned)nr_own, 1024, shsel, g->stream>>>(
+        g->Dk, (int)n, Q.n_pad, g->lab, g->lab8, dcc, C, (int)k, r_lo, tkey, tneed, teq, nbr,
+        nfound, band_abs, band_rel, fcap, g->list_count, xk, Q.p_in, (int)Q.pc, (int)Q.PC,
+        (int)Q.pd, g->src_col, g->scl, xlds);
   else
-    k_rf_select<false, true><<<(unsigned)nr_own, 256, shsel, g->stream>>>(
-        g->D, g->Dk, n, Q.n_pad, inv_sc, g->lab, dcc, C, k, r_lo, tkey, tneed, teq, nbr,
-        nfound, band_abs, band_rel, fcap, g->list_count, xk, Q.p_in, Q.pc, Q.PC, Q.pd,
-        g->src_col, g->scl, xlds);
+    k_rf_select<false><<<(unsigned)nr_own, 256, shsel, g->stream>>>(
+        g->Dk, (int)n, Q.n_pad, g->lab, g->lab8, dcc, C, (int)k, r_lo, tkey, tneed, teq, nbr,
+        nfound, band_abs, band_rel, fcap, g->list_count, xk, Q.p_in, (int)Q.pc, (int)Q.PC,
+        (int)Q.pd, g->src_col, g->scl, xlds);
   FS_TRY(launch_check("k_rf_select"));
   FS_HIP(hipEventRecord(g->ev[5], g->stream));
   // exact keys computed (list_count), read with the tie counts below

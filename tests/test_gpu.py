@@ -195,7 +195,7 @@ def test_relieff_unstaged_rows(oracle):
 @pytest.mark.parametrize("n", [2500, 33000])
 def test_relieff_exact_keys_lds_and_global(n, monkeypatch):
     """k_rf_select's in-kernel exact keys: candidate rows gathered into LDS
-    in batches (default; one row per batch with FS_RF_XLDS=3*pc) or summed
+    in batches (default; one row per batch with FS_RF_XLDS=4*pc) or summed
     straight from HBM (FS_RF_XLDS=0), and the
     exact k-th key comes from the row's candidate list (default) or from a
     second selection over the whole row (FS_RF_FCAP=0, the route of rows with
@@ -212,7 +212,7 @@ def test_relieff_exact_keys_lds_and_global(n, monkeypatch):
     out = {}
     pc = 1100 if n < 10000 else 70
     for mode, env in (("default", {}), ("hbm", {"FS_RF_XLDS": "0"}),
-                      ("batch1", {"FS_RF_XLDS": str(3 * pc)}),
+                      ("batch1", {"FS_RF_XLDS": str(4 * pc)}),
                       ("general", {"FS_RF_FCAP": "0"})):
         for key, val in env.items():
             monkeypatch.setenv(key, val)
@@ -232,6 +232,20 @@ def test_relieff_ties_large_rows(oracle):
     y = rng.integers(0, 2, 3000)
     s = _fit(ReliefF, X, y, n_neighbors=10, discrete_limit=4)
     assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=10, discrete_limit=4), TOL)
+
+
+def test_relieff_collection_overflow(oracle):
+    """Rows where most keys tie at the k-th key (90% of the samples are one
+    point): the per-wave hit lists of k_rf_select's collection overflow and
+    its pass 2 sweeps the row again; numba's quicksort order then decides
+    (k_rf_ties).  GPU == oracle."""
+    from fastselect_amd import ReliefF
+    rng = np.random.default_rng(9)
+    X = rng.standard_normal((2400, 5))
+    X[rng.random(2400) < 0.9] = X[0]
+    y = rng.integers(0, 2, 2400)
+    s = _fit(ReliefF, X, y, n_neighbors=10)
+    assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=10), TOL)
 
 
 def test_relieff_large_n_boundary(oracle):
