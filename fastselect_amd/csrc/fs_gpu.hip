@@ -2796,6 +2796,272 @@ __device__ int wave_argsort_focus(int64_t len, int32_t* R, KeyFn key, int32_t* b
   return 0;
 }
 
+// Tie rows with n <= kTieMwMaxN: one 1024-thread workgroup per row, the
+// row's exact keys (float32) and its permutation (16-bit handles: sample
+// index | 0x8000 for a tied candidate) in LDS, 6 bytes per sample.  The
+// quicksort replay is numba_argsort_focus's, run by 16 waves at once: the
+// sub-ranges a partition leaves are disjoint, so the order in which they are
+// processed does not change the result.  A wave pops a range from a shared
+// queue, partitions it as wave_argsort_focus does (ballot-collected stops,
+// up to 64 swaps per step), pushes the larger side when it holds a tied
+// candidate and keeps partitioning the smaller, then insertion-sorts it;
+// idle waves wait on the queue until it is empty and no wave is busy.
+constexpr int64_t kTieMwMaxN = 25000;  // 6 B per sample + 12 KB static LDS
+constexpr int kTieQ = 512;
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__global__ __launch_bounds__(1024) void k_rf_ties_mw(
+    const int32_t* __restrict__ rows, int n, const float* __restrict__ keys_all,
+    const float* __restrict__ Dk, int64_t n_pad, const int32_t* __restrict__ lab, int n_classes, int k, const uint32_t* __restrict__ tkey,
+    const int32_t* __restrict__ tneed, const int32_t* __restrict__ teq,
+    int32_t* __restrict__ nbr, int* __restrict__ status) {
+  extern __shared__ __align__(16) uint32_t tie_lds[];
+  float* key = (float*)tie_lds;                 // [n] by sample index
+  uint16_t* R = (uint16_t*)(key + n);           // [n] the permutation
+  __shared__ int q_lo[kTieQ], q_hi[kTieQ];
+  __shared__ int q_n, q_busy, q_lock, q_err;
+  __shared__ int32_t bufL_all[16][64], bufR_all[16][64];
+  const int tid = threadIdx.x, nt = blockDim.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int64_t r = blockIdx.x;
+  const int i = rows[r];
+  // keys_all: the row's exact keys (k_rf_exact_rows); null: no continuous
+  // features, the plan's keys are exact already (the row of Dk)
+  const float* kg = keys_all != nullptr ? keys_all + r * n : Dk + (int64_t)i * n_pad;
+  const uint32_t* Ti = tkey + (int64_t)i * n_classes;
+  const int32_t* need = tneed + (int64_t)i * n_classes;
+  const int32_t* eq = teq + (int64_t)i * n_classes;
+  for (int j = tid; j < n; j += nt) {
+    const float kv = (keys_all == nullptr && j == i) ? __builtin_inff() : kg[j];
+    const int c = lab[j];
+    key[j] = kv;
+    const bool t = j != i && eq[c] > need[c] && __float_as_uint(kv) == Ti[c];
+    R[j] = (uint16_t)(j | (t ? 0x8000 : 0));
+  }
+  if (tid == 0) {
+    q_n = n >= 2 ? 1 : 0;
+    q_lo[0] = 0;
+    q_hi[0] = n - 1;
+    q_busy = 0;
+    q_lock = 0;
+    q_err = 0;
+  }
+  __syncthreads();
+  {
+    int32_t* bufL = bufL_all[wave];
+    int32_t* bufR = bufR_all[wave];
+    const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    auto key_h = [&](uint32_t h) { return key[h & 0x7FFFu]; };
+    auto lock = [&]() {  // lane 0 only
+      while (atomicCAS(&q_lock, 0, 1) != 0) __builtin_amdgcn_s_sleep(2);
+      __threadfence_block();
+    };
+    auto unlock = [&]() {
+      __threadfence_block();
+      atomicExch(&q_lock, 0);
+    };
+    auto has_interest = [&](int lo, int hi) {
+      for (int t0 = lo; t0 <= hi; t0 += 64) {
+        const int t = t0 + lane;
+        if (__ballot(t <= hi && (R[t] & 0x8000u)) != 0ull) return true;
+      }
+      return false;
+    };
+    // up to 64 stops of one side inside [a, b], in scan order, into buf
+    auto collect = [&](int a, int b, float pivot, bool left, int32_t* buf) {
+      int cnt = 0;
+      for (int c0 = 0; cnt < 64 && c0 <= b - a; c0 += 64) {
+        const int t = left ? a + c0 + lane : b - c0 - lane;
+        bool stop = false;
+        if (left ? t <= b : t >= a) {
+          const float kv = key_h(R[t]);
+          stop = left ? !(kv < pivot) : !(pivot < kv);
+        }
+        const uint64_t m = __ballot(stop);
+        const int rank = cnt + __popcll(m & below);
+        if (stop && rank < 64) buf[rank] = t;
+        cnt += __popcll(m);
+      }
+      wave_sync();
+      return cnt < 64 ? cnt : 64;
+    };
+    auto push = [&](int lo, int hi) {
+      if (lane == 0) {
+        lock();
+        if (q_n < kTieQ) {
+          q_lo[q_n] = lo;
+          q_hi[q_n] = hi;
+          q_n++;
+        } else {
+          q_err = 1;  // queue overflow
+        }
+        unlock();
+      }
+      wave_sync();
+    };
+    constexpr int kSmall = 15;
+    // numba's partition loop from [low, high], keeping the smaller side
+    auto chain = [&](int low, int high) {
+      while (high - low >= kSmall) {
+        const int mid = (low + high) >> 1;
+        // median of three and pivot stash: identical on every lane, one writer
+        uint32_t rl = R[low], rm = R[mid], rh = R[high], tmp;
+        if (key_h(rm) < key_h(rl)) { tmp = rl; rl = rm; rm = tmp; }
+        if (key_h(rh) < key_h(rm)) { tmp = rh; rh = rm; rm = tmp; }
+        if (key_h(rm) < key_h(rl)) { tmp = rl; rl = rm; rm = tmp; }
+        const float pivot = key_h(rm);
+        wave_sync();
+        if (lane == 0) {
+          R[low] = (uint16_t)rl;
+          R[mid] = (uint16_t)rh;  // stash: R[high] <-> R[mid]
+          R[high] = (uint16_t)rm;
+        }
+        wave_sync();
+        // partition [low, high - 1] around pivot
+        int a = low, b = high - 1, jprev = high, ifinal = -1;
+        while (ifinal < 0) {
+          const int cl = collect(a, b, pivot, true, bufL);
+          const int cr = collect(a, b, pivot, false, bufR);
+          const int Lm = lane < cl ? bufL[lane] : INT32_MAX;
+          const int Rm = lane < cr ? bufR[lane] : -1;
+          const uint64_t fail = __ballot(!(Lm < Rm));
+          const int f = fail ? (int)__builtin_ctzll(fail) : 64;
+          // swaps m < f, all positions distinct: read, then write
+          uint16_t vl = 0, vr = 0;
+          if (lane < f) { vl = R[Lm]; vr = R[Rm]; }
+          wave_sync();
+          if (lane < f) { R[Lm] = vr; R[Rm] = vl; }
+          wave_sync();
+          if (f < 64) {
+            const int jlast = f > 0 ? bufR[f - 1] : jprev;
+            ifinal = f < cl ? bufL[f] : jlast;
+            if (ifinal > jlast) ifinal = jlast;
+          } else {
+            a = bufL[63] + 1;
+            b = bufR[63] - 1;
+            jprev = bufR[63];
+          }
+          wave_sync();
+        }
+        const int ip = ifinal;
+        {
+          const uint16_t ri = R[ip], rh2 = R[high];
+          wave_sync();
+          if (lane == 0) { R[ip] = rh2; R[high] = ri; }
+          wave_sync();
+        }
+        int push_lo, push_hi, keep_lo, keep_hi;
+        if (high - ip > ip - low) {
+          push_lo = ip + 1; push_hi = high; keep_lo = low; keep_hi = ip - 1;
+        } else {
+          push_lo = low; push_hi = ip - 1; keep_lo = ip + 1; keep_hi = high;
+        }
+        if (push_hi >= push_lo && has_interest(push_lo, push_hi)) push(push_lo, push_hi);
+        low = keep_lo;
+        high = keep_hi;
+        if (high < low || !has_interest(low, high)) return;
+      }
+      if (lane == 0) {  // insertion sort [low, high]
+        for (int ii = low + 1; ii <= high; ii++) {
+          const uint16_t kk = R[ii];
+          const float v = key_h(kk);
+          int j = ii;
+          while (j > low && v < key_h(R[j - 1])) {
+            R[j] = R[j - 1];
+            j--;
+          }
+          R[j] = kk;
+        }
+      }
+      wave_sync();
+    };
+    // the work queue; a wave waiting more than 2^22 naps (~2 s) gives up
+    // (idle waves poll without the lock and take it only to pop or to
+    // confirm the end: pollers holding it would starve the busy waves'
+    // pushes)
+    int spins = 0;
+    while (true) {
+      int st = 1, lo = 0, hi = 0;
+      if (lane == 0) {
+        const int qn = *(volatile int*)&q_n, qb = *(volatile int*)&q_busy;
+        if (*(volatile int*)&q_err) {
+          st = 2;
+        } else if (qn > 0 || qb == 0) {
+          lock();
+          if (q_err) {
+            st = 2;
+          } else if (q_n > 0) {
+            q_n--;
+            lo = q_lo[q_n];
+            hi = q_hi[q_n];
+            q_busy++;
+            st = 0;
+          } else if (q_busy == 0) {
+            st = 2;
+          }
+          unlock();
+        }
+      }
+      st = __shfl(st, 0);
+      lo = __shfl(lo, 0);
+      hi = __shfl(hi, 0);
+      if (st == 2) break;
+      if (st == 1) {
+        if (++spins > (1 << 22)) {
+          if (lane == 0) atomicExch(&q_err, 2 + (q_busy << 8) + (q_n << 20));  // wait timeout
+          break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+        continue;
+      }
+      chain(lo, hi);
+      if (lane == 0) {
+        lock();
+        q_busy--;
+        unlock();
+      }
+    }
+  }
+  __syncthreads();
+  if (q_err) {
+    if (tid == 0) atomicExch(status, q_err);
+    return;
+  }
+  if (wave != 0) return;
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  for (int c = 0; c < n_classes; c++) {
+    if (!(eq[c] > need[c])) continue;
+    int32_t* out = nbr + ((int64_t)i * n_classes + c) * k;
+    const float T = __uint_as_float(Ti[c]);
+    int cnt = 0;
+    // every key < T of class c, in index order
+    for (int j0 = 0; j0 < n; j0 += 64) {
+      const int j = j0 + lane;
+      const bool take = j < n && j != i && lab[j] == c && key[j] < T;
+      const uint64_t m = __ballot(take);
+      if (take) out[cnt + __popcll(m & below)] = j;
+      cnt += __popcll(m);
+    }
+    // then the first need[c] tied keys of class c in numba's order
+    int left = need[c];
+    for (int t0 = 0; t0 < n && left > 0; t0 += 64) {
+      const int t = t0 + lane;
+      const uint32_t h = t < n ? R[t] : 0u;
+      const bool take = (h & 0x8000u) && lab[h & 0x7FFFu] == c;
+      const uint64_t m = __ballot(take);
+      const int rank = __popcll(m & below);
+      if (take && rank < left) out[cnt + rank] = (int32_t)(h & 0x7FFFu);
+      const int got = __popcll(m);
+      cnt += got < left ? got : left;
+      left -= got < left ? got : left;
+    }
+  }
+}
+
 template <bool IN_LDS>
 __global__ __launch_bounds__(64) void k_rf_ties(const int32_t* __restrict__ rows, int64_t n,
                                                 const float* __restrict__ keys_all,
@@ -4783,30 +5049,48 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
       }
   g->n_tie_rows = (int64_t)tie_rows.size();
   if (tie_rows.empty()) return FS_OK;
-  // batches bounded to ~512 MB of per-row scratch (keys + permutation)
-  const int64_t batch = std::max<int64_t>(1, std::min<int64_t>((int64_t)tie_rows.size(),
-                                                               (int64_t)(512ll << 20) / (8 * n)));
+  // n <= kTieMwMaxN: 16 waves per row, the row in LDS (6 B per sample)
+  const bool mw = n <= kTieMwMaxN && !std::getenv("FS_TIES_1W");  // FS_TIES_1W: A/B
+  const size_t mw_lds = ((size_t)n * 6 + 15) & ~(size_t)15;
+  // per-row scratch: exact keys (unless all-discrete under mw) and the
+  // one-wave replay's permutation; batches bounded to ~512 MB of it
+  const bool need_keys = !(mw && Q.pc == 0);
+  const int64_t row_bytes = (need_keys ? 4 * n : 0) + (mw ? 0 : 4 * n);
+  const int64_t batch = std::max<int64_t>(
+      1, std::min<int64_t>((int64_t)tie_rows.size(),
+                           row_bytes > 0 ? (int64_t)(512ll << 20) / row_bytes : INT64_MAX));
   int32_t *drows = nullptr, *R = nullptr;
   float* keys = nullptr;
   int* status = nullptr;
   g->alloc_target = 2;
   FS_TRY(dalloc(g, &drows, (size_t)batch));
-  FS_TRY(dalloc(g, &R, (size_t)batch * n));
-  FS_TRY(dalloc(g, &keys, (size_t)batch * n));
+  if (!mw) FS_TRY(dalloc(g, &R, (size_t)batch * n));
+  if (need_keys) FS_TRY(dalloc(g, &keys, (size_t)batch * n));
   FS_TRY(dalloc(g, &status, 1));
   g->alloc_target = 0;
   FS_HIP(hipMemsetAsync(status, 0, sizeof(int), g->stream));
-  if (n <= kTieLdsMaxN)
+  if (mw)
+    FS_HIP(hipFuncSetAttribute((const void*)k_rf_ties_mw,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)mw_lds));
+  else if (n <= kTieLdsMaxN)
     FS_HIP(hipFuncSetAttribute((const void*)k_rf_ties<true>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(8 * n)));
   for (int64_t r0 = 0; r0 < (int64_t)tie_rows.size(); r0 += batch) {
     const int64_t nr = std::min<int64_t>(batch, (int64_t)tie_rows.size() - r0);
     FS_TRY(h2d(g, drows, tie_rows.data() + r0, (size_t)nr));
-    k_rf_exact_rows<float><<<dim3((unsigned)nr, (unsigned)((n + 3) / 4)), 256, 0, g->stream>>>(
-        (const float*)g->x, n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, drows, g->D, g->Dk,
-        Q.n_pad, inv_sc, keys);
-    FS_TRY(launch_check("k_rf_exact_rows"));
-    if (n <= kTieLdsMaxN)
+    // (all-discrete: the multi-wave replay reads the plan's keys, exact
+    // already, straight from Dk)
+    if (need_keys) {
+      k_rf_exact_rows<float><<<dim3((unsigned)nr, (unsigned)((n + 3) / 4)), 256, 0, g->stream>>>(
+          (const float*)g->x, n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, drows, g->D,
+          g->Dk, Q.n_pad, inv_sc, keys);
+      FS_TRY(launch_check("k_rf_exact_rows"));
+    }
+    if (mw)
+      k_rf_ties_mw<<<(unsigned)nr, 1024, mw_lds, g->stream>>>(
+          drows, (int)n, need_keys ? keys : nullptr, g->Dk, Q.n_pad, g->lab, C, (int)k, tkey,
+          tneed, teq, nbr, status);
+    else if (n <= kTieLdsMaxN)
       k_rf_ties<true><<<(unsigned)nr, 64, (size_t)8 * n, g->stream>>>(
           drows, n, keys, g->lab, C, k, tkey, tneed, teq, R, nbr, status);
     else
@@ -4818,7 +5102,9 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   FS_HIP(hipMemcpyAsync(&hstatus, status, sizeof(int), hipMemcpyDeviceToHost, g->stream));
   FS_HIP(hipStreamSynchronize(g->stream));
   if (hstatus != 0) {
-    set_error("ReliefF tie ordering: quicksort stack overflow");
+    set_error(hstatus == 1 ? "ReliefF tie ordering: quicksort stack overflow"
+                           : ("ReliefF tie ordering: work queue stalled (status " +
+                              std::to_string(hstatus) + ")").c_str());
     return FS_EHIP;
   }
   return FS_OK;

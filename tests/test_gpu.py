@@ -234,6 +234,21 @@ def test_relieff_ties_large_rows(oracle):
     assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=10, discrete_limit=4), TOL)
 
 
+def test_relieff_ties_multiwave_matches_single_wave(monkeypatch):
+    """k_rf_ties_mw (16 waves per tie row taking quicksort sub-ranges from a
+    shared queue) against the one-wave replay (FS_TIES_1W): every row of
+    all-discrete data is a tie row; the orders, so the scores, must be
+    bit-identical."""
+    from fastselect_amd import ReliefF
+    rng = np.random.default_rng(12)
+    X = rng.integers(0, 3, size=(4000, 40)).astype(float)
+    y = rng.integers(0, 3, 4000)
+    a = _fit(ReliefF, X, y, n_neighbors=10)
+    monkeypatch.setenv("FS_TIES_1W", "1")
+    b = _fit(ReliefF, X, y, n_neighbors=10)
+    assert np.array_equal(a, b)
+
+
 def test_relieff_collection_overflow(oracle):
     """Rows where most keys tie at the k-th key (90% of the samples are one
     point): the per-wave hit lists of k_rf_select's collection overflow and
