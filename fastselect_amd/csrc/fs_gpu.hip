@@ -2818,7 +2818,8 @@ __global__ __launch_bounds__(1024) void k_rf_ties_mw(
     const int32_t* __restrict__ rows, int n, const float* __restrict__ keys_all,
     const float* __restrict__ Dk, int64_t n_pad, const int32_t* __restrict__ lab, int n_classes, int k, const uint32_t* __restrict__ tkey,
     const int32_t* __restrict__ tneed, const int32_t* __restrict__ teq,
-    int32_t* __restrict__ nbr, int* __restrict__ status) {
+    int32_t* __restrict__ nbr, int32_t* __restrict__ scr_all, int coop_min,
+    int* __restrict__ status) {
   extern __shared__ __align__(16) uint32_t tie_lds[];
   float* key = (float*)tie_lds;                 // [n] by sample index
   uint16_t* R = (uint16_t*)(key + n);           // [n] the permutation
@@ -2842,15 +2843,161 @@ __global__ __launch_bounds__(1024) void k_rf_ties_mw(
     const bool t = j != i && eq[c] > need[c] && __float_as_uint(kv) == Ti[c];
     R[j] = (uint16_t)(j | (t ? 0x8000 : 0));
   }
+  // Ranges of at least coop_min samples are partitioned by the whole
+  // workgroup first (the top of the tree, where one wave would work alone):
+  // the m-th swap of numba's Hoare loop exchanges the m-th left stop
+  // (ascending, key >= pivot, `high` included) with the m-th right stop
+  // (descending, key <= pivot), and the loop ends at the first m whose left
+  // stop has at most m right stops after it; the pivot then goes to
+  // min(L_f, R_{f-1}) (R_{-1} = high).  Stops are ranked by a block scan,
+  // the right stops' positions pass through `scr` (global, per row), and
+  // every swap is done by its left stop's thread.  Smaller ranges go to the
+  // per-wave queue below.
+  __shared__ int big_lo[64], big_hi[64], big_n;
+  __shared__ int sc_a[16], sc_b[16], s_f, s_lf, s_rprev;
+  __shared__ float s_pivot;
+  int32_t* scr = scr_all + r * n;
   if (tid == 0) {
-    q_n = n >= 2 ? 1 : 0;
-    q_lo[0] = 0;
-    q_hi[0] = n - 1;
+    q_n = 0;
+    big_n = 0;
+    if (n >= 2) {
+      if (n >= coop_min) big_lo[0] = 0, big_hi[0] = n - 1, big_n = 1;
+      else q_lo[0] = 0, q_hi[0] = n - 1, q_n = 1;
+    }
     q_busy = 0;
     q_lock = 0;
     q_err = 0;
   }
   __syncthreads();
+  {
+    auto key_h = [&](uint32_t h) { return key[h & 0x7FFFu]; };
+    // exclusive block scan of (a, b) in thread order, and the totals
+    auto block_scan2 = [&](int a, int b, int& ea, int& eb, int& ta, int& tb) {
+      int ia = a, ib = b;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int xa = __shfl_up(ia, o), xb = __shfl_up(ib, o);
+        if (lane >= o) ia += xa, ib += xb;
+      }
+      if (lane == 63) sc_a[wave] = ia, sc_b[wave] = ib;
+      __syncthreads();
+      int pa = 0, pb = 0, sa = 0, sb = 0;
+      for (int w = 0; w < (nt >> 6); w++) {
+        const int va = sc_a[w], vb = sc_b[w];
+        if (w < wave) pa += va, pb += vb;
+        sa += va;
+        sb += vb;
+      }
+      ea = pa + ia - a;
+      eb = pb + ib - b;
+      ta = sa;
+      tb = sb;
+      __syncthreads();
+    };
+    while (true) {
+      const int nb = big_n;
+      if (nb == 0) break;
+      const int low = big_lo[nb - 1], high = big_hi[nb - 1];
+      const int mid = (low + high) >> 1;
+      __syncthreads();
+      if (tid == 0) {
+        big_n = nb - 1;
+        s_f = INT32_MAX;
+        // median of three and pivot stash (numba_argsort_focus)
+        uint32_t rl = R[low], rm = R[mid], rh = R[high], tmp;
+        if (key_h(rm) < key_h(rl)) { tmp = rl; rl = rm; rm = tmp; }
+        if (key_h(rh) < key_h(rm)) { tmp = rh; rh = rm; rm = tmp; }
+        if (key_h(rm) < key_h(rl)) { tmp = rl; rl = rm; rm = tmp; }
+        R[low] = (uint16_t)rl;
+        R[mid] = (uint16_t)rh;
+        R[high] = (uint16_t)rm;
+        s_pivot = key_h(rm);
+      }
+      __syncthreads();
+      const float pivot = s_pivot;
+      const int seg = (high - low + nt) / nt;  // <= 32: n <= kTieMwMaxN
+      const int s0 = low + tid * seg;
+      uint32_t mL = 0u, mR = 0u;
+      for (int u = 0; u < seg; u++) {
+        const int q = s0 + u;
+        if (q > high) break;
+        const float kv = key_h(R[q]);
+        if (!(kv < pivot)) mL |= 1u << u;
+        if (q < high && !(pivot < kv)) mR |= 1u << u;
+      }
+      int eL, eR, TL, TR;
+      block_scan2(__popc(mL), __popc(mR), eL, eR, TL, TR);
+      (void)TL;
+      // the crossing f: the first left stop (rank m) with after <= m
+      for (uint32_t w = mL; w != 0u;) {
+        const int u = __builtin_ctz(w);
+        w &= w - 1u;
+        const int rank = eL + __popc(mL & ((1u << u) - 1u));
+        const uint32_t upto = u >= 31 ? 0xFFFFFFFFu : ((2u << u) - 1u);
+        const int after = TR - (eR + __popc(mR & upto));
+        if (after <= rank) {
+          atomicMin(&s_f, rank);
+          break;
+        }
+      }
+      __syncthreads();
+      const int f = s_f;
+      for (uint32_t w = mL; w != 0u;) {
+        const int u = __builtin_ctz(w);
+        w &= w - 1u;
+        if (eL + __popc(mL & ((1u << u) - 1u)) == f) s_lf = s0 + u;
+      }
+      for (uint32_t w = mR; w != 0u;) {
+        const int u = __builtin_ctz(w);
+        w &= w - 1u;
+        const int d = TR - 1 - (eR + __popc(mR & ((1u << u) - 1u)));
+        if (d < f) scr[d] = s0 + u;
+        if (d == f - 1) s_rprev = s0 + u;
+      }
+      __syncthreads();
+      for (uint32_t w = mL; w != 0u;) {
+        const int u = __builtin_ctz(w);
+        w &= w - 1u;
+        const int rank = eL + __popc(mL & ((1u << u) - 1u));
+        if (rank < f) {
+          const int q = s0 + u, q2 = scr[rank];
+          const uint16_t a = R[q];
+          R[q] = R[q2];
+          R[q2] = a;
+        }
+      }
+      __syncthreads();
+      const int ip = f > 0 ? (s_lf < s_rprev ? s_lf : s_rprev) : s_lf;
+      if (tid == 0) {
+        const uint16_t a = R[ip];
+        R[ip] = R[high];
+        R[high] = a;
+      }
+      __syncthreads();
+      // the two sides: with a tied candidate, back to the big list or to
+      // the queue
+#pragma unroll
+      for (int side = 0; side < 2; side++) {
+        const int a = side ? ip + 1 : low, b = side ? high : ip - 1;
+        if (b < a) continue;
+        const int sg = (b - a + nt) / nt;
+        bool any = false;
+        for (int u = 0; u < sg; u++) {
+          const int q = a + tid * sg + u;
+          if (q <= b && (R[q] & 0x8000u)) any = true;
+        }
+        if (__syncthreads_or(any) && tid == 0) {
+          if (b - a + 1 >= coop_min && big_n < 64) {
+            big_lo[big_n] = a, big_hi[big_n] = b, big_n++;
+          } else if (q_n < kTieQ) {
+            q_lo[q_n] = a, q_hi[q_n] = b, q_n++;
+          } else {
+            q_err = 1;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
   {
     int32_t* bufL = bufL_all[wave];
     int32_t* bufR = bufR_all[wave];
@@ -5052,10 +5199,13 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   // n <= kTieMwMaxN: 16 waves per row, the row in LDS (6 B per sample)
   const bool mw = n <= kTieMwMaxN && !std::getenv("FS_TIES_1W");  // FS_TIES_1W: A/B
   const size_t mw_lds = ((size_t)n * 6 + 15) & ~(size_t)15;
+  int coop_min = 2048;  // ranges the whole workgroup partitions (FS_TIES_COOP: A/B)
+  if (const char* e = std::getenv("FS_TIES_COOP")) coop_min = std::max(16, std::atoi(e));
   // per-row scratch: exact keys (unless all-discrete under mw) and the
   // one-wave replay's permutation; batches bounded to ~512 MB of it
   const bool need_keys = !(mw && Q.pc == 0);
-  const int64_t row_bytes = (need_keys ? 4 * n : 0) + (mw ? 0 : 4 * n);
+  // (mw: the cooperative partitions' scratch; else the permutation)
+  const int64_t row_bytes = (need_keys ? 4 * n : 0) + 4 * n;
   const int64_t batch = std::max<int64_t>(
       1, std::min<int64_t>((int64_t)tie_rows.size(),
                            row_bytes > 0 ? (int64_t)(512ll << 20) / row_bytes : INT64_MAX));
@@ -5064,7 +5214,7 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   int* status = nullptr;
   g->alloc_target = 2;
   FS_TRY(dalloc(g, &drows, (size_t)batch));
-  if (!mw) FS_TRY(dalloc(g, &R, (size_t)batch * n));
+  FS_TRY(dalloc(g, &R, (size_t)batch * n));
   if (need_keys) FS_TRY(dalloc(g, &keys, (size_t)batch * n));
   FS_TRY(dalloc(g, &status, 1));
   g->alloc_target = 0;
@@ -5089,7 +5239,7 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
     if (mw)
       k_rf_ties_mw<<<(unsigned)nr, 1024, mw_lds, g->stream>>>(
           drows, (int)n, need_keys ? keys : nullptr, g->Dk, Q.n_pad, g->lab, C, (int)k, tkey,
-          tneed, teq, nbr, status);
+          tneed, teq, nbr, R, coop_min, status);
     else if (n <= kTieLdsMaxN)
       k_rf_ties<true><<<(unsigned)nr, 64, (size_t)8 * n, g->stream>>>(
           drows, n, keys, g->lab, C, k, tkey, tneed, teq, R, nbr, status);

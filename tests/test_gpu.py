@@ -235,18 +235,28 @@ def test_relieff_ties_large_rows(oracle):
 
 
 def test_relieff_ties_multiwave_matches_single_wave(monkeypatch):
-    """k_rf_ties_mw (16 waves per tie row taking quicksort sub-ranges from a
-    shared queue) against the one-wave replay (FS_TIES_1W): every row of
+    """k_rf_ties_mw (whole-workgroup partitions of the ranges of >= 2048
+    samples, then 16 waves taking the smaller ranges from a shared queue)
+    against the one-wave replay (FS_TIES_1W) and against workgroup
+    partitions down to 16 samples (FS_TIES_COOP=16): every row of
     all-discrete data is a tie row; the orders, so the scores, must be
-    bit-identical."""
+    bit-identical.  Mixed data (exact keys from k_rf_exact_rows) too."""
     from fastselect_amd import ReliefF
     rng = np.random.default_rng(12)
     X = rng.integers(0, 3, size=(4000, 40)).astype(float)
+    X2 = X.copy()
+    X2[:, :3] = np.round(rng.standard_normal((4000, 3)), 1)
     y = rng.integers(0, 3, 4000)
-    a = _fit(ReliefF, X, y, n_neighbors=10)
-    monkeypatch.setenv("FS_TIES_1W", "1")
-    b = _fit(ReliefF, X, y, n_neighbors=10)
-    assert np.array_equal(a, b)
+    for data in (X, X2):
+        out = []
+        for env in ({}, {"FS_TIES_1W": "1"}, {"FS_TIES_COOP": "16"}):
+            for key, val in env.items():
+                monkeypatch.setenv(key, val)
+            out.append(_fit(ReliefF, data, y, n_neighbors=10))
+            for key in env:
+                monkeypatch.delenv(key)
+        assert np.array_equal(out[0], out[1])
+        assert np.array_equal(out[0], out[2])
 
 
 def test_relieff_collection_overflow(oracle):
