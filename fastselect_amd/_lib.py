@@ -44,7 +44,7 @@ EXPORTED = (
     "fs_version", "fs_last_error", "fs_device_count", "fs_device_cache_release",
     "fs_stage_x", "fs_stage_x_device", "fs_stage_x_cast", "fs_unstage_x", "fs_all_finite",
     "fs_host_alloc", "fs_host_free",
-    "fs_column_stats", "fs_multisurf_score", "fs_multisurf_score_rows",
+    "fs_column_stats", "fs_multisurf_score", "fs_multisurf_last_guard", "fs_multisurf_score_rows",
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_set_rows",
@@ -81,6 +81,8 @@ def _load() -> ctypes.CDLL:
     lib.fs_last_error.restype = ctypes.c_char_p
     lib.fs_device_count.restype = _int
     lib.fs_device_cache_release.restype = _int
+    lib.fs_multisurf_last_guard.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_int)]
+    lib.fs_multisurf_last_guard.restype = _int
     lib.fs_stage_x.argtypes = [_int, _vp, _int, _i64, _i64, ctypes.POINTER(ctypes.c_uint64)]
     lib.fs_stage_x.restype = _int
     lib.fs_host_alloc.argtypes = [ctypes.c_uint64, ctypes.POINTER(_vp)]
@@ -282,6 +284,16 @@ def host_threads(n_jobs=-1) -> int:
 def release_device_cache() -> None:
     """Free the device blocks kept between fits (fs_device_cache_release)."""
     _lib.fs_device_cache_release()
+
+
+def multisurf_last_guard():
+    """(risk, rerun) of this thread's last GPU MultiSURF one-shot call
+    (fs_multisurf_last_guard): the 16-bit decision risk (-1 when not
+    evaluated) and whether the call scored again on 32-bit operands."""
+    risk = ctypes.c_double(-1.0)
+    rerun = _int(0)
+    _lib.fs_multisurf_last_guard(ctypes.byref(risk), ctypes.byref(rerun))
+    return float(risk.value), bool(rerun.value)
 
 
 def device_count() -> int:

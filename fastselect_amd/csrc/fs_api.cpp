@@ -85,6 +85,10 @@ const char* fs_last_error(void) { return g_last_error.c_str(); }
 
 int fs_device_count(void) { return gpu::device_count(); }
 
+int fs_multisurf_last_guard(double* risk_out, int* rerun_out) {
+  return gpu::multisurf_last_guard(risk_out, rerun_out);
+}
+
 int fs_device_cache_release(void) {
   gpu::dev_cache_release();
   return FS_OK;

@@ -3943,7 +3943,7 @@ static int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats) 
 // the environment forces the choice (tests).  SURF has its own float64 pass.
 constexpr int64_t kQ16MinRowsRF = 4096, kQ16MinRowsMS = 16384, kQ16MinRowsMSStar = 10000;
 static int choose_q16(const Prepared& P) {
-  if (P.algo == ALGO_SURF) return 0;
+  if (P.algo == ALGO_SURF || P.no_q16) return 0;
   const char* env = std::getenv("FS_Q16");
   if (env && *env) return std::atoi(env) != 0 ? 1 : 0;
   const int64_t min_rows = P.algo == ALGO_RELIEFF ? kQ16MinRowsRF
@@ -4941,8 +4941,60 @@ static int run_multisurf_shards(Plan* g, int shards, int rank, int world, double
   return FS_OK;
 }
 
+// Decision risk of a MultiSURF score vector computed with 16-bit pass-1
+// operands.  Their thresholds mu - sigma/2 come from quantised row moments
+// (mean corrected by k_colrank / k_rowcorr), so T_i is off by about a
+// quantum (kQ16ThrErr), and every pair whose exact distance lies between the
+// two thresholds is decided differently from MultiSURF.py:193-217.  Row i
+// holds ~ n * phi(1/2) / sigma_i such pairs per quantum of T error (Gaussian
+// row distances, phi(1/2) = 0.352); each moves one sample across its near
+// boundary, changing the row's hit or miss average by ~ dbar / m_i (m_i =
+// the smaller of its near hit / miss counts, dbar the mean per-feature diff
+// from the rows' mean distances, x2 for the features above the mean), i.e.
+// the final score (divided by n) by dbar / (n m_i).  With random signs the
+// expected score error is sqrt(sum_i flips_i * effect_i^2); the risk is that
+// over max |score|.  Measured against the oracle (tests/test_gpu_families.py):
+// uniform noise with unrelated labels, n = 16384: risk ~5e-4, error 1.6e-4
+// (16-bit) vs 5e-5 (32-bit: the reference's own float32 sums, attributed);
+// cfg4 (make_classification, signal): error 1.9e-6 against the float64 sums.
+// Above kQ16MaxRisk the one-shot call scores again on 32-bit operands.
+constexpr double kQ16ThrErr = 1.0, kQ16MaxRisk = 5e-6;
+static thread_local double g_last_risk = -1.0;
+static thread_local int g_last_rerun = 0;
+
+static double q16_decision_risk(const Prepared& P, const std::vector<double>& rs,
+                                const std::vector<double>& cnt, const float* scores) {
+  const double n = (double)P.n, nm1 = n - 1.0;
+  double smax = 0.0;
+  for (int64_t k = 0; k < P.n_kept; k++) smax = std::max(smax, (double)std::fabs(scores[k]));
+  const double nfeat = (double)(P.pc + P.pd);
+  if (n < 3.0 || nfeat <= 0.0 || P.SC <= 0.0) return 0.0;
+  if (smax <= 0.0) return HUGE_VAL;
+  double mu_sum = 0.0;
+  for (int64_t i = 0; i < P.n; i++) mu_sum += (rs[3 * i] - rs[3 * i + 2]) / nm1;
+  const double dbar = 2.0 * mu_sum / n / (P.SC * nfeat);
+  double acc = 0.0;
+  for (int64_t i = 0; i < P.n; i++) {
+    const double mu = rs[3 * i] / nm1, var = rs[3 * i + 1] / nm1 - mu * mu;
+    if (!(var > 0.0)) continue;
+    const double flips = n * 0.352 * kQ16ThrErr / std::sqrt(var);
+    const double m = std::max(1.0, std::min(cnt[2 * i], cnt[2 * i + 1]));
+    const double eff = dbar / (n * m);
+    acc += flips * eff * eff;
+  }
+  return std::sqrt(acc) / smax;
+}
+
+int multisurf_last_guard(double* risk, int* rerun) {
+  if (risk) *risk = g_last_risk;
+  if (rerun) *rerun = g_last_rerun;
+  return FS_OK;
+}
+
 int multisurf_run(const Prepared& P, const void* x, int device, float* scores_out) {
   Plan* g = nullptr;
+  g_last_risk = -1.0;
+  g_last_rerun = 0;
   const int shards = multisurf_shards(P, device, 1);
   FS_TRY(plan_create(&g, P, x, 0, device, 0, shards, 0));
   double *rs = nullptr, *cnt = nullptr, *sc = nullptr;
@@ -4953,7 +5005,33 @@ int multisurf_run(const Prepared& P, const void* x, int device, float* scores_ou
     plan_destroy(g);
     return rc;
   }
+  // MultiSURF* weighs the pairs between the thresholds both ways (far misses)
+  // and is not re-run; an FS_Q16 setting is obeyed as given
+  const char* force = std::getenv("FS_Q16");
+  const bool check = g->use_q16 && !P.use_star && !(force && *force);
+  if (check) {
+    std::vector<double> hrs(3 * P.n), hcnt(2 * P.n);
+    if (hipMemcpyAsync(hrs.data(), rs, sizeof(double) * 3 * P.n, hipMemcpyDeviceToHost,
+                       g->stream) != hipSuccess ||
+        hipMemcpyAsync(hcnt.data(), cnt, sizeof(double) * 2 * P.n, hipMemcpyDeviceToHost,
+                       g->stream) != hipSuccess ||
+        hipStreamSynchronize(g->stream) != hipSuccess) {
+      plan_destroy(g);
+      set_error("multisurf: row statistics copy failed");
+      return FS_EHIP;
+    }
+    g_last_risk = q16_decision_risk(g->P, hrs, hcnt, scores_out);  // the plan's scale (SC)
+  }
   plan_destroy(g);
+  if (check && g_last_risk > kQ16MaxRisk) {
+    Prepared P32 = P;
+    P32.no_q16 = 1;
+    trace_mark("multisurf: 16-bit decision risk above bound, 32-bit re-run");
+    const double risk = g_last_risk;
+    FS_TRY(multisurf_run(P32, x, device, scores_out));
+    g_last_risk = risk;
+    g_last_rerun = 1;
+  }
   return FS_OK;
 }
 
@@ -5413,6 +5491,12 @@ int multisurf_run_devices(const Prepared& P, const void* x, const int* devices, 
   std::vector<std::vector<double>> h_rs(N, std::vector<double>(3 * n)),
       h_cnt(N, std::vector<double>(2 * n)), h_sc(N, std::vector<double>(nk));
   std::vector<double> result;
+  int q16_used = 0;
+  double sc_used = 0.0;  // the plans' integer scale (set on the device side)
+  if (r_lo == 0 && r_hi == n) {
+    g_last_risk = -1.0;
+    g_last_rerun = 0;
+  }
   auto worker = [&](int r) {
     Plan* g = nullptr;
     double *rs = nullptr, *cnt = nullptr, *sc = nullptr, *tmp = nullptr;
@@ -5475,6 +5559,10 @@ int multisurf_run_devices(const Prepared& P, const void* x, const int* devices, 
       }
     }
     if (ok && !rc && r == 0) result = sum;  // every thread holds the same sums
+    if (r == 0 && g) {
+      q16_used = g->use_q16;
+      sc_used = g->P.SC;
+    }
     if (g) plan_destroy(g);
     if (ok) fail_out(rc);  // final agreement: a late failure fails the call
     return rc;
@@ -5488,6 +5576,26 @@ int multisurf_run_devices(const Prepared& P, const void* x, const int* devices, 
     return bar.rc();
   }
   std::copy(result.begin(), result.end(), sums_out);
+  // the one-shot decision check (multisurf_run) on a whole-range call
+  const char* force = std::getenv("FS_Q16");
+  if (q16_used && !P.use_star && r_lo == 0 && r_hi == n && !(force && *force)) {
+    std::vector<double> rs_t, cnt_t;
+    rank_sum(h_rs, rs_t);
+    rank_sum(h_cnt, cnt_t);
+    std::vector<float> s32(nk);
+    for (int64_t k = 0; k < nk; k++) s32[k] = (float)(result[k] / (double)n);
+    Prepared Ps = P;
+    Ps.SC = sc_used;
+    const double risk = q16_decision_risk(Ps, rs_t, cnt_t, s32.data());
+    g_last_risk = risk;
+    if (risk > kQ16MaxRisk) {
+      Prepared P32 = P;
+      P32.no_q16 = 1;
+      FS_TRY(multisurf_run_devices(P32, x, devices, ndev, r_lo, r_hi, sums_out));
+      g_last_risk = risk;
+      g_last_rerun = 1;
+    }
+  }
   return FS_OK;
 }
 

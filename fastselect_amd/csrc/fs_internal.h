@@ -95,6 +95,9 @@ struct Prepared {
   // the wider quantisation error is absorbed by amb_delta (more pairs are
   // recomputed exactly) and the mean correction (k_colrank).
   int q16 = 0;
+  // 1: never 16-bit pass-1 operands (the one-shot MultiSURF re-run after the
+  // decision-risk check, fs_gpu.hip q16_decision_risk)
+  int no_q16 = 0;
 };
 
 // Build the permutation, label codes, discrete tables and integer scale.
@@ -349,6 +352,8 @@ void plan_destroy(Plan* g);
 // by n.  SURF / ReliefF: float64 score sums of the focal samples [r_lo, r_hi)
 // (row sharding; the full range gives the single-GPU result times n).
 int multisurf_run(const Prepared& P, const void* x, int device, float* scores_out);
+// The 16-bit decision check of this thread's last multisurf_run (risk, re-run).
+int multisurf_last_guard(double* risk, int* rerun);
 // One process, several devices (devices[0..ndev), repeats allowed): MultiSURF
 // tile partition / ReliefF and SURF row partition with host-side rank-order
 // sums in place of the all-reduces.  Score sums of [r_lo, r_hi) (not / n).

@@ -133,6 +133,18 @@ FS_API int fs_multisurf_score(int backend, int device, const float* x, int64_t n
                        float* scores_out);
 
 /*
+ * The decision check of this thread's last GPU fs_multisurf_score call
+ * (new; the reference has no quantised pass).  MultiSURF (not MultiSURF*)
+ * scored on 16-bit pass-1 operands estimates how far the near/far decisions
+ * its quantised thresholds could change move the scores, relative to their
+ * largest magnitude (risk_out; -1 when not evaluated: 32-bit operands,
+ * MultiSURF*, FS_Q16 set, CPU backend); above 5e-6 the call scores again on
+ * 32-bit operands and rerun_out is 1.  Signal-free inputs (scores at the
+ * noise floor of the decisions) are what trips it.
+ */
+FS_API int fs_multisurf_last_guard(double* risk_out, int* rerun_out);
+
+/*
  * MultiSURF / MultiSURF* score SUMS (not divided by n) of the focal samples
  * [row_begin, row_end) only, written to sums_out[n_kept] (host memory).
  * The reference's kernel is a prange over focal samples whose rows are
