@@ -94,12 +94,13 @@ def test_lognormal_multisurf_star(F):
 
 @pytest.mark.xfail(strict=False, reason=(
     "open (round 3): lognormal columns (ranges set by a few values ~1e5 x the "
-    "median) give 2.7e-4 of max |s| against the oracle on the 32-bit path the "
-    "calibration picks, and the CPU backend reproduces it (n = 3000, p = 2000: "
-    "6.2e-3), while the oracle's float32 sums are 3e-5 from the float64 ones; "
-    "the largest errors sit on single features, ~1/(n * n_near) each, i.e. "
-    "individual near/far decisions of pairs holding an outlier; not the mean "
-    "correction (FS_MEANCORR=0 gives the same)"))
+    "median) give 2.7e-4 of max |s| against the oracle on the 32-bit path; the "
+    "CPU backend reproduces it (n = 3000, p = 2000: 6.2e-3).  A numpy model of "
+    "that case (same quantisation, reference decisions exact) flips 4 near/far "
+    "decisions with the quantised row means and none with exact ones: the mean "
+    "correction's 4096-bin rank histogram puts nearly all samples of such a "
+    "column in one bin, so its ranks, and the thresholds, stay ~1e-7 off; each "
+    "flip is ~1.5e-3 of these tiny scores.  Needs exact per-column ranks"))
 def test_lognormal_multisurf(F):
     s, ref, _ = _fit(F, "lognormal_16k", False)
     assert_parity(s, ref, 1e-5, 10)
