@@ -279,11 +279,14 @@ __device__ __forceinline__ void col_hist_decode(unsigned long long v, double& cn
   esum = (double)s / kColEpsScale;
 }
 
+template <int REFINE>
 __global__ __launch_bounds__(256) void k_colrank(const uint32_t* __restrict__ xqT, int64_t n,
                                                  int64_t n_pad, int shift, int q16, int64_t c_lo,
                                                  float* __restrict__ epsT) {
   __shared__ unsigned long long hist[kRankBins];
+  __shared__ unsigned long long sub[REFINE ? kRankBins : 1];
   __shared__ unsigned long long wsum[4];
+  __shared__ unsigned int wbest[4];
   const int64_t c = c_lo + blockIdx.x;
   float* e = epsT + c * n_pad;
   for (int b = threadIdx.x; b < kRankBins; b += 256) hist[b] = 0ull;
@@ -296,15 +299,67 @@ __global__ __launch_bounds__(256) void k_colrank(const uint32_t* __restrict__ xq
   const unsigned long long tot = scan_bins_4096(hist, wsum);  // exclusive prefix
   double n_all, e_all;
   col_hist_decode(tot, n_all, e_all);
+  // Opt-in (FS_RANK2=1): the most crowded bin is histogrammed again on the
+  // next 12 key bits, so its samples get refined ranks and eps sums.
+  int bstar = -1, s2 = 0;
+  if (REFINE && shift > 0) {
+    unsigned int best = 0u;  // (count << 12) | bin, max over bins
+    for (int k = 0; k < 16; k++) {
+      const int b = threadIdx.x * 16 + k;
+      const unsigned long long hi = b + 1 < kRankBins ? hist[b + 1] : tot;
+      const unsigned int cnt = (unsigned int)((hi >> kColHistShift) - (hist[b] >> kColHistShift));
+      best = max(best, (min(cnt, 0xFFFFFu) << 12) | (unsigned int)b);
+    }
+    for (int o = 32; o > 0; o >>= 1) best = max(best, (unsigned int)__shfl_xor((int)best, o));
+    if ((threadIdx.x & 63) == 0) wbest[threadIdx.x >> 6] = best;
+    for (int b = threadIdx.x; b < kRankBins; b += 256) sub[b] = 0ull;
+    __syncthreads();
+    best = max(max(wbest[0], wbest[1]), max(wbest[2], wbest[3]));
+    if ((best >> 12) > 1u) {
+      bstar = (int)(best & 0xFFFu);
+      s2 = shift > 12 ? shift - 12 : 0;
+      const uint32_t m = (1u << (shift - s2)) - 1u;
+      for (int64_t i = threadIdx.x; i < n; i += 256) {
+        const uint32_t q = col_q(xqT, c, i, n_pad, q16);
+        if (min((int)(q >> shift), kRankBins - 1) == bstar)
+          atomicAdd(&sub[min((int)((q >> s2) & m), kRankBins - 1)], col_hist_code(e[i]));
+      }
+      __syncthreads();
+      scan_bins_4096(sub, wsum);  // exclusive prefix; uniform branch (best is shared)
+    }
+  }
   for (int64_t i = threadIdx.x; i < n; i += 256) {
-    const int b = min((int)(col_q(xqT, c, i, n_pad, q16) >> shift), kRankBins - 1);
+    const uint32_t q = col_q(xqT, c, i, n_pad, q16);
+    const int b = min((int)(q >> shift), kRankBins - 1);
     double c_lo_, e_lo, c_hi_, e_hi;
     col_hist_decode(hist[b], c_lo_, e_lo);
     col_hist_decode(b + 1 < kRankBins ? hist[b + 1] : tot, c_hi_, e_hi);
+    if (b == bstar) {
+      const int sb = min((int)((q >> s2) & ((1u << (shift - s2)) - 1u)), kRankBins - 1);
+      const unsigned long long s_hi = sb + 1 < kRankBins ? sub[sb + 1] : 0ull;
+      double sc_lo, se_lo, sc_hi, se_hi;
+      col_hist_decode(sub[sb], sc_lo, se_lo);
+      if (sb + 1 < kRankBins && sb + 1 < (1 << (shift - s2))) {
+        col_hist_decode(s_hi, sc_hi, se_hi);
+      } else {  // last sub-bin: its end is the bin's end
+        sc_hi = c_hi_ - c_lo_;
+        se_hi = e_hi - e_lo;
+      }
+      c_hi_ = c_lo_ + sc_hi;
+      e_hi = e_lo + se_hi;
+      c_lo_ += sc_lo;
+      e_lo += se_lo;
+    }
     const double rank = c_lo_ + 0.5 * (c_hi_ - c_lo_ - 1.0);
     const double B = e_lo - (e_all - e_hi);
     e[i] = (float)((double)e[i] * (2.0 * rank - (double)(n - 1)) - B);
   }
+}
+
+// FS_RANK2=1: two-level rank histogram in k_colrank (experiment, default off).
+static int rank2_enabled() {
+  const char* e = std::getenv("FS_RANK2");
+  return e && *e == '1';
 }
 
 // corr[i] = sum over continuous columns [c_lo, c_hi) (this rank's share) of
@@ -4172,7 +4227,11 @@ static int row_guard(Plan* g) {
         g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, 0, Q.pc, g->xqT, g->xs, g->epsT);
   rc = launch_check("k_quantize (row guard)");
   if (!rc) {
-    k_colrank<<<(unsigned)Q.pc, 256, 0, g->stream>>>(g->xqT, Q.n, Q.n_pad, g->rank_shift, Q.q16, 0,
+    if (rank2_enabled())
+      k_colrank<1><<<(unsigned)Q.pc, 256, 0, g->stream>>>(g->xqT, Q.n, Q.n_pad, g->rank_shift, Q.q16, 0,
+                                                     g->epsT);
+    else
+      k_colrank<0><<<(unsigned)Q.pc, 256, 0, g->stream>>>(g->xqT, Q.n, Q.n_pad, g->rank_shift, Q.q16, 0,
                                                      g->epsT);
     rc = launch_check("k_colrank (row guard)");
   }
@@ -4569,8 +4628,12 @@ static int run_quantize_dist(Plan* g) {
       FS_HIP(hipMemsetAsync(g->corr, 0, sizeof(double) * Q.n_pad, cs));
     } else {
       if (g->c_hi > g->c_lo) {
-        k_colrank<<<(unsigned)(g->c_hi - g->c_lo), 256, 0, cs>>>(
-            g->xqT, Q.n, Q.n_pad, g->rank_shift, Q.q16, g->c_lo, g->epsT);
+        if (rank2_enabled())
+          k_colrank<1><<<(unsigned)(g->c_hi - g->c_lo), 256, 0, cs>>>(
+              g->xqT, Q.n, Q.n_pad, g->rank_shift, Q.q16, g->c_lo, g->epsT);
+        else
+          k_colrank<0><<<(unsigned)(g->c_hi - g->c_lo), 256, 0, cs>>>(
+              g->xqT, Q.n, Q.n_pad, g->rank_shift, Q.q16, g->c_lo, g->epsT);
         FS_TRY(launch_check("k_colrank"));
       }
       k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, cs>>>(g->epsT, Q.n, Q.n_pad, g->c_lo,
