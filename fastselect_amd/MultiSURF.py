@@ -38,11 +38,13 @@ class MultiSURF(TransformerMixin, BaseEstimator):
         CPU threads for backend='cpu' (-1 = all).
     verbose : bool, default=False
         Print progress messages.
-    devices : None, int or sequence of int, default=None
+    devices : None, 'all', int or sequence of int, default=None
         GPU ordinals the GPU backend scores on, one host thread each (the
-        pair tiles dealt round-robin, the exchange vectors summed on the
-        host).  None: every visible device the job has work for (one per
-        4096 samples).  Not a reference parameter (the reference is
+        pair tiles dealt round-robin; X crosses the host link once, 1/N of
+        the rows per device and the rest by peer copies; the exchange
+        vectors are summed device-side).  None: device 0, as the reference;
+        'all': every visible device the job has work for (one per 4096
+        samples).  Not a reference parameter (the reference is
         single-device); ignored by backend='cpu'.
     """
 

@@ -46,12 +46,13 @@ class SURF(TransformerMixin, BaseEstimator):
         CPU threads for backend='cpu' (-1 = all).
     verbose : bool, default=False
         Print progress messages.
-    devices : None, int or sequence of int, default=None
+    devices : None, 'all', int or sequence of int, default=None
         GPU ordinals the GPU backend scores on, one host thread each (whole
-        128-sample blocks of the focal samples per thread, the score sums
-        added on the host).  None: every visible device the job has work for
-        (one per 4096 samples).  Not a reference parameter; ignored by
-        backend='cpu'.
+        128-sample blocks of the focal samples per thread, X moved over the
+        host link once and shared by peer copies, the score sums added on
+        the host).  None: device 0, as the reference; 'all': every visible
+        device the job has work for (one per 4096 samples).  Not a reference
+        parameter; ignored by backend='cpu'.
     """
 
     def __init__(

@@ -67,9 +67,12 @@ AUTO_ROWS_PER_DEVICE = 4096
 
 
 def _device_list(devices, count: int):
-    """devices as a list of ordinals, or None when it is not a valid value."""
+    """devices as a list of ordinals, or None when it is not a valid value.
+    None -> [0] (one device, as the reference); 'all' -> every visible one."""
     if devices is None:
-        return list(range(count))
+        return [0] if count > 0 else None
+    if isinstance(devices, str) and devices == "all":
+        return list(range(count)) or None
     def ordinal(d):
         return isinstance(d, (int, np.integer)) and not isinstance(d, (bool, np.bool_))
 
@@ -91,18 +94,20 @@ def fit_devices(devices, backend: str, n_samples: int):
     """The GPU ordinals a fit scores on (SURVEY.md §5 "Config / flags", §8(b)
     "one host thread per device"), or None for backend 'cpu'.
 
-    devices=None: every visible device, as many as the job has work for (one
-    per AUTO_ROWS_PER_DEVICE samples, at least one); an int: that device; a
-    sequence: those ordinals, repeats allowed (several plans share a
-    device).  Raises ValueError for anything else."""
+    devices=None: device 0, as the reference (fanning out by
+    default changed the code path, and the last bits of the scores, with the
+    number of visible GPUs); 'all': every visible device, as many as the job
+    has work for (one per AUTO_ROWS_PER_DEVICE samples, at least one); an
+    int: that device; a sequence: those ordinals, repeats allowed (several
+    plans share a device).  Raises ValueError for anything else."""
     if backend != "gpu":
         return None
     count = _lib.device_count()
     devs = _device_list(devices, count)
     if devs is None:
-        raise ValueError(f"devices must be None, a device ordinal or a non-empty sequence of "
-                         f"ordinals in [0, {count}); got {devices!r}")
-    if devices is None:
+        raise ValueError(f"devices must be None, 'all', a device ordinal or a non-empty "
+                         f"sequence of ordinals in [0, {count}); got {devices!r}")
+    if isinstance(devices, str):
         devs = devs[:max(1, min(len(devs), int(n_samples) // AUTO_ROWS_PER_DEVICE))]
     return devs
 
@@ -118,7 +123,7 @@ def stage_device(backend: str, devices=None, n_samples=None):
     devs = _device_list(devices, _lib.device_count())
     if devs is None:
         return None
-    if devices is None and n_samples is not None:
+    if isinstance(devices, str) and n_samples is not None:
         devs = devs[:max(1, min(len(devs), int(n_samples) // AUTO_ROWS_PER_DEVICE))]
     return devs[0] if len(devs) == 1 else None
 

@@ -21,11 +21,6 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libfastselect_amd.so")
-# A/B experiments only: FS_LIB_VARIANT=<name> loads a variant build of the
-# same sources (tools/build_variant.sh -> _variants/libfastselect_amd_<name>.so)
-if os.environ.get("FS_LIB_VARIANT"):
-    LIB_PATH = os.path.join(_HERE, "_variants",
-                            f"libfastselect_amd_{os.environ['FS_LIB_VARIANT']}.so")
 
 FS_OK, FS_EINVAL, FS_ENODEV, FS_EOOM, FS_EHIP, FS_ENOTSUP = 0, -1, -2, -3, -4, -5
 BACKEND_CPU, BACKEND_GPU = 0, 1
@@ -47,7 +42,7 @@ EXPORTED = (
     "fs_column_stats", "fs_multisurf_score", "fs_multisurf_last_guard", "fs_multisurf_score_rows",
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
-    "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_set_rows",
+    "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_decision_guard", "fs_plan_set_rows",
     "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs", "fs_plan_kernel_ms",
     "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
     "fs_surf_score_devices",
@@ -134,6 +129,8 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_pass1.argtypes = [_vp, _vp]
     lib.fs_plan_select.argtypes = [_vp, _vp, _vp]
     lib.fs_plan_pass2.argtypes = [_vp, _vp, _vp]
+    lib.fs_plan_decision_guard.argtypes = [_vp, _vp, _vp, _vp, ctypes.POINTER(ctypes.c_double),
+                                           ctypes.POINTER(_int)]
     lib.fs_plan_info.argtypes = [_vp, _i64p, _f64p, _i64p]
     lib.fs_plan_calibration.argtypes = [_vp, _f64p]
     lib.fs_plan_set_shard.argtypes = [_vp, _int, _int]
@@ -146,7 +143,7 @@ def _load() -> ctypes.CDLL:
                  "fs_plan_set_rows", "fs_relieff_score", "fs_surf_score",
                  "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create",
                  "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
-                 "fs_plan_pass2", "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs",
+                 "fs_plan_pass2", "fs_plan_decision_guard", "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs",
                  "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
                  "fs_surf_score_devices"):
         getattr(lib, name).restype = _int
@@ -519,6 +516,16 @@ class Plan:
     def pass2(self, counts_ptr: int, scores_ptr: int) -> None:
         check(_lib.fs_plan_pass2(self._h, _vp(counts_ptr), _vp(scores_ptr)))
 
+    def decision_guard(self, rowstats_ptr: int, counts_ptr: int, scores_ptr: int):
+        """(risk, switched) of the 16-bit decision check after a step whose
+        exchange vectors are all-reduced (``fs_plan_decision_guard``);
+        switched: the plan now runs on 32-bit operands -- run the step again."""
+        risk = ctypes.c_double(-1.0)
+        sw = _int(0)
+        check(_lib.fs_plan_decision_guard(self._h, _vp(rowstats_ptr), _vp(counts_ptr),
+                                          _vp(scores_ptr), ctypes.byref(risk), ctypes.byref(sw)))
+        return float(risk.value), bool(sw.value)
+
     def set_rows(self, begin: int, end: int) -> None:
         """Score only the focal samples [begin, end) in the next pass2
         (``fs_plan_set_rows``; MultiSURF plans)."""
@@ -539,10 +546,11 @@ class Plan:
 
     def calibration(self) -> dict:
         """Refinement-band calibration of the current layout (fs_plan_calibration)."""
-        v = (ctypes.c_double * 6)()
+        v = (ctypes.c_double * 8)()
         check(_lib.fs_plan_calibration(self._h, v))
         return {"q16": bool(v[0]), "rms": v[1], "max": v[2], "model_sigma": v[3],
-                "band_vs_model": v[4], "guard": bool(v[5]), "row_guard": v[5] == 2.0}
+                "band_vs_model": v[4], "guard": bool(v[5]), "row_guard": v[5] == 2.0,
+                "row_bias_vs_limit": v[6], "SC": v[7]}
 
     def weighted_pairs(self) -> int:
         """Owned pairs with a non-zero weight in the last pass 2 (-1: not counted)."""

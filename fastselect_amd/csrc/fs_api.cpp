@@ -652,6 +652,20 @@ int fs_plan_pass2(fs_plan* pl, const double* counts, double* scores) {
                               pl->r_hi, scores);
 }
 
+int fs_plan_decision_guard(fs_plan* pl, const double* rowstats, const double* counts,
+                           const double* scores, double* risk_out, int* switched_out) {
+  if (!pl || !rowstats || !counts || !scores || !risk_out || !switched_out) {
+    set_error("NULL plan or buffer");
+    return FS_EINVAL;
+  }
+  if (!is_multisurf_plan(pl)) return FS_EINVAL;
+  *risk_out = -1.0;
+  *switched_out = 0;
+  // the CPU backend always runs pass 1 on 32-bit operands
+  if (!pl->g) return FS_OK;
+  return gpu::plan_decision_guard(pl->g, rowstats, counts, scores, risk_out, switched_out);
+}
+
 int fs_plan_set_rows(fs_plan* pl, int64_t row_begin, int64_t row_end) {
   if (!pl) {
     set_error("plan is NULL");
@@ -726,8 +740,9 @@ int fs_plan_calibration(const fs_plan* pl, double* out) {
     return FS_EINVAL;
   }
   if (pl->g) return gpu::plan_calibration(pl->g, out);
-  const double v[6] = {0.0, 0.0, 0.0, std::sqrt((double)pl->P.pc / 6.0 + 1.0), 1.0, 0.0};
-  for (int k = 0; k < 6; k++) out[k] = v[k];
+  const double v[8] = {0.0, 0.0, 0.0, std::sqrt((double)pl->P.pc / 6.0 + 1.0), 1.0, 0.0, 0.0,
+                       pl->P.SC};
+  for (int k = 0; k < 8; k++) out[k] = v[k];
   return FS_OK;
 }
 

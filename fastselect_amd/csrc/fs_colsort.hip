@@ -1,0 +1,293 @@
+// fs_colsort.hip -- exact per-column ranks for MultiSURF's mean correction.
+//
+// MultiSURF's threshold is mu_i - sigma_i / 2 with mu_i the mean of row i's
+// distances, summed in float64 from float32 diffs (MultiSURF.py:177-196).
+// Pass 1 computes quantised distances D_q; their row sum is off from the
+// reference's by the per-column terms
+//   corr_if = sum_j sign(t_if - t_jf) (eps_if - eps_jf)
+// (t = (x - min) * recip * SC, q = round(t), eps = q - t; fs_gpu.hip,
+// k_quantize).  With the column ordered by t (position k of sample i, prefix
+// sum P_k of eps over the samples before it, total T):
+//   corr_if = eps_i (2k - n) - 2 P_k + T.
+// Round 3 took the order from a 4096-bin histogram and treated samples that
+// share a bin as tied; a column whose range is set by a few extreme values
+// (lognormal data) puts nearly every sample in one bin and the thresholds
+// moved (VERDICT r3 missing #1).  Here every continuous column is sorted
+// exactly:
+//
+//   key = (q << s) | floor((1/2 - eps) * 2^s)     (32 bits, s = 32 - bits(q))
+//
+// is monotone in t (within one q a larger t has a smaller eps) and resolves
+// t to 2^-s quanta; samples with equal keys are ordered by index (stable
+// sorts), which errs by at most 2^(1-s) quanta per such pair -- 2^-7 of a
+// quantum on 32-bit operands, 2^-15 on 16-bit ones, and only between samples
+// whose t agree to that resolution.  The eps sums are exact integers (fixed
+// point 2^24, as round 3), so the CPU backend (fs_cpu.cpp mean_correction,
+// std::sort on (key, index)) gives bit-identical terms.
+//
+// Two routes:
+//   n <= 24576  k_colsort<IPT>: one 1024-thread workgroup per column, the
+//               column's (key, 16-bit index) pairs sorted in LDS by rocPRIM's
+//               block radix sort (stable, 8-bit digits: 4 passes), one block
+//               scan of the fixed-point eps, terms written in place.
+//   larger n    keys built per batch of columns, rocPRIM's device segmented
+//               radix sort (stable), then k_colsort_scan: one workgroup per
+//               column walks the sorted order in chunks with a running prefix.
+#include <hip/hip_runtime.h>
+
+#include <rocprim/block/block_radix_sort.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
+
+#include "fs_internal.h"
+
+namespace fs {
+namespace gpu {
+
+namespace {
+
+constexpr double kEpsFx = 16777216.0;  // eps fixed point 2^24 (|eps| <= 1/2 -> |fx| <= 2^23)
+constexpr int kCsThreads = 1024;
+constexpr int kCsMaxIpt = 24;          // LDS route up to 24576 samples
+
+__device__ __forceinline__ uint32_t cs_col_q(const uint32_t* __restrict__ xqT, int64_t c,
+                                             int64_t i, int64_t n_pad, int q16) {
+  return q16 ? (xqT[(c >> 1) * n_pad + i] >> ((c & 1) * 16)) & 0xFFFFu : xqT[c * n_pad + i];
+}
+
+// colsort_key (fs_internal.h) on the device: same IEEE operations
+__device__ __forceinline__ uint32_t cs_key(uint32_t q, float eps, int s) {
+  const double sc = (double)(1u << s);
+  const double f = floor((0.5 - (double)eps) * sc);
+  const double m = sc - 1.0;
+  const uint32_t fr = (uint32_t)(f < 0.0 ? 0.0 : (f > m ? m : f));
+  return (q << s) | fr;
+}
+
+__device__ __forceinline__ long long cs_fx(float eps) {
+  return __double2ll_rn((double)eps * kEpsFx);
+}
+
+__device__ __forceinline__ float cs_term(long long e, long long pos, long long n, long long P,
+                                         long long T) {
+  return (float)((double)(e * (2 * pos - n) - 2 * P + T) / kEpsFx);
+}
+
+// Exclusive scan of one int64 per thread over a 1024-thread workgroup
+// (wave shuffles, 16 wave totals in LDS); returns the prefix, sets total.
+__device__ __forceinline__ long long cs_block_scan(long long v, long long* wsum,
+                                                   long long& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  long long x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const long long t = __shfl_up(x, o);
+    if (lane >= o) x += t;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  long long pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kCsThreads / 64; w++) {
+    const long long s = wsum[w];
+    pre += w < wave ? s : 0;
+    tot += s;
+  }
+  __syncthreads();  // wsum is reused by the next call
+  total = tot;
+  return pre + x - v;
+}
+
+template <int IPT>
+__global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restrict__ xqT,
+                                                        int64_t n, int64_t n_pad, int s, int q16,
+                                                        int64_t c_lo, float* __restrict__ epsT) {
+  using Sort = rocprim::block_radix_sort<uint32_t, kCsThreads, IPT, uint16_t>;
+  __shared__ typename Sort::storage_type st;
+  __shared__ long long wsum[kCsThreads / 64];
+  const int64_t c = c_lo + blockIdx.x;
+  float* __restrict__ e = epsT + c * n_pad;
+  const int base = threadIdx.x * IPT;
+  uint32_t key[IPT];
+  uint16_t idx[IPT];
+#pragma unroll
+  for (int k = 0; k < IPT; k++) {
+    const int i = base + k;
+    // padding sorts last: its keys are the largest and its indices follow
+    // every sample's (stable)
+    key[k] = i < n ? cs_key(cs_col_q(xqT, c, i, n_pad, q16), e[i], s) : 0xFFFFFFFFu;
+    idx[k] = (uint16_t)i;
+  }
+  Sort().sort(key, idx, st);
+  long long ef[IPT], loc = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; k++) {
+    ef[k] = base + k < n ? cs_fx(e[idx[k]]) : 0;
+    loc += ef[k];
+  }
+  long long T;
+  long long P = cs_block_scan(loc, wsum, T);
+  // each sample's eps is read and its term written by the same thread
+#pragma unroll
+  for (int k = 0; k < IPT; k++) {
+    const int pos = base + k;
+    if (pos < n) e[idx[k]] = cs_term(ef[k], pos, n, P, T);
+    P += ef[k];
+  }
+}
+
+// Large-n route, step 1: keys and indices of columns [c0, c0 + nc).
+__global__ __launch_bounds__(256) void k_colsort_keys(const uint32_t* __restrict__ xqT, int64_t n,
+                                                      int64_t n_pad, int s, int q16, int64_t c0,
+                                                      const float* __restrict__ epsT,
+                                                      uint32_t* __restrict__ keys,
+                                                      uint32_t* __restrict__ vals) {
+  const int64_t cc = blockIdx.y;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int64_t c = c0 + cc;
+  keys[cc * n + i] = cs_key(cs_col_q(xqT, c, i, n_pad, q16), epsT[c * n_pad + i], s);
+  vals[cc * n + i] = (uint32_t)i;
+}
+
+// Large-n route, step 3: one workgroup per column walks the sorted indices
+// in chunks of 1024 x 8 with a running prefix (the column total first).
+constexpr int kScanIpt = 8;
+__global__ __launch_bounds__(kCsThreads) void k_colsort_scan(const uint32_t* __restrict__ vals,
+                                                             int64_t n, int64_t n_pad, int64_t c0,
+                                                             float* __restrict__ epsT) {
+  __shared__ long long wsum[kCsThreads / 64];
+  const int64_t cc = blockIdx.x;
+  float* __restrict__ e = epsT + (c0 + cc) * n_pad;
+  const uint32_t* __restrict__ v = vals + cc * n;
+  long long loc = 0;
+  for (int64_t i = threadIdx.x; i < n; i += kCsThreads) loc += cs_fx(e[i]);
+  long long T;
+  (void)cs_block_scan(loc, wsum, T);
+  long long carry = 0;
+  for (int64_t b = 0; b < n; b += (int64_t)kCsThreads * kScanIpt) {
+    const int64_t base = b + (int64_t)threadIdx.x * kScanIpt;
+    uint32_t id[kScanIpt];
+    long long ef[kScanIpt], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kScanIpt; k++) {
+      const bool in = base + k < n;
+      id[k] = in ? v[base + k] : 0u;
+      ef[k] = in ? cs_fx(e[id[k]]) : 0;
+      sum += ef[k];
+    }
+    long long chunk;
+    long long P = carry + cs_block_scan(sum, wsum, chunk);
+#pragma unroll
+    for (int k = 0; k < kScanIpt; k++) {
+      if (base + k < n) e[id[k]] = cs_term(ef[k], base + k, n, P, T);
+      P += ef[k];
+    }
+    carry += chunk;
+  }
+}
+
+__global__ void k_colsort_offsets(int64_t n, int64_t nc, unsigned* __restrict__ off) {
+  const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k <= nc) off[k] = (unsigned)(k * n);
+}
+
+// columns per batch of the large-n route: keys + indices double-buffered
+// (16 B per sample) within ~512 MB, at most 4096 columns
+int64_t batch_cols(int64_t n, int64_t ncols) {
+  int64_t b = std::max<int64_t>(1, ((int64_t)512 << 20) / (16 * std::max<int64_t>(n, 1)));
+  b = std::min<int64_t>(b, 4096);
+  return std::min<int64_t>(b, std::max<int64_t>(ncols, 1));
+}
+
+size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// bytes of the batch buffers in front of rocPRIM's temporary storage
+size_t batch_bytes(int64_t n, int64_t nb) {
+  return 4 * align256(sizeof(uint32_t) * (size_t)(n * nb)) + align256(sizeof(unsigned) * (nb + 1));
+}
+
+}  // namespace
+
+bool colsort_lds(int64_t n) { return n <= (int64_t)kCsThreads * kCsMaxIpt; }
+
+size_t colsort_scratch_bytes(int64_t n, int64_t ncols) {
+  if (colsort_lds(n) || ncols <= 0) return 0;
+  const int64_t nb = batch_cols(n, ncols);
+  if ((unsigned long long)n * nb >= (1ull << 32)) return 0;
+  size_t temp = 0;
+  uint32_t* nk = nullptr;
+  unsigned* no = nullptr;
+  if (rocprim::segmented_radix_sort_pairs(nullptr, temp, nk, nk, nk, nk, (unsigned)(n * nb),
+                                          (unsigned)nb, no, no + 1, 0, 32) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return batch_bytes(n, nb) + align256(temp);
+}
+
+int colsort_terms(const uint32_t* xqT, float* epsT, int64_t n, int64_t n_pad, int64_t c_lo,
+                  int64_t c_hi, int q16, int key_shift, void* scratch, size_t scratch_bytes,
+                  void* stream_v) {
+  hipStream_t stream = (hipStream_t)stream_v;
+  const int64_t nc = c_hi - c_lo;
+  if (nc <= 0 || n < 1) return 0;
+  if (colsort_lds(n)) {
+    const unsigned grid = (unsigned)nc;
+#define FS_COLSORT(IPT)                                                                    \
+  k_colsort<IPT><<<grid, kCsThreads, 0, stream>>>(xqT, n, n_pad, key_shift, q16, c_lo, epsT)
+    const int64_t ipt = (n + kCsThreads - 1) / kCsThreads;
+    if (ipt <= 4) FS_COLSORT(4);
+    else if (ipt <= 8) FS_COLSORT(8);
+    else if (ipt <= 12) FS_COLSORT(12);
+    else if (ipt <= 16) FS_COLSORT(16);
+    else if (ipt <= 20) FS_COLSORT(20);
+    else FS_COLSORT(24);
+#undef FS_COLSORT
+    if (hipGetLastError() != hipSuccess) {
+      set_error("k_colsort: launch failed");
+      return -1;
+    }
+    return 0;
+  }
+  const int64_t nb = batch_cols(n, nc);
+  const size_t need = colsort_scratch_bytes(n, nc);
+  if (need == 0 || scratch_bytes < need || !scratch) {
+    set_error("k_colsort: scratch too small for the large-n route");
+    return -1;
+  }
+  char* p = (char*)scratch;
+  const size_t kb = align256(sizeof(uint32_t) * (size_t)(n * nb));
+  uint32_t* k_in = (uint32_t*)p;
+  uint32_t* k_out = (uint32_t*)(p + kb);
+  uint32_t* v_in = (uint32_t*)(p + 2 * kb);
+  uint32_t* v_out = (uint32_t*)(p + 3 * kb);
+  unsigned* off = (unsigned*)(p + 4 * kb);
+  void* temp = p + batch_bytes(n, nb);
+  size_t temp_bytes = scratch_bytes - batch_bytes(n, nb);
+  for (int64_t c0 = c_lo; c0 < c_hi; c0 += nb) {
+    const int64_t m = std::min<int64_t>(nb, c_hi - c0);
+    k_colsort_offsets<<<(unsigned)((m + 256) / 256), 256, 0, stream>>>(n, m, off);
+    k_colsort_keys<<<dim3((unsigned)((n + 255) / 256), (unsigned)m), 256, 0, stream>>>(
+        xqT, n, n_pad, key_shift, q16, c0, epsT, k_in, v_in);
+    if (hipGetLastError() != hipSuccess) {
+      set_error("k_colsort_keys: launch failed");
+      return -1;
+    }
+    if (rocprim::segmented_radix_sort_pairs(temp, temp_bytes, k_in, k_out, v_in, v_out,
+                                            (unsigned)(n * m), (unsigned)m, off, off + 1, 0, 32,
+                                            stream) != hipSuccess) {
+      (void)hipGetLastError();
+      set_error("k_colsort: segmented radix sort failed");
+      return -1;
+    }
+    k_colsort_scan<<<(unsigned)m, kCsThreads, 0, stream>>>(v_out, n, n_pad, c0, epsT);
+    if (hipGetLastError() != hipSuccess) {
+      set_error("k_colsort_scan: launch failed");
+      return -1;
+    }
+  }
+  return 0;
+}
+
+}  // namespace gpu
+}  // namespace fs

@@ -163,39 +163,37 @@ static void distances(const Prepared& P, const std::vector<uint32_t>& xq, int ra
   });
 }
 
-// Mean correction of k_colrank / k_rowcorr: per continuous column a
-// 4096-bin histogram of q (counts and fixed-point eps sums) gives
-// corr[i] = sum_c eps_i (2 rank_i - (n-1)) - (sum_{below} eps - sum_{above} eps).
-// The correction of the continuous columns [c_lo, c_hi) (a rank's share;
-// the shares are summed across ranks with the row moments).
+// Mean correction of k_colsort / k_rowcorr (fs_colsort.hip): every
+// continuous column ordered exactly by t (colsort_key, ties by index, as the
+// GPU's stable sorts), then with position k, the eps prefix P before it and
+// the column total T (fixed point 2^24, exact integers):
+//   term_i = eps_i (2k - n) - 2 P + T,   corr[i] = sum_c term_ic,
+// bit-identical terms to the GPU's.  The correction of the continuous
+// columns [c_lo, c_hi) (a rank's share; the shares are summed across ranks
+// with the row moments).
 static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
                             const std::vector<float>& eps, int64_t c_lo, int64_t c_hi,
                             int n_jobs, std::vector<double>& corr) {
   const int64_t n = P.n;
-  constexpr int kBins = 4096;
-  int shift = 0;
-  while (P.qmax / std::ldexp(1.0, shift) >= (double)kBins) shift++;
+  const int s = colsort_key_shift(P.qmax);
   std::vector<float> term((size_t)n * std::max<int64_t>(P.pc, 1), 0.0f);
   parallel_for(c_hi - c_lo, n_jobs, [&](int64_t cc) {
     const int64_t c = c_lo + cc;
-    constexpr double kFx = 16777216.0;  // eps fixed point 2^24, as k_colrank
-    std::vector<uint32_t> cum(kBins + 1, 0);
-    std::vector<int64_t> ecum(kBins + 1, 0);
+    constexpr double kFx = 16777216.0;  // eps fixed point 2^24, as k_colsort
+    std::vector<uint64_t> ord((size_t)n);
+    int64_t T = 0;
     for (int64_t i = 0; i < n; i++) {
-      const int64_t b = std::min<int64_t>(xq[(size_t)i * P.PW + c] >> shift, kBins - 1);
-      cum[b + 1]++;
-      ecum[b + 1] += (int64_t)std::llrint((double)eps[(size_t)i * P.PW + c] * kFx);
+      const float e = eps[(size_t)i * P.PW + c];
+      ord[i] = ((uint64_t)colsort_key(xq[(size_t)i * P.PW + c], e, s) << 32) | (uint64_t)i;
+      T += (int64_t)std::llrint((double)e * kFx);
     }
-    for (int b = 0; b < kBins; b++) {
-      cum[b + 1] += cum[b];
-      ecum[b + 1] += ecum[b];
-    }
-    for (int64_t i = 0; i < n; i++) {
-      const int64_t b = std::min<int64_t>(xq[(size_t)i * P.PW + c] >> shift, kBins - 1);
-      const double rank = (double)cum[b] + 0.5 * (double)(cum[b + 1] - cum[b] - 1u);
-      const double B = (double)(ecum[b] - (ecum[kBins] - ecum[b + 1])) / kFx;
-      term[(size_t)i * P.pc + c] =
-          (float)((double)eps[(size_t)i * P.PW + c] * (2.0 * rank - (double)(n - 1)) - B);
+    std::sort(ord.begin(), ord.end());
+    int64_t Pk = 0;
+    for (int64_t k = 0; k < n; k++) {
+      const int64_t i = (int64_t)(ord[k] & 0xFFFFFFFFull);
+      const int64_t e = (int64_t)std::llrint((double)eps[(size_t)i * P.PW + c] * kFx);
+      term[(size_t)i * P.pc + c] = (float)((double)(e * (2 * k - n) - 2 * Pk + T) / kFx);
+      Pk += e;
     }
   });
   corr.assign(n, 0.0);
@@ -260,14 +258,8 @@ int multisurf_pass1(const Prepared& P, const void* x, int rank, int world, int n
                     CpuState& S, double* rowstats) {
   std::vector<uint32_t> xq;
   std::vector<float> eps;
-  // FS_MEANCORR=0 drops the mean correction, as on the GPU (A/B only)
-  const char* mc = std::getenv("FS_MEANCORR");
-  const bool mean_corr = !(mc && *mc && std::atoi(mc) == 0);
-  quantize(P, x, 0, n_jobs, xq, S.xs, mean_corr ? &eps : nullptr);
-  if (mean_corr)
-    mean_correction(P, xq, eps, P.pc * rank / world, P.pc * (rank + 1) / world, n_jobs, S.corr);
-  else
-    S.corr.assign(P.n, 0.0);
+  quantize(P, x, 0, n_jobs, xq, S.xs, &eps);
+  mean_correction(P, xq, eps, P.pc * rank / world, P.pc * (rank + 1) / world, n_jobs, S.corr);
   distances(P, xq, rank, world, n_jobs, S.D);
   const int64_t n = P.n, nb = P.n_pad / kTile;
   parallel_for(n, n_jobs, [&](int64_t i) {

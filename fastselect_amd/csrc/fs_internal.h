@@ -18,6 +18,7 @@
 // problem so that the pass-1 accumulators cannot overflow; see choose_scale).
 #pragma once
 
+#include <cmath>
 #include <cstdint>
 #include <string>
 #include <utility>
@@ -125,6 +126,23 @@ constexpr int64_t kCalibPairs = 4096;
 void calib_pairs(int64_t n, int64_t pc, int64_t count,
                  std::vector<std::pair<int64_t, int64_t>>& out);
 double calibrated_delta(double model, double SC, double rms, double max_abs);
+// Sort key of a quantised continuous value for the exact per-column order
+// of MultiSURF's mean correction (fs_colsort.hip, fs_cpu.cpp
+// mean_correction): (q << s) | floor((1/2 - eps) * 2^s), monotone in
+// t = q - eps; s = 32 - bits(qmax - 1), at most 24.  The device copy
+// (fs_colsort.hip cs_key) performs the same IEEE operations.
+inline int colsort_key_shift(double qmax) {
+  int b = 0;
+  while (b < 32 && std::ldexp(1.0, b) < qmax) b++;
+  return 32 - b < 24 ? 32 - b : 24;
+}
+inline uint32_t colsort_key(uint32_t q, float eps, int s) {
+  const double sc = (double)(1u << s);
+  const double f = std::floor((0.5 - (double)eps) * sc);
+  const double m = sc - 1.0;
+  const uint32_t fr = (uint32_t)(f < 0.0 ? 0.0 : (f > m ? m : f));
+  return (q << s) | fr;
+}
 int encode_labels_f64(Prepared& P, const double* y);
 int encode_labels_i32(Prepared& P, const int32_t* y);
 
@@ -314,6 +332,17 @@ int column_minmax(const void* dx, int x_is_f64, int64_t n, int64_t p, void* hmin
 // a hipStream_t.
 size_t pair_sort_scratch_bytes(int64_t count);
 int sort_pairs(void* list, int64_t count, void* scratch, size_t scratch_bytes, void* stream);
+// MultiSURF mean-correction terms of the continuous columns [c_lo, c_hi)
+// from exact per-column order (fs_colsort.hip; colsort_key): epsT[c][i]
+// (quantisation errors, from k_quantize) is overwritten with
+// eps_i (2 k_i - n) - 2 P_i + T.  Columns of n <= 24576 samples sort in LDS
+// (no scratch); larger n needs colsort_scratch_bytes(n, c_hi - c_lo) bytes
+// of device memory.  `stream` is a hipStream_t.
+bool colsort_lds(int64_t n);
+size_t colsort_scratch_bytes(int64_t n, int64_t ncols);
+int colsort_terms(const uint32_t* xqT, float* epsT, int64_t n, int64_t n_pad, int64_t c_lo,
+                  int64_t c_hi, int q16, int key_shift, void* scratch, size_t scratch_bytes,
+                  void* stream);
 struct Plan;
 // Tile sharding (MultiSURF): tile t belongs to rank t % world.  Row
 // sharding (r_hi >= 0): the tiles touching the 128-row blocks of [r_lo, r_hi).
@@ -325,6 +354,11 @@ int plan_set_features(Plan* g, const Prepared& P);
 int plan_pass1(Plan* g, double* rowstats_dev);
 int plan_select(Plan* g, const double* rowstats_dev, double* counts_dev);
 int plan_pass2(Plan* g, const double* counts_dev, double* scores_dev);
+// After a step on 16-bit operands: decision risk from the step's summed
+// exchange vectors (device memory); above the bound the plan switches to
+// 32-bit operands and *switched = 1 (run the step again).  risk = -1: no check.
+int plan_decision_guard(Plan* g, const double* rowstats, const double* counts,
+                        const double* sums, double* risk, int* switched);
 // MultiSURF focal-sample slice: the next pass2 sums the pair sides of the
 // focal samples [r_lo, r_hi) only (thresholds and counts stay global).
 int plan_set_rows(Plan* g, int64_t r_lo, int64_t r_hi);
@@ -333,8 +367,9 @@ int plan_set_rows(Plan* g, int64_t r_lo, int64_t r_hi);
 // new ones.  X and its quantised operands stay resident.
 int plan_set_shard(Plan* g, int rank, int world);
 // Tile shards per device for a MultiSURF job of `world` ranks so that the
-// tile buffers fit the device (1 = no sharding; FS_SHARDS forces it).
-int multisurf_shards(const Prepared& P, int device, int world);
+// tile buffers fit the device (1 = no sharding; FS_SHARDS forces it); with
+// share > 1 that many plans split the device's memory (repeated ordinals).
+int multisurf_shards(const Prepared& P, int device, int world, int share = 1);
 // ReliefF / SURF plans: float64 score sums of the plan's focal rows
 // (sums_dev[n_kept], device memory), for the plan's current feature subset.
 int plan_score(Plan* g, double* sums_dev);

@@ -250,8 +250,7 @@ class ShardedMultiSURF:
         self._allreduce(self.scores)
         return (self.scores / self.n).float()
 
-    def step(self):
-        """One full scoring pass; returns float32 scores (device tensor)."""
+    def _step_once(self):
         if self.shards > 1:
             return self._step_shards()
         self.plan.pass1(self.rowstats.data_ptr())
@@ -261,6 +260,23 @@ class ShardedMultiSURF:
         self.plan.pass2(self.counts.data_ptr(), self.scores.data_ptr())
         self._allreduce(self.scores)
         return (self.scores / self.n).float()
+
+    def step(self):
+        """One full scoring pass; returns float32 scores (device tensor).
+
+        With 16-bit pass-1 operands the step ends with the decision check of
+        the one-shot call (``fs_plan_decision_guard`` on the all-reduced
+        vectors, so every rank decides alike): above its bound the plan moves
+        to 32-bit operands for good and the step runs again.  ``last_guard``
+        holds (risk, re-run) of the last step."""
+        s = self._step_once()
+        risk, switched = self.plan.decision_guard(self.rowstats.data_ptr(),
+                                                  self.counts.data_ptr(),
+                                                  self.scores.data_ptr())
+        if switched:
+            s = self._step_once()
+        self.last_guard = (risk, switched)
+        return s
 
     def info(self):
         return self.plan.info()

@@ -304,6 +304,18 @@ FS_API int fs_plan_select(fs_plan* plan, const double* rowstats, double* counts)
 /* Stage 3: pair weights from the all-reduced counts[2n]; partial per-feature
  * score sums (NOT divided by n) -> scores[n_kept], in feat_idx order. */
 FS_API int fs_plan_pass2(fs_plan* plan, const double* counts, double* scores);
+/* After the three stages of a MultiSURF step, with rowstats[3n], counts[2n]
+ * and scores[n_kept] all-reduced (identical on every rank): the 16-bit
+ * decision check of fs_multisurf_score (see fs_multisurf_last_guard) for
+ * plans whose pass 1 runs on 16-bit operands.  risk_out = the estimated score
+ * error of threshold-moved decisions over max |score| (-1: nothing to check:
+ * 32-bit operands, MultiSURF*, the CPU backend).  Above the bound the plan
+ * switches to 32-bit operands for good and *switched_out = 1: every rank
+ * computed the same risk and switched alike, and the caller runs the step
+ * again (the reference's single threshold rule, MultiSURF.py:193-217, and
+ * TuRF's refits, TuRF.py:87,111, through the same plan). */
+FS_API int fs_plan_decision_guard(fs_plan* plan, const double* rowstats, const double* counts,
+                                  const double* scores, double* risk_out, int* switched_out);
 /* Restrict the next pass2 of a MultiSURF plan to the focal samples
  * [row_begin, row_end) (as fs_multisurf_score_rows; a new plan scores
  * [0, n)).  pass1 / select are unchanged: thresholds and counts are global. */
@@ -354,14 +366,17 @@ FS_API int fs_plan_info(const fs_plan* plan, int64_t* owned_tiles, double* pair_
 /* Refinement-band calibration of the plan's current feature layout (GPU
  * MultiSURF / ReliefF plans; no reference counterpart -- it guards the
  * integer pass 1 that replaces the reference's float distance loop,
- * MultiSURF.py:176-188).  out[6]: [0] 1 if pass 1 runs on 16-bit operands,
+ * MultiSURF.py:176-188).  out[8]: [0] 1 if pass 1 runs on 16-bit operands,
  * [1] / [2] rms / max |quantised - reference| distance error over 4096
  * sampled pairs (integer units), [3] the independent-rounding model's
  * standard deviation sqrt(pc/6 + 1), [4] band / model band, [5] 1 if the
  * coherence guard turned 16-bit operands off, 2 if the per-row guard did (a
  * row whose mean pass-1 error, measured by the mean correction, exceeds 12
- * standard deviations of independent rounding).  CPU plans: out[0..5] =
- * {0, 0, 0, model sigma, 1, 0}. */
+ * standard deviations of independent rounding), [6] that row guard's largest
+ * row bias over its limit (0 when it did not run), [7] SC, the integer units
+ * per scaled-diff unit of pass 1 (the row statistics of fs_plan_pass1 are in
+ * these units: mu_i = (rowstats[3i] - rowstats[3i+2]) / (n - 1) / SC).  CPU
+ * plans: out[0..7] = {0, 0, 0, model sigma, 1, 0, 0, SC}. */
 FS_API int fs_plan_calibration(const fs_plan* plan, double* out);
 /* Owned pairs that carried a non-zero pass-2 weight in the last pass 2 (the
  * pairs the sparse GPU pass 2 evaluates; -1 when the plan does not count

@@ -60,6 +60,9 @@ def _load():
     lib.oracle_relieff_acc.argtypes = lib.oracle_relieff.argtypes[:-1] + [ctypes.c_int, _f32p]
     lib.oracle_surf_acc.argtypes = lib.oracle_surf.argtypes[:-1] + [ctypes.c_int, _f32p]
     lib.numba_argsort_f32.argtypes = [_f32p, _i64, _i64p]
+    lib.oracle_multisurf_decisions.argtypes = [_f32p, _i64, _i64, _f64p, _f32p, _i64p, _i64, _u8p,
+                                               _i64, _i64, ctypes.c_int, _f64p, _i64p]
+    lib.oracle_multisurf_decisions.restype = ctypes.c_int
     lib.oracle_max_threads.restype = ctypes.c_int
     for fn in (lib.oracle_multisurf, lib.oracle_relieff, lib.oracle_surf, lib.oracle_multisurf_acc,
                lib.oracle_relieff_acc, lib.oracle_surf_acc):
@@ -111,6 +114,31 @@ def multisurf_scores(X, y, use_star=False, discrete_limit=10, i_range=None, n_jo
     if rc != 0:
         raise RuntimeError(f"oracle_multisurf failed: {rc}")
     return out
+
+
+def multisurf_decisions(X, y, discrete_limit=10, i_range=None, n_jobs=-1, feat_idx=None):
+    """(thresholds float64[m], counts int64[m, 2]) of MultiSURF.py:175-217 for
+    the focal samples i_range (default all): mu - sigma/2 and the near hit /
+    near miss counts in the reference's arithmetic (parity attribution: a
+    score difference is flipped decisions or accumulation)."""
+    x = np.ascontiguousarray(X, dtype=np.float32)
+    yv = np.ascontiguousarray(np.asarray(y), dtype=np.float64)
+    n, p = x.shape
+    ranges = (x.max(axis=0) - x.min(axis=0)).astype(np.float32)
+    ranges[ranges == 0] = 1
+    recip = np.ascontiguousarray((1.0 / ranges).astype(np.float32))
+    is_disc = np.ascontiguousarray(is_discrete_mask(x, discrete_limit).astype(np.uint8))
+    fidx = np.arange(p, dtype=np.int64) if feat_idx is None else np.ascontiguousarray(feat_idx, dtype=np.int64)
+    i0, i1 = (0, n) if i_range is None else i_range
+    thr = np.zeros(i1 - i0, dtype=np.float64)
+    cnt = np.zeros((i1 - i0, 2), dtype=np.int64)
+    rc = _load().oracle_multisurf_decisions(_ptr(x, _f32p), n, p, _ptr(yv, _f64p),
+                                            _ptr(recip, _f32p), _ptr(fidx, _i64p), fidx.size,
+                                            _ptr(is_disc, _u8p), i0, i1, int(n_jobs),
+                                            _ptr(thr, _f64p), _ptr(cnt, _i64p))
+    if rc != 0:
+        raise RuntimeError(f"oracle_multisurf_decisions failed: {rc}")
+    return thr, cnt
 
 
 def relieff_scores(X, y, n_neighbors=3, discrete_limit=10, i_range=None, n_jobs=-1, accum="f32"):

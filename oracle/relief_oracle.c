@@ -177,6 +177,56 @@ ORACLE_API int oracle_multisurf_acc(const float* x, int64_t n, int64_t p, const 
   return 0;
 }
 
+/* The near/far decisions of MultiSURF.py:175-217 alone (parity attribution:
+ * a score difference is either flipped decisions or accumulation): per focal
+ * sample i in [i_begin, i_end) the threshold mu - sigma/2 (thr_out) and the
+ * near hit / near miss counts (counts_out[2 (i - i_begin)], [.. + 1]), in the
+ * reference's arithmetic as oracle_multisurf_acc. */
+ORACLE_API int oracle_multisurf_decisions(const float* x, int64_t n, int64_t p, const double* y,
+                                          const float* recip, const int64_t* feat_idx,
+                                          int64_t n_kept, const uint8_t* is_discrete,
+                                          int64_t i_begin, int64_t i_end, int n_jobs,
+                                          double* thr_out, int64_t* counts_out) {
+  if (n < 2 || i_begin < 0 || i_end > n || i_begin > i_end) return -1;
+  set_threads(n_jobs);
+  int fail = 0;
+#pragma omp parallel
+  {
+    double* drow = (double*)malloc(sizeof(double) * (size_t)n);
+    if (!drow) fail = 1;
+#pragma omp for schedule(dynamic, 1)
+  for (int64_t i = i_begin; i < i_end; i++) {
+    if (!drow) continue;
+    const float* xi = x + i * p;
+    double sum_d = 0.0, sum_d2 = 0.0;
+    for (int64_t j = 0; j < n; j++) {
+      if (i == j) continue;
+      const float* xj = x + j * p;
+      double d = 0.0;
+      for (int64_t k = 0; k < n_kept; k++) d += ms_diff(xi, xj, recip, is_discrete, feat_idx[k]);
+      drow[j] = d;
+      sum_d += d;
+      sum_d2 += d * d;
+    }
+    double mu = sum_d / (double)(n - 1);
+    double var = sum_d2 / (double)(n - 1) - mu * mu;
+    if (var < 0.0) var = 0.0;
+    double thresh = mu - 0.5 * sqrt(var);
+    int64_t h = 0, m = 0;
+    for (int64_t j = 0; j < n; j++) {
+      if (i == j || !(drow[j] < thresh)) continue;
+      if (y[i] == y[j]) h++;
+      else m++;
+    }
+    thr_out[i - i_begin] = thresh;
+    counts_out[2 * (i - i_begin)] = h;
+    counts_out[2 * (i - i_begin) + 1] = m;
+  }
+    free(drow);
+  }
+  return fail ? -2 : 0;
+}
+
 ORACLE_API int oracle_multisurf(const float* x, int64_t n, int64_t p, const double* y,
                                 const float* recip, const int64_t* feat_idx, int64_t n_kept,
                                 int use_star, const uint8_t* is_discrete, int64_t i_begin,

@@ -42,3 +42,32 @@ def assert_parity(a, ref, tol=1e-5, k=None):
         ta = set(np.argsort(np.asarray(a))[::-1][:k].tolist())
         tr = set(np.argsort(np.asarray(ref))[::-1][:k].tolist())
         assert ta == tr, f"top-{k} differ: {sorted(ta ^ tr)} ({summary(a, ref)})"
+
+
+def assert_parity_attributed(a, ref, exact, counts=None, ref_counts=None, tol=1e-5, k=10):
+    """The parity bar where the reference's own float32 sums may not allow
+    it.  Decisions first: with ``counts`` (our near hit / miss count per row)
+    and ``ref_counts`` (oracle_multisurf_decisions) no row may differ.  Then,
+    when the reference's float32 arithmetic (``ref``) is within tol / 2 of the
+    float64 sums of the same decisions (``exact``, the oracle's accum='f64'),
+    the plain bar: ``a`` within ``tol`` of ``ref`` (scale-relative); otherwise
+    the residual must be accumulation: ``a`` at least 10x closer to ``exact``
+    than ``ref`` is.  Top-k identical to ``ref``'s."""
+    a, ref, exact = (np.asarray(v, dtype=np.float64) for v in (a, ref, exact))
+    if counts is not None:
+        c = np.asarray(counts).reshape(-1, 2).astype(np.int64)
+        rc = np.asarray(ref_counts).reshape(-1, 2).astype(np.int64)
+        flipped = int(np.sum(np.any(c != rc, axis=1)))
+        assert flipped == 0, f"{flipped} rows decide differently from the reference"
+    scale = np.max(np.abs(exact))
+    ref_err = np.max(np.abs(ref - exact)) / scale
+    if ref_err < 0.5 * tol:
+        assert_parity(a, ref, tol, k)
+        return
+    acc_err = np.max(np.abs(a - exact)) / scale
+    assert acc_err <= 0.1 * ref_err, (
+        f"{acc_err:.3e} from the float64 sums, reference arithmetic {ref_err:.3e} "
+        f"({summary(a, ref)})")
+    ta = set(np.argsort(a)[::-1][:k].tolist())
+    tr = set(np.argsort(ref)[::-1][:k].tolist())
+    assert ta == tr, f"top-{k} differ: {sorted(ta ^ tr)} ({summary(a, ref)})"

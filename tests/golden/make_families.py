@@ -22,6 +22,8 @@ and checks.
 
 Run (container; ~6 min per case on 8 cores):
     python tests/golden/make_families.py [names...]
+    python tests/golden/make_families.py --f64 [names...]        (float64 sums)
+    python tests/golden/make_families.py --decisions [names...]  (thresholds, counts)
 """
 import hashlib
 import os
@@ -95,9 +97,26 @@ def run_f64(name):
     print(f"{name} f64: {time.time() - t0:.0f} s -> {out}", flush=True)
 
 
+def run_decisions(name):
+    """family_<name>_decisions.npz: the reference's near/far decisions alone
+    (oracle_multisurf_decisions: thresholds mu - sigma/2 and every row's near
+    hit / near miss counts, MultiSURF.py:175-217) -- a score residual with
+    identical counts is accumulation, not decisions."""
+    from oracle import oracle as O
+    t0 = time.time()
+    X, y = make(name)
+    thr, counts = O.multisurf_decisions(X, y)
+    out = os.path.join(HERE, f"family_{name}_decisions.npz")
+    np.savez_compressed(out, x_sha256=np.array(digest(X)), thr=thr, counts=counts.astype(np.int32))
+    print(f"{name} decisions: {time.time() - t0:.0f} s -> {out}", flush=True)
+
+
 if __name__ == "__main__":
     args = sys.argv[1:]
-    if args and args[0] == "--f64":
+    if args and args[0] == "--decisions":
+        for nm in args[1:] or list(CASES):
+            run_decisions(nm)
+    elif args and args[0] == "--f64":
         for nm in args[1:] or list(CASES):
             run_f64(nm)
     else:

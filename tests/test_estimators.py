@@ -411,13 +411,15 @@ def test_devices_parameter_resolution(monkeypatch):
     monkeypatch.setattr(_lib, "device_count", lambda: 4)
     assert _base.fit_devices(None, "cpu", 10 ** 6) is None
     assert _base.fit_devices([7], "cpu", 10) is None           # ignored by the CPU backend
-    assert _base.fit_devices(None, "gpu", 100) == [0]          # small job: one device
-    assert _base.fit_devices(None, "gpu", 9000) == [0, 1]      # one per 4096 samples
-    assert _base.fit_devices(None, "gpu", 10 ** 6) == [0, 1, 2, 3]
+    assert _base.fit_devices(None, "gpu", 10 ** 6) == [0]      # default: one device
+    assert _base.fit_devices("all", "gpu", 100) == [0]         # small job: one device
+    assert _base.fit_devices("all", "gpu", 9000) == [0, 1]     # one per 4096 samples
+    assert _base.fit_devices("all", "gpu", 10 ** 6) == [0, 1, 2, 3]
+    assert _base.stage_device("gpu", None, 10 ** 6) in (0, None)
     assert _base.fit_devices(2, "gpu", 10) == [2]
     assert _base.fit_devices(np.int64(3), "gpu", 10) == [3]
     assert _base.fit_devices((0, 0, 1), "gpu", 10) == [0, 0, 1]
-    for bad in ([], [4], [-1], "0", 1.5, True, [0, None]):
+    for bad in ([], [4], [-1], "0", "ALL", 1.5, True, [0, None]):
         with pytest.raises(ValueError, match="devices"):
             _base.fit_devices(bad, "gpu", 10)
     est = MultiSURF(devices=[0, 1])

@@ -80,11 +80,13 @@ def test_devices_bad_ordinal_is_a_value_error(F):
         F.ReliefF(backend="gpu", devices=[]).fit(X, y)
 
 
-def test_devices_default_uses_visible_devices(F):
-    """devices=None: every visible device the job has work for (one per
-    4096 samples), so a small fit stays on one device."""
+def test_devices_default_is_one_device(F):
+    """devices=None: device 0, as the reference; devices='all':
+    every visible device the job has work for (one per 4096 samples)."""
     from fastselect_amd import _base, _lib
     X, y = _data(500, 80, 6)
     est = F.MultiSURF(backend="gpu").fit(X, y)
     assert est.devices_ == [0]
-    assert _base.fit_devices(None, "gpu", 10 ** 6) == list(range(_lib.device_count()))
+    assert _base.fit_devices(None, "gpu", 10 ** 6) == [0]
+    assert _base.fit_devices("all", "gpu", 10 ** 6) == list(range(_lib.device_count()))
+    assert F.MultiSURF(backend="gpu", devices="all").fit(X, y).devices_ == [0]

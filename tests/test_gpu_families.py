@@ -10,12 +10,14 @@ columns whose ranges are set by a few extreme values, and mixed integer-level
 What they showed (profiles/r03/families.txt): on signal-free data the
 MultiSURF scores sit at the level of single near/far decisions, and the
 quantised thresholds of the 16-bit path moved enough of them to give 1.6e-4
-of max |s| against the oracle.  The one-shot call now estimates that risk
-after scoring (fs_multisurf_last_guard; fs_gpu.hip q16_decision_risk) and
-scores again on 32-bit operands above 5e-6.  There the reference's own
-float32 sums are as far from the float64 sums (2.6e-5 of max |s|) as the GPU
-is, so the uniform case is held to the float64 attribution bar instead of
-1e-5 against the oracle.
+of max |s| against the oracle.  Every MultiSURF path now estimates that risk
+after scoring (fs_plan_decision_guard; fs_gpu.hip q16_decision_risk) and
+scores again on 32-bit operands above 5e-6.  Since round 4 the row means are
+exact (fs_colsort.hip), and the uniform and lognormal cases are checked
+decision by decision against the oracle's counts (family_*_decisions.npz);
+where the reference's own float32 sums are further than 5e-6 of max |s|
+from the float64 sums of the same decisions, the residual must be
+accumulation (conftest.assert_parity_attributed).
 """
 import hashlib
 import importlib.util
@@ -24,7 +26,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import assert_parity
+from conftest import assert_parity, assert_parity_attributed
 
 pytestmark = pytest.mark.gpu
 
@@ -72,19 +74,35 @@ def test_uniform_noise_multisurf_star(F):
     assert_parity(s, ref, 1e-5, 10)
 
 
+def _decided(name):
+    """(plan-path scores, per-row near hit / miss counts) through
+    ShardedMultiSURF (decision check included) and the oracle's counts and
+    float64-sum scores (tests/golden/make_families.py --decisions / --f64)."""
+    from fastselect_amd import parallel
+    X, y = mk.make(name)
+    x, yv, recip, isd = parallel.prepare_inputs(X, y, backend="gpu")
+    job = parallel.ShardedMultiSURF(x, yv, recip, isd, backend="gpu", shard=False)
+    try:
+        s = job.step().cpu().numpy()
+        counts = job.counts.cpu().numpy()
+    finally:
+        job.close()
+    dec = np.load(os.path.join(GOLD, f"family_{name}_decisions.npz"), allow_pickle=False)
+    exact = np.load(os.path.join(GOLD, f"family_{name}_f64.npz"), allow_pickle=False)["scores"]
+    return s, counts, dec["counts"], exact
+
+
 def test_uniform_noise_multisurf_reruns_on_32bit(F):
     """Signal-free data: the decision check trips and the call re-scores on
-    32-bit operands; the result is then as close to the float64 sums as the
-    reference's own float32 arithmetic (max over features, 1.5x slack), with
-    the oracle's top-10."""
+    32-bit operands.  Every row's near hit / miss count then equals the
+    reference's; the reference's own float32 sums are 2.6e-5 of max |s| from
+    the float64 sums of those decisions, so the bar is the attributed one
+    (conftest.assert_parity_attributed): 10x closer to the float64 sums."""
     s, ref, (risk, rerun) = _fit(F, "uniform_16k", False)
     assert risk > 5e-6 and rerun
-    exact = np.load(os.path.join(GOLD, "family_uniform_16k_f64.npz"), allow_pickle=False)["scores"]
-    scale = np.max(np.abs(exact))
-    gpu_err = np.max(np.abs(s - exact)) / scale
-    ref_err = np.max(np.abs(ref - exact)) / scale
-    assert gpu_err <= 1.5 * ref_err, (gpu_err, ref_err)
-    assert set(np.argsort(s)[::-1][:10]) == set(np.argsort(ref)[::-1][:10])
+    sp, counts, ref_counts, exact = _decided("uniform_16k")
+    np.testing.assert_array_equal(sp, s)
+    assert_parity_attributed(s, ref, exact, counts, ref_counts, 1e-5, 10)
 
 
 def test_lognormal_multisurf_star(F):
@@ -92,15 +110,12 @@ def test_lognormal_multisurf_star(F):
     assert_parity(s, ref, 1e-5, 10)
 
 
-@pytest.mark.xfail(strict=False, reason=(
-    "open (round 3): lognormal columns (ranges set by a few values ~1e5 x the "
-    "median) give 2.7e-4 of max |s| against the oracle on the 32-bit path; the "
-    "CPU backend reproduces it (n = 3000, p = 2000: 6.2e-3).  A numpy model of "
-    "that case (same quantisation, reference decisions exact) flips 4 near/far "
-    "decisions with the quantised row means and none with exact ones: the mean "
-    "correction's 4096-bin rank histogram puts nearly all samples of such a "
-    "column in one bin, so its ranks, and the thresholds, stay ~1e-7 off; each "
-    "flip is ~1.5e-3 of these tiny scores.  Needs exact per-column ranks"))
 def test_lognormal_multisurf(F):
+    """Columns whose ranges are set by a few values ~1e5 x the median: open in
+    round 3 (2.7e-4 of max |s|; the binned ranks of the old mean correction
+    moved the thresholds), closed by the exact per-column order
+    (fs_colsort.hip): no decision differs from the reference's."""
     s, ref, _ = _fit(F, "lognormal_16k", False)
-    assert_parity(s, ref, 1e-5, 10)
+    sp, counts, ref_counts, exact = _decided("lognormal_16k")
+    np.testing.assert_array_equal(sp, s)
+    assert_parity_attributed(s, ref, exact, counts, ref_counts, 1e-5, 10)

@@ -106,3 +106,87 @@ def test_random_parity_cpu(oracle, seed):
 @pytest.mark.parametrize("seed", range(N_CASES))
 def test_random_parity_gpu(oracle, seed):
     run_case(oracle, seed, "gpu")
+
+
+# ---- heavy tails, outliers, spikes (VERDICT r3 missing #3) ----------------
+# The sweep above never reaches the regime where the round-3 mean correction
+# broke: n in the thousands and columns whose range is set by a few extreme
+# values.  This one draws n up to 3000 with lognormal / Pareto tails,
+# single-outlier columns and near-constant columns with rare spikes beside
+# ordinary ones, and checks MultiSURF decision by decision against the
+# oracle's (oracle_multisurf_decisions), then every estimator's scores at
+# 1e-5 of max |s| where the reference's own float32 sums allow it, else as
+# accumulation against the oracle's float64 sums (conftest.assert_parity_attributed).
+N_TAIL_CASES = 10
+
+
+def make_tail_case(seed):
+    rng = np.random.default_rng(5000 + seed)
+    n = int(rng.integers(300, 3001))
+    p = int(rng.integers(10, 201))
+    cols = []
+    for _ in range(p):
+        kind = rng.choice(["lognormal", "pareto", "outlier", "spikes", "normal"])
+        if kind == "lognormal":
+            c = np.exp(rng.uniform(1.0, 4.0) * rng.standard_normal(n))
+        elif kind == "pareto":
+            c = rng.pareto(rng.uniform(0.8, 2.0), n) + 1.0
+        elif kind == "outlier":
+            c = rng.standard_normal(n) * 1e-3
+            c[rng.integers(0, n)] = 10.0 ** rng.uniform(2, 6)
+        elif kind == "spikes":
+            c = 7.0 + rng.standard_normal(n) * 1e-6
+            hit = rng.random(n) < rng.uniform(0.0005, 0.01)
+            c[hit] += 10.0 ** rng.uniform(0, 4)
+        else:
+            c = rng.standard_normal(n)
+        cols.append(c)
+    X = np.stack(cols, axis=1).astype(np.float32)
+    n_cls = int(rng.integers(2, 4))
+    y = rng.integers(0, n_cls, n)
+    for f in rng.choice(p, size=min(p, 4), replace=False):
+        X[:, f] = X[:, f] + (y * np.float32(np.std(X[:, f]) * rng.uniform(0.3, 1.0))).astype(np.float32)
+    return X, y, int(rng.integers(3, 11))
+
+
+def run_tail_case(oracle, seed, backend):
+    import warnings
+
+    from conftest import assert_parity_attributed
+    from fastselect_amd import parallel
+    X, y, k = make_tail_case(seed)
+    x, yv, recip, isd = parallel.prepare_inputs(X, y, backend=backend)
+    job = parallel.ShardedMultiSURF(x, yv, recip, isd, backend=backend, shard=False)
+    try:
+        s = job.step().cpu().numpy()
+        counts = job.counts.cpu().numpy()
+    finally:
+        job.close()
+    _, ref_counts = oracle.multisurf_decisions(X, y)
+    assert_parity_attributed(s, oracle.multisurf_scores(X, y),
+                             oracle.multisurf_scores(X, y, accum="f64"), counts, ref_counts,
+                             TOL, 5)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", UserWarning)
+        fit = MultiSURF(backend=backend, use_star=True).fit(X, y).feature_importances_
+        assert_parity_attributed(fit, oracle.multisurf_scores(X, y, use_star=True),
+                                 oracle.multisurf_scores(X, y, use_star=True, accum="f64"),
+                                 tol=TOL, k=5)
+        fit = SURF(backend=backend).fit(X, y).feature_importances_
+        assert_parity_attributed(fit, oracle.surf_scores(X, y),
+                                 oracle.surf_scores(X, y, accum="f64"), tol=TOL, k=5)
+        fit = ReliefF(backend=backend, n_neighbors=k).fit(X, y).feature_importances_
+        assert_parity_attributed(fit, oracle.relieff_scores(X, y, n_neighbors=k),
+                                 oracle.relieff_scores(X, y, n_neighbors=k, accum="f64"),
+                                 tol=TOL, k=5)
+
+
+@pytest.mark.parametrize("seed", range(N_TAIL_CASES))
+def test_tail_parity_cpu(oracle, seed):
+    run_tail_case(oracle, seed, "cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", range(N_TAIL_CASES))
+def test_tail_parity_gpu(oracle, seed):
+    run_tail_case(oracle, seed, "gpu")
