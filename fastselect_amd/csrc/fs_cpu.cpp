@@ -163,14 +163,19 @@ static void distances(const Prepared& P, const std::vector<uint32_t>& xq, int ra
   });
 }
 
-// Mean correction of k_colsort / k_rowcorr (fs_colsort.hip): every
-// continuous column ordered exactly by t (colsort_key, ties by index, as the
-// GPU's stable sorts), then with position k, the eps prefix P before it and
-// the column total T (fixed point 2^24, exact integers):
-//   term_i = eps_i (2k - n) - 2 P + T,   corr[i] = sum_c term_ic,
-// bit-identical terms to the GPU's.  The correction of the continuous
-// columns [c_lo, c_hi) (a rank's share; the shares are summed across ranks
-// with the row moments).
+// Mean correction of k_colsort / k_rowcorr (fs_colsort.hip), the same
+// integer arithmetic: every continuous column is ordered by t (colsort_key).
+// Binned on the key's top 12 bits, a sample is ordered exactly against every
+// other bin by the bin counts and fixed-point eps sums, and within its own
+// bin against its neighbours' low key bits (their eps at 2^-12 of a quantum,
+// equal keys tied); a column with a bin fuller than kColsortMaxFill is
+// sorted whole instead (std::sort on (key, index), as the GPU's stable sort),
+// where position k, the eps prefix P before it and the column total T give
+//   term_i = eps_i (2k - n) - 2 P + T.
+// Either way term_i = eps_i (L - G) - (E_below - E_above), and
+// corr[i] = sum_c term_ic: bit-identical terms to the GPU's.  The correction
+// of the continuous columns [c_lo, c_hi) (a rank's share; the shares are
+// summed across ranks with the row moments).
 static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
                             const std::vector<float>& eps, int64_t c_lo, int64_t c_hi,
                             int n_jobs, std::vector<double>& corr) {
@@ -180,20 +185,61 @@ static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
   parallel_for(c_hi - c_lo, n_jobs, [&](int64_t cc) {
     const int64_t c = c_lo + cc;
     constexpr double kFx = 16777216.0;  // eps fixed point 2^24, as k_colsort
-    std::vector<uint64_t> ord((size_t)n);
+    std::vector<uint32_t> key((size_t)n);
+    std::vector<int64_t> fx((size_t)n);
+    std::vector<int64_t> cnt(kColsortBins + 1, 0), esum(kColsortBins + 1, 0);
     int64_t T = 0;
     for (int64_t i = 0; i < n; i++) {
-      const float e = eps[(size_t)i * P.PW + c];
-      ord[i] = ((uint64_t)colsort_key(xq[(size_t)i * P.PW + c], e, s) << 32) | (uint64_t)i;
-      T += (int64_t)std::llrint((double)e * kFx);
+      fx[i] = colsort_fx(eps[(size_t)i * P.PW + c]);
+      key[i] = colsort_key(xq[(size_t)i * P.PW + c], (int32_t)fx[i], s);
+      cnt[(key[i] >> kColsortBinShift) + 1]++;
+      esum[(key[i] >> kColsortBinShift) + 1] += fx[i];
+      T += fx[i];
     }
-    std::sort(ord.begin(), ord.end());
-    int64_t Pk = 0;
-    for (int64_t k = 0; k < n; k++) {
-      const int64_t i = (int64_t)(ord[k] & 0xFFFFFFFFull);
-      const int64_t e = (int64_t)std::llrint((double)eps[(size_t)i * P.PW + c] * kFx);
-      term[(size_t)i * P.pc + c] = (float)((double)(e * (2 * k - n) - 2 * Pk + T) / kFx);
-      Pk += e;
+    int64_t fill = 0;
+    for (int b = 0; b < kColsortBins; b++) {
+      fill = std::max(fill, cnt[b + 1]);
+      cnt[b + 1] += cnt[b];     // exclusive prefix at b, inclusive at b + 1
+      esum[b + 1] += esum[b];
+    }
+    if (fill > kColsortMaxFill) {
+      std::vector<uint64_t> ord((size_t)n);
+      for (int64_t i = 0; i < n; i++) ord[i] = ((uint64_t)key[i] << 32) | (uint64_t)i;
+      std::sort(ord.begin(), ord.end());
+      int64_t Pk = 0;
+      for (int64_t k = 0; k < n; k++) {
+        const int64_t i = (int64_t)(ord[k] & 0xFFFFFFFFull);
+        term[(size_t)i * P.pc + c] = (float)((double)(fx[i] * (2 * k - n) - 2 * Pk + T) / kFx);
+        Pk += fx[i];
+      }
+      return;
+    }
+    // the samples of bins holding >= 2, in bin order (low key bits, eps code)
+    std::vector<uint32_t> seg((size_t)n), cur(cnt.begin(), cnt.end() - 1);
+    for (int64_t i = 0; i < n; i++) {
+      const uint32_t b = key[i] >> kColsortBinShift;
+      if (cnt[b + 1] - cnt[b] < 2) continue;
+      seg[cur[b]++] = ((key[i] & ((1u << kColsortBinShift) - 1u)) << 12) |
+                      colsort_eq12((int32_t)fx[i]);
+    }
+    for (int64_t i = 0; i < n; i++) {
+      const uint32_t b = key[i] >> kColsortBinShift;
+      int64_t L = cnt[b], G = n - cnt[b + 1], Eb = esum[b], Ea = T - esum[b + 1];
+      if (cnt[b + 1] - cnt[b] >= 2) {
+        const uint32_t mine = key[i] & ((1u << kColsortBinShift) - 1u);
+        for (int64_t j = cnt[b]; j < cnt[b + 1]; j++) {
+          const uint32_t kl = seg[j] >> 12;
+          const int64_t q = colsort_eq12_fx(seg[j] & 0xFFFu);
+          if (kl < mine) {
+            L++;
+            Eb += q;
+          } else if (kl > mine) {
+            G++;
+            Ea += q;
+          }
+        }
+      }
+      term[(size_t)i * P.pc + c] = (float)((double)(fx[i] * (L - G) - (Eb - Ea)) / kFx);
     }
   });
   corr.assign(n, 0.0);

@@ -290,8 +290,7 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
                                                  const int2* __restrict__ tiles, int64_t n_full,
                                                  int splits, int tiled, int2 win,
                                                  double* __restrict__ D,
-                                                 double* __restrict__ Dpart, int64_t sk_wgs,
-                                                 int64_t sk_units, float* __restrict__ Dk,
+                                                 double* __restrict__ Dpart, float* __restrict__ Dk,
                                                  double inv_sc) {
   // Two distinct LDS objects (not one indexed array) so the compiler can
   // prove a pending global_load_lds into one buffer does not alias the
@@ -454,21 +453,6 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
   };
 
   const int64_t b_id = blockIdx.x;
-  if (sk_wgs > 0) {
-    // Stream-K: the (tile, chunk) units [b U / W, (b + 1) U / W), U = tiles
-    // x chunks, tile by tile.  A segment that starts a tile writes D; one
-    // that starts inside it (only the workgroup's first) writes the partial
-    // block Dpart[b], added by k_dist_merge_sk.
-    const int64_t u_lo = b_id * sk_units / sk_wgs, u_hi = (b_id + 1) * sk_units / sk_wgs;
-    for (int64_t u = u_lo; u < u_hi;) {
-      const int64_t t = u / nck_all;
-      const int cb = (int)(u - t * nck_all);
-      const int ce = (int)std::min<int64_t>(nck_all, cb + (u_hi - u));
-      segment(t, cb, ce, cb > 0 ? b_id : -1);
-      u += ce - cb;
-    }
-    return;
-  }
   const int64_t q = b_id - n_full;  // >= 0: a split tile's part
   const int part = q < 0 ? 0 : (int)(q % splits);
   const int nparts = q < 0 ? 1 : splits;
@@ -476,46 +460,6 @@ __global__ __launch_bounds__(256, 3) void k_dist(const uint32_t* __restrict__ xq
   const int c_begin = (int)((int64_t)nck_all * part / nparts);
   const int c_end = (int)((int64_t)nck_all * (part + 1) / nparts);  // this part's chunks
   segment(t, c_begin, c_end, part > 0 ? (q / splits) * (splits - 1) + part - 1 : -1);
-}
-
-// Stream-K merge: tile t (grid.x) adds the partial blocks of the workgroups
-// whose unit range starts strictly inside it (Dpart[b], tile-local T[b][a])
-// to the block its first segment wrote.  Integer-valued doubles: exact, the
-// same D as one workgroup per tile.
-__global__ __launch_bounds__(256) void k_dist_merge_sk(double* __restrict__ D,
-                                                      const double* __restrict__ Dpart,
-                                                      const int2* __restrict__ tiles, int64_t nck,
-                                                      int64_t sk_wgs, int64_t sk_units,
-                                                      int64_t n_pad, int tiled, int2 win) {
-  const int64_t t = blockIdx.x;
-  const int64_t base = t * nck;
-  // first workgroup whose range starts after `base`
-  int64_t b = base * sk_wgs / sk_units;
-  while (b > 0 && (b * sk_units / sk_wgs) > base) b--;
-  while (b * sk_units / sk_wgs <= base) b++;
-  if (b >= sk_wgs || b * sk_units / sk_wgs >= base + nck) return;  // tile computed whole
-  const int2 tl = tiles[t];
-  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
-  int64_t at[4];
-  double v[4];
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int e = blockIdx.y * 1024 + k * 256 + threadIdx.x;
-    at[k] = d_rd(tiled, win, n_pad, t, i0, j0, e % kTile, e / kTile);  // (i0 + a, j0 + b)
-    v[k] = D[at[k]];
-  }
-  for (; b < sk_wgs && b * sk_units / sk_wgs < base + nck; b++) {
-    const double* __restrict__ ps = Dpart + b * kTile * kTile + blockIdx.y * 1024 + threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < 4; k++) v[k] += ps[k * 256];
-  }
-#pragma unroll
-  for (int k = 0; k < 4; k++) {
-    const int e = blockIdx.y * 1024 + k * 256 + threadIdx.x;
-    D[at[k]] = v[k];
-    if (!tiled && tl.x != tl.y && d_row_in(win, j0 + e / kTile) && d_row_in(win, i0 + e % kTile))
-      D[(i0 + e % kTile) * n_pad + j0 + e / kTile] = v[k];
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1223,66 +1167,17 @@ __global__ __launch_bounds__(256) void k_weights(const double* __restrict__ D, i
 }
 
 // Sparse pair weights (pass 2 skips zero weights; MultiSURF: ~42% of the
-// pairs are near one of their two samples).  The 128 columns of owned tile t
-// are dealt to kSWaves = 16 streams, stream w taking jj = w, w + 16, ... (8
-// columns); a stream holds its columns' non-zero weights of rows ii in
-// ascending ii as entries (ii * 1024, w) -- 1024 = the byte stride of a row
-// in k_score_sparse's LDS block -- each column padded with (0, 0) to whole
-// groups of kGroup entries (at least one), columns back to back.  The lowest
-// mantissa bit of the first weight of a column's last group is set and that
-// of every other weight cleared (a <= 1-ulp change, far below the 1e-5 bar).
-// Stream (t, w) starts at ent + (t * 16 + w) * kStreamEntries.
-constexpr int kGroup = 8;
-constexpr int kSWaves = 16;                                // waves of k_score_sparse
-constexpr int kStreamEntries = (kTile / kSWaves) * kTile;  // 8 columns x 128 rows
+// pairs are near one of their two samples): k_weights_sparse2 / k_score_sparse2
+// below.  A workgroup of the sparse kernels has kSWaves waves.
+constexpr int kSWaves = 16;
+// entries a tile's streams may hold: 16 streams x 8 columns x 128 rows (both halves)
+constexpr int kStreamEntries = (kTile / kSWaves) * kTile;
 // floats past xs's last spare row that a pass-2 B-row read may touch (the
-// widest feature block of k_score_sparse)
+// widest feature block of k_score_sparse2)
 constexpr int64_t kXsSlack = 512;
 
 __device__ __forceinline__ uint32_t weight_bits(float w, bool last) {
   return (__float_as_uint(w) & ~1u) | (last ? 1u : 0u);
-}
-
-__global__ __launch_bounds__(1024) void k_weights_sparse(
-    const double* __restrict__ D, int64_t n, int64_t n_pad, int tiled, int2 win,
-    const int2* __restrict__ tiles, const double* __restrict__ thr,
-    const int32_t* __restrict__ lab,
-    const double* __restrict__ counts, int algo, int use_star, double inv_sc, int64_t r_lo,
-    int64_t r_hi, uint2* __restrict__ ent, unsigned long long* __restrict__ nnz) {
-  __shared__ int wave_nnz[kSWaves];
-  const int2 tl = tiles[blockIdx.x];
-  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint2* out = ent + ((int64_t)blockIdx.x * kSWaves + wave) * kStreamEntries;
-  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
-  int off = 0, nz = 0;
-  for (int jj = wave; jj < kTile; jj += kSWaves) {
-    const float w0 = pair_weight(D, n, n_pad, tiled, win, blockIdx.x, i0, j0, lane, jj,
-                                 tl.x < tl.y || lane < jj, thr, lab, counts, algo, use_star,
-                                 inv_sc, r_lo, r_hi);
-    const float w1 = pair_weight(D, n, n_pad, tiled, win, blockIdx.x, i0, j0, lane + 64, jj,
-                                 tl.x < tl.y || lane + 64 < jj, thr, lab, counts, algo, use_star,
-                                 inv_sc, r_lo, r_hi);
-    const uint64_t m0 = __ballot(w0 != 0.0f), m1 = __ballot(w1 != 0.0f);
-    const int n0 = __popcll(m0), total = n0 + __popcll(m1);
-    const int padded = total == 0 ? kGroup : (total + kGroup - 1) / kGroup * kGroup;
-    const int last = padded - kGroup;  // first entry of the column's last group
-    const int e0 = __popcll(m0 & below), e1 = n0 + __popcll(m1 & below), ep = total + lane;
-    if (w0 != 0.0f) out[off + e0] = make_uint2((uint32_t)lane * 1024u, weight_bits(w0, e0 == last));
-    if (w1 != 0.0f)
-      out[off + e1] = make_uint2((uint32_t)(lane + 64) * 1024u, weight_bits(w1, e1 == last));
-    if (ep < padded) out[off + ep] = make_uint2(0u, ep == last ? 1u : 0u);
-    off += padded;
-    nz += total;
-  }
-  // non-zero pairs of the tile (throughput accounting)
-  if (lane == 0) wave_nnz[wave] = nz;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    unsigned long long t = 0;
-    for (int w = 0; w < kSWaves; w++) t += (unsigned long long)wave_nnz[w];
-    atomicAdd(nnz, t);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1430,136 +1325,16 @@ __global__ __launch_bounds__(256) void k_score(const float* __restrict__ xs, int
   }
 }
 
-// Pass 2 over the sparse weights.  Grid as k_score (XCD-aware, segments of
-// consecutive tiles) but with 256-feature blocks and 16 waves per workgroup
-// (one workgroup per CU).  The 128 rows of the current row block sit in LDS
-// (128 KB: row r, lane l = features f0 + l + 64k, k = 0..3, as one float4),
-// staged when the segment reaches a new row block.  Wave w walks its stream
-// of each tile (k_weights_sparse): per column the four B values are VGPRs and
-// every entry is one ds_read_b128 of its row and 4 x (sub, fma |.|) with the
-// weight in an SGPR -- the hand-pipelined loop of fs_sparse_asm.inc for
-// continuous blocks, plain HIP below for blocks holding discrete features.
-template <bool DISC>
-__device__ __forceinline__ float pair_term_d(float a, float b, float w, float acc) {
-  return pair_term<DISC>(a, b, w, acc);
-}
-
-__device__ __forceinline__ void sparse_stream_generic(const float4* __restrict__ As,
-                                                      const uint2* __restrict__ e,
-                                                      const float* __restrict__ xb, int64_t PW,
-                                                      int lane, const bool (&disc)[4],
-                                                      float (&acc)[8]) {
-  int col = 0;
-  float4 b = make_float4(xb[0], xb[64], xb[128], xb[192]);
-  for (int g = 0; col < kTile / kSWaves && g < kStreamEntries; g += kGroup) {
-    uint2 E[kGroup];
-#pragma unroll
-    for (int q = 0; q < kGroup; q++) E[q] = e[g + q];
-#pragma unroll
-    for (int q = 0; q < kGroup; q++) {
-      const float4 a = As[(E[q].x >> 4) + lane];
-      const float w = __uint_as_float(E[q].y);
-      const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        float& c = acc[2 * k + (q & 1)];
-        c = disc[k] ? pair_term_d<true>(av[k], bv[k], w, c) : pair_term_d<false>(av[k], bv[k], w, c);
-      }
-    }
-    if (E[0].y & 1u) {  // end of the column
-      col++;
-      if (col < kTile / kSWaves) {
-        const float* __restrict__ xn = xb + (int64_t)col * kSWaves * PW;
-        b = make_float4(xn[0], xn[64], xn[128], xn[192]);
-      }
-    }
-  }
-}
-
-__global__ __launch_bounds__(1024) void k_score_sparse(
-    const float* __restrict__ xs, int64_t PW, int64_t PC, const int2* __restrict__ tiles,
-    const uint2* __restrict__ ent, int64_t n_tiles, int64_t seg_len, int64_t nseg, int64_t nfb,
-    int jit, double* __restrict__ spart) {
-  __shared__ float4 As[kTile * 64];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t wg = blockIdx.x;
-  const int64_t xcd = wg % kXcds, k = wg / kXcds;
-  const int64_t seg = xcd + kXcds * (k / nfb), fb = k % nfb;
-  if (seg >= nseg) return;
-  const int64_t f0 = fb * 256;
-  const int64_t t_begin = seg * seg_len;
-  const int64_t t_end = t_begin + seg_len < n_tiles ? t_begin + seg_len : n_tiles;
-  // chunk c (features f0 + 64c ..) is real if below PW, discrete from PC on
-  bool disc[4], real[4];
-#pragma unroll
-  for (int c = 0; c < 4; c++) {
-    real[c] = f0 + 64 * c < PW;
-    disc[c] = f0 + 64 * c >= PC;
-  }
-  // the asm loop when every real chunk is continuous: a last, partial block
-  // of an all-continuous layout (cfg4: 64 real features in block 78) stages
-  // zeros for the chunks past PW and discards their accumulators, whose B
-  // values (read past the row's end, inside xs's spare rows) are not used
-  const bool fast = (f0 + 256 < PW ? f0 + 256 : PW) <= PC;
-  const uint32_t lane16 = (uint32_t)(uintptr_t)As + (uint32_t)lane * 16u;
-  const uint32_t lane4 = (uint32_t)lane * 4u;
-  const uint32_t bstride = (uint32_t)(kSWaves * PW * sizeof(float));
-  const uint32_t ncols = kTile / kSWaves;
-  double s[4] = {0.0, 0.0, 0.0, 0.0};
-  int cur_bi = -1;
-  for (int64_t t = t_begin; t < t_end; t++) {
-    const int2 tl = tiles[t];
-    if (tl.x != cur_bi) {
-      __syncthreads();
-      const float* __restrict__ xa = xs + (int64_t)tl.x * kTile * PW + f0 + lane;
-      for (int r = wave; r < kTile; r += kSWaves) {
-        const float* __restrict__ xr = xa + (int64_t)r * PW;
-        As[r * 64 + lane] = make_float4(xr[0], real[1] ? xr[64] : 0.0f, real[2] ? xr[128] : 0.0f,
-                                        real[3] ? xr[192] : 0.0f);
-      }
-      __syncthreads();
-      cur_bi = tl.x;
-    }
-    float acc[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    const uint2* __restrict__ e = ent + (t * kSWaves + wave) * kStreamEntries;
-    const float* __restrict__ xb = xs + ((int64_t)tl.y * kTile + wave) * PW + f0;
-    if (fast) {
-      const uint64_t eb = (uint64_t)(uintptr_t)e, bp = (uint64_t)(uintptr_t)xb;
-      if (jit)
-        FS_SPARSE_STREAM_ASM_JIT(acc, lane16, lane4, eb, bp, bstride, ncols);
-      else
-        FS_SPARSE_STREAM_ASM(acc, lane16, lane4, eb, bp, bstride, ncols);
-    } else {
-      sparse_stream_generic(As, e, xb + lane, PW, lane, disc, acc);
-    }
-#pragma unroll
-    for (int c = 0; c < 4; c++) s[c] += (double)acc[2 * c] + (double)acc[2 * c + 1];
-  }
-  // fixed-order reduction of the 16 waves' partials through the LDS block
-  __syncthreads();
-  double* red = (double*)As;  // [4 chunks][kSWaves][64]
-#pragma unroll
-  for (int c = 0; c < 4; c++) red[(c * kSWaves + wave) * 64 + lane] = s[c];
-  __syncthreads();
-  if (wave < 4 && real[wave]) {
-    const double* r = red + wave * kSWaves * 64 + lane;
-    double v = 0.0;
-#pragma unroll
-    for (int q = 0; q < kSWaves; q += 4)
-      v += (r[q * 64] + r[(q + 1) * 64]) + (r[(q + 2) * 64] + r[(q + 3) * 64]);
-    spart[seg * PW + f0 + 64 * wave + lane] = v;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Pass 2, sparse v2: 64-row half tiles, 8 features per lane
 // ---------------------------------------------------------------------------
-// The v1 streams above hold a whole 128-row tile per wave, so a workgroup
-// keeps 128 rows x 256 features (128 KB) in LDS and every entry feeds 4
-// features per lane: the entry streams are re-read once per 256-feature block
-// (79 times at cfg4) and each scalar load of 8 entries covers 8 x 9 VALU.
-// v2 splits each tile into its two 64-row halves: a workgroup keeps 64 rows x
+// Grid as k_score (XCD-aware, segments of consecutive tiles), 16 waves per
+// workgroup (one workgroup per CU).  The round-1/2 form (v1, retired in
+// round 4) held a whole 128-row tile per wave, so a workgroup
+// kept 128 rows x 256 features (128 KB) in LDS and every entry fed 4
+// features per lane: the entry streams were re-read once per 256-feature
+// block (79 times at cfg4) and each scalar load of 8 entries covered 8 x 9
+// VALU.  v2 splits each tile into its two 64-row halves: a workgroup keeps 64 rows x
 // 512 features (the same 128 KB) and every entry feeds 8 features per lane --
 // one v_add_u32 address, two ds_read_b128, 8 x (v_sub_f32, v_fma_f32 |.|): 17
 // VALU per 8 pair-features instead of 18, half the scalar loads and half the
@@ -1580,14 +1355,6 @@ __global__ __launch_bounds__(1024) void k_score_sparse(
 // kStreamEntries2; 8 columns x 64 rows fill it at most.
 constexpr int kHalf = 64;
 constexpr int kRowBytes2 = 2048;                           // 64 lanes x 8 floats
-// Entries of a column padded with zero weights to a multiple of kGroup2
-// (the generated loop then tests the column-end flag once per group; A/B
-// builds set FS_V2_GROUP, tools/build_variant.sh)
-#ifndef FS_V2_GROUP
-#define FS_V2_GROUP 1
-#endif
-constexpr int kGroup2 = FS_V2_GROUP;
-static_assert(kHalf % kGroup2 == 0, "a full column must need no padding");
 constexpr int kStreamEntries2 = (kTile / kSWaves) * kHalf;  // 512
 static_assert(kStreamEntries2 * 2 == kStreamEntries, "v2 streams reuse the v1 buffer size");
 
@@ -1615,9 +1382,9 @@ __global__ __launch_bounds__(1024) void k_weights_sparse2(
                                  inv_sc, r_lo, r_hi);
     const uint64_t m0 = __ballot(w0 != 0.0f), m1 = __ballot(w1 != 0.0f);
     const int n0 = __popcll(m0), n1 = __popcll(m1);
-    // padded lengths (at least one entry: an empty column still ends)
-    const int p0 = n0 == 0 ? kGroup2 : (n0 + kGroup2 - 1) / kGroup2 * kGroup2;
-    const int p1 = n1 == 0 ? kGroup2 : (n1 + kGroup2 - 1) / kGroup2 * kGroup2;
+    // stream lengths (at least one entry: an empty column still ends)
+    const int p0 = n0 == 0 ? 1 : n0;
+    const int p1 = n1 == 0 ? 1 : n1;
     const int e0 = __popcll(m0 & below), e1 = __popcll(m1 & below);
     if (w0 != 0.0f) out0[off0 + e0] = make_uint2(roff, weight_bits(w0, e0 == p0 - 1));
     if (w1 != 0.0f) out1[off1 + e1] = make_uint2(roff, weight_bits(w1, e1 == p1 - 1));
@@ -1690,7 +1457,7 @@ template <int F>
 __global__ __launch_bounds__(1024) void k_score_sparse2(
     const float* __restrict__ xs, int64_t PW, int64_t PC, const int2* __restrict__ tiles,
     const uint2* __restrict__ ent, int64_t n_tiles, int64_t seg_len, int64_t nseg, int64_t nfb,
-    int64_t f_base, int use_asm, double* __restrict__ spart) {
+    int64_t f_base, double* __restrict__ spart) {
   constexpr int C = F / 4;
   __shared__ float4 As[kHalf * 2 * 64];  // 64 rows x 2 chunks x 64 lanes (128 KB)
   const int lane = threadIdx.x & 63;
@@ -1712,7 +1479,7 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
   // features past PW stage zeros and their accumulators are discarded (their
   // B values are read past the row's end: xs has kXsSlack floats of slack)
   const int64_t f_end = f0 + 64 * F < PW ? f0 + 64 * F : PW;
-  const bool fast = use_asm && f_end <= PC;
+  const bool fast = f_end <= PC;
   const uint32_t lds_lane = (uint32_t)(uintptr_t)As + (uint32_t)lane * 16u;
   const uint32_t glb_lane = (uint32_t)lane * 16u;
   const uint32_t pf_lane = (uint32_t)lane * 32u;
@@ -1744,11 +1511,7 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
     const float* __restrict__ xb = xs + ((int64_t)tl.y * kTile + wave) * PW + f0;
     if (fast) {
       const uint64_t eb = (uint64_t)(uintptr_t)e;
-#ifdef FS_V2_DIAG_BHOT  // A/B diagnostic only (wrong scores): every B from one hot row
-      const uint64_t bp = (uint64_t)(uintptr_t)(xs + (int64_t)wave * PW + f0);
-#else
       const uint64_t bp = (uint64_t)(uintptr_t)xb;
-#endif
       // the next tile's B rows (warmed into L2 by the loop; the last tile
       // of a segment warms its own again)
       const int64_t tn = t + 1 < t_end ? t + 1 : t;
@@ -3264,8 +3027,6 @@ struct Plan {
   int64_t nb = 0, n_tiles = 0, seg_len = 1, nseg = 1;
   int64_t nsegpart = 1;         // rows of spart (nseg, or 2 * nseg for the v2 sparse pass)
   int ksplit = 1;               // pass-1 K-split parts of the tail tiles (k_dist)
-  int64_t sk_wgs = 0;           // pass-1 stream-K workgroups (0: off; choose_streamk)
-  int64_t sk_units = 0;         // stream-K units: tiles x chunks
   int64_t kfull = 0;            // tiles k_dist computes whole (the rest are split)
   int use_q16 = 0;              // pass 1 on packed 16-bit continuous operands
   double calib[7] = {0, 0, 0, 0, 1, 0, 0};  // plan_calibration (calibrate_band, row_guard)
@@ -3307,7 +3068,6 @@ struct Plan {
   unsigned long long* nnz = nullptr;  // non-zero weights of the last pass 2
   bool nnz_valid = false;
   int sparse = 0;               // pass 2 over non-zero weights only
-  int sparse_v = 2;             // sparse stream layout: 2 = half tiles x 8 features (v1: A/B)
   double* spart = nullptr;       // pass-2 segment partials (own block, shard_segments)
   size_t spart_cap = 0;           // doubles of spart
   // ambiguous-pair refinement
@@ -3764,46 +3524,6 @@ void plan_destroy(Plan* g) {
 // tile planes (~66.5 / p of the tile's compute time each); S > 1 only when
 // the model gains at least 3%.  (Splitting only the last round's tiles was
 // measured too: no better than S = 1 at cfg2, profiles/r02/ksplit_sweep.txt.)
-// k_dist workgroups resident on the device at once (CUs x occupancy), 0 if
-// the runtime cannot say.
-static int64_t kdist_slots(int device) {
-  int cus = 0, per_cu = 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
-      cus <= 0) {
-    (void)hipGetLastError();
-    return 0;
-  }
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_dist, 256, 0) != hipSuccess ||
-      per_cu <= 0) {
-    (void)hipGetLastError();
-    per_cu = 2;
-  }
-  return (int64_t)per_cu * cus;
-}
-
-// Pass-1 stream-K (round 3): instead of splitting every tile's feature range
-// into S parts (S - 1 partial blocks per tile, all merged), the T x C
-// (tile, chunk) units are dealt in equal contiguous ranges to W = R x slots
-// workgroups, R = ceil(T / slots) rounds, so every round is full and only
-// the tiles a range boundary falls into (about one per workgroup) leave a
-// partial block.  Measured against the K-split where the model splits (few
-// tiles per slot): cfg2 k_dist 2.42 vs 2.39 ms (S = 8), one rank of N = 8
-// 8.70 vs 8.56 ms -- the merge was not what the split costs, and the
-// coarser ranges balance worse against k_colrank beside k_dist -- so it is
-// opt-in: FS_STREAMK=1 on R x slots workgroups, FS_STREAMK=w >= 2 on w
-// (tests: ranges spanning many tiles).  Bit-identical to the unsplit pass.
-static int64_t choose_streamk(int64_t tiles, int device, int64_t nchunks, int ksplit) {
-  (void)ksplit;
-  const char* e = std::getenv("FS_STREAMK");
-  const int64_t force = (e && *e) ? std::atoll(e) : 0;
-  if (force <= 0 || tiles <= 0 || nchunks <= 0) return 0;
-  if (force >= 2) return std::min<int64_t>(force, tiles * nchunks);
-  const int64_t slots = kdist_slots(device);
-  if (slots <= 0) return 0;
-  const int64_t rounds = (tiles + slots - 1) / slots;
-  return std::min<int64_t>(rounds * slots, tiles * nchunks);
-}
-
 static int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
@@ -4022,17 +3742,14 @@ static int shard_segments(Plan* g) {
   // (tile, block) units as the target, at least 4096: segments of ~4 tiles
   // amortise each workgroup's row-block stage (tools/cfg2_sweep.sh,
   // profiles/r02/cfg2_sweep.txt: cfg2 step 6.11 -> 5.83 ms at 4096-8192).
-  // v2 sparse: (512-feature block, half) units, two per 512 features
-  const int64_t nfb = !g->sparse       ? (Q.PW + 127) / 128
-                      : g->sparse_v == 1 ? (Q.PW + 255) / 256
-                                         : 2 * ((Q.PW + 511) / 512);
-  int64_t wgs = g->sparse ? std::min<int64_t>(32768, std::max<int64_t>(4096, g->n_tiles * nfb / 4))
-                          : 65536;
-  if (const char* e = std::getenv("FS_PASS2_WGS")) wgs = std::max<int64_t>(256, std::atoll(e));
+  // sparse: (512-feature block, half) units, two per 512 features
+  const int64_t nfb = !g->sparse ? (Q.PW + 127) / 128 : 2 * ((Q.PW + 511) / 512);
+  const int64_t wgs =
+      g->sparse ? std::min<int64_t>(32768, std::max<int64_t>(4096, g->n_tiles * nfb / 4)) : 65536;
   g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + wgs - 1) / wgs);
   g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
-  // partial rows per segment: one per half with the v2 streams
-  g->nsegpart = (g->sparse && g->sparse_v == 2) ? 2 * g->nseg : g->nseg;
+  // partial rows per segment: one per half with the sparse streams
+  g->nsegpart = g->sparse ? 2 * g->nseg : g->nseg;
   if (Q.algo == ALGO_RELIEFF) return FS_OK;
   const size_t need = (size_t)g->nsegpart * Q.PW;
   if (need > g->spart_cap) {
@@ -4055,7 +3772,7 @@ static int shard_segments(Plan* g) {
 static int run_colsort(Plan* g, int64_t c_lo, int64_t c_hi, hipStream_t s) {
   const Prepared& Q = g->P;
   if (c_hi <= c_lo) return FS_OK;
-  if (!colsort_lds(Q.n)) {
+  {
     const size_t need = colsort_scratch_bytes(Q.n, c_hi - c_lo);
     if (need == 0) {
       set_error("mean correction: column sort scratch query failed");
@@ -4186,6 +3903,10 @@ static int plan_layout(Plan* g) {
                             : (double)((const float*)g->colmax.data())[col];
     }
     if (finalize_scale(Q, cmin.data(), cmax.data())) return FS_EINVAL;
+  } else if (set_integer_scale(Q, Q.q16)) {
+    // the integer scale of the operand width in use (a plan switched to
+    // 32-bit operands by plan_decision_guard keeps its ranges)
+    return FS_EINVAL;
   }
   g->key_shift = colsort_key_shift(Q.qmax);
   g->alloc_target = 1;
@@ -4272,12 +3993,6 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
   // tiles: no K-split (partial sums cannot be keyed before they are added)
   const bool dkeys = Q.algo == ALGO_RELIEFF;
   if (dkeys) g->ksplit = 1;
-  g->sk_wgs = 0;
-  if (Q.algo != ALGO_SURF && !dkeys && !std::getenv("FS_KSPLIT")) {
-    g->sk_wgs = choose_streamk(g->n_tiles, g->device, rows_q / kBKQ, g->ksplit);
-    if (g->sk_wgs > 0) g->ksplit = 1;
-  }
-  g->sk_units = g->n_tiles * (rows_q / kBKQ);
   g->kfull = g->ksplit > 1 ? 0 : g->n_tiles;  // k_dist can split only a tail; all or none here
   g->alloc_target = 3;
   int rc = FS_OK;
@@ -4303,7 +4018,6 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
   if (!rc && g->ksplit > 1)
     rc = dalloc(g, &g->Dpart,
                 (size_t)(g->n_tiles - g->kfull) * (g->ksplit - 1) * kTile * kTile);
-  if (!rc && g->sk_wgs > 0) rc = dalloc(g, &g->Dpart, (size_t)g->sk_wgs * kTile * kTile);
   g->alloc_target = 0;
   if (rc) return rc;
   g->nnz_valid = false;
@@ -4415,7 +4129,6 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       (rc = dalloc(g, &g->list, g->list_cap)) || (rc = dalloc(g, &g->list_count, 1)))
     return fail(rc);
   g->sparse = choose_sparse(g, Q);
-  if (const char* e = std::getenv("FS_SPARSE_V")) g->sparse_v = std::atoi(e) == 1 ? 1 : 2;
   if ((rc = setup_shard(g, bi, bj))) return fail(rc);
   trace_mark("plan: hipMalloc");
   std::vector<int32_t> lab(Q.n_pad, -1);
@@ -4502,19 +4215,10 @@ static int run_quantize_dist(Plan* g) {
     const int64_t n_split = g->ksplit > 1 ? g->n_tiles - g->kfull : 0;
     const int64_t n_full = g->n_tiles - n_split;
     const int nck = (int)((Q.q16 ? Q.PC / 2 : Q.PC) / kBKQ), nckd = (int)(Q.PD / kBKQ);
-    if (g->sk_wgs > 0) {
-      k_dist<<<(unsigned)g->sk_wgs, 256, 0, g->stream>>>(
-          g->xqT, Q.n_pad, nck, nckd, Q.SCu, Q.q16, g->tiles, g->n_tiles, 1, g->tiled, g->win,
-          g->D, g->Dpart, g->sk_wgs, g->sk_units, g->Dk, 1.0 / Q.SC);
-      FS_TRY(launch_check("k_dist"));
-      k_dist_merge_sk<<<dim3((unsigned)g->n_tiles, kMergeSlices), 256, 0, g->stream>>>(
-          g->D, g->Dpart, g->tiles, (int64_t)(nck + nckd), g->sk_wgs, g->sk_units, Q.n_pad,
-          g->tiled, g->win);
-      FS_TRY(launch_check("k_dist_merge_sk"));
-    } else {
+    {
       k_dist<<<(unsigned)(n_full + n_split * g->ksplit), 256, 0, g->stream>>>(
           g->xqT, Q.n_pad, nck, nckd, Q.SCu, Q.q16, g->tiles, n_full, g->ksplit, g->tiled,
-          g->win, g->D, g->Dpart, 0, 0, g->Dk, 1.0 / Q.SC);
+          g->win, g->D, g->Dpart, g->Dk, 1.0 / Q.SC);
       FS_TRY(launch_check("k_dist"));
       if (n_split > 0) {
         k_dist_merge<<<dim3((unsigned)n_split, kMergeSlices), 256, 0, g->stream>>>(
@@ -4593,16 +4297,10 @@ static int run_weights(Plan* g, const double* counts, int algo, double inv_sc) {
   if (g->sparse) {
     FS_HIP(hipMemsetAsync(g->nnz, 0, sizeof(unsigned long long), g->stream));
     g->nnz_valid = true;
-    if (g->sparse_v == 2) {
-      k_weights_sparse2<<<(unsigned)g->n_tiles, 64 * kSWaves, 0, g->stream>>>(
-          g->D, Q.n, Q.n_pad, g->tiled, g->win, g->tiles, g->thr, g->lab, counts, algo,
-          Q.use_star, inv_sc, g->r_lo, g->r_hi, g->ent, g->nnz);
-      return launch_check("k_weights_sparse2");
-    }
-    k_weights_sparse<<<(unsigned)g->n_tiles, 64 * kSWaves, 0, g->stream>>>(
-        g->D, Q.n, Q.n_pad, g->tiled, g->win, g->tiles, g->thr, g->lab, counts, algo, Q.use_star,
-        inv_sc, g->r_lo, g->r_hi, g->ent, g->nnz);
-    return launch_check("k_weights_sparse");
+    k_weights_sparse2<<<(unsigned)g->n_tiles, 64 * kSWaves, 0, g->stream>>>(
+        g->D, Q.n, Q.n_pad, g->tiled, g->win, g->tiles, g->thr, g->lab, counts, algo,
+        Q.use_star, inv_sc, g->r_lo, g->r_hi, g->ent, g->nnz);
+    return launch_check("k_weights_sparse2");
   }
   k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiled, g->win,
                                                          g->tiles,
@@ -4612,32 +4310,6 @@ static int run_weights(Plan* g, const double* counts, int algo, double inv_sc) {
   return launch_check("k_weights");
 }
 
-// Sparse pass-2 loop variant (fs_sparse_asm.inc): 1 (default) = 16-entry
-// steps with rows read just in time 12 entries ahead (FS_SPARSE_STREAM_ASM_JIT:
-// twice the scalar-load cover), 0 = the round-1 loop of 8-entry groups with
-// the next group's rows double-buffered.  Same box, alternating, cfg4
-// (tools/jit_ab.sh, profiles/r02/jit_ab.txt): 102.2-102.4 vs 103.0-103.2 ms.
-// FS_SPARSE_JIT=0/1 overrides.
-static int sparse_jit() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = std::getenv("FS_SPARSE_JIT");
-    v = (e && *e) ? (std::atoi(e) != 0) : 1;
-  }
-  return v;
-}
-
-// The generated loop of k_score_sparse2 for continuous feature blocks (1,
-// default) or the plain-HIP walk for every block (0: FS_SPARSE_ASM=0, A/B).
-static int sparse_asm() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = std::getenv("FS_SPARSE_ASM");
-    v = (e && *e) ? (std::atoi(e) != 0) : 1;
-  }
-  return v;
-}
-
 static int run_pass2(Plan* g, double* scores_dev) {
   const Prepared& Q = g->P;
   const int64_t nfb = (Q.PW + 127) / 128;
@@ -4645,7 +4317,7 @@ static int run_pass2(Plan* g, double* scores_dev) {
   if (g->n_tiles == 0) return FS_OK;
   FS_HIP(hipEventRecord(g->ev[2], g->stream));
   const int64_t seg_per_xcd = (g->nseg + kXcds - 1) / kXcds;
-  if (g->sparse && g->sparse_v == 2) {
+  if (g->sparse) {
     // 512-feature blocks, then a tail of at most 256 features in one
     // 256-feature block (a longer tail takes one more, partial, 512-feature
     // block: a block's cost is mostly its entry walk, so one F = 8 block is
@@ -4654,25 +4326,18 @@ static int run_pass2(Plan* g, double* scores_dev) {
     if (Q.PW - nfb8 * 512 > 256) nfb8++;
     const int64_t f_tail = std::min<int64_t>(nfb8 * 512, Q.PW);
     const int64_t nfb4 = (Q.PW - f_tail + 255) / 256;
-    const int use_asm = sparse_asm();
     if (nfb8 > 0) {
       k_score_sparse2<8><<<(unsigned)(kXcds * seg_per_xcd * 2 * nfb8), 64 * kSWaves, 0,
                            g->stream>>>(g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->n_tiles,
-                                        g->seg_len, g->nseg, nfb8, 0, use_asm, g->spart);
+                                        g->seg_len, g->nseg, nfb8, 0, g->spart);
       FS_TRY(launch_check("k_score_sparse2<8>"));
     }
     if (nfb4 > 0) {
       k_score_sparse2<4><<<(unsigned)(kXcds * seg_per_xcd * 2 * nfb4), 64 * kSWaves, 0,
                            g->stream>>>(g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->n_tiles,
-                                        g->seg_len, g->nseg, nfb4, f_tail, use_asm, g->spart);
+                                        g->seg_len, g->nseg, nfb4, f_tail, g->spart);
       FS_TRY(launch_check("k_score_sparse2<4>"));
     }
-  } else if (g->sparse) {
-    const int64_t nfb4 = (Q.PW + 255) / 256;
-    k_score_sparse<<<(unsigned)(kXcds * seg_per_xcd * nfb4), 64 * kSWaves, 0, g->stream>>>(
-        g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->n_tiles, g->seg_len, g->nseg, nfb4, sparse_jit(),
-        g->spart);
-    FS_TRY(launch_check("k_score_sparse"));
   } else {
     k_score<<<(unsigned)(kXcds * seg_per_xcd * nfb), 256, 0, g->stream>>>(
         g->xs, Q.PW, Q.PC, g->tiles, g->Wt, g->n_tiles, g->seg_len, g->nseg, nfb, g->spart);

@@ -128,21 +128,34 @@ void calib_pairs(int64_t n, int64_t pc, int64_t count,
 double calibrated_delta(double model, double SC, double rms, double max_abs);
 // Sort key of a quantised continuous value for the exact per-column order
 // of MultiSURF's mean correction (fs_colsort.hip, fs_cpu.cpp
-// mean_correction): (q << s) | floor((1/2 - eps) * 2^s), monotone in
+// mean_correction): with fx = rint(eps 2^24) (eps = q - t in (-1/2, 1/2]),
+// key = (q << s) | min((2^23 - fx) >> (24 - s), 2^s - 1), monotone in
 // t = q - eps; s = 32 - bits(qmax - 1), at most 24.  The device copy
-// (fs_colsort.hip cs_key) performs the same IEEE operations.
+// (fs_colsort.hip cs_key / cs_fx) computes the same integers.
 inline int colsort_key_shift(double qmax) {
   int b = 0;
   while (b < 32 && std::ldexp(1.0, b) < qmax) b++;
   return 32 - b < 24 ? 32 - b : 24;
 }
-inline uint32_t colsort_key(uint32_t q, float eps, int s) {
-  const double sc = (double)(1u << s);
-  const double f = std::floor((0.5 - (double)eps) * sc);
-  const double m = sc - 1.0;
-  const uint32_t fr = (uint32_t)(f < 0.0 ? 0.0 : (f > m ? m : f));
-  return (q << s) | fr;
+inline int32_t colsort_fx(float eps) { return (int32_t)std::llrint((double)eps * 16777216.0); }
+inline uint32_t colsort_key(uint32_t q, int32_t fx, int s) {
+  const uint32_t fr = (uint32_t)(((1 << 23) - fx) >> (24 - s));
+  const uint32_t m = (1u << s) - 1u;
+  return (q << s) | (fr < m ? fr : m);
 }
+// The per-column order of the mean correction (fs_colsort.hip k_colsort,
+// fs_cpu.cpp mean_correction): samples binned on the key's top 12 bits; a
+// column whose fullest bin holds more than kColsortMaxFill samples is sorted
+// whole, else each sample is ordered within its bin against its neighbours'
+// low 20 key bits, with their eps at 2^-12 of a quantum: the eps code
+// colsort_eq12(fx) = (fx + 2^23) >> 12 clamped to [0, 4095], worth
+// colsort_eq12_fx(q) = (2q + 1) 2^11 - 2^23 in 2^-24 units.
+constexpr int kColsortBins = 4096, kColsortBinShift = 20, kColsortMaxFill = 64;
+inline uint32_t colsort_eq12(int32_t fx) {
+  const int32_t u = fx + (1 << 23);
+  return (uint32_t)(u < 0 ? 0 : (u >= (1 << 24) ? 4095 : (u >> 12)));
+}
+inline int64_t colsort_eq12_fx(uint32_t q) { return (int64_t)(2 * q + 1) * 2048 - (int64_t(1) << 23); }
 int encode_labels_f64(Prepared& P, const double* y);
 int encode_labels_i32(Prepared& P, const int32_t* y);
 
@@ -335,9 +348,10 @@ int sort_pairs(void* list, int64_t count, void* scratch, size_t scratch_bytes, v
 // MultiSURF mean-correction terms of the continuous columns [c_lo, c_hi)
 // from exact per-column order (fs_colsort.hip; colsort_key): epsT[c][i]
 // (quantisation errors, from k_quantize) is overwritten with
-// eps_i (2 k_i - n) - 2 P_i + T.  Columns of n <= 24576 samples sort in LDS
-// (no scratch); larger n needs colsort_scratch_bytes(n, c_hi - c_lo) bytes
-// of device memory.  `stream` is a hipStream_t.
+// eps_i (L_i - G_i) - (E_below - E_above).  Columns of n <= 24576 samples
+// are ordered in LDS, larger n by a device segmented sort; either way the
+// call needs colsort_scratch_bytes(n, c_hi - c_lo) bytes of device scratch.
+// `stream` is a hipStream_t.
 bool colsort_lds(int64_t n);
 size_t colsort_scratch_bytes(int64_t n, int64_t ncols);
 int colsort_terms(const uint32_t* xqT, float* epsT, int64_t n, int64_t n_pad, int64_t c_lo,

@@ -27,7 +27,7 @@ import numpy as np
 import pytest
 
 from conftest import assert_parity_attributed
-from meancorr import exact_row_means, plan_row_means
+from meancorr import assert_means_exact, exact_row_means, plan_row_means
 from test_meancorr import TOL, lognormal, pareto_spikes
 
 pytestmark = pytest.mark.gpu
@@ -71,11 +71,11 @@ def test_gpu_row_means_exact(case):
     try:
         mu = plan_row_means(job)
         q16 = job.plan.calibration()["q16"]
+        sc = job.plan.calibration()["SC"]
     finally:
         job.close()
     ex = exact_row_means(x, recip, isd)
-    rel = np.max(np.abs(mu - ex) / ex)
-    assert rel < 1e-10, (rel, q16)
+    assert_means_exact(mu, ex, sc, q16)
 
 
 def test_gpu_and_cpu_corrections_agree():
@@ -139,3 +139,28 @@ def test_plan_path_runs_the_decision_check():
     r1, rerun1 = _lib.multisurf_last_guard()
     assert rerun1 and r1 == pytest.approx(risk, rel=1e-12)
     np.testing.assert_array_equal(s, one)
+
+
+def test_large_n_route_matches_cpu_at_small_n():
+    """FS_COLSORT_GLOBAL=1 (read once per process, so in a child process)
+    sends every column through the large-n route (device segmented sort +
+    k_colsort_scan); its corrections equal the CPU backend's exactly."""
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np, sys; sys.path[:0] = [%r, %r]\n"
+        "from test_meancorr import lognormal, gaussian\n"
+        "from fastselect_amd import parallel\n"
+        "for X, y in (lognormal(3000, 64, seed=7), gaussian(2000, 100)):\n"
+        "    out = []\n"
+        "    for be in ('cpu', 'gpu'):\n"
+        "        x, yv, recip, isd = parallel.prepare_inputs(X, y, backend=be)\n"
+        "        job = parallel.ShardedMultiSURF(x, yv, recip, isd, backend=be, shard=False)\n"
+        "        job.step(); out.append(job.rowstats.cpu().numpy()[2::3].copy()); job.close()\n"
+        "    d = np.max(np.abs(out[0] - out[1]) / np.maximum(np.abs(out[0]), 1.0))\n"
+        "    assert d < 1e-12, d\n"
+        "print('ok')\n" % (os.path.dirname(HERE), HERE))
+    env = dict(os.environ, FS_COLSORT_GLOBAL="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

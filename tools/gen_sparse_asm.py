@@ -240,7 +240,7 @@ def gen(name="FS_SPARSE_STREAM_ASM", no_ds=False, same_stream=False, feats=4, sp
 
 
 HEADER = """// Generated by tools/gen_sparse_asm.py -- do not edit by hand.
-// Inner loop of k_score_sparse for continuous feature blocks (see the
+// Inner loops of k_score_sparse2 for continuous feature blocks (see the
 // generator's docstring for the layout, the pipeline and the fixed registers).
 """
 
@@ -1160,41 +1160,13 @@ def gen_v2x(name, F=8, lead=3, S=8):
 
 
 if __name__ == "__main__":
+    # The product uses the v2 loops only (k_score_sparse2; round 4 retired the
+    # round-1/2 v1 loop and its A/B variants -- the functions above stay for
+    # the microbenchmarks under tools/ubench and their logs in profiles/).
     path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "fastselect_amd", "csrc",
                         "fs_sparse_asm.inc")
-    text = HEADER + gen()
-    if os.environ.get("FS_GEN_V2X", "0") != "0":   # cross-step lookahead (A/B)
-        text += "\n" + gen_v2x("FS_SPARSE2_ASM_F8", F=8,
-                               lead=int(os.environ.get("FS_GEN_V2_LEAD8", "3")),
-                               S=int(os.environ.get("FS_GEN_V2X", "8")))
-    else:
-        text += "\n" + gen_v2("FS_SPARSE2_ASM_F8", F=8,
-                              lead=int(os.environ.get("FS_GEN_V2_LEAD8", "3")),
-                              diag=os.environ.get("FS_GEN_V2_DIAG", ""),
-                              grp=int(os.environ.get("FS_GEN_V2_GROUP", "1")),
-                              pfn=os.environ.get("FS_GEN_V2_PFN", "0") != "0")
-    text += "\n" + gen_v2("FS_SPARSE2_ASM_F4", F=4,
-                          lead=int(os.environ.get("FS_GEN_V2_LEAD4", "6")),
-                          pfn=os.environ.get("FS_GEN_V2_PFN", "0") != "0")
-    text += "\n" + gen_jit(name="FS_SPARSE_STREAM_ASM_JIT",   # A/B: FS_SPARSE_JIT=1
-                            lead=int(os.environ.get("FS_GEN_JIT_LEAD", "12")),
-                            bank_shift=bool(int(os.environ.get("FS_GEN_BANK_SHIFT", "0"))))
-    # A/B build only (FS_GEN_WARM=<groups>): FS_SPARSE_STREAM_ASM_WARM, an L2
-    # warm-up vector load per group `warm` groups ahead of the scalar load.
-    # Measured at cfg4 (tools/warm_ab.sh, profiles/r02/warm_ab.txt, with a
-    # runtime switch in k_score_sparse): 102.9-103.1 ms against 102.0 without
-    # -- the entry groups already come from L2 (the XCD-aware grid shares a
-    # segment's streams among the workgroups running at once), so the scalar
-    # loads' wait is L2 latency, which this cannot shorten.  Not shipped.
-    if os.environ.get("FS_GEN_WAIT_EVERY"):  # A/B: FS_SPARSE_JIT=2
-        text += "\n" + gen_jit(name="FS_SPARSE_STREAM_ASM_HALF", lead=12,
-                                wait_every=int(os.environ["FS_GEN_WAIT_EVERY"]))
-    if os.environ.get("FS_GEN_HALF_LDS"):  # diagnostic A/B: FS_SPARSE_JIT=2 (wrong scores)
-        text += "\n" + gen_jit(name="FS_SPARSE_STREAM_ASM_HALF", lead=12, half_lds=True)
-    if os.environ.get("FS_GEN_WARM"):
-        text += "\n" + gen(name="FS_SPARSE_STREAM_ASM_WARM", warm=int(os.environ["FS_GEN_WARM"]))
-    if os.environ.get("FS_GEN_LEAD_VARIANTS"):  # A/B build: FS_SPARSE_STREAM_ASM_L<n>
-        for pr in (1, 3):
-            text += "\n" + gen(name=f"FS_SPARSE_STREAM_ASM_P{pr}", prio=pr)
+    text = HEADER
+    text += "\n" + gen_v2("FS_SPARSE2_ASM_F8", F=8, lead=3, pfn=False)
+    text += "\n" + gen_v2("FS_SPARSE2_ASM_F4", F=4, lead=6, pfn=False)
     open(path, "w").write(text)
     print("wrote", os.path.normpath(path))

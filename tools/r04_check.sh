@@ -18,7 +18,7 @@ if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 > "$out/bench.json" 2> "$out/bench.err" || exit $?
 cat "$out/bench.json"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$out/prof" -o run \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$GRAFT_REPO_ROOT/$out/prof" -o run \
   -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-q32 --no-fit \
   > "$GRAFT_REPO_ROOT/$out/prof.log" 2>&1 || exit $?
 find "$GRAFT_REPO_ROOT/$out/prof" -name "*kernel_stats.csv" -exec head -25 {} \;
