@@ -5031,44 +5031,6 @@ namespace fs {
 namespace gpu {
 
 namespace {
-// Barrier of the device threads that also agrees on failure: every thread
-// hands in its status; when one failed, all of them return after the barrier
-// instead of waiting for a peer that will never arrive at the next one.
-class StageBarrier {
- public:
-  explicit StageBarrier(int n) : n_(n) {}
-  bool arrive(int rc, const std::string& err) {
-    std::unique_lock<std::mutex> lk(mu_);
-    if (rc != FS_OK && rc_ == FS_OK) {
-      rc_ = rc;
-      err_ = err;
-    }
-    const uint64_t gen = gen_;
-    if (++count_ == n_) {
-      // the stage's verdict, fixed when the last thread arrives: a faster
-      // thread may fail the NEXT stage (setting rc_) before a slow waiter
-      // wakes, and that waiter must still see this stage as passed
-      count_ = 0;
-      last_ok_ = rc_ == FS_OK;
-      gen_++;
-      cv_.notify_all();
-    } else {
-      cv_.wait(lk, [&] { return gen_ != gen; });
-    }
-    return last_ok_;
-  }
-  int rc() const { return rc_; }
-  const std::string& err() const { return err_; }
-
- private:
-  std::mutex mu_;
-  std::condition_variable cv_;
-  int n_, count_ = 0, rc_ = FS_OK;
-  bool last_ok_ = true;
-  uint64_t gen_ = 0;
-  std::string err_;
-};
-
 // dst[k] = sum over r = 0..N-1, in that order, of parts[r][k]: every device
 // sums the gathered vectors in the same order, so all get bit-identical sums
 __global__ void k_rank_sum(double* __restrict__ dst, const double* __restrict__ parts, int N,

@@ -19,7 +19,9 @@
 #pragma once
 
 #include <cmath>
+#include <condition_variable>
 #include <cstdint>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -311,6 +313,50 @@ int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap,
 }  // namespace cpu
 
 // ---- GPU backend ---------------------------------------------------------
+// Barrier of the device threads that also agrees on failure: every thread
+// hands in its status; when one failed, all of them return after the barrier
+// instead of waiting for a peer that will never arrive at the next one.
+// Status 0 is success (FS_OK).  Host code; tests/native/stage_barrier_check.cpp.
+class StageBarrier {
+ public:
+  explicit StageBarrier(int n) : n_(n) {}
+  bool arrive(int rc, const std::string& err) {
+    std::unique_lock<std::mutex> lk(mu_);
+    if (rc != 0 && rc_ == 0) {
+      rc_ = rc;
+      err_ = err;
+    }
+    const uint64_t gen = gen_;
+    if (++count_ == n_) {
+      // the stage's verdict, fixed when the last thread arrives: a faster
+      // thread may fail the NEXT stage (setting rc_) before a slow waiter
+      // wakes, and that waiter must still see this stage as passed
+      count_ = 0;
+      last_ok_ = rc_ == 0;
+      gen_++;
+      cv_.notify_all();
+    } else {
+      cv_.wait(lk, [&] { return gen_ != gen; });
+    }
+    return last_ok_;
+  }
+  int rc() const { return rc_; }
+  const std::string& err() const { return err_; }
+  int waiting() {  // threads blocked in the current stage (tests)
+    std::lock_guard<std::mutex> lk(mu_);
+    return count_;
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  int n_, count_ = 0, rc_ = 0;
+  bool last_ok_ = true;
+  uint64_t gen_ = 0;
+  std::string err_;
+};
+
+
 namespace gpu {
 int device_count();
 // Device block cache (fs_gpu.hip): dev_alloc hands out a cached block of

@@ -1,12 +1,11 @@
-"""Pass-1 K-split (k_dist + k_dist_merge) and stream-K (k_dist over equal
-(tile, chunk) ranges + k_dist_merge_sk): tiles are split over their feature
-range and the integer partial blocks added afterwards.  Distances are exact
-integers, so every split gives bit-identical scores; forced here
-(FS_KSPLIT=s splits every tile into s parts, 1 disables both; FS_STREAMK=1
-stream-K on the default workgroup count, =w on w workgroups -- ranges that
-span many tiles) against the unsplit job, for the tiled layout (MultiSURF,
-MultiSURF*) and the full layout (ReliefF, MultiSURF's focal-row slices), with
-continuous and discrete chunks in one split range.
+"""Pass-1 K-split (k_dist + k_dist_merge): tiles are split over their
+feature range and the integer partial blocks added afterwards.  Distances are
+exact integers, so every split gives bit-identical scores; forced here
+(FS_KSPLIT=s splits every tile into s parts, 1 disables it) against the
+unsplit job, for the tiled layout (MultiSURF, MultiSURF*) and the full layout
+(ReliefF, MultiSURF's focal-row slices), with continuous and discrete chunks
+in one split range.  (The stream-K variant, measured no faster, was retired
+in round 4.)
 """
 import numpy as np
 import pytest
@@ -24,13 +23,9 @@ def _data(n=1500, p=400, n_disc=40, seed=5):
 
 
 def _scores(monkeypatch, split, fn):
-    """split: None (automatic), an int (FS_KSPLIT) or "sk<w>" (FS_STREAMK=w)."""
-    monkeypatch.delenv("FS_STREAMK", raising=False)
+    """split: None (automatic) or an int (FS_KSPLIT)."""
     if split is None:
         monkeypatch.delenv("FS_KSPLIT", raising=False)
-    elif isinstance(split, str):
-        monkeypatch.delenv("FS_KSPLIT", raising=False)
-        monkeypatch.setenv("FS_STREAMK", split[2:])
     else:
         monkeypatch.setenv("FS_KSPLIT", str(split))
     return fn()
@@ -45,7 +40,7 @@ def test_multisurf_split_is_bit_identical(monkeypatch, use_star):
     fn = lambda: _lib.multisurf_score("gpu", x, yv, recip, None, use_star, isd)
     ref = _scores(monkeypatch, 1, fn)
     # None: the automatic choice (the K-split model: every tile split here)
-    for split in (None, 2, 5, 16, "sk1", "sk7", "sk300"):
+    for split in (None, 2, 5, 16):
         np.testing.assert_array_equal(_scores(monkeypatch, split, fn), ref)
 
 
@@ -56,7 +51,7 @@ def test_multisurf_rows_split_is_bit_identical(monkeypatch):
     x, yv, recip, isd = prepare_inputs(X, y, backend="gpu")
     fn = lambda: _lib.multisurf_score("gpu", x, yv, recip, None, False, isd, rows=(100, 700))
     ref = _scores(monkeypatch, 1, fn)
-    for split in (None, 3, "sk1", "sk5"):
+    for split in (None, 3):
         np.testing.assert_array_equal(_scores(monkeypatch, split, fn), ref)
 
 
@@ -67,18 +62,18 @@ def test_relieff_split_is_bit_identical(monkeypatch):
     x, ye, recip, isd, priors = relieff_inputs(X, y, 10, "gpu")
     fn = lambda: _lib.relieff_score("gpu", x, ye, recip, isd, 10, priors)
     ref = _scores(monkeypatch, 1, fn)
-    for split in (None, 4, "sk1", "sk9"):
+    for split in (None, 4):
         np.testing.assert_array_equal(_scores(monkeypatch, split, fn), ref)
 
 
-def test_streamk_many_tiles_is_bit_identical(monkeypatch):
+def test_ksplit_many_tiles_is_bit_identical(monkeypatch):
     """More tiles than one round of workgroups (872 tiles; MultiSURF, 32-bit
-    pass 1): stream-K on two rounds of workgroups and on forced ranges."""
+    pass 1), split and unsplit."""
     from fastselect_amd import _lib
     from fastselect_amd.parallel import prepare_inputs
     X, y = _data(n=5300, p=150, n_disc=20)
     x, yv, recip, isd = prepare_inputs(X, y, backend="gpu")
     fn = lambda: _lib.multisurf_score("gpu", x, yv, recip, None, False, isd)
     ref = _scores(monkeypatch, 1, fn)
-    for split in (None, "sk1", "sk1000", "sk2000"):
+    for split in (None, 3, 8):
         np.testing.assert_array_equal(_scores(monkeypatch, split, fn), ref)
