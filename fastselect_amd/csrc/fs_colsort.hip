@@ -110,7 +110,8 @@ __device__ __forceinline__ long long cs_block_scan(long long v, long long* wsum,
 // (count << 44 | sum of (eps_fx + 2^23): one 64-bit LDS add per sample).
 constexpr int kBins = 4096, kBinShift = 20;
 constexpr int kHistShift = 44;
-constexpr int kMaxBinFill = 64;  // larger bins: the column takes the full sort
+constexpr int kMaxBinFill = 64;  // larger mixed bins: the column takes the full sort
+constexpr uint32_t kPureEmpty = 0x7FFFFFFFu, kMixed = 0x80000000u, kPure = 0x80000000u;
 
 __device__ __forceinline__ unsigned long long cs_code(int32_t fx) {
   return (1ull << kHistShift) + (unsigned long long)(uint32_t)(fx + (1 << 23));
@@ -175,17 +176,22 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort_full(const uint32_t* __r
 // bin's packed entries: low key bits and eps at 2^-12 of a quantum); equal
 // keys are ties (zero sign, whatever the order).  So the order is exact and
 // only the eps of a sample's bin neighbours is rounded (<= 2^-13 of a quantum
-// each).  Typical data put a handful of samples in a bin (cfg4: ~17); a
-// column with a bin holding more than kMaxBinFill (one extreme value setting
-// the range, integer levels) is left to k_colsort_full.  Cost: one
+// each).  Typical data put a handful of samples in a bin (cfg4: ~17); a bin
+// whose samples all share one key (integer levels, a value grid) needs no
+// within-bin work at any size; a column with a mixed bin holding more than
+// kMaxBinFill (one extreme value setting the range) is left to
+// k_colsort_full.  Cost: one
 // histogram pass instead of four radix passes (round-4 first cut: the full
 // sort of every column, 9.9 ms at cfg4 alone and ~8 ms of the step beside
 // k_dist).
 template <int IPT>
 struct ColbinSmem {
   unsigned long long hist[kBins];  // exclusive prefix after the scan
-  uint32_t cur[kBins];             // scatter cursors
-  uint32_t seg[kCsThreads * IPT];  // samples of bins holding >= 2, in bin order
+  // hist pass: the bin's first low key (kPureEmpty: none yet) | kMixed once a
+  // different one arrives; after the scan: the scatter cursor | kPure for a
+  // bin whose samples all share one key (its within-bin terms are zero)
+  uint32_t cur[kBins];
+  alignas(16) uint32_t seg[kCsThreads * IPT + 4];  // samples of bins holding >= 2, bin order
   long long wsum[kCsThreads / 64];
   int max_fill;
 };
@@ -206,7 +212,10 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
   // spilled at n = 20000)
   uint32_t key[IPT];
   int32_t fx[IPT];
-  for (int b = tid; b < kBins; b += kCsThreads) sm.hist[b] = 0ull;
+  for (int b = tid; b < kBins; b += kCsThreads) {
+    sm.hist[b] = 0ull;
+    sm.cur[b] = kPureEmpty;
+  }
   if (tid == 0) sm.max_fill = 0;
   // every load of the column issued before any is used (one memory latency
   // per column, not one per sample): the operand word and the eps bits, at
@@ -228,19 +237,29 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
   __builtin_amdgcn_sched_barrier(0);
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < IPT; k++)
-    if (tid + kCsThreads * k < nn) atomicAdd(&sm.hist[key[k] >> kBinShift], cs_code(fx[k]));
+  for (int k = 0; k < IPT; k++) {
+    if (tid + kCsThreads * k >= nn) continue;
+    const int b = (int)(key[k] >> kBinShift);
+    atomicAdd(&sm.hist[b], cs_code(fx[k]));
+    const uint32_t kl = key[k] & ((1u << kBinShift) - 1u);
+    const uint32_t old = atomicCAS(&sm.cur[b], kPureEmpty, kl);
+    if (old != kPureEmpty && (old & ((1u << kBinShift) - 1u)) != kl) atomicOr(&sm.cur[b], kMixed);
+  }
   __syncthreads();
-  // exclusive scan of the packed counters, 4 bins per thread; the fullest bin
+  // exclusive scan of the packed counters, 4 bins per thread; the fullest
+  // mixed bin
   constexpr int kPer = kBins / kCsThreads;
   unsigned long long loc[kPer], run = 0;
+  uint32_t pure_bits = 0;
   int fill = 0;
 #pragma unroll
   for (int q = 0; q < kPer; q++) {
     const unsigned long long v = sm.hist[tid * kPer + q];
+    const bool mixed = (sm.cur[tid * kPer + q] & kMixed) != 0u;
     loc[q] = run;
     run += v;
-    fill = max(fill, (int)(v >> kHistShift));
+    if (mixed) fill = max(fill, (int)(v >> kHistShift));
+    else pure_bits |= 1u << q;
   }
   long long tot_packed;
   const unsigned long long pre = (unsigned long long)cs_block_scan((long long)run, sm.wsum, tot_packed);
@@ -248,7 +267,7 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
   for (int q = 0; q < kPer; q++) {
     const unsigned long long ex = pre + loc[q];
     sm.hist[tid * kPer + q] = ex;
-    sm.cur[tid * kPer + q] = (uint32_t)(ex >> kHistShift);
+    sm.cur[tid * kPer + q] = (uint32_t)(ex >> kHistShift) | ((pure_bits >> q) & 1u ? kPure : 0u);
   }
   atomicMax(&sm.max_fill, fill);
   __syncthreads();
@@ -264,7 +283,7 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
     const int b = (int)(key[k] >> kBinShift);
     const uint32_t c_lo_b = (uint32_t)(sm.hist[b] >> kHistShift);
     const uint32_t c_hi_b = b + 1 < kBins ? (uint32_t)(sm.hist[b + 1] >> kHistShift) : (uint32_t)nn;
-    if (c_hi_b - c_lo_b < 2) continue;
+    if (c_hi_b - c_lo_b < 2 || (sm.cur[b] & kPure)) continue;
     const uint32_t pos = atomicAdd(&sm.cur[b], 1u);
     sm.seg[pos] = ((key[k] & ((1u << kBinShift) - 1u)) << 12) | cs_eq12_of_fx(fx[k]);
     __builtin_amdgcn_sched_barrier(0);
@@ -282,19 +301,27 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
     cs_decode(lo, c_below, e_below);
     cs_decode(hi, c_to, e_to);
     long long L = c_below, G = nn - c_to, Eb = e_below, Ea = T - e_to;
-    if (c_to - c_below >= 2) {
+    // (bin cursors are final after the scatter's barrier; a pure bin's
+    // samples all tie)
+    if (c_to - c_below >= 2 && !(sm.cur[b] & kPure)) {
       const uint32_t mine = key[k] & ((1u << kBinShift) - 1u);
       int l = 0, g = 0, sl = 0, sg = 0;  // within-bin counts and eps codes (<= 64 x 4095)
-      for (int j = (int)c_below; j < (int)c_to; j++) {
-        const uint32_t ent = sm.seg[j];
-        const uint32_t kl = ent >> 12;
-        const int q = (int)(ent & 0xFFFu);
-        if (kl < mine) {
-          l++;
-          sl += q;
-        } else if (kl > mine) {
-          g++;
-          sg += q;
+      // the bin's entries four at a time (16-byte aligned ds_read_b128,
+      // entries outside [c_below, c_to) masked off)
+      const int j0 = (int)c_below, j1 = (int)c_to;
+      for (int j = j0 & ~3; j < j1; j += 4) {
+        const uint4 v = *(const uint4*)&sm.seg[j];
+        const uint32_t ev4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const bool in = j + u >= j0 && j + u < j1;
+          const uint32_t kl = ev4[u] >> 12;
+          const int q = (int)(ev4[u] & 0xFFFu);
+          const bool lt = in && kl < mine, gt = in && kl > mine;
+          l += lt ? 1 : 0;
+          sl += lt ? q : 0;
+          g += gt ? 1 : 0;
+          sg += gt ? q : 0;
         }
       }
       // eps code q is worth (2q + 1) 2^11 - 2^23 in 2^-24 units

@@ -168,8 +168,8 @@ static void distances(const Prepared& P, const std::vector<uint32_t>& xq, int ra
 // Binned on the key's top 12 bits, a sample is ordered exactly against every
 // other bin by the bin counts and fixed-point eps sums, and within its own
 // bin against its neighbours' low key bits (their eps at 2^-12 of a quantum,
-// equal keys tied); a column with a bin fuller than kColsortMaxFill is
-// sorted whole instead (std::sort on (key, index), as the GPU's stable sort),
+// equal keys tied; a bin whose samples share one key needs nothing); a
+// column with a mixed bin fuller than kColsortMaxFill is sorted whole instead (std::sort on (key, index), as the GPU's stable sort),
 // where position k, the eps prefix P before it and the column total T give
 //   term_i = eps_i (2k - n) - 2 P + T.
 // Either way term_i = eps_i (L - G) - (E_below - E_above), and
@@ -188,17 +188,23 @@ static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
     std::vector<uint32_t> key((size_t)n);
     std::vector<int64_t> fx((size_t)n);
     std::vector<int64_t> cnt(kColsortBins + 1, 0), esum(kColsortBins + 1, 0);
+    // per bin: first low key seen, and whether another one followed (mixed)
+    std::vector<uint32_t> first(kColsortBins, 0xFFFFFFFFu);
+    std::vector<char> mixed(kColsortBins, 0);
     int64_t T = 0;
     for (int64_t i = 0; i < n; i++) {
       fx[i] = colsort_fx(eps[(size_t)i * P.PW + c]);
       key[i] = colsort_key(xq[(size_t)i * P.PW + c], (int32_t)fx[i], s);
-      cnt[(key[i] >> kColsortBinShift) + 1]++;
-      esum[(key[i] >> kColsortBinShift) + 1] += fx[i];
+      const uint32_t b = key[i] >> kColsortBinShift, kl = key[i] & ((1u << kColsortBinShift) - 1u);
+      cnt[b + 1]++;
+      esum[b + 1] += fx[i];
       T += fx[i];
+      if (first[b] == 0xFFFFFFFFu) first[b] = kl;
+      else if (first[b] != kl) mixed[b] = 1;
     }
     int64_t fill = 0;
     for (int b = 0; b < kColsortBins; b++) {
-      fill = std::max(fill, cnt[b + 1]);
+      if (mixed[b]) fill = std::max(fill, cnt[b + 1]);
       cnt[b + 1] += cnt[b];     // exclusive prefix at b, inclusive at b + 1
       esum[b + 1] += esum[b];
     }
@@ -218,14 +224,14 @@ static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
     std::vector<uint32_t> seg((size_t)n), cur(cnt.begin(), cnt.end() - 1);
     for (int64_t i = 0; i < n; i++) {
       const uint32_t b = key[i] >> kColsortBinShift;
-      if (cnt[b + 1] - cnt[b] < 2) continue;
+      if (cnt[b + 1] - cnt[b] < 2 || !mixed[b]) continue;
       seg[cur[b]++] = ((key[i] & ((1u << kColsortBinShift) - 1u)) << 12) |
                       colsort_eq12((int32_t)fx[i]);
     }
     for (int64_t i = 0; i < n; i++) {
       const uint32_t b = key[i] >> kColsortBinShift;
       int64_t L = cnt[b], G = n - cnt[b + 1], Eb = esum[b], Ea = T - esum[b + 1];
-      if (cnt[b + 1] - cnt[b] >= 2) {
+      if (cnt[b + 1] - cnt[b] >= 2 && mixed[b]) {  // a pure bin's samples all tie
         const uint32_t mine = key[i] & ((1u << kColsortBinShift) - 1u);
         for (int64_t j = cnt[b]; j < cnt[b + 1]; j++) {
           const uint32_t kl = seg[j] >> 12;
