@@ -111,7 +111,7 @@ __device__ __forceinline__ long long cs_block_scan(long long v, long long* wsum,
 constexpr int kBins = 4096, kBinShift = 20;
 constexpr int kHistShift = 44;
 constexpr int kMaxBinFill = 64;  // larger mixed bins: the column takes the full sort
-constexpr uint32_t kPureEmpty = 0x7FFFFFFFu, kMixed = 0x80000000u, kPure = 0x80000000u;
+constexpr uint32_t kPureEmpty = 0x7FFFFFFFu, kMixed = 0x80000000u;
 
 __device__ __forceinline__ unsigned long long cs_code(int32_t fx) {
   return (1ull << kHistShift) + (unsigned long long)(uint32_t)(fx + (1 << 23));
@@ -172,29 +172,53 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort_full(const uint32_t* __r
 // on the key's top 12 bits (4096 bins, counts and fixed-point eps sums by
 // 64-bit LDS adds, one scan): a sample's order against every other bin is
 // exact from the scanned bin counters.  Within its own bin it is ordered by
-// the key's low 20 bits against the bin's other samples (a loop over the
-// bin's packed entries: low key bits and eps at 2^-12 of a quantum); equal
-// keys are ties (zero sign, whatever the order).  So the order is exact and
-// only the eps of a sample's bin neighbours is rounded (<= 2^-13 of a quantum
-// each).  Typical data put a handful of samples in a bin (cfg4: ~17); a bin
-// whose samples all share one key (integer levels, a value grid) needs no
+// the key's low 20 bits against the bin's other samples (their packed
+// entries: low key bits and eps at 2^-12 of a quantum); equal keys are ties
+// (zero sign, whatever the order).  So the order is exact and only the eps
+// of a sample's bin neighbours is rounded (<= 2^-13 of a quantum each).
+// Typical data put a handful of samples in a bin (cfg4: ~17); a bin whose
+// samples all share one key (integer levels, a value grid) needs no
 // within-bin work at any size; a column with a mixed bin holding more than
 // kMaxBinFill (one extreme value setting the range) is left to
-// k_colsort_full.  Cost: one
-// histogram pass instead of four radix passes (round-4 first cut: the full
-// sort of every column, 9.9 ms at cfg4 alone and ~8 ms of the step beside
-// k_dist).
+// k_colsort_full.
+//
+// Phases (barriers between): (1) keys, bin counters, per-bin purity;
+// (2) scan, bin cursors, bitmaps of bin starts and of positions that need
+// no within-bin work; (3) scatter of the mixed bins' entries in bin order;
+// (4) within-bin counts by POSITION: lane j of the sorted layout compares
+// its entry with its bin's entries -- the lanes of a wave cover 64
+// consecutive positions, i.e. one or a few neighbouring bins, so they loop
+// alike and read the same LDS words -- and leaves (l - g, sl - sg) packed
+// in its slot; (5) each sample's term from the bin counters and its slot.
 template <int IPT>
 struct ColbinSmem {
   unsigned long long hist[kBins];  // exclusive prefix after the scan
-  // hist pass: the bin's first low key (kPureEmpty: none yet) | kMixed once a
-  // different one arrives; after the scan: the scatter cursor | kPure for a
-  // bin whose samples all share one key (its within-bin terms are zero)
+  // after the scan: the scatter cursor of bin b | kSkip (pure or single)
   uint32_t cur[kBins];
-  alignas(16) uint32_t seg[kCsThreads * IPT + 4];  // samples of bins holding >= 2, bin order
+  // phase 1: seg[b] = bin b's first low key | kMixed once another arrives;
+  // phases 3-4: the mixed bins' entries (low key << 12 | eps code) in bin
+  // order at their sorted positions; phase 5: the packed within-bin counts
+  alignas(16) uint32_t seg[(kCsThreads * IPT > kBins ? kCsThreads * IPT : kBins) + 4];
+  uint32_t starts[(kCsThreads * IPT + 31) / 32];  // bit p: a non-empty bin starts at p
+  uint32_t skip[(kCsThreads * IPT + 31) / 32];    // bit p: p's bin is pure or single
   long long wsum[kCsThreads / 64];
   int max_fill;
 };
+
+constexpr uint32_t kSkip = 0x80000000u;
+
+// Hides a value's origin from the compiler, so that what a later phase
+// derives from it is computed there instead of being kept live (spilled)
+// from an earlier phase.
+#define FS_OPAQUE(v) asm volatile("" : "+v"(v))
+
+// (l - g, sl - sg) of a within-bin comparison, one word: d in [-64, 64],
+// ds in [-64 * 4095, 64 * 4095]
+__device__ __forceinline__ int32_t cs_pack(int d, int ds) { return ds * 256 + (d + 128); }
+__device__ __forceinline__ void cs_unpack(int32_t r, int& d, int& ds) {
+  d = (r & 255) - 128;
+  ds = r >> 8;
+}
 
 template <int IPT>
 __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restrict__ xqT,
@@ -202,73 +226,96 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
                                                         int64_t c_lo, int* __restrict__ crowded,
                                                         float* __restrict__ epsT) {
   __shared__ ColbinSmem<IPT> sm;
+  constexpr int kWords = (kCsThreads * IPT + 31) / 32;
   const int tid = threadIdx.x;
   const int64_t c = c_lo + blockIdx.x;
   float* __restrict__ e = epsT + c * n_pad;
-  const int nn = (int)n;  // < 2^20 (plan_create)
-  // samples i = tid + 1024 k (coalesced), key and fixed-point eps held in
-  // registers for the three passes; a sched_barrier between samples keeps
-  // the compiler from hoisting every sample's LDS reads at once (which
-  // spilled at n = 20000)
+  const int nn = (int)n;  // <= 1024 IPT (colsort_lds)
   uint32_t key[IPT];
   int32_t fx[IPT];
   for (int b = tid; b < kBins; b += kCsThreads) {
     sm.hist[b] = 0ull;
-    sm.cur[b] = kPureEmpty;
+    sm.seg[b] = kPureEmpty;
+  }
+  for (int w = tid; w < kWords; w += kCsThreads) {
+    sm.starts[w] = 0u;
+    sm.skip[w] = 0u;
   }
   if (tid == 0) sm.max_fill = 0;
   // every load of the column issued before any is used (one memory latency
-  // per column, not one per sample): the operand word and the eps bits, at
-  // indices clamped into [0, n) (the extra samples are masked below)
-  const uint32_t* __restrict__ qrow = xqT + (q16 ? (c >> 1) : c) * n_pad;
+  // per column): the operand word and the eps bits of samples tid + 1024 k
+  // through buffer descriptors of the column's n words (one 32-bit offset
+  // per thread instead of a 64-bit address per sample; reads past n give 0,
+  // those samples are masked below)
+  const __amdgpu_buffer_rsrc_t qbuf = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(xqT + (q16 ? (c >> 1) : c) * n_pad), (short)0, nn * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t ebuf =
+      __builtin_amdgcn_make_buffer_rsrc((void*)e, (short)0, nn * 4, 0x00020000);
+  const int voff = tid * 4;
   const uint32_t qsh = q16 ? (uint32_t)(c & 1) * 16u : 0u;
   const uint32_t qmask = q16 ? 0xFFFFu : 0xFFFFFFFFu;
 #pragma unroll
   for (int k = 0; k < IPT; k++) {
-    const int i = min(tid + kCsThreads * k, nn - 1);
-    key[k] = qrow[i];
-    fx[k] = __float_as_int(e[i]);
+    key[k] = __builtin_amdgcn_raw_buffer_load_b32(qbuf, voff, kCsThreads * 4 * k, 0);
+    fx[k] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ebuf, voff, kCsThreads * 4 * k, 0);
   }
 #pragma unroll
   for (int k = 0; k < IPT; k++) {
     fx[k] = cs_fx(__int_as_float(fx[k]));
     key[k] = cs_key((key[k] >> qsh) & qmask, fx[k], s);
   }
-  __builtin_amdgcn_sched_barrier(0);
   __syncthreads();
+  // (1) bin counters and purity
 #pragma unroll
   for (int k = 0; k < IPT; k++) {
     if (tid + kCsThreads * k >= nn) continue;
     const int b = (int)(key[k] >> kBinShift);
     atomicAdd(&sm.hist[b], cs_code(fx[k]));
     const uint32_t kl = key[k] & ((1u << kBinShift) - 1u);
-    const uint32_t old = atomicCAS(&sm.cur[b], kPureEmpty, kl);
-    if (old != kPureEmpty && (old & ((1u << kBinShift) - 1u)) != kl) atomicOr(&sm.cur[b], kMixed);
+    const uint32_t old = atomicCAS(&sm.seg[b], kPureEmpty, kl);
+    if (old != kPureEmpty && (old & ((1u << kBinShift) - 1u)) != kl) atomicOr(&sm.seg[b], kMixed);
   }
   __syncthreads();
-  // exclusive scan of the packed counters, 4 bins per thread; the fullest
-  // mixed bin
+  // (2) exclusive scan of the packed counters, 4 bins per thread; the
+  // fullest mixed bin
   constexpr int kPer = kBins / kCsThreads;
   unsigned long long loc[kPer], run = 0;
-  uint32_t pure_bits = 0;
+  uint32_t skip_bits = 0;
   int fill = 0;
 #pragma unroll
   for (int q = 0; q < kPer; q++) {
     const unsigned long long v = sm.hist[tid * kPer + q];
-    const bool mixed = (sm.cur[tid * kPer + q] & kMixed) != 0u;
+    const bool mixed = (sm.seg[tid * kPer + q] & kMixed) != 0u;
     loc[q] = run;
     run += v;
     if (mixed) fill = max(fill, (int)(v >> kHistShift));
-    else pure_bits |= 1u << q;
+    else skip_bits |= 1u << q;  // pure, single or empty
   }
   long long tot_packed;
   const unsigned long long pre = (unsigned long long)cs_block_scan((long long)run, sm.wsum, tot_packed);
 #pragma unroll
   for (int q = 0; q < kPer; q++) {
     const unsigned long long ex = pre + loc[q];
-    sm.hist[tid * kPer + q] = ex;
-    sm.cur[tid * kPer + q] = (uint32_t)(ex >> kHistShift) | ((pure_bits >> q) & 1u ? kPure : 0u);
+    const uint32_t lo = (uint32_t)(ex >> kHistShift);
+    const uint32_t m = (uint32_t)(sm.hist[tid * kPer + q] >> kHistShift);  // not yet overwritten
+    const bool skip = ((skip_bits >> q) & 1u) != 0u;
+    sm.cur[tid * kPer + q] = lo | (skip ? kSkip : 0u);
+    if (m != 0u) {
+      atomicOr(&sm.starts[lo >> 5], 1u << (lo & 31));
+      if (skip) {  // every position of the bin
+        const uint32_t hi = lo + m;
+        for (uint32_t w = lo >> 5; w <= (hi - 1) >> 5; w++) {
+          const uint32_t a = w == (lo >> 5) ? (lo & 31) : 0u;
+          const uint32_t z = w == ((hi - 1) >> 5) ? ((hi - 1) & 31) : 31u;
+          const uint32_t bits = (0xFFFFFFFFu >> (31u - z)) & (0xFFFFFFFFu << a);
+          atomicOr(&sm.skip[w], bits);
+        }
+      }
+    }
   }
+  __syncthreads();  // every bin's count read before any prefix is written
+#pragma unroll
+  for (int q = 0; q < kPer; q++) sm.hist[tid * kPer + q] = pre + loc[q];
   atomicMax(&sm.max_fill, fill);
   __syncthreads();
   const bool crowd = sm.max_fill > kMaxBinFill;  // uniform
@@ -276,61 +323,101 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
   if (crowd) return;  // k_colsort_full writes this column's terms
   long long n_all, T;
   cs_decode((unsigned long long)tot_packed, n_all, T);
-  // bins holding >= 2 samples: their packed entries in bin order
+  // (3) the mixed bins' entries at their sorted positions; from here on a
+  // sample keeps only its bin and position (0xFFFF: no within-bin work) in
+  // one register, its eps is read again in (5)
+  int t3 = tid;
+  FS_OPAQUE(t3);
 #pragma unroll
   for (int k = 0; k < IPT; k++) {
-    if (tid + kCsThreads * k >= nn) continue;
-    const int b = (int)(key[k] >> kBinShift);
-    const uint32_t c_lo_b = (uint32_t)(sm.hist[b] >> kHistShift);
-    const uint32_t c_hi_b = b + 1 < kBins ? (uint32_t)(sm.hist[b + 1] >> kHistShift) : (uint32_t)nn;
-    if (c_hi_b - c_lo_b < 2 || (sm.cur[b] & kPure)) continue;
-    const uint32_t pos = atomicAdd(&sm.cur[b], 1u);
-    sm.seg[pos] = ((key[k] & ((1u << kBinShift) - 1u)) << 12) | cs_eq12_of_fx(fx[k]);
-    __builtin_amdgcn_sched_barrier(0);
+    FS_OPAQUE(key[k]);
+    FS_OPAQUE(fx[k]);
+    const uint32_t b = key[k] >> kBinShift;
+    uint32_t pos = 0xFFFFu;
+    if (t3 + kCsThreads * k < nn && !(sm.cur[b] & kSkip)) {
+      pos = atomicAdd(&sm.cur[b], 1u);
+      sm.seg[pos] = ((key[k] & ((1u << kBinShift) - 1u)) << 12) | cs_eq12_of_fx(fx[k]);
+    }
+    key[k] = (b << 16) | pos;
+    FS_OPAQUE(key[k]);  // packed here, not re-derived from b and pos later
+    __builtin_amdgcn_sched_barrier(0);  // one sample at a time (no hoisted reads)
   }
   __syncthreads();
-  // terms (each sample's eps is overwritten by the thread that read it)
+  // (4) within-bin counts by position: packed sums of (eps code + 2^20) over
+  // the bin's entries below (lt) / not above (le) / all; g = all - le, so
+  // ties (own entry included) cancel
+  int32_t res[IPT];
+  int t4 = tid;
+  FS_OPAQUE(t4);
 #pragma unroll
   for (int k = 0; k < IPT; k++) {
-    const int i = tid + kCsThreads * k;
+    const int j = t4 + kCsThreads * k;
+    res[k] = 0;
+    if (j >= nn || ((sm.skip[j >> 5] >> (j & 31)) & 1u)) continue;
+    // bin start: the last start bit at or before j (<= 64 positions back)
+    int w = j >> 5;
+    uint32_t bits = sm.starts[w] & (0xFFFFFFFFu >> (31 - (j & 31)));
+    while (bits == 0u) bits = sm.starts[--w];
+    const int lo = w * 32 + 31 - __clz(bits);
+    // bin end: the next start bit after j, or n
+    int hi = nn;
+    w = j >> 5;
+    bits = (j & 31) == 31 ? 0u : sm.starts[w] & (0xFFFFFFFFu << ((j & 31) + 1));
+    while (bits == 0u && ++w < kWords && w * 32 < nn) bits = sm.starts[w];
+    if (bits != 0u) hi = min(nn, w * 32 + __ffs(bits) - 1);
+    const uint32_t v = sm.seg[j];
+    const uint32_t mine_lo = v & ~0xFFFu, mine_hi = v | 0xFFFu;
+    uint32_t a_lt = 0u, a_le = 0u, a_all = 0u;
+    for (int jj = lo; jj < hi; jj++) {
+      const uint32_t u = sm.seg[jj];
+      const uint32_t wv = (u & 0xFFFu) | (1u << 20);
+      a_lt += u < mine_lo ? wv : 0u;
+      a_le += u <= mine_hi ? wv : 0u;
+      a_all += wv;
+    }
+    const int l = (int)(a_lt >> 20), sl = (int)(a_lt & 0xFFFFFu);
+    const int g = (int)(a_all >> 20) - (int)(a_le >> 20);
+    const int sg = (int)(a_all & 0xFFFFFu) - (int)(a_le & 0xFFFFFu);
+    res[k] = cs_pack(l - g, sl - sg);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __syncthreads();  // every entry read
+#pragma unroll
+  for (int k = 0; k < IPT; k++) {
+    const int j = t4 + kCsThreads * k;
+    if (j < nn && !((sm.skip[j >> 5] >> (j & 31)) & 1u)) sm.seg[j] = (uint32_t)res[k];
+  }
+  __syncthreads();
+  // (5) terms (each sample's eps is overwritten by the thread that read it)
+#pragma unroll
+  for (int k = 0; k < IPT; k++)
+    fx[k] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ebuf, voff, kCsThreads * 4 * k, 0);
+  int t5 = tid;
+  FS_OPAQUE(t5);
+#pragma unroll
+  for (int k = 0; k < IPT; k++) {
+    FS_OPAQUE(key[k]);
+    const int i = t5 + kCsThreads * k;
     if (i >= nn) continue;
-    const int b = (int)(key[k] >> kBinShift);
+    const int32_t f = cs_fx(__int_as_float(fx[k]));
+    const int b = (int)(key[k] >> 16);
     const unsigned long long lo = sm.hist[b];
     const unsigned long long hi = b + 1 < kBins ? sm.hist[b + 1] : (unsigned long long)tot_packed;
     long long c_below, e_below, c_to, e_to;
     cs_decode(lo, c_below, e_below);
     cs_decode(hi, c_to, e_to);
-    long long L = c_below, G = nn - c_to, Eb = e_below, Ea = T - e_to;
-    // (bin cursors are final after the scatter's barrier; a pure bin's
-    // samples all tie)
-    if (c_to - c_below >= 2 && !(sm.cur[b] & kPure)) {
-      const uint32_t mine = key[k] & ((1u << kBinShift) - 1u);
-      int l = 0, g = 0, sl = 0, sg = 0;  // within-bin counts and eps codes (<= 64 x 4095)
-      // the bin's entries four at a time (16-byte aligned ds_read_b128,
-      // entries outside [c_below, c_to) masked off)
-      const int j0 = (int)c_below, j1 = (int)c_to;
-      for (int j = j0 & ~3; j < j1; j += 4) {
-        const uint4 v = *(const uint4*)&sm.seg[j];
-        const uint32_t ev4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-          const bool in = j + u >= j0 && j + u < j1;
-          const uint32_t kl = ev4[u] >> 12;
-          const int q = (int)(ev4[u] & 0xFFFu);
-          const bool lt = in && kl < mine, gt = in && kl > mine;
-          l += lt ? 1 : 0;
-          sl += lt ? q : 0;
-          g += gt ? 1 : 0;
-          sg += gt ? q : 0;
-        }
-      }
-      // eps code q is worth (2q + 1) 2^11 - 2^23 in 2^-24 units
-      L += l;
-      G += g;
-      Eb += (long long)(2 * sl + l) * 2048 - (long long)l * (1ll << 23);
-      Ea += (long long)(2 * sg + g) * 2048 - (long long)g * (1ll << 23);
+    // L - G and Eb - Ea over the other bins, then the within-bin part: an
+    // eps code q is worth (2q + 1) 2^11 - 2^23 in 2^-24 units
+    long long dLG = c_below - (nn - c_to), dE = e_below - (T - e_to);
+    const uint32_t pos = key[k] & 0xFFFFu;
+    if (pos != 0xFFFFu) {
+      int d, ds;
+      cs_unpack((int32_t)sm.seg[pos], d, ds);
+      dLG += d;
+      dE += (long long)(2 * ds + d) * 2048 - (long long)d * (1ll << 23);
     }
-    e[i] = (float)((double)((long long)fx[k] * (L - G) - (Eb - Ea)) * (1.0 / kEpsFx));
+    const float term = (float)((double)((long long)f * dLG - dE) * (1.0 / kEpsFx));
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(term), ebuf, voff, kCsThreads * 4 * k, 0);
     __builtin_amdgcn_sched_barrier(0);
   }
 }

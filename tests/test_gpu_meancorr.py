@@ -28,7 +28,7 @@ import pytest
 
 from conftest import assert_parity_attributed
 from meancorr import assert_means_exact, exact_row_means, plan_row_means
-from test_meancorr import TOL, lognormal, pareto_spikes
+from test_meancorr import TOL, gaussian, lognormal, pareto_spikes
 
 pytestmark = pytest.mark.gpu
 
@@ -78,14 +78,33 @@ def test_gpu_row_means_exact(case):
     assert_means_exact(mu, ex, sc, q16)
 
 
-def test_gpu_and_cpu_corrections_agree():
-    """Same keys, same stable order, integer eps sums on both backends: the
-    per-row corrections differ only by k_rowcorr's float64 summation order."""
-    X, y = lognormal(3000, 2000)
+def _grid_columns(n, p, seed=9):
+    """Integer levels (bins of one key: no within-bin work at any size) with
+    2% of the samples nudged off their level (mixed bins of a few samples)."""
+    rng = np.random.default_rng(seed)
+    X = rng.integers(0, 40, (n, p)).astype(np.float32) * 25.0
+    X += (rng.random((n, p)) < 0.02) * rng.random((n, p)).astype(np.float32)
+    return X.astype(np.float32), rng.integers(0, 2, n)
+
+
+CORR_CASES = {
+    "lognormal_3000x2000_crowded": lambda: lognormal(3000, 2000),
+    "gaussian_3000x500_binned": lambda: gaussian(3000, 500),
+    "grid_3000x300_pure_and_mixed_bins": lambda: _grid_columns(3000, 300),
+}
+
+
+@pytest.mark.parametrize("case", sorted(CORR_CASES))
+def test_gpu_and_cpu_corrections_agree(case):
+    """Same keys, same order, integer eps sums on both backends, on the
+    crowded (full sort) and binned routes (k_colsort's within-bin pass by
+    sorted position): the per-row corrections differ only by k_rowcorr's
+    float64 summation order."""
+    X, y = CORR_CASES[case]()
     jg, *_ = _job(X, y, "gpu")
     jc, *_ = _job(X, y, "cpu")
     try:
-        assert not jg.plan.calibration()["q16"]
+        assert jg.plan.calibration()["q16"] == jc.plan.calibration()["q16"]
         cg = jg.rowstats.cpu().numpy()[2::3]
         cc = jc.rowstats.numpy()[2::3]
         s1 = jc.rowstats.numpy()[0::3]

@@ -12,6 +12,5 @@ run() {
   python3 -c "import json,sys; d=json.loads(sys.argv[2]); r=d['roofline']; print(sys.argv[1], round(d['ms_per_step'],3), {k: round(v,3) for k,v in r['kernel_ms'].items()})" "$label" "$line" >> "$OUT"
 }
 run default FS_NOOP=1
-for w in 1024 2048 4096 8192 16384; do run wgs$w FS_PASS2_WGS=$w; done
 for s in 1 2 4; do run ksplit$s FS_KSPLIT=$s; done
 cat "$OUT"

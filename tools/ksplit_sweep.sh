@@ -14,9 +14,7 @@ run() {
 for rep in 1 2; do
   run cfg2_auto 5000 20 FS_NOOP=1 || exit 1
   for s in 1 4 6 8; do run cfg2_s$s 5000 20 FS_KSPLIT=$s || exit 1; done
-  run cfg2_s6_side1 5000 20 FS_KSPLIT=6 FS_SIDE=1 || exit 1
 done
 run cfg4_auto 20000 5 FS_NOOP=1 || exit 1
-run cfg4_side0 20000 5 FS_SIDE=0 || exit 1
 run cfg4_auto 20000 5 FS_NOOP=1 || exit 1
 cat "$OUT"
