@@ -42,6 +42,9 @@
 #include "../../include/fastselect_amd.h"
 #include "fs_internal.h"
 #include "fs_sparse_asm.inc"
+#ifdef FS_SP2_PROF
+#include "fs_sparse_asm_prof.inc"
+#endif
 
 namespace fs {
 namespace gpu {
@@ -1453,6 +1456,13 @@ __device__ __forceinline__ void sparse2_stream_generic(const float4* __restrict_
 // tail of a layout whose width is not a multiple of 512).  Lane l scores
 // features f0 + 4l + k and (F = 8) f0 + 256 + 4l + k, k = 0..3; partials go
 // to spart[(seg * 2 + h) * PW + f].
+// -DFS_SP2_PROF (profiling builds only, tools/sp2_prof.sh): per-wave shader
+// clock sums of the F = 8 walk -- [0] tile start (entries and the first B
+// rows landing), [1] the stream walk, [2] outside the walk (row-block
+// staging, barriers, tile bookkeeping), [3] tiles -- printed under FS_TRACE
+#ifdef FS_SP2_PROF
+__device__ unsigned long long fs_sp2_prof[4];
+#endif
 template <int F>
 __global__ __launch_bounds__(1024) void k_score_sparse2(
     const float* __restrict__ xs, int64_t PW, int64_t PC, const int2* __restrict__ tiles,
@@ -1490,7 +1500,39 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
 #pragma unroll
   for (int q = 0; q < F; q++) s[q] = 0.0;
   int cur_bi = -1;
-  for (int64_t t = t_begin; t < t_end; t++) {
+#ifdef FS_SP2_PROF
+  uint64_t pr_pro = 0, pr_body = 0, pr_out = 0, pr_tiles = 0;
+  uint64_t pr_last = __builtin_amdgcn_s_memtime();
+#endif
+#ifdef FS_SP2_ROT
+  // A/B (-DFS_SP2_ROT): within each run of tiles sharing a row block, wave w
+  // starts w/16 of the way in and wraps, so the 16 waves' tile starts (entry
+  // and B-row latency) do not coincide.  Every wave changes runs at the same
+  // k, so the staging barriers stay uniform.
+  int64_t r0 = t_begin, r1 = t_begin, run_len = 1, run_off = 0;
+#endif
+  for (int64_t k = t_begin; k < t_end; k++) {
+#ifdef FS_SP2_ROT
+    if (k == r1) {
+      r0 = k;
+      const int bx = tiles[r0].x;
+      r1 = r0 + 1;
+      for (;;) {  // first tile of another row block (64 tiles per ballot)
+        const int64_t tt = r1 + lane;
+        const uint64_t m = __ballot(tt >= t_end || tiles[tt].x != bx);
+        if (m) {
+          r1 += __builtin_ctzll(m);
+          break;
+        }
+        r1 += 64;
+      }
+      run_len = r1 - r0;
+      run_off = (wave * run_len) >> 4;
+    }
+    const int64_t t = r0 + ((k - r0) + run_off) % run_len;
+#else
+    const int64_t t = k;
+#endif
     const int2 tl = tiles[t];
     if (tl.x != cur_bi) {
       __syncthreads();
@@ -1518,9 +1560,21 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
       const uint64_t bpn =
           (uint64_t)(uintptr_t)(xs + ((int64_t)tiles[tn].y * kTile + wave) * PW + f0);
       const uint64_t enb = (uint64_t)(uintptr_t)(ent + ((tn * 2 + h) * kSWaves + wave) * kStreamEntries2);
-      if constexpr (F == 8)
+      if constexpr (F == 8) {
+#ifdef FS_SP2_PROF
+        const uint64_t t0 = __builtin_amdgcn_s_memtime();
+        uint64_t tp;
+        FS_SPARSE2_ASM_F8_PROF(acc, lds_lane, glb_lane, eb, bp, bstride_b, ncols, bpn, pf_lane, enb, tp);
+        const uint64_t t1 = __builtin_amdgcn_s_memtime();
+        pr_out += t0 - pr_last;
+        pr_pro += tp - t0;
+        pr_body += t1 - tp;
+        pr_last = t1;
+        pr_tiles++;
+#else
         FS_SPARSE2_ASM_F8(acc, lds_lane, glb_lane, eb, bp, bstride_b, ncols, bpn, pf_lane, enb);
-      else
+#endif
+      } else
         FS_SPARSE2_ASM_F4(acc, lds_lane, glb_lane, eb, bp, bstride_b, ncols, bpn, pf_lane, enb);
     } else {
       sparse2_stream_generic<F>(As, e, xb + 4 * lane, bstride, lane, disc, acc);
@@ -1528,6 +1582,15 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
 #pragma unroll
     for (int q = 0; q < F; q++) s[q] += (double)acc[q];
   }
+#ifdef FS_SP2_PROF
+  if (F == 8 && lane == 0 && pr_tiles > 0) {
+    pr_out += __builtin_amdgcn_s_memtime() - pr_last;  // the last tile to the end of the walk
+    atomicAdd(&fs_sp2_prof[0], (unsigned long long)pr_pro);
+    atomicAdd(&fs_sp2_prof[1], (unsigned long long)pr_body);
+    atomicAdd(&fs_sp2_prof[2], (unsigned long long)pr_out);
+    atomicAdd(&fs_sp2_prof[3], (unsigned long long)pr_tiles);
+  }
+#endif
   // fixed-order reduction of the 16 waves' partials through the LDS block
   __syncthreads();
   double* red = (double*)As;  // [F][kSWaves][64] (64 KB at F = 8)
@@ -4326,6 +4389,11 @@ static int run_pass2(Plan* g, double* scores_dev) {
     if (Q.PW - nfb8 * 512 > 256) nfb8++;
     const int64_t f_tail = std::min<int64_t>(nfb8 * 512, Q.PW);
     const int64_t nfb4 = (Q.PW - f_tail + 255) / 256;
+#ifdef FS_SP2_PROF
+    void* prp = nullptr;
+    FS_HIP(hipGetSymbolAddress(&prp, HIP_SYMBOL(fs_sp2_prof)));
+    FS_HIP(hipMemsetAsync(prp, 0, 4 * sizeof(unsigned long long), g->stream));
+#endif
     if (nfb8 > 0) {
       k_score_sparse2<8><<<(unsigned)(kXcds * seg_per_xcd * 2 * nfb8), 64 * kSWaves, 0,
                            g->stream>>>(g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->n_tiles,
@@ -4338,6 +4406,19 @@ static int run_pass2(Plan* g, double* scores_dev) {
                                         g->seg_len, g->nseg, nfb4, f_tail, g->spart);
       FS_TRY(launch_check("k_score_sparse2<4>"));
     }
+#ifdef FS_SP2_PROF
+    if (trace_on()) {
+      unsigned long long pr[4] = {0, 0, 0, 0};
+      FS_HIP(hipMemcpyAsync(pr, prp, sizeof(pr), hipMemcpyDeviceToHost, g->stream));
+      FS_HIP(hipStreamSynchronize(g->stream));
+      const double tot = (double)(pr[0] + pr[1] + pr[2]);
+      std::fprintf(stderr,
+                   "[fs_trace] k_score_sparse2<8> per wave-tile (shader clocks): start %.0f, walk "
+                   "%.0f, outside %.0f; shares %.3f / %.3f / %.3f over %llu wave-tiles\n",
+                   pr[0] / (double)pr[3], pr[1] / (double)pr[3], pr[2] / (double)pr[3],
+                   pr[0] / tot, pr[1] / tot, pr[2] / tot, pr[3]);
+    }
+#endif
   } else {
     k_score<<<(unsigned)(kXcds * seg_per_xcd * nfb), 256, 0, g->stream>>>(
         g->xs, Q.PW, Q.PC, g->tiles, g->Wt, g->n_tiles, g->seg_len, g->nseg, nfb, g->spart);

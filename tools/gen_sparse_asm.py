@@ -847,10 +847,13 @@ s36..s99 as the v1 JIT loop.
 """
 
 
-def gen_v2(name, F=8, lead=4, diag="", grp=1, pfn=True):
+def gen_v2(name, F=8, lead=4, diag="", grp=1, pfn=True, tprof=False):
     """diag (A/B diagnostics only, wrong scores): "lds1" skips the chunk-1
     row read (half the LDS traffic), "nosub" drops the v_sub_f32 (half the
-    VALU), "nolds" skips every row read (the slots keep stale values)."""
+    VALU), "nolds" skips every row read (the slots keep stale values).
+    tprof (profiling builds, -DFS_SP2_PROF): one more output, the s_memtime
+    stamp taken once the stream's first entries and B rows have landed (the
+    caller stamps the macro's start and end: tile-start stall vs walk)."""
     L = lead
     R = F // 4                      # ds_read_b128 per entry
     SET = [36, 68]
@@ -984,8 +987,10 @@ def gen_v2(name, F=8, lead=4, diag="", grp=1, pfn=True):
               f"s_load_dwordx16 s[{SET[0]}:{SET[0] + 15}], s[{BASE}:{BASE + 1}], 0x0",
               f"s_load_dwordx16 s[{SET[0] + 16}:{SET[0] + 31}], s[{BASE}:{BASE + 1}], 0x40",
               f"s_mov_b32 s{OFF}, 128",
-              f"s_waitcnt vmcnt({(NB - 1) * R + (2 if pfn else 0)})",
-              "7:"]
+              f"s_waitcnt vmcnt({(NB - 1) * R + (2 if pfn else 0)})"]
+    if tprof:
+        lines += ["s_waitcnt lgkmcnt(0)", "s_memtime %[tpro]", "s_waitcnt lgkmcnt(0)"]
+    lines += ["7:"]
     for x in range(2):
         lines += step(x)
     # safety bound: a stream holds at most 8 columns x 64 rows (4 KB)
@@ -999,10 +1004,12 @@ def gen_v2(name, F=8, lead=4, diag="", grp=1, pfn=True):
         for lo, hi in re.findall(r"(?<![a-z_])s\[?(\d+)(?::(\d+)\])?", l):
             named.update(range(int(lo), int(hi or lo) + 1))
     sclob = ", ".join(f'"s{i}"' for i in sorted(named))
-    return f"""#define {name}(acc_, lds_lane_, glb_lane_, eb_, bp_, bstride_, ncols_, bpn_, pf_lane_, enb_)  \\
+    targ = ", tpro_" if tprof else ""
+    tout = ', [tpro] "=s"(tpro_)' if tprof else ""
+    return f"""#define {name}(acc_, lds_lane_, glb_lane_, eb_, bp_, bstride_, ncols_, bpn_, pf_lane_, enb_{targ})  \\
   asm volatile(  \\
 {body}
-      : {", ".join(f'[acc{i}] "+v"(acc_[{i}])' for i in range(F))}  \\
+      : {", ".join(f'[acc{i}] "+v"(acc_[{i}])' for i in range(F))}{tout}  \\
       : [lds_lane] "v"(lds_lane_), [glb_lane] "v"(glb_lane_), [eb] "s"(eb_), [bp] "s"(bp_),  \\
         [bstride] "s"(bstride_), [ncols] "s"(ncols_), [bpn] "s"(bpn_), [pf_lane] "v"(pf_lane_),  \\
         [enb] "s"(enb_)  \\
@@ -1170,3 +1177,9 @@ if __name__ == "__main__":
     text += "\n" + gen_v2("FS_SPARSE2_ASM_F4", F=4, lead=6, pfn=False)
     open(path, "w").write(text)
     print("wrote", os.path.normpath(path))
+    # profiling builds only (-DFS_SP2_PROF, tools/sp2_prof.sh): the F = 8
+    # loop with the tile-start stamp
+    ppath = path.replace("fs_sparse_asm.inc", "fs_sparse_asm_prof.inc")
+    open(ppath, "w").write(HEADER + "\n" + gen_v2("FS_SPARSE2_ASM_F8_PROF", F=8, lead=3, pfn=False,
+                                                    tprof=True))
+    print("wrote", os.path.normpath(ppath))
