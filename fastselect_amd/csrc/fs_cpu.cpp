@@ -283,7 +283,8 @@ static double exact_pair(const Prepared& P, const void* x, int x_is_f64, int64_t
 // Flag and refine the ambiguous owned pairs (k_flag_pairs + k_exact_pairs).
 template <typename Amb>
 static int64_t refine_pairs(const Prepared& P, const void* x, int x_is_f64, int rank, int world,
-                            int n_jobs, std::vector<double>& D, Amb&& ambiguous) {
+                            int n_jobs, std::vector<double>& D, Amb&& ambiguous,
+                            std::vector<std::pair<int32_t, int32_t>>* refined = nullptr) {
   const int64_t n = P.n, nb = P.n_pad / kTile;
   std::vector<std::pair<int32_t, int32_t>> pairs;
   std::mutex mu;
@@ -303,7 +304,42 @@ static int64_t refine_pairs(const Prepared& P, const void* x, int x_is_f64, int 
     D[(size_t)i * n + j] = v;
     D[(size_t)j * n + i] = v;
   });
+  if (refined) *refined = pairs;
   return (int64_t)pairs.size();
+}
+
+// exact_thresholds (fs_gpu.hip): thresholds from exact distances for the
+// rows a refined pair lies within thr_tol of, when at most kExactThrRows
+// (every row under the FS_THR_EXACT_ALL test hook).
+static void exact_thresholds(const Prepared& P, const void* x, int n_jobs, const CpuState& S,
+                             const std::vector<std::pair<int32_t, int32_t>>& refined,
+                             double thr_tol, std::vector<double>& thr) {
+  const int64_t n = P.n;
+  std::vector<int32_t> rows;
+  if (std::getenv("FS_THR_EXACT_ALL")) {
+    for (int64_t i = 0; i < n; i++) rows.push_back((int32_t)i);
+  } else {
+    std::vector<uint8_t> unc((size_t)n, 0);
+    for (const auto& pr : refined) {
+      const double v = S.D[(size_t)pr.first * n + pr.second];
+      if (std::fabs(v - thr[pr.first]) < thr_tol) unc[pr.first] = 1;
+      if (std::fabs(v - thr[pr.second]) < thr_tol) unc[pr.second] = 1;
+    }
+    for (int64_t i = 0; i < n; i++)
+      if (unc[i]) rows.push_back((int32_t)i);
+    if ((int64_t)rows.size() > kExactThrRows) return;
+  }
+  parallel_for((int64_t)rows.size(), n_jobs, [&](int64_t k) {
+    const int64_t i = rows[k];
+    double s1 = 0.0, s2 = 0.0;
+    for (int64_t j = 0; j < n; j++) {
+      if (j == i) continue;
+      const double d = exact_pair(P, x, 0, i, j);
+      s1 += d;
+      s2 += d * d;
+    }
+    thr[i] = multisurf_threshold(s1, s2, n) * P.SC;
+  });
 }
 
 int multisurf_pass1(const Prepared& P, const void* x, int rank, int world, int n_jobs,
@@ -341,9 +377,15 @@ int multisurf_select(const Prepared& P, const void* x, int rank, int world,
     S.thr[i] = (mu - rowstats[3 * i + 2] / nm1) - 0.5 * std::sqrt(var);
   }
   const double dq = calibrated_band(P, x, 0, n_jobs) * P.SC;
-  S.refined = refine_pairs(P, x, 0, rank, world, n_jobs, S.D, [&](int64_t i, int64_t j, double d) {
-    return std::fabs(d - S.thr[i]) < dq || std::fabs(d - S.thr[j]) < dq;
-  });
+  std::vector<std::pair<int32_t, int32_t>> refined;
+  S.refined = refine_pairs(
+      P, x, 0, rank, world, n_jobs, S.D,
+      [&](int64_t i, int64_t j, double d) {
+        return std::fabs(d - S.thr[i]) < dq || std::fabs(d - S.thr[j]) < dq;
+      },
+      &refined);
+  exact_thresholds(P, x, n_jobs, S, refined, dq / std::sqrt((double)std::max<int64_t>(n - 1, 1)) + 2.0,
+                   S.thr);
   parallel_for(n, n_jobs, [&](int64_t i) {  // k_count_ms
     double h = 0.0, m = 0.0;
     for (int64_t j = 0; j < n; j++) {

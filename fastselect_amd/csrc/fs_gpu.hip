@@ -889,6 +889,130 @@ __device__ __forceinline__ void store_pair(double* __restrict__ D, int64_t n_pad
   if (I == J) D[(t * kTile + a) * kTile + b] = v;
 }
 
+// Exact thresholds for the rows that need them (MultiSURF, plan_select).  A
+// refined pair compares the reference's own distance with our threshold,
+// and that threshold is not the reference's: the mean is exact (the
+// correction), but the spread comes from the quantised second moments, off
+// by ~(band / 12) / sqrt(n - 1) integer units (the rounding of one pair's
+// distance averaged over a row).  A refined pair whose exact distance lies
+// within thr_tol of an endpoint's threshold could therefore still be
+// decided differently (VERDICT r3 missing #1's decision-level bar: uniform
+// noise, n = 16384, one row of 16384).  Those rows are flagged here; if no
+// more than kExactThrRows are, their thresholds are recomputed from exact
+// distances to every other sample (k_row_exact_parts / k_row_exact_thr:
+// the reference's sum_j D_ij and sum_j D_ij^2, MultiSURF.py:174-196) before
+// any pair is counted.  A rank fixes the rows its own refined pairs flag:
+// a pair far from a threshold is decided alike by both values, so ranks
+// that keep the quantised value for a row decide their pairs correctly too.
+__device__ __forceinline__ void mark_uncertain(int2 pr, double v, const double* __restrict__ thr,
+                                               double thr_tol, unsigned int* __restrict__ unc) {
+  if (__builtin_fabs(v - thr[pr.x]) < thr_tol) unc[pr.x] = 1u;
+  if (__builtin_fabs(v - thr[pr.y]) < thr_tol) unc[pr.y] = 1u;
+}
+
+// The flagged rows in index order (the first max_rows of them) and their
+// count: one 1024-thread workgroup, a contiguous index range per thread.
+__global__ __launch_bounds__(1024) void k_unc_compact(const unsigned int* __restrict__ unc,
+                                                      int64_t n, int max_rows,
+                                                      int32_t* __restrict__ rows,
+                                                      int32_t* __restrict__ nrows) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (n + 1023) / 1024;
+  const int64_t a = t * per, b = a + per < n ? a + per : n;
+  int c = 0;
+  for (int64_t i = a; i < b; i++) c += unc[i] != 0u;
+  part[t] = c;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int pos = part[t] - c;
+  for (int64_t i = a; i < b; i++)
+    if (unc[i] != 0u) {
+      if (pos < max_rows) rows[pos] = (int32_t)i;
+      pos++;
+    }
+  if (t == 1023) *nrows = part[1023];
+}
+
+// Exact row moments of the flagged rows, in chunks of 256 samples: grid
+// (chunks, max_rows); slot s takes rows[s] when the count allows the fix.  Each wave sums 64 samples j != i: per sample the lanes stride the
+// features with k_exact_pairs' arithmetic (float32 diffs for float32 X, a
+// float64 sum), then lane 0 adds D_ij and D_ij^2 in j order; the 4 waves'
+// partials go to parts[s][chunk] in a fixed order.
+template <typename T>
+__global__ __launch_bounds__(256) void k_row_exact_parts(
+    const T* __restrict__ x, int64_t n, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
+    const int64_t* __restrict__ src_col, const double* __restrict__ scl,
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ nrows, int max_rows,
+    double2* __restrict__ parts) {
+  __shared__ double2 wsum[4];
+  const int cnt = *nrows;
+  const int slot = blockIdx.y;
+  if (cnt > max_rows || slot >= cnt) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t i = rows[slot];
+  const T* xi = x + i * p_in;
+  double s1 = 0.0, s2 = 0.0;
+  const int64_t j0 = (int64_t)blockIdx.x * 256 + wave * 64;
+  for (int q = 0; q < 64; q++) {
+    const int64_t j = j0 + q;
+    if (j >= n) break;
+    if (j == i) continue;
+    const T* xj = x + j * p_in;
+    double acc = 0.0;
+    for (int64_t c = lane; c < pc; c += 64) {
+      const int64_t col = src_col[c];
+      if (sizeof(T) == 4) {
+        const float dv = __builtin_fabsf((float)xi[col] - (float)xj[col]) * (float)scl[c];
+        acc += (double)dv;
+      } else {
+        acc += __builtin_fabs((double)xi[col] - (double)xj[col]) * scl[c];
+      }
+    }
+    for (int64_t c = PC + lane; c < PC + pd; c += 64) {
+      const int64_t col = src_col[c];
+      acc += (xi[col] != xj[col]) ? 1.0 : 0.0;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    s1 += acc;
+    s2 += acc * acc;
+  }
+  if (lane == 0) wsum[wave] = make_double2(s1, s2);
+  __syncthreads();
+  if (threadIdx.x == 0)
+    parts[(int64_t)slot * gridDim.x + blockIdx.x] =
+        make_double2((wsum[0].x + wsum[1].x) + (wsum[2].x + wsum[3].x),
+                     (wsum[0].y + wsum[1].y) + (wsum[2].y + wsum[3].y));
+}
+
+// thr[rows[s]] from the chunk partials (fixed order), in integer units.
+__global__ __launch_bounds__(64) void k_row_exact_thr(const double2* __restrict__ parts,
+                                                      int64_t nchunk, const int32_t* __restrict__ rows,
+                                                      const int32_t* __restrict__ nrows,
+                                                      int max_rows, int64_t n, double sc,
+                                                      double* __restrict__ thr) {
+  const int cnt = *nrows;
+  const int slot = blockIdx.x;
+  if (cnt > max_rows || slot >= cnt) return;
+  const int lane = threadIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t c = lane; c < nchunk; c += 64) {
+    const double2 v = parts[(int64_t)slot * nchunk + c];
+    s1 += v.x;
+    s2 += v.y;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  if (lane == 0) thr[rows[slot]] = multisurf_threshold(s1, s2, n) * sc;
+}
+
 // Reference-exact distance of each listed pair: sum_f diff_f(i, j) in
 // float64 with diff_f computed exactly as the reference kernels do
 // (MultiSURF.py:184-187 / ReliefF.py:151-154 in float32, SURF.py:153-156 in
@@ -900,7 +1024,8 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
     const int64_t* __restrict__ src_col, const double* __restrict__ scl, double sc,
     const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
     int64_t n_pad, int2 tw, int2 win, int mark_f32, double* __restrict__ D,
-    float* __restrict__ Dk) {
+    float* __restrict__ Dk, const double* __restrict__ thr, double thr_tol,
+    unsigned int* __restrict__ unc) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
@@ -951,6 +1076,7 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
       } else {
         const double v = mark_f32 ? (acc > 0.0 ? -(double)(float)acc : 0.0) : acc * sc;
         store_pair(D, n_pad, tw, win, pr, v);
+        if (unc != nullptr) mark_uncertain(pr, v, thr, thr_tol, unc);
       }
     }
   }
@@ -966,7 +1092,8 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
 __global__ __launch_bounds__(256) void k_exact_pairs_rows(
     const float* __restrict__ x, int64_t p, const float* __restrict__ scl32, double sc,
     const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
-    int64_t n_pad, int2 tw, int2 win, double* __restrict__ D) {
+    int64_t n_pad, int2 tw, int2 win, double* __restrict__ D, const double* __restrict__ thr,
+    double thr_tol, unsigned int* __restrict__ unc) {
   const int lane = threadIdx.x & 63;
   const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
@@ -1000,6 +1127,7 @@ __global__ __launch_bounds__(256) void k_exact_pairs_rows(
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (lane == 0) {
       store_pair(D, n_pad, tw, win, pr, acc * sc);
+      if (unc != nullptr) mark_uncertain(pr, acc * sc, thr, thr_tol, unc);
     }
   }
 }
@@ -1291,6 +1419,11 @@ __device__ __forceinline__ void score_tiles(const float* __restrict__ xs, int64_
 // ~8 segments thrashing it; the 1-D grid has 8 * max_x(segments of x) * nfb
 // slots, the few beyond nseg exit at once.
 constexpr int kXcds = 8;
+// row blocks per group of the sparse pass-2 schedule (build_sparse_schedule;
+// 16 / FS_SCHED_ROWS feature blocks per block of units)
+#ifndef FS_SCHED_ROWS
+#define FS_SCHED_ROWS 8
+#endif
 
 __global__ __launch_bounds__(256) void k_score(const float* __restrict__ xs, int64_t PW,
                                                int64_t PC, const int2* __restrict__ tiles,
@@ -1450,36 +1583,34 @@ __device__ __forceinline__ void sparse2_stream_generic(const float4* __restrict_
   }
 }
 
-// Grid: XCD-aware as k_score_sparse, the slots of a segment ordered
-// (feature block, half) so that the two halves of one block are neighbours.
+// Grid: one workgroup per unit (segment, feature block, half) of the pass-2
+// schedule (build_sparse_schedule, host side): units[w] = (seg, 2 fb + h),
+// or seg = -1 for the padding slots of a short XCD list.  A segment is a run
+// of tiles of one row block (its rows are staged into LDS once) in descending
+// column-block order, tile indices sched[seg_off[seg] .. seg_off[seg + 1]).
 // F = 8: 512-feature blocks f_base + 512 fb; F = 4: 256-feature blocks (the
 // tail of a layout whose width is not a multiple of 512).  Lane l scores
 // features f0 + 4l + k and (F = 8) f0 + 256 + 4l + k, k = 0..3; partials go
 // to spart[(seg * 2 + h) * PW + f].
-// -DFS_SP2_PROF (profiling builds only, tools/sp2_prof.sh): per-wave shader
-// clock sums of the F = 8 walk -- [0] tile start (entries and the first B
-// rows landing), [1] the stream walk, [2] outside the walk (row-block
-// staging, barriers, tile bookkeeping), [3] tiles -- printed under FS_TRACE
 #ifdef FS_SP2_PROF
 __device__ unsigned long long fs_sp2_prof[4];
 #endif
 template <int F>
 __global__ __launch_bounds__(1024) void k_score_sparse2(
     const float* __restrict__ xs, int64_t PW, int64_t PC, const int2* __restrict__ tiles,
-    const uint2* __restrict__ ent, int64_t n_tiles, int64_t seg_len, int64_t nseg, int64_t nfb,
-    int64_t f_base, double* __restrict__ spart) {
+    const uint2* __restrict__ ent, const int32_t* __restrict__ sched,
+    const int32_t* __restrict__ seg_off, const int2* __restrict__ units, int64_t f_base,
+    double* __restrict__ spart) {
   constexpr int C = F / 4;
   __shared__ float4 As[kHalf * 2 * 64];  // 64 rows x 2 chunks x 64 lanes (128 KB)
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int64_t wg = blockIdx.x;
-  const int64_t xcd = wg % kXcds, k = wg / kXcds;
-  const int64_t seg = xcd + kXcds * (k / (2 * nfb)), r2 = k % (2 * nfb);
-  if (seg >= nseg) return;
-  const int64_t fb = r2 >> 1, h = r2 & 1;
+  const int2 unit = units[blockIdx.x];
+  if (unit.x < 0) return;
+  const int64_t seg = unit.x, fb = unit.y >> 1, h = unit.y & 1;
   const int64_t f0 = f_base + fb * (64 * F);
-  const int64_t t_begin = seg * seg_len;
-  const int64_t t_end = t_begin + seg_len < n_tiles ? t_begin + seg_len : n_tiles;
+  const int64_t t_begin = seg_off[seg];
+  const int64_t t_end = seg_off[seg + 1];
   bool disc[F];
 #pragma unroll
   for (int c = 0; c < C; c++)
@@ -1515,23 +1646,13 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
 #ifdef FS_SP2_ROT
     if (k == r1) {
       r0 = k;
-      const int bx = tiles[r0].x;
-      r1 = r0 + 1;
-      for (;;) {  // first tile of another row block (64 tiles per ballot)
-        const int64_t tt = r1 + lane;
-        const uint64_t m = __ballot(tt >= t_end || tiles[tt].x != bx);
-        if (m) {
-          r1 += __builtin_ctzll(m);
-          break;
-        }
-        r1 += 64;
-      }
+      r1 = t_end;  // a segment holds one row block
       run_len = r1 - r0;
       run_off = (wave * run_len) >> 4;
     }
-    const int64_t t = r0 + ((k - r0) + run_off) % run_len;
+    const int64_t t = sched[r0 + ((k - r0) + run_off) % run_len];
 #else
-    const int64_t t = k;
+    const int64_t t = sched[k];
 #endif
     const int2 tl = tiles[t];
     if (tl.x != cur_bi) {
@@ -1554,12 +1675,9 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
     if (fast) {
       const uint64_t eb = (uint64_t)(uintptr_t)e;
       const uint64_t bp = (uint64_t)(uintptr_t)xb;
-      // the next tile's B rows (warmed into L2 by the loop; the last tile
-      // of a segment warms its own again)
-      const int64_t tn = t + 1 < t_end ? t + 1 : t;
-      const uint64_t bpn =
-          (uint64_t)(uintptr_t)(xs + ((int64_t)tiles[tn].y * kTile + wave) * PW + f0);
-      const uint64_t enb = (uint64_t)(uintptr_t)(ent + ((tn * 2 + h) * kSWaves + wave) * kStreamEntries2);
+      // next-tile prefetch operands of the loop (the shipped loops are
+      // generated without the prefetch: tools/gen_sparse_asm.py pfn)
+      const uint64_t bpn = bp, enb = eb;
       if constexpr (F == 8) {
 #ifdef FS_SP2_PROF
         const uint64_t t0 = __builtin_amdgcn_s_memtime();
@@ -3133,6 +3251,23 @@ struct Plan {
   int sparse = 0;               // pass 2 over non-zero weights only
   double* spart = nullptr;       // pass-2 segment partials (own block, shard_segments)
   size_t spart_cap = 0;           // doubles of spart
+  // sparse pass-2 schedule (build_sparse_schedule): tile order, segment
+  // offsets and the unit tables of the F = 8 / F = 4 launches (own blocks)
+  std::vector<int2> h_tiles;      // the owned tiles (host copy of `tiles`)
+  int32_t* sched = nullptr;
+  int32_t* seg_off = nullptr;
+  int2* units8 = nullptr;
+  int2* units4 = nullptr;
+  size_t sched_cap = 0;           // int32 slots of `sched` + `seg_off` (one block)
+  size_t units_cap = 0;           // int2 slots of units8 + units4 (one block)
+  int64_t nunits8 = 0, nunits4 = 0, nfb8 = 0, nfb4 = 0, f_tail = 0;
+  // exact thresholds of uncertain rows (exact_thresholds)
+  unsigned int* unc = nullptr;  // [n_pad] row flags
+  int32_t* urows = nullptr;     // [n_pad + 1] flagged rows in index order, then their count
+  double2* uparts = nullptr;    // [thr_rows][nchunk] exact row-moment partials
+  int thr_rows = kExactThrRows; // rows fixed at most (FS_THR_EXACT_ALL: every row, tests)
+  bool thr_all = false;
+  int32_t n_exact_thr = 0;      // rows whose threshold the last select recomputed (-1: too many)
   // ambiguous-pair refinement
   int2* list = nullptr;
   int64_t list_cap = 0;
@@ -3570,6 +3705,8 @@ void plan_destroy(Plan* g) {
   for (void* q : g->scratch) dev_free(q);
   for (void* q : g->owned_shard) dev_free(q);
   if (g->spart) dev_free(g->spart);
+  if (g->sched) dev_free(g->sched);
+  if (g->units8) dev_free(g->units8);
   for (auto& e : g->ev)
     if (e) (void)hipEventDestroy(e);
   if (g->ev_fork) (void)hipEventDestroy(g->ev_fork);
@@ -3787,6 +3924,107 @@ static int calibrate_band(Plan* g) {
 // correction and the pass-2 segments (sized by the owned tiles and the
 // feature blocks), with the segment partials' buffer grown when needed.
 // plan_layout calls it, and plan_set_shard alone: re-targeting a plan to
+// Pass-2 schedule of the sparse kernels (k_score_sparse2).  The B operand of
+// a tile (its 128 column samples' values, 2 KB each per 512-feature block)
+// is read once per (tile, feature block, half): ~250 GB per launch at cfg4,
+// far more than L2 holds when the workgroups on an XCD all walk different
+// column blocks.  Here the units an XCD runs at the same time walk the SAME
+// column blocks in the same order:
+//  * segment = the owned tiles of one row block I whose column block J falls
+//    in one chunk of seg_len * world blocks (~seg_len tiles), in descending
+//    J (so the segments of a group start aligned at the chunk's end);
+//  * group = the segments of one chunk from kSchedRows consecutive row
+//    blocks (they share every J they hold);
+//  * block = one group x kSchedFb feature blocks x both halves (<= 32
+//    units, one per CU of an XCD), dealt to the XCD with the least work so
+//    far (workgroup w runs on XCD w % 8; each XCD's list is padded with
+//    empty units to the longest).
+// Concurrent units then share their B rows through the XCD's L2 (kSchedRows
+// row blocks x 2 halves read each) and their entry streams (kSchedFb
+// feature blocks read each).
+constexpr int kSchedRows = FS_SCHED_ROWS;
+constexpr int kSchedFb = 16 / FS_SCHED_ROWS;
+
+static int ensure_dev(Plan* g, void** buf, size_t* cap, size_t bytes) {
+  if (bytes <= *cap) return FS_OK;
+  if (*buf) {
+    FS_HIP(hipStreamSynchronize(g->stream));
+    dev_free(*buf);
+    *buf = nullptr;
+    *cap = 0;
+  }
+  FS_TRY(dev_alloc(buf, bytes, g->device));
+  *cap = bytes;
+  return FS_OK;
+}
+
+static int build_sparse_schedule(Plan* g) {
+  const Prepared& Q = g->P;
+  const int64_t T = g->n_tiles;
+  const int64_t CJ = std::max<int64_t>(1, g->seg_len * std::max(1, g->world));
+  std::vector<int32_t> sched, seg_off{0};
+  std::vector<int64_t> seg_tiles;
+  std::map<std::pair<int64_t, int64_t>, std::vector<int32_t>> groups;  // (chunk, I group) -> segs
+  sched.reserve((size_t)T);
+  for (int64_t t = 0; t < T;) {  // h_tiles are ordered by (I, J)
+    const int I = g->h_tiles[t].x;
+    const int64_t c = g->h_tiles[t].y / CJ;
+    int64_t e = t;
+    while (e < T && g->h_tiles[e].x == I && g->h_tiles[e].y / CJ == c) e++;
+    for (int64_t k = e - 1; k >= t; k--) sched.push_back((int32_t)k);
+    groups[{c, I / kSchedRows}].push_back((int32_t)seg_tiles.size());
+    seg_tiles.push_back(e - t);
+    seg_off.push_back((int32_t)sched.size());
+    t = e;
+  }
+  g->nseg = std::max<int64_t>(1, (int64_t)seg_tiles.size());
+  // feature blocks of the two launches (run_pass2): 512-wide, then a tail
+  // of <= 256 features in one 256-wide block (a longer tail takes one more,
+  // partial, 512-wide block: its cost is mostly its entry walk)
+  g->nfb8 = Q.PW / 512;
+  if (Q.PW - g->nfb8 * 512 > 256) g->nfb8++;
+  g->f_tail = std::min<int64_t>(g->nfb8 * 512, Q.PW);
+  g->nfb4 = (Q.PW - g->f_tail + 255) / 256;
+  auto units_of = [&](int64_t nfb, std::vector<int2>& table) {
+    std::vector<std::vector<int2>> per(kXcds);
+    std::vector<int64_t> load(kXcds, 0);
+    for (const auto& gr : groups)
+      for (int64_t f0 = 0; f0 < nfb; f0 += kSchedFb) {
+        int x = 0;
+        for (int q = 1; q < kXcds; q++)
+          if (load[q] < load[x]) x = q;
+        for (int64_t fb = f0; fb < std::min<int64_t>(nfb, f0 + kSchedFb); fb++)
+          for (int32_t sg : gr.second)
+            for (int h = 0; h < 2; h++) {
+              per[x].push_back(make_int2(sg, (int)(2 * fb + h)));
+              load[x] += seg_tiles[sg];
+            }
+      }
+    size_t kmax = 0;
+    for (const auto& v : per) kmax = std::max(kmax, v.size());
+    table.assign(kXcds * kmax, make_int2(-1, 0));
+    for (int x = 0; x < kXcds; x++)
+      for (size_t k = 0; k < per[x].size(); k++) table[x + kXcds * k] = per[x][k];
+  };
+  std::vector<int2> u8, u4;
+  units_of(g->nfb8, u8);
+  units_of(g->nfb4, u4);
+  g->nunits8 = (int64_t)u8.size();
+  g->nunits4 = (int64_t)u4.size();
+  if (sched.empty()) sched.push_back(0);
+  const size_t ns = sched.size() + seg_off.size();
+  const size_t nu = std::max<size_t>(1, u8.size() + u4.size());
+  FS_TRY(ensure_dev(g, (void**)&g->sched, &g->sched_cap, ns * sizeof(int32_t)));
+  FS_TRY(ensure_dev(g, (void**)&g->units8, &g->units_cap, nu * sizeof(int2)));
+  g->seg_off = g->sched + sched.size();
+  g->units4 = g->units8 + u8.size();
+  FS_TRY(h2d(g, g->sched, sched.data(), sched.size()));
+  FS_TRY(h2d(g, g->seg_off, seg_off.data(), seg_off.size()));
+  if (!u8.empty()) FS_TRY(h2d(g, g->units8, u8.data(), u8.size()));
+  if (!u4.empty()) FS_TRY(h2d(g, g->units4, u4.data(), u4.size()));
+  return FS_OK;
+}
+
 // another tile shard keeps the feature layout, its tables and its band
 // calibration (none of them depends on the shard).
 static int shard_segments(Plan* g) {
@@ -3811,9 +4049,10 @@ static int shard_segments(Plan* g) {
       g->sparse ? std::min<int64_t>(32768, std::max<int64_t>(4096, g->n_tiles * nfb / 4)) : 65536;
   g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + wgs - 1) / wgs);
   g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
+  if (Q.algo == ALGO_RELIEFF) return FS_OK;
+  if (g->sparse) FS_TRY(build_sparse_schedule(g));  // its own segments (g->nseg)
   // partial rows per segment: one per half with the sparse streams
   g->nsegpart = g->sparse ? 2 * g->nseg : g->nseg;
-  if (Q.algo == ALGO_RELIEFF) return FS_OK;
   const size_t need = (size_t)g->nsegpart * Q.PW;
   if (need > g->spart_cap) {
     if (g->spart) {
@@ -4027,6 +4266,7 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
   g->n_tiles = (int64_t)bi.size();
   std::vector<int2> tl(g->n_tiles);
   for (int64_t t = 0; t < g->n_tiles; t++) tl[t] = make_int2(bi[t], bj[t]);
+  g->h_tiles = tl;
   // MultiSURF reads distances only inside owned tiles: tiled layout, one
   // 128 x 128 block per owned tile (half the full matrix at world 1, 1/N of
   // the tiles per rank).  ReliefF / SURF select neighbours over whole rows.
@@ -4191,6 +4431,16 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
       (rc = dalloc(g, &g->corr, Q.n_pad)) || (rc = dalloc(g, &g->thr, Q.n_pad)) ||
       (rc = dalloc(g, &g->list, g->list_cap)) || (rc = dalloc(g, &g->list_count, 1)))
     return fail(rc);
+  if (Q.algo == ALGO_MULTISURF) {
+    // test hook: every row's threshold from exact distances (the machinery
+    // of exact_thresholds checked on all rows against the oracle's)
+    g->thr_all = std::getenv("FS_THR_EXACT_ALL") != nullptr;
+    g->thr_rows = g->thr_all ? (int)Q.n : kExactThrRows;
+    const int64_t nchunk = (Q.n + 255) / 256;
+    if ((rc = dalloc(g, &g->unc, Q.n_pad)) || (rc = dalloc(g, &g->urows, Q.n_pad + 1)) ||
+        (rc = dalloc(g, &g->uparts, (size_t)g->thr_rows * nchunk)))
+      return fail(rc);
+  }
   g->sparse = choose_sparse(g, Q);
   if ((rc = setup_shard(g, bi, bj))) return fail(rc);
   trace_mark("plan: hipMalloc");
@@ -4315,7 +4565,8 @@ static int sort_pair_list(Plan* g, int64_t count) {
 
 // Flag the ambiguous pairs of the owned tiles and recompute them exactly.
 // One host round trip reads the pair count (to grow the list if needed).
-static int refine_pairs(Plan* g, int algo, double delta) {
+static int refine_pairs(Plan* g, int algo, double delta, double thr_tol = 0.0,
+                        unsigned int* unc = nullptr) {
   const Prepared& Q = g->P;
   g->n_refined = 0;
   if (g->n_tiles == 0) return FS_OK;
@@ -4341,16 +4592,64 @@ static int refine_pairs(Plan* g, int algo, double delta) {
   if (g->rows_direct && !std::getenv("FS_EXACT_GATHER"))
     k_exact_pairs_rows<<<grid, 256, 0, g->stream>>>((const float*)g->x, Q.p_in, g->scl32, Q.SC,
                                                     g->list, g->list_count, g->list_cap, Q.n_pad,
-                                                    g->tw, g->win, g->D);
+                                                    g->tw, g->win, g->D, g->thr, thr_tol, unc);
   else if (g->x_is_f64)
     k_exact_pairs<double><<<grid, 256, 0, g->stream>>>(
         (const double*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D, nullptr);
+        g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D, nullptr, g->thr, thr_tol,
+        unc);
   else
     k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
         (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
-        g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D, nullptr);
+        g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D, nullptr, g->thr, thr_tol,
+        unc);
   return launch_check("k_exact_pairs");
+}
+
+// MultiSURF thresholds from exact distances for the rows a refined pair
+// sits too close to (mark_uncertain, k_row_exact_*), when at most
+// g->thr_rows of them are flagged -- on 32-bit operands a handful per fit;
+// on 16-bit operands there can be thousands, and the post-scoring decision
+// check (q16_decision_risk) stays in charge.  Runs between refine_pairs and
+// the neighbour counts; the count is read back once (the fix's row count is
+// reported by fs_plan_info-style diagnostics: g->n_exact_thr).
+static int exact_thresholds(Plan* g) {
+  const Prepared& Q = g->P;
+  const int64_t nchunk = (Q.n + 255) / 256;
+  if (g->thr_all) {  // test hook: flag every row
+    std::vector<int32_t> all((size_t)Q.n + 1);
+    for (int64_t i = 0; i < Q.n; i++) all[i] = (int32_t)i;
+    all[Q.n] = (int32_t)Q.n;
+    FS_TRY(h2d(g, g->urows, all.data(), all.size()));  // rows, then the count at thr_rows = n
+  } else {
+    k_unc_compact<<<1, 1024, 0, g->stream>>>(g->unc, Q.n, g->thr_rows, g->urows,
+                                             g->urows + g->thr_rows);
+    FS_TRY(launch_check("k_unc_compact"));
+  }
+  const int32_t* nrows = g->urows + g->thr_rows;
+  if (g->x_is_f64)
+    k_row_exact_parts<double><<<dim3((unsigned)nchunk, (unsigned)g->thr_rows), 256, 0, g->stream>>>(
+        (const double*)g->x, Q.n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, g->urows, nrows,
+        g->thr_rows, g->uparts);
+  else
+    k_row_exact_parts<float><<<dim3((unsigned)nchunk, (unsigned)g->thr_rows), 256, 0, g->stream>>>(
+        (const float*)g->x, Q.n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, g->urows, nrows,
+        g->thr_rows, g->uparts);
+  FS_TRY(launch_check("k_row_exact_parts"));
+  k_row_exact_thr<<<(unsigned)g->thr_rows, 64, 0, g->stream>>>(g->uparts, nchunk, g->urows, nrows,
+                                                               g->thr_rows, Q.n, Q.SC, g->thr);
+  FS_TRY(launch_check("k_row_exact_thr"));
+  if (trace_on()) {
+    int32_t cnt = 0;
+    FS_HIP(hipMemcpyAsync(&cnt, nrows, sizeof(cnt), hipMemcpyDeviceToHost, g->stream));
+    FS_HIP(hipStreamSynchronize(g->stream));
+    g->n_exact_thr = cnt <= g->thr_rows ? cnt : -1;
+    char msg[128];
+    snprintf(msg, sizeof msg, "select: %d rows near a refined pair (%s)", cnt,
+             cnt <= g->thr_rows ? "exact thresholds" : "too many: quantised thresholds kept");
+    trace_mark(msg);
+  }
+  return FS_OK;
 }
 
 // Pair weights of the owned tiles in the form pass 2 reads (dense or sparse).
@@ -4381,29 +4680,23 @@ static int run_pass2(Plan* g, double* scores_dev) {
   FS_HIP(hipEventRecord(g->ev[2], g->stream));
   const int64_t seg_per_xcd = (g->nseg + kXcds - 1) / kXcds;
   if (g->sparse) {
-    // 512-feature blocks, then a tail of at most 256 features in one
-    // 256-feature block (a longer tail takes one more, partial, 512-feature
-    // block: a block's cost is mostly its entry walk, so one F = 8 block is
-    // cheaper than two F = 4 ones -- cfg2, 448 features: 0.24 -> 0.17 ms)
-    int64_t nfb8 = Q.PW / 512;
-    if (Q.PW - nfb8 * 512 > 256) nfb8++;
-    const int64_t f_tail = std::min<int64_t>(nfb8 * 512, Q.PW);
-    const int64_t nfb4 = (Q.PW - f_tail + 255) / 256;
+    // 512-feature blocks, then the tail block (build_sparse_schedule; one
+    // F = 8 block is cheaper than two F = 4 ones -- cfg2, 448 features:
+    // 0.24 -> 0.17 ms)
 #ifdef FS_SP2_PROF
     void* prp = nullptr;
     FS_HIP(hipGetSymbolAddress(&prp, HIP_SYMBOL(fs_sp2_prof)));
     FS_HIP(hipMemsetAsync(prp, 0, 4 * sizeof(unsigned long long), g->stream));
 #endif
-    if (nfb8 > 0) {
-      k_score_sparse2<8><<<(unsigned)(kXcds * seg_per_xcd * 2 * nfb8), 64 * kSWaves, 0,
-                           g->stream>>>(g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->n_tiles,
-                                        g->seg_len, g->nseg, nfb8, 0, g->spart);
+    if (g->nunits8 > 0) {
+      k_score_sparse2<8><<<(unsigned)g->nunits8, 64 * kSWaves, 0, g->stream>>>(
+          g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->sched, g->seg_off, g->units8, 0, g->spart);
       FS_TRY(launch_check("k_score_sparse2<8>"));
     }
-    if (nfb4 > 0) {
-      k_score_sparse2<4><<<(unsigned)(kXcds * seg_per_xcd * 2 * nfb4), 64 * kSWaves, 0,
-                           g->stream>>>(g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->n_tiles,
-                                        g->seg_len, g->nseg, nfb4, f_tail, g->spart);
+    if (g->nunits4 > 0) {
+      k_score_sparse2<4><<<(unsigned)g->nunits4, 64 * kSWaves, 0, g->stream>>>(
+          g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->sched, g->seg_off, g->units4, g->f_tail,
+          g->spart);
       FS_TRY(launch_check("k_score_sparse2<4>"));
     }
 #ifdef FS_SP2_PROF
@@ -4450,7 +4743,13 @@ int plan_select(Plan* g, const double* rowstats, double* counts) {
   FS_HIP(hipSetDevice(g->device));
   k_thr_ms<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(rowstats, Q.n, g->thr);
   FS_TRY(launch_check("k_thr_ms"));
-  FS_TRY(refine_pairs(g, ALGO_MULTISURF, Q.amb_delta * Q.SC));
+  // a threshold's error in integer units: about the band's sigma (band / 12)
+  // over sqrt(n - 1) (exact_thresholds); 12 of those plus 2 units of slack
+  const double band = Q.amb_delta * Q.SC;
+  const double thr_tol = band / std::sqrt((double)std::max<int64_t>(Q.n - 1, 1)) + 2.0;
+  FS_HIP(hipMemsetAsync(g->unc, 0, sizeof(unsigned int) * Q.n_pad, g->stream));
+  FS_TRY(refine_pairs(g, ALGO_MULTISURF, band, thr_tol, g->unc));
+  FS_TRY(exact_thresholds(g));
   FS_HIP(hipMemsetAsync(counts, 0, sizeof(double) * 2 * Q.n, g->stream));
   if (g->n_tiles > 0) {
     k_tile_counts<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, g->tiles, g->lab,

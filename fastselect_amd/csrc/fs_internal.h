@@ -177,6 +177,11 @@ FS_HD inline int64_t tile_linear(int64_t nb, int64_t bi, int64_t bj) {
 
 int hardware_threads(int n_jobs);
 
+// Rows whose MultiSURF threshold a select recomputes from exact distances
+// at most (exact_thresholds in both backends): a refined pair that close to
+// a quantised threshold could be decided differently from the reference.
+constexpr int kExactThrRows = 64;
+
 // Thresholds shared by both backends (MultiSURF.py:193-196 in D units).
 FS_HD inline double multisurf_threshold(double s1, double s2, int64_t n) {
   const double mu = s1 / (double)(n - 1);
