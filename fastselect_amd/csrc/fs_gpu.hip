@@ -1593,7 +1593,7 @@ __device__ __forceinline__ void sparse2_stream_generic(const float4* __restrict_
 // features f0 + 4l + k and (F = 8) f0 + 256 + 4l + k, k = 0..3; partials go
 // to spart[(seg * 2 + h) * PW + f].
 #ifdef FS_SP2_PROF
-__device__ unsigned long long fs_sp2_prof[4];
+__device__ unsigned long long fs_sp2_prof[9];
 #endif
 template <int F>
 __global__ __launch_bounds__(1024) void k_score_sparse2(
@@ -1630,42 +1630,50 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
   double s[F];
 #pragma unroll
   for (int q = 0; q < F; q++) s[q] = 0.0;
-  int cur_bi = -1;
 #ifdef FS_SP2_PROF
-  uint64_t pr_pro = 0, pr_body = 0, pr_out = 0, pr_tiles = 0;
-  uint64_t pr_last = __builtin_amdgcn_s_memtime();
+  uint64_t pr_pro = 0, pr_body = 0, pr_out = 0, pr_tiles = 0, pr_stage = 0;
+  const uint64_t pr_t0 = __builtin_amdgcn_s_memtime(), pr_r0 = wall_clock64();
+  uint64_t pr_last = pr_t0;
 #endif
-#ifdef FS_SP2_ROT
-  // A/B (-DFS_SP2_ROT): within each run of tiles sharing a row block, wave w
-  // starts w/16 of the way in and wraps, so the 16 waves' tile starts (entry
-  // and B-row latency) do not coincide.  Every wave changes runs at the same
-  // k, so the staging barriers stay uniform.
-  int64_t r0 = t_begin, r1 = t_begin, run_len = 1, run_off = 0;
-#endif
+  // The segment's tile list, 64 tiles per lane-indexed load: tile k - t_begin
+  // is lane (k - t_begin) % 64 of my_t / my_x / my_y (v_readlane per tile,
+  // instead of two dependent scalar loads -- sched, then tiles -- per tile).
+  int my_t = 0, my_x = -1, my_y = 0;
+  int cur_bi = -1;
   for (int64_t k = t_begin; k < t_end; k++) {
-#ifdef FS_SP2_ROT
-    if (k == r1) {
-      r0 = k;
-      r1 = t_end;  // a segment holds one row block
-      run_len = r1 - r0;
-      run_off = (wave * run_len) >> 4;
+    const int idx = (int)((k - t_begin) & 63);
+    if (idx == 0) {
+      const int64_t kk = k + lane;
+      my_t = kk < t_end ? sched[kk] : sched[k];
+      const int2 tt = tiles[my_t];
+      my_x = tt.x;
+      my_y = tt.y;
     }
-    const int64_t t = sched[r0 + ((k - r0) + run_off) % run_len];
-#else
-    const int64_t t = sched[k];
+    const int64_t t = __builtin_amdgcn_readlane(my_t, idx);
+    const int2 tl = make_int2(__builtin_amdgcn_readlane(my_x, idx), __builtin_amdgcn_readlane(my_y, idx));
+    if (tl.x != cur_bi) {  // once per segment: its tiles share one row block
+#ifdef FS_SP2_PROF
+      const uint64_t ps = __builtin_amdgcn_s_memtime();
 #endif
-    const int2 tl = tiles[t];
-    if (tl.x != cur_bi) {
       __syncthreads();
+      // 64 rows x 2 chunks = 128 float4 per lane: 8 per wave, all requested
+      // before the first store (one HBM latency per segment, not eight)
       const float* __restrict__ xa = xs + ((int64_t)tl.x * kTile + h * kHalf) * PW + f0 + 4 * lane;
-      for (int rc = wave; rc < kHalf * 2; rc += kSWaves) {
-        const int r = rc >> 1, c = rc & 1;
-        float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (c < C && f0 + 256 * c + 4 * lane < PW) v = *(const float4*)(xa + (int64_t)r * PW + 256 * c);
-        As[rc * 64 + lane] = v;
+      constexpr int kPer = kHalf * 2 / kSWaves;
+      float4 v[kPer];
+#pragma unroll
+      for (int m = 0; m < kPer; m++) {
+        const int rc = wave + kSWaves * m, r = rc >> 1, c = rc & 1;
+        v[m] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (c < C && f0 + 256 * c + 4 * lane < PW) v[m] = *(const float4*)(xa + (int64_t)r * PW + 256 * c);
       }
+#pragma unroll
+      for (int m = 0; m < kPer; m++) As[(wave + kSWaves * m) * 64 + lane] = v[m];
       __syncthreads();
       cur_bi = tl.x;
+#ifdef FS_SP2_PROF
+      pr_stage += __builtin_amdgcn_s_memtime() - ps;
+#endif
     }
     float acc[F];
 #pragma unroll
@@ -1701,13 +1709,7 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
     for (int q = 0; q < F; q++) s[q] += (double)acc[q];
   }
 #ifdef FS_SP2_PROF
-  if (F == 8 && lane == 0 && pr_tiles > 0) {
-    pr_out += __builtin_amdgcn_s_memtime() - pr_last;  // the last tile to the end of the walk
-    atomicAdd(&fs_sp2_prof[0], (unsigned long long)pr_pro);
-    atomicAdd(&fs_sp2_prof[1], (unsigned long long)pr_body);
-    atomicAdd(&fs_sp2_prof[2], (unsigned long long)pr_out);
-    atomicAdd(&fs_sp2_prof[3], (unsigned long long)pr_tiles);
-  }
+  const uint64_t pr_loop_end = __builtin_amdgcn_s_memtime();
 #endif
   // fixed-order reduction of the 16 waves' partials through the LDS block
   __syncthreads();
@@ -1725,6 +1727,21 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
       v += (rr[w * 64] + rr[(w + 1) * 64]) + (rr[(w + 2) * 64] + rr[(w + 3) * 64]);
     if (f < PW) spart[(seg * 2 + h) * PW + f] = v;
   }
+#ifdef FS_SP2_PROF
+  if (F == 8 && lane == 0 && pr_tiles > 0) {
+    const uint64_t te = __builtin_amdgcn_s_memtime(), re = wall_clock64();
+    pr_out += pr_loop_end - pr_last;  // the last tile to the end of the walk
+    atomicAdd(&fs_sp2_prof[0], (unsigned long long)pr_pro);
+    atomicAdd(&fs_sp2_prof[1], (unsigned long long)pr_body);
+    atomicAdd(&fs_sp2_prof[2], (unsigned long long)(pr_out - pr_stage));
+    atomicAdd(&fs_sp2_prof[3], (unsigned long long)pr_tiles);
+    atomicAdd(&fs_sp2_prof[4], (unsigned long long)pr_stage);
+    atomicAdd(&fs_sp2_prof[5], (unsigned long long)(te - pr_loop_end));  // reduction + write
+    atomicAdd(&fs_sp2_prof[6], (unsigned long long)(te - pr_t0));        // the wave's life
+    atomicAdd(&fs_sp2_prof[7], (unsigned long long)(re - pr_r0));        // same, 100 MHz
+    atomicAdd(&fs_sp2_prof[8], 1ull);
+  }
+#endif
 }
 
 // dst[k] += src[k] (the tile shards' partial vectors, summed in shard order).
@@ -4686,7 +4703,7 @@ static int run_pass2(Plan* g, double* scores_dev) {
 #ifdef FS_SP2_PROF
     void* prp = nullptr;
     FS_HIP(hipGetSymbolAddress(&prp, HIP_SYMBOL(fs_sp2_prof)));
-    FS_HIP(hipMemsetAsync(prp, 0, 4 * sizeof(unsigned long long), g->stream));
+    FS_HIP(hipMemsetAsync(prp, 0, 9 * sizeof(unsigned long long), g->stream));
 #endif
     if (g->nunits8 > 0) {
       k_score_sparse2<8><<<(unsigned)g->nunits8, 64 * kSWaves, 0, g->stream>>>(
@@ -4701,15 +4718,20 @@ static int run_pass2(Plan* g, double* scores_dev) {
     }
 #ifdef FS_SP2_PROF
     if (trace_on()) {
-      unsigned long long pr[4] = {0, 0, 0, 0};
+      unsigned long long pr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
       FS_HIP(hipMemcpyAsync(pr, prp, sizeof(pr), hipMemcpyDeviceToHost, g->stream));
       FS_HIP(hipStreamSynchronize(g->stream));
-      const double tot = (double)(pr[0] + pr[1] + pr[2]);
+      const double life = (double)pr[6];
       std::fprintf(stderr,
                    "[fs_trace] k_score_sparse2<8> per wave-tile (shader clocks): start %.0f, walk "
-                   "%.0f, outside %.0f; shares %.3f / %.3f / %.3f over %llu wave-tiles\n",
+                   "%.0f, between %.0f, staging %.0f; of the waves' lives: start %.3f walk %.3f "
+                   "between %.3f staging %.3f reduction %.3f other %.3f; %llu wave-tiles, %llu "
+                   "waves, %.0f clocks / %.2f us per wave (%.2f GHz)\n",
                    pr[0] / (double)pr[3], pr[1] / (double)pr[3], pr[2] / (double)pr[3],
-                   pr[0] / tot, pr[1] / tot, pr[2] / tot, pr[3]);
+                   pr[4] / (double)pr[3], pr[0] / life, pr[1] / life, pr[2] / life, pr[4] / life,
+                   pr[5] / life, 1.0 - (pr[0] + pr[1] + pr[2] + pr[4] + pr[5]) / life, pr[3], pr[8],
+                   life / pr[8], pr[7] / (double)pr[8] / 100.0,
+                   life / (pr[7] / 100.0) / 1e3);
     }
 #endif
   } else {
