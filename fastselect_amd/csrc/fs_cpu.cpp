@@ -181,6 +181,10 @@ static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
                             int n_jobs, std::vector<double>& corr) {
   const int64_t n = P.n;
   const int s = colsort_key_shift(P.qmax);
+  // the GPU's route for this n: binned columns (k_colsort) up to 24576
+  // samples, beyond that (or under FS_COLSORT_GLOBAL) every column sorted
+  // whole by the device segmented sort -- position terms, ties by index
+  const bool binned = gpu::colsort_lds(n);
   std::vector<float> term((size_t)n * std::max<int64_t>(P.pc, 1), 0.0f);
   parallel_for(c_hi - c_lo, n_jobs, [&](int64_t cc) {
     const int64_t c = c_lo + cc;
@@ -208,7 +212,7 @@ static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
       cnt[b + 1] += cnt[b];     // exclusive prefix at b, inclusive at b + 1
       esum[b + 1] += esum[b];
     }
-    if (fill > kColsortMaxFill) {
+    if (fill > kColsortMaxFill || !binned) {
       std::vector<uint64_t> ord((size_t)n);
       for (int64_t i = 0; i < n; i++) ord[i] = ((uint64_t)key[i] << 32) | (uint64_t)i;
       std::sort(ord.begin(), ord.end());
@@ -309,7 +313,7 @@ static int64_t refine_pairs(const Prepared& P, const void* x, int x_is_f64, int 
 }
 
 // exact_thresholds (fs_gpu.hip): thresholds from exact distances for the
-// rows a refined pair lies within thr_tol of, when at most kExactThrRows
+// rows a refined pair lies within thr_tol of, when at most exact_thr_rows(n)
 // (every row under the FS_THR_EXACT_ALL test hook).
 static void exact_thresholds(const Prepared& P, const void* x, int n_jobs, const CpuState& S,
                              const std::vector<std::pair<int32_t, int32_t>>& refined,
@@ -327,7 +331,7 @@ static void exact_thresholds(const Prepared& P, const void* x, int n_jobs, const
     }
     for (int64_t i = 0; i < n; i++)
       if (unc[i]) rows.push_back((int32_t)i);
-    if ((int64_t)rows.size() > kExactThrRows) return;
+    if ((int64_t)rows.size() > exact_thr_rows(n)) return;
   }
   parallel_for((int64_t)rows.size(), n_jobs, [&](int64_t k) {
     const int64_t i = rows[k];

@@ -898,7 +898,7 @@ __device__ __forceinline__ void store_pair(double* __restrict__ D, int64_t n_pad
 // within thr_tol of an endpoint's threshold could therefore still be
 // decided differently (VERDICT r3 missing #1's decision-level bar: uniform
 // noise, n = 16384, one row of 16384).  Those rows are flagged here; if no
-// more than kExactThrRows are, their thresholds are recomputed from exact
+// more than exact_thr_rows(n) are, their thresholds are recomputed from exact
 // distances to every other sample (k_row_exact_parts / k_row_exact_thr:
 // the reference's sum_j D_ij and sum_j D_ij^2, MultiSURF.py:174-196) before
 // any pair is counted.  A rank fixes the rows its own refined pairs flag:
@@ -1635,6 +1635,17 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
   const uint64_t pr_t0 = __builtin_amdgcn_s_memtime(), pr_r0 = wall_clock64();
   uint64_t pr_last = pr_t0;
 #endif
+  // VALU issue goes to the oldest ready wave of a SIMD (MI355X_MICROARCH.md,
+  // "Two waves per SIMD" item 2), so with equal static shares the 16 waves
+  // of a unit finished staggered -- the oldest first, the youngest last with
+  // few partners to hide its latency: 26% of the waves' lives waited at the
+  // final barrier (FS_SP2_PROF, profiles/r04/pass2_prio.txt).  A wave behind
+  // the workgroup's mean progress (tiles done, an LDS counter) raises its
+  // priority until it has caught up: 4.9% left waiting, pass 2 88.0 -> 81.2
+  // ms at cfg4.  The scores do not change (same streams per wave, same order).
+  __shared__ unsigned int wg_done;
+  if (threadIdx.x == 0) wg_done = 0u;  // before the first staging barrier
+  unsigned int my_done = 0;
   // The segment's tile list, 64 tiles per lane-indexed load: tile k - t_begin
   // is lane (k - t_begin) % 64 of my_t / my_x / my_y (v_readlane per tile,
   // instead of two dependent scalar loads -- sched, then tiles -- per tile).
@@ -1707,6 +1718,28 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
     }
 #pragma unroll
     for (int q = 0; q < F; q++) s[q] += (double)acc[q];
+    unsigned int tot = 0;
+    if (lane == 0) tot = atomicAdd(&wg_done, 1u) + 1u;
+    tot = __builtin_amdgcn_readfirstlane(tot);
+    ++my_done;
+#ifdef FS_SP2_PRIO_GRADED
+    // A/B: priority graded by the deficit in tiles (wave-tiles / 16)
+    const unsigned int need = my_done * kSWaves;
+    const unsigned int def = tot > need ? (tot - need) : 0u;
+    if (def >= 3 * kSWaves)
+      __builtin_amdgcn_s_setprio(3);
+    else if (def >= 2 * kSWaves)
+      __builtin_amdgcn_s_setprio(2);
+    else if (def > 0)
+      __builtin_amdgcn_s_setprio(1);
+    else
+      __builtin_amdgcn_s_setprio(0);
+#else
+    if (my_done * kSWaves < tot)
+      __builtin_amdgcn_s_setprio(2);
+    else
+      __builtin_amdgcn_s_setprio(0);
+#endif
   }
 #ifdef FS_SP2_PROF
   const uint64_t pr_loop_end = __builtin_amdgcn_s_memtime();
@@ -3282,7 +3315,7 @@ struct Plan {
   unsigned int* unc = nullptr;  // [n_pad] row flags
   int32_t* urows = nullptr;     // [n_pad + 1] flagged rows in index order, then their count
   double2* uparts = nullptr;    // [thr_rows][nchunk] exact row-moment partials
-  int thr_rows = kExactThrRows; // rows fixed at most (FS_THR_EXACT_ALL: every row, tests)
+  int thr_rows = kExactThrRows; // rows fixed at most: exact_thr_rows(n) (FS_THR_EXACT_ALL: all, tests)
   bool thr_all = false;
   int32_t n_exact_thr = 0;      // rows whose threshold the last select recomputed (-1: too many)
   // ambiguous-pair refinement
@@ -4452,7 +4485,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     // test hook: every row's threshold from exact distances (the machinery
     // of exact_thresholds checked on all rows against the oracle's)
     g->thr_all = std::getenv("FS_THR_EXACT_ALL") != nullptr;
-    g->thr_rows = g->thr_all ? (int)Q.n : kExactThrRows;
+    g->thr_rows = (int)(g->thr_all ? Q.n : exact_thr_rows(Q.n));
     const int64_t nchunk = (Q.n + 255) / 256;
     if ((rc = dalloc(g, &g->unc, Q.n_pad)) || (rc = dalloc(g, &g->urows, Q.n_pad + 1)) ||
         (rc = dalloc(g, &g->uparts, (size_t)g->thr_rows * nchunk)))

@@ -180,7 +180,14 @@ int hardware_threads(int n_jobs);
 // Rows whose MultiSURF threshold a select recomputes from exact distances
 // at most (exact_thresholds in both backends): a refined pair that close to
 // a quantised threshold could be decided differently from the reference.
+// Each such row costs n p exact pair-features (~1/(n / 64) of pass 1's
+// pair-features in float64 sums, ~8x the issue cost per feature of the
+// integer pass 1): up to max(64, n / 64) rows, i.e. at most ~1/4 of a 32-bit
+// pass 1 and mostly far less (32-bit operands: a handful of rows; the
+// heavy-tailed family at n = 16384: 167; 16-bit operands: ~1000 rows, above
+// the cap, where the decision check stays in charge).
 constexpr int kExactThrRows = 64;
+inline int64_t exact_thr_rows(int64_t n) { return n / 64 > kExactThrRows ? n / 64 : kExactThrRows; }
 
 // Thresholds shared by both backends (MultiSURF.py:193-196 in D units).
 FS_HD inline double multisurf_threshold(double s1, double s2, int64_t n) {

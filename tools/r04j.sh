@@ -16,4 +16,5 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$GRAFT_REPO_ROOT/$
   -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-q32 --no-fit \
   > "$GRAFT_REPO_ROOT/$out/prof.log" 2>&1 || exit $?
 cd "$GRAFT_REPO_ROOT" || exit 1
-bash tools/sp2_prof.sh r04j_sp2 sp2prof2 || exit $?
+bash tools/sp2_prof.sh r04j_sp2 sp2prof || exit $?
+bash tools/variant_ab.sh r04j_ab 2 default graded || exit $?
