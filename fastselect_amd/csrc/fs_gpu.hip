@@ -4565,6 +4565,18 @@ static int run_quantize_dist(Plan* g) {
     // coherently and heavy-tailed columns crowd most samples into a few
     // quanta, and both move the thresholds (intgrid, n = 3000: 2.2e-5
     // without it; lognormal: VERDICT r3 missing #1).
+#if defined(FS_NO_MEANCORR)
+    // A/B timing only (wrong thresholds): no mean correction at all
+    FS_HIP(hipMemsetAsync(g->corr, 0, sizeof(double) * Q.n_pad, g->stream));
+    FS_HIP(hipEventRecord(g->ev_join, g->stream));
+#elif defined(FS_MC_MAIN)
+    // A/B timing only: the mean correction on the main stream, before k_dist
+    FS_TRY(run_colsort(g, g->c_lo, g->c_hi, g->stream));
+    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, g->stream>>>(g->epsT, Q.n, Q.n_pad, g->c_lo,
+                                                                 g->c_hi, g->corr);
+    FS_TRY(launch_check("k_rowcorr"));
+    FS_HIP(hipEventRecord(g->ev_join, g->stream));
+#else
     FS_HIP(hipEventRecord(g->ev_fork, g->stream));
     FS_HIP(hipStreamWaitEvent(g->side, g->ev_fork, 0));
     FS_TRY(run_colsort(g, g->c_lo, g->c_hi, g->side));
@@ -4572,6 +4584,7 @@ static int run_quantize_dist(Plan* g) {
                                                                g->c_hi, g->corr);
     FS_TRY(launch_check("k_rowcorr"));
     FS_HIP(hipEventRecord(g->ev_join, g->side));
+#endif
   }
   if (g->n_tiles > 0) {
     FS_HIP(hipEventRecord(g->ev[0], g->stream));

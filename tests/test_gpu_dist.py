@@ -108,3 +108,77 @@ def test_pinned_float32_cast_equals_numpy():
         assert got.flags.c_contiguous and got.dtype == np.float32
         np.testing.assert_array_equal(got, x.astype(np.float32))
         del got
+
+
+def _uniform_family():
+    import importlib.util
+    here = os.path.dirname(os.path.abspath(__file__))
+    spec = importlib.util.spec_from_file_location("mk_families",
+                                                  os.path.join(here, "golden", "make_families.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    return mk.make("uniform_16k")
+
+
+def test_nccl_world1_decision_check_reruns():
+    """The 16-bit decision check on the RCCL path: on
+    signal-free data the all-reduced risk trips it, the plan moves to 32-bit
+    operands and the step runs again -- the result is the one-shot fit's."""
+    import torch
+    import torch.distributed as dist
+
+    import fastselect_amd as F
+    from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_port())
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        X, y = _uniform_family()
+        x, yv, recip, isd = prepare_inputs(X, y, backend="gpu", device=0)
+        job = ShardedMultiSURF(x, yv, recip, isd, backend="gpu", device=0)
+        assert job.dist is not None
+        s = job.step().cpu().numpy()
+        risk, switched = job.last_guard
+        job.close()
+    finally:
+        dist.destroy_process_group()
+    assert risk > 5e-6 and switched
+    one = F.MultiSURF(backend="gpu", n_features_to_select=10).fit(X, y).feature_importances_
+    np.testing.assert_array_equal(s, one)
+
+
+def _guard_rank_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
+    X, y = _uniform_family()
+    x, yv, recip, isd = prepare_inputs(X, y, backend="gpu", device=0)
+    job = ShardedMultiSURF(x, yv, recip, isd, backend="gpu", device=0)
+    s = job.step().cpu().numpy()
+    np.save(f"{out_path}.{rank}.npy", s)
+    np.save(f"{out_path}.{rank}.guard.npy", np.array(job.last_guard, dtype=np.float64))
+    job.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_decide_the_rerun_together(tmp_path):
+    """World 2 (two ranks sharing cuda:0, gloo): each rank holds half the
+    tiles, both see the same all-reduced risk and re-run on 32-bit operands
+    together; both end with the one-shot fit's scores."""
+    import torch.multiprocessing as mp
+
+    import fastselect_amd as F
+    out = str(tmp_path / "guard")
+    mp.spawn(_guard_rank_worker, args=(2, _port(), out), nprocs=2, join=True)
+    a, b = np.load(out + ".0.npy"), np.load(out + ".1.npy")
+    ga, gb = np.load(out + ".0.guard.npy"), np.load(out + ".1.guard.npy")
+    np.testing.assert_array_equal(ga, gb)
+    assert ga[0] > 5e-6 and ga[1] == 1.0
+    np.testing.assert_array_equal(a, b)
+    X, y = _uniform_family()
+    one = F.MultiSURF(backend="gpu", n_features_to_select=10).fit(X, y).feature_importances_
+    assert np.max(np.abs(a - one)) <= 1e-6 * np.max(np.abs(one))
