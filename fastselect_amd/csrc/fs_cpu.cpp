@@ -313,7 +313,7 @@ static int64_t refine_pairs(const Prepared& P, const void* x, int x_is_f64, int 
 }
 
 // exact_thresholds (fs_gpu.hip): thresholds from exact distances for the
-// rows a refined pair lies within thr_tol of, when at most exact_thr_rows(n)
+// rows a refined pair lies within thr_tol of, when at most exact_thr_rows(n, p)
 // (every row under the FS_THR_EXACT_ALL test hook).
 static void exact_thresholds(const Prepared& P, const void* x, int n_jobs, const CpuState& S,
                              const std::vector<std::pair<int32_t, int32_t>>& refined,
@@ -331,7 +331,7 @@ static void exact_thresholds(const Prepared& P, const void* x, int n_jobs, const
     }
     for (int64_t i = 0; i < n; i++)
       if (unc[i]) rows.push_back((int32_t)i);
-    if ((int64_t)rows.size() > exact_thr_rows(n)) return;
+    if ((int64_t)rows.size() > exact_thr_rows(n, P.pc + P.pd)) return;
   }
   parallel_for((int64_t)rows.size(), n_jobs, [&](int64_t k) {
     const int64_t i = rows[k];

@@ -939,55 +939,99 @@ __global__ __launch_bounds__(1024) void k_unc_compact(const unsigned int* __rest
   if (t == 1023) *nrows = part[1023];
 }
 
-// Exact row moments of the flagged rows, in chunks of 256 samples: grid
-// (chunks, max_rows); slot s takes rows[s] when the count allows the fix.  Each wave sums 64 samples j != i: per sample the lanes stride the
-// features with k_exact_pairs' arithmetic (float32 diffs for float32 X, a
-// float64 sum), then lane 0 adds D_ij and D_ij^2 in j order; the 4 waves'
-// partials go to parts[s][chunk] in a fixed order.
+// Exact row moments of the flagged rows: grid (chunks of 64 samples j,
+// groups of 8 flagged rows); the group's slots take rows[8 g + k] when the
+// count allows the fix (slots past the count repeat the group's last row and
+// are discarded).  A wave sums 4 samples at a time against the 8 rows: lane l
+// strides the features (k_exact_pairs' arithmetic per feature: float32
+// |a - b| * recip, a float64 sum), each of the 12 row values per feature is
+// read once for 32 pair-features, so X streams once per 8 flagged rows
+// rather than once per row; each pair's lane sums are then reduced across
+// the wave and D_ij, D_ij^2 added in j order (j != i).  The 4 waves'
+// partials go to parts[8 g + k][chunk] in a fixed order.
+constexpr int kExRows = 8, kExJ = 4;
 template <typename T>
 __global__ __launch_bounds__(256) void k_row_exact_parts(
     const T* __restrict__ x, int64_t n, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
     const int64_t* __restrict__ src_col, const double* __restrict__ scl,
     const int32_t* __restrict__ rows, const int32_t* __restrict__ nrows, int max_rows,
     double2* __restrict__ parts) {
-  __shared__ double2 wsum[4];
+  __shared__ double2 wsum[4][kExRows];
   const int cnt = *nrows;
-  const int slot = blockIdx.y;
-  if (cnt > max_rows || slot >= cnt) return;
+  const int g = blockIdx.y;
+  if (cnt > max_rows || g * kExRows >= cnt) return;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t i = rows[slot];
-  const T* xi = x + i * p_in;
-  double s1 = 0.0, s2 = 0.0;
-  const int64_t j0 = (int64_t)blockIdx.x * 256 + wave * 64;
-  for (int q = 0; q < 64; q++) {
-    const int64_t j = j0 + q;
-    if (j >= n) break;
-    if (j == i) continue;
-    const T* xj = x + j * p_in;
-    double acc = 0.0;
+  const int nr = cnt - g * kExRows < kExRows ? cnt - g * kExRows : kExRows;
+  int64_t ri[kExRows];
+#pragma unroll
+  for (int k = 0; k < kExRows; k++) ri[k] = rows[g * kExRows + (k < nr ? k : nr - 1)];
+  double s1[kExRows], s2[kExRows];
+#pragma unroll
+  for (int k = 0; k < kExRows; k++) s1[k] = s2[k] = 0.0;
+  const int64_t jw = (int64_t)blockIdx.x * 64 + wave * 16;
+  for (int jb = 0; jb < 16; jb += kExJ) {
+    int64_t jj[kExJ];
+#pragma unroll
+    for (int m = 0; m < kExJ; m++) jj[m] = jw + jb + m < n ? jw + jb + m : n - 1;
+    double acc[kExRows][kExJ];
+#pragma unroll
+    for (int k = 0; k < kExRows; k++)
+#pragma unroll
+      for (int m = 0; m < kExJ; m++) acc[k][m] = 0.0;
     for (int64_t c = lane; c < pc; c += 64) {
       const int64_t col = src_col[c];
+      T a[kExRows], b[kExJ];
+#pragma unroll
+      for (int k = 0; k < kExRows; k++) a[k] = x[ri[k] * p_in + col];
+#pragma unroll
+      for (int m = 0; m < kExJ; m++) b[m] = x[jj[m] * p_in + col];
       if (sizeof(T) == 4) {
-        const float dv = __builtin_fabsf((float)xi[col] - (float)xj[col]) * (float)scl[c];
-        acc += (double)dv;
+        const float r = (float)scl[c];
+#pragma unroll
+        for (int k = 0; k < kExRows; k++)
+#pragma unroll
+          for (int m = 0; m < kExJ; m++)
+            acc[k][m] += (double)(__builtin_fabsf((float)a[k] - (float)b[m]) * r);
       } else {
-        acc += __builtin_fabs((double)xi[col] - (double)xj[col]) * scl[c];
+        const double r = scl[c];
+#pragma unroll
+        for (int k = 0; k < kExRows; k++)
+#pragma unroll
+          for (int m = 0; m < kExJ; m++)
+            acc[k][m] += __builtin_fabs((double)a[k] - (double)b[m]) * r;
       }
     }
     for (int64_t c = PC + lane; c < PC + pd; c += 64) {
       const int64_t col = src_col[c];
-      acc += (xi[col] != xj[col]) ? 1.0 : 0.0;
+#pragma unroll
+      for (int k = 0; k < kExRows; k++)
+#pragma unroll
+        for (int m = 0; m < kExJ; m++)
+          acc[k][m] += (x[ri[k] * p_in + col] != x[jj[m] * p_in + col]) ? 1.0 : 0.0;
     }
-    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-    s1 += acc;
-    s2 += acc * acc;
+#pragma unroll
+    for (int k = 0; k < kExRows; k++)
+#pragma unroll
+      for (int m = 0; m < kExJ; m++) {
+        double v = acc[k][m];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        const int64_t j = jw + jb + m;
+        if (j < n && j != ri[k]) {
+          s1[k] += v;
+          s2[k] += v * v;
+        }
+      }
   }
-  if (lane == 0) wsum[wave] = make_double2(s1, s2);
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < kExRows; k++) wsum[wave][k] = make_double2(s1[k], s2[k]);
   __syncthreads();
-  if (threadIdx.x == 0)
-    parts[(int64_t)slot * gridDim.x + blockIdx.x] =
-        make_double2((wsum[0].x + wsum[1].x) + (wsum[2].x + wsum[3].x),
-                     (wsum[0].y + wsum[1].y) + (wsum[2].y + wsum[3].y));
+  if (threadIdx.x < nr) {
+    const int k = threadIdx.x;
+    parts[(int64_t)(g * kExRows + k) * gridDim.x + blockIdx.x] =
+        make_double2((wsum[0][k].x + wsum[1][k].x) + (wsum[2][k].x + wsum[3][k].x),
+                     (wsum[0][k].y + wsum[1][k].y) + (wsum[2][k].y + wsum[3][k].y));
+  }
 }
 
 // thr[rows[s]] from the chunk partials (fixed order), in integer units.
@@ -4485,8 +4529,8 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     // test hook: every row's threshold from exact distances (the machinery
     // of exact_thresholds checked on all rows against the oracle's)
     g->thr_all = std::getenv("FS_THR_EXACT_ALL") != nullptr;
-    g->thr_rows = (int)(g->thr_all ? Q.n : exact_thr_rows(Q.n));
-    const int64_t nchunk = (Q.n + 255) / 256;
+    g->thr_rows = (int)(g->thr_all ? Q.n : exact_thr_rows(Q.n, Q.pc + Q.pd));
+    const int64_t nchunk = (Q.n + 63) / 64;
     if ((rc = dalloc(g, &g->unc, Q.n_pad)) || (rc = dalloc(g, &g->urows, Q.n_pad + 1)) ||
         (rc = dalloc(g, &g->uparts, (size_t)g->thr_rows * nchunk)))
       return fail(rc);
@@ -4678,7 +4722,8 @@ static int refine_pairs(Plan* g, int algo, double delta, double thr_tol = 0.0,
 // reported by fs_plan_info-style diagnostics: g->n_exact_thr).
 static int exact_thresholds(Plan* g) {
   const Prepared& Q = g->P;
-  const int64_t nchunk = (Q.n + 255) / 256;
+  const int64_t nchunk = (Q.n + 63) / 64;
+  const unsigned ngroups = (unsigned)((g->thr_rows + kExRows - 1) / kExRows);
   if (g->thr_all) {  // test hook: flag every row
     std::vector<int32_t> all((size_t)Q.n + 1);
     for (int64_t i = 0; i < Q.n; i++) all[i] = (int32_t)i;
@@ -4691,11 +4736,11 @@ static int exact_thresholds(Plan* g) {
   }
   const int32_t* nrows = g->urows + g->thr_rows;
   if (g->x_is_f64)
-    k_row_exact_parts<double><<<dim3((unsigned)nchunk, (unsigned)g->thr_rows), 256, 0, g->stream>>>(
+    k_row_exact_parts<double><<<dim3((unsigned)nchunk, ngroups), 256, 0, g->stream>>>(
         (const double*)g->x, Q.n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, g->urows, nrows,
         g->thr_rows, g->uparts);
   else
-    k_row_exact_parts<float><<<dim3((unsigned)nchunk, (unsigned)g->thr_rows), 256, 0, g->stream>>>(
+    k_row_exact_parts<float><<<dim3((unsigned)nchunk, ngroups), 256, 0, g->stream>>>(
         (const float*)g->x, Q.n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, g->urows, nrows,
         g->thr_rows, g->uparts);
   FS_TRY(launch_check("k_row_exact_parts"));

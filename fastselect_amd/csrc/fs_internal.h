@@ -180,14 +180,18 @@ int hardware_threads(int n_jobs);
 // Rows whose MultiSURF threshold a select recomputes from exact distances
 // at most (exact_thresholds in both backends): a refined pair that close to
 // a quantised threshold could be decided differently from the reference.
-// Each such row costs n p exact pair-features (~1/(n / 64) of pass 1's
-// pair-features in float64 sums, ~8x the issue cost per feature of the
-// integer pass 1): up to max(64, n / 64) rows, i.e. at most ~1/4 of a 32-bit
-// pass 1 and mostly far less (32-bit operands: a handful of rows; the
-// heavy-tailed family at n = 16384: 167; 16-bit operands: ~1000 rows, above
-// the cap, where the decision check stays in charge).
+// Each such row costs n p exact pair-features with float64 sums: up to
+// max(64, min(n / 64, 3e10 / (n p))) rows -- at most ~3e10 pair-features
+// (a few ms on an MI355X) beyond the first 64.  32-bit operands flag a
+// handful of rows (the heavy-tailed family at n = 16384: 167); 16-bit ones
+// ~1000 at n >= 16384, above the cap, where the decision check stays in
+// charge.
 constexpr int kExactThrRows = 64;
-inline int64_t exact_thr_rows(int64_t n) { return n / 64 > kExactThrRows ? n / 64 : kExactThrRows; }
+inline int64_t exact_thr_rows(int64_t n, int64_t p) {
+  const double budget = 3e10 / ((double)(n > 1 ? n : 1) * (double)(p > 1 ? p : 1));
+  int64_t r = n / 64 < (int64_t)budget ? n / 64 : (int64_t)budget;
+  return r > kExactThrRows ? r : kExactThrRows;
+}
 
 // Thresholds shared by both backends (MultiSURF.py:193-196 in D units).
 FS_HD inline double multisurf_threshold(double s1, double s2, int64_t n) {
