@@ -939,7 +939,8 @@ __global__ __launch_bounds__(1024) void k_unc_compact(const unsigned int* __rest
   if (t == 1023) *nrows = part[1023];
 }
 
-// Exact row moments of the flagged rows: grid (chunks of 64 samples j,
+// Exact row moments of the flagged rows: grid (chunks of 16 samples j --
+// many workgroups even for one flagged row: the loop is latency-bound --,
 // groups of 8 flagged rows); the group's slots take rows[8 g + k] when the
 // count allows the fix (slots past the count repeat the group's last row and
 // are discarded).  A wave sums 4 samples at a time against the 8 rows: lane l
@@ -968,8 +969,9 @@ __global__ __launch_bounds__(256) void k_row_exact_parts(
   double s1[kExRows], s2[kExRows];
 #pragma unroll
   for (int k = 0; k < kExRows; k++) s1[k] = s2[k] = 0.0;
-  const int64_t jw = (int64_t)blockIdx.x * 64 + wave * 16;
-  for (int jb = 0; jb < 16; jb += kExJ) {
+  const int64_t jw = (int64_t)blockIdx.x * 16 + wave * kExJ;
+  {
+    constexpr int jb = 0;
     int64_t jj[kExJ];
 #pragma unroll
     for (int m = 0; m < kExJ; m++) jj[m] = jw + jb + m < n ? jw + jb + m : n - 1;
@@ -978,6 +980,7 @@ __global__ __launch_bounds__(256) void k_row_exact_parts(
     for (int k = 0; k < kExRows; k++)
 #pragma unroll
       for (int m = 0; m < kExJ; m++) acc[k][m] = 0.0;
+#pragma unroll 2
     for (int64_t c = lane; c < pc; c += 64) {
       const int64_t col = src_col[c];
       T a[kExRows], b[kExJ];
@@ -4139,8 +4142,13 @@ static int shard_segments(Plan* g) {
   // profiles/r02/cfg2_sweep.txt: cfg2 step 6.11 -> 5.83 ms at 4096-8192).
   // sparse: (512-feature block, half) units, two per 512 features
   const int64_t nfb = !g->sparse ? (Q.PW + 127) / 128 : 2 * ((Q.PW + 511) / 512);
+  // Round 4 (progress priority, build_sparse_schedule): small problems take
+  // a sixteenth of their units as the target, at least 1024 -- longer
+  // segments amortise each unit's staging and final barrier (cfg2: 16 tiles
+  // per segment, pass 2 1.50-1.54 -> 1.39-1.42 ms, profiles/r04/seg_len_ab.txt;
+  // cfg4 keeps ~31)
   const int64_t wgs =
-      g->sparse ? std::min<int64_t>(32768, std::max<int64_t>(4096, g->n_tiles * nfb / 4)) : 65536;
+      g->sparse ? std::min<int64_t>(32768, std::max<int64_t>(1024, g->n_tiles * nfb / 16)) : 65536;
   g->seg_len = std::max<int64_t>(1, (g->n_tiles * nfb + wgs - 1) / wgs);
   g->nseg = std::max<int64_t>(1, (g->n_tiles + g->seg_len - 1) / g->seg_len);
   if (Q.algo == ALGO_RELIEFF) return FS_OK;
@@ -4530,7 +4538,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     // of exact_thresholds checked on all rows against the oracle's)
     g->thr_all = std::getenv("FS_THR_EXACT_ALL") != nullptr;
     g->thr_rows = (int)(g->thr_all ? Q.n : exact_thr_rows(Q.n, Q.pc + Q.pd));
-    const int64_t nchunk = (Q.n + 63) / 64;
+    const int64_t nchunk = (Q.n + 15) / 16;
     if ((rc = dalloc(g, &g->unc, Q.n_pad)) || (rc = dalloc(g, &g->urows, Q.n_pad + 1)) ||
         (rc = dalloc(g, &g->uparts, (size_t)g->thr_rows * nchunk)))
       return fail(rc);
@@ -4722,7 +4730,7 @@ static int refine_pairs(Plan* g, int algo, double delta, double thr_tol = 0.0,
 // reported by fs_plan_info-style diagnostics: g->n_exact_thr).
 static int exact_thresholds(Plan* g) {
   const Prepared& Q = g->P;
-  const int64_t nchunk = (Q.n + 63) / 64;
+  const int64_t nchunk = (Q.n + 15) / 16;
   const unsigned ngroups = (unsigned)((g->thr_rows + kExRows - 1) / kExRows);
   if (g->thr_all) {  // test hook: flag every row
     std::vector<int32_t> all((size_t)Q.n + 1);
