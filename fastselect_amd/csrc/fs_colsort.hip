@@ -228,11 +228,6 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
   __shared__ ColbinSmem<IPT> sm;
   constexpr int kWords = (kCsThreads * IPT + 31) / 32;
   const int tid = threadIdx.x;
-#ifdef FS_COLSORT_FULL_ALL
-  // A/B timing only: every column through k_colsort_full
-  if (tid == 0) crowded[blockIdx.x] = 1;
-  return;
-#endif
   const int64_t c = c_lo + blockIdx.x;
   float* __restrict__ e = epsT + c * n_pad;
   const int nn = (int)n;  // <= 1024 IPT (colsort_lds)

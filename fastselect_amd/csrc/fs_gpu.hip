@@ -1769,24 +1769,10 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
     if (lane == 0) tot = atomicAdd(&wg_done, 1u) + 1u;
     tot = __builtin_amdgcn_readfirstlane(tot);
     ++my_done;
-#ifdef FS_SP2_PRIO_GRADED
-    // A/B: priority graded by the deficit in tiles (wave-tiles / 16)
-    const unsigned int need = my_done * kSWaves;
-    const unsigned int def = tot > need ? (tot - need) : 0u;
-    if (def >= 3 * kSWaves)
-      __builtin_amdgcn_s_setprio(3);
-    else if (def >= 2 * kSWaves)
-      __builtin_amdgcn_s_setprio(2);
-    else if (def > 0)
-      __builtin_amdgcn_s_setprio(1);
-    else
-      __builtin_amdgcn_s_setprio(0);
-#else
     if (my_done * kSWaves < tot)
       __builtin_amdgcn_s_setprio(2);
     else
       __builtin_amdgcn_s_setprio(0);
-#endif
   }
 #ifdef FS_SP2_PROF
   const uint64_t pr_loop_end = __builtin_amdgcn_s_memtime();
@@ -4067,7 +4053,8 @@ static int build_sparse_schedule(Plan* g) {
     const int I = g->h_tiles[t].x;
     const int64_t c = g->h_tiles[t].y / CJ;
     int64_t e = t;
-    while (e < T && g->h_tiles[e].x == I && g->h_tiles[e].y / CJ == c) e++;
+    // at most 64 tiles (a lane-indexed tile list per segment)
+    while (e < T && e - t < 64 && g->h_tiles[e].x == I && g->h_tiles[e].y / CJ == c) e++;
     for (int64_t k = e - 1; k >= t; k--) sched.push_back((int32_t)k);
     groups[{c, I / kSchedRows}].push_back((int32_t)seg_tiles.size());
     seg_tiles.push_back(e - t);

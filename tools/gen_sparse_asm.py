@@ -1166,6 +1166,211 @@ def gen_v2x(name, F=8, lead=3, S=8):
 """
 
 
+SEG_DOC = """
+Segment walk (measured in round 4, not shipped: profiles/r04/pass2_seg_ab.txt,
++0.7 ms at cfg4; the function stays for the record): the
+tile loop of one unit inside the asm block.  Per tile: the stream base and
+the B pointer from the lane-indexed tile list (v_readlane), the v2 stream
+walk (16 entries per step, rows read 3 entries ahead), the tile's f32
+partials flushed into the unit's f64 sums, the progress counter in LDS and
+s_setprio as in the C++ loop.  What the C++ loop cannot do: the next tile's
+columns 0 and 1 are loaded into spare VGPRs (BN0 / BN1) when the current
+stream enters its last column, so a tile starts with its B rows in
+registers, and no SGPR is spilled around a per-tile asm statement.
+"""
+
+
+def gen_v2seg(name, lead=3):
+    F, L, R = 8, lead, 2
+    SET = [36, 68]
+    BCUR, BNXT = 24, 32
+    RING = 40                       # (L + 1) slots of 8
+    ACC = RING + F * (L + 1)        # 72: the tile's f32 partials
+    BN0, BN1 = ACC + 8, ACC + 16    # 80, 88: next tile's columns 0 / 1
+    T64 = ACC + 24                  # 96-97: f64 temporary
+    VTOT = T64 + 2                  # 98
+    OFF, TMP, BASE, COLS, TMP2, BPTR = 24, 25, 26, 22, 23, 20
+    # s32 / s33 are the ABI's stack and frame pointers: not touched
+    KT, DONE, TT, NB, TY = 28, 29, 30, 34, 25
+    assert RING + F * (L + 1) == ACC
+
+    def slot(e):
+        return RING + F * (e % (L + 1))
+
+    def entry_sgprs(k, e):
+        base = SET[k] + 2 * e
+        return base, base + 1
+
+    def read(k, e):
+        r, _ = entry_sgprs(k, e)
+        a = slot(e)
+        return [f"v_add_u32 v{a}, s{r}, %[lds_lane]",
+                f"ds_read_b128 v[{a + 4}:{a + 7}], v{a} offset:1024",
+                f"ds_read_b128 v[{a}:{a + 3}], v{a}"]
+
+    def compute(k, e):
+        _, w = entry_sgprs(k, e)
+        a = slot(e)
+        L_ = [f"v_sub_f32 v{a + f}, v{a + f}, v{BCUR + f}" for f in range(F)]
+        L_ += [f"v_fma_f32 v{ACC + f}, s{w}, |v{a + f}|, v{ACC + f}" for f in range(F)]
+        return L_
+
+    def bload(dst, ptr):
+        return [f"global_load_dwordx4 v[{dst}:{dst + 3}], %[glb_lane], s[{ptr}:{ptr + 1}]",
+                f"global_load_dwordx4 v[{dst + 4}:{dst + 7}], %[glb_lane], s[{ptr}:{ptr + 1}] offset:1024"]
+
+    def next_tile_ptr(idx_sgpr):
+        # NB = xs_wave + y(tile idx) * tstride  (64-bit product)
+        return [f"v_readlane_b32 s{TY}, %[ys], s{idx_sgpr}",
+                f"s_mul_i32 s{TT}, s{TY}, %[tstride]",
+                f"s_mul_hi_u32 s{TT + 1}, s{TY}, %[tstride]",
+                f"s_add_u32 s{NB}, %[xsw_lo], s{TT}",
+                f"s_addc_u32 s{NB + 1}, %[xsw_hi], s{TT + 1}"]
+
+    def prefetch_next():
+        # the next tile's columns 0 / 1 into BN0 / BN1 (if there is one)
+        return [f"s_add_u32 s{TMP2}, s{KT}, 1",
+                f"s_cmp_ge_u32 s{TMP2}, %[nt]",
+                "s_cbranch_scc1 61f",
+                *next_tile_ptr(TMP2),
+                *bload(BN0, NB),
+                f"s_add_u32 s{NB}, s{NB}, %[bstride]",
+                f"s_addc_u32 s{NB + 1}, s{NB + 1}, 0",
+                *bload(BN1, NB),
+                "61:"]
+
+    out_of_line = []
+
+    def switch(lab, ret):
+        pf_lab = 300 + (lab - 100)
+        # column switch; entering the last column, prefetch the next tile
+        out_of_line.extend([
+            f"{lab}:",
+            f"s_add_u32 s{COLS}, s{COLS}, 1",
+            f"s_cmp_ge_u32 s{COLS}, %[ncols]",
+            "s_cbranch_scc1 8f",
+            "s_waitcnt vmcnt(0)",
+            *[f"v_mov_b32 v{BCUR + f}, v{BNXT + f}" for f in range(F)],
+            f"s_add_u32 s{TMP2}, s{COLS}, 1",
+            f"s_cmp_ge_u32 s{TMP2}, %[ncols]",
+            f"s_cbranch_scc1 {pf_lab}f",
+            f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
+            f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0",
+            *bload(BNXT, BPTR),
+            f"s_branch {ret}b",
+            f"{pf_lab}:"])
+        # (prefetch_next uses the local labels 61; each copy is its own block)
+        blk = prefetch_next()
+        blk = [l.replace("61f", f"{pf_lab + 1000}f").replace("61:", f"{pf_lab + 1000}:") for l in blk]
+        out_of_line.extend(blk)
+        out_of_line.append(f"s_branch {ret}b")
+
+    def step(x):
+        k, o = x % 2, 1 - x % 2
+        S = ["s_waitcnt lgkmcnt(0)",
+             f"s_load_dwordx16 s[{SET[o]}:{SET[o] + 15}], s[{BASE}:{BASE + 1}], s{OFF}",
+             f"s_add_u32 s{TMP}, s{OFF}, 64",
+             f"s_load_dwordx16 s[{SET[o] + 16}:{SET[o] + 31}], s[{BASE}:{BASE + 1}], s{TMP}",
+             f"s_add_u32 s{OFF}, s{OFF}, 128"]
+        for e in range(min(L, 16)):
+            S += read(k, e)
+        issued = min(L, 16)
+        for e in range(16):
+            if e + L < 16:
+                S += read(k, e + L)
+                issued = e + L + 1
+            after = (issued - (e + 1)) * R
+            S.append(f"s_waitcnt lgkmcnt({min(after, 15)})")
+            S += compute(k, e)
+            _, w = entry_sgprs(k, e)
+            sw, ret = 100 + 16 * x + e, 200 + 16 * x + e
+            S += [f"s_bitcmp1_b32 s{w}, 0", f"s_cbranch_scc1 {sw}f", f"{ret}:"]
+            switch(sw, ret)
+        return S
+
+    lines = [f"s_mov_b32 s{KT}, 0",
+             f"s_mov_b32 s{DONE}, %[done0]",
+             # tile 0's columns 0 / 1 into the prefetch registers
+             *next_tile_ptr(KT),
+             *bload(BN0, NB),
+             f"s_add_u32 s{NB}, s{NB}, %[bstride]",
+             f"s_addc_u32 s{NB + 1}, s{NB + 1}, 0",
+             *bload(BN1, NB),
+             "50:",
+             # this tile: stream base and B pointer (column 1)
+             f"v_readlane_b32 s{TY}, %[tiles], s{KT}",
+             f"s_lshl_b32 s{TT}, s{TY}, 17",
+             f"s_lshr_b32 s{TT + 1}, s{TY}, 15",
+             f"s_add_u32 s{BASE}, %[entw_lo], s{TT}",
+             f"s_addc_u32 s{BASE + 1}, %[entw_hi], s{TT + 1}",
+             f"v_readlane_b32 s{TY}, %[ys], s{KT}",
+             f"s_mul_i32 s{TT}, s{TY}, %[tstride]",
+             f"s_mul_hi_u32 s{TT + 1}, s{TY}, %[tstride]",
+             f"s_add_u32 s{BPTR}, %[xsw_lo], s{TT}",
+             f"s_addc_u32 s{BPTR + 1}, %[xsw_hi], s{TT + 1}",
+             f"s_add_u32 s{BPTR}, s{BPTR}, %[bstride]",
+             f"s_addc_u32 s{BPTR + 1}, s{BPTR + 1}, 0",
+             f"s_mov_b32 s{COLS}, 0",
+             *[f"v_mov_b32 v{ACC + f}, 0" for f in range(F)],
+             f"s_load_dwordx16 s[{SET[0]}:{SET[0] + 15}], s[{BASE}:{BASE + 1}], 0x0",
+             f"s_load_dwordx16 s[{SET[0] + 16}:{SET[0] + 31}], s[{BASE}:{BASE + 1}], 0x40",
+             f"s_mov_b32 s{OFF}, 128",
+             "s_waitcnt vmcnt(0)",
+             *[f"v_mov_b32 v{BCUR + f}, v{BN0 + f}" for f in range(F)],
+             *[f"v_mov_b32 v{BNXT + f}, v{BN1 + f}" for f in range(F)],
+             "7:"]
+    for x in range(2):
+        lines += step(x)
+    lines += [f"s_cmp_gt_u32 s{OFF}, 0x1100", "s_cbranch_scc0 7b", "s_branch 8f"]
+    lines += out_of_line
+    # Every column of a stream ends with a flagged entry (an empty one holds
+    # a single flagged zero entry), so with ncols >= 2 the switch into the
+    # last column -- and with it the next tile's prefetch -- always runs.
+    lines += ["8:",
+              "s_waitcnt lgkmcnt(0)",
+              # the tile's partials into the unit's float64 sums
+              *sum(([f"v_cvt_f64_f32 v[{T64}:{T64 + 1}], v{ACC + f}",
+                     f"v_add_f64 %[s{f}], %[s{f}], v[{T64}:{T64 + 1}]"] for f in range(F)), []),
+              # progress: lane 0 adds 1 to the LDS counter (the other lanes 0,
+              # so EXEC stays whole); behind the mean -> priority 2
+              f"ds_add_rtn_u32 v{VTOT}, %[wgd], %[one0]",
+              "s_waitcnt lgkmcnt(0)",
+              f"v_readfirstlane_b32 s{TY}, v{VTOT}",
+              f"s_add_u32 s{TY}, s{TY}, 1",
+              f"s_add_u32 s{DONE}, s{DONE}, 1",
+              f"s_lshl_b32 s{TMP2}, s{DONE}, 4",
+              f"s_cmp_lt_u32 s{TMP2}, s{TY}",
+              "s_cbranch_scc1 64f",
+              "s_setprio 0",
+              "s_branch 65f",
+              "64:",
+              "s_setprio 2",
+              "65:",
+              f"s_add_u32 s{KT}, s{KT}, 1",
+              f"s_cmp_lt_u32 s{KT}, %[nt]",
+              "s_cbranch_scc1 50b",
+              "s_waitcnt vmcnt(0) lgkmcnt(0)"]
+    body = "\n".join(f'      "{l}\\n"  \\' for l in lines)
+    vclob = ", ".join(f'"v{i}"' for i in range(BCUR, VTOT + 1))
+    named = set()
+    for l in lines:
+        for lo, hi in re.findall(r"(?<![a-z_])s\[?(\d+)(?::(\d+)\])?", l):
+            named.update(range(int(lo), int(hi or lo) + 1))
+    sclob = ", ".join(f'"s{i}"' for i in sorted(named))
+    outs = ", ".join(f'[s{i}] "+v"(s_[{i}])' for i in range(F))
+    return f"""#define {name}(s_, lds_lane_, glb_lane_, tiles_, ys_, nt_, entw_lo_, entw_hi_, xsw_lo_, xsw_hi_, tstride_, bstride_, ncols_, wgd_, done0_, one0_)  \\
+  asm volatile(  \\
+{body}
+      : {outs}  \\
+      : [lds_lane] "v"(lds_lane_), [glb_lane] "v"(glb_lane_), [tiles] "v"(tiles_), [ys] "v"(ys_),  \\
+        [nt] "s"(nt_), [entw_lo] "s"(entw_lo_), [entw_hi] "s"(entw_hi_), [xsw_lo] "s"(xsw_lo_),  \\
+        [xsw_hi] "s"(xsw_hi_), [tstride] "s"(tstride_), [bstride] "s"(bstride_), [ncols] "s"(ncols_),  \\
+        [wgd] "v"(wgd_), [done0] "s"(done0_), [one0] "v"(one0_)  \\
+      : {vclob},  \\
+        {sclob}, "scc", "memory")
+"""
+
+
 if __name__ == "__main__":
     # The product uses the v2 loops only (k_score_sparse2; round 4 retired the
     # round-1/2 v1 loop and its A/B variants -- the functions above stay for
