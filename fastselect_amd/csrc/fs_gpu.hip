@@ -3368,6 +3368,9 @@ struct Plan {
   std::vector<void*> owned_shard;   // buffers sized by the owned tiles (plan_set_shard)
   int alloc_target = 0;             // dalloc target: 0 owned, 1 owned_layout, 2 scratch, 3 shard
   bool row_mode = false;
+  // the row guard's quantised operands and mean correction are the first
+  // step's (one plan over every continuous column): pass 1 takes them
+  bool corr_ready = false;
   std::vector<char> colmin, colmax; // per input column, x's dtype (device-measured)
 };
 
@@ -4113,6 +4116,7 @@ static int build_sparse_schedule(Plan* g) {
 // calibration (none of them depends on the shard).
 static int shard_segments(Plan* g) {
   const Prepared& Q = g->P;
+  g->corr_ready = false;  // a new column share: the row guard's correction is not this shard's
   g->c_lo = Q.pc * g->rank / g->world;
   g->c_hi = Q.pc * (g->rank + 1) / g->world;
   // Pass-2 workgroups: ~64k for the dense pass (256 threads, 128-feature
@@ -4207,8 +4211,12 @@ static int row_guard(Plan* g) {
   const char* guard = std::getenv("FS_Q16_GUARD");
   if (!Q.q16 || Q.pc == 0 || Q.n < 2 || Q.algo == ALGO_SURF || (guard && *guard == '0'))
     return FS_OK;
-  double* corr = nullptr;
-  FS_TRY(dev_alloc((void**)&corr, sizeof(double) * Q.n_pad, g->device));
+  // a plan over every continuous column (one rank, one shard) keeps the
+  // guard's work for its first pass 1: operands, terms and the correction
+  // itself (g->corr) are what that pass would compute again
+  const bool reuse = g->c_lo == 0 && g->c_hi == Q.pc;
+  double* corr = g->corr;
+  if (!reuse) FS_TRY(dev_alloc((void**)&corr, sizeof(double) * Q.n_pad, g->device));
   dim3 gq((unsigned)(Q.PW / 64), (unsigned)(Q.n_pad / 64));
   int rc = FS_OK;
   if (g->x_is_f64)
@@ -4236,7 +4244,7 @@ static int row_guard(Plan* g) {
     set_error("row guard: device-to-host copy failed");
     rc = FS_EHIP;
   }
-  dev_free(corr);
+  if (!reuse) dev_free(corr);
   if (rc) return rc;
   double worst = 0.0;
   for (double c : h) worst = std::max(worst, std::fabs(c) / (double)(Q.n - 1));
@@ -4251,6 +4259,8 @@ static int row_guard(Plan* g) {
     g->calib[1] = g->cal32[0];
     g->calib[2] = g->cal32[1];
     g->calib[4] = Q.amb_delta / Q.amb_delta_model;
+  } else {
+    g->corr_ready = reuse;
   }
   if (trace_on()) {
     char msg[160];
@@ -4266,6 +4276,7 @@ static int row_guard(Plan* g) {
 // the plan is re-targeted to another feature subset (fs_plan_set_features).
 static int plan_layout(Plan* g) {
   Prepared& Q = g->P;
+  g->corr_ready = false;
   FS_HIP(hipStreamSynchronize(g->stream));
   if (g->side) FS_HIP(hipStreamSynchronize(g->side));
   for (void* q : g->owned_layout) dev_free(q);
@@ -4581,18 +4592,24 @@ static int run_quantize_dist(Plan* g) {
     }
     return FS_OK;
   }
-  if (g->x_is_f64)
+  const bool reuse = g->corr_ready && Q.algo == ALGO_MULTISURF;
+  g->corr_ready = false;  // later steps quantise again (the terms overwrote epsT)
+  if (reuse) {
+    // the row guard's operands and correction (row_guard): nothing to redo
+    FS_HIP(hipEventRecord(g->ev_join, g->stream));
+  } else if (g->x_is_f64) {
     k_quantize<double><<<gq, 256, 0, g->stream>>>(
         (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
         g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, g->c_lo, g->c_hi, g->xqT, g->xs,
         g->epsT);
-  else
+  } else {
     k_quantize<float><<<gq, 256, 0, g->stream>>>(
         (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
         g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, g->c_lo, g->c_hi, g->xqT, g->xs,
         g->epsT);
-  FS_TRY(launch_check("k_quantize"));
-  if (Q.algo == ALGO_MULTISURF) {
+  }
+  if (!reuse) FS_TRY(launch_check("k_quantize"));
+  if (Q.algo == ALGO_MULTISURF && !reuse) {
     // mean correction of this rank's feature share (summed across ranks
     // with the row moments), on the side stream beside k_dist: it reads
     // xqT as k_dist does and writes only epsT / corr, which k_dist leaves
