@@ -106,9 +106,9 @@ __device__ __forceinline__ long long cs_block_scan(long long v, long long* wsum,
   return pre + x - v;
 }
 
-// Level-1 bins of the key (its top 12 bits) and the packed bin counters
-// (count << 44 | sum of (eps_fx + 2^23): one 64-bit LDS add per sample).
-constexpr int kBins = 4096, kBinShift = 20;
+// Level-1 bins of the key (its top BB bits, colsort_bin_bits) and the
+// packed bin counters (count << 44 | sum of (eps_fx + 2^23): one 64-bit LDS
+// add per sample).
 constexpr int kHistShift = 44;
 constexpr int kMaxBinFill = 64;  // larger mixed bins: the column takes the full sort
 constexpr uint32_t kPureEmpty = 0x7FFFFFFFu, kMixed = 0x80000000u;
@@ -169,43 +169,49 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort_full(const uint32_t* __r
 }
 
 // One column per 1024-thread workgroup, n <= 1024 IPT.  Samples are binned
-// on the key's top 12 bits (4096 bins, counts and fixed-point eps sums by
-// 64-bit LDS adds, one scan): a sample's order against every other bin is
-// exact from the scanned bin counters.  Within its own bin it is ordered by
-// the key's low 20 bits against the bin's other samples (their packed
-// entries: low key bits and eps at 2^-12 of a quantum); equal keys are ties
-// (zero sign, whatever the order).  So the order is exact and only the eps
-// of a sample's bin neighbours is rounded (<= 2^-13 of a quantum each).
-// Typical data put a handful of samples in a bin (cfg4: ~17); a bin whose
+// on the key's top BB bits (colsort_bin_bits: 4096 or 8192 bins, counts and
+// fixed-point eps sums by 64-bit LDS adds, one scan): a sample's order
+// against every other bin is exact from the scanned bin counters.  Within
+// its own bin it is ordered by the key's low 32 - BB bits against the bin's
+// other samples (their packed entries: low key bits and eps at 2^-12 of a
+// quantum); equal keys are ties (zero sign, whatever the order).  So the
+// order is exact and only the eps of a sample's bin neighbours is rounded
+// (<= 2^-13 of a quantum each).  Typical data put a handful of samples in a
+// bin (cfg4: ~17 in 4096 bins, ~9 in the 8192 it uses); a bin whose
 // samples all share one key (integer levels, a value grid) needs no
 // within-bin work at any size; a column with a mixed bin holding more than
 // kMaxBinFill (one extreme value setting the range) is left to
 // k_colsort_full.
 //
 // Phases (barriers between): (1) keys, bin counters, per-bin purity;
-// (2) scan, bin cursors, bitmaps of bin starts and of positions that need
-// no within-bin work; (3) scatter of the mixed bins' entries in bin order;
-// (4) within-bin counts by POSITION: lane j of the sorted layout compares
-// its entry with its bin's entries -- the lanes of a wave cover 64
-// consecutive positions, i.e. one or a few neighbouring bins, so they loop
-// alike and read the same LDS words -- and leaves (l - g, sl - sg) packed
-// in its slot; (5) each sample's term from the bin counters and its slot.
-template <int IPT>
+// (2) scan, bitmaps of the bins that need no within-bin work, of bin starts
+// and of positions that need none; (3) every sample takes the next position
+// of its bin from the bin's own counter (the prefix's count field doubles as
+// the scatter cursor, so bin b's count ends at bin b + 1's start), the mixed
+// bins' entries are scattered in bin order; (4) within-bin counts by
+// POSITION: lane j of the sorted layout compares its entry with its bin's
+// entries -- the lanes of a wave cover 64 consecutive positions, i.e. one or
+// a few neighbouring bins, so they loop alike and read the same LDS words --
+// and leaves (l - g, sl - sg) packed in its slot; (5) each sample's term from
+// the bin counters and its slot.
+//
+// LDS (BB = 13, IPT = 20; cfg4): 64 KB counters + 80 KB entries + 6 KB
+// bitmaps; a separate cursor array (round 4's first layout) would not fit
+// beside 8192 bins.
+template <int IPT, int BB>
 struct ColbinSmem {
+  static constexpr int kBins = 1 << BB;
   unsigned long long hist[kBins];  // exclusive prefix after the scan
-  // after the scan: the scatter cursor of bin b | kSkip (pure or single)
-  uint32_t cur[kBins];
   // phase 1: seg[b] = bin b's first low key | kMixed once another arrives;
   // phases 3-4: the mixed bins' entries (low key << 12 | eps code) in bin
   // order at their sorted positions; phase 5: the packed within-bin counts
   alignas(16) uint32_t seg[(kCsThreads * IPT > kBins ? kCsThreads * IPT : kBins) + 4];
   uint32_t starts[(kCsThreads * IPT + 31) / 32];  // bit p: a non-empty bin starts at p
   uint32_t skip[(kCsThreads * IPT + 31) / 32];    // bit p: p's bin is pure or single
+  uint32_t binskip[kBins / 32];                   // bit b: bin b is pure, single or empty
   long long wsum[kCsThreads / 64];
   int max_fill;
 };
-
-constexpr uint32_t kSkip = 0x80000000u;
 
 // Hides a value's origin from the compiler, so that what a later phase
 // derives from it is computed there instead of being kept live (spilled)
@@ -220,13 +226,15 @@ __device__ __forceinline__ void cs_unpack(int32_t r, int& d, int& ds) {
   ds = r >> 8;
 }
 
-template <int IPT>
+template <int IPT, int BB>
 __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restrict__ xqT,
                                                         int64_t n, int64_t n_pad, int s, int q16,
                                                         int64_t c_lo, int* __restrict__ crowded,
                                                         float* __restrict__ epsT) {
-  __shared__ ColbinSmem<IPT> sm;
+  __shared__ ColbinSmem<IPT, BB> sm;
+  constexpr int kBins = 1 << BB, kBinShift = 32 - BB;
   constexpr int kWords = (kCsThreads * IPT + 31) / 32;
+  static_assert(sizeof(ColbinSmem<IPT, BB>) <= 160 * 1024, "k_colsort: LDS");
   const int tid = threadIdx.x;
   const int64_t c = c_lo + blockIdx.x;
   float* __restrict__ e = epsT + c * n_pad;
@@ -241,6 +249,7 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
     sm.starts[w] = 0u;
     sm.skip[w] = 0u;
   }
+  if (tid < kBins / 32) sm.binskip[tid] = 0u;
   if (tid == 0) sm.max_fill = 0;
   // every load of the column issued before any is used (one memory latency
   // per column): the operand word and the eps bits of samples tid + 1024 k
@@ -276,30 +285,34 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
     if (old != kPureEmpty && (old & ((1u << kBinShift) - 1u)) != kl) atomicOr(&sm.seg[b], kMixed);
   }
   __syncthreads();
-  // (2) exclusive scan of the packed counters, 4 bins per thread; the
-  // fullest mixed bin
+  // (2) exclusive scan of the packed counters, kPer (4 or 8) bins per
+  // thread; the fullest mixed bin
   constexpr int kPer = kBins / kCsThreads;
-  unsigned long long loc[kPer], run = 0;
+  unsigned long long run = 0;
   uint32_t skip_bits = 0;
   int fill = 0;
 #pragma unroll
   for (int q = 0; q < kPer; q++) {
     const unsigned long long v = sm.hist[tid * kPer + q];
     const bool mixed = (sm.seg[tid * kPer + q] & kMixed) != 0u;
-    loc[q] = run;
     run += v;
     if (mixed) fill = max(fill, (int)(v >> kHistShift));
     else skip_bits |= 1u << q;  // pure, single or empty
   }
   long long tot_packed;
   const unsigned long long pre = (unsigned long long)cs_block_scan((long long)run, sm.wsum, tot_packed);
+  // a thread's own bins: count read, exclusive prefix written in its place
+  // (the local prefix re-summed from the counters, not kept in registers
+  // across the scan: 8 bins' worth would spill beside the column's keys)
+  unsigned long long ex = pre;
 #pragma unroll
   for (int q = 0; q < kPer; q++) {
-    const unsigned long long ex = pre + loc[q];
+    const unsigned long long v = sm.hist[tid * kPer + q];
     const uint32_t lo = (uint32_t)(ex >> kHistShift);
-    const uint32_t m = (uint32_t)(sm.hist[tid * kPer + q] >> kHistShift);  // not yet overwritten
+    const uint32_t m = (uint32_t)(v >> kHistShift);
     const bool skip = ((skip_bits >> q) & 1u) != 0u;
-    sm.cur[tid * kPer + q] = lo | (skip ? kSkip : 0u);
+    sm.hist[tid * kPer + q] = ex;
+    ex += v;
     if (m != 0u) {
       atomicOr(&sm.starts[lo >> 5], 1u << (lo & 31));
       if (skip) {  // every position of the bin
@@ -313,9 +326,7 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
       }
     }
   }
-  __syncthreads();  // every bin's count read before any prefix is written
-#pragma unroll
-  for (int q = 0; q < kPer; q++) sm.hist[tid * kPer + q] = pre + loc[q];
+  atomicOr(&sm.binskip[(tid * kPer) >> 5], skip_bits << ((tid * kPer) & 31));
   atomicMax(&sm.max_fill, fill);
   __syncthreads();
   const bool crowd = sm.max_fill > kMaxBinFill;  // uniform
@@ -323,9 +334,11 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
   if (crowd) return;  // k_colsort_full writes this column's terms
   long long n_all, T;
   cs_decode((unsigned long long)tot_packed, n_all, T);
-  // (3) the mixed bins' entries at their sorted positions; from here on a
-  // sample keeps only its bin and position (0xFFFF: no within-bin work) in
-  // one register, its eps is read again in (5)
+  // (3) every sample counts itself into its bin's prefix (the count field
+  // is the bin's cursor: afterwards hist[b] counts start(b + 1)); the mixed
+  // bins' entries at their sorted positions.  From here on a sample keeps
+  // only its bin and position (0xFFFF: no within-bin work) in one register,
+  // its eps is read again in (5)
   int t3 = tid;
   FS_OPAQUE(t3);
 #pragma unroll
@@ -334,9 +347,12 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
     FS_OPAQUE(fx[k]);
     const uint32_t b = key[k] >> kBinShift;
     uint32_t pos = 0xFFFFu;
-    if (t3 + kCsThreads * k < nn && !(sm.cur[b] & kSkip)) {
-      pos = atomicAdd(&sm.cur[b], 1u);
-      sm.seg[pos] = ((key[k] & ((1u << kBinShift) - 1u)) << 12) | cs_eq12_of_fx(fx[k]);
+    if (t3 + kCsThreads * k < nn) {
+      const uint32_t at = (uint32_t)(atomicAdd(&sm.hist[b], 1ull << kHistShift) >> kHistShift);
+      if (!((sm.binskip[b >> 5] >> (b & 31)) & 1u)) {
+        pos = at;
+        sm.seg[pos] = ((key[k] & ((1u << kBinShift) - 1u)) << 12) | cs_eq12_of_fx(fx[k]);
+      }
     }
     key[k] = (b << 16) | pos;
     FS_OPAQUE(key[k]);  // packed here, not re-derived from b and pos later
@@ -401,11 +417,15 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
     if (i >= nn) continue;
     const int32_t f = cs_fx(__int_as_float(fx[k]));
     const int b = (int)(key[k] >> 16);
-    const unsigned long long lo = sm.hist[b];
-    const unsigned long long hi = b + 1 < kBins ? sm.hist[b + 1] : (unsigned long long)tot_packed;
-    long long c_below, e_below, c_to, e_to;
-    cs_decode(lo, c_below, e_below);
-    cs_decode(hi, c_to, e_to);
+    // after (3) hist[b] = (count start(b + 1), eps field of the bins below
+    // b), so a field's eps sum is decoded with the count at its own start
+    constexpr unsigned long long kLow = (1ull << kHistShift) - 1ull;
+    const unsigned long long here = sm.hist[b];
+    const unsigned long long above = b + 1 < kBins ? sm.hist[b + 1] : (unsigned long long)tot_packed;
+    const long long c_below = b ? (long long)(sm.hist[b - 1] >> kHistShift) : 0ll;
+    const long long c_to = (long long)(here >> kHistShift);
+    const long long e_below = (long long)(here & kLow) - (c_below << 23);
+    const long long e_to = (long long)(above & kLow) - (c_to << 23);
     // L - G and Eb - Ea over the other bins, then the within-bin part: an
     // eps code q is worth (2q + 1) 2^11 - 2^23 in 2^-24 units
     long long dLG = c_below - (nn - c_to), dE = e_below - (T - e_to);
@@ -495,6 +515,14 @@ size_t batch_bytes(int64_t n, int64_t nb) {
 
 }  // namespace
 
+int colsort_bin_bits(int64_t n) {
+  static const bool force12 = [] {
+    const char* e = std::getenv("FS_COLSORT_BINS12");
+    return e && *e == '1';
+  }();
+  return !force12 && n > 12 * (int64_t)kCsThreads && n <= 20 * (int64_t)kCsThreads ? 13 : 12;
+}
+
 // FS_COLSORT_GLOBAL=1 (tests): the large-n route at any n, so that it is
 // checked against the LDS route and the CPU backend on small inputs
 bool colsort_lds(int64_t n) {
@@ -534,26 +562,30 @@ int colsort_terms(const uint32_t* xqT, float* epsT, int64_t n, int64_t n_pad, in
       return -1;
     }
     const unsigned grid = (unsigned)nc;
-#define FS_COLSORT(IPT)                                                                          \
+#define FS_COLSORT(IPT, BB)                                                                      \
   do {                                                                                           \
-    k_colsort<IPT><<<grid, kCsThreads, 0, stream>>>(xqT, n, n_pad, key_shift, q16, c_lo, crowded, \
-                                                    epsT);                                       \
+    k_colsort<IPT, BB><<<grid, kCsThreads, 0, stream>>>(xqT, n, n_pad, key_shift, q16, c_lo,      \
+                                                        crowded, epsT);                          \
     k_colsort_full<IPT><<<grid, kCsThreads, 0, stream>>>(xqT, n, n_pad, key_shift, q16, c_lo,     \
                                                          crowded, epsT);                          \
   } while (0)
     // the smallest instantiated items-per-thread that covers n (cfg2,
-    // n = 5000: 5; cfg4, n = 20000: 20)
+    // n = 5000: 5; cfg4, n = 20000: 20) and colsort_bin_bits(n) (13 only
+    // for 16 and 20 items per thread)
     const int64_t ipt = (n + kCsThreads - 1) / kCsThreads;
-    if (ipt <= 2) FS_COLSORT(2);
-    else if (ipt <= 4) FS_COLSORT(4);
-    else if (ipt <= 5) FS_COLSORT(5);
-    else if (ipt <= 6) FS_COLSORT(6);
-    else if (ipt <= 8) FS_COLSORT(8);
-    else if (ipt <= 10) FS_COLSORT(10);
-    else if (ipt <= 12) FS_COLSORT(12);
-    else if (ipt <= 16) FS_COLSORT(16);
-    else if (ipt <= 20) FS_COLSORT(20);
-    else FS_COLSORT(24);
+    const bool b13 = colsort_bin_bits(n) == 13;
+    if (ipt <= 2) FS_COLSORT(2, 12);
+    else if (ipt <= 4) FS_COLSORT(4, 12);
+    else if (ipt <= 5) FS_COLSORT(5, 12);
+    else if (ipt <= 6) FS_COLSORT(6, 12);
+    else if (ipt <= 8) FS_COLSORT(8, 12);
+    else if (ipt <= 10) FS_COLSORT(10, 12);
+    else if (ipt <= 12) FS_COLSORT(12, 12);
+    else if (ipt <= 16 && b13) FS_COLSORT(16, 13);
+    else if (ipt <= 16) FS_COLSORT(16, 12);
+    else if (ipt <= 20 && b13) FS_COLSORT(20, 13);
+    else if (ipt <= 20) FS_COLSORT(20, 12);
+    else FS_COLSORT(24, 12);
 #undef FS_COLSORT
     if (hipGetLastError() != hipSuccess) {
       set_error("k_colsort: launch failed");

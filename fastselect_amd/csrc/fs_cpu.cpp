@@ -165,7 +165,7 @@ static void distances(const Prepared& P, const std::vector<uint32_t>& xq, int ra
 
 // Mean correction of k_colsort / k_rowcorr (fs_colsort.hip), the same
 // integer arithmetic: every continuous column is ordered by t (colsort_key).
-// Binned on the key's top 12 bits, a sample is ordered exactly against every
+// Binned on the key's top gpu::colsort_bin_bits(n) bits, a sample is ordered exactly against every
 // other bin by the bin counts and fixed-point eps sums, and within its own
 // bin against its neighbours' low key bits (their eps at 2^-12 of a quantum,
 // equal keys tied; a bin whose samples share one key needs nothing); a
@@ -185,21 +185,23 @@ static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
   // samples, beyond that (or under FS_COLSORT_GLOBAL) every column sorted
   // whole by the device segmented sort -- position terms, ties by index
   const bool binned = gpu::colsort_lds(n);
+  const int bins = 1 << gpu::colsort_bin_bits(n), shift = 32 - gpu::colsort_bin_bits(n);
+  const uint32_t low_mask = (1u << shift) - 1u;
   std::vector<float> term((size_t)n * std::max<int64_t>(P.pc, 1), 0.0f);
   parallel_for(c_hi - c_lo, n_jobs, [&](int64_t cc) {
     const int64_t c = c_lo + cc;
     constexpr double kFx = 16777216.0;  // eps fixed point 2^24, as k_colsort
     std::vector<uint32_t> key((size_t)n);
     std::vector<int64_t> fx((size_t)n);
-    std::vector<int64_t> cnt(kColsortBins + 1, 0), esum(kColsortBins + 1, 0);
+    std::vector<int64_t> cnt(bins + 1, 0), esum(bins + 1, 0);
     // per bin: first low key seen, and whether another one followed (mixed)
-    std::vector<uint32_t> first(kColsortBins, 0xFFFFFFFFu);
-    std::vector<char> mixed(kColsortBins, 0);
+    std::vector<uint32_t> first(bins, 0xFFFFFFFFu);
+    std::vector<char> mixed(bins, 0);
     int64_t T = 0;
     for (int64_t i = 0; i < n; i++) {
       fx[i] = colsort_fx(eps[(size_t)i * P.PW + c]);
       key[i] = colsort_key(xq[(size_t)i * P.PW + c], (int32_t)fx[i], s);
-      const uint32_t b = key[i] >> kColsortBinShift, kl = key[i] & ((1u << kColsortBinShift) - 1u);
+      const uint32_t b = key[i] >> shift, kl = key[i] & low_mask;
       cnt[b + 1]++;
       esum[b + 1] += fx[i];
       T += fx[i];
@@ -207,7 +209,7 @@ static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
       else if (first[b] != kl) mixed[b] = 1;
     }
     int64_t fill = 0;
-    for (int b = 0; b < kColsortBins; b++) {
+    for (int b = 0; b < bins; b++) {
       if (mixed[b]) fill = std::max(fill, cnt[b + 1]);
       cnt[b + 1] += cnt[b];     // exclusive prefix at b, inclusive at b + 1
       esum[b + 1] += esum[b];
@@ -227,16 +229,15 @@ static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
     // the samples of bins holding >= 2, in bin order (low key bits, eps code)
     std::vector<uint32_t> seg((size_t)n), cur(cnt.begin(), cnt.end() - 1);
     for (int64_t i = 0; i < n; i++) {
-      const uint32_t b = key[i] >> kColsortBinShift;
+      const uint32_t b = key[i] >> shift;
       if (cnt[b + 1] - cnt[b] < 2 || !mixed[b]) continue;
-      seg[cur[b]++] = ((key[i] & ((1u << kColsortBinShift) - 1u)) << 12) |
-                      colsort_eq12((int32_t)fx[i]);
+      seg[cur[b]++] = ((key[i] & low_mask) << 12) | colsort_eq12((int32_t)fx[i]);
     }
     for (int64_t i = 0; i < n; i++) {
-      const uint32_t b = key[i] >> kColsortBinShift;
+      const uint32_t b = key[i] >> shift;
       int64_t L = cnt[b], G = n - cnt[b + 1], Eb = esum[b], Ea = T - esum[b + 1];
       if (cnt[b + 1] - cnt[b] >= 2 && mixed[b]) {  // a pure bin's samples all tie
-        const uint32_t mine = key[i] & ((1u << kColsortBinShift) - 1u);
+        const uint32_t mine = key[i] & low_mask;
         for (int64_t j = cnt[b]; j < cnt[b + 1]; j++) {
           const uint32_t kl = seg[j] >> 12;
           const int64_t q = colsort_eq12_fx(seg[j] & 0xFFFu);

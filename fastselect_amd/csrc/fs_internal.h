@@ -146,13 +146,15 @@ inline uint32_t colsort_key(uint32_t q, int32_t fx, int s) {
   return (q << s) | (fr < m ? fr : m);
 }
 // The per-column order of the mean correction (fs_colsort.hip k_colsort,
-// fs_cpu.cpp mean_correction): samples binned on the key's top 12 bits; a
-// column whose fullest bin holds more than kColsortMaxFill samples is sorted
-// whole, else each sample is ordered within its bin against its neighbours'
-// low 20 key bits, with their eps at 2^-12 of a quantum: the eps code
-// colsort_eq12(fx) = (fx + 2^23) >> 12 clamped to [0, 4095], worth
-// colsort_eq12_fx(q) = (2q + 1) 2^11 - 2^23 in 2^-24 units.
-constexpr int kColsortBins = 4096, kColsortBinShift = 20, kColsortMaxFill = 64;
+// fs_cpu.cpp mean_correction): samples binned on the key's top
+// colsort_bin_bits(n) bits; a column whose fullest mixed bin holds more than
+// kColsortMaxFill samples is sorted whole, else each sample is ordered within
+// its bin against its neighbours' low 32 - bits key bits, with their eps at
+// 2^-12 of a quantum: the eps code colsort_eq12(fx) = (fx + 2^23) >> 12
+// clamped to [0, 4095], worth colsort_eq12_fx(q) = (2q + 1) 2^11 - 2^23 in
+// 2^-24 units.
+// The bin count is gpu::colsort_bin_bits(n).
+constexpr int kColsortMaxFill = 64;
 inline uint32_t colsort_eq12(int32_t fx) {
   const int32_t u = fx + (1 << 23);
   return (uint32_t)(u < 0 ? 0 : (u >= (1 << 24) ? 4095 : (u >> 12)));
@@ -415,6 +417,12 @@ int sort_pairs(void* list, int64_t count, void* scratch, size_t scratch_bytes, v
 // call needs colsort_scratch_bytes(n, c_hi - c_lo) bytes of device scratch.
 // `stream` is a hipStream_t.
 bool colsort_lds(int64_t n);
+// Bits of the key the LDS route bins on: 13 (8192 bins) where the
+// workgroup's LDS holds them next to the column's entries (12288 < n <=
+// 20480: half the within-bin work of 4096 bins at cfg4's n = 20000), 12
+// elsewhere; FS_COLSORT_BINS12=1 (timing A/B) keeps 12 everywhere.  Both
+// backends bin alike, so their terms stay identical.
+int colsort_bin_bits(int64_t n);
 size_t colsort_scratch_bytes(int64_t n, int64_t ncols);
 int colsort_terms(const uint32_t* xqT, float* epsT, int64_t n, int64_t n_pad, int64_t c_lo,
                   int64_t c_hi, int q16, int key_shift, void* scratch, size_t scratch_bytes,

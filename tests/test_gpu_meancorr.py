@@ -91,6 +91,11 @@ CORR_CASES = {
     "lognormal_3000x2000_crowded": lambda: lognormal(3000, 2000),
     "gaussian_3000x500_binned": lambda: gaussian(3000, 500),
     "grid_3000x300_pure_and_mixed_bins": lambda: _grid_columns(3000, 300),
+    # 12288 < n <= 20480: 8192 bins (colsort_bin_bits), the cursor in the
+    # bin counters; cfg4's route
+    "gaussian_13000x48_8192_bins": lambda: gaussian(13000, 48),
+    "grid_13000x32_8192_bins_pure_and_mixed": lambda: _grid_columns(13000, 32),
+    "lognormal_13000x32_8192_bins_crowded": lambda: lognormal(13000, 32),
 }
 
 

@@ -94,6 +94,21 @@ def test_row_means_exact(case):
     assert_means_exact(mu, ex, sc)
 
 
+@pytest.mark.parametrize("make", [lambda: gaussian(13000, 40), lambda: lognormal(13000, 8)],
+                         ids=["gaussian_13000x40", "lognormal_13000x8"])
+def test_row_means_exact_8192_bins(make):
+    """12288 < n <= 20480 bins the keys on 13 bits (colsort_bin_bits, the
+    GPU's LDS layout at cfg4's n): the CPU mirror stays exact there."""
+    X, y = make()
+    job, _, x, recip, isd = _job(X, y)
+    try:
+        mu = plan_row_means(job)
+        sc = job.plan.calibration()["SC"]
+    finally:
+        job.close()
+    assert_means_exact(mu, exact_row_means(x, recip, isd), sc)
+
+
 @pytest.mark.parametrize("case", sorted(CASES))
 def test_decisions_and_scores(case):
     X, y = CASES[case]()
