@@ -939,25 +939,28 @@ __global__ __launch_bounds__(1024) void k_unc_compact(const unsigned int* __rest
   if (t == 1023) *nrows = part[1023];
 }
 
-// Exact row moments of the flagged rows: grid (chunks of 16 samples j --
-// many workgroups even for one flagged row: the loop is latency-bound --,
-// groups of 8 flagged rows); the group's slots take rows[8 g + k] when the
-// count allows the fix (slots past the count repeat the group's last row and
-// are discarded).  A wave sums 4 samples at a time against the 8 rows: lane l
-// strides the features (k_exact_pairs' arithmetic per feature: float32
-// |a - b| * recip, a float64 sum), each of the 12 row values per feature is
-// read once for 32 pair-features, so X streams once per 8 flagged rows
-// rather than once per row; each pair's lane sums are then reduced across
-// the wave and D_ij, D_ij^2 added in j order (j != i).  The 4 waves'
-// partials go to parts[8 g + k][chunk] in a fixed order.
-constexpr int kExRows = 8, kExJ = 4;
+// Exact row moments of the flagged rows: grid (chunks of kExChunk = 4
+// samples j -- many workgroups even for one flagged row: the loop is
+// latency-bound --, groups of 8 flagged rows); the group's slots take
+// rows[8 g + k] when the count allows the fix (slots past the count repeat
+// the group's last row and are discarded).  The 4 waves split the features
+// (wave w, lane l: features w * 64 + l + 256 k), so each wave's chain of
+// dependent loads is p / 256 long, not p / 64 as when a wave walked every
+// feature of its own samples (cfg2: 0.39 ms for one flagged row).  Per
+// feature k_exact_pairs' arithmetic (float32 |a - b| * recip, a float64
+// sum); each of the 12 row values per feature is read once for 32
+// pair-features, so X streams once per 8 flagged rows.  Each pair's lane sums
+// are reduced across the wave, the 4 waves' sums added in a fixed order in
+// LDS, and D_ij, D_ij^2 summed in j order (j != i) into
+// parts[8 g + k][chunk].
+constexpr int kExRows = 8, kExJ = 4, kExChunk = kExJ;
 template <typename T>
 __global__ __launch_bounds__(256) void k_row_exact_parts(
     const T* __restrict__ x, int64_t n, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
     const int64_t* __restrict__ src_col, const double* __restrict__ scl,
     const int32_t* __restrict__ rows, const int32_t* __restrict__ nrows, int max_rows,
     double2* __restrict__ parts) {
-  __shared__ double2 wsum[4][kExRows];
+  __shared__ double wd[4][kExRows][kExJ];
   const int cnt = *nrows;
   const int g = blockIdx.y;
   if (cnt > max_rows || g * kExRows >= cnt) return;
@@ -966,74 +969,71 @@ __global__ __launch_bounds__(256) void k_row_exact_parts(
   int64_t ri[kExRows];
 #pragma unroll
   for (int k = 0; k < kExRows; k++) ri[k] = rows[g * kExRows + (k < nr ? k : nr - 1)];
-  double s1[kExRows], s2[kExRows];
+  const int64_t j0 = (int64_t)blockIdx.x * kExChunk;
+  int64_t jj[kExJ];
 #pragma unroll
-  for (int k = 0; k < kExRows; k++) s1[k] = s2[k] = 0.0;
-  const int64_t jw = (int64_t)blockIdx.x * 16 + wave * kExJ;
-  {
-    constexpr int jb = 0;
-    int64_t jj[kExJ];
+  for (int m = 0; m < kExJ; m++) jj[m] = j0 + m < n ? j0 + m : n - 1;
+  double acc[kExRows][kExJ];
 #pragma unroll
-    for (int m = 0; m < kExJ; m++) jj[m] = jw + jb + m < n ? jw + jb + m : n - 1;
-    double acc[kExRows][kExJ];
+  for (int k = 0; k < kExRows; k++)
 #pragma unroll
-    for (int k = 0; k < kExRows; k++)
-#pragma unroll
-      for (int m = 0; m < kExJ; m++) acc[k][m] = 0.0;
+    for (int m = 0; m < kExJ; m++) acc[k][m] = 0.0;
+  const int c0 = wave * 64 + lane;
 #pragma unroll 2
-    for (int64_t c = lane; c < pc; c += 64) {
-      const int64_t col = src_col[c];
-      T a[kExRows], b[kExJ];
+  for (int64_t c = c0; c < pc; c += 256) {
+    const int64_t col = src_col[c];
+    T a[kExRows], b[kExJ];
 #pragma unroll
-      for (int k = 0; k < kExRows; k++) a[k] = x[ri[k] * p_in + col];
+    for (int k = 0; k < kExRows; k++) a[k] = x[ri[k] * p_in + col];
 #pragma unroll
-      for (int m = 0; m < kExJ; m++) b[m] = x[jj[m] * p_in + col];
-      if (sizeof(T) == 4) {
-        const float r = (float)scl[c];
-#pragma unroll
-        for (int k = 0; k < kExRows; k++)
-#pragma unroll
-          for (int m = 0; m < kExJ; m++)
-            acc[k][m] += (double)(__builtin_fabsf((float)a[k] - (float)b[m]) * r);
-      } else {
-        const double r = scl[c];
-#pragma unroll
-        for (int k = 0; k < kExRows; k++)
-#pragma unroll
-          for (int m = 0; m < kExJ; m++)
-            acc[k][m] += __builtin_fabs((double)a[k] - (double)b[m]) * r;
-      }
-    }
-    for (int64_t c = PC + lane; c < PC + pd; c += 64) {
-      const int64_t col = src_col[c];
+    for (int m = 0; m < kExJ; m++) b[m] = x[jj[m] * p_in + col];
+    if (sizeof(T) == 4) {
+      const float r = (float)scl[c];
 #pragma unroll
       for (int k = 0; k < kExRows; k++)
 #pragma unroll
         for (int m = 0; m < kExJ; m++)
-          acc[k][m] += (x[ri[k] * p_in + col] != x[jj[m] * p_in + col]) ? 1.0 : 0.0;
+          acc[k][m] += (double)(__builtin_fabsf((float)a[k] - (float)b[m]) * r);
+    } else {
+      const double r = scl[c];
+#pragma unroll
+      for (int k = 0; k < kExRows; k++)
+#pragma unroll
+        for (int m = 0; m < kExJ; m++)
+          acc[k][m] += __builtin_fabs((double)a[k] - (double)b[m]) * r;
     }
+  }
+  for (int64_t c = PC + c0; c < PC + pd; c += 256) {
+    const int64_t col = src_col[c];
 #pragma unroll
     for (int k = 0; k < kExRows; k++)
 #pragma unroll
-      for (int m = 0; m < kExJ; m++) {
-        double v = acc[k][m];
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-        const int64_t j = jw + jb + m;
-        if (j < n && j != ri[k]) {
-          s1[k] += v;
-          s2[k] += v * v;
-        }
-      }
+      for (int m = 0; m < kExJ; m++)
+        acc[k][m] += (x[ri[k] * p_in + col] != x[jj[m] * p_in + col]) ? 1.0 : 0.0;
   }
-  if (lane == 0)
 #pragma unroll
-    for (int k = 0; k < kExRows; k++) wsum[wave][k] = make_double2(s1[k], s2[k]);
+  for (int k = 0; k < kExRows; k++)
+#pragma unroll
+    for (int m = 0; m < kExJ; m++) {
+      double v = acc[k][m];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) wd[wave][k][m] = v;
+    }
   __syncthreads();
   if (threadIdx.x < nr) {
     const int k = threadIdx.x;
-    parts[(int64_t)(g * kExRows + k) * gridDim.x + blockIdx.x] =
-        make_double2((wsum[0][k].x + wsum[1][k].x) + (wsum[2][k].x + wsum[3][k].x),
-                     (wsum[0][k].y + wsum[1][k].y) + (wsum[2][k].y + wsum[3][k].y));
+    const int64_t i = rows[g * kExRows + k];
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int m = 0; m < kExJ; m++) {
+      const double d = (wd[0][k][m] + wd[1][k][m]) + (wd[2][k][m] + wd[3][k][m]);
+      const int64_t j = j0 + m;
+      if (j < n && j != i) {
+        s1 += d;
+        s2 += d * d;
+      }
+    }
+    parts[(int64_t)(g * kExRows + k) * gridDim.x + blockIdx.x] = make_double2(s1, s2);
   }
 }
 
@@ -4536,7 +4536,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     // of exact_thresholds checked on all rows against the oracle's)
     g->thr_all = std::getenv("FS_THR_EXACT_ALL") != nullptr;
     g->thr_rows = (int)(g->thr_all ? Q.n : exact_thr_rows(Q.n, Q.pc + Q.pd));
-    const int64_t nchunk = (Q.n + 15) / 16;
+    const int64_t nchunk = (Q.n + kExChunk - 1) / kExChunk;
     if ((rc = dalloc(g, &g->unc, Q.n_pad)) || (rc = dalloc(g, &g->urows, Q.n_pad + 1)) ||
         (rc = dalloc(g, &g->uparts, (size_t)g->thr_rows * nchunk)))
       return fail(rc);
@@ -4734,7 +4734,7 @@ static int refine_pairs(Plan* g, int algo, double delta, double thr_tol = 0.0,
 // reported by fs_plan_info-style diagnostics: g->n_exact_thr).
 static int exact_thresholds(Plan* g) {
   const Prepared& Q = g->P;
-  const int64_t nchunk = (Q.n + 15) / 16;
+  const int64_t nchunk = (Q.n + kExChunk - 1) / kExChunk;
   const unsigned ngroups = (unsigned)((g->thr_rows + kExRows - 1) / kExRows);
   if (g->thr_all) {  // test hook: flag every row
     std::vector<int32_t> all((size_t)Q.n + 1);
