@@ -1131,17 +1131,11 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
 
 // k_exact_pairs for the common layout -- every kept feature continuous, in
 // input order (src_col = identity), float32 X with a 16-byte row pitch --
-// reading the rows as float4 (16 B per lane, 4 KB per wave per row and step)
-// instead of a column-indexed dword gather.  Same arithmetic per feature: f32
-// |a - b| * f32 recip, summed in f64 by each lane in feature order, then
-// across the wave.  The list is sorted by (i, j), so a window of kEpGroup
-// consecutive pairs usually shares row i (cfg4: ~11 refined pairs per row):
-// a wave takes one window, and when its pairs share i it reads row i and the
-// reciprocals once for all of them (2 + kEpGroup row reads per step instead
-// of 3 kEpGroup -- the loop is bound by those reads, not by its arithmetic);
-// a mixed window takes its pairs one at a time.  Either way each pair's sum
-// is formed in the same order, so the distances are bit-identical.
-constexpr int kEpGroup = 4;
+// reading both rows as float4 (16 B per lane, 4 KB per wave per row and
+// step, 8 loads in flight per lane) instead of a column-indexed dword
+// gather.  Same arithmetic per feature: f32 |a - b| * f32 recip, summed in
+// f64.  The list is sorted by (i, j), so consecutive waves share row i
+// through L2; row j is the HBM read.
 __global__ __launch_bounds__(256) void k_exact_pairs_rows(
     const float* __restrict__ x, int64_t p, const float* __restrict__ scl32, double sc,
     const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
@@ -1153,80 +1147,34 @@ __global__ __launch_bounds__(256) void k_exact_pairs_rows(
   const int64_t total = (int64_t)*count < cap ? (int64_t)*count : cap;
   const int64_t p4 = p / 4;
   const float4* __restrict__ s4 = (const float4*)scl32;
-  const float4 zero = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-  auto finish = [&](int2 pr, double acc) {
+  for (int64_t k = wave; k < total; k += nw) {
+    const int2 pr = list[k];
+    const float4* __restrict__ xi = (const float4*)(x + (int64_t)pr.x * p);
+    const float4* __restrict__ xj = (const float4*)(x + (int64_t)pr.y * p);
+    double acc = 0.0;
+    constexpr int kU = 4;
+    for (int64_t c0 = lane; c0 < p4; c0 += 64 * kU) {
+      float4 a[kU], b[kU], w[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const int64_t c = c0 + 64 * u;
+        const bool in = c < p4;
+        a[u] = in ? xi[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        b[u] = in ? xj[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        w[u] = in ? s4[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        acc += (double)(__builtin_fabsf(a[u].x - b[u].x) * w[u].x);
+        acc += (double)(__builtin_fabsf(a[u].y - b[u].y) * w[u].y);
+        acc += (double)(__builtin_fabsf(a[u].z - b[u].z) * w[u].z);
+        acc += (double)(__builtin_fabsf(a[u].w - b[u].w) * w[u].w);
+      }
+    }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (lane == 0) {
       store_pair(D, n_pad, tw, win, pr, acc * sc);
       if (unc != nullptr) mark_uncertain(pr, acc * sc, thr, thr_tol, unc);
-    }
-  };
-  for (int64_t k0 = wave * kEpGroup; k0 < total; k0 += nw * kEpGroup) {
-    const int m = total - k0 < kEpGroup ? (int)(total - k0) : kEpGroup;
-    int2 pr[kEpGroup];
-#pragma unroll
-    for (int u = 0; u < kEpGroup; u++) pr[u] = list[k0 + (u < m ? u : m - 1)];
-    bool shared = m == kEpGroup;
-#pragma unroll
-    for (int u = 1; u < kEpGroup; u++) shared = shared && pr[u].x == pr[0].x;
-    if (shared) {
-      const float4* __restrict__ xi = (const float4*)(x + (int64_t)pr[0].x * p);
-      const float4* __restrict__ xj[kEpGroup];
-#pragma unroll
-      for (int u = 0; u < kEpGroup; u++) xj[u] = (const float4*)(x + (int64_t)pr[u].y * p);
-      double acc[kEpGroup];
-#pragma unroll
-      for (int u = 0; u < kEpGroup; u++) acc[u] = 0.0;
-      constexpr int kU = 2;
-      for (int64_t c0 = lane; c0 < p4; c0 += 64 * kU) {
-        float4 a[kU], w[kU], b[kEpGroup][kU];
-#pragma unroll
-        for (int v = 0; v < kU; v++) {
-          const int64_t c = c0 + 64 * v;
-          const bool in = c < p4;
-          a[v] = in ? xi[c] : zero;
-          w[v] = in ? s4[c] : zero;
-#pragma unroll
-          for (int u = 0; u < kEpGroup; u++) b[u][v] = in ? xj[u][c] : zero;
-        }
-#pragma unroll
-        for (int v = 0; v < kU; v++)
-#pragma unroll
-          for (int u = 0; u < kEpGroup; u++) {
-            acc[u] += (double)(__builtin_fabsf(a[v].x - b[u][v].x) * w[v].x);
-            acc[u] += (double)(__builtin_fabsf(a[v].y - b[u][v].y) * w[v].y);
-            acc[u] += (double)(__builtin_fabsf(a[v].z - b[u][v].z) * w[v].z);
-            acc[u] += (double)(__builtin_fabsf(a[v].w - b[u][v].w) * w[v].w);
-          }
-      }
-#pragma unroll
-      for (int u = 0; u < kEpGroup; u++) finish(pr[u], acc[u]);
-      continue;
-    }
-    for (int u = 0; u < m; u++) {
-      const float4* __restrict__ xi = (const float4*)(x + (int64_t)pr[u].x * p);
-      const float4* __restrict__ xj = (const float4*)(x + (int64_t)pr[u].y * p);
-      double acc = 0.0;
-      constexpr int kU = 4;
-      for (int64_t c0 = lane; c0 < p4; c0 += 64 * kU) {
-        float4 a[kU], b[kU], w[kU];
-#pragma unroll
-        for (int v = 0; v < kU; v++) {
-          const int64_t c = c0 + 64 * v;
-          const bool in = c < p4;
-          a[v] = in ? xi[c] : zero;
-          b[v] = in ? xj[c] : zero;
-          w[v] = in ? s4[c] : zero;
-        }
-#pragma unroll
-        for (int v = 0; v < kU; v++) {
-          acc += (double)(__builtin_fabsf(a[v].x - b[v].x) * w[v].x);
-          acc += (double)(__builtin_fabsf(a[v].y - b[v].y) * w[v].y);
-          acc += (double)(__builtin_fabsf(a[v].z - b[v].z) * w[v].z);
-          acc += (double)(__builtin_fabsf(a[v].w - b[v].w) * w[v].w);
-        }
-      }
-      finish(pr[u], acc);
     }
   }
 }
@@ -4760,10 +4708,8 @@ static int refine_pairs(Plan* g, int algo, double delta, double thr_tol = 0.0,
   if (g->n_refined == 0) return FS_OK;
   FS_TRY(sort_pair_list(g, g->n_refined));
   const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
-  if (g->rows_direct && !std::getenv("FS_EXACT_GATHER"))  // a window of kEpGroup pairs per wave
-    k_exact_pairs_rows<<<(unsigned)std::min<int64_t>((g->n_refined + 4 * kEpGroup - 1) /
-                                                         (4 * kEpGroup), 8192),
-                         256, 0, g->stream>>>((const float*)g->x, Q.p_in, g->scl32, Q.SC,
+  if (g->rows_direct && !std::getenv("FS_EXACT_GATHER"))
+    k_exact_pairs_rows<<<grid, 256, 0, g->stream>>>((const float*)g->x, Q.p_in, g->scl32, Q.SC,
                                                     g->list, g->list_count, g->list_cap, Q.n_pad,
                                                     g->tw, g->win, g->D, g->thr, thr_tol, unc);
   else if (g->x_is_f64)
