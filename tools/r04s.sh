@@ -21,3 +21,12 @@ for v in 13 12; do
     -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-q32 --no-fit \
     > "$GRAFT_REPO_ROOT/$out/prof$v.log" 2>&1 || exit $?
 done
+cd "$GRAFT_REPO_ROOT" || exit 1
+unset FS_COLSORT_BINS12
+timeout -k 10 300 python3 -u bench.py --config cfg2 --steps 20 --warmup 3 --no-fit \
+  > "$out/cfg2_bench.json" 2> "$out/cfg2_bench.err" || exit $?
+python3 -c "import json; d=json.load(open('$out/cfg2_bench.json')); print('cfg2', d['ms_per_step'], d['roofline']['kernel_ms'])"
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$GRAFT_REPO_ROOT/$out/cfg2_prof" -o run \
+  -- python3 "$GRAFT_REPO_ROOT/bench.py" --config cfg2 --steps 10 --warmup 2 --no-cpu-baseline --no-fit \
+  > "$GRAFT_REPO_ROOT/$out/cfg2_prof.log" 2>&1 || exit $?
