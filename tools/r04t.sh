@@ -20,3 +20,7 @@ for r in csv.DictReader(open('$GRAFT_REPO_ROOT/$out/cs$v/run_kernel_stats.csv'))
 " | tee -a "$GRAFT_REPO_ROOT/$out/cs_ab.txt"
 done
 cp "$GRAFT_REPO_ROOT/$out/.product.so" "$GRAFT_REPO_ROOT/$lib"
+cd "$GRAFT_REPO_ROOT" || exit 1
+unset FS_COLSORT_BINS12
+# cfg2: is the mean correction on the step's critical path (beside k_dist)?
+bash tools/variant_ab.sh r04t_cfg2 2 default mcmain nomc -- --config cfg2
