@@ -23,4 +23,4 @@ cp "$GRAFT_REPO_ROOT/$out/.product.so" "$GRAFT_REPO_ROOT/$lib"
 cd "$GRAFT_REPO_ROOT" || exit 1
 unset FS_COLSORT_BINS12
 # cfg2: is the mean correction on the step's critical path (beside k_dist)?
-bash tools/variant_ab.sh r04t_cfg2 2 default mcmain nomc -- --config cfg2
+bash tools/variant_ab.sh r04t_cfg2 2 default mcmain nomc sideprio -- --config cfg2 && bash tools/variant_ab.sh r04t_cfg4 2 default sideprio
