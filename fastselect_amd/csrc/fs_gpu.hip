@@ -4504,15 +4504,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   };
   for (auto& e : g->ev)
     if (hipEventCreate(&e) != hipSuccess) return fail(FS_EHIP);
-#if defined(FS_SIDE_PRIO)
-  // A/B: the side stream (mean correction) at the device's greatest priority,
-  // so that its workgroups are dispatched ahead of k_dist's
-  int prio_lo = 0, prio_hi = 0;
-  if (hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi) != hipSuccess) return fail(FS_EHIP);
-  if (hipStreamCreateWithPriority(&g->side, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-#else
   if (hipStreamCreateWithFlags(&g->side, hipStreamNonBlocking) != hipSuccess ||
-#endif
       hipEventCreateWithFlags(&g->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&g->ev_join, hipEventDisableTiming) != hipSuccess)
     return fail(FS_EHIP);
