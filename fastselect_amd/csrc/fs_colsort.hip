@@ -305,7 +305,7 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
   // (the local prefix re-summed from the counters, not kept in registers
   // across the scan: 8 bins' worth would spill beside the column's keys)
   unsigned long long ex = pre;
-#pragma unroll
+#pragma unroll 1
   for (int q = 0; q < kPer; q++) {
     const unsigned long long v = sm.hist[tid * kPer + q];
     const uint32_t lo = (uint32_t)(ex >> kHistShift);
