@@ -222,26 +222,55 @@ __global__ __launch_bounds__(256) void k_quantize(
 // in column c, in integer units.
 
 // corr[i] = sum over continuous columns [c_lo, c_hi) (this rank's share) of
-// the per-feature bias terms.
-// Workgroup = 64 rows x 16 waves; wave w sums columns w, w+16, ... (one
-// coalesced 256-byte read per column), then the 16 partials are added in a
-// fixed order (deterministic).
-__global__ __launch_bounds__(1024) void k_rowcorr(const float* __restrict__ epsT, int64_t n,
-                                                  int64_t n_pad, int64_t c_lo, int64_t c_hi,
-                                                  double* __restrict__ corr) {
-  __shared__ double part[16][64];
+// the per-feature bias terms, in two launches.  k_rowcorr: grid (row blocks
+// of 64, column slices); workgroup = 64 rows x 16 waves, wave w sums the
+// slice's columns w, w + 16, ... (one coalesced 256-byte read per column, two
+// independent chains), the 16 partials are added in a fixed order into
+// part[slice][i].  The slices fill the chip when there are few row blocks
+// (cfg2: 79 row blocks alone left two thirds of the CUs idle, 0.14 ms;
+// rowcorr_slices).  k_rowcorr_sum adds the slices in order (deterministic).
+constexpr int kRowcorrMaxSlices = 16;
+__global__ __launch_bounds__(1024) void k_rowcorr(const float* __restrict__ epsT, int64_t n_pad,
+                                                  int64_t c_lo, int64_t c_hi,
+                                                  double* __restrict__ part) {
+  __shared__ double wp[16][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t i = (int64_t)blockIdx.x * 64 + lane;  // < n_pad
-  double s = 0.0;
-  for (int64_t c = c_lo + wave; c < c_hi; c += 16) s += (double)epsT[c * n_pad + i];
-  part[wave][lane] = s;
+  const int64_t nc = c_hi - c_lo, ns = gridDim.y;
+  const int64_t a = c_lo + nc * blockIdx.y / ns, b = c_lo + nc * (blockIdx.y + 1) / ns;
+  double s0 = 0.0, s1 = 0.0;
+  int64_t c = a + wave;
+  for (; c + 16 < b; c += 32) {
+    s0 += (double)epsT[c * n_pad + i];
+    s1 += (double)epsT[(c + 16) * n_pad + i];
+  }
+  if (c < b) s0 += (double)epsT[c * n_pad + i];
+  wp[wave][lane] = s0 + s1;
   __syncthreads();
-  if (wave == 0 && i < n) {
+  if (wave == 0) {
     double t = 0.0;
 #pragma unroll
-    for (int w = 0; w < 16; w++) t += part[w][lane];
-    corr[i] = t;
+    for (int w = 0; w < 16; w++) t += wp[w][lane];
+    part[(int64_t)blockIdx.y * n_pad + i] = t;
   }
+}
+
+__global__ __launch_bounds__(256) void k_rowcorr_sum(const double* __restrict__ part, int slices,
+                                                     int64_t n, int64_t n_pad,
+                                                     double* __restrict__ corr) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double t = 0.0;
+  for (int sl = 0; sl < slices; sl++) t += part[(int64_t)sl * n_pad + i];
+  corr[i] = t;
+}
+
+// column slices of k_rowcorr: about 1024 workgroups, at least 64 columns each
+static int rowcorr_slices(int64_t n_pad, int64_t ncols) {
+  const int64_t rb = std::max<int64_t>(1, n_pad / 64);
+  int64_t sl = (1024 + rb - 1) / rb;
+  sl = std::min<int64_t>(sl, std::max<int64_t>(1, ncols / 64));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(sl, kRowcorrMaxSlices));
 }
 
 // ---------------------------------------------------------------------------
@@ -3317,6 +3346,7 @@ struct Plan {
   float* xs = nullptr;
   float* epsT = nullptr;
   double* corr = nullptr;
+  double* corr_part = nullptr;  // [rowcorr_slices][n_pad] k_rowcorr slice partials
   double* xT64 = nullptr;      // SURF: float64 feature-major operands
   double* D = nullptr;
   int tiled = 0;                // D in the tiled layout (MultiSURF; d_at)
@@ -4164,6 +4194,18 @@ static int shard_segments(Plan* g) {
 
 // Mean-correction terms of the continuous columns [c_lo, c_hi) on stream s
 // (fs_colsort.hip); the large-n route's scratch is kept with the plan.
+// out[i] = the mean correction of row i over columns [c_lo, c_hi) from the
+// terms in epsT (k_rowcorr over column slices, then their fixed-order sum).
+static int run_rowcorr(Plan* g, int64_t c_lo, int64_t c_hi, double* out, hipStream_t st) {
+  const Prepared& Q = g->P;
+  const int sl = rowcorr_slices(Q.n_pad, c_hi - c_lo);
+  k_rowcorr<<<dim3((unsigned)(Q.n_pad / 64), (unsigned)sl), 1024, 0, st>>>(g->epsT, Q.n_pad, c_lo,
+                                                                          c_hi, g->corr_part);
+  FS_TRY(launch_check("k_rowcorr"));
+  k_rowcorr_sum<<<(unsigned)((Q.n + 255) / 256), 256, 0, st>>>(g->corr_part, sl, Q.n, Q.n_pad, out);
+  return launch_check("k_rowcorr_sum");
+}
+
 static int run_colsort(Plan* g, int64_t c_lo, int64_t c_hi, hipStream_t s) {
   const Prepared& Q = g->P;
   if (c_hi <= c_lo) return FS_OK;
@@ -4232,9 +4274,7 @@ static int row_guard(Plan* g) {
     rc = run_colsort(g, 0, Q.pc, g->stream);
   }
   if (!rc) {
-    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, g->stream>>>(g->epsT, Q.n, Q.n_pad, 0, Q.pc,
-                                                                corr);
-    rc = launch_check("k_rowcorr (row guard)");
+    rc = run_rowcorr(g, 0, Q.pc, corr, g->stream);
   }
   std::vector<double> h((size_t)Q.n);
   if (!rc && (hipMemcpyAsync(h.data(), corr, sizeof(double) * Q.n, hipMemcpyDeviceToHost,
@@ -4528,7 +4568,9 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   int rc;
   trace_mark("plan: host setup");
   if ((rc = dalloc(g, (char**)&g->x, xbytes)) || (rc = dalloc(g, &g->lab, Q.n_pad)) ||
-      (rc = dalloc(g, &g->corr, Q.n_pad)) || (rc = dalloc(g, &g->thr, Q.n_pad)) ||
+      (rc = dalloc(g, &g->corr, Q.n_pad)) ||
+      (rc = dalloc(g, &g->corr_part, (int64_t)kRowcorrMaxSlices * Q.n_pad)) ||
+      (rc = dalloc(g, &g->thr, Q.n_pad)) ||
       (rc = dalloc(g, &g->list, g->list_cap)) || (rc = dalloc(g, &g->list_count, 1)))
     return fail(rc);
   if (Q.algo == ALGO_MULTISURF) {
@@ -4628,17 +4670,13 @@ static int run_quantize_dist(Plan* g) {
 #elif defined(FS_MC_MAIN)
     // A/B timing only: the mean correction on the main stream, before k_dist
     FS_TRY(run_colsort(g, g->c_lo, g->c_hi, g->stream));
-    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, g->stream>>>(g->epsT, Q.n, Q.n_pad, g->c_lo,
-                                                                 g->c_hi, g->corr);
-    FS_TRY(launch_check("k_rowcorr"));
+    FS_TRY(run_rowcorr(g, g->c_lo, g->c_hi, g->corr, g->stream));
     FS_HIP(hipEventRecord(g->ev_join, g->stream));
 #else
     FS_HIP(hipEventRecord(g->ev_fork, g->stream));
     FS_HIP(hipStreamWaitEvent(g->side, g->ev_fork, 0));
     FS_TRY(run_colsort(g, g->c_lo, g->c_hi, g->side));
-    k_rowcorr<<<(unsigned)(Q.n_pad / 64), 1024, 0, g->side>>>(g->epsT, Q.n, Q.n_pad, g->c_lo,
-                                                               g->c_hi, g->corr);
-    FS_TRY(launch_check("k_rowcorr"));
+    FS_TRY(run_rowcorr(g, g->c_lo, g->c_hi, g->corr, g->side));
     FS_HIP(hipEventRecord(g->ev_join, g->side));
 #endif
   }
