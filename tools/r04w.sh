@@ -17,3 +17,6 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$GRAFT_REPO_ROOT/$out/cfg2_prof" -o run \
   -- python3 "$GRAFT_REPO_ROOT/bench.py" --config cfg2 --steps 10 --warmup 2 --no-cpu-baseline --no-fit \
   > "$GRAFT_REPO_ROOT/$out/cfg2_prof.log" 2>&1 || exit $?
+cd "$GRAFT_REPO_ROOT" || exit 1
+# A/B: short-column k_colsort at two workgroups per CU (<= 64 VGPRs)
+bash tools/variant_ab.sh r04w_cswpe8 2 default cswpe8 -- --config cfg2
