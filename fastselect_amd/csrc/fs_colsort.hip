@@ -226,14 +226,8 @@ __device__ __forceinline__ void cs_unpack(int32_t r, int& d, int& ds) {
   ds = r >> 8;
 }
 
-#if defined(FS_CS_WPE8)
-// A/B only: two workgroups per CU for short columns (<= 64 VGPRs, spills)
-#define FS_CS_WPE(IPT) __attribute__((amdgpu_waves_per_eu((IPT) <= 8 ? 8 : 4)))
-#else
-#define FS_CS_WPE(IPT)
-#endif
 template <int IPT, int BB>
-__global__ __launch_bounds__(kCsThreads) FS_CS_WPE(IPT) void k_colsort(const uint32_t* __restrict__ xqT,
+__global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restrict__ xqT,
                                                         int64_t n, int64_t n_pad, int s, int q16,
                                                         int64_t c_lo, int* __restrict__ crowded,
                                                         float* __restrict__ epsT) {
