@@ -96,6 +96,11 @@ CORR_CASES = {
     "gaussian_13000x48_8192_bins": lambda: gaussian(13000, 48),
     "grid_13000x32_8192_bins_pure_and_mixed": lambda: _grid_columns(13000, 32),
     "lognormal_13000x32_8192_bins_crowded": lambda: lognormal(13000, 32),
+    # the edges of colsort_bin_bits / the instantiated items per thread:
+    # 12289 (16 per thread, 8192 bins), 20480 (20, 8192), 20481 (24, 4096)
+    "gaussian_12289x32_edge": lambda: gaussian(12289, 32),
+    "gaussian_20480x32_edge": lambda: gaussian(20480, 32),
+    "grid_20481x16_edge": lambda: _grid_columns(20481, 16),
 }
 
 

@@ -94,8 +94,9 @@ def test_row_means_exact(case):
     assert_means_exact(mu, ex, sc)
 
 
-@pytest.mark.parametrize("make", [lambda: gaussian(13000, 40), lambda: lognormal(13000, 8)],
-                         ids=["gaussian_13000x40", "lognormal_13000x8"])
+@pytest.mark.parametrize("make", [lambda: gaussian(13000, 40), lambda: lognormal(13000, 8),
+                                  lambda: lognormal(12289, 4, seed=3)],
+                         ids=["gaussian_13000x40", "lognormal_13000x8", "lognormal_12289x4_edge"])
 def test_row_means_exact_8192_bins(make):
     """12288 < n <= 20480 bins the keys on 13 bits (colsort_bin_bits, the
     GPU's LDS layout at cfg4's n): the CPU mirror stays exact there."""
