@@ -46,6 +46,17 @@ class MultiSURF(TransformerMixin, BaseEstimator):
         'all': every visible device the job has work for (one per 4096
         samples).  Not a reference parameter (the reference is
         single-device); ignored by backend='cpu'.
+    accumulation : {'fast', 'reference'}, default='fast'
+        'reference' replays the reference's float32 arithmetic: each focal
+        sample's near-hit / near-miss diffs summed in float32 in sample
+        order, then each feature's float32 sequential column sum
+        (MultiSURF.py:198-253), on 32-bit pass-1 operands with exact
+        thresholds -- the reference's scores bit for bit, at roughly the
+        cost of a second pass 2 (DESIGN.md §Reference-order accumulation).
+        'fast' (the default) sums each pair once in float32 streams and
+        float64 partials: closer to the exact sums than the reference's own
+        float32 sums, not equal to them.  Not a reference parameter;
+        'reference' runs on one device.
     """
 
     def __init__(
@@ -57,6 +68,7 @@ class MultiSURF(TransformerMixin, BaseEstimator):
         n_jobs: int = -1,
         verbose: bool = False,
         devices=None,
+        accumulation: str = "fast",
     ):
         self.n_features_to_select = n_features_to_select
         self.backend = backend
@@ -65,8 +77,10 @@ class MultiSURF(TransformerMixin, BaseEstimator):
         self.n_jobs = n_jobs
         self.verbose = verbose
         self.devices = devices
+        self.accumulation = accumulation
 
     def _validate_parameters(self, n_samples, n_features):
+        _lib.accumulation_code(self.accumulation)
         return _base.resolve_n_select("MultiSURF", self.backend, self.n_features_to_select,
                                       n_samples, n_features)
 
@@ -81,6 +95,7 @@ class MultiSURF(TransformerMixin, BaseEstimator):
             n_select = self._validate_parameters(n_samples, self.n_features_in_)
             self.effective_backend_ = _base.effective_backend(self.backend)
             self.devices_ = _base.fit_devices(self.devices, self.effective_backend_, n_samples)
+            _base.check_accumulation_devices(self.accumulation, self.devices_)
             x = np.ascontiguousarray(x)
             # one upload of X for the whole fit (already done when staged);
             # a multi-device fit uploads X per device
@@ -106,9 +121,10 @@ class MultiSURF(TransformerMixin, BaseEstimator):
             name = "MultiSURF*" if self.use_star else "MultiSURF"
             where = "GPU" if self.effective_backend_ == "gpu" else "CPU"
             print(f"Running {name} on the {where} now...")
-        return _lib.multisurf_score(self.effective_backend_, x, y, recip_full,
-                                    all_feature_indices, self.use_star, is_discrete,
-                                    self.n_jobs, devices=self.devices_)
+        with _lib.accumulation(self.accumulation):
+            return _lib.multisurf_score(self.effective_backend_, x, y, recip_full,
+                                        all_feature_indices, self.use_star, is_discrete,
+                                        self.n_jobs, devices=self.devices_)
 
     def _resident_scorer(self, x, y):
         """A scorer for TuRF that keeps X resident (on the GPU for the GPU
@@ -135,6 +151,7 @@ class _ResidentMultiSURF:
 
     def __init__(self, est: MultiSURF, x, y):
         self.est = est
+        _lib.accumulation_code(est.accumulation)
         x, y = _base.validate_xy(est, x, y, np.float32, est.n_jobs,
                                  pinned=_base.stage_device(est.backend) is not None)
         est.effective_backend_ = _base.effective_backend(est.backend)
@@ -146,7 +163,8 @@ class _ResidentMultiSURF:
         recip = (1.0 / ranges).astype(np.float32)
         from .parallel import ShardedMultiSURF
         self.job = ShardedMultiSURF(x, y, recip, self.is_discrete, use_star=est.use_star,
-                                    backend=est.effective_backend_, shard=False)
+                                    backend=est.effective_backend_, shard=False,
+                                    accumulation=est.accumulation)
         self.active = None
 
     def refit(self, active: np.ndarray):

@@ -57,6 +57,13 @@ class ReliefF(TransformerMixin, BaseEstimator):
         the host).  None: device 0, as the reference; 'all': every visible
         device the job has work for (one per 4096 samples).  Not a reference
         parameter; ignored by backend='cpu'.
+    accumulation : {'fast', 'reference'}, default='fast'
+        'reference': each sample's neighbours in the reference's argsort
+        order, its float64 update rounded to a float32 row, and each
+        feature's float32 sequential column sum (ReliefF.py:181-220) -- the
+        reference's scores bit for bit.  'fast': the update summed in
+        float64 throughout.  Not a reference parameter; 'reference' runs on
+        one device.
     """
 
     def __init__(
@@ -68,6 +75,7 @@ class ReliefF(TransformerMixin, BaseEstimator):
         verbose: bool = False,
         n_jobs: int = -1,
         devices=None,
+        accumulation: str = "fast",
     ):
         self.n_features_to_select = n_features_to_select
         self.discrete_limit = discrete_limit
@@ -76,8 +84,10 @@ class ReliefF(TransformerMixin, BaseEstimator):
         self.verbose = verbose
         self.n_jobs = n_jobs
         self.devices = devices
+        self.accumulation = accumulation
 
     def _validate_parameters(self, n_samples, n_features):
+        _lib.accumulation_code(self.accumulation)
         if self.backend not in ["auto", "gpu", "cpu"]:
             raise ValueError("backend must be one of 'auto', 'gpu', or 'cpu'")
         if n_samples < 2:
@@ -121,12 +131,14 @@ class ReliefF(TransformerMixin, BaseEstimator):
 
         self.effective_backend_ = _base.effective_backend(self.backend)
         self.devices_ = _base.fit_devices(self.devices, self.effective_backend_, n_samples)
+        _base.check_accumulation_devices(self.accumulation, self.devices_)
         if self.verbose:
             where = "GPU" if self.effective_backend_ == "gpu" else "CPU"
             print(f"Running ReliefF on the {where} now...")
-        scores = _lib.relieff_score(self.effective_backend_, x32, y_enc, recip_full, is_discrete,
-                                    self.n_neighbors, class_probs, self.n_jobs,
-                                    devices=self.devices_)
+        with _lib.accumulation(self.accumulation):
+            scores = _lib.relieff_score(self.effective_backend_, x32, y_enc, recip_full,
+                                        is_discrete, self.n_neighbors, class_probs, self.n_jobs,
+                                        devices=self.devices_)
         self.feature_importances_ = scores
         self.top_features_ = _base.top_features(scores, n_select)
         return self
@@ -157,8 +169,10 @@ class ReliefF(TransformerMixin, BaseEstimator):
         x32, y_enc, recip, is_discrete, class_probs = relieff_inputs(
             x, y, self.discrete_limit, where, n_jobs=self.n_jobs)
         self.effective_backend_ = _base.effective_backend(self.backend)
-        plan = _lib.RowsPlan(self.effective_backend_, "relieff", x32, y_enc, recip, is_discrete,
-                             k=self.n_neighbors, class_probs=class_probs, n_jobs=self.n_jobs)
+        with _lib.accumulation(self.accumulation):  # the plan keeps its creation mode
+            plan = _lib.RowsPlan(self.effective_backend_, "relieff", x32, y_enc, recip,
+                                 is_discrete, k=self.n_neighbors, class_probs=class_probs,
+                                 n_jobs=self.n_jobs)
         return ResidentRows(self, "ReliefF", plan, n, is_discrete, self.effective_backend_,
                             before_score=warn_small_class)
 

@@ -112,6 +112,14 @@ def fit_devices(devices, backend: str, n_samples: int):
     return devs
 
 
+def check_accumulation_devices(accumulation: str, devices) -> None:
+    """accumulation='reference' replays one sequential float32 column sum
+    per feature, so it scores on one device (ValueError for several)."""
+    if accumulation == "reference" and devices is not None and len(devices) > 1:
+        raise ValueError("accumulation='reference' runs on one device; got devices="
+                         f"{list(devices)!r}")
+
+
 def stage_device(backend: str, devices=None, n_samples=None):
     """The device a fit may stage X on while validating it: the fit's one
     device when backend is 'auto' or 'gpu', a HIP device is visible and the

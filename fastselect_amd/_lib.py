@@ -45,7 +45,7 @@ EXPORTED = (
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_decision_guard", "fs_plan_set_rows",
     "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs", "fs_plan_kernel_ms",
     "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
-    "fs_surf_score_devices",
+    "fs_surf_score_devices", "fs_set_accumulation", "fs_get_accumulation",
 )
 
 
@@ -139,6 +139,10 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_kernel_ms.argtypes = [_vp, _int]
     lib.fs_plan_kernel_ms.restype = ctypes.c_double
     lib.fs_plan_destroy.argtypes = [_vp]
+    lib.fs_set_accumulation.argtypes = [_int, ctypes.POINTER(_int)]
+    lib.fs_set_accumulation.restype = _int
+    lib.fs_get_accumulation.argtypes = []
+    lib.fs_get_accumulation.restype = _int
     for name in ("fs_column_stats", "fs_multisurf_score", "fs_multisurf_score_rows",
                  "fs_plan_set_rows", "fs_relieff_score", "fs_surf_score",
                  "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create",
@@ -312,6 +316,32 @@ def check(rc: int) -> None:
     if rc == FS_EOOM:
         raise MemoryError(msg)
     raise RuntimeError(msg)
+
+
+ACCUM_MODES = {"fast": 0, "reference": 1}
+
+
+def accumulation_code(mode: str) -> int:
+    """FS_ACCUM_FAST / FS_ACCUM_REFERENCE for the estimators' ``accumulation``
+    parameter ('fast' or 'reference'); ValueError for anything else."""
+    if not isinstance(mode, str) or mode not in ACCUM_MODES:
+        raise ValueError(f"accumulation must be 'fast' or 'reference'; got {mode!r}")
+    return ACCUM_MODES[mode]
+
+
+@contextlib.contextmanager
+def accumulation(mode: str = "fast"):
+    """The calling thread's accumulation mode for the native calls (and plan
+    creations) inside the block (fs_set_accumulation), restored afterwards.
+    'reference' replays the reference's float32 per-sample sums and column
+    sums (MultiSURF.py:198-253, ReliefF.py:181-220) bit for bit."""
+    code = accumulation_code(mode)
+    prev = _int(0)
+    check(_lib.fs_set_accumulation(code, ctypes.byref(prev)))
+    try:
+        yield
+    finally:
+        _lib.fs_set_accumulation(prev.value, None)
 
 
 def _p(a: np.ndarray, t):

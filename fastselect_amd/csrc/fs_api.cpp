@@ -17,6 +17,9 @@ namespace fs {
 static thread_local std::string g_last_error;
 void set_error(const std::string& msg) { g_last_error = msg; }
 
+static thread_local int g_accum = FS_ACCUM_FAST;
+int accumulation_mode() { return g_accum; }
+
 bool trace_on() {
   static const bool on = std::getenv("FS_TRACE") != nullptr;
   return on;
@@ -36,6 +39,29 @@ void trace_mark(const char* phase) {
 using namespace fs;
 
 static int map_prep_rc(int rc) { return rc == 0 ? FS_OK : FS_EINVAL; }
+
+// The calling thread's accumulation mode into a prepared problem
+// (fs_set_accumulation).  Reference order exists for MultiSURF and ReliefF,
+// whose per-sample sums and column sums have a fixed order (MultiSURF.py:
+// 198-253, ReliefF.py:181-220); MultiSURF then takes 32-bit pass-1 operands.
+static int apply_accumulation(Prepared& P) {
+  P.ref_accum = g_accum == FS_ACCUM_REFERENCE ? 1 : 0;
+  if (!P.ref_accum) return FS_OK;
+  if (P.algo == ALGO_SURF) {
+    set_error("reference-order accumulation is not defined for SURF: the reference sums its "
+              "per-thread score rows in thread-schedule order (SURF.py:195, 216)");
+    return FS_ENOTSUP;
+  }
+  if (P.algo == ALGO_MULTISURF) P.no_q16 = 1;
+  return FS_OK;
+}
+
+static int no_reference_devices() {
+  if (g_accum != FS_ACCUM_REFERENCE) return FS_OK;
+  set_error("reference-order accumulation runs on one device (its column sums are one "
+            "sequential float32 sum per feature)");
+  return FS_ENOTSUP;
+}
 
 static int check_backend(int backend, int device) {
   if (backend != FS_BACKEND_CPU && backend != FS_BACKEND_GPU) {
@@ -84,6 +110,18 @@ const char* fs_version(void) { return "fastselect_amd 0.1.0 (gfx950)"; }
 const char* fs_last_error(void) { return g_last_error.c_str(); }
 
 int fs_device_count(void) { return gpu::device_count(); }
+
+int fs_set_accumulation(int mode, int* previous) {
+  if (mode != FS_ACCUM_FAST && mode != FS_ACCUM_REFERENCE) {
+    set_error("accumulation mode must be FS_ACCUM_FAST or FS_ACCUM_REFERENCE");
+    return FS_EINVAL;
+  }
+  if (previous) *previous = g_accum;
+  g_accum = mode;
+  return FS_OK;
+}
+
+int fs_get_accumulation(void) { return g_accum; }
 
 int fs_multisurf_last_guard(double* risk_out, int* rerun_out) {
   return gpu::multisurf_last_guard(risk_out, rerun_out);
@@ -198,12 +236,13 @@ int fs_multisurf_score(int backend, int device, const float* x, int64_t n, int64
   if (rc) return map_prep_rc(rc);
   if (encode_labels_f64(P, y)) return FS_EINVAL;
   P.use_star = use_star ? 1 : 0;
+  if ((rc = apply_accumulation(P)) != FS_OK) return rc;
   if (backend == FS_BACKEND_GPU) return gpu::multisurf_run(P, x, device, scores_out);
   cpu::CpuState st;
   std::vector<double> rs(3 * n), cnt(2 * n), S(P.n_kept);
   cpu::multisurf_pass1(P, x, 0, 1, n_jobs, st, rs.data());
   cpu::multisurf_select(P, x, 0, 1, rs.data(), n_jobs, st, cnt.data());
-  cpu::multisurf_pass2(P, st, cnt.data(), 0, 1, n_jobs, 0, n, S.data());
+  cpu::multisurf_pass2(P, x, st, cnt.data(), 0, 1, n_jobs, 0, n, S.data());
   for (int64_t k = 0; k < P.n_kept; k++) scores_out[k] = (float)(S[k] / (double)n);
   return FS_OK;
 }
@@ -228,12 +267,13 @@ int fs_multisurf_score_rows(int backend, int device, const float* x, int64_t n, 
   if (rc) return map_prep_rc(rc);
   if (encode_labels_f64(P, y)) return FS_EINVAL;
   P.use_star = use_star ? 1 : 0;
+  if ((rc = apply_accumulation(P)) != FS_OK) return rc;
   if (backend == FS_BACKEND_GPU) return gpu::multisurf_rows(P, x, device, row_begin, row_end, sums_out);
   cpu::CpuState st;
   std::vector<double> rs(3 * n), cnt(2 * n);
   cpu::multisurf_pass1(P, x, 0, 1, n_jobs, st, rs.data());
   cpu::multisurf_select(P, x, 0, 1, rs.data(), n_jobs, st, cnt.data());
-  return cpu::multisurf_pass2(P, st, cnt.data(), 0, 1, n_jobs, row_begin, row_end, sums_out);
+  return cpu::multisurf_pass2(P, x, st, cnt.data(), 0, 1, n_jobs, row_begin, row_end, sums_out);
 }
 
 // Shared by the one-shot and the row-range entry points: validate, prepare,
@@ -269,7 +309,9 @@ static int relieff_sums(int backend, int device, const float* x, int64_t n, int6
   P.class_prior.assign(n_classes, 0.0);
   for (int64_t c = 0; c < n_classes; c++) P.class_prior[c] = (double)class_probs[c];
   P.k_neighbors = k;
+  if ((rc = apply_accumulation(P)) != FS_OK) return rc;
   if (devices) {
+    if ((rc = no_reference_devices()) != FS_OK) return rc;
     if (n_classes > 64) {
       set_error("GPU ReliefF supports at most 64 classes");
       return FS_ENOTSUP;
@@ -298,6 +340,7 @@ static int surf_sums(int backend, int device, const double* x, int64_t n, int64_
   if (rc) return map_prep_rc(rc);
   if (encode_labels_i32(P, y)) return FS_EINVAL;
   P.use_star = use_star ? 1 : 0;
+  if ((rc = apply_accumulation(P)) != FS_OK) return rc;
   if (devices) return gpu::rows_run_devices(P, x, devices, n_devices, r_lo, r_hi, sums);
   if (backend == FS_BACKEND_GPU) return gpu::surf_run(P, x, device, r_lo, r_hi, sums);
   return cpu::surf_run(P, x, n_jobs, r_lo, r_hi, sums);
@@ -378,6 +421,7 @@ int fs_multisurf_score_devices(const int* devices, int n_devices, const float* x
   if (rc) return map_prep_rc(rc);
   if (encode_labels_f64(P, y)) return FS_EINVAL;
   P.use_star = use_star ? 1 : 0;
+  if ((rc = no_reference_devices()) != FS_OK) return rc;
   return gpu::multisurf_run_devices(P, x, devices, n_devices, row_begin, row_end, sums_out);
 }
 
@@ -464,6 +508,16 @@ int fs_plan_create(fs_plan** plan_out, int backend, int device, const float* x, 
     return FS_EINVAL;
   }
   pl->P.use_star = use_star ? 1 : 0;
+  if ((rc = apply_accumulation(pl->P)) != FS_OK) {
+    delete pl;
+    return rc;
+  }
+  if (pl->P.ref_accum && world > 1) {
+    delete pl;
+    set_error("reference-order accumulation: pass 2 needs every pair tile's decisions in one "
+              "plan (world 1)");
+    return FS_ENOTSUP;
+  }
   pl->r_lo = 0;
   pl->r_hi = n;
   if (backend == FS_BACKEND_GPU) {
@@ -535,7 +589,8 @@ int fs_plan_create_relieff(fs_plan** plan_out, int backend, int device, const fl
   pl->P.class_prior.assign(n_classes, 0.0);
   for (int64_t c = 0; c < n_classes; c++) pl->P.class_prior[c] = (double)class_probs[c];
   pl->P.k_neighbors = k;
-  if ((rc = finish_rows_plan(pl, device, x, row_begin, row_end, stream)) != FS_OK) {
+  if ((rc = apply_accumulation(pl->P)) != FS_OK ||
+      (rc = finish_rows_plan(pl, device, x, row_begin, row_end, stream)) != FS_OK) {
     delete pl;
     return rc;
   }
@@ -569,7 +624,8 @@ int fs_plan_create_surf(fs_plan** plan_out, int backend, int device, const doubl
     return FS_EINVAL;
   }
   pl->P.use_star = use_star ? 1 : 0;
-  if ((rc = finish_rows_plan(pl, device, x, row_begin, row_end, stream)) != FS_OK) {
+  if ((rc = apply_accumulation(pl->P)) != FS_OK ||
+      (rc = finish_rows_plan(pl, device, x, row_begin, row_end, stream)) != FS_OK) {
     delete pl;
     return rc;
   }
@@ -611,6 +667,8 @@ int fs_plan_set_features(fs_plan* pl, const int64_t* feat_idx, int64_t n_kept) {
   P.class_prior = O.class_prior;
   P.use_star = O.use_star;
   P.k_neighbors = O.k_neighbors;
+  P.ref_accum = O.ref_accum;  // the plan's mode, fixed at creation
+  P.no_q16 = O.ref_accum && O.algo == ALGO_MULTISURF ? 1 : 0;
   if (gpu) {
     rc = gpu::plan_set_features(pl->g, P);
     if (rc != FS_OK) return rc;
@@ -648,8 +706,8 @@ int fs_plan_pass2(fs_plan* pl, const double* counts, double* scores) {
   }
   if (!is_multisurf_plan(pl)) return FS_EINVAL;
   if (pl->g) return gpu::plan_pass2(pl->g, counts, scores);
-  return cpu::multisurf_pass2(pl->P, pl->st, counts, pl->rank, pl->world, pl->n_jobs, pl->r_lo,
-                              pl->r_hi, scores);
+  return cpu::multisurf_pass2(pl->P, pl->xp(), pl->st, counts, pl->rank, pl->world, pl->n_jobs,
+                              pl->r_lo, pl->r_hi, scores);
 }
 
 int fs_plan_decision_guard(fs_plan* pl, const double* rowstats, const double* counts,
@@ -694,6 +752,11 @@ int fs_plan_set_shard(fs_plan* pl, int rank, int world) {
   if (world < 1 || rank < 0 || rank >= world) {
     set_error("shard rank/world must satisfy 0 <= rank < world");
     return FS_EINVAL;
+  }
+  if (pl->P.ref_accum && world > 1) {
+    set_error("reference-order accumulation: pass 2 needs every pair tile's decisions in one "
+              "plan (world 1)");
+    return FS_ENOTSUP;
   }
   if (pl->g) {
     const int rc = gpu::plan_set_shard(pl->g, rank, world);

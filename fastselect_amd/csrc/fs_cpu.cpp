@@ -438,8 +438,71 @@ static void scatter_scores(const Prepared& P, const std::vector<double>& S_perm,
     if (P.out_pos[c] >= 0) scores[P.out_pos[c]] = S_perm[c];
 }
 
-int multisurf_pass2(const Prepared& P, const CpuState& S, const double* counts, int rank,
-                    int world, int n_jobs, int64_t r_lo, int64_t r_hi, double* scores) {
+// The reference's diff of kept feature k between samples i and j
+// (MultiSURF.py:184-187, ReliefF.py:151-154): float32 |x_i - x_j| * recip,
+// or 1 / 0 for a discrete feature.
+static inline float ref_diff(const Prepared& P, const float* X, int64_t i, int64_t j, int64_t k) {
+  const int64_t col = P.kept_col[k];
+  const float a = X[i * P.p_in + col], b = X[j * P.p_in + col];
+  if (P.disc_in[col]) return a != b ? 1.0f : 0.0f;
+  return std::fabs(a - b) * P.recip_in[col];
+}
+
+// temp[:, k].sum() of the reference (numba's float32 .sum(): sequential,
+// MultiSURF.py:252-253, ReliefF.py:219-220) over rows [0, rows).
+static void ref_column_sums(const std::vector<float>& temp, int64_t rows, int64_t nk,
+                            double* scores) {
+  for (int64_t k = 0; k < nk; k++) {
+    float s = 0.0f;
+    for (int64_t r = 0; r < rows; r++) s += temp[(size_t)r * nk + k];
+    scores[k] = (double)s;
+  }
+}
+
+// Reference-order pass 2 (P.ref_accum; fs_refacc.hip k_ms_chains): per focal
+// sample the float32 hit / miss chains over j in ascending order, the
+// float64 division rounded to float32, temp = miss - hit in float32, then
+// the float32 column sums over the focal rows (MultiSURF.py:198-253).
+static int multisurf_pass2_ref(const Prepared& P, const float* X, const CpuState& S,
+                               const double* counts, int n_jobs, int64_t r_lo, int64_t r_hi,
+                               double* scores) {
+  const int64_t n = P.n, nk = P.n_kept, rows = r_hi - r_lo;
+  std::vector<float> temp((size_t)std::max<int64_t>(rows, 0) * nk);
+  parallel_for(rows, n_jobs, [&](int64_t r) {
+    const int64_t i = r_lo + r;
+    std::vector<float> hit((size_t)nk, 0.0f), miss((size_t)nk, 0.0f);
+    for (int64_t j = 0; j < n; j++) {
+      if (j == i) continue;
+      const bool near = S.D[(size_t)i * n + j] < S.thr[i];
+      const bool is_hit = P.labels[j] == P.labels[i];
+      if (near) {
+        float* acc = is_hit ? hit.data() : miss.data();
+        for (int64_t k = 0; k < nk; k++) acc[k] += ref_diff(P, X, i, j, k);
+      } else if (P.use_star && !is_hit) {
+        for (int64_t k = 0; k < nk; k++) miss[k] -= ref_diff(P, X, i, j, k);
+      }
+    }
+    const double H = counts[2 * i], M = counts[2 * i + 1];
+    float* row = temp.data() + (size_t)r * nk;
+    for (int64_t k = 0; k < nk; k++) {
+      const float h = H > 0.0 ? (float)((double)hit[k] / H) : hit[k];
+      const float m = M > 0.0 ? (float)((double)miss[k] / M) : miss[k];
+      row[k] = m - h;
+    }
+  });
+  ref_column_sums(temp, rows, nk, scores);
+  return FS_OK;
+}
+
+int multisurf_pass2(const Prepared& P, const void* x, const CpuState& S, const double* counts,
+                    int rank, int world, int n_jobs, int64_t r_lo, int64_t r_hi, double* scores) {
+  if (P.ref_accum) {
+    if (world != 1 || !x) {
+      set_error("reference-order accumulation: pass 2 needs every pair's decisions (world 1)");
+      return FS_ENOTSUP;
+    }
+    return multisurf_pass2_ref(P, (const float*)x, S, counts, n_jobs, r_lo, r_hi, scores);
+  }
   const int64_t n = P.n, nb = P.n_pad / kTile;
   std::vector<PairW> pairs;
   for (int64_t i = 0; i < n; i++)
@@ -617,6 +680,47 @@ int relieff_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int6
   const int64_t n = P.n, k = P.k_neighbors;
   const int C = P.n_classes;
   const double amb = calibrated_band(P, x, 0, n_jobs);
+  if (P.ref_accum) {
+    // the reference's order (ReliefF.py:157-220): each class's neighbours in
+    // argsort order (exact float32 keys ascending; equal keys by index, see
+    // fs_refacc.hip k_rf_ref_sort), float64 sums in that order, temp =
+    // f32(update), float32 column sums
+    const float* X = (const float*)x;
+    const int64_t nk = P.n_kept, rows = r_hi - r_lo;
+    std::vector<float> temp((size_t)std::max<int64_t>(rows, 0) * nk);
+    parallel_for(rows, n_jobs, [&](int64_t r) {
+      const int64_t i = r_lo + r;
+      std::vector<std::vector<int32_t>> nbr(C);
+      relieff_select_row(P, X, D, i, amb, nbr);
+      for (int c = 0; c < C; c++) {
+        std::vector<std::pair<float, int32_t>> kv;
+        for (int32_t j : nbr[c]) kv.push_back({relieff_exact_key(P, X, i, j), j});
+        std::sort(kv.begin(), kv.end());
+        for (size_t t = 0; t < kv.size(); t++) nbr[c][t] = kv[t].second;
+      }
+      const int32_t li = P.labels[i];
+      double denom = 1.0 - P.class_prior[li];
+      if (denom == 0.0) denom = 1.0;
+      const int64_t kc_own = (int64_t)nbr[li].size();
+      const int64_t h_found = kc_own < k ? kc_own + 1 : k;
+      float* row = temp.data() + (size_t)r * nk;
+      for (int64_t f = 0; f < nk; f++) {
+        double hit_sum = 0.0, miss_sum = 0.0;
+        for (int c = 0; c < C; c++) {
+          double s = 0.0;
+          for (int32_t j : nbr[c]) s += (double)ref_diff(P, X, i, j, f);
+          if (c == li) hit_sum = s;
+          else miss_sum += (P.class_prior[c] / denom) * s;
+        }
+        double update = 0.0;
+        if (h_found > 0) update -= hit_sum / (double)h_found;
+        if (k > 0) update += miss_sum / (double)k;
+        row[f] = (float)update;
+      }
+    });
+    ref_column_sums(temp, rows, nk, scores);
+    return FS_OK;
+  }
   // per-row partial sums, folded in row order for determinism
   std::vector<double> part((size_t)n * P.PW, 0.0);
   parallel_for(n, n_jobs, [&](int64_t i) {

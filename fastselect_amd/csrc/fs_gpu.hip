@@ -3402,6 +3402,24 @@ struct Plan {
   // step's (one plan over every continuous column): pass 1 takes them
   bool corr_ready = false;
   std::vector<char> colmin, colmax; // per input column, x's dtype (device-measured)
+  // reference-order accumulation (P.ref_accum, fs_refacc.hip): the kept
+  // columns of X (float32 [n_pad][Kp]), their recip / discreteness, the
+  // discrete flag of each 256-feature block (layout buffers); MultiSURF's
+  // decision masks [n_pad][n_pad / 64][4] (plan buffer) and the per-batch
+  // flagged-row counts of exact_thresholds
+  float* xk = nullptr;
+  int64_t Kp = 0;
+  int64_t* kcol = nullptr;
+  float* krecip = nullptr;
+  uint8_t* kdisc = nullptr;
+  uint8_t* kblk = nullptr;
+  uint64_t* masks = nullptr;
+  int32_t* bcnt = nullptr;
+  float* temp = nullptr;        // the reference's temp rows [rows][Kp] (own block)
+  size_t temp_cap = 0;
+  float* rkeys = nullptr;       // ReliefF neighbour keys (own block)
+  size_t rkeys_cap = 0;
+  bool ref_seeded = false;      // ReliefF: the column sums continue from the sums buffer
 };
 
 // ---------------------------------------------------------------------------
@@ -3821,6 +3839,8 @@ void plan_destroy(Plan* g) {
   for (void* q : g->scratch) dev_free(q);
   for (void* q : g->owned_shard) dev_free(q);
   if (g->spart) dev_free(g->spart);
+  if (g->temp) dev_free(g->temp);
+  if (g->rkeys) dev_free(g->rkeys);
   if (g->sched) dev_free(g->sched);
   if (g->units8) dev_free(g->units8);
   for (auto& e : g->ev)
@@ -3893,6 +3913,9 @@ static int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats) 
 constexpr int64_t kQ16MinRowsRF = 4096, kQ16MinRowsMS = 16384, kQ16MinRowsMSStar = 10000;
 static int choose_q16(const Prepared& P) {
   if (P.algo == ALGO_SURF || P.no_q16) return 0;
+  // reference-order MultiSURF replays the reference's decisions: 32-bit
+  // operands, whose thresholds need exact recomputation on a handful of rows
+  if (P.algo == ALGO_MULTISURF && P.ref_accum) return 0;
   const char* env = std::getenv("FS_Q16");
   if (env && *env) return std::atoi(env) != 0 ? 1 : 0;
   const int64_t min_rows = P.algo == ALGO_RELIEFF ? kQ16MinRowsRF
@@ -4314,6 +4337,46 @@ static int row_guard(Plan* g) {
 // Feature-layout part of a plan: everything sized by the kept features
 // (permutation tables, quantised operands, pass-2 partials), rebuilt when
 // the plan is re-targeted to another feature subset (fs_plan_set_features).
+// Reference-order accumulation (P.ref_accum): the kept columns of X in kept
+// order, 256-padded (xk), with each kept feature's float32 recip and
+// discreteness as the reference's kernels read them (MultiSURF.py:184-187,
+// ReliefF.py:151-154), and a flag per 256-feature block that holds a
+// discrete one.  Layout buffers: rebuilt with the feature subset.
+static int ref_layout(Plan* g) {
+  const Prepared& Q = g->P;
+  if (g->x_is_f64) {
+    set_error("reference-order accumulation needs float32 X (MultiSURF / ReliefF)");
+    return FS_ENOTSUP;
+  }
+  g->Kp = (Q.n_kept + 255) / 256 * 256;
+  std::vector<float> rec((size_t)g->Kp, 0.0f);
+  std::vector<uint8_t> dsc((size_t)g->Kp, 0), blk((size_t)(g->Kp / 256), 0);
+  for (int64_t k = 0; k < Q.n_kept; k++) {
+    const int64_t col = Q.kept_col[k];
+    rec[k] = Q.recip_in[col];
+    dsc[k] = Q.disc_in[col] ? 1 : 0;
+    if (dsc[k]) blk[k / 256] = 1;
+  }
+  g->alloc_target = 1;
+  int rc;
+  if ((rc = dalloc(g, &g->xk, (size_t)Q.n_pad * g->Kp)) || (rc = dalloc(g, &g->kcol, Q.n_kept)) ||
+      (rc = dalloc(g, &g->krecip, g->Kp)) || (rc = dalloc(g, &g->kdisc, g->Kp)) ||
+      (rc = dalloc(g, &g->kblk, g->Kp / 256))) {
+    g->alloc_target = 0;
+    return rc;
+  }
+  g->alloc_target = 0;
+  if ((rc = h2d(g, g->kcol, Q.kept_col.data(), Q.n_kept)) ||
+      (rc = h2d(g, g->krecip, rec.data(), rec.size())) ||
+      (rc = h2d(g, g->kdisc, dsc.data(), dsc.size())) ||
+      (rc = h2d(g, g->kblk, blk.data(), blk.size())))
+    return rc;
+  rc = refacc::gather_kept((const float*)g->x, Q.n, Q.n_pad, Q.p_in, g->kcol, Q.n_kept, g->Kp,
+                           g->xk, g->stream);
+  if (rc == FS_OK) FS_HIP(hipStreamSynchronize(g->stream));  // host vectors above
+  return rc;
+}
+
 static int plan_layout(Plan* g) {
   Prepared& Q = g->P;
   g->corr_ready = false;
@@ -4385,6 +4448,7 @@ static int plan_layout(Plan* g) {
       (rc = h2d(g, g->dtab_off, Q.dtab_off.data(), Q.PW + 1)) ||
       (rc = h2d(g, g->dtab, Q.dtab.data(), Q.dtab.size())))
     return rc;
+  if (Q.ref_accum && Q.algo != ALGO_SURF && (rc = ref_layout(g))) return rc;
   if ((rc = calibrate_band(g))) return rc;
   if ((rc = row_guard(g))) return rc;
   if (g->calib[5] != 0.0) {
@@ -4582,6 +4646,13 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     if ((rc = dalloc(g, &g->unc, Q.n_pad)) || (rc = dalloc(g, &g->urows, Q.n_pad + 1)) ||
         (rc = dalloc(g, &g->uparts, (size_t)g->thr_rows * nchunk)))
       return fail(rc);
+    // reference-order accumulation: the decision masks (n_pad^2 / 2 bytes)
+    // and exact_thresholds' batch counts (every flagged row is fixed, in
+    // batches of thr_rows)
+    if (Q.ref_accum &&
+        ((rc = dalloc(g, &g->masks, (size_t)Q.n_pad * (Q.n_pad / 64) * 4)) ||
+         (rc = dalloc(g, &g->bcnt, (size_t)(Q.n / std::max(g->thr_rows, 1) + 2)))))
+      return fail(rc);
   }
   g->sparse = choose_sparse(g, Q);
   if ((rc = setup_shard(g, bi, bj))) return fail(rc);
@@ -4770,8 +4841,47 @@ static int refine_pairs(Plan* g, int algo, double delta, double thr_tol = 0.0,
 // check (q16_decision_risk) stays in charge.  Runs between refine_pairs and
 // the neighbour counts; the count is read back once (the fix's row count is
 // reported by fs_plan_info-style diagnostics: g->n_exact_thr).
+// Reference-order accumulation: every flagged row, in batches of thr_rows
+// (the count is read back once; the decisions are then the reference's
+// wherever its arithmetic is replayed exactly).
+static int exact_thresholds_all(Plan* g) {
+  const Prepared& Q = g->P;
+  const int64_t nchunk = (Q.n + kExChunk - 1) / kExChunk;
+  const int B = std::max(g->thr_rows, 1);
+  const unsigned ngroups = (unsigned)((B + kExRows - 1) / kExRows);
+  k_unc_compact<<<1, 1024, 0, g->stream>>>(g->unc, Q.n, (int)Q.n, g->urows, g->urows + Q.n);
+  FS_TRY(launch_check("k_unc_compact"));
+  int32_t cnt = 0;
+  FS_HIP(hipMemcpyAsync(&cnt, g->urows + Q.n, sizeof(cnt), hipMemcpyDeviceToHost, g->stream));
+  FS_HIP(hipStreamSynchronize(g->stream));
+  g->n_exact_thr = cnt;
+  if (cnt == 0) return FS_OK;
+  const int nbatch = (cnt + B - 1) / B;
+  std::vector<int32_t> bc((size_t)nbatch);
+  for (int b = 0; b < nbatch; b++) bc[b] = std::min(B, cnt - b * B);
+  FS_TRY(h2d(g, g->bcnt, bc.data(), bc.size()));
+  for (int b = 0; b < nbatch; b++) {
+    const int32_t* rows = g->urows + (int64_t)b * B;
+    k_row_exact_parts<float><<<dim3((unsigned)nchunk, ngroups), 256, 0, g->stream>>>(
+        (const float*)g->x, Q.n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, rows, g->bcnt + b,
+        B, g->uparts);
+    FS_TRY(launch_check("k_row_exact_parts"));
+    k_row_exact_thr<<<(unsigned)B, 64, 0, g->stream>>>(g->uparts, nchunk, rows, g->bcnt + b, B,
+                                                        Q.n, Q.SC, g->thr);
+    FS_TRY(launch_check("k_row_exact_thr"));
+  }
+  FS_HIP(hipStreamSynchronize(g->stream));  // bc
+  if (trace_on()) {
+    char msg[128];
+    snprintf(msg, sizeof msg, "select: %d rows near a refined pair (exact thresholds, all)", cnt);
+    trace_mark(msg);
+  }
+  return FS_OK;
+}
+
 static int exact_thresholds(Plan* g) {
   const Prepared& Q = g->P;
+  if (Q.ref_accum && !g->thr_all) return exact_thresholds_all(g);
   const int64_t nchunk = (Q.n + kExChunk - 1) / kExChunk;
   const unsigned ngroups = (unsigned)((g->thr_rows + kExRows - 1) / kExRows);
   if (g->thr_all) {  // test hook: flag every row
@@ -4923,9 +5033,63 @@ int plan_select(Plan* g, const double* rowstats, double* counts) {
   return FS_OK;
 }
 
+// Reference-order pass 2 (P.ref_accum), split at the point where every
+// owned tile's decisions are known: ref_masks writes the masks of the
+// current shard's tiles; ref_chains, once every tile of the triangle has
+// written its masks, runs the chains of the focal rows [r_lo, r_hi) and the
+// float32 column sums into scores[n_kept] (as doubles; the reference's
+// float32 sums, not yet divided by n).
+static int ref_masks(Plan* g) {
+  const Prepared& Q = g->P;
+  return refacc::multisurf_masks(g->D, Q.n, Q.n_pad, g->tiles, g->n_tiles, g->thr, g->lab,
+                                 Q.use_star, g->masks, g->stream);
+}
+
+// temp[rows][Kp] (float32 rows of the reference's temp matrix), kept between
+// steps and grown on demand.
+static int ref_temp(Plan* g, int64_t rows, float** out) {
+  const size_t need = (size_t)std::max<int64_t>(rows, 1) * (size_t)g->Kp;
+  if (need > g->temp_cap) {
+    if (g->temp) dev_free(g->temp);
+    g->temp = nullptr;
+    g->temp_cap = 0;
+    void* p = nullptr;
+    FS_TRY(dev_alloc(&p, need * sizeof(float), g->device));
+    g->temp = (float*)p;
+    g->temp_cap = need;
+  }
+  *out = g->temp;
+  return FS_OK;
+}
+
+static int ref_chains(Plan* g, const double* counts, double* scores) {
+  const Prepared& Q = g->P;
+  const int64_t rows = g->r_hi - g->r_lo;
+  FS_HIP(hipMemsetAsync(scores, 0, sizeof(double) * Q.n_kept, g->stream));
+  if (rows <= 0) return FS_OK;
+  float* temp = nullptr;
+  FS_TRY(ref_temp(g, rows, &temp));
+  FS_HIP(hipEventRecord(g->ev[2], g->stream));
+  FS_TRY(refacc::multisurf_chains(g->xk, g->Kp, g->krecip, g->kdisc, g->kblk, g->masks, Q.n,
+                                  Q.n_pad, counts, Q.use_star, g->r_lo, g->r_hi, temp, g->stream));
+  FS_HIP(hipEventRecord(g->ev[3], g->stream));
+  return refacc::column_sums(temp, rows, g->Kp, Q.n_kept, nullptr, scores, g->stream);
+}
+
 int plan_pass2(Plan* g, const double* counts, double* scores) {
   const Prepared& Q = g->P;
   FS_HIP(hipSetDevice(g->device));
+  if (Q.ref_accum) {
+    if (g->world > 1) {
+      set_error("reference-order accumulation: pass 2 needs every pair tile's decisions in one "
+                "plan (world 1; the one-shot calls shard internally)");
+      return FS_ENOTSUP;
+    }
+    FS_TRY(ref_masks(g));
+    FS_TRY(ref_chains(g, counts, scores));
+    if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
+    return FS_OK;
+  }
   FS_TRY(run_weights(g, counts, ALGO_MULTISURF, 1.0 / Q.SC));
   FS_TRY(run_pass2(g, scores));
   if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
@@ -5057,6 +5221,21 @@ static int run_multisurf_shards(Plan* g, int shards, int rank, int world, double
     FS_TRY(plan_pass1(g, rs_v));
     FS_TRY(plan_select(g, rs, cnt_v));
     FS_TRY(add(cnt, cnt_v, 2 * Q.n, v == 0));
+  }
+  if (Q.ref_accum) {
+    // reference order: every shard's decisions into the masks, then the
+    // chains of all focal rows once (one device holds the whole job here)
+    if (world != 1) {
+      set_error("reference-order accumulation: one device per job in the one-shot calls");
+      return FS_ENOTSUP;
+    }
+    for (int v = 0; v < shards; v++) {
+      FS_TRY(plan_set_shard(g, rank + world * v, W));
+      FS_TRY(plan_pass1(g, rs_v));
+      FS_TRY(plan_select(g, rs, cnt_v));
+      FS_TRY(ref_masks(g));
+    }
+    return ref_chains(g, cnt, sc);
   }
   for (int v = 0; v < shards; v++) {  // round 3: weights, pass 2
     FS_TRY(plan_set_shard(g, rank + world * v, W));
@@ -5265,7 +5444,7 @@ static int run_panels(const Prepared& P, int64_t r_lo, int64_t r_hi, int64_t pan
 static int surf_run_one(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
                         double* sums_out);
 static int relieff_run_one(const Prepared& P, const void* x, int device, int64_t r_lo,
-                           int64_t r_hi, double* sums_out);
+                           int64_t r_hi, double* sums_out, const double* seed = nullptr);
 
 int surf_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
              double* sums_out) {
@@ -5280,6 +5459,17 @@ int relieff_run(const Prepared& P, const void* x, int device, int64_t r_lo, int6
                 double* sums_out) {
   const int64_t panel = row_panel_rows(P, device, r_hi - r_lo);
   if (r_hi - r_lo <= panel) return relieff_run_one(P, x, device, r_lo, r_hi, sums_out);
+  if (P.ref_accum) {
+    // one float32 column sum over all panels, each continuing the last
+    std::vector<double> prev((size_t)P.n_kept, 0.0);
+    for (int64_t lo = r_lo; lo < r_hi;) {
+      const int64_t hi = std::min(r_hi, (lo / kTile * kTile) + panel);
+      FS_TRY(relieff_run_one(P, x, device, lo, hi, sums_out, lo == r_lo ? nullptr : prev.data()));
+      std::copy(sums_out, sums_out + P.n_kept, prev.begin());
+      lo = hi;
+    }
+    return FS_OK;
+  }
   return run_panels(P, r_lo, r_hi, panel, sums_out, [&](int64_t lo, int64_t hi, double* o) {
     return relieff_run_one(P, x, device, lo, hi, o);
   });
@@ -5514,6 +5704,31 @@ static int plan_score_relieff(Plan* g, double* sums_dev) {
     std::fprintf(stderr, "[fs_trace] relieff: %lld exact pairs, %lld tie rows\n",
                  (long long)g->n_refined, (long long)g->n_tie_rows);
   }
+  if (Q.ref_accum) {
+    // the reference's order (fs_refacc.hip): neighbour lists in argsort
+    // order, float32 temp rows, float32 sequential column sums, continuing
+    // from the previous row panel's sums when seeded (relieff_run)
+    const int64_t rows = g->r_hi - g->r_lo;
+    const size_t nkeys = (size_t)std::max<int64_t>(rows * C * std::max<int64_t>(k, 1), 1);
+    if (nkeys > g->rkeys_cap) {
+      if (g->rkeys) dev_free(g->rkeys);
+      g->rkeys = nullptr;
+      g->rkeys_cap = 0;
+      void* p = nullptr;
+      FS_TRY(dev_alloc(&p, nkeys * sizeof(float), g->device));
+      g->rkeys = (float*)p;
+      g->rkeys_cap = nkeys;
+    }
+    float* temp = nullptr;
+    FS_TRY(ref_temp(g, rows, &temp));
+    FS_TRY(refacc::relieff_rows(g->xk, g->Kp, g->krecip, g->kdisc, Q.n_kept, g->lab, dprior, C, k,
+                                nbr, nfound, g->r_lo, g->r_hi, g->rkeys, temp, g->stream));
+    FS_HIP(hipEventRecord(g->ev[3], g->stream));
+    if (!g->ref_seeded) FS_HIP(hipMemsetAsync(sums_dev, 0, sizeof(double) * Q.n_kept, g->stream));
+    if (rows <= 0) return FS_OK;
+    return refacc::column_sums(temp, rows, g->Kp, Q.n_kept, g->ref_seeded ? sums_dev : nullptr,
+                                sums_dev, g->stream);
+  }
   k_rf_update<<<dim3((unsigned)(Q.PW / 64), (unsigned)nrb), 256, 0, g->stream>>>(
       g->xs, g->r_lo, g->r_hi, Q.PW, Q.PC, g->lab, dprior, C, k, nbr, nfound, part);
   FS_TRY(launch_check("k_rf_update"));
@@ -5525,7 +5740,7 @@ static int plan_score_relieff(Plan* g, double* sums_dev) {
 }
 
 static int relieff_run_one(const Prepared& P, const void* x, int device, int64_t r_lo,
-                           int64_t r_hi, double* sums_out) {
+                           int64_t r_hi, double* sums_out, const double* seed) {
   if (P.n_classes > 64) {
     set_error("GPU ReliefF supports at most 64 classes");
     return FS_ENOTSUP;
@@ -5534,6 +5749,12 @@ static int relieff_run_one(const Prepared& P, const void* x, int device, int64_t
   FS_TRY(plan_create(&g, P, x, 0, device, 0, 1, 0, r_lo, r_hi));
   double* sc = nullptr;
   int rc = dalloc(g, &sc, g->P.n_kept);
+  if (rc == FS_OK && seed) {
+    // reference order, a later row panel: the float32 column sums go on
+    // from the previous panels' (ReliefF.py:219-220 is one sequential sum)
+    g->ref_seeded = true;
+    rc = h2d(g, sc, seed, (size_t)g->P.n_kept);
+  }
   if (rc == FS_OK) rc = plan_score_relieff(g, sc);
   if (rc == FS_OK) rc = copy_sums(g, sc, sums_out);
   plan_destroy(g);

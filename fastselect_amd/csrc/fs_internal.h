@@ -101,7 +101,18 @@ struct Prepared {
   // 1: never 16-bit pass-1 operands (the one-shot MultiSURF re-run after the
   // decision-risk check, fs_gpu.hip q16_decision_risk)
   int no_q16 = 0;
+  // 1: reference-order accumulation (fs_set_accumulation(FS_ACCUM_REFERENCE),
+  // fs_refacc.hip): MultiSURF's per-(sample, feature) float32 hit / miss
+  // chains in ascending j and ReliefF's float32 temp of its float64 update,
+  // each followed by the reference's sequential float32 column sums.
+  // MultiSURF then takes 32-bit pass-1 operands and exact thresholds for
+  // every flagged row, however many.
+  int ref_accum = 0;
 };
+
+// Accumulation mode of the calling thread's next calls (fs_api.cpp,
+// fs_set_accumulation): FS_ACCUM_FAST (0) or FS_ACCUM_REFERENCE (1).
+int accumulation_mode();
 
 // Build the permutation, label codes, discrete tables and integer scale.
 // x is row-major [n][p_in], float32 (x_is_f64 == 0) or float64.
@@ -319,8 +330,10 @@ int multisurf_select(const Prepared& P, const void* x, int rank, int world,
                      const double* rowstats, int n_jobs, CpuState& S, double* counts);
 // Score sums of the focal samples [r_lo, r_hi) only (each pair side counts
 // for its own focal sample; [0, n) = the whole fit).
-int multisurf_pass2(const Prepared& P, const CpuState& S, const double* counts, int rank,
-                    int world, int n_jobs, int64_t r_lo, int64_t r_hi, double* scores);
+// x: the problem's float32 X (read only by reference-order accumulation,
+// whose chains use the reference's raw diffs; world must then be 1).
+int multisurf_pass2(const Prepared& P, const void* x, const CpuState& S, const double* counts,
+                    int rank, int world, int n_jobs, int64_t r_lo, int64_t r_hi, double* scores);
 // Score sums (not divided by n) of the focal samples [r_lo, r_hi).
 int surf_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int64_t r_hi,
              double* scores);
@@ -487,6 +500,37 @@ int surf_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t
              double* sums_out);
 int relieff_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
                 double* sums_out);
+
+// Reference-order accumulation kernels (fs_refacc.hip); `stream` is a
+// hipStream_t, `tiles` the plan's int2 tile list.
+namespace refacc {
+// xk[j][k] = x[j][kcol[k]] (k < n_kept, j < n), zero padding to [n_pad][Kp];
+// Kp a multiple of 256.
+int gather_kept(const float* x, int64_t n, int64_t n_pad, int64_t p_in, const int64_t* kcol,
+                int64_t n_kept, int64_t Kp, float* xk, void* stream);
+// Near-hit / miss-chain / far-miss bit masks of the owned tiles' pairs:
+// masks[(row * (n_pad / 64) + word) * 4 + type].
+int multisurf_masks(const double* D, int64_t n, int64_t n_pad, const void* tiles, int64_t n_tiles,
+                    const double* thr, const int32_t* lab, int use_star, uint64_t* masks,
+                    void* stream);
+// temp[i - r_lo][k] = f32(miss chain / M_i) - f32(hit chain / H_i) for the
+// focal rows [r_lo, r_hi) (MultiSURF.py:198-251).
+int multisurf_chains(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
+                     const uint8_t* blkdisc, const uint64_t* masks, int64_t n, int64_t n_pad,
+                     const double* counts, int use_star, int64_t r_lo, int64_t r_hi, float* temp,
+                     void* stream);
+// out[k] = float32 sequential sum of temp[0..rows)[k] (starting from
+// (float) init[k] when init is not null; init may alias out), as a double.
+int column_sums(const float* temp, int64_t rows, int64_t Kp, int64_t n_kept, const double* init,
+                double* out, void* stream);
+// ReliefF: each (row, class) neighbour list put in argsort order (exact
+// keys; keys[(rows) * C * k] scratch), then temp[i - r_lo][k] = f32(update)
+// (ReliefF.py:177-216).
+int relieff_rows(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
+                 int64_t n_kept, const int32_t* lab, const double* prior, int C, int64_t k,
+                 int32_t* nbr, const int32_t* nfound, int64_t r_lo, int64_t r_hi, float* keys,
+                 float* temp, void* stream);
+}  // namespace refacc
 }  // namespace gpu
 
 }  // namespace fs

@@ -155,11 +155,15 @@ class ShardedMultiSURF:
     """
 
     def __init__(self, x, y, recip, is_discrete, use_star=False, backend="gpu", device=0,
-                 shard=True, rows=None, shards=None):
+                 shard=True, rows=None, shards=None, accumulation="fast"):
         import os
 
         import torch
         self.dist, self.rank, self.world = _dist() if shard else (None, 0, 1)
+        _lib.accumulation_code(accumulation)
+        if accumulation == "reference" and self.world > 1:
+            raise ValueError("accumulation='reference' needs every pair tile's decisions in "
+                             "one plan: world 1")
         self.n, self.p = x.shape
         self.backend = backend
         # tile shards per device (n beyond HBM): the device holds the distance
@@ -180,9 +184,13 @@ class ShardedMultiSURF:
         # tiles twice and others never.  Each rank sizes V from its own free
         # memory; the largest V fits on every rank.
         self.shards = self._agree_max(max(1, int(shards)))
-        self.plan = _lib.Plan(backend, x, y, recip, is_discrete, use_star=use_star,
-                              rank=self.rank, world=self.world * self.shards, device=device,
-                              stream=stream)
+        if accumulation == "reference":
+            # one plan holding every tile (the one-shot calls shard by themselves)
+            self.shards = 1
+        with _lib.accumulation(accumulation):  # the plan keeps its creation mode
+            self.plan = _lib.Plan(backend, x, y, recip, is_discrete, use_star=use_star,
+                                  rank=self.rank, world=self.world * self.shards, device=device,
+                                  stream=stream)
         if rows is not None:  # focal-sample slice: pass 2 sums those samples only
             self.plan.set_rows(*rows)
         f64 = torch.float64

@@ -62,6 +62,36 @@ extern "C" {
 #define FS_BACKEND_CPU 0
 #define FS_BACKEND_GPU 1
 
+#define FS_ACCUM_FAST 0       /* default: symmetric pair weights, float64 partial sums */
+#define FS_ACCUM_REFERENCE 1  /* the reference's float32 per-sample chains and column sums */
+
+/*
+ * Accumulation mode of the calling thread's subsequent scoring calls and
+ * plan creations (a plan keeps the mode it was created with).  No reference
+ * counterpart: the reference has one arithmetic, its kernels' float32 sums
+ * (MultiSURF.py:198-253, ReliefF.py:181-220).
+ *   FS_ACCUM_FAST       the default pass 2: each pair's two directed weights
+ *                       folded into one, float32 streams summed in float64.
+ *                       10-60x closer to the exact (float64) sums than the
+ *                       reference's own float32 sums (DESIGN.md §The oracle).
+ *   FS_ACCUM_REFERENCE  MultiSURF / MultiSURF*: every focal sample's hit and
+ *                       miss diffs summed in float32 in ascending j, divided,
+ *                       temp = miss - hit in float32, then each feature's
+ *                       float32 sequential column sum; ReliefF: float32 temp of
+ *                       the float64 update over argsort-ordered neighbours and
+ *                       the same column sums.  MultiSURF then runs pass 1 on
+ *                       32-bit operands with exact thresholds for every
+ *                       flagged row.  The scores are then the reference's
+ *                       arithmetic bit for bit (tests/test_refacc*.py).  SURF
+ *                       has no fixed reference order (its per-thread rows,
+ *                       SURF.py:195, 216): FS_ENOTSUP.  One device only:
+ *                       the fs_*_score_devices calls and plans with world > 1
+ *                       return FS_ENOTSUP.
+ * previous (nullable) receives the mode in force before the call.
+ */
+FS_API int fs_set_accumulation(int mode, int* previous);
+FS_API int fs_get_accumulation(void);
+
 /* Library identity and device discovery. */
 FS_API const char* fs_version(void);
 FS_API const char* fs_last_error(void);

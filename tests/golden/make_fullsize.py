@@ -97,9 +97,34 @@ def run(name, n_jobs):
     print(f"{name}: {time.time() - t0:.0f} s -> {out}", flush=True)
 
 
+def run_decisions(name, n_jobs):
+    """fullsize_<name>_decisions.npz: the reference's near/far decisions alone
+    at a full-size MultiSURF configuration (oracle_multisurf_decisions, pass 1
+    only: thresholds mu - sigma/2 and every row's near hit / near miss
+    counts, MultiSURF.py:174-217), so the GPU test can assert the default
+    path's decisions row by row (VERDICT r4 next #2)."""
+    from oracle import oracle as O
+    algo, n, p, red, _, extra = CONFIGS[name]
+    assert algo == "multisurf"
+    t0 = time.time()
+    X, y = make_data(n, p, red, n_classes=extra.get("n_classes", 2))
+    x = X.astype(np.float32)
+    thr, counts = O.multisurf_decisions(x, y, n_jobs=n_jobs)
+    out = os.path.join(HERE, f"fullsize_{name}_decisions.npz")
+    np.savez_compressed(out, x_sha256=np.array(x_digest(x)),
+                        y_sum=np.array(int(np.asarray(y).sum())), thr=thr,
+                        counts=counts.astype(np.int32), n=np.array(n), p=np.array(p))
+    print(f"{name} decisions: {time.time() - t0:.0f} s -> {out}", flush=True)
+
+
 def main():
-    names = sys.argv[1:] or list(CONFIGS)
+    args = sys.argv[1:]
     n_jobs = int(os.environ.get("ORACLE_THREADS", "-1"))
+    if args and args[0] == "--decisions":
+        for nm in args[1:] or ["cfg4_multisurf"]:
+            run_decisions(nm, n_jobs)
+        return
+    names = args or list(CONFIGS)
     for nm in names:
         run(nm, n_jobs)
 
