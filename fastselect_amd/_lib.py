@@ -43,7 +43,7 @@ EXPORTED = (
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_decision_guard", "fs_plan_set_rows",
-    "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs", "fs_plan_kernel_ms",
+    "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_calibration_ex", "fs_plan_weighted_pairs", "fs_plan_kernel_ms",
     "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
     "fs_surf_score_devices", "fs_set_accumulation", "fs_get_accumulation",
 )
@@ -133,6 +133,8 @@ def _load() -> ctypes.CDLL:
                                            ctypes.POINTER(_int)]
     lib.fs_plan_info.argtypes = [_vp, _i64p, _f64p, _i64p]
     lib.fs_plan_calibration.argtypes = [_vp, _f64p]
+    lib.fs_plan_calibration_ex.argtypes = [_vp, _f64p, _int]
+    lib.fs_plan_calibration_ex.restype = _int
     lib.fs_plan_set_shard.argtypes = [_vp, _int, _int]
     lib.fs_multisurf_shards.argtypes = [_int, _i64, _i64, _int, ctypes.POINTER(_int)]
     lib.fs_plan_weighted_pairs.argtypes = [_vp, _i64p]
@@ -577,7 +579,8 @@ class Plan:
     def calibration(self) -> dict:
         """Refinement-band calibration of the current layout (fs_plan_calibration)."""
         v = (ctypes.c_double * 8)()
-        check(_lib.fs_plan_calibration(self._h, v))
+        m = _lib.fs_plan_calibration_ex(self._h, v, 8)
+        check(min(m, 0))
         return {"q16": bool(v[0]), "rms": v[1], "max": v[2], "model_sigma": v[3],
                 "band_vs_model": v[4], "guard": bool(v[5]), "row_guard": v[5] == 2.0,
                 "row_bias_vs_limit": v[6], "SC": v[7]}

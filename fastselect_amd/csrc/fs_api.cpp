@@ -797,16 +797,26 @@ int fs_plan_info(const fs_plan* pl, int64_t* owned_tiles_out, double* pfe,
   return FS_OK;
 }
 
-int fs_plan_calibration(const fs_plan* pl, double* out) {
-  if (!pl || !out) {
-    set_error("NULL plan or output");
+int fs_plan_calibration_ex(const fs_plan* pl, double* out, int n_out) {
+  if (!pl || !out || n_out < 0) {
+    set_error("NULL plan or output, or n_out < 0");
     return FS_EINVAL;
   }
-  if (pl->g) return gpu::plan_calibration(pl->g, out);
-  const double v[8] = {0.0, 0.0, 0.0, std::sqrt((double)pl->P.pc / 6.0 + 1.0), 1.0, 0.0, 0.0,
-                       pl->P.SC};
-  for (int k = 0; k < 8; k++) out[k] = v[k];
-  return FS_OK;
+  double v[8] = {0.0, 0.0, 0.0, std::sqrt((double)pl->P.pc / 6.0 + 1.0), 1.0, 0.0, 0.0, pl->P.SC};
+  if (pl->g) {
+    const int rc = gpu::plan_calibration(pl->g, v);
+    if (rc != FS_OK) return rc;
+  }
+  const int m = n_out < 8 ? n_out : 8;
+  for (int k = 0; k < m; k++) out[k] = v[k];
+  return m;
+}
+
+// The six values documented since the first release (writing
+// out[6] / out[7] through the old signature overran double[6] callers).
+int fs_plan_calibration(const fs_plan* pl, double* out) {
+  const int rc = fs_plan_calibration_ex(pl, out, 6);
+  return rc < 0 ? rc : FS_OK;
 }
 
 int fs_plan_weighted_pairs(const fs_plan* pl, int64_t* pairs) {

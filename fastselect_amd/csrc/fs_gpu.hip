@@ -3378,6 +3378,7 @@ struct Plan {
   unsigned int* unc = nullptr;  // [n_pad] row flags
   int32_t* urows = nullptr;     // [n_pad + 1] flagged rows in index order, then their count
   double2* uparts = nullptr;    // [thr_rows][nchunk] exact row-moment partials
+  size_t uparts_cap = 0;        // double2 slots of uparts
   int thr_rows = kExactThrRows; // rows fixed at most: exact_thr_rows(n) (FS_THR_EXACT_ALL: all, tests)
   bool thr_all = false;
   int32_t n_exact_thr = 0;      // rows whose threshold the last select recomputed (-1: too many)
@@ -4377,6 +4378,28 @@ static int ref_layout(Plan* g) {
   return rc;
 }
 
+// Rows exact_thresholds fixes per select, from the current layout's feature
+// count (both backends use exact_thr_rows(n, pc + pd) of the layout in use,
+// a TuRF refit with fewer features may fix more rows); the
+// partials buffer grows with it.
+static int size_exact_rows(Plan* g) {
+  const Prepared& Q = g->P;
+  if (Q.algo != ALGO_MULTISURF) return FS_OK;
+  g->thr_rows = (int)(g->thr_all ? Q.n : exact_thr_rows(Q.n, Q.pc + Q.pd));
+  const int64_t nchunk = (Q.n + kExChunk - 1) / kExChunk;
+  const size_t need = (size_t)g->thr_rows * nchunk;
+  if (need <= g->uparts_cap) return FS_OK;
+  if (g->uparts) {
+    g->owned.erase(std::remove(g->owned.begin(), g->owned.end(), (void*)g->uparts),
+                   g->owned.end());
+    dev_free(g->uparts);
+    g->uparts = nullptr;
+  }
+  FS_TRY(dalloc(g, &g->uparts, need));
+  g->uparts_cap = need;
+  return FS_OK;
+}
+
 static int plan_layout(Plan* g) {
   Prepared& Q = g->P;
   g->corr_ready = false;
@@ -4448,6 +4471,7 @@ static int plan_layout(Plan* g) {
       (rc = h2d(g, g->dtab_off, Q.dtab_off.data(), Q.PW + 1)) ||
       (rc = h2d(g, g->dtab, Q.dtab.data(), Q.dtab.size())))
     return rc;
+  if ((rc = size_exact_rows(g))) return rc;
   if (Q.ref_accum && Q.algo != ALGO_SURF && (rc = ref_layout(g))) return rc;
   if ((rc = calibrate_band(g))) return rc;
   if ((rc = row_guard(g))) return rc;
@@ -4641,10 +4665,9 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     // test hook: every row's threshold from exact distances (the machinery
     // of exact_thresholds checked on all rows against the oracle's)
     g->thr_all = std::getenv("FS_THR_EXACT_ALL") != nullptr;
+    // thr_rows and uparts: size_exact_rows (plan_layout, per feature layout)
     g->thr_rows = (int)(g->thr_all ? Q.n : exact_thr_rows(Q.n, Q.pc + Q.pd));
-    const int64_t nchunk = (Q.n + kExChunk - 1) / kExChunk;
-    if ((rc = dalloc(g, &g->unc, Q.n_pad)) || (rc = dalloc(g, &g->urows, Q.n_pad + 1)) ||
-        (rc = dalloc(g, &g->uparts, (size_t)g->thr_rows * nchunk)))
+    if ((rc = dalloc(g, &g->unc, Q.n_pad)) || (rc = dalloc(g, &g->urows, Q.n_pad + 1)))
       return fail(rc);
     // reference-order accumulation: the decision masks (n_pad^2 / 2 bytes)
     // and exact_thresholds' batch counts (every flagged row is fixed, in
@@ -5310,6 +5333,10 @@ int plan_decision_guard(Plan* g, const double* rowstats, const double* counts,
   const Prepared& Q = g->P;
   const char* force = std::getenv("FS_Q16");
   if (Q.algo != ALGO_MULTISURF || !g->use_q16 || Q.use_star || (force && *force)) return FS_OK;
+  // a focal-row slice holds only its rows' partial sums: as the one-shot
+  // slice calls (multisurf_rows, a partial multisurf_run_devices), no check
+  // (max |score| of a partial sum would inflate the risk)
+  if (g->r_lo != 0 || g->r_hi != Q.n) return FS_OK;
   FS_HIP(hipSetDevice(g->device));
   std::vector<double> h((size_t)(5 * Q.n + Q.n_kept));
   FS_HIP(hipMemcpyAsync(h.data(), rowstats, sizeof(double) * 3 * Q.n, hipMemcpyDeviceToHost,

@@ -396,18 +396,22 @@ FS_API int fs_plan_info(const fs_plan* plan, int64_t* owned_tiles, double* pair_
 /* Refinement-band calibration of the plan's current feature layout (GPU
  * MultiSURF / ReliefF plans; no reference counterpart -- it guards the
  * integer pass 1 that replaces the reference's float distance loop,
- * MultiSURF.py:176-188).  out[8]: [0] 1 if pass 1 runs on 16-bit operands,
- * [1] / [2] rms / max |quantised - reference| distance error over 4096
- * sampled pairs (integer units), [3] the independent-rounding model's
- * standard deviation sqrt(pc/6 + 1), [4] band / model band, [5] 1 if the
- * coherence guard turned 16-bit operands off, 2 if the per-row guard did (a
- * row whose mean pass-1 error, measured by the mean correction, exceeds 12
- * standard deviations of independent rounding), [6] that row guard's largest
- * row bias over its limit (0 when it did not run), [7] SC, the integer units
- * per scaled-diff unit of pass 1 (the row statistics of fs_plan_pass1 are in
- * these units: mu_i = (rowstats[3i] - rowstats[3i+2]) / (n - 1) / SC).  CPU
- * plans: out[0..7] = {0, 0, 0, model sigma, 1, 0, 0, SC}. */
+ * MultiSURF.py:176-188).  fs_plan_calibration writes out[6] (its size since
+ * the first release): [0] 1 if pass 1 runs on 16-bit operands, [1] / [2] rms
+ * / max |quantised - reference| distance error over 4096 sampled pairs
+ * (integer units), [3] the independent-rounding model's standard deviation
+ * sqrt(pc/6 + 1), [4] band / model band, [5] 1 if the coherence guard turned
+ * 16-bit operands off, 2 if the per-row guard did (a row whose mean pass-1
+ * error, measured by the mean correction, exceeds 12 standard deviations of
+ * independent rounding).  fs_plan_calibration_ex writes min(n_out, 8)
+ * values -- the six above, then [6] that row guard's largest row bias over
+ * its limit (0 when it did not run) and [7] SC, the integer units per
+ * scaled-diff unit of pass 1 (the row statistics of fs_plan_pass1 are in
+ * these units: mu_i = (rowstats[3i] - rowstats[3i+2]) / (n - 1) / SC) -- and
+ * returns how many it wrote (or a negative FS_E* code).  CPU plans:
+ * {0, 0, 0, model sigma, 1, 0, 0, SC}. */
 FS_API int fs_plan_calibration(const fs_plan* plan, double* out);
+FS_API int fs_plan_calibration_ex(const fs_plan* plan, double* out, int n_out);
 /* Owned pairs that carried a non-zero pass-2 weight in the last pass 2 (the
  * pairs the sparse GPU pass 2 evaluates; -1 when the plan does not count
  * them: CPU backend, dense pass 2, or before the first pass 2). */

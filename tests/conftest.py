@@ -70,6 +70,13 @@ def assert_parity_attributed(a, ref, exact, counts=None, ref_counts=None, tol=1e
     assert acc_err <= 0.2 * ref_err, (
         f"{acc_err:.3e} from the float64 sums, reference arithmetic {ref_err:.3e} "
         f"({summary(a, ref)})")
+    # an absolute ceiling against the reference too: a regression
+    # that moved the scores away from both the reference and the exact sums
+    # would fail here even where the 5x bar above held
+    ref_dist = np.max(np.abs(a - ref)) / scale
+    assert ref_dist <= ref_err + tol, (
+        f"{ref_dist:.3e} from the reference, above its own {ref_err:.3e} + {tol:.0e} "
+        f"({summary(a, ref)})")
     ta = set(np.argsort(a)[::-1][:k].tolist())
     tr = set(np.argsort(ref)[::-1][:k].tolist())
     assert ta == tr, f"top-{k} differ: {sorted(ta ^ tr)} ({summary(a, ref)})"

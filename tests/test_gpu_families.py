@@ -97,7 +97,8 @@ def test_uniform_noise_multisurf_reruns_on_32bit(F):
     32-bit operands.  Every row's near hit / miss count then equals the
     reference's; the reference's own float32 sums are 2.6e-5 of max |s| from
     the float64 sums of those decisions, so the bar is the attributed one
-    (conftest.assert_parity_attributed): 10x closer to the float64 sums."""
+    (conftest.assert_parity_attributed): at least 5x closer to the float64
+    sums, and within the reference's own error + 1e-5 of the reference."""
     s, ref, (risk, rerun) = _fit(F, "uniform_16k", False)
     assert risk > 5e-6 and rerun
     sp, counts, ref_counts, exact = _decided("uniform_16k")

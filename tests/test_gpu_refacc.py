@@ -1,0 +1,171 @@
+"""Reference-order accumulation on the HIP path (fs_refacc.hip): scores
+BIT-IDENTICAL to the oracle's float32 arithmetic on
+
+  * the n = 16384 uniform-noise and lognormal families, whose reference
+    float32 sums sit 2.6-2.9e-5 of max |s| from the float64 sums
+    (tests/golden/family_*.npz, oracle vectors);
+  * the heavy-tail sweep of tests/test_random_parity.py and the small sweep;
+  * VERDICT r4's n = 2500, p = 600 signal-free cases (exp(4z), Pareto(1),
+    one 1e7 outlier per column: MultiSURF*'s top-10 there is the reference's
+    only when its float32 rounding is replayed);
+  * the BASELINE configurations cfg2, cfg3 (2 and 3 classes) and cfg4 -- the
+    north star, 20000 x 20000 -- against the full-size oracle fixtures.
+
+The oracle runs live for the small cases (oracle/_build, C, the box's host
+threads); the large ones use the committed fixtures with the sha256 of X.
+"""
+import hashlib
+import importlib.util
+import os
+import warnings
+
+import numpy as np
+import pytest
+
+from test_random_parity import make_case, make_tail_case
+from test_refacc import assert_bitexact, verdict_case
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+
+
+@pytest.fixture(scope="module")
+def F():
+    import fastselect_amd
+    from fastselect_amd import _lib
+    if _lib.device_count() < 1:
+        pytest.fail("no HIP device visible")
+    return fastselect_amd
+
+
+def fit_ref(est, X, y):
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", UserWarning)
+        return est.fit(X, y).feature_importances_
+
+
+def _families():
+    spec = importlib.util.spec_from_file_location("mk_families",
+                                                  os.path.join(GOLD, "make_families.py"))
+    mk = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mk)
+    return mk
+
+
+@pytest.mark.parametrize("name", ["uniform_16k", "lognormal_16k", "mixed_16k"])
+@pytest.mark.parametrize("star", [False, True])
+def test_family_bitexact(F, name, star):
+    fx = np.load(os.path.join(GOLD, f"family_{name}.npz"), allow_pickle=False)
+    X, y = _families().make(name)
+    assert hashlib.sha256(X.tobytes()).hexdigest() == str(fx["x_sha256"])
+    s = fit_ref(F.MultiSURF(backend="gpu", use_star=star, accumulation="reference"), X, y)
+    assert_bitexact(s, fx["scores_star" if star else "scores"])
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_tail_sweep_bitexact(F, oracle, seed):
+    X, y, k = make_tail_case(seed)
+    for star in (False, True):
+        assert_bitexact(
+            fit_ref(F.MultiSURF(backend="gpu", use_star=star, accumulation="reference"), X, y),
+            oracle.multisurf_scores(X, y, use_star=star))
+    assert_bitexact(
+        fit_ref(F.ReliefF(backend="gpu", n_neighbors=k, accumulation="reference"), X, y),
+        oracle.relieff_scores(X, y, n_neighbors=k))
+
+
+@pytest.mark.parametrize("seed", range(0, 40, 2))
+def test_small_sweep_bitexact(F, oracle, seed):
+    X, y, dl, k = make_case(seed)
+    for star in (False, True):
+        assert_bitexact(
+            fit_ref(F.MultiSURF(backend="gpu", use_star=star, discrete_limit=dl,
+                                accumulation="reference"), X, y),
+            oracle.multisurf_scores(X, y, use_star=star, discrete_limit=dl))
+    if X.shape[0] > k:
+        assert_bitexact(
+            fit_ref(F.ReliefF(backend="gpu", n_neighbors=k, discrete_limit=dl,
+                              accumulation="reference"), X, y),
+            oracle.relieff_scores(X, y, n_neighbors=k, discrete_limit=dl))
+
+
+@pytest.mark.parametrize("kind", ["exp4z", "pareto1", "outlier"])
+def test_verdict_cases_bitexact(F, oracle, kind):
+    X, y = verdict_case(kind, 2500, 600)
+    for star in (False, True):
+        ref = oracle.multisurf_scores(X, y, use_star=star)
+        got = fit_ref(F.MultiSURF(backend="gpu", use_star=star, accumulation="reference"), X, y)
+        assert_bitexact(got, ref)
+        assert np.array_equal(np.argsort(got)[::-1][:10], np.argsort(ref)[::-1][:10])
+
+
+def test_relieff_panels_chain_the_column_sums(F, oracle, monkeypatch):
+    """A one-shot ReliefF scored in row panels (FS_ROW_PANEL forces their
+    height) continues one float32 column sum across the panels."""
+    monkeypatch.setenv("FS_ROW_PANEL", "256")
+    rng = np.random.default_rng(21)
+    X = np.exp(2.0 * rng.standard_normal((1000, 80)))
+    y = rng.integers(0, 3, 1000)
+    assert_bitexact(
+        fit_ref(F.ReliefF(backend="gpu", n_neighbors=7, accumulation="reference"), X, y),
+        oracle.relieff_scores(X, y, n_neighbors=7))
+
+
+def test_rows_slice_is_the_oracle_slice(F, oracle):
+    from fastselect_amd import _lib
+    from fastselect_amd.parallel import prepare_inputs
+    X, y = verdict_case("exp4z", 1500, 300, seed=3)
+    x, yv, recip, isd = prepare_inputs(X, y, backend="gpu")
+    with _lib.accumulation("reference"):
+        sums = _lib.multisurf_score("gpu", x, yv, recip, None, False, isd, rows=(300, 1100))
+    assert_bitexact((sums / X.shape[0]).astype(np.float32),
+                    oracle.multisurf_scores(X, y, i_range=(300, 1100)))
+
+
+def test_forced_tile_shards_bitexact(F, oracle, monkeypatch):
+    """n beyond HBM: the one-shot call in V tile shards writes every shard's
+    decisions into the masks before the chains run."""
+    monkeypatch.setenv("FS_SHARDS", "3")
+    X, y = verdict_case("pareto1", 1300, 200, seed=8)
+    for star in (False, True):
+        assert_bitexact(
+            fit_ref(F.MultiSURF(backend="gpu", use_star=star, accumulation="reference"), X, y),
+            oracle.multisurf_scores(X, y, use_star=star))
+
+
+def test_turf_resident_bitexact(F, oracle):
+    from test_refacc import turf_oracle
+    X, y = verdict_case("exp4z", 1200, 120, seed=6)
+    cases = ((F.MultiSURF(backend="gpu", accumulation="reference"),
+              lambda Z: oracle.multisurf_scores(Z, y)),
+             (F.ReliefF(backend="gpu", n_neighbors=5, accumulation="reference"),
+              lambda Z: oracle.relieff_scores(Z, y, n_neighbors=5)))
+    for base, score in cases:
+        t = F.TuRF(base, n_features_to_select=12, pct_remove=0.3).fit(X, y)
+        first, top = turf_oracle(score, X, 12, 0.3)
+        assert_bitexact(t.feature_importances_, first)
+        assert np.array_equal(t.top_features_, top)
+
+
+# ---- BASELINE configurations at full size --------------------------------------------
+from test_gpu_baseline import _fixture, _inputs  # noqa: E402
+
+
+@pytest.mark.parametrize("name,algo,kw", [
+    ("cfg2_multisurf", "multisurf", {}),
+    ("cfg3_relieff_k10", "relieff", {"n_neighbors": 10}),
+    ("cfg3_relieff_k10_3class", "relieff", {"n_neighbors": 10}),
+    ("cfg5_multisurfstar", "multisurf", {"use_star": True}),
+    ("cfg4_multisurf", "multisurf", {}),
+])
+def test_fullsize_bitexact(F, name, algo, kw):
+    """The reference's scores bit for bit at the BASELINE sizes, cfg4 (the
+    north star, 20000 x 20000) included."""
+    fx = _fixture(name)
+    X, y = _inputs(fx)
+    cls = F.MultiSURF if algo == "multisurf" else F.ReliefF
+    est = cls(backend="gpu", accumulation="reference", n_features_to_select=10, **kw).fit(X, y)
+    assert est.effective_backend_ == "gpu"
+    assert_bitexact(est.feature_importances_, fx["scores"])
