@@ -45,7 +45,7 @@ EXPORTED = (
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_decision_guard", "fs_plan_set_rows",
     "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_calibration_ex", "fs_plan_weighted_pairs", "fs_plan_kernel_ms",
     "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
-    "fs_surf_score_devices", "fs_set_accumulation", "fs_get_accumulation",
+    "fs_surf_score_devices", "fs_set_accumulation", "fs_get_accumulation", "fs_test_hook",
 )
 
 
@@ -145,6 +145,8 @@ def _load() -> ctypes.CDLL:
     lib.fs_set_accumulation.restype = _int
     lib.fs_get_accumulation.argtypes = []
     lib.fs_get_accumulation.restype = _int
+    lib.fs_test_hook.argtypes = [ctypes.c_char_p, _i64]
+    lib.fs_test_hook.restype = _int
     for name in ("fs_column_stats", "fs_multisurf_score", "fs_multisurf_score_rows",
                  "fs_plan_set_rows", "fs_relieff_score", "fs_surf_score",
                  "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create",
@@ -344,6 +346,24 @@ def accumulation(mode: str = "fast"):
         yield
     finally:
         _lib.fs_set_accumulation(prev.value, None)
+
+
+def set_test_hook(name: str, value: int = 1) -> None:
+    """TEST-ONLY (fs_test_hook): override one internal choice of the library
+    process-wide; ``set_test_hook("reset")`` restores every default."""
+    check(_lib.fs_test_hook(name.encode(), int(value)))
+
+
+@contextlib.contextmanager
+def test_hooks(**hooks):
+    """TEST-ONLY: the given fs_test_hook overrides inside the block, every
+    default restored afterwards."""
+    try:
+        for k, v in hooks.items():
+            set_test_hook(k, int(v))
+        yield
+    finally:
+        set_test_hook("reset")
 
 
 def _p(a: np.ndarray, t):

@@ -20,6 +20,11 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 static thread_local int g_accum = FS_ACCUM_FAST;
 int accumulation_mode() { return g_accum; }
 
+TestHooks& test_hooks() {
+  static TestHooks h;
+  return h;
+}
+
 bool trace_on() {
   static const bool on = std::getenv("FS_TRACE") != nullptr;
   return on;
@@ -122,6 +127,32 @@ int fs_set_accumulation(int mode, int* previous) {
 }
 
 int fs_get_accumulation(void) { return g_accum; }
+
+int fs_test_hook(const char* name, int64_t value) {
+  if (!name) {
+    set_error("fs_test_hook: name is NULL");
+    return FS_EINVAL;
+  }
+  TestHooks& h = test_hooks();
+  const std::string k(name);
+  if (k == "reset") h = TestHooks();
+  else if (k == "ksplit") h.ksplit = value;
+  else if (k == "q16_guard_off") h.q16_guard_off = value;
+  else if (k == "thr_exact_all") h.thr_exact_all = value;
+  else if (k == "exact_gather") h.exact_gather = value;
+  else if (k == "row_panel") h.row_panel = value;
+  else if (k == "rf_xlds") h.rf_xlds = value;
+  else if (k == "rf_fcap") h.rf_fcap = value;
+  else if (k == "ties_1w") h.ties_1w = value;
+  else if (k == "ties_coop") h.ties_coop = value;
+  else if (k == "colsort_bins12") h.colsort_bins12 = value;
+  else if (k == "colsort_global") h.colsort_global = value;
+  else {
+    set_error("fs_test_hook: unknown hook '" + k + "'");
+    return FS_EINVAL;
+  }
+  return FS_OK;
+}
 
 int fs_multisurf_last_guard(double* risk_out, int* rerun_out) {
   return gpu::multisurf_last_guard(risk_out, rerun_out);

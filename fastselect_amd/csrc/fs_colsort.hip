@@ -516,21 +516,14 @@ size_t batch_bytes(int64_t n, int64_t nb) {
 }  // namespace
 
 int colsort_bin_bits(int64_t n) {
-  static const bool force12 = [] {
-    const char* e = std::getenv("FS_COLSORT_BINS12");
-    return e && *e == '1';
-  }();
+  const bool force12 = test_hooks().colsort_bins12 != 0;
   return !force12 && n > 12 * (int64_t)kCsThreads && n <= 20 * (int64_t)kCsThreads ? 13 : 12;
 }
 
-// FS_COLSORT_GLOBAL=1 (tests): the large-n route at any n, so that it is
+// The colsort_global test hook: the large-n route at any n, so that it is
 // checked against the LDS route and the CPU backend on small inputs
 bool colsort_lds(int64_t n) {
-  static const bool force_global = [] {
-    const char* e = std::getenv("FS_COLSORT_GLOBAL");
-    return e && *e == '1';
-  }();
-  return !force_global && n <= (int64_t)kCsThreads * kCsMaxIpt;
+  return !test_hooks().colsort_global && n <= (int64_t)kCsThreads * kCsMaxIpt;
 }
 
 size_t colsort_scratch_bytes(int64_t n, int64_t ncols) {

@@ -182,7 +182,7 @@ static void mean_correction(const Prepared& P, const std::vector<uint32_t>& xq,
   const int64_t n = P.n;
   const int s = colsort_key_shift(P.qmax);
   // the GPU's route for this n: binned columns (k_colsort) up to 24576
-  // samples, beyond that (or under FS_COLSORT_GLOBAL) every column sorted
+  // samples, beyond that (or under the colsort_global test hook) every column sorted
   // whole by the device segmented sort -- position terms, ties by index
   const bool binned = gpu::colsort_lds(n);
   const int bins = 1 << gpu::colsort_bin_bits(n), shift = 32 - gpu::colsort_bin_bits(n);
@@ -315,13 +315,13 @@ static int64_t refine_pairs(const Prepared& P, const void* x, int x_is_f64, int 
 
 // exact_thresholds (fs_gpu.hip): thresholds from exact distances for the
 // rows a refined pair lies within thr_tol of, when at most exact_thr_rows(n, p)
-// (every row under the FS_THR_EXACT_ALL test hook).
+// (every row under the thr_exact_all test hook, fs_test_hook).
 static void exact_thresholds(const Prepared& P, const void* x, int n_jobs, const CpuState& S,
                              const std::vector<std::pair<int32_t, int32_t>>& refined,
                              double thr_tol, std::vector<double>& thr) {
   const int64_t n = P.n;
   std::vector<int32_t> rows;
-  if (std::getenv("FS_THR_EXACT_ALL")) {
+  if (test_hooks().thr_exact_all) {
     for (int64_t i = 0; i < n; i++) rows.push_back((int32_t)i);
   } else {
     std::vector<uint8_t> unc((size_t)n, 0);

@@ -3379,7 +3379,7 @@ struct Plan {
   int32_t* urows = nullptr;     // [n_pad + 1] flagged rows in index order, then their count
   double2* uparts = nullptr;    // [thr_rows][nchunk] exact row-moment partials
   size_t uparts_cap = 0;        // double2 slots of uparts
-  int thr_rows = kExactThrRows; // rows fixed at most: exact_thr_rows(n) (FS_THR_EXACT_ALL: all, tests)
+  int thr_rows = kExactThrRows; // rows fixed at most: exact_thr_rows(n) (thr_exact_all test hook: all)
   bool thr_all = false;
   int32_t n_exact_thr = 0;      // rows whose threshold the last select recomputed (-1: too many)
   // ambiguous-pair refinement
@@ -3953,7 +3953,7 @@ static int choose_sparse(const Plan* g, const Prepared& P) {
 //  * 16-bit operands are given up (coherence guard) when the measured rms
 //    error exceeds kCoherence x the model's standard deviation: with errors
 //    that large the quantised threshold mu - sigma/2 drifts as well, and the
-//    32-bit operands make every error 256x smaller.  FS_Q16_GUARD=0 keeps them.
+//    32-bit operands make every error 256x smaller.  The q16_guard_off test hook keeps them.
 //  * The band becomes max(model, 3 max|err| + rms/2): three times the largest
 //    sampled error covers the distance error (the model's 12 sigma is ~3.3x
 //    the expected maximum of 4096 Gaussian samples), and rms/2 bounds the
@@ -4037,8 +4037,7 @@ static int calibrate_band(Plan* g) {
   g->cal32[0] = rms[1];
   g->cal32[1] = mx[1];
   const double sigma = g->calib[3];
-  const char* guard = std::getenv("FS_Q16_GUARD");
-  if (Q.q16 && rms[0] > kCoherence * sigma && !(guard && *guard == '0')) {
+  if (Q.q16 && rms[0] > kCoherence * sigma && !test_hooks().q16_guard_off) {
     g->use_q16 = 0;
     g->calib[5] = 1.0;
     if (set_integer_scale(Q, 0)) return FS_EINVAL;
@@ -4271,11 +4270,10 @@ static int run_colsort(Plan* g, int64_t c_lo, int64_t c_hi, hipStream_t s) {
 // all continuous columns on the 16-bit operands; a row beyond 12 standard
 // deviations turns the 16-bit operands off (32-bit: 256x smaller errors).
 // Every rank computes the same full correction, so every rank decides alike.
-// ~5 ms per fit at cfg4, none per step; FS_Q16_GUARD=0 disables it.
+// ~5 ms per fit at cfg4, none per step; the q16_guard_off test hook disables it.
 static int row_guard(Plan* g) {
   Prepared& Q = g->P;
-  const char* guard = std::getenv("FS_Q16_GUARD");
-  if (!Q.q16 || Q.pc == 0 || Q.n < 2 || Q.algo == ALGO_SURF || (guard && *guard == '0'))
+  if (!Q.q16 || Q.pc == 0 || Q.n < 2 || Q.algo == ALGO_SURF || test_hooks().q16_guard_off)
     return FS_OK;
   // a plan over every continuous column (one rank, one shard) keeps the
   // guard's work for its first pass 1: operands, terms and the correction
@@ -4517,8 +4515,7 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
   const int64_t rows_q = (g->use_q16 ? Q.PC / 2 : Q.PC) + Q.PD;
   g->ksplit = choose_ksplit(g->n_tiles, g->device, (int)(rows_q / kBKQ),
                             (g->use_q16 ? Q.pc / 2 : Q.pc) + Q.pd);
-  if (const char* e = std::getenv("FS_KSPLIT"))  // A/B and tests
-    if (std::atoi(e) >= 1) g->ksplit = std::min(16, std::atoi(e));
+  if (test_hooks().ksplit >= 1) g->ksplit = (int)std::min<int64_t>(16, test_hooks().ksplit);
   if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
   // ReliefF stores float32 keys (Dk), formed in k_dist's epilogue from whole
   // tiles: no K-split (partial sums cannot be keyed before they are added)
@@ -4664,7 +4661,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   if (Q.algo == ALGO_MULTISURF) {
     // test hook: every row's threshold from exact distances (the machinery
     // of exact_thresholds checked on all rows against the oracle's)
-    g->thr_all = std::getenv("FS_THR_EXACT_ALL") != nullptr;
+    g->thr_all = test_hooks().thr_exact_all != 0;
     // thr_rows and uparts: size_exact_rows (plan_layout, per feature layout)
     g->thr_rows = (int)(g->thr_all ? Q.n : exact_thr_rows(Q.n, Q.pc + Q.pd));
     if ((rc = dalloc(g, &g->unc, Q.n_pad)) || (rc = dalloc(g, &g->urows, Q.n_pad + 1)))
@@ -4840,7 +4837,7 @@ static int refine_pairs(Plan* g, int algo, double delta, double thr_tol = 0.0,
   if (g->n_refined == 0) return FS_OK;
   FS_TRY(sort_pair_list(g, g->n_refined));
   const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
-  if (g->rows_direct && !std::getenv("FS_EXACT_GATHER"))
+  if (g->rows_direct && !test_hooks().exact_gather)
     k_exact_pairs_rows<<<grid, 256, 0, g->stream>>>((const float*)g->x, Q.p_in, g->scl32, Q.SC,
                                                     g->list, g->list_count, g->list_cap, Q.n_pad,
                                                     g->tw, g->win, g->D, g->thr, thr_tol, unc);
@@ -5433,10 +5430,10 @@ static int plan_score_surf(Plan* g, double* sums_dev) {
 // device memory are scored in panels of whole 128-sample blocks, one plan
 // each, and their sums added -- the reference streams each focal sample's
 // distance row the same way (ReliefF.py:143-157, SURF.py:139-163).
-// FS_ROW_PANEL=<rows> forces the panel height (tests).
+// The row_panel test hook forces the panel height.
 static int64_t row_panel_rows(const Prepared& P, int device, int64_t rows) {
-  if (const char* e = std::getenv("FS_ROW_PANEL"))
-    if (std::atoll(e) >= 1) return std::max<int64_t>(kTile, std::atoll(e) / kTile * kTile);
+  if (const int64_t e = test_hooks().row_panel; e >= 1)
+    return std::max<int64_t>(kTile, e / kTile * kTile);
   size_t free_b = 0, total_b = 0;
   if (hipSetDevice(device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
     (void)hipGetLastError();
@@ -5549,8 +5546,7 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   const size_t lds_cap = stage ? kSelLds : 40 * 1024;
   const size_t lds_left = lds_cap > shsel + 16 ? lds_cap - 16 - shsel : 0;
   if (Q.pc > 0 && lds_left / 4 >= (size_t)Q.pc * 4) xlds = (int)(lds_left / 4);
-  if (const char* e = std::getenv("FS_RF_XLDS")) {  // A/B, tests: a cap in floats
-    const long v = std::atol(e);
+  if (const int64_t v = test_hooks().rf_xlds; v >= 0) {  // tests: a cap in floats
     if (v < xlds) xlds = v >= 4 * Q.pc ? (int)v : 0;
   }
   if (xlds) shsel += 16 + (size_t)xlds * 4;
@@ -5571,10 +5567,10 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   // Continuous features only need the exact keys (discrete distances are
   // exact integers already).
   const float* xk = Q.pc > 0 ? (const float*)g->x : nullptr;
-  // candidates listed in LDS per row (above: the general route); FS_RF_FCAP
-  // lowers it (0 forces the general route: tests)
+  // candidates listed in LDS per row (above: the general route); the rf_fcap
+  // test hook lowers it (0 forces the general route)
   int fcap = 256;
-  if (const char* e = std::getenv("FS_RF_FCAP")) fcap = std::max(0, std::atoi(e));
+  if (test_hooks().rf_fcap >= 0) fcap = (int)std::min<int64_t>(256, test_hooks().rf_fcap);
   FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
 #ifdef FS_RF_PROF
   {
@@ -5637,10 +5633,10 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   g->n_tie_rows = (int64_t)tie_rows.size();
   if (tie_rows.empty()) return FS_OK;
   // n <= kTieMwMaxN: 16 waves per row, the row in LDS (6 B per sample)
-  const bool mw = n <= kTieMwMaxN && !std::getenv("FS_TIES_1W");  // FS_TIES_1W: A/B
+  const bool mw = n <= kTieMwMaxN && !test_hooks().ties_1w;  // ties_1w: tests
   const size_t mw_lds = ((size_t)n * 6 + 15) & ~(size_t)15;
-  int coop_min = 2048;  // ranges the whole workgroup partitions (FS_TIES_COOP: A/B)
-  if (const char* e = std::getenv("FS_TIES_COOP")) coop_min = std::max(16, std::atoi(e));
+  int coop_min = 2048;  // ranges the whole workgroup partitions (ties_coop: tests)
+  if (test_hooks().ties_coop > 0) coop_min = (int)std::max<int64_t>(16, test_hooks().ties_coop);
   // per-row scratch: exact keys (unless all-discrete under mw) and the
   // one-wave replay's permutation; batches bounded to ~512 MB of it
   const bool need_keys = !(mw && Q.pc == 0);

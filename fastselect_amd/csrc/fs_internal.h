@@ -114,6 +114,24 @@ struct Prepared {
 // fs_set_accumulation): FS_ACCUM_FAST (0) or FS_ACCUM_REFERENCE (1).
 int accumulation_mode();
 
+// Overrides of internal choices for the tests (fs_test_hook, the one
+// test-only entry point; every field 0 = the product's own choice).  No
+// environment variable selects a kernel or a route.
+struct TestHooks {
+  int64_t ksplit = 0;          // pass-1 K-split parts of every tile (choose_ksplit)
+  int64_t q16_guard_off = 0;   // 1: no coherence / row guard on 16-bit operands
+  int64_t thr_exact_all = 0;   // 1: every MultiSURF row's threshold exact (exact_thresholds)
+  int64_t exact_gather = 0;    // 1: k_exact_pairs (column gather) for every layout
+  int64_t row_panel = 0;       // ReliefF / SURF one-shot row-panel height
+  int64_t rf_xlds = -1;        // k_rf_select's LDS x cap in floats (-1: automatic)
+  int64_t rf_fcap = -1;        // candidates listed per row in LDS (-1: 256)
+  int64_t ties_1w = 0;         // 1: the one-wave quicksort replay
+  int64_t ties_coop = 0;       // smallest range the tie workgroup partitions (0: 2048)
+  int64_t colsort_bins12 = 0;  // 1: 4096 bins at every n
+  int64_t colsort_global = 0;  // 1: the large-n (device sort) route at every n
+};
+TestHooks& test_hooks();
+
 // Build the permutation, label codes, discrete tables and integer scale.
 // x is row-major [n][p_in], float32 (x_is_f64 == 0) or float64.
 // With device_ranges != 0 the continuous column minima/maxima (and, for a
@@ -433,7 +451,7 @@ bool colsort_lds(int64_t n);
 // Bits of the key the LDS route bins on: 13 (8192 bins) where the
 // workgroup's LDS holds them next to the column's entries (12288 < n <=
 // 20480: half the within-bin work of 4096 bins at cfg4's n = 20000), 12
-// elsewhere; FS_COLSORT_BINS12=1 (timing A/B) keeps 12 everywhere.  Both
+// elsewhere; the colsort_bins12 test hook keeps 12 everywhere.  Both
 // backends bin alike, so their terms stay identical.
 int colsort_bin_bits(int64_t n);
 size_t colsort_scratch_bytes(int64_t n, int64_t ncols);

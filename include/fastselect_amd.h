@@ -92,6 +92,18 @@ extern "C" {
 FS_API int fs_set_accumulation(int mode, int* previous);
 FS_API int fs_get_accumulation(void);
 
+/*
+ * TEST-ONLY: override one internal choice of the library for the calls that
+ * follow, process-wide (tests/ uses it to reach routes the automatic choices
+ * take only at other sizes; no product code calls it).  name = "reset"
+ * restores every default; the others are listed in INTEGRATION.md §4
+ * ("ksplit", "q16_guard_off", "thr_exact_all", "exact_gather", "row_panel",
+ * "rf_xlds", "rf_fcap", "ties_1w", "ties_coop", "colsort_bins12",
+ * "colsort_global").  FS_EINVAL for an unknown name.  Not thread-safe
+ * against concurrent scoring calls.
+ */
+FS_API int fs_test_hook(const char* name, int64_t value);
+
 /* Library identity and device discovery. */
 FS_API const char* fs_version(void);
 FS_API const char* fs_last_error(void);

@@ -80,3 +80,13 @@ def assert_parity_attributed(a, ref, exact, counts=None, ref_counts=None, tol=1e
     ta = set(np.argsort(a)[::-1][:k].tolist())
     tr = set(np.argsort(ref)[::-1][:k].tolist())
     assert ta == tr, f"top-{k} differ: {sorted(ta ^ tr)} ({summary(a, ref)})"
+
+
+@pytest.fixture
+def hooks():
+    """fs_test_hook overrides for one test (``hooks("ksplit", 4)``), reset
+    afterwards (the library reads no environment variable for these)."""
+    from fastselect_amd import _lib
+    _lib.set_test_hook("reset")
+    yield _lib.set_test_hook
+    _lib.set_test_hook("reset")

@@ -9,7 +9,7 @@ row of 16384 on the uniform-noise family, tests/test_gpu_families.py).  The
 rows whose refined pairs lie that close now get their threshold from exact
 distances to every other sample (MultiSURF.py:174-196).
 
-FS_THR_EXACT_ALL (test hook) takes every row through that route, so the
+The thr_exact_all test hook (fs_test_hook) takes every row through that route, so the
 decisions must then be the oracle's (oracle_multisurf_decisions) row by row,
 on both backends and on 16-bit operands too; the default route must give
 the oracle's decisions on the same data.
@@ -53,11 +53,8 @@ def _step(X, y, backend):
     return s, counts
 
 
-def _check(X, y, backend, monkeypatch, all_rows):
-    if all_rows:
-        monkeypatch.setenv("FS_THR_EXACT_ALL", "1")
-    else:
-        monkeypatch.delenv("FS_THR_EXACT_ALL", raising=False)
+def _check(X, y, backend, hooks, all_rows):
+    hooks("thr_exact_all", 1 if all_rows else 0)
     s, counts = _step(X, y, backend)
     _, ref_counts = O.multisurf_decisions(X, y)
     flipped = np.flatnonzero(np.any(counts != ref_counts, axis=1))
@@ -71,26 +68,26 @@ CASES = [("classification", 400, 300, 0), ("lognormal", 400, 200, 1), ("mixed", 
 
 @pytest.mark.parametrize("kind,n,p,seed", CASES)
 @pytest.mark.parametrize("all_rows", [True, False])
-def test_cpu_backend_decisions(kind, n, p, seed, all_rows, monkeypatch):
+def test_cpu_backend_decisions(kind, n, p, seed, all_rows, hooks):
     X, y = _data(kind, n, p, seed)
-    _check(X, y, "cpu", monkeypatch, all_rows)
+    _check(X, y, "cpu", hooks, all_rows)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind,n,p,seed", CASES)
 @pytest.mark.parametrize("all_rows", [True, False])
-def test_gpu_decisions(kind, n, p, seed, all_rows, monkeypatch):
+def test_gpu_decisions(kind, n, p, seed, all_rows, hooks):
     X, y = _data(kind, n, p, seed)
-    _check(X, y, "gpu", monkeypatch, all_rows)
+    _check(X, y, "gpu", hooks, all_rows)
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["uniform", "classification"])
-def test_gpu_16bit_operands_exact_thresholds_everywhere(kind, monkeypatch):
+def test_gpu_16bit_operands_exact_thresholds_everywhere(kind, monkeypatch, hooks):
     """16-bit pass-1 operands (thresholds 256x coarser than on 32-bit ones):
     with every threshold exact, the refinement band alone must bring each
     decision to the reference's."""
     monkeypatch.setenv("FS_Q16", "1")
-    monkeypatch.setenv("FS_Q16_GUARD", "0")
+    hooks("q16_guard_off", 1)
     X, y = _data(kind, 1200, 400, 5)
-    _check(X, y, "gpu", monkeypatch, True)
+    _check(X, y, "gpu", hooks, True)

@@ -195,10 +195,10 @@ def test_relieff_unstaged_rows(oracle):
 @pytest.mark.parametrize("n", [2500, 33000])
 def test_relieff_exact_keys_lds_and_global(n, monkeypatch):
     """k_rf_select's in-kernel exact keys: candidate rows gathered into LDS
-    in batches (default; one row per batch with FS_RF_XLDS=4*pc) or summed
-    straight from HBM (FS_RF_XLDS=0), and the
+    in batches (default; one row per batch with the rf_xlds hook at 4*pc) or summed
+    straight from HBM (rf_xlds = 0), and the
     exact k-th key comes from the row's candidate list (default) or from a
-    second selection over the whole row (FS_RF_FCAP=0, the route of rows with
+    second selection over the whole row (rf_fcap = 0, the route of rows with
     over 256 candidates): the keys are the same float32 numbers and the
     selections agree, so the scores are bit-identical.  Mixed data (a
     discrete block), 1100 continuous columns (not a multiple of the unrolled
@@ -211,14 +211,12 @@ def test_relieff_exact_keys_lds_and_global(n, monkeypatch):
     X[:, -100 if n < 10000 else -10:] = rng.integers(0, 4, size=(n, 100 if n < 10000 else 10))
     out = {}
     pc = 1100 if n < 10000 else 70
-    for mode, env in (("default", {}), ("hbm", {"FS_RF_XLDS": "0"}),
-                      ("batch1", {"FS_RF_XLDS": str(4 * pc)}),
-                      ("general", {"FS_RF_FCAP": "0"})):
-        for key, val in env.items():
-            monkeypatch.setenv(key, val)
-        out[mode] = _fit(ReliefF, X, y, n_neighbors=7)
-        for key in env:
-            monkeypatch.delenv(key)
+    from fastselect_amd import _lib
+    for mode, hk in (("default", {}), ("hbm", {"rf_xlds": 0}),
+                     ("batch1", {"rf_xlds": 4 * pc}),
+                     ("general", {"rf_fcap": 0})):
+        with _lib.test_hooks(**hk):
+            out[mode] = _fit(ReliefF, X, y, n_neighbors=7)
     for mode in ("hbm", "batch1", "general"):
         assert np.array_equal(out["default"], out[mode]), mode
 
@@ -237,8 +235,8 @@ def test_relieff_ties_large_rows(oracle):
 def test_relieff_ties_multiwave_matches_single_wave(monkeypatch):
     """k_rf_ties_mw (whole-workgroup partitions of the ranges of >= 2048
     samples, then 16 waves taking the smaller ranges from a shared queue)
-    against the one-wave replay (FS_TIES_1W) and against workgroup
-    partitions down to 16 samples (FS_TIES_COOP=16): every row of
+    against the one-wave replay (ties_1w test hook) and against workgroup
+    partitions down to 16 samples (ties_coop=16): every row of
     all-discrete data is a tie row; the orders, so the scores, must be
     bit-identical.  Mixed data (exact keys from k_rf_exact_rows) too."""
     from fastselect_amd import ReliefF
@@ -249,12 +247,10 @@ def test_relieff_ties_multiwave_matches_single_wave(monkeypatch):
     y = rng.integers(0, 3, 4000)
     for data in (X, X2):
         out = []
-        for env in ({}, {"FS_TIES_1W": "1"}, {"FS_TIES_COOP": "16"}):
-            for key, val in env.items():
-                monkeypatch.setenv(key, val)
-            out.append(_fit(ReliefF, data, y, n_neighbors=10))
-            for key in env:
-                monkeypatch.delenv(key)
+        from fastselect_amd import _lib
+        for hk in ({}, {"ties_1w": 1}, {"ties_coop": 16}):
+            with _lib.test_hooks(**hk):
+                out.append(_fit(ReliefF, data, y, n_neighbors=10))
         assert np.array_equal(out[0], out[1])
         assert np.array_equal(out[0], out[2])
 
@@ -572,10 +568,10 @@ def test_sparse_pass2_matches_dense(monkeypatch, algo, star):
     assert_parity(out["1"], ref, TOL, k=10)
 
 
-def test_exact_pairs_row_reads_match_gather(monkeypatch):
+def test_exact_pairs_row_reads_match_gather(monkeypatch, hooks):
     """k_exact_pairs_rows (float4 reads of whole rows, all-continuous
     float32 data in input order) against the column-indexed gather
-    (FS_EXACT_GATHER forces it): the 16-bit pass 1 (FS_Q16=1) refines
+    (the exact_gather test hook forces it): the 16-bit pass 1 (FS_Q16=1) refines
     hundreds of pairs here; 1500 features is not a multiple of 256.
     Both refine the same pairs, so the scores agree to f64 summation order."""
     from fastselect_amd.parallel import ShardedMultiSURF
@@ -587,7 +583,7 @@ def test_exact_pairs_row_reads_match_gather(monkeypatch):
     out = {}
     for mode in ("rows", "gather"):
         if mode == "gather":
-            monkeypatch.setenv("FS_EXACT_GATHER", "1")
+            hooks("exact_gather", 1)
         job = ShardedMultiSURF(x, y, recip, np.zeros(x.shape[1], bool), backend="gpu", device=0)
         out[mode] = job.step().cpu().numpy()
         refined = job.info()[2]

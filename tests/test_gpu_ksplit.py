@@ -1,7 +1,7 @@
 """Pass-1 K-split (k_dist + k_dist_merge): tiles are split over their
 feature range and the integer partial blocks added afterwards.  Distances are
 exact integers, so every split gives bit-identical scores; forced here
-(FS_KSPLIT=s splits every tile into s parts, 1 disables it) against the
+(the ksplit test hook: s splits every tile into s parts, 1 disables it) against the
 unsplit job, for the tiled layout (MultiSURF, MultiSURF*) and the full layout
 (ReliefF, MultiSURF's focal-row slices), with continuous and discrete chunks
 in one split range.  (The stream-K variant, measured no faster, was retired
@@ -23,12 +23,10 @@ def _data(n=1500, p=400, n_disc=40, seed=5):
 
 
 def _scores(monkeypatch, split, fn):
-    """split: None (automatic) or an int (FS_KSPLIT)."""
-    if split is None:
-        monkeypatch.delenv("FS_KSPLIT", raising=False)
-    else:
-        monkeypatch.setenv("FS_KSPLIT", str(split))
-    return fn()
+    """split: None (automatic) or an int (the ksplit test hook)."""
+    from fastselect_amd import _lib
+    with _lib.test_hooks(ksplit=0 if split is None else split):
+        return fn()
 
 
 @pytest.mark.parametrize("use_star", [False, True])

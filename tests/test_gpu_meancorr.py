@@ -171,15 +171,16 @@ def test_plan_path_runs_the_decision_check():
 
 
 def test_large_n_route_matches_cpu_at_small_n():
-    """FS_COLSORT_GLOBAL=1 (read once per process, so in a child process)
-    sends every column through the large-n route (device segmented sort +
-    k_colsort_scan); its corrections equal the CPU backend's exactly."""
+    """The colsort_global test hook sends every column through the large-n
+    route (device segmented sort + k_colsort_scan); its corrections equal
+    the CPU backend's exactly (a child process, as before the hook)."""
     import subprocess
     import sys
     code = (
         "import numpy as np, sys; sys.path[:0] = [%r, %r]\n"
         "from test_meancorr import lognormal, gaussian\n"
-        "from fastselect_amd import parallel\n"
+        "from fastselect_amd import parallel, _lib\n"
+        "_lib.set_test_hook('colsort_global', 1)\n"
         "for X, y in (lognormal(3000, 64, seed=7), gaussian(2000, 100)):\n"
         "    out = []\n"
         "    for be in ('cpu', 'gpu'):\n"
@@ -189,7 +190,6 @@ def test_large_n_route_matches_cpu_at_small_n():
         "    d = np.max(np.abs(out[0] - out[1]) / np.maximum(np.abs(out[0]), 1.0))\n"
         "    assert d < 1e-12, d\n"
         "print('ok')\n" % (os.path.dirname(HERE), HERE))
-    env = dict(os.environ, FS_COLSORT_GLOBAL="1")
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True,
                        timeout=600)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr

@@ -101,10 +101,10 @@ def test_verdict_cases_bitexact(F, oracle, kind):
         assert np.array_equal(np.argsort(got)[::-1][:10], np.argsort(ref)[::-1][:10])
 
 
-def test_relieff_panels_chain_the_column_sums(F, oracle, monkeypatch):
-    """A one-shot ReliefF scored in row panels (FS_ROW_PANEL forces their
-    height) continues one float32 column sum across the panels."""
-    monkeypatch.setenv("FS_ROW_PANEL", "256")
+def test_relieff_panels_chain_the_column_sums(F, oracle, hooks):
+    """A one-shot ReliefF scored in row panels (the row_panel test hook
+    forces their height) continues one float32 column sum across the panels."""
+    hooks("row_panel", 256)
     rng = np.random.default_rng(21)
     X = np.exp(2.0 * rng.standard_normal((1000, 80)))
     y = rng.integers(0, 3, 1000)

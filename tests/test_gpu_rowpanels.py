@@ -4,7 +4,7 @@ ranges scored in row panels.
 A ReliefF / SURF plan keeps the distance rows of its own 128-sample blocks
 (fs_gpu.hip d_row_in: a row-sharded rank holds 1/N of D instead of all of
 it), and a one-shot call whose rows exceed the device is scored in panels of
-whole blocks (row_panel_rows; FS_ROW_PANEL forces the height here) -- the
+whole blocks (row_panel_rows; the row_panel test hook forces the height here) -- the
 reference streams each focal sample's distance row (ReliefF.py:143-157,
 SURF.py:139-163).  Panels and slices must reproduce the one-panel scores
 (ReliefF: float64 sums in another order, <= 1e-9 scale-relative; SURF:
@@ -30,22 +30,22 @@ def F():
 
 
 @pytest.mark.parametrize("panel", ["128", "384", "1000"])
-def test_relieff_row_panels(F, oracle, monkeypatch, panel):
+def test_relieff_row_panels(F, oracle, hooks, panel):
     X, y = make_classification(n_samples=1100, n_features=300, n_informative=10, n_redundant=20,
                                n_classes=3, random_state=21)
     one = F.ReliefF(backend="gpu", n_neighbors=5).fit(X, y).feature_importances_
-    monkeypatch.setenv("FS_ROW_PANEL", panel)
+    hooks("row_panel", int(panel))
     s = F.ReliefF(backend="gpu", n_neighbors=5).fit(X, y).feature_importances_
     assert scale_rel_err(s, one) <= 1e-9
     assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=5), 1e-5)
 
 
 @pytest.mark.parametrize("star", [False, True])
-def test_surf_row_panels(F, oracle, monkeypatch, star):
+def test_surf_row_panels(F, oracle, hooks, star):
     X, y = make_classification(n_samples=900, n_features=400, n_informative=10, n_redundant=20,
                                random_state=22)
     one = F.SURF(backend="gpu", use_star=star).fit(X, y).feature_importances_
-    monkeypatch.setenv("FS_ROW_PANEL", "256")
+    hooks("row_panel", 256)
     s = F.SURF(backend="gpu", use_star=star).fit(X, y).feature_importances_
     # a panel is a row slice, which takes the sparse pass 2 where the whole
     # fit takes the dense one (choose_sparse): float32 partials in another
