@@ -231,6 +231,69 @@ def cpu_baseline(x, y, budget_s=25.0):
     return out
 
 
+GOLD = os.path.join(ROOT, "tests", "golden")
+# FMA-equivalent FLOPs per PFE of the reference-order chains (k_ms_chains):
+# v_sub_f32, v_mul_f32 |.| and v_add_f32, three full-rate issue slots
+FLOP_PER_PFE_CHAINS = 6
+
+
+def decisions_vs_fixture(counts, n, p, config):
+    """Rows whose near hit / near miss counts differ from the reference's
+    (the oracle's multisurf_decisions, committed as
+    tests/golden/fullsize_<config>_multisurf_decisions.npz by
+    tests/golden/make_fullsize.py --decisions), or None without a fixture
+    for this workload."""
+    path = os.path.join(GOLD, f"fullsize_{config}_multisurf_decisions.npz")
+    if not os.path.exists(path):
+        return None
+    d = np.load(path, allow_pickle=False)
+    if int(d["n"]) != n or int(d["p"]) != p:
+        return None
+    ref = d["counts"].astype(np.int64).reshape(-1, 2)
+    got = np.asarray(counts, dtype=np.float64).reshape(-1, 2).astype(np.int64)
+    bad = np.any(got != ref, axis=1)
+    return {"flipped_rows": int(bad.sum()), "rows": int(n),
+            "near_pairs_differing": int(np.abs(got - ref).sum()),
+            "fixture": os.path.relpath(path, ROOT)}
+
+
+def chain_entries(counts, y, star):
+    """Directed (focal, neighbour) entries the reference-order chains walk:
+    near hits + near misses, plus every far miss for MultiSURF*."""
+    c = np.asarray(counts, dtype=np.float64).reshape(-1, 2)
+    if not star:
+        return float(c.sum())
+    yv = np.asarray(y)
+    _, inv, cnt = np.unique(yv, return_inverse=True, return_counts=True)
+    misses = len(yv) - cnt[inv]
+    return float(c[:, 0].sum() + misses.sum())
+
+
+def reference_step(make_job, y, star, p, sync, steps=3):
+    """The same step in reference-order accumulation (bit-identical to the
+    oracle): ms per step and the chain kernel's rate."""
+    job = make_job()
+    try:
+        job.step()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            job.step()
+        sync()
+        ms = (time.perf_counter() - t0) / steps * 1e3
+        d_ms, c_ms = job.kernel_ms(0), job.kernel_ms(1)
+        pfe = chain_entries(job.counts.cpu().numpy(), y, star) * p
+        rate = pfe / (c_ms * 1e-3)
+        return {"ms_per_step": ms, "steps": steps,
+                "kernel_ms": {"k_dist": d_ms, "k_ms_chains": c_ms},
+                "chain_pfe_per_launch": pfe, "chain_pfe_per_s": rate,
+                "chain_valu_frac": FLOP_PER_PFE_CHAINS * rate / 1e12 / VALU_PEAK_TFLOPS,
+                "pass1_operands": "32-bit",
+                "parity": "bit-identical to the oracle (tests/test_gpu_refacc.py)"}
+    finally:
+        job.close()
+
+
 def fit_ms(X, y, star, repeats=5):
     """End-to-end ``MultiSURF(backend='gpu').fit`` (validation + float32
     cast, column statistics, H2D of X, scoring, top-k): median of `repeats`
@@ -296,8 +359,11 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
     barrier()
     sync()
     t0 = time.perf_counter()
-    plan = _lib.RowsPlan(args.backend, algo, xin, ye, recip, isd, rows=rows, device=local,
-                         stream=stream, **kw)
+    if algo != "relieff" and args.accumulation == "reference":
+        raise SystemExit("bench.py: reference-order accumulation is MultiSURF / ReliefF only")
+    with _lib.accumulation(args.accumulation):
+        plan = _lib.RowsPlan(args.backend, algo, xin, ye, recip, isd, rows=rows, device=local,
+                             stream=stream, **kw)
     sums = torch.zeros(p, dtype=torch.float64, device=tdev)
     sync()
     setup_ms = (time.perf_counter() - t0) * 1e3
@@ -365,6 +431,27 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
             roofline["peak_note"] = ("float64 vector peak (AMD MI355X figure, half the fp32 rate); "
                                      "2 v_add_f64 per PFE, each priced as one FMA")
     plan.close()
+    # ReliefF in reference order beside the default (N = 1): same plan type
+    refacc = None
+    if (on_gpu and world == 1 and algo == "relieff" and not args.no_ref
+            and args.accumulation == "fast"):
+        with _lib.accumulation("reference"):
+            rplan = _lib.RowsPlan(args.backend, algo, xin, ye, recip, isd, rows=rows,
+                                  device=local, stream=stream, **kw)
+        try:
+            rplan.score(sums.data_ptr())
+            sync()
+            ks = max(1, min(args.steps, 3))
+            t_r = time.perf_counter()
+            for _ in range(ks):
+                rplan.score(sums.data_ptr())
+            sync()
+            refacc = {"ms_per_step": (time.perf_counter() - t_r) / ks * 1e3, "steps": ks,
+                      "kernel_ms": {"k_dist": rplan.kernel_ms(0),
+                                    "selection_to_scores": rplan.kernel_ms(1)},
+                      "parity": "bit-identical to the oracle (tests/test_gpu_refacc.py)"}
+        finally:
+            rplan.close()
     out = None
     if rank == 0:
         name = "ReliefF k=%d" % cfg["k"] if algo == "relieff" else ("SURF*" if args.star else "SURF")
@@ -382,7 +469,10 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
                                       + (f", {'RCCL' if dist_backend == 'nccl' else dist_backend}"
                                          f" all-reduce" if world > 1 else "")},
             "roofline": roofline, "setup_ms": setup_ms,
+            "accumulation": args.accumulation,
         }
+        if refacc is not None:
+            out["reference_accumulation"] = refacc
         if world == 1 and not args.no_cpu_baseline:
             log("timing CPU baseline (oracle) ...")
             out["cpu_baseline"] = cpu_baseline_rows(algo, X, y, cfg.get("k", 0), args.star)
@@ -405,6 +495,11 @@ def main():
     ap.add_argument("--no-q32", action="store_true",
                     help="skip the 32-bit pass-1 comparison step time (MultiSURF at N=1)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--accumulation", default="fast", choices=("fast", "reference"),
+                    help="the timed step's accumulation mode (reference: the reference's "
+                         "float32 per-sample chains and column sums, bit-identical scores)")
+    ap.add_argument("--no-ref", action="store_true",
+                    help="skip the reference-order step time beside the default (N=1)")
     ap.add_argument("--no-fit", action="store_true", help="skip the end-to-end fit() timing")
     ap.add_argument("--backend", default="gpu", choices=("gpu", "cpu"),
                     help="cpu: rehearse the multi-rank job on host threads (gloo, tests only)")
@@ -481,9 +576,10 @@ def main():
     t0 = time.perf_counter()
     with resident_x(x, args.backend, local):
         job = ShardedMultiSURF(x, y, recip, is_disc, use_star=args.star, backend=args.backend,
-                               device=local)
+                               device=local, accumulation=args.accumulation)
     sync()
     setup_ms = (time.perf_counter() - t0) * 1e3
+    ref_mode = args.accumulation == "reference"
     tiles, _, _ = job.info()
     q16_used = bool(job.plan.calibration()["q16"]) if on_gpu else False
 
@@ -505,6 +601,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     _, _, refined = job.info()
     weighted = job.weighted_pairs()  # non-zero pass-2 weights (sparse pass 2), -1 if dense
+    step_counts = job.counts.cpu().numpy()
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -523,12 +620,17 @@ def main():
         pairs_dense = n * (n - 1) / 2.0 / world
         pairs_score = weighted if weighted >= 0 else pairs_dense
         score_name = "k_score_sparse" if weighted >= 0 else "k_score"
+        if ref_mode:  # the chains walk directed entries (one per focal side)
+            score_name, weighted = "k_ms_chains", -1
+            pairs_score = chain_entries(step_counts, y, args.star)
         pfe = {"k_dist": pairs_dense * p, score_name: pairs_score * p}
         kern = {"k_dist": d_ms, score_name: s_ms}
         dom = max(kern, key=kern.get)
         # FMA-equivalent FLOPs per PFE: k_dist 2 on 16-bit operands (one
-        # v_sad_u16 per 2 PFE), 4 on 32-bit (half-rate v_sad_u32); pass 2 4
-        fpp = {"k_dist": FLOP_PER_PFE // 2 if q16_used else FLOP_PER_PFE, score_name: FLOP_PER_PFE}
+        # v_sad_u16 per 2 PFE), 4 on 32-bit (half-rate v_sad_u32); pass 2 4;
+        # the reference-order chains 6 (sub, mul, add)
+        fpp = {"k_dist": FLOP_PER_PFE // 2 if q16_used else FLOP_PER_PFE,
+               score_name: FLOP_PER_PFE_CHAINS if ref_mode else FLOP_PER_PFE}
         achieved = fpp[dom] * pfe[dom] / (kern[dom] * 1e-3) / 1e12
         # bytes the tiles stream from L2/HBM into the CUs (both row panels of
         # every owned tile, + the D write / the pair weights): on-chip reuse
@@ -565,7 +667,7 @@ def main():
     # the decision-finer 32-bit pass 1 (FS_Q16=0) beside the default step
     # (VERDICT r2 next #6): same job, 32-bit operands forced
     q32 = None
-    if on_gpu and world == 1 and not args.no_q32:
+    if on_gpu and world == 1 and not args.no_q32 and not ref_mode:
         os.environ["FS_Q16"] = "0"
         try:
             with resident_x(x, args.backend, local):
@@ -584,6 +686,16 @@ def main():
             job32.close()
         finally:
             del os.environ["FS_Q16"]
+    # the reference-order step beside the default (its
+    # cost at cfg2 / cfg4): same job, accumulation='reference'
+    refacc = None
+    if on_gpu and world == 1 and not args.no_ref and not ref_mode:
+        def make_ref():
+            with resident_x(x, args.backend, local):
+                return ShardedMultiSURF(x, y, recip, is_disc, use_star=args.star,
+                                        backend=args.backend, device=local,
+                                        accumulation="reference")
+        refacc = reference_step(make_ref, y, args.star, p, sync, max(1, min(args.steps, 3)))
     setup = torch.tensor([setup_ms], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
     if world > 1:
         dist.all_reduce(setup, op=dist.ReduceOp.MAX)
@@ -620,9 +732,22 @@ def main():
             # creation (device ranges, calibration, layout), max over ranks
             "setup_ms": float(setup.item()),
             "pass1_operands": "16-bit" if q16_used else "32-bit",
+            "accumulation": args.accumulation,
+            # the timed step's near/far decisions against the reference's
+            # (VERDICT r4 next #2), when the oracle's decisions are committed
+            "decisions_vs_reference": decisions_vs_fixture(step_counts, n, p, args.config)
+            if args.seed == 42 else None,
         }
+        if ref_mode:
+            out["arith"] = ("pass 1: integer L1 distances on 32-bit operands, pairs near a "
+                            "threshold and the thresholds of flagged rows recomputed in the "
+                            "reference's arithmetic; pass 2: the reference's float32 per-sample "
+                            "hit / miss chains in sample order and float32 sequential column "
+                            "sums (bit-identical to the oracle)")
         if q32 is not None:
             out["q32_pass1"] = q32
+        if refacc is not None:
+            out["reference_accumulation"] = refacc
     if on_gpu and world == 1 and not args.no_fit:
         log("timing end-to-end fit() ...")
         med, ts = fit_ms(X, y, args.star)
