@@ -55,14 +55,15 @@ class GatherFailed(RuntimeError):
 
 
 def gather_rows(x, device=None, force=False):
-    """All of the float32 host matrix ``x`` in one tensor on ``device`` (a
-    CUDA ordinal; None = host tensors, the gloo rehearsal), with this rank
-    copying only its ``row_chunk`` from the host and the rest all-gathered
-    from the other ranks.  Returns a (world * rows, p) tensor whose first n
-    rows are x."""
+    """All of the float32 / float64 host matrix ``x`` in one tensor on
+    ``device`` (a CUDA ordinal; None = host tensors, the gloo rehearsal), with
+    this rank copying only its ``row_chunk`` from the host and the rest
+    all-gathered from the other ranks.  Returns a (world * rows, p) tensor of
+    x's dtype whose first n rows are x."""
     import torch
     dist, rank, world = _dist()
     n, p = x.shape
+    tdt = torch.float64 if x.dtype == np.float64 else torch.float32
     if dist is None or (world == 1 and not force):
         dev = "cpu" if device is None else torch.device("cuda", device)
         return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
@@ -74,7 +75,7 @@ def gather_rows(x, device=None, force=False):
     # blocked in the collective while it went on to the next one.
     err = None
     try:
-        buf = torch.empty((rows * world, p), dtype=torch.float32, device=dev)
+        buf = torch.empty((rows * world, p), dtype=tdt, device=dev)
         mine = buf[rank * rows:(rank + 1) * rows]
         if hi > lo:
             mine[:hi - lo].copy_(torch.from_numpy(x[lo:hi]))
@@ -99,18 +100,20 @@ def gather_rows(x, device=None, force=False):
 def resident_x(x, backend="gpu", device=0, gather=None):
     """X on the GPU for the calls inside the block.  Multi-GPU with RCCL:
     per-rank rows + all-gather (``gather_rows``), registered as the staged
-    copy of ``x`` (fs_stage_x_device).  One GPU (or gloo): one host-to-device
-    copy (fs_stage_x).  ``x`` must be C-contiguous float32.  gather=True
-    takes the all-gather path at any world size with an 'nccl' group (tests)."""
+    copy of ``x`` (fs_stage_x_device); the block receives the gathered
+    device tensor (n first rows = x).  One GPU (or gloo): one host-to-device
+    copy (fs_stage_x), and the block receives None.  ``x`` must be
+    C-contiguous float32 or float64 (SURF's dtype).  gather=True takes the
+    all-gather path at any world size with an 'nccl' group (tests)."""
     dist, _, world = _dist()
     if backend != "gpu":
-        yield
+        yield None
         return
     if gather is None:
         gather = dist is not None and world > 1
     if not gather or dist is None or dist.get_backend() != "nccl":
         with _lib.staged_x(backend, x, device):
-            yield
+            yield None
         return
     try:
         buf = gather_rows(x, device, force=True)
@@ -123,11 +126,11 @@ def resident_x(x, backend="gpu", device=0, gather=None):
         print(f"fastselect_amd: RCCL all-gather of X failed ({e}); uploading X per rank",
               file=sys.stderr, flush=True)
         with _lib.staged_x(backend, x, device):
-            yield
+            yield None
         return
     try:
         with _lib.staged_device_x(x, buf.data_ptr(), device):
-            yield
+            yield buf
     finally:
         import torch
         torch.cuda.current_stream(device).synchronize()
@@ -351,12 +354,40 @@ def _allreduce_sums(sums, backend, device):
     return t.cpu().numpy()
 
 
-def relieff_scores(X, y, n_neighbors=3, discrete_limit=10, backend="gpu", device=0, n_jobs=-1):
+@contextlib.contextmanager
+def resident_cast(xd, x32, device=0):
+    """The float32 copy ``x32`` of a host matrix whose float64 rows are
+    already on the GPU (``xd``, the tensor resident_x yields: RCCL-gathered)
+    made there by one device cast -- round to nearest even, the rounding of
+    numpy's astype, so the copy is bit-identical to x32 -- and registered as
+    x32's staged copy (fs_stage_x_device) for the calls inside the block.
+    xd None (no gather: one GPU, gloo, the CPU backend): nothing to do, the
+    calls upload x32 themselves."""
+    if xd is None:
+        yield
+        return
+    import torch
+    n = x32.shape[0]
+    buf = xd[:n].to(torch.float32).contiguous()
+    torch.cuda.current_stream(device).synchronize()   # the library reads it on its own streams
+    try:
+        with _lib.staged_device_x(x32, buf.data_ptr(), device):
+            yield
+    finally:
+        torch.cuda.current_stream(device).synchronize()
+        del buf
+
+
+def relieff_scores(X, y, n_neighbors=3, discrete_limit=10, backend="gpu", device=0, n_jobs=-1,
+                   gather=None):
     """ReliefF feature scores with the focal samples sharded over the ranks:
     this rank scores ``shard_rows(n, rank, world)``, one all-reduce sums the
     slices.  Returns the full float32 score vector (identical on every rank)
     -- ``ReliefF(n_neighbors=...).fit(X, y).feature_importances_`` up to
-    float64 summation order."""
+    float64 summation order.  X crosses the host link once over all ranks
+    (``resident_x``: each rank uploads its n/N float64 rows, RCCL all-gathers
+    the rest; the column statistics read that copy, and the float32 copy
+    the plan scores is cast from it on the device, ``resident_cast``)."""
     from .ReliefF import relieff_inputs
     x = np.ascontiguousarray(X, dtype=np.float64)
     yv = np.asarray(y)
@@ -364,22 +395,28 @@ def relieff_scores(X, y, n_neighbors=3, discrete_limit=10, backend="gpu", device
     if np.unique(yv).size < 2:
         return np.zeros(p, dtype=np.float32)
     backend = _base.effective_backend(backend)
-    x32, y_enc, recip, isd, priors = relieff_inputs(x, yv, discrete_limit, backend, device, n_jobs)
     _, rank, world = _dist()
-    sums = _lib.relieff_score(backend, x32, y_enc, recip, isd, n_neighbors, priors, n_jobs,
-                              device=device, rows=shard_rows(n, rank, world))
+    with resident_x(x, backend, device, gather) as xd:
+        x32, y_enc, recip, isd, priors = relieff_inputs(x, yv, discrete_limit, backend, device,
+                                                        n_jobs)
+        with resident_cast(xd, x32, device):
+            sums = _lib.relieff_score(backend, x32, y_enc, recip, isd, n_neighbors, priors,
+                                      n_jobs, device=device, rows=shard_rows(n, rank, world))
     return (_allreduce_sums(sums, backend, device) / n).astype(np.float32)
 
 
-def surf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", device=0, n_jobs=-1):
+def surf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", device=0, n_jobs=-1,
+                gather=None):
     """SURF / SURF* feature scores with the focal samples sharded over the
-    ranks (see ``relieff_scores``)."""
+    ranks (see ``relieff_scores``); X (float64, SURF.py:330-332) reaches the
+    GPUs by per-rank rows + one RCCL all-gather of float64 rows."""
     from .SURF import surf_inputs
     x = np.ascontiguousarray(X, dtype=np.float64)
     n, p = x.shape
     backend = _base.effective_backend(backend)
-    isd, recip = surf_inputs(x, discrete_limit, backend, device)
     _, rank, world = _dist()
-    sums = _lib.surf_score(backend, x, np.asarray(y).astype(np.int32), recip, use_star, isd,
-                           n_jobs, device=device, rows=shard_rows(n, rank, world))
+    with resident_x(x, backend, device, gather):
+        isd, recip = surf_inputs(x, discrete_limit, backend, device)
+        sums = _lib.surf_score(backend, x, np.asarray(y).astype(np.int32), recip, use_star, isd,
+                               n_jobs, device=device, rows=shard_rows(n, rank, world))
     return (_allreduce_sums(sums, backend, device) / n).astype(np.float32)

@@ -84,6 +84,35 @@ def test_nccl_gathered_x_matches_uploaded_x():
         dist.destroy_process_group()
 
 
+def test_nccl_gathered_rows_relieff_surf():
+    """ReliefF and SURF's row-sharded jobs through the multi-GPU data path at
+    world 1: X's float64 rows all-gathered over RCCL
+    and registered for the column statistics, SURF's plan reading them and
+    ReliefF's float32 copy cast on the device -- bit-identical scores to the
+    per-rank upload (gather=False)."""
+    import torch
+    import torch.distributed as dist
+    from sklearn.datasets import make_classification
+
+    from fastselect_amd import parallel
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = str(_port())
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        X, y = make_classification(n_samples=1300, n_features=240, n_informative=15,
+                                   n_redundant=30, n_classes=3, random_state=5)
+        X[:, :6] = np.round(X[:, :6])          # discrete columns too
+        for fn, kw in ((parallel.relieff_scores, {"n_neighbors": 6}),
+                       (parallel.surf_scores, {"use_star": True})):
+            a = fn(X, y, backend="gpu", device=0, gather=True, **kw)
+            b = fn(X, y, backend="gpu", device=0, gather=False, **kw)
+            np.testing.assert_array_equal(a, b)
+    finally:
+        dist.destroy_process_group()
+
+
 def test_column_stats_run_on_the_ranks_device():
     """prepare_inputs(device=d) computes the column statistics on GPU d
     (they used to default to GPU 0 on every rank)."""

@@ -152,28 +152,31 @@ def test_relieff_boundary_ties_follow_numba_quicksort(oracle, kind, k):
     assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=k, discrete_limit=dl), TOL)
 
 
-def _gather_worker(rank, world, port, out_path):
+def _gather_worker(rank, world, port, out_path, dtype):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from fastselect_amd.parallel import gather_rows
-    x = np.random.default_rng(4).normal(size=(301, 17)).astype(np.float32)
+    x = np.random.default_rng(4).normal(size=(301, 17)).astype(dtype)
     buf = gather_rows(x, None)           # host tensors: the gloo rehearsal of the RCCL gather
     np.save(f"{out_path}.{rank}.npy", buf.numpy()[:301])
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gather_rows_assembles_x(tmp_path, world):
+@pytest.mark.parametrize("world,dtype", [(2, "float32"), (3, "float32"), (2, "float64")])
+def test_gather_rows_assembles_x(tmp_path, world, dtype):
     """Multi-GPU data path: each rank contributes only its row_chunk and the
-    all-gather assembles all of X on every rank (gloo here, RCCL on GPUs)."""
+    all-gather assembles all of X on every rank (gloo here, RCCL on GPUs);
+    float64 rows for SURF and ReliefF's row-sharded jobs."""
     import torch.multiprocessing as mp
     out = str(tmp_path / "x")
-    mp.spawn(_gather_worker, args=(world, _free_port(), out), nprocs=world, join=True)
-    x = np.random.default_rng(4).normal(size=(301, 17)).astype(np.float32)
+    mp.spawn(_gather_worker, args=(world, _free_port(), out, dtype), nprocs=world, join=True)
+    x = np.random.default_rng(4).normal(size=(301, 17)).astype(dtype)
     for r in range(world):
-        np.testing.assert_array_equal(np.load(f"{out}.{r}.npy"), x)
+        got = np.load(f"{out}.{r}.npy")
+        assert got.dtype == np.dtype(dtype)
+        np.testing.assert_array_equal(got, x)
 
 
 def test_row_chunks_cover_every_row_once():
