@@ -42,9 +42,6 @@
 #include "../../include/fastselect_amd.h"
 #include "fs_internal.h"
 #include "fs_sparse_asm.inc"
-#ifdef FS_SP2_PROF
-#include "fs_sparse_asm_prof.inc"
-#endif
 
 namespace fs {
 namespace gpu {
@@ -1496,10 +1493,7 @@ __device__ __forceinline__ void score_tiles(const float* __restrict__ xs, int64_
 // slots, the few beyond nseg exit at once.
 constexpr int kXcds = 8;
 // row blocks per group of the sparse pass-2 schedule (build_sparse_schedule;
-// 16 / FS_SCHED_ROWS feature blocks per block of units)
-#ifndef FS_SCHED_ROWS
-#define FS_SCHED_ROWS 8
-#endif
+// 16 / kSchedRows feature blocks per block of units)
 
 __global__ __launch_bounds__(256) void k_score(const float* __restrict__ xs, int64_t PW,
                                                int64_t PC, const int2* __restrict__ tiles,
@@ -1668,9 +1662,6 @@ __device__ __forceinline__ void sparse2_stream_generic(const float4* __restrict_
 // tail of a layout whose width is not a multiple of 512).  Lane l scores
 // features f0 + 4l + k and (F = 8) f0 + 256 + 4l + k, k = 0..3; partials go
 // to spart[(seg * 2 + h) * PW + f].
-#ifdef FS_SP2_PROF
-__device__ unsigned long long fs_sp2_prof[9];
-#endif
 template <int F>
 __global__ __launch_bounds__(1024) void k_score_sparse2(
     const float* __restrict__ xs, int64_t PW, int64_t PC, const int2* __restrict__ tiles,
@@ -1706,16 +1697,11 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
   double s[F];
 #pragma unroll
   for (int q = 0; q < F; q++) s[q] = 0.0;
-#ifdef FS_SP2_PROF
-  uint64_t pr_pro = 0, pr_body = 0, pr_out = 0, pr_tiles = 0, pr_stage = 0;
-  const uint64_t pr_t0 = __builtin_amdgcn_s_memtime(), pr_r0 = wall_clock64();
-  uint64_t pr_last = pr_t0;
-#endif
   // VALU issue goes to the oldest ready wave of a SIMD (MI355X_MICROARCH.md,
   // "Two waves per SIMD" item 2), so with equal static shares the 16 waves
   // of a unit finished staggered -- the oldest first, the youngest last with
   // few partners to hide its latency: 26% of the waves' lives waited at the
-  // final barrier (FS_SP2_PROF, profiles/r04/pass2_prio.txt).  A wave behind
+  // final barrier (round 4's clock-stamp build, profiles/r04/pass2_prio.txt).  A wave behind
   // the workgroup's mean progress (tiles done, an LDS counter) raises its
   // priority until it has caught up: 4.9% left waiting, pass 2 88.0 -> 81.2
   // ms at cfg4.  The scores do not change (same streams per wave, same order).
@@ -1739,9 +1725,6 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
     const int64_t t = __builtin_amdgcn_readlane(my_t, idx);
     const int2 tl = make_int2(__builtin_amdgcn_readlane(my_x, idx), __builtin_amdgcn_readlane(my_y, idx));
     if (tl.x != cur_bi) {  // once per segment: its tiles share one row block
-#ifdef FS_SP2_PROF
-      const uint64_t ps = __builtin_amdgcn_s_memtime();
-#endif
       __syncthreads();
       // 64 rows x 2 chunks = 128 float4 per lane: 8 per wave, all requested
       // before the first store (one HBM latency per segment, not eight)
@@ -1758,9 +1741,6 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
       for (int m = 0; m < kPer; m++) As[(wave + kSWaves * m) * 64 + lane] = v[m];
       __syncthreads();
       cur_bi = tl.x;
-#ifdef FS_SP2_PROF
-      pr_stage += __builtin_amdgcn_s_memtime() - ps;
-#endif
     }
     float acc[F];
 #pragma unroll
@@ -1774,19 +1754,7 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
       // generated without the prefetch: tools/gen_sparse_asm.py pfn)
       const uint64_t bpn = bp, enb = eb;
       if constexpr (F == 8) {
-#ifdef FS_SP2_PROF
-        const uint64_t t0 = __builtin_amdgcn_s_memtime();
-        uint64_t tp;
-        FS_SPARSE2_ASM_F8_PROF(acc, lds_lane, glb_lane, eb, bp, bstride_b, ncols, bpn, pf_lane, enb, tp);
-        const uint64_t t1 = __builtin_amdgcn_s_memtime();
-        pr_out += t0 - pr_last;
-        pr_pro += tp - t0;
-        pr_body += t1 - tp;
-        pr_last = t1;
-        pr_tiles++;
-#else
         FS_SPARSE2_ASM_F8(acc, lds_lane, glb_lane, eb, bp, bstride_b, ncols, bpn, pf_lane, enb);
-#endif
       } else
         FS_SPARSE2_ASM_F4(acc, lds_lane, glb_lane, eb, bp, bstride_b, ncols, bpn, pf_lane, enb);
     } else {
@@ -1803,9 +1771,6 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
     else
       __builtin_amdgcn_s_setprio(0);
   }
-#ifdef FS_SP2_PROF
-  const uint64_t pr_loop_end = __builtin_amdgcn_s_memtime();
-#endif
   // fixed-order reduction of the 16 waves' partials through the LDS block
   __syncthreads();
   double* red = (double*)As;  // [F][kSWaves][64] (64 KB at F = 8)
@@ -1822,21 +1787,6 @@ __global__ __launch_bounds__(1024) void k_score_sparse2(
       v += (rr[w * 64] + rr[(w + 1) * 64]) + (rr[(w + 2) * 64] + rr[(w + 3) * 64]);
     if (f < PW) spart[(seg * 2 + h) * PW + f] = v;
   }
-#ifdef FS_SP2_PROF
-  if (F == 8 && lane == 0 && pr_tiles > 0) {
-    const uint64_t te = __builtin_amdgcn_s_memtime(), re = wall_clock64();
-    pr_out += pr_loop_end - pr_last;  // the last tile to the end of the walk
-    atomicAdd(&fs_sp2_prof[0], (unsigned long long)pr_pro);
-    atomicAdd(&fs_sp2_prof[1], (unsigned long long)pr_body);
-    atomicAdd(&fs_sp2_prof[2], (unsigned long long)(pr_out - pr_stage));
-    atomicAdd(&fs_sp2_prof[3], (unsigned long long)pr_tiles);
-    atomicAdd(&fs_sp2_prof[4], (unsigned long long)pr_stage);
-    atomicAdd(&fs_sp2_prof[5], (unsigned long long)(te - pr_loop_end));  // reduction + write
-    atomicAdd(&fs_sp2_prof[6], (unsigned long long)(te - pr_t0));        // the wave's life
-    atomicAdd(&fs_sp2_prof[7], (unsigned long long)(re - pr_r0));        // same, 100 MHz
-    atomicAdd(&fs_sp2_prof[8], 1ull);
-  }
-#endif
 }
 
 // dst[k] += src[k] (the tile shards' partial vectors, summed in shard order).
@@ -1903,20 +1853,7 @@ __device__ __forceinline__ uint32_t rf_key(double d, double inv_sc) {
 // k_dist's epilogue writes them, this kernel the refined ones).  STAGE: the
 // row and its class codes are staged in LDS (n <= 32768); else read from HBM
 // on every sweep (256 threads per row).
-// -DFS_RF_PROF (profiling builds only): per-phase wall-clock stamps of the
-// first 4096 rows of a k_rf_select launch, printed under FS_TRACE
-#ifdef FS_RF_PROF
-__device__ uint64_t fs_rf_prof[4096 * 8];
-#define RF_T(k)                                                  \
-  do {                                                           \
-    if (threadIdx.x == 0 && blockIdx.x < 4096)                   \
-      fs_rf_prof[blockIdx.x * 8 + (k)] = wall_clock64();         \
-  } while (0)
-#else
-#define RF_T(k) \
-  do {          \
-  } while (0)
-#endif
+// (Per-phase clock stamps of round 3's profiling build: DESIGN.md, Kernels.)
 template <bool STAGE>
 __global__ __launch_bounds__(1024) void k_rf_select(
     const float* __restrict__ Dk, int n, int64_t n_pad, const int32_t* __restrict__ lab,
@@ -2055,7 +1992,6 @@ __global__ __launch_bounds__(1024) void k_rf_select(
   // buffer's fixed rows (x_i, scales, columns) load under the row's read:
   // column indices first, the keys, then x_i at those columns.
   uint32_t kor = 0u, kand = 0xFFFFFFFFu;
-  RF_T(0);
   if (STAGE) {
     // one round trip: 8 quads per thread cover n <= 32768 (STAGE's range)
     constexpr int kQ = 8;
@@ -2129,7 +2065,6 @@ __global__ __launch_bounds__(1024) void k_rf_select(
   }
   if (lane == 0) red_or[wave] = kor, red_and[wave] = kand;
   __syncthreads();
-  RF_T(1);
   if (tid == 0) {
     uint32_t o = 0u, a = 0xFFFFFFFFu;
     for (int w = 0; w < nwaves; w++) o |= red_or[w], a &= red_and[w];
@@ -2226,7 +2161,6 @@ __global__ __launch_bounds__(1024) void k_rf_select(
       __syncthreads();
     };
     radix_pass(lo1, top + 1);
-    RF_T(2);
     if (lo1 > 0) {
       // Small buckets (<= 64 keys: the common case, the k nearest sit in the
       // sparse low tail) finish in one gather: the bucket's keys go to a list
@@ -2273,7 +2207,6 @@ __global__ __launch_bounds__(1024) void k_rf_select(
       if (any_big)
         for (int hi = lo1; hi > 0; hi -= 8) radix_pass(hi - 8 > 0 ? hi - 8 : 0, hi);
     }
-    RF_T(3);
     if (round + 1 >= rounds) break;
 
     // 3. Exact keys.  The band |key - T| <= band_abs + band_rel * T (in f64)
@@ -2321,7 +2254,6 @@ __global__ __launch_bounds__(1024) void k_rf_select(
       }
     });
     __syncthreads();
-    RF_T(4);
     const int F = nflag;
     if (F == 0) break;  // nothing near any k-th key: round 0's keys are final
     if (F <= (fcap < kFCap ? fcap : kFCap)) {
@@ -2368,7 +2300,6 @@ __global__ __launch_bounds__(1024) void k_rf_select(
         }
         __syncthreads();
       }
-      RF_T(5);
       for (int c = wave; c < C; c += nwaves) {
         if (need[c] == 0) continue;
         const int64_t members = class_count[c] - (c == li ? 1 : 0);
@@ -2400,7 +2331,6 @@ __global__ __launch_bounds__(1024) void k_rf_select(
       }
       if (tid == 0) n_ex = F;
       __syncthreads();
-      RF_T(6);
       break;
     }
     // general route: every candidate of a wave's chunk, in ballot order
@@ -2577,7 +2507,6 @@ __global__ __launch_bounds__(1024) void k_rf_select(
       for (int u = 0; u < kCU; u++) emit(lt[u], eq[u], cv[u], j0 + 64 * u + lane);
     }
   }
-  RF_T(7);
 }
 
 // Exact reference keys of whole rows (tie rows of a problem with continuous
@@ -4081,8 +4010,8 @@ static int calibrate_band(Plan* g) {
 // Concurrent units then share their B rows through the XCD's L2 (kSchedRows
 // row blocks x 2 halves read each) and their entry streams (kSchedFb
 // feature blocks read each).
-constexpr int kSchedRows = FS_SCHED_ROWS;
-constexpr int kSchedFb = 16 / FS_SCHED_ROWS;
+constexpr int kSchedRows = 8;
+constexpr int kSchedFb = 16 / kSchedRows;
 
 static int ensure_dev(Plan* g, void** buf, size_t* cap, size_t bytes) {
   if (bytes <= *cap) return FS_OK;
@@ -4754,22 +4683,11 @@ static int run_quantize_dist(Plan* g) {
     // coherently and heavy-tailed columns crowd most samples into a few
     // quanta, and both move the thresholds (intgrid, n = 3000: 2.2e-5
     // without it; lognormal: VERDICT r3 missing #1).
-#if defined(FS_NO_MEANCORR)
-    // A/B timing only (wrong thresholds): no mean correction at all
-    FS_HIP(hipMemsetAsync(g->corr, 0, sizeof(double) * Q.n_pad, g->stream));
-    FS_HIP(hipEventRecord(g->ev_join, g->stream));
-#elif defined(FS_MC_MAIN)
-    // A/B timing only: the mean correction on the main stream, before k_dist
-    FS_TRY(run_colsort(g, g->c_lo, g->c_hi, g->stream));
-    FS_TRY(run_rowcorr(g, g->c_lo, g->c_hi, g->corr, g->stream));
-    FS_HIP(hipEventRecord(g->ev_join, g->stream));
-#else
     FS_HIP(hipEventRecord(g->ev_fork, g->stream));
     FS_HIP(hipStreamWaitEvent(g->side, g->ev_fork, 0));
     FS_TRY(run_colsort(g, g->c_lo, g->c_hi, g->side));
     FS_TRY(run_rowcorr(g, g->c_lo, g->c_hi, g->corr, g->side));
     FS_HIP(hipEventRecord(g->ev_join, g->side));
-#endif
   }
   if (g->n_tiles > 0) {
     FS_HIP(hipEventRecord(g->ev[0], g->stream));
@@ -4971,11 +4889,6 @@ static int run_pass2(Plan* g, double* scores_dev) {
     // 512-feature blocks, then the tail block (build_sparse_schedule; one
     // F = 8 block is cheaper than two F = 4 ones -- cfg2, 448 features:
     // 0.24 -> 0.17 ms)
-#ifdef FS_SP2_PROF
-    void* prp = nullptr;
-    FS_HIP(hipGetSymbolAddress(&prp, HIP_SYMBOL(fs_sp2_prof)));
-    FS_HIP(hipMemsetAsync(prp, 0, 9 * sizeof(unsigned long long), g->stream));
-#endif
     if (g->nunits8 > 0) {
       k_score_sparse2<8><<<(unsigned)g->nunits8, 64 * kSWaves, 0, g->stream>>>(
           g->xs, Q.PW, Q.PC, g->tiles, g->ent, g->sched, g->seg_off, g->units8, 0, g->spart);
@@ -4987,24 +4900,6 @@ static int run_pass2(Plan* g, double* scores_dev) {
           g->spart);
       FS_TRY(launch_check("k_score_sparse2<4>"));
     }
-#ifdef FS_SP2_PROF
-    if (trace_on()) {
-      unsigned long long pr[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-      FS_HIP(hipMemcpyAsync(pr, prp, sizeof(pr), hipMemcpyDeviceToHost, g->stream));
-      FS_HIP(hipStreamSynchronize(g->stream));
-      const double life = (double)pr[6];
-      std::fprintf(stderr,
-                   "[fs_trace] k_score_sparse2<8> per wave-tile (shader clocks): start %.0f, walk "
-                   "%.0f, between %.0f, staging %.0f; of the waves' lives: start %.3f walk %.3f "
-                   "between %.3f staging %.3f reduction %.3f other %.3f; %llu wave-tiles, %llu "
-                   "waves, %.0f clocks / %.2f us per wave (%.2f GHz)\n",
-                   pr[0] / (double)pr[3], pr[1] / (double)pr[3], pr[2] / (double)pr[3],
-                   pr[4] / (double)pr[3], pr[0] / life, pr[1] / life, pr[2] / life, pr[4] / life,
-                   pr[5] / life, 1.0 - (pr[0] + pr[1] + pr[2] + pr[4] + pr[5]) / life, pr[3], pr[8],
-                   life / pr[8], pr[7] / (double)pr[8] / 100.0,
-                   life / (pr[7] / 100.0) / 1e3);
-    }
-#endif
   } else {
     k_score<<<(unsigned)(kXcds * seg_per_xcd * nfb), 256, 0, g->stream>>>(
         g->xs, Q.PW, Q.PC, g->tiles, g->Wt, g->n_tiles, g->seg_len, g->nseg, nfb, g->spart);
@@ -5572,13 +5467,6 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   int fcap = 256;
   if (test_hooks().rf_fcap >= 0) fcap = (int)std::min<int64_t>(256, test_hooks().rf_fcap);
   FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
-#ifdef FS_RF_PROF
-  {
-    void* pp = nullptr;
-    FS_HIP(hipGetSymbolAddress(&pp, HIP_SYMBOL(fs_rf_prof)));
-    FS_HIP(hipMemsetAsync(pp, 0, 4096 * 8 * 8, g->stream));
-  }
-#endif
   FS_HIP(hipEventRecord(g->ev[4], g->stream));
   if (stage)
     k_rf_select<true><<<(unsigned)nr_own, 1024, shsel, g->stream>>>(
@@ -5603,26 +5491,6 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
                         g->stream));
   FS_HIP(hipStreamSynchronize(g->stream));
   g->n_refined = (int64_t)ex_cnt;
-#ifdef FS_RF_PROF
-  if (trace_on()) {
-    std::vector<uint64_t> pr(4096 * 8);
-    FS_HIP(hipMemcpyFromSymbol(pr.data(), HIP_SYMBOL(fs_rf_prof), pr.size() * 8));
-    const int64_t nrow = std::min<int64_t>(4096, nr_own);
-    double acc[8] = {0};
-    for (int64_t r = 0; r < nrow; r++) {
-      uint64_t last = pr[r * 8];
-      for (int q = 1; q < 8; q++) {
-        const uint64_t b = pr[r * 8 + q];
-        if (b == 0) continue;  // phase skipped
-        acc[q] += (double)(b - last);
-        last = b;
-      }
-    }
-    std::fprintf(stderr, "[fs_trace] k_rf_select phases (us/row, 100 MHz):");
-    for (int q = 1; q < 8; q++) std::fprintf(stderr, " %d:%.2f", q, acc[q] / nrow / 100.0);
-    std::fprintf(stderr, "\n");
-  }
-#endif
   std::vector<int32_t> tie_rows;
   for (int64_t r = 0; r < nr_own; r++)
     for (int c = 0; c < C; c++)

@@ -1382,9 +1382,6 @@ if __name__ == "__main__":
     text += "\n" + gen_v2("FS_SPARSE2_ASM_F4", F=4, lead=6, pfn=False)
     open(path, "w").write(text)
     print("wrote", os.path.normpath(path))
-    # profiling builds only (-DFS_SP2_PROF, tools/sp2_prof.sh): the F = 8
-    # loop with the tile-start stamp
-    ppath = path.replace("fs_sparse_asm.inc", "fs_sparse_asm_prof.inc")
-    open(ppath, "w").write(HEADER + "\n" + gen_v2("FS_SPARSE2_ASM_F8_PROF", F=8, lead=3, pfn=False,
-                                                    tprof=True))
-    print("wrote", os.path.normpath(ppath))
+    # (round 4's clock-stamp variant of the F = 8 loop, gen_v2(tprof=True),
+    # fed a profiling build that is no longer part of the library sources:
+    # its measurements are in profiles/r04/pass2_prio.txt)
