@@ -69,7 +69,7 @@ int check(const char* what) {
 constexpr int kChunk = 64;   // samples j per staged chunk (one mask word)
 constexpr int kFeat = 256;   // features per workgroup (64 lanes x 4)
 constexpr int kWaves = 16;   // waves per k_ms_chains workgroup
-constexpr int kRowsW = 8;    // focal rows per wave
+constexpr int kRowsW = 6;    // focal rows per wave
 constexpr int kRowsWG = kWaves * kRowsW;
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
@@ -209,28 +209,53 @@ __device__ __forceinline__ void chain_step(const float4 v, const float (&a)[4],
   }
 }
 
+__device__ __forceinline__ int pop_bit(uint64_t& m) {
+  const int b = __builtin_ctzll(m);
+  m &= m - 1;
+  return b;
+}
+
 // Walk the set bits of one 64-sample mask word in ascending j (the
-// reference's j loop), one LDS row read ahead of its use.
+// reference's j loop) in groups of 4 entries: the group's four LDS row reads
+// are issued together ahead of its arithmetic (each step then waits only for
+// its own read, counted lgkmcnt), the last 1-3 entries likewise.
 template <bool SIGNED, bool DISC>
 __device__ __forceinline__ void chain_walk(uint64_t m, uint64_t neg, const float4* __restrict__ buf,
                                            int lane, const float (&a)[4], const float (&rc)[4],
                                            uint32_t dk, float (&acc)[4]) {
-  if (m == 0) return;
-  int b = __builtin_ctzll(m);
-  m &= m - 1;
-  float4 v = buf[b * 64 + lane];
-  while (m != 0) {
-    const int b2 = __builtin_ctzll(m);
-    m &= m - 1;
-    const float4 v2 = buf[b2 * 64 + lane];
-    chain_step<DISC>(v, a, rc, dk, SIGNED && ((neg >> b) & 1ull) ? -1.0f : 1.0f, acc);
-    v = v2;
-    b = b2;
+  auto sg = [&](int b) { return SIGNED && ((neg >> b) & 1ull) ? -1.0f : 1.0f; };
+  while (__builtin_popcountll(m) >= 4) {
+    const int b0 = pop_bit(m), b1 = pop_bit(m), b2 = pop_bit(m), b3 = pop_bit(m);
+    const float4 v0 = buf[b0 * 64 + lane], v1 = buf[b1 * 64 + lane];
+    const float4 v2 = buf[b2 * 64 + lane], v3 = buf[b3 * 64 + lane];
+    chain_step<DISC>(v0, a, rc, dk, sg(b0), acc);
+    chain_step<DISC>(v1, a, rc, dk, sg(b1), acc);
+    chain_step<DISC>(v2, a, rc, dk, sg(b2), acc);
+    chain_step<DISC>(v3, a, rc, dk, sg(b3), acc);
   }
-  chain_step<DISC>(v, a, rc, dk, SIGNED && ((neg >> b) & 1ull) ? -1.0f : 1.0f, acc);
+  if (m == 0) return;
+  const int b0 = pop_bit(m);
+  const float4 v0 = buf[b0 * 64 + lane];
+  if (m == 0) {
+    chain_step<DISC>(v0, a, rc, dk, sg(b0), acc);
+    return;
+  }
+  const int b1 = pop_bit(m);
+  const float4 v1 = buf[b1 * 64 + lane];
+  if (m == 0) {
+    chain_step<DISC>(v0, a, rc, dk, sg(b0), acc);
+    chain_step<DISC>(v1, a, rc, dk, sg(b1), acc);
+    return;
+  }
+  const int b2 = pop_bit(m);
+  const float4 v2 = buf[b2 * 64 + lane];
+  chain_step<DISC>(v0, a, rc, dk, sg(b0), acc);
+  chain_step<DISC>(v1, a, rc, dk, sg(b1), acc);
+  chain_step<DISC>(v2, a, rc, dk, sg(b2), acc);
 }
 
-// The 8 rows of a wave over one staged chunk: hits, then the miss chain.
+// The rows of a wave over one staged chunk: each row's hit chain, then
+// its miss chain.
 template <bool STAR, bool DISC>
 __device__ __forceinline__ void chunk_rows(const float4* __restrict__ buf, uint64_t mw, int lane,
                                            const float (&a)[kRowsW][4], const float (&rc)[4],
