@@ -5,7 +5,7 @@
 // Pass 1 computes quantised distances D_q; their row sum is off from the
 // reference's by the per-column terms
 //   corr_if = sum_j sign(t_if - t_jf) (eps_if - eps_jf)
-// (t = (x - min) * recip * SC, q = round(t), eps = q - t; fs_gpu.hip,
+// (t = (x - min) * recip * SC, q = round(t), eps = q - t; fs_pass1.hip,
 // k_quantize).  With the column ordered by t (position k of sample i, prefix
 // sum P_k of eps over the samples before it, total T):
 //   corr_if = eps_i (2k - n) - 2 P_k + T.

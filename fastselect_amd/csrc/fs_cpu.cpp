@@ -97,7 +97,7 @@ static double calibrated_band(const Prepared& P, const void* x, int x_is_f64, in
                           std::sqrt(ss / (double)err.size()), mx);
 }
 
-// Same arithmetic as k_quantize (fs_gpu.hip): t = (x - off) * qs,
+// Same arithmetic as k_quantize (fs_pass1.hip): t = (x - off) * qs,
 // q = trunc(t + 0.5), eps = q - t, every double operation rounded separately.
 static void quantize(const Prepared& P, const void* x, int x_is_f64, int n_jobs,
                      std::vector<uint32_t>& xq, std::vector<float>& xs,
@@ -313,7 +313,7 @@ static int64_t refine_pairs(const Prepared& P, const void* x, int x_is_f64, int 
   return (int64_t)pairs.size();
 }
 
-// exact_thresholds (fs_gpu.hip): thresholds from exact distances for the
+// exact_thresholds (fs_select.hip): thresholds from exact distances for the
 // rows a refined pair lies within thr_tol of, when at most exact_thr_rows(n, p)
 // (every row under the thr_exact_all test hook, fs_test_hook).
 static void exact_thresholds(const Prepared& P, const void* x, int n_jobs, const CpuState& S,

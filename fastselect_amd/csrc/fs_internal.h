@@ -99,7 +99,7 @@ struct Prepared {
   // recomputed exactly) and the mean correction (k_colrank).
   int q16 = 0;
   // 1: never 16-bit pass-1 operands (the one-shot MultiSURF re-run after the
-  // decision-risk check, fs_gpu.hip q16_decision_risk)
+  // decision-risk check, fs_plan.hip q16_decision_risk)
   int no_q16 = 0;
   // 1: reference-order accumulation (fs_set_accumulation(FS_ACCUM_REFERENCE),
   // fs_refacc.hip): MultiSURF's per-(sample, feature) float32 hit / miss
@@ -149,7 +149,7 @@ int finalize_scale(Prepared& P, const double* cmin, const double* cmax);
 // Integer scale, qmax and the model band for 16-bit (q16 = 1) or 32-bit
 // operands, from the ranges finalize_scale measured (P.Rmax).
 int set_integer_scale(Prepared& P, int q16);
-// Refinement-band calibration (fs_gpu.hip calibrate_band, and the CPU
+// Refinement-band calibration (fs_pass1.hip calibrate_band, and the CPU
 // backend's): `count` pairs i < j from a fixed generator over [0, n) (the
 // same on every rank and backend), and the band from their measured errors:
 // max(model, (3 max|err| + rms / 2) / SC) in real distance units.
@@ -408,7 +408,7 @@ class StageBarrier {
 
 namespace gpu {
 int device_count();
-// Device block cache (fs_gpu.hip): dev_alloc hands out a cached block of
+// Device block cache (fs_gpu_mem.hip): dev_alloc hands out a cached block of
 // `device` that covers `bytes` (within 2x) or a fresh hipMalloc; dev_free
 // keeps the block for the next request (up to the cache cap) or frees it.
 // Blocks come back with stale contents.  Returns FS_OK / FS_EOOM.

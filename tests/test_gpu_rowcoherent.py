@@ -9,7 +9,7 @@ refinement band of independent rounding -- while the whole-matrix sampled
 calibration meets those rows only by chance (minrow4: ~2 sampled pairs).  The
 default GPU path (16-bit pass 1 for MultiSURF at n >= 16384, MultiSURF* from
 10000) must still match the oracle within the 1e-5 bar with identical top-10,
-which the per-row guard provides (fs_gpu.hip: rows whose mean pass-1 error,
+which the per-row guard provides (fs_pass1.hip row_guard: rows whose mean pass-1 error,
 from the mean correction, is coherent get a band that covers it).
 """
 import hashlib

@@ -2,7 +2,7 @@
 ranges scored in row panels.
 
 A ReliefF / SURF plan keeps the distance rows of its own 128-sample blocks
-(fs_gpu.hip d_row_in: a row-sharded rank holds 1/N of D instead of all of
+(fs_gpu_internal.h d_row_in: a row-sharded rank holds 1/N of D instead of all of
 it), and a one-shot call whose rows exceed the device is scored in panels of
 whole blocks (row_panel_rows; the row_panel test hook forces the height here) -- the
 reference streams each focal sample's distance row (ReliefF.py:143-157,

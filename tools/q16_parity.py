@@ -2,7 +2,7 @@
 exact (fs_colsort.hip): per configuration, the rows whose near hit / miss
 counts differ between the two (decision flips; the 32-bit decisions are the
 reference's, tests/test_gpu_meancorr.py), the scale-relative score gap, the
-16-bit decision risk the plan's guard would estimate (fs_gpu.hip
+16-bit decision risk the plan's guard would estimate (fs_plan.hip
 q16_decision_risk, restated), and for cfg2 the gap to the oracle fixture.
 
     python tools/q16_parity.py [cfg2 n8k cfg4 ...]
