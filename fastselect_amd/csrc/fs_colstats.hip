@@ -214,9 +214,12 @@ int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap,
       !sx && (e = hipMemcpyAsync(dx, x, (size_t)n * p * esz, hipMemcpyHostToDevice, s)) != hipSuccess)
     fail("hipMemcpy H2D", e);
   const void* xd = sx ? sx : dx;
+  // a staged copy cast by fs_stage_x_cast knows its extrema already
+  const bool known = sx && staged_extrema(sx, colmin, colmax);
   if (rc == FS_OK) {
     const size_t lds = sizeof(unsigned long long) << tbits;
-    launch_minmax(xd, x_is_f64, n, p, rows_per_chunk, nchunks, pmin, pmax, dmin, dmax, s);
+    if (!known)
+      launch_minmax(xd, x_is_f64, n, p, rows_per_chunk, nchunks, pmin, pmax, dmin, dmax, s);
     if (x_is_f64)
       k_coldistinct<double><<<(unsigned)p, 256, lds, s>>>((const double*)xd, n, p, (int)cap,
                                                           tbits, dcnt);
@@ -226,10 +229,11 @@ int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap,
     if ((e = hipGetLastError()) != hipSuccess) fail("column statistics kernels", e);
   }
   if (rc == FS_OK &&
-      ((e = hipMemcpyAsync(colmin, dmin, (size_t)p * esz, hipMemcpyDeviceToHost, s)) !=
-           hipSuccess ||
-       (e = hipMemcpyAsync(colmax, dmax, (size_t)p * esz, hipMemcpyDeviceToHost, s)) !=
-           hipSuccess ||
+      ((!known &&
+        ((e = hipMemcpyAsync(colmin, dmin, (size_t)p * esz, hipMemcpyDeviceToHost, s)) !=
+             hipSuccess ||
+         (e = hipMemcpyAsync(colmax, dmax, (size_t)p * esz, hipMemcpyDeviceToHost, s)) !=
+             hipSuccess)) ||
        (e = hipMemcpyAsync(ndistinct, dcnt, (size_t)p * 8, hipMemcpyDeviceToHost, s)) !=
            hipSuccess))
     fail("hipMemcpy D2H", e);

@@ -157,7 +157,8 @@ struct Plan {
   void* colsort_scratch = nullptr;  // large-n route of colsort_terms
   size_t colsort_scratch_bytes = 0;
   // device buffers
-  void* x = nullptr;
+  void* x = nullptr;            // X on the device: the plan's own, or a staged copy
+  const void* x_staged = nullptr;  // the staged copy x reads (staged_acquire), released by plan_destroy
   int64_t* src_col = nullptr;
   int64_t* out_pos = nullptr;
   double *off = nullptr, *qs = nullptr, *scl = nullptr;
@@ -227,6 +228,7 @@ struct Plan {
   // the row guard's quantised operands and mean correction are the first
   // step's (one plan over every continuous column): pass 1 takes them
   bool corr_ready = false;
+  bool guard_pending = false;       // the row guard waits for the first pass 1 (P.defer_guard)
   std::vector<char> colmin, colmax; // per input column, x's dtype (device-measured)
   // reference-order accumulation (P.ref_accum, fs_refacc.hip): the kept
   // columns of X (float32 [n_pad][Kp]), their recip / discreteness, the
@@ -287,10 +289,17 @@ inline int launch_check(const char* what) {
 // ---------------------------------------------------------------------------
 // Entry points between units
 // ---------------------------------------------------------------------------
+// fs_gpu_mem.hip: pooled streams (non-blocking) and events (timing or not)
+hipStream_t stream_get(int device);
+void stream_put(int device, hipStream_t s);
+hipEvent_t event_get(int device, bool timing);
+void event_put(int device, hipEvent_t e, bool timing);
 // fs_pass1.hip
 int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats);
 int calibrate_band(Plan* g);
 int row_guard(Plan* g);
+// after a 32-bit switch: the operand scale and sort key on the device
+int apply_operand_width(Plan* g);
 int run_quantize_dist(Plan* g);
 int plan_score_surf(Plan* g, double* sums_dev);
 // fs_pass2.hip

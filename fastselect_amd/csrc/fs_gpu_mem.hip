@@ -190,11 +190,95 @@ void dev_cache_release() {
 }
 
 // ---------------------------------------------------------------------------
+// Stream and event pool: a plan takes two streams and eight events, and
+// creating and destroying them cost ~1 ms per fit; released ones are kept
+// per device (idle: every plan synchronises its streams before returning
+// them) and handed to the next plan.
+// ---------------------------------------------------------------------------
+namespace {
+std::mutex pool_mu;
+std::map<int, std::vector<hipStream_t>> stream_pool;
+std::map<std::pair<int, bool>, std::vector<hipEvent_t>> event_pool;
+constexpr size_t kPoolCap = 16;
+}  // namespace
+
+hipStream_t stream_get(int device) {
+  {
+    std::lock_guard<std::mutex> lk(pool_mu);
+    auto& v = stream_pool[device];
+    if (!v.empty()) {
+      hipStream_t s = v.back();
+      v.pop_back();
+      return s;
+    }
+  }
+  hipStream_t s = nullptr;
+  if (hipSetDevice(device) != hipSuccess ||
+      hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("hipStreamCreate failed");
+    return nullptr;
+  }
+  return s;
+}
+
+void stream_put(int device, hipStream_t s) {
+  if (!s) return;
+  {
+    std::lock_guard<std::mutex> lk(pool_mu);
+    auto& v = stream_pool[device];
+    if (v.size() < kPoolCap) {
+      v.push_back(s);
+      return;
+    }
+  }
+  (void)hipStreamDestroy(s);
+}
+
+hipEvent_t event_get(int device, bool timing) {
+  {
+    std::lock_guard<std::mutex> lk(pool_mu);
+    auto& v = event_pool[{device, timing}];
+    if (!v.empty()) {
+      hipEvent_t e = v.back();
+      v.pop_back();
+      return e;
+    }
+  }
+  hipEvent_t e = nullptr;
+  if (hipSetDevice(device) != hipSuccess ||
+      (timing ? hipEventCreate(&e) : hipEventCreateWithFlags(&e, hipEventDisableTiming)) !=
+          hipSuccess) {
+    (void)hipGetLastError();
+    set_error("hipEventCreate failed");
+    return nullptr;
+  }
+  return e;
+}
+
+void event_put(int device, hipEvent_t e, bool timing) {
+  if (!e) return;
+  {
+    std::lock_guard<std::mutex> lk(pool_mu);
+    auto& v = event_pool[{device, timing}];
+    if (v.size() < 4 * kPoolCap) {
+      v.push_back(e);
+      return;
+    }
+  }
+  (void)hipEventDestroy(e);
+}
+
+// ---------------------------------------------------------------------------
 // Staged X: an estimator's fit uploads X once (fs_stage_x) and both the
-// column statistics and the scoring plan read that copy; the plan takes its
-// own by a device-to-device copy.  The caller keeps the host array unchanged
-// until fs_unstage_x.  Saves one host-to-device copy of X per fit (1.6 GB at
-// cfg4, 4 GB of float64 at cfg5).
+// column statistics and the scoring plans read that copy in place (a plan
+// holds a reference: staged_acquire / staged_release, so fs_unstage_x while a
+// plan lives defers the free to the last release).  The caller keeps the
+// host array unchanged until fs_unstage_x.  Saves one host-to-device copy of
+// X per fit (1.6 GB at cfg4, 4 GB of float64 at cfg5) and the plan's own
+// device copy.  A copy made by fs_stage_x_cast also carries its column
+// extrema, taken by the casting threads, so that neither the column
+// statistics nor the plan measure them again.
 // ---------------------------------------------------------------------------
 namespace {
 struct Staged {
@@ -205,6 +289,9 @@ struct Staged {
   std::thread::id owner;  // only the staging thread's calls read it (concurrent
                           // fits of one array stage and free their own copies)
   bool borrowed;          // caller-owned device copy (stage_x_device): not freed
+  int refs = 0;           // plans reading it (staged_acquire)
+  bool released = false;  // fs_unstage_x came while refs > 0: freed by the last release
+  std::vector<char> cmin, cmax;  // column extrema in X's dtype (empty: not known)
 };
 std::mutex staged_mu;
 std::vector<Staged> staged;
@@ -228,7 +315,7 @@ int stage_x(int device, const void* x, int x_is_f64, int64_t n, int64_t p, uint6
   }
   std::lock_guard<std::mutex> lk(staged_mu);
   staged.push_back(
-      Staged{x, n, p, x_is_f64 ? 1 : 0, device, d, std::this_thread::get_id(), false});
+      Staged{x, n, p, x_is_f64 ? 1 : 0, device, d, std::this_thread::get_id(), false, 0, false, {}, {}});
   *handle = (uint64_t)(uintptr_t)d;
   return FS_OK;
 }
@@ -249,7 +336,7 @@ int stage_x_device(int device, const void* x, const void* x_dev, int x_is_f64, i
       return FS_EINVAL;
     }
   staged.push_back(Staged{x, n, p, x_is_f64 ? 1 : 0, device, const_cast<void*>(x_dev),
-                          std::this_thread::get_id(), true});
+                          std::this_thread::get_id(), true, 0, false, {}, {}});
   *handle = (uint64_t)(uintptr_t)x_dev;
   return FS_OK;
 }
@@ -284,32 +371,52 @@ int stage_x_cast(int device, const void* x, int x_is_f64, int64_t n, int64_t p, 
   }
   const int64_t blk_rows = std::max<int64_t>(1, (int64_t(8) << 20) / p);
   const int64_t nblk = (n + blk_rows - 1) / blk_rows;
+  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(hardware_threads(n_jobs), nblk));
+  // per-thread column extrema of the float32 values (merged below): what
+  // x32.min(0) / x32.max(0) give, for the column statistics and the plans
+  std::vector<std::vector<float>> tmin((size_t)nt), tmax((size_t)nt);
   std::vector<char> done((size_t)nblk, 0);
   std::mutex mu;
   std::condition_variable cv;
   std::atomic<int64_t> next{0};
   std::atomic<int> bad{0};
-  auto work = [&]() {
+  auto work = [&](int w) {
+    std::vector<float>& mn = tmin[(size_t)w];
+    std::vector<float>& mx = tmax[(size_t)w];
     for (int64_t b = next++; b < nblk; b = next++) {
-      const int64_t lo = b * blk_rows * p, hi = std::min(n, (b + 1) * blk_rows) * p;
+      const int64_t r0 = b * blk_rows, r1 = std::min(n, (b + 1) * blk_rows);
+      if (mn.empty()) {  // this thread's first row block seeds its extrema
+        mn.resize((size_t)p);
+        mx.resize((size_t)p);
+        for (int64_t c = 0; c < p; c++)
+          mn[c] = mx[c] = x_is_f64 ? (float)((const double*)x)[r0 * p + c]
+                                   : ((const float*)x)[r0 * p + c];
+      }
+      float* __restrict__ lo_ = mn.data();
+      float* __restrict__ hi_ = mx.data();
       uint32_t any = 0;
-      if (x_is_f64) {
-        const double* xd = (const double*)x;
-        for (int64_t i = lo; i < hi; i++) {
-          const float v = (float)xd[i];  // round to nearest, as numpy's astype
-          out[i] = v;
-          uint32_t u;
-          std::memcpy(&u, &v, 4);
-          any |= (uint32_t)((u & 0x7f800000u) == 0x7f800000u);
+      for (int64_t r = r0; r < r1; r++) {
+        float* __restrict__ o = out + r * p;
+        if (x_is_f64) {
+          const double* __restrict__ xd = (const double*)x + r * p;
+          for (int64_t c = 0; c < p; c++) {
+            const float v = (float)xd[c];  // round to nearest, as numpy's astype
+            o[c] = v;
+            lo_[c] = v < lo_[c] ? v : lo_[c];
+            hi_[c] = v > hi_[c] ? v : hi_[c];
+          }
+        } else {
+          const float* __restrict__ xf = (const float*)x + r * p;
+          for (int64_t c = 0; c < p; c++) {
+            const float v = xf[c];
+            o[c] = v;
+            lo_[c] = v < lo_[c] ? v : lo_[c];
+            hi_[c] = v > hi_[c] ? v : hi_[c];
+          }
         }
-      } else {
-        const uint32_t* xu = (const uint32_t*)x;
-        uint32_t* ou = (uint32_t*)out;
-        for (int64_t i = lo; i < hi; i++) {
-          const uint32_t u = xu[i];
-          ou[i] = u;
-          any |= (uint32_t)((u & 0x7f800000u) == 0x7f800000u);
-        }
+        // non-finite values: the row's exponent bits (one pass over what was written)
+        const uint32_t* ou = (const uint32_t*)o;
+        for (int64_t c = 0; c < p; c++) any |= (uint32_t)((ou[c] & 0x7f800000u) == 0x7f800000u);
       }
       if (any) bad.store(1, std::memory_order_relaxed);
       {
@@ -319,10 +426,9 @@ int stage_x_cast(int device, const void* x, int x_is_f64, int64_t n, int64_t p, 
       cv.notify_all();
     }
   };
-  const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(hardware_threads(n_jobs), nblk));
   std::vector<std::thread> th;
   th.reserve(nt);
-  for (int w = 0; w < nt; w++) th.emplace_back(work);
+  for (int w = 0; w < nt; w++) th.emplace_back(work, w);
   bool copy_ok = d != nullptr;
   for (int64_t b = 0; b < nblk; b++) {
     {
@@ -351,8 +457,26 @@ int stage_x_cast(int device, const void* x, int x_is_f64, int64_t n, int64_t p, 
     d = nullptr;
   }
   if (d) {
+    Staged e{out, n, p, 0, device, d, std::this_thread::get_id(), false, 0, false, {}, {}};
+    if (*finite) {
+      std::vector<float> mn, mx;
+      for (int w = 0; w < nt; w++) {
+        if (tmin[(size_t)w].empty()) continue;
+        if (mn.empty()) {
+          mn = tmin[(size_t)w];
+          mx = tmax[(size_t)w];
+          continue;
+        }
+        for (int64_t c = 0; c < p; c++) {
+          mn[c] = tmin[(size_t)w][c] < mn[c] ? tmin[(size_t)w][c] : mn[c];
+          mx[c] = tmax[(size_t)w][c] > mx[c] ? tmax[(size_t)w][c] : mx[c];
+        }
+      }
+      e.cmin.assign((const char*)mn.data(), (const char*)(mn.data() + mn.size()));
+      e.cmax.assign((const char*)mx.data(), (const char*)(mx.data() + mx.size()));
+    }
     std::lock_guard<std::mutex> lk(staged_mu);
-    staged.push_back(Staged{out, n, p, 0, device, d, std::this_thread::get_id(), false});
+    staged.push_back(std::move(e));
     *handle = (uint64_t)(uintptr_t)d;
   }
   return FS_OK;
@@ -364,10 +488,14 @@ int unstage_x(uint64_t handle) {
   {
     std::lock_guard<std::mutex> lk(staged_mu);
     auto it = std::find_if(staged.begin(), staged.end(),
-                           [&](const Staged& e) { return e.dev == d; });
+                           [&](const Staged& e) { return e.dev == d && !e.released; });
     if (it == staged.end()) {
       set_error("fs_unstage_x: unknown handle");
       return FS_EINVAL;
+    }
+    if (it->refs > 0) {  // plans still read it: the last staged_release frees it
+      it->released = true;
+      return FS_OK;
     }
     borrowed = it->borrowed;
     staged.erase(it);
@@ -376,10 +504,51 @@ int unstage_x(uint64_t handle) {
   return FS_OK;
 }
 
+const void* staged_acquire(const void* host, int64_t n, int64_t p, int x_is_f64, int device) {
+  std::lock_guard<std::mutex> lk(staged_mu);
+  // only the library's own copies: a caller-owned one (stage_x_device) may
+  // be freed by its owner while a plan still lives, so plans copy those
+  for (Staged& e : staged)
+    if (!e.released && !e.borrowed && e.host == host && e.n == n && e.p == p &&
+        e.f64 == (x_is_f64 ? 1 : 0) && e.device == device &&
+        e.owner == std::this_thread::get_id()) {
+      e.refs++;
+      return e.dev;
+    }
+  return nullptr;
+}
+
+void staged_release(const void* dev) {
+  void* q = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(staged_mu);
+    auto it = std::find_if(staged.begin(), staged.end(), [&](const Staged& e) {
+      return e.dev == dev && e.refs > 0;
+    });
+    if (it == staged.end()) return;
+    if (--it->refs == 0 && it->released) {
+      if (!it->borrowed) q = it->dev;
+      staged.erase(it);
+    }
+  }
+  if (q) dev_free(q);  // the releasing plan synchronised its streams
+}
+
+bool staged_extrema(const void* dev, void* cmin, void* cmax) {
+  std::lock_guard<std::mutex> lk(staged_mu);
+  for (const Staged& e : staged)
+    if (e.dev == dev && !e.cmin.empty()) {
+      std::memcpy(cmin, e.cmin.data(), e.cmin.size());
+      std::memcpy(cmax, e.cmax.data(), e.cmax.size());
+      return true;
+    }
+  return false;
+}
+
 const void* staged_lookup(const void* host, int64_t n, int64_t p, int x_is_f64, int device) {
   std::lock_guard<std::mutex> lk(staged_mu);
   for (const Staged& e : staged)
-    if (e.host == host && e.n == n && e.p == p && e.f64 == (x_is_f64 ? 1 : 0) &&
+    if (!e.released && e.host == host && e.n == n && e.p == p && e.f64 == (x_is_f64 ? 1 : 0) &&
         e.device == device && e.owner == std::this_thread::get_id())
       return e.dev;
   return nullptr;

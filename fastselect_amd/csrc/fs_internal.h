@@ -108,6 +108,11 @@ struct Prepared {
   // MultiSURF then takes 32-bit pass-1 operands and exact thresholds for
   // every flagged row, however many.
   int ref_accum = 0;
+  // 1: the row guard (fs_pass1.hip row_guard) of a plan over every continuous
+  // column is decided after its first pass 1, from the correction that pass
+  // computes beside k_dist, instead of before it (one-shot calls; a plan
+  // switched to 32-bit operands then runs pass 1 again)
+  int defer_guard = 0;
 };
 
 // Accumulation mode of the calling thread's next calls (fs_api.cpp,
@@ -429,6 +434,13 @@ int stage_x_device(int device, const void* x, const void* x_dev, int x_is_f64, i
                    int64_t p, uint64_t* handle);
 int unstage_x(uint64_t handle);
 const void* staged_lookup(const void* host, int64_t n, int64_t p, int x_is_f64, int device);
+// staged_lookup of a library-owned copy (fs_stage_x, fs_stage_x_cast) plus a
+// reference that keeps it alive past fs_unstage_x until staged_release
+// (plans read such copies in place); nullptr for caller-owned copies
+const void* staged_acquire(const void* host, int64_t n, int64_t p, int x_is_f64, int device);
+void staged_release(const void* dev);
+// the column extrema of a staged copy (X's dtype, p values each), when known
+bool staged_extrema(const void* dev, void* cmin, void* cmax);
 int column_stats(const void* x, int x_is_f64, int64_t n, int64_t p, int64_t cap, int device,
                  void* colmin, void* colmax, int64_t* ndistinct);
 // Column minima / maxima of a device-resident X, copied to host arrays in

@@ -932,43 +932,12 @@ static int run_colsort(Plan* g, int64_t c_lo, int64_t c_hi, hipStream_t s) {
 // deviations turns the 16-bit operands off (32-bit: 256x smaller errors).
 // Every rank computes the same full correction, so every rank decides alike.
 // ~5 ms per fit at cfg4, none per step; the q16_guard_off test hook disables it.
-int row_guard(Plan* g) {
+// The row guard's decision from the host copy of corr (every continuous
+// column): a row whose mean is off by more than the limit keeps 32-bit
+// operands (the plan's scale is switched here; the caller re-uploads it).
+static int row_guard_decide(Plan* g, const std::vector<double>& h, bool* switched) {
   Prepared& Q = g->P;
-  if (!Q.q16 || Q.pc == 0 || Q.n < 2 || Q.algo == ALGO_SURF || test_hooks().q16_guard_off)
-    return FS_OK;
-  // a plan over every continuous column (one rank, one shard) keeps the
-  // guard's work for its first pass 1: operands, terms and the correction
-  // itself (g->corr) are what that pass would compute again
-  const bool reuse = g->c_lo == 0 && g->c_hi == Q.pc;
-  double* corr = g->corr;
-  if (!reuse) FS_TRY(dev_alloc((void**)&corr, sizeof(double) * Q.n_pad, g->device));
-  dim3 gq((unsigned)(Q.PW / 64), (unsigned)(Q.n_pad / 64));
-  int rc = FS_OK;
-  if (g->x_is_f64)
-    k_quantize<double><<<gq, 256, 0, g->stream>>>(
-        (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
-        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, 0, Q.pc, g->xqT, g->xs, g->epsT);
-  else
-    k_quantize<float><<<gq, 256, 0, g->stream>>>(
-        (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
-        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, 0, Q.pc, g->xqT, g->xs, g->epsT);
-  rc = launch_check("k_quantize (row guard)");
-  if (!rc) {
-    rc = run_colsort(g, 0, Q.pc, g->stream);
-  }
-  if (!rc) {
-    rc = run_rowcorr(g, 0, Q.pc, corr, g->stream);
-  }
-  std::vector<double> h((size_t)Q.n);
-  if (!rc && (hipMemcpyAsync(h.data(), corr, sizeof(double) * Q.n, hipMemcpyDeviceToHost,
-                             g->stream) != hipSuccess ||
-              hipStreamSynchronize(g->stream) != hipSuccess)) {
-    (void)hipGetLastError();
-    set_error("row guard: device-to-host copy failed");
-    rc = FS_EHIP;
-  }
-  if (!reuse) dev_free(corr);
-  if (rc) return rc;
+  *switched = false;
   double worst = 0.0;
   for (double c : h) worst = std::max(worst, std::fabs(c) / (double)(Q.n - 1));
   const double limit = 12.0 * std::sqrt((double)Q.pc / 36.0 + 1.0);
@@ -982,8 +951,7 @@ int row_guard(Plan* g) {
     g->calib[1] = g->cal32[0];
     g->calib[2] = g->cal32[1];
     g->calib[4] = Q.amb_delta / Q.amb_delta_model;
-  } else {
-    g->corr_ready = reuse;
+    *switched = true;
   }
   if (trace_on()) {
     char msg[160];
@@ -991,6 +959,58 @@ int row_guard(Plan* g) {
              limit, Q.q16);
     trace_mark(msg);
   }
+  return FS_OK;
+}
+
+static int copy_corr(Plan* g, const double* corr, std::vector<double>& h) {
+  h.resize((size_t)g->P.n);
+  if (hipMemcpyAsync(h.data(), corr, sizeof(double) * g->P.n, hipMemcpyDeviceToHost,
+                     g->stream) != hipSuccess ||
+      hipStreamSynchronize(g->stream) != hipSuccess) {
+    (void)hipGetLastError();
+    set_error("row guard: device-to-host copy failed");
+    return FS_EHIP;
+  }
+  return FS_OK;
+}
+
+int row_guard(Plan* g) {
+  Prepared& Q = g->P;
+  g->guard_pending = false;
+  if (!Q.q16 || Q.pc == 0 || Q.n < 2 || Q.algo == ALGO_SURF || test_hooks().q16_guard_off)
+    return FS_OK;
+  // a plan over every continuous column (one rank, one shard) keeps the
+  // guard's work for its first pass 1: operands, terms and the correction
+  // itself (g->corr) are what that pass would compute again
+  const bool reuse = g->c_lo == 0 && g->c_hi == Q.pc;
+  if (reuse && Q.defer_guard && !Q.ref_accum) {
+    // decided after the first pass 1 instead (plan_pass1), whose correction
+    // runs beside k_dist on the side stream rather than before it
+    g->guard_pending = true;
+    return FS_OK;
+  }
+  double* corr = g->corr;
+  if (!reuse) FS_TRY(dev_alloc((void**)&corr, sizeof(double) * Q.n_pad, g->device));
+  dim3 gq((unsigned)(Q.PW / 64), (unsigned)(Q.n_pad / 64));
+  int rc = FS_OK;
+  if (g->x_is_f64)
+    k_quantize<double><<<gq, 256, 0, g->stream>>>(
+        (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
+        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, 0, Q.pc, g->xqT, g->xs, g->epsT);
+  else
+    k_quantize<float><<<gq, 256, 0, g->stream>>>(
+        (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
+        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, 0, Q.pc, g->xqT, g->xs, g->epsT);
+  rc = launch_check("k_quantize (row guard)");
+  if (!rc) rc = run_colsort(g, 0, Q.pc, g->stream);
+  if (!rc) rc = run_rowcorr(g, 0, Q.pc, corr, g->stream);
+  std::vector<double> h;
+  if (!rc) rc = copy_corr(g, corr, h);
+  if (!reuse) dev_free(corr);
+  if (rc) return rc;
+  bool switched = false;
+  FS_TRY(row_guard_decide(g, h, &switched));
+  if (!switched) g->corr_ready = reuse;
   return FS_OK;
 }
 
@@ -1077,6 +1097,20 @@ int plan_pass1(Plan* g, double* rowstats) {
     FS_TRY(launch_check("k_tile_rowstats"));
   }
   FS_HIP(hipStreamWaitEvent(g->stream, g->ev_join, 0));  // corr (side stream)
+  if (g->guard_pending) {
+    // the deferred row guard (P.defer_guard): this pass's correction covers
+    // every continuous column; a coherent row switches the plan to 32-bit
+    // operands and pass 1 runs again on them
+    g->guard_pending = false;
+    std::vector<double> h;
+    FS_TRY(copy_corr(g, g->corr, h));
+    bool switched = false;
+    FS_TRY(row_guard_decide(g, h, &switched));
+    if (switched) {
+      FS_TRY(apply_operand_width(g));
+      return plan_pass1(g, rowstats);
+    }
+  }
   k_rowstats_reduce<<<(unsigned)((Q.n + 255) / 256), 256, 0, g->stream>>>(
       g->rspart, Q.n, g->nb, g->rank, g->world, g->corr, rowstats);
   FS_TRY(launch_check("k_rowstats_reduce"));

@@ -19,12 +19,12 @@ void plan_destroy(Plan* g) {
   if (g->rkeys) dev_free(g->rkeys);
   if (g->sched) dev_free(g->sched);
   if (g->units8) dev_free(g->units8);
-  for (auto& e : g->ev)
-    if (e) (void)hipEventDestroy(e);
-  if (g->ev_fork) (void)hipEventDestroy(g->ev_fork);
-  if (g->ev_join) (void)hipEventDestroy(g->ev_join);
-  if (g->side) (void)hipStreamDestroy(g->side);
-  if (g->own_stream && g->stream) (void)hipStreamDestroy(g->stream);
+  if (g->x_staged) staged_release(g->x_staged);
+  for (auto& e : g->ev) event_put(g->device, e, true);
+  event_put(g->device, g->ev_fork, false);
+  event_put(g->device, g->ev_join, false);
+  stream_put(g->device, g->side);
+  if (g->own_stream) stream_put(g->device, g->stream);
   delete g;
   trace_mark("plan: free");
 }
@@ -152,12 +152,15 @@ int plan_layout(Plan* g) {
     if (g->colmin.empty()) {
       g->colmin.resize((size_t)Q.p_in * esz);
       g->colmax.resize((size_t)Q.p_in * esz);
-      if ((rc = column_minmax(g->x, g->x_is_f64, Q.n, Q.p_in, g->colmin.data(), g->colmax.data(),
-                              g->stream))) {
-        g->colmin.clear();
-        return rc;
+      // a staged copy's extrema were taken while it was cast (stage_x_cast)
+      if (!(g->x_staged && staged_extrema(g->x_staged, g->colmin.data(), g->colmax.data()))) {
+        if ((rc = column_minmax(g->x, g->x_is_f64, Q.n, Q.p_in, g->colmin.data(),
+                                g->colmax.data(), g->stream))) {
+          g->colmin.clear();
+          return rc;
+        }
+        trace_mark("plan: device ranges");
       }
-      trace_mark("plan: device ranges");
     }
     std::vector<double> cmin((size_t)Q.pc), cmax((size_t)Q.pc);
     for (int64_t c = 0; c < Q.pc; c++) {
@@ -212,12 +215,18 @@ int plan_layout(Plan* g) {
   if (Q.ref_accum && Q.algo != ALGO_SURF && (rc = ref_layout(g))) return rc;
   if ((rc = calibrate_band(g))) return rc;
   if ((rc = row_guard(g))) return rc;
-  if (g->calib[5] != 0.0) {
-    // the coherence guard switched to 32-bit operands: new scale and sort key
-    for (int64_t c = 0; c < Q.PW; c++) qs[c] = Q.scale[c] * Q.SC;
-    g->key_shift = colsort_key_shift(Q.qmax);
-    if ((rc = h2d(g, g->qs, qs.data(), Q.PW))) return rc;
-  }
+  if (g->calib[5] != 0.0 && (rc = apply_operand_width(g))) return rc;
+  FS_HIP(hipStreamSynchronize(g->stream));
+  return FS_OK;
+}
+
+int apply_operand_width(Plan* g) {
+  // the coherence guard switched to 32-bit operands: new scale and sort key
+  const Prepared& Q = g->P;
+  std::vector<double> qs(Q.PW, 0.0);
+  for (int64_t c = 0; c < Q.PW; c++) qs[c] = Q.scale[c] * Q.SC;
+  g->key_shift = colsort_key_shift(Q.qmax);
+  FS_TRY(h2d(g, g->qs, qs.data(), Q.PW));
   FS_HIP(hipStreamSynchronize(g->stream));
   return FS_OK;
 }
@@ -355,9 +364,8 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   if (stream) {
     g->stream = (hipStream_t)(uintptr_t)stream;
   } else {
-    if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (!(g->stream = stream_get(device))) {
       delete g;
-      set_error("hipStreamCreate failed");
       return FS_EHIP;
     }
     g->own_stream = true;
@@ -367,10 +375,9 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     return rc;
   };
   for (auto& e : g->ev)
-    if (hipEventCreate(&e) != hipSuccess) return fail(FS_EHIP);
-  if (hipStreamCreateWithFlags(&g->side, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&g->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&g->ev_join, hipEventDisableTiming) != hipSuccess)
+    if (!(e = event_get(device, true))) return fail(FS_EHIP);
+  if (!(g->side = stream_get(device)) || !(g->ev_fork = event_get(device, false)) ||
+      !(g->ev_join = event_get(device, false)))
     return fail(FS_EHIP);
   const Prepared& Q = g->P;
   g->nb = Q.n_pad / kTile;
@@ -391,7 +398,12 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   const size_t xbytes = (size_t)Q.n * Q.p_in * (x_is_f64 ? 8 : 4);
   int rc;
   trace_mark("plan: host setup");
-  if ((rc = dalloc(g, (char**)&g->x, xbytes)) || (rc = dalloc(g, &g->lab, Q.n_pad)) ||
+  // the library's staged copy of X (fs_stage_x, fs_stage_x_cast) is read in
+  // place, else X is copied from a caller's staged copy or uploaded
+  g->x_staged = staged_acquire(x, Q.n, Q.p_in, x_is_f64, g->device);
+  if (g->x_staged) g->x = const_cast<void*>(g->x_staged);
+  if ((!g->x_staged && (rc = dalloc(g, (char**)&g->x, xbytes))) ||
+      (rc = dalloc(g, &g->lab, Q.n_pad)) ||
       (rc = dalloc(g, &g->corr, Q.n_pad)) ||
       (rc = dalloc(g, &g->corr_part, (int64_t)kRowcorrMaxSlices * Q.n_pad)) ||
       (rc = dalloc(g, &g->thr, Q.n_pad)) ||
@@ -418,13 +430,15 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   trace_mark("plan: hipMalloc");
   std::vector<int32_t> lab(Q.n_pad, -1);
   std::copy(Q.labels.begin(), Q.labels.end(), lab.begin());
-  const void* sx = staged_lookup(x, Q.n, Q.p_in, x_is_f64, g->device);
+  // a caller-owned staged copy (fs_stage_x_device) is copied: its owner may
+  // free it while the plan lives
+  const void* sx = g->x_staged ? nullptr : staged_lookup(x, Q.n, Q.p_in, x_is_f64, g->device);
   if (sx && hipMemcpyAsync(g->x, sx, xbytes, hipMemcpyDeviceToDevice, g->stream) != hipSuccess) {
     (void)hipGetLastError();
     set_error("plan: device-to-device copy of the staged X failed");
     return fail(FS_EHIP);
   }
-  if ((!sx && (rc = h2d(g, (char*)g->x, (const char*)x, xbytes))) ||
+  if ((!g->x_staged && !sx && (rc = h2d(g, (char*)g->x, (const char*)x, xbytes))) ||
       (rc = h2d(g, g->lab, lab.data(), Q.n_pad)))
     return fail(rc);
   if (Q.algo == ALGO_RELIEFF) {
@@ -693,7 +707,9 @@ int multisurf_run(const Prepared& P, const void* x, int device, float* scores_ou
   g_last_risk = -1.0;
   g_last_rerun = 0;
   const int shards = multisurf_shards(P, device, 1);
-  FS_TRY(plan_create(&g, P, x, 0, device, 0, shards, 0));
+  Prepared Q = P;
+  Q.defer_guard = 1;  // decided beside the first pass 1 (row_guard)
+  FS_TRY(plan_create(&g, Q, x, 0, device, 0, shards, 0));
   double *rs = nullptr, *cnt = nullptr, *sc = nullptr;
   int rc, switched = 0;
   double risk = -1.0;

@@ -73,3 +73,29 @@ def test_row_guard_takes_32bit_operands(F, name):
     cal = job.plan.calibration()
     job.close()
     assert cal["q16"] and not cal["guard"]
+
+
+@pytest.mark.parametrize("name", ["minrows_16k", "make_classification"])
+def test_one_shot_guard_after_pass1_matches_plan(F, name):
+    """The one-shot call decides the row guard after its first pass 1 (from
+    the correction computed beside k_dist; fs_pass1.hip plan_pass1), a plan
+    object before it: the operand width, and so the scores, are the same
+    bit for bit -- the coherent case switched to 32-bit operands by the
+    deferred guard, ordinary data kept on 16-bit ones."""
+    from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
+    if name == "make_classification":
+        from sklearn.datasets import make_classification
+        X, y = make_classification(n_samples=mk.N, n_features=mk.P, n_informative=20,
+                                   n_redundant=50, random_state=7)
+    else:
+        X, y = mk.make(name)
+    one_shot = F.MultiSURF(backend="gpu", n_features_to_select=10).fit(X, y).feature_importances_
+    x, yv, recip, isd = prepare_inputs(X, y, backend="gpu")
+    job = ShardedMultiSURF(x, yv, recip, isd, backend="gpu", shard=False)
+    try:
+        q16 = job.plan.calibration()["q16"]
+        stepped = job.step().cpu().numpy()
+    finally:
+        job.close()
+    assert bool(q16) == (name == "make_classification")
+    np.testing.assert_array_equal(one_shot, stepped)
