@@ -35,8 +35,8 @@
 //   k_ref_gather   kept columns of X into a 256-padded row-major copy.  HBM
 //   k_ref_masks    near-hit / miss-chain / far-miss bit masks per row and
 //                  64-sample word, one owned distance tile per workgroup. HBM
-//   k_ms_chains    the chains: 128 focal rows x 256 features per workgroup,
-//                  8 rows per wave, 4 features per lane, the 64-sample j
+//   k_ms_chains    the chains: 96 focal rows x 256 features per workgroup,
+//                  6 rows per wave, 4 features per lane, the 64-sample j
 //                  chunks staged HBM -> LDS by global_load_lds (double-
 //                  buffered); each wave walks its rows' mask bits in
 //                  ascending j: per entry one ds_read_b128 and 4 x
