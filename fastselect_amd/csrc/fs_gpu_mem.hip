@@ -479,6 +479,7 @@ int stage_x_cast(int device, const void* x, int x_is_f64, int64_t n, int64_t p, 
     staged.push_back(std::move(e));
     *handle = (uint64_t)(uintptr_t)d;
   }
+  trace_mark("stage: cast + upload of X");
   return FS_OK;
 }
 
