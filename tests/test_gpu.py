@@ -633,6 +633,40 @@ def test_staged_x_matches_uploads():
     np.testing.assert_array_equal(plain_sf, st_sf)
 
 
+def test_plan_outlives_its_staged_x():
+    """A plan reads the library's staged copy in place and holds a
+    reference to it: fs_unstage_x while the plan lives defers the free to
+    the plan's end, so later steps still score the same X (bit-identical to
+    a plan that uploaded X itself).  A copy cast by fs_stage_x_cast carries
+    its column extrema: the column statistics give x32.min(0) / x32.max(0)
+    exactly."""
+    from fastselect_amd import _lib
+    from fastselect_amd.parallel import ShardedMultiSURF
+    X, y = make_classification(n_samples=700, n_features=600, random_state=32)
+    x32 = np.ascontiguousarray(X, dtype=np.float32)
+    recip = (1 / (x32.max(0) - x32.min(0))).astype(np.float32)
+    isd = np.zeros(600, bool)
+    plain = ShardedMultiSURF(x32, y, recip, isd, backend="gpu", shard=False)
+    try:
+        ref = plain.step().cpu().numpy()
+    finally:
+        plain.close()
+    with _lib.staged_x("gpu", x32):
+        job = ShardedMultiSURF(x32, y, recip, isd, backend="gpu", shard=False)
+    try:
+        # the staged block has ended: the plan's reference keeps the copy
+        np.testing.assert_array_equal(job.step().cpu().numpy(), ref)
+        np.testing.assert_array_equal(job.step().cpu().numpy(), ref)
+    finally:
+        job.close()
+    xc, finite, h = _lib.stage_x_cast(X, -1, 0)
+    assert finite and h
+    with _lib.unstaged(h):
+        mn, mx, _ = _lib.column_stats("gpu", xc, 10)
+    np.testing.assert_array_equal(mn, x32.min(0))
+    np.testing.assert_array_equal(mx, x32.max(0))
+
+
 def test_concurrent_fits_on_one_array():
     """Fits of the same host array in several threads each stage and free
     their own device copy (staged X is per thread): results equal the
