@@ -68,8 +68,15 @@ int check(const char* what) {
 
 constexpr int kChunk = 64;   // samples j per staged chunk (one mask word)
 constexpr int kFeat = 256;   // features per workgroup (64 lanes x 4)
-constexpr int kWaves = 16;   // waves per k_ms_chains workgroup
-constexpr int kRowsW = 6;    // focal rows per wave
+#ifndef FS_CHAINS_WAVES
+#define FS_CHAINS_WAVES 16
+#endif
+#ifndef FS_CHAINS_ROWS
+#define FS_CHAINS_ROWS 6
+#endif
+constexpr int kWaves = FS_CHAINS_WAVES;  // waves per k_ms_chains workgroup
+constexpr int kRowsW = FS_CHAINS_ROWS;   // focal rows per wave
+static_assert(kChunk % kWaves == 0 && 4 * kRowsW <= 64, "k_ms_chains shape");
 constexpr int kRowsWG = kWaves * kRowsW;
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
@@ -209,21 +216,35 @@ __device__ __forceinline__ void chain_step(const float4 v, const float (&a)[4],
   }
 }
 
+// the lowest set bit of m, cleared: s_ff1 + s_bitset0 (2 SALU; the builtin
+// form, ctz and m &= m - 1, compiles to 5, and the chains are issue-bound
+// enough that this alone took k_ms_chains 195.5 -> 186.7 ms at cfg4,
+// profiles/r05/chains_ab.txt)
 __device__ __forceinline__ int pop_bit(uint64_t& m) {
-  const int b = __builtin_ctzll(m);
-  m &= m - 1;
+  int b;
+  asm("s_ff1_i32_b64 %0, %1\n\ts_bitset0_b64 %1, %0" : "=&s"(b), "+s"(m));
   return b;
 }
 
 // Walk the set bits of one 64-sample mask word in ascending j (the
-// reference's j loop) in groups of 4 entries: the group's four LDS row reads
-// are issued together ahead of its arithmetic (each step then waits only for
-// its own read, counted lgkmcnt), the last 1-3 entries likewise.
+// reference's j loop) in groups of 8, then 4 entries: the group's LDS row
+// reads are issued together ahead of its arithmetic (each step then waits
+// only for its own read, counted lgkmcnt), the last 1-3 entries likewise.
 template <bool SIGNED, bool DISC>
 __device__ __forceinline__ void chain_walk(uint64_t m, uint64_t neg, const float4* __restrict__ buf,
                                            int lane, const float (&a)[4], const float (&rc)[4],
                                            uint32_t dk, float (&acc)[4]) {
   auto sg = [&](int b) { return SIGNED && ((neg >> b) & 1ull) ? -1.0f : 1.0f; };
+  while (__builtin_popcountll(m) >= 8) {
+    int b[8];
+    float4 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) b[q] = pop_bit(m);
+#pragma unroll
+    for (int q = 0; q < 8; q++) v[q] = buf[b[q] * 64 + lane];
+#pragma unroll
+    for (int q = 0; q < 8; q++) chain_step<DISC>(v[q], a, rc, dk, sg(b[q]), acc);
+  }
   while (__builtin_popcountll(m) >= 4) {
     const int b0 = pop_bit(m), b1 = pop_bit(m), b2 = pop_bit(m), b3 = pop_bit(m);
     const float4 v0 = buf[b0 * 64 + lane], v1 = buf[b1 * 64 + lane];
@@ -369,7 +390,7 @@ __device__ __forceinline__ void chains_body(
 }
 
 template <bool STAR>
-__global__ __launch_bounds__(1024) void k_ms_chains(
+__global__ __launch_bounds__(64 * kWaves) void k_ms_chains(
     const float* __restrict__ xk, int64_t Kp, const float* __restrict__ krecip,
     const uint8_t* __restrict__ kdisc, const uint8_t* __restrict__ blkdisc,
     const uint64_t* __restrict__ masks, int64_t nw, int64_t nch, const double* __restrict__ counts,

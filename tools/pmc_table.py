@@ -10,7 +10,7 @@ def main(d):
     for f in glob.glob(f"{d}/*/run_counter_collection.csv"):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("void ", "")
-            k = k.split("(")[0].replace("fs::gpu::", "")
+            k = k.split("(")[0].replace("fs::gpu::", "").replace("refacc::", "")
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     for k, c in vals.items():
         if not k.startswith("k_"):
