@@ -847,7 +847,7 @@ s36..s99 as the v1 JIT loop.
 """
 
 
-def gen_v2(name, F=8, lead=4, diag="", grp=1, pfn=True, tprof=False):
+def gen_v2(name, F=8, lead=4, diag="", grp=1, pfn=True, tprof=False, salu_pad=0):
     """diag (A/B diagnostics only, wrong scores): "lds1" skips the chunk-1
     row read (half the LDS traffic), "nosub" drops the v_sub_f32 (half the
     VALU), "nolds" skips every row read (the slots keep stale values).
@@ -888,6 +888,9 @@ def gen_v2(name, F=8, lead=4, diag="", grp=1, pfn=True, tprof=False):
         a = slot(e)
         L_ = [] if diag == "nosub" else [f"v_sub_f32 v{a + f}, v{a + f}, v{BCUR + f}" for f in range(F)]
         L_ += [f"v_fma_f32 %[acc{f}], s{w}, |v{a + f}|, %[acc{f}]" for f in range(F)]
+        # A/B diagnostics only: salu_pad extra SALU instructions per entry
+        # (results unchanged) price the per-entry scalar work of the walk
+        L_ += ["s_mov_b32 s29, s28"] * salu_pad
         return L_
 
     ntm = " nt" if diag == "bnt" else ""   # A/B: B rows as non-temporal loads
