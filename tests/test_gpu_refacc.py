@@ -171,18 +171,20 @@ def test_fullsize_bitexact(F, name, algo, kw):
     assert_bitexact(est.feature_importances_, fx["scores"])
 
 
-def test_cfg4_decisions_row_by_row(F):
-    """the north-star data's near / far decisions row by
-    row against the oracle's (tests/golden/fullsize_cfg4_multisurf_decisions
-    .npz, oracle_multisurf_decisions on the 20000 x 20000 input).  Reference
-    order (32-bit operands, every flagged row's threshold exact): every row
-    identical.  The default path (16-bit operands; 2070 rows flagged, above
-    the exact-threshold budget, so their thresholds stay quantised): the
-    flipped rows are counted and bounded -- 22 measured (one near pair each),
-    reported by bench.py as decisions_vs_reference."""
+@pytest.mark.parametrize("name,fast_bound", [("cfg2_multisurf", 0), ("cfg4_multisurf", 40)])
+def test_decisions_row_by_row(F, name, fast_bound):
+    """near / far decisions row by row against the
+    oracle's (tests/golden/fullsize_<cfg>_multisurf_decisions.npz,
+    oracle_multisurf_decisions on the full-size input).  Reference order
+    (32-bit operands, every flagged row's threshold exact): every row
+    identical.  The default path: cfg2 (32-bit operands, the flagged rows
+    within the exact-threshold budget) identical too; cfg4 (16-bit operands;
+    2070 rows flagged, above the budget, so their thresholds stay quantised)
+    counted and bounded -- 22 measured (one near pair each), reported by
+    bench.py as decisions_vs_reference."""
     from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
-    dec = np.load(os.path.join(GOLD, "fullsize_cfg4_multisurf_decisions.npz"), allow_pickle=False)
-    fx = _fixture("cfg4_multisurf")
+    dec = np.load(os.path.join(GOLD, f"fullsize_{name}_decisions.npz"), allow_pickle=False)
+    fx = _fixture(name)
     X, y = _inputs(fx)
     assert str(dec["x_sha256"]) == str(fx["x_sha256"])
     ref = dec["counts"].astype(np.int64).reshape(-1, 2)
@@ -196,6 +198,6 @@ def test_cfg4_decisions_row_by_row(F):
         finally:
             job.close()
         flipped[mode] = int(np.sum(np.any(got != ref, axis=1)))
-    print("cfg4 rows decided differently from the reference:", flipped)
+    print(name, "rows decided differently from the reference:", flipped)
     assert flipped["reference"] == 0
-    assert flipped["fast"] <= 40
+    assert flipped["fast"] <= fast_bound
