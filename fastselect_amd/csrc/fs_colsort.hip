@@ -206,7 +206,7 @@ struct ColbinSmem {
   // phases 3-4: the mixed bins' entries (low key << 12 | eps code) in bin
   // order at their sorted positions; phase 5: the packed within-bin counts
   alignas(16) uint32_t seg[(kCsThreads * IPT > kBins ? kCsThreads * IPT : kBins) + 4];
-  alignas(8) uint32_t starts[(kCsThreads * IPT + 31) / 32];  // bit p: a non-empty bin starts at p (read 64 bits at a time)
+  uint32_t starts[(kCsThreads * IPT + 31) / 32];  // bit p: a non-empty bin starts at p
   uint32_t skip[(kCsThreads * IPT + 31) / 32];    // bit p: p's bin is pure or single
   uint32_t binskip[kBins / 32];                   // bit b: bin b is pure, single or empty
   long long wsum[kCsThreads / 64];
@@ -365,37 +365,22 @@ __global__ __launch_bounds__(kCsThreads) void k_colsort(const uint32_t* __restri
   int32_t res[IPT];
   int t4 = tid;
   FS_OPAQUE(t4);
-  const int lane4 = t4 & 63;
 #pragma unroll
   for (int k = 0; k < IPT; k++) {
     const int j = t4 + kCsThreads * k;
     res[k] = 0;
     if (j >= nn || ((sm.skip[j >> 5] >> (j & 31)) & 1u)) continue;
-    // the wave's 64 consecutive positions [j0, j0 + 64) are one 64-bit word
-    // of the bin-start bitmap (j0 a multiple of 64): a bin's start and end
-    // inside it come from bit scans of that word; only a bin that begins
-    // before j0 or ends past j0 + 63 walks the neighbouring words
-    const int j0 = j - lane4;
-    const uint64_t win = ((const uint64_t*)sm.starts)[j0 >> 6];
-    const uint64_t upto = lane4 == 63 ? ~0ull : ((2ull << lane4) - 1ull);  // bits 0..lane
-    int lo, hi;
-    if (win & upto) {
-      lo = j0 + 63 - __clzll(win & upto);
-    } else {  // the bin starts before the window (<= 64 positions back)
-      int w = (j0 >> 5) - 1;
-      uint32_t bits = sm.starts[w];
-      while (bits == 0u) bits = sm.starts[--w];
-      lo = w * 32 + 31 - __clz(bits);
-    }
-    if (win & ~upto) {
-      hi = min(nn, j0 + __ffsll((unsigned long long)(win & ~upto)) - 1);
-    } else {  // the next bin starts past the window, or none does
-      hi = nn;
-      int w = (j0 >> 5) + 2;
-      uint32_t bits = 0u;
-      while (bits == 0u && w < kWords && w * 32 < nn) bits = sm.starts[w++];
-      if (bits != 0u) hi = min(nn, (w - 1) * 32 + __ffs(bits) - 1);
-    }
+    // bin start: the last start bit at or before j (<= 64 positions back)
+    int w = j >> 5;
+    uint32_t bits = sm.starts[w] & (0xFFFFFFFFu >> (31 - (j & 31)));
+    while (bits == 0u) bits = sm.starts[--w];
+    const int lo = w * 32 + 31 - __clz(bits);
+    // bin end: the next start bit after j, or n
+    int hi = nn;
+    w = j >> 5;
+    bits = (j & 31) == 31 ? 0u : sm.starts[w] & (0xFFFFFFFFu << ((j & 31) + 1));
+    while (bits == 0u && ++w < kWords && w * 32 < nn) bits = sm.starts[w];
+    if (bits != 0u) hi = min(nn, w * 32 + __ffs(bits) - 1);
     const uint32_t v = sm.seg[j];
     const uint32_t mine_lo = v & ~0xFFFu, mine_hi = v | 0xFFFu;
     uint32_t a_lt = 0u, a_le = 0u, a_all = 0u;
