@@ -66,7 +66,10 @@ int check(const char* what) {
   return FS_OK;
 }
 
-constexpr int kChunk = 64;   // samples j per staged chunk (one mask word)
+#ifndef FS_CHAINS_CHUNK
+#define FS_CHAINS_CHUNK 64
+#endif
+constexpr int kChunk = FS_CHAINS_CHUNK;  // samples j per staged chunk (a mask word, or half of one)
 constexpr int kFeat = 256;   // features per workgroup (64 lanes x 4)
 #ifndef FS_CHAINS_WAVES
 #define FS_CHAINS_WAVES 16
@@ -76,7 +79,14 @@ constexpr int kFeat = 256;   // features per workgroup (64 lanes x 4)
 #endif
 constexpr int kWaves = FS_CHAINS_WAVES;  // waves per k_ms_chains workgroup
 constexpr int kRowsW = FS_CHAINS_ROWS;   // focal rows per wave
-static_assert(kChunk % kWaves == 0 && 4 * kRowsW <= 64, "k_ms_chains shape");
+static_assert(kChunk % kWaves == 0 && 4 * kRowsW <= 64 && (kChunk == 64 || kChunk == 32),
+              "k_ms_chains shape");
+
+// chunk c's bits of a row's mask words (kChunk = 32: half a 64-sample word)
+__device__ __forceinline__ uint64_t chunk_word(const uint64_t* mrow, int64_t c) {
+  if (kChunk == 64) return mrow[c * 4];
+  return (mrow[(c >> 1) * 4] >> ((c & 1) * 32)) & 0xFFFFFFFFull;
+}
 constexpr int kRowsWG = kWaves * kRowsW;
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
@@ -349,13 +359,13 @@ __device__ __forceinline__ void chains_body(
   const bool mload = lane < 4 * kRowsW && row0 + mr < r_hi;
   const uint64_t* mrow = masks + ((size_t)(row0 + (mload ? mr : 0)) * nw) * 4 + mt;
 
-  uint64_t mw = mload ? mrow[0] : 0ull;
+  uint64_t mw = mload ? chunk_word(mrow, 0) : 0ull;
   stage_chunk(xk, Kp, f0, wave, lane, bufA, 0);
   __syncthreads();
   for (int64_t c = 0; c < nch; c += 2) {
     uint64_t mn = 0;
     if (c + 1 < nch) {
-      mn = mload ? mrow[(c + 1) * 4] : 0ull;
+      mn = mload ? chunk_word(mrow, c + 1) : 0ull;
       stage_chunk(xk, Kp, f0, wave, lane, bufB, c + 1);
     }
     chunk_rows<STAR, DISC>(bufA, mw, lane, a, rc, dk, ah, am);
@@ -363,7 +373,7 @@ __device__ __forceinline__ void chains_body(
     if (c + 1 >= nch) break;
     mw = mn;
     if (c + 2 < nch) {
-      mn = mload ? mrow[(c + 2) * 4] : 0ull;
+      mn = mload ? chunk_word(mrow, c + 2) : 0ull;
       stage_chunk(xk, Kp, f0, wave, lane, bufA, c + 2);
     }
     chunk_rows<STAR, DISC>(bufB, mw, lane, a, rc, dk, ah, am);
