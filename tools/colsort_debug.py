@@ -1,7 +1,8 @@
 """Large-n route of the column sort (fs_colsort.hip) against the CPU
 backend's exact correction: per-row corrections of a GPU plan and a CPU plan
-on the same lognormal data, LDS route and FS_COLSORT_GLOBAL=1 route.
-Run on the GPU box:  python tools/colsort_debug.py [n p]"""
+on the same lognormal data, LDS route or (third argument "global") the
+large-n route forced by the colsort_global test hook.
+Run on the GPU box:  python tools/colsort_debug.py [n p [global]]"""
 import os
 import sys
 
@@ -11,10 +12,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
 from test_meancorr import lognormal  # noqa: E402
 
-from fastselect_amd import parallel  # noqa: E402
+from fastselect_amd import _lib, parallel  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 3000
 p = int(sys.argv[2]) if len(sys.argv) > 2 else 64
+glob_route = len(sys.argv) > 3 and sys.argv[3] == "global"
+if glob_route:
+    _lib.set_test_hook("colsort_global", 1)
 X, y = lognormal(n, p, seed=7)
 out = {}
 for be in ("cpu", "gpu"):
@@ -25,7 +29,7 @@ for be in ("cpu", "gpu"):
     out[be] = (rs, job.plan.calibration())
     job.close()
 (rc, cc), (rg, cg) = out["cpu"], out["gpu"]
-print("route", "global" if os.environ.get("FS_COLSORT_GLOBAL") == "1" else "auto",
+print("route", "global" if glob_route else "auto",
       "n", n, "p", p, "q16 gpu", cg["q16"], "SC cpu/gpu", cc["SC"], cg["SC"])
 print("corr cpu", rc[:4, 2], "gpu", rg[:4, 2])
 print("s1 cpu", rc[:4, 0], "gpu", rg[:4, 0])
