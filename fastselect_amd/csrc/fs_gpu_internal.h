@@ -248,6 +248,7 @@ struct Plan {
   float* rkeys = nullptr;       // ReliefF neighbour keys (own block)
   size_t rkeys_cap = 0;
   bool ref_seeded = false;      // ReliefF: the column sums continue from the sums buffer
+  double* risk_dev = nullptr;   // plan_decision_guard's result (owned, allocated on first use)
 };
 
 template <typename T>

@@ -633,29 +633,54 @@ constexpr double kQ16MaxRisk = 5e-6;
 thread_local double g_last_risk = -1.0;
 thread_local int g_last_rerun = 0;
 
-static double q16_decision_risk(const Prepared& P, const double* rs, const double* cnt,
-                                const double* sums) {
-  const double n = (double)P.n, nm1 = n - 1.0;
-  double smax = 0.0;
-  for (int64_t k = 0; k < P.n_kept; k++)
-    smax = std::max(smax, (double)std::fabs((float)(sums[k] / n)));
-  const double nfeat = (double)(P.pc + P.pd);
-  if (n < 3.0 || nfeat <= 0.0 || P.SC <= 0.0) return 0.0;
-  if (smax <= 0.0) return HUGE_VAL;
-  const double thr_err = std::sqrt((double)P.pc / 6.0 + 1.0) / std::sqrt(n);
-  double mu_sum = 0.0;
-  for (int64_t i = 0; i < P.n; i++) mu_sum += (rs[3 * i] - rs[3 * i + 2]) / nm1;
-  const double dbar = 2.0 * mu_sum / n / (P.SC * nfeat);
+// The risk above, on the device (q16_decision_risk): the step's exchange
+// vectors stay in HBM and one double comes back (until round 5 three
+// pageable copies of 5n + p doubles went to a host loop, ~0.15 ms of every
+// cfg4 step).  One 256-thread workgroup; every sum is a fixed-order block
+// reduction (block_sum_256), so every rank, holding the same all-reduced
+// vectors, computes the same risk.
+__global__ __launch_bounds__(256) void q16_decision_risk(const double* __restrict__ rs,
+                                                       const double* __restrict__ cnt,
+                                                       const double* __restrict__ sums, int64_t n64,
+                                                       int64_t n_kept, double pc, double nfeat,
+                                                       double SC, double* __restrict__ out) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
+  const double n = (double)n64, nm1 = n - 1.0;
+  double m = 0.0;
+  for (int64_t k = tid; k < n_kept; k += 256) m = fmax(m, (double)fabsf((float)(sums[k] / n)));
+  red[tid] = m;
+  __syncthreads();
+  for (int st = 128; st > 0; st >>= 1) {
+    if (tid < st) red[tid] = fmax(red[tid], red[tid + st]);
+    __syncthreads();
+  }
+  const double smax = red[0];
+  __syncthreads();
+  if (n < 3.0 || nfeat <= 0.0 || SC <= 0.0) {
+    if (tid == 0) out[0] = 0.0;
+    return;
+  }
+  if (smax <= 0.0) {
+    if (tid == 0) out[0] = HUGE_VAL;
+    return;
+  }
+  double mu = 0.0;
+  for (int64_t i = tid; i < n64; i += 256) mu += (rs[3 * i] - rs[3 * i + 2]) / nm1;
+  const double mu_sum = block_sum_256(mu, red);
+  const double thr_err = sqrt(pc / 6.0 + 1.0) / sqrt(n);
+  const double dbar = 2.0 * mu_sum / n / (SC * nfeat);
   double acc = 0.0;
-  for (int64_t i = 0; i < P.n; i++) {
-    const double mu = rs[3 * i] / nm1, var = rs[3 * i + 1] / nm1 - mu * mu;
+  for (int64_t i = tid; i < n64; i += 256) {
+    const double mi = rs[3 * i] / nm1, var = rs[3 * i + 1] / nm1 - mi * mi;
     if (!(var > 0.0)) continue;
-    const double flips = n * 0.352 * thr_err / std::sqrt(var);
-    const double m = std::max(1.0, std::min(cnt[2 * i], cnt[2 * i + 1]));
-    const double eff = dbar / (n * m);
+    const double flips = n * 0.352 * thr_err / sqrt(var);
+    const double mm = fmax(1.0, fmin(cnt[2 * i], cnt[2 * i + 1]));
+    const double eff = dbar / (n * mm);
     acc += flips * eff * eff;
   }
-  return std::sqrt(acc) / smax;
+  acc = block_sum_256(acc, red);
+  if (tid == 0) out[0] = sqrt(acc) / smax;
 }
 
 // After a MultiSURF step with 16-bit operands: the decision risk from the
@@ -677,15 +702,15 @@ int plan_decision_guard(Plan* g, const double* rowstats, const double* counts,
   // (max |score| of a partial sum would inflate the risk)
   if (g->r_lo != 0 || g->r_hi != Q.n) return FS_OK;
   FS_HIP(hipSetDevice(g->device));
-  std::vector<double> h((size_t)(5 * Q.n + Q.n_kept));
-  FS_HIP(hipMemcpyAsync(h.data(), rowstats, sizeof(double) * 3 * Q.n, hipMemcpyDeviceToHost,
-                        g->stream));
-  FS_HIP(hipMemcpyAsync(h.data() + 3 * Q.n, counts, sizeof(double) * 2 * Q.n,
-                        hipMemcpyDeviceToHost, g->stream));
-  FS_HIP(hipMemcpyAsync(h.data() + 5 * Q.n, sums, sizeof(double) * Q.n_kept,
-                        hipMemcpyDeviceToHost, g->stream));
+  if (!g->risk_dev) FS_TRY(dalloc(g, &g->risk_dev, 1));  // owned: lives as long as the plan
+  q16_decision_risk<<<1, 256, 0, g->stream>>>(rowstats, counts, sums, Q.n, Q.n_kept,
+                                              (double)Q.pc, (double)(Q.pc + Q.pd), Q.SC,
+                                              g->risk_dev);
+  FS_TRY(launch_check("q16_decision_risk"));
+  double r = 0.0;
+  FS_HIP(hipMemcpyAsync(&r, g->risk_dev, sizeof(double), hipMemcpyDeviceToHost, g->stream));
   FS_HIP(hipStreamSynchronize(g->stream));
-  *risk = q16_decision_risk(Q, h.data(), h.data() + 3 * Q.n, h.data() + 5 * Q.n);
+  *risk = r;
   if (!(*risk > kQ16MaxRisk)) return FS_OK;
   trace_mark("multisurf: 16-bit decision risk above bound, 32-bit operands");
   g->use_q16 = 0;
