@@ -622,7 +622,9 @@ def main():
         score_name = "k_score_sparse" if weighted >= 0 else "k_score"
         if ref_mode:  # the chains walk directed entries (one per focal side)
             score_name, weighted = "k_ms_chains", -1
-            pairs_score = chain_entries(step_counts, y, args.star)
+            # rank-local: each rank walks the chains of its 1/world of the
+            # focal rows (ShardedMultiSURF._step_reference)
+            pairs_score = chain_entries(step_counts, y, args.star) / world
         pfe = {"k_dist": pairs_dense * p, score_name: pairs_score * p}
         kern = {"k_dist": d_ms, score_name: s_ms}
         dom = max(kern, key=kern.get)
@@ -725,7 +727,9 @@ def main():
                        "n_samples": n, "n_features": p,
                        "parallelism": f"pair-tile shard x{world}"
                                       + (f", {'RCCL' if dist_backend == 'nccl' else dist_backend}"
-                                         f" all-reduce" if world > 1 else "")},
+                                         f" all-reduce" if world > 1 else "")
+                                      + (", decision-mask all-reduce + column sums chained "
+                                         "over the ranks" if world > 1 and ref_mode else "")},
             "roofline": roofline,
             "refined_pairs": refined,
             # X to the GPUs (per-rank rows + all-gather at N > 1) + plan

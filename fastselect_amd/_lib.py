@@ -43,6 +43,7 @@ EXPORTED = (
     "fs_relieff_score", "fs_surf_score", "fs_relieff_score_rows", "fs_surf_score_rows",
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_decision_guard", "fs_plan_set_rows",
+    "fs_plan_ref_mask_words", "fs_plan_ref_masks", "fs_plan_ref_pass2", "fs_plan_ref_sums",
     "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_calibration_ex", "fs_plan_weighted_pairs", "fs_plan_kernel_ms",
     "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
     "fs_surf_score_devices", "fs_set_accumulation", "fs_get_accumulation", "fs_test_hook",
@@ -131,6 +132,10 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_pass2.argtypes = [_vp, _vp, _vp]
     lib.fs_plan_decision_guard.argtypes = [_vp, _vp, _vp, _vp, ctypes.POINTER(ctypes.c_double),
                                            ctypes.POINTER(_int)]
+    lib.fs_plan_ref_mask_words.argtypes = [_vp, _i64p]
+    lib.fs_plan_ref_masks.argtypes = [_vp, _vp, _i64]
+    lib.fs_plan_ref_pass2.argtypes = [_vp, _vp, _vp, _i64, _i64]
+    lib.fs_plan_ref_sums.argtypes = [_vp, _vp, _vp]
     lib.fs_plan_info.argtypes = [_vp, _i64p, _f64p, _i64p]
     lib.fs_plan_calibration.argtypes = [_vp, _f64p]
     lib.fs_plan_calibration_ex.argtypes = [_vp, _f64p, _int]
@@ -151,7 +156,8 @@ def _load() -> ctypes.CDLL:
                  "fs_plan_set_rows", "fs_relieff_score", "fs_surf_score",
                  "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create",
                  "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
-                 "fs_plan_pass2", "fs_plan_decision_guard", "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs",
+                 "fs_plan_pass2", "fs_plan_decision_guard", "fs_plan_ref_mask_words", "fs_plan_ref_masks",
+                 "fs_plan_ref_pass2", "fs_plan_ref_sums", "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs",
                  "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
                  "fs_surf_score_devices"):
         getattr(lib, name).restype = _int
@@ -567,6 +573,27 @@ class Plan:
 
     def pass2(self, counts_ptr: int, scores_ptr: int) -> None:
         check(_lib.fs_plan_pass2(self._h, _vp(counts_ptr), _vp(scores_ptr)))
+
+    def ref_mask_words(self) -> int:
+        """int64 words of the reference-order decision masks (``fs_plan_ref_mask_words``)."""
+        w = _i64(0)
+        check(_lib.fs_plan_ref_mask_words(self._h, ctypes.byref(w)))
+        return int(w.value)
+
+    def ref_masks(self, masks_ptr: int, words: int) -> None:
+        """This rank's tile decisions into the zeroed masks (``fs_plan_ref_masks``)."""
+        check(_lib.fs_plan_ref_masks(self._h, _vp(masks_ptr), _i64(words)))
+
+    def ref_pass2(self, masks_ptr: int, counts_ptr: int, row_begin: int, row_end: int) -> None:
+        """Reference-order chains of the focal rows [row_begin, row_end) into
+        the plan's temp rows (``fs_plan_ref_pass2``)."""
+        check(_lib.fs_plan_ref_pass2(self._h, _vp(masks_ptr), _vp(counts_ptr), _i64(row_begin),
+                                     _i64(row_end)))
+
+    def ref_sums(self, init_ptr: int, sums_ptr: int) -> None:
+        """float32 column sums of the temp rows continuing init (0 = none)
+        into sums (``fs_plan_ref_sums``)."""
+        check(_lib.fs_plan_ref_sums(self._h, _vp(init_ptr or None), _vp(sums_ptr)))
 
     def decision_guard(self, rowstats_ptr: int, counts_ptr: int, scores_ptr: int):
         """(risk, switched) of the 16-bit decision check after a step whose

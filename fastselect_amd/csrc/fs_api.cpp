@@ -543,10 +543,10 @@ int fs_plan_create(fs_plan** plan_out, int backend, int device, const float* x, 
     delete pl;
     return rc;
   }
-  if (pl->P.ref_accum && world > 1) {
+  if (pl->P.ref_accum && world > 1 && backend != FS_BACKEND_GPU) {
     delete pl;
-    set_error("reference-order accumulation: pass 2 needs every pair tile's decisions in one "
-              "plan (world 1)");
+    set_error("reference-order accumulation with world > 1 (fs_plan_ref_masks / "
+              "fs_plan_ref_pass2) runs on the GPU backend only");
     return FS_ENOTSUP;
   }
   pl->r_lo = 0;
@@ -741,6 +741,58 @@ int fs_plan_pass2(fs_plan* pl, const double* counts, double* scores) {
                               pl->r_lo, pl->r_hi, scores);
 }
 
+int fs_plan_ref_mask_words(fs_plan* pl, int64_t* words) {
+  if (!pl || !words) {
+    set_error("NULL plan or buffer");
+    return FS_EINVAL;
+  }
+  if (!is_multisurf_plan(pl)) return FS_EINVAL;
+  if (!pl->g || !pl->P.ref_accum) {
+    set_error("fs_plan_ref_mask_words: a GPU plan created in reference-order accumulation");
+    return FS_ENOTSUP;
+  }
+  *words = gpu::ref_mask_words(pl->g);
+  return FS_OK;
+}
+
+int fs_plan_ref_masks(fs_plan* pl, uint64_t* masks, int64_t words) {
+  int64_t need = 0;
+  int rc = fs_plan_ref_mask_words(pl, &need);
+  if (rc) return rc;
+  if (!masks || words < need) {
+    set_error("fs_plan_ref_masks: mask buffer NULL or smaller than fs_plan_ref_mask_words");
+    return FS_EINVAL;
+  }
+  return gpu::plan_ref_masks(pl->g, masks);
+}
+
+int fs_plan_ref_pass2(fs_plan* pl, const uint64_t* masks, const double* counts, int64_t row_begin,
+                      int64_t row_end) {
+  int64_t need = 0;
+  int rc = fs_plan_ref_mask_words(pl, &need);
+  if (rc) return rc;
+  if (!masks || !counts) {
+    set_error("NULL plan or buffer");
+    return FS_EINVAL;
+  }
+  if (!(0 <= row_begin && row_begin <= row_end && row_end <= pl->P.n)) {
+    set_error("fs_plan_ref_pass2: row range outside [0, n)");
+    return FS_EINVAL;
+  }
+  return gpu::plan_ref_pass2(pl->g, masks, counts, row_begin, row_end);
+}
+
+int fs_plan_ref_sums(fs_plan* pl, const double* init, double* sums) {
+  int64_t need = 0;
+  int rc = fs_plan_ref_mask_words(pl, &need);
+  if (rc) return rc;
+  if (!sums) {
+    set_error("NULL sums buffer");
+    return FS_EINVAL;
+  }
+  return gpu::plan_ref_sums(pl->g, init, sums);
+}
+
 int fs_plan_decision_guard(fs_plan* pl, const double* rowstats, const double* counts,
                            const double* scores, double* risk_out, int* switched_out) {
   if (!pl || !rowstats || !counts || !scores || !risk_out || !switched_out) {
@@ -784,9 +836,9 @@ int fs_plan_set_shard(fs_plan* pl, int rank, int world) {
     set_error("shard rank/world must satisfy 0 <= rank < world");
     return FS_EINVAL;
   }
-  if (pl->P.ref_accum && world > 1) {
-    set_error("reference-order accumulation: pass 2 needs every pair tile's decisions in one "
-              "plan (world 1)");
+  if (pl->P.ref_accum && world > 1 && !pl->g) {
+    set_error("reference-order accumulation with world > 1 (fs_plan_ref_masks / "
+              "fs_plan_ref_pass2) runs on the GPU backend only");
     return FS_ENOTSUP;
   }
   if (pl->g) {

@@ -771,13 +771,71 @@ int ref_chains(Plan* g, const double* counts, double* scores) {
   return refacc::column_sums(temp, rows, g->Kp, Q.n_kept, nullptr, scores, g->stream);
 }
 
+// Reference order across ranks (fs_plan_ref_masks / fs_plan_ref_pass2):
+// this plan's tile decisions into a caller-owned mask buffer, zeroed first
+// (every (row, word) belongs to one tile, so the ranks' buffers add up to
+// the whole matrix's -- a SUM all-reduce of the words), then the chains of
+// the focal rows [lo, hi) over the combined masks into the plan's temp rows
+// (every rank at once), and their float32 sequential column sums continuing
+// from `init` (the previous rank's sums: the only serial link).
+int64_t ref_mask_words(const Plan* g) {
+  return g->P.n_pad * (g->P.n_pad / 64) * 4;
+}
+
+int plan_ref_masks(Plan* g, uint64_t* masks) {
+  const Prepared& Q = g->P;
+  FS_HIP(hipSetDevice(g->device));
+  FS_HIP(hipMemsetAsync(masks, 0, sizeof(uint64_t) * (size_t)ref_mask_words(g), g->stream));
+  FS_TRY(refacc::multisurf_masks(g->D, Q.n, Q.n_pad, g->tiles, g->n_tiles, g->thr, g->lab,
+                                 Q.use_star, masks, g->stream));
+  if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
+  return FS_OK;
+}
+
+int plan_ref_pass2(Plan* g, const uint64_t* masks, const double* counts, int64_t lo,
+                   int64_t hi) {
+  const Prepared& Q = g->P;
+  FS_HIP(hipSetDevice(g->device));
+  g->ref_rows = std::max<int64_t>(hi - lo, 0);
+  if (g->ref_rows > 0) {
+    float* temp = nullptr;
+    FS_TRY(ref_temp(g, g->ref_rows, &temp));
+    FS_HIP(hipEventRecord(g->ev[2], g->stream));
+    FS_TRY(refacc::multisurf_chains(g->xk, g->Kp, g->krecip, g->kdisc, g->kblk, masks, Q.n,
+                                    Q.n_pad, counts, Q.use_star, lo, hi, temp, g->stream));
+    FS_HIP(hipEventRecord(g->ev[3], g->stream));
+  }
+  if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
+  return FS_OK;
+}
+
+int plan_ref_sums(Plan* g, const double* init, double* sums) {
+  const Prepared& Q = g->P;
+  FS_HIP(hipSetDevice(g->device));
+  if (g->ref_rows < 0) {
+    set_error("fs_plan_ref_sums: no fs_plan_ref_pass2 since the plan was created or re-targeted");
+    return FS_EINVAL;
+  }
+  if (g->ref_rows == 0) {  // no rows: the running sums pass through
+    if (init)
+      FS_HIP(hipMemcpyAsync(sums, init, sizeof(double) * Q.n_kept, hipMemcpyDeviceToDevice,
+                            g->stream));
+    else
+      FS_HIP(hipMemsetAsync(sums, 0, sizeof(double) * Q.n_kept, g->stream));
+  } else {
+    FS_TRY(refacc::column_sums(g->temp, g->ref_rows, g->Kp, Q.n_kept, init, sums, g->stream));
+  }
+  if (g->own_stream) FS_HIP(hipStreamSynchronize(g->stream));
+  return FS_OK;
+}
+
 int plan_pass2(Plan* g, const double* counts, double* scores) {
   const Prepared& Q = g->P;
   FS_HIP(hipSetDevice(g->device));
   if (Q.ref_accum) {
     if (g->world > 1) {
-      set_error("reference-order accumulation: pass 2 needs every pair tile's decisions in one "
-                "plan (world 1; the one-shot calls shard internally)");
+      set_error("reference-order accumulation with world > 1: pass 2 is fs_plan_ref_masks, a "
+                "SUM all-reduce of the masks, then fs_plan_ref_pass2 chained over the ranks");
       return FS_ENOTSUP;
     }
     FS_TRY(ref_masks(g));

@@ -456,6 +456,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
 int plan_set_features(Plan* g, const Prepared& P) {
   FS_HIP(hipSetDevice(g->device));
   g->P = P;
+  g->ref_rows = -1;  // temp rows of the old feature layout
   return plan_layout(g);
 }
 

@@ -152,9 +152,13 @@ def prepare_inputs(X, y, discrete_limit: int = 10, backend: str = "cpu", device:
 class ShardedMultiSURF:
     """One rank's share of a MultiSURF scoring job.
 
-    backend 'gpu': buffers are CUDA tensors on ``device`` and every kernel runs
-    on torch's current stream, so the all-reduces are stream-ordered with the
-    HIP kernels.  backend 'cpu': host tensors (use the gloo backend).
+    backend 'gpu': buffers are CUDA tensors on ``device``, and the plan's
+    kernels, the torch ops on the exchange buffers and the collectives all run
+    on one stream (``self.stream``: torch's current stream, or a stream of the
+    job's own when that is the default stream, whose handle 0 would give the
+    plan a stream unordered with torch's work), so each stage waits for the
+    all-reduce before it without a host synchronisation.  backend 'cpu': host
+    tensors (use the gloo backend).
     """
 
     def __init__(self, x, y, recip, is_discrete, use_star=False, backend="gpu", device=0,
@@ -164,9 +168,13 @@ class ShardedMultiSURF:
         import torch
         self.dist, self.rank, self.world = _dist() if shard else (None, 0, 1)
         _lib.accumulation_code(accumulation)
-        if accumulation == "reference" and self.world > 1:
-            raise ValueError("accumulation='reference' needs every pair tile's decisions in "
-                             "one plan: world 1")
+        if accumulation == "reference" and self.world > 1 and backend != "gpu":
+            raise ValueError("accumulation='reference' over world > 1 ranks runs on the GPU "
+                             "backend (fs_plan_ref_masks / fs_plan_ref_pass2)")
+        # reference order over ranks (_step_reference): pass 2 is the masks'
+        # all-reduce, every rank's chains, then the float32 column sums handed
+        # from rank to rank
+        self.ref_chain = accumulation == "reference" and self.world > 1
         self.n, self.p = x.shape
         self.backend = backend
         # tile shards per device (n beyond HBM): the device holds the distance
@@ -178,9 +186,12 @@ class ShardedMultiSURF:
         if backend == "gpu":
             torch.cuda.set_device(device)
             self.tdev = torch.device("cuda", device)
-            stream = torch.cuda.current_stream().cuda_stream
+            cur = torch.cuda.current_stream(self.tdev)
+            self.stream = cur if cur.cuda_stream != 0 else torch.cuda.Stream(self.tdev)
+            stream = self.stream.cuda_stream
         else:
             self.tdev = torch.device("cpu")
+            self.stream = None
             stream = 0
         # Every rank must use the same shard count: ownership is tile t ->
         # shard t % (world * V), so ranks with different V would score some
@@ -188,18 +199,42 @@ class ShardedMultiSURF:
         # memory; the largest V fits on every rank.
         self.shards = self._agree_max(max(1, int(shards)))
         if accumulation == "reference":
-            # one plan holding every tile (the one-shot calls shard by themselves)
+            # one plan per rank holding all of its tiles (the one-shot calls
+            # shard by themselves)
             self.shards = 1
-        with _lib.accumulation(accumulation):  # the plan keeps its creation mode
+        with self._on_stream(), _lib.accumulation(accumulation):  # plans keep their mode
             self.plan = _lib.Plan(backend, x, y, recip, is_discrete, use_star=use_star,
                                   rank=self.rank, world=self.world * self.shards, device=device,
                                   stream=stream)
         if rows is not None:  # focal-sample slice: pass 2 sums those samples only
             self.plan.set_rows(*rows)
+        if self.ref_chain:
+            f0, f1 = rows if rows is not None else (0, self.n)
+            b, e = shard_rows(f1 - f0, self.rank, self.world)
+            self.ref_rows = (f0 + b, f0 + e)
+            self.masks = None
         f64 = torch.float64
-        self.rowstats = torch.zeros(3 * self.n, dtype=f64, device=self.tdev)
-        self.counts = torch.zeros(2 * self.n, dtype=f64, device=self.tdev)
-        self.scores = torch.zeros(self.p, dtype=f64, device=self.tdev)
+        with self._on_stream():
+            self.rowstats = torch.zeros(3 * self.n, dtype=f64, device=self.tdev)
+            self.counts = torch.zeros(2 * self.n, dtype=f64, device=self.tdev)
+            self.scores = torch.zeros(self.p, dtype=f64, device=self.tdev)
+
+    @contextlib.contextmanager
+    def _on_stream(self):
+        """Run the block on the job's stream, ordered after the caller's
+        stream on entry and before it on exit."""
+        if self.stream is None:
+            yield
+            return
+        import torch
+        caller = torch.cuda.current_stream(self.tdev)
+        if caller == self.stream:
+            yield
+            return
+        self.stream.wait_stream(caller)
+        with torch.cuda.stream(self.stream):
+            yield
+        caller.wait_stream(self.stream)
 
     def _agree_max(self, v: int) -> int:
         """MAX of an integer over the ranks (no collective without a group)."""
@@ -214,10 +249,11 @@ class ShardedMultiSURF:
         """Score another feature subset of the resident samples from the next
         step on (fs_plan_set_features: X stays on the device)."""
         import torch
-        self.plan.set_features(feat_idx)
-        n_kept = self.plan.n_kept
-        if self.scores.numel() != n_kept:
-            self.scores = torch.zeros(n_kept, dtype=torch.float64, device=self.tdev)
+        with self._on_stream():
+            self.plan.set_features(feat_idx)
+            n_kept = self.plan.n_kept
+            if self.scores.numel() != n_kept:
+                self.scores = torch.zeros(n_kept, dtype=torch.float64, device=self.tdev)
 
     def _allreduce(self, t):
         # issued whenever a process group is up, world 1 included (one RCCL
@@ -261,7 +297,48 @@ class ShardedMultiSURF:
         self._allreduce(self.scores)
         return (self.scores / self.n).float()
 
+    def _p2p(self, t):
+        """``t`` as the process group moves it point to point (gloo: host)."""
+        return t.cpu() if self.dist.get_backend() == "gloo" else t
+
+    def _step_reference(self):
+        """Reference-order step over world > 1 ranks (fs_plan_ref_masks,
+        fs_plan_ref_pass2, fs_plan_ref_sums).  The reference sums every focal
+        sample's float32 temp row into one sequential float32 column sum
+        (MultiSURF.py:231-253, np.sum(temp, axis=0)), which no all-reduce of
+        partials reproduces.  So: the ranks' pair-tile decisions as bit masks,
+        combined by a SUM all-reduce (each word is written by one rank);
+        every rank's chains for its contiguous block of focal rows at once;
+        then the column sums continue from rank to rank in sample order --
+        n_kept float64 values per hop -- and the last rank's are broadcast."""
+        import torch
+        self.plan.pass1(self.rowstats.data_ptr())
+        self._allreduce(self.rowstats)
+        self.plan.select(self.rowstats.data_ptr(), self.counts.data_ptr())
+        self._allreduce(self.counts)
+        if self.masks is None:
+            self.masks = torch.empty(self.plan.ref_mask_words(), dtype=torch.int64,
+                                     device=self.tdev)
+        self.plan.ref_masks(self.masks.data_ptr(), self.masks.numel())
+        self._allreduce(self.masks)
+        self.plan.ref_pass2(self.masks.data_ptr(), self.counts.data_ptr(), *self.ref_rows)
+        init = None
+        if self.rank > 0:
+            buf = self._p2p(torch.empty_like(self.scores))
+            self.dist.recv(buf, src=self.rank - 1)
+            init = buf.to(self.tdev)
+        self.plan.ref_sums(init.data_ptr() if init is not None else 0, self.scores.data_ptr())
+        if self.rank < self.world - 1:
+            self.dist.send(self._p2p(self.scores), dst=self.rank + 1)
+        last = self._p2p(self.scores)
+        self.dist.broadcast(last, src=self.world - 1)
+        if last is not self.scores:
+            self.scores.copy_(last)
+        return (self.scores / self.n).float()
+
     def _step_once(self):
+        if self.ref_chain:
+            return self._step_reference()
         if self.shards > 1:
             return self._step_shards()
         self.plan.pass1(self.rowstats.data_ptr())
@@ -280,12 +357,16 @@ class ShardedMultiSURF:
         vectors, so every rank decides alike): above its bound the plan moves
         to 32-bit operands for good and the step runs again.  ``last_guard``
         holds (risk, re-run) of the last step."""
-        s = self._step_once()
-        risk, switched = self.plan.decision_guard(self.rowstats.data_ptr(),
-                                                  self.counts.data_ptr(),
-                                                  self.scores.data_ptr())
-        if switched:
+        with self._on_stream():
             s = self._step_once()
+            risk, switched = self.plan.decision_guard(self.rowstats.data_ptr(),
+                                                      self.counts.data_ptr(),
+                                                      self.scores.data_ptr())
+            if switched:
+                s = self._step_once()
+        if self.stream is not None:  # s is consumed on the caller's stream
+            import torch
+            s.record_stream(torch.cuda.current_stream(self.tdev))
         self.last_guard = (risk, switched)
         return s
 
@@ -303,6 +384,8 @@ class ShardedMultiSURF:
         torch's caching allocator shares the GPU with this job and cannot
         reclaim blocks held in the library's cache (fs_device_cache_release).
         release_cache=False keeps them for the next job (repeated fits)."""
+        if self.stream is not None:
+            self.stream.synchronize()
         self.plan.close()
         if self.backend == "gpu" and release_cache:
             _lib.release_device_cache()

@@ -84,9 +84,11 @@ extern "C" {
  *                       flagged row.  The scores are then the reference's
  *                       arithmetic bit for bit (tests/test_refacc*.py).  SURF
  *                       has no fixed reference order (its per-thread rows,
- *                       SURF.py:195, 216): FS_ENOTSUP.  One device only:
- *                       the fs_*_score_devices calls and plans with world > 1
- *                       return FS_ENOTSUP.
+ *                       SURF.py:195, 216): FS_ENOTSUP.  The one-shot calls
+ *                       and fs_*_score_devices run on one device (FS_ENOTSUP
+ *                       otherwise); GPU MultiSURF plans with world > 1 run
+ *                       pass 2 as fs_plan_ref_masks / fs_plan_ref_pass2 /
+ *                       fs_plan_ref_sums (CPU backend: FS_ENOTSUP).
  * previous (nullable) receives the mode in force before the call.
  */
 FS_API int fs_set_accumulation(int mode, int* previous);
@@ -358,6 +360,30 @@ FS_API int fs_plan_pass2(fs_plan* plan, const double* counts, double* scores);
  * TuRF's refits, TuRF.py:87,111, through the same plan). */
 FS_API int fs_plan_decision_guard(fs_plan* plan, const double* rowstats, const double* counts,
                                   const double* scores, double* risk_out, int* switched_out);
+/* Reference-order accumulation (fs_set_accumulation(FS_ACCUM_REFERENCE))
+ * over world > 1 ranks, GPU backend.  The reference's float32 sums run over
+ * every focal sample in order (MultiSURF.py:231-253, then
+ * np.sum(temp, axis=0)), so pass 2 is not a sum of rank partials; after
+ * pass1 / all-reduce / select / all-reduce, instead of fs_plan_pass2:
+ *   1. fs_plan_ref_masks: this rank's pair-tile decisions as bit masks in
+ *      masks[words] (device memory, words >= fs_plan_ref_mask_words; zeroed
+ *      first, so every word outside this rank's tiles is 0);
+ *   2. a SUM all-reduce of the masks as int64 (each word is nonzero on at
+ *      most one rank, so the sum is the whole triangle's masks);
+ *   3. fs_plan_ref_pass2 on every rank at once: the per-sample hit / miss
+ *      chains of the focal rows [row_begin, row_end) of the rank's contiguous
+ *      block (counts = the all-reduced counts[2n]) into the plan's float32
+ *      temp rows;
+ *   4. fs_plan_ref_sums on the ranks in order: rank r continues the float32
+ *      column sums init[n_kept] it received from rank r - 1 (NULL on the
+ *      first rank) over its temp rows and hands sums[n_kept] to rank r + 1;
+ *      the last rank's sums, divided by n, are the reference's scores bit
+ *      for bit (fastselect_amd/parallel.py ShardedMultiSURF). */
+FS_API int fs_plan_ref_mask_words(fs_plan* plan, int64_t* words);
+FS_API int fs_plan_ref_masks(fs_plan* plan, uint64_t* masks, int64_t words);
+FS_API int fs_plan_ref_pass2(fs_plan* plan, const uint64_t* masks, const double* counts,
+                             int64_t row_begin, int64_t row_end);
+FS_API int fs_plan_ref_sums(fs_plan* plan, const double* init, double* sums);
 /* Restrict the next pass2 of a MultiSURF plan to the focal samples
  * [row_begin, row_end) (as fs_multisurf_score_rows; a new plan scores
  * [0, n)).  pass1 / select are unchanged: thresholds and counts are global. */

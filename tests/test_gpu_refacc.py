@@ -124,6 +124,48 @@ def test_rows_slice_is_the_oracle_slice(F, oracle):
                     oracle.multisurf_scores(X, y, i_range=(300, 1100)))
 
 
+def _ref_rank_worker(rank, world, port, out_path, rows):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
+    X, y = verdict_case("pareto1", 1300, 200, seed=8)
+    x, yv, recip, isd = prepare_inputs(X, y, backend="gpu", device=0)
+    for star in (False, True):
+        job = ShardedMultiSURF(x, yv, recip, isd, use_star=star, backend="gpu", device=0,
+                               rows=rows, accumulation="reference")
+        assert job.ref_chain and job.world == world
+        np.save(f"{out_path}.{int(star)}.{rank}.npy", job.step().cpu().numpy())
+        np.save(f"{out_path}.{int(star)}.{rank}.again.npy", job.step().cpu().numpy())
+        job.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,rows", [(2, None), (3, None), (2, (170, 1111))])
+def test_ranks_chain_the_column_sums_bitexact(F, oracle, tmp_path, world, rows):
+    """Reference order over world ranks (two or three processes sharing
+    cuda:0, gloo): each rank's pair-tile decisions as masks, their SUM
+    all-reduce, every rank's chains for its block of focal rows, then the
+    float32 column sums handed from rank to rank -- every rank ends with the
+    oracle's scores bit for bit, step after step (fs_plan_ref_masks /
+    fs_plan_ref_pass2 / fs_plan_ref_sums)."""
+    import torch.multiprocessing as mp
+
+    from test_gpu_dist import _port
+    out = str(tmp_path / "ref")
+    mp.spawn(_ref_rank_worker, args=(world, _port(), out, rows), nprocs=world, join=True)
+    X, y = verdict_case("pareto1", 1300, 200, seed=8)
+    for star in (False, True):
+        if rows is None:
+            ref = oracle.multisurf_scores(X, y, use_star=star)
+        else:  # a focal slice: the sums over those samples, divided by n
+            ref = oracle.multisurf_scores(X, y, use_star=star, i_range=rows)
+        for r in range(world):
+            for tag in ("", ".again"):
+                assert_bitexact(np.load(f"{out}.{int(star)}.{r}{tag}.npy"), ref)
+
+
 def test_forced_tile_shards_bitexact(F, oracle, monkeypatch):
     """n beyond HBM: the one-shot call in V tile shards writes every shard's
     decisions into the masks before the chains run."""
@@ -201,3 +243,32 @@ def test_decisions_row_by_row(F, name, fast_bound):
     print(name, "rows decided differently from the reference:", flipped)
     assert flipped["reference"] == 0
     assert flipped["fast"] <= fast_bound
+
+
+def _fullsize_rank_worker(rank, world, port, name, out_path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
+    X, y = _inputs(_fixture(name))
+    x, yv, recip, isd = prepare_inputs(X, y, backend="gpu", device=0)
+    job = ShardedMultiSURF(x, yv, recip, isd, backend="gpu", device=0, accumulation="reference")
+    np.save(f"{out_path}.{rank}.npy", job.step().cpu().numpy())
+    job.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("name", ["cfg2_multisurf", "cfg4_multisurf"])
+def test_fullsize_two_ranks_bitexact(F, tmp_path, name):
+    """Reference order over two ranks at the BASELINE sizes (cfg4: the north
+    star's 20000 x 20000, each rank half the pair tiles; two processes on
+    cuda:0, gloo): the reference's scores bit for bit on both ranks."""
+    import torch.multiprocessing as mp
+
+    from test_gpu_dist import _port
+    out = str(tmp_path / name)
+    mp.spawn(_fullsize_rank_worker, args=(2, _port(), name, out), nprocs=2, join=True)
+    fx = _fixture(name)
+    for r in range(2):
+        assert_bitexact(np.load(f"{out}.{r}.npy"), fx["scores"])

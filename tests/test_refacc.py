@@ -174,6 +174,26 @@ def test_accumulation_errors():
         _base.check_accumulation_devices("reference", [0, 1])
 
 
+def test_reference_over_ranks_is_gpu_only_cpu():
+    """Reference order over world > 1 ranks is the GPU plans' masks / chains
+    / chained column sums (fs_plan_ref_*); the CPU backend refuses it, and the
+    fs_plan_ref_* calls refuse CPU plans."""
+    from fastselect_amd import parallel
+    X, y = verdict_case("exp4z", 200, 30, seed=2)
+    x, yv, recip, isd = parallel.prepare_inputs(X, y, backend="cpu")
+    with _lib.accumulation("reference"):
+        with pytest.raises(RuntimeError, match="GPU backend"):
+            _lib.Plan("cpu", x, yv, recip, isd, rank=0, world=2)
+        plan = _lib.Plan("cpu", x, yv, recip, isd)
+    try:
+        with pytest.raises(RuntimeError, match="reference-order"):
+            plan.ref_mask_words()
+        with pytest.raises(RuntimeError, match="GPU backend"):
+            plan.set_shard(1, 2)
+    finally:
+        plan.close()
+
+
 def test_fast_mode_unchanged_cpu():
     """The default stays the fast path: same scores as before the option."""
     X, y = verdict_case("exp4z", 200, 40, seed=9)
