@@ -368,7 +368,20 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
     sync()
     setup_ms = (time.perf_counter() - t0) * 1e3
 
+    # reference order over ranks: every rank's float32 temp rows, then the
+    # column sums passed rank to rank (parallel._chain_column_sums)
+    chain = args.accumulation == "reference" and world > 1 and on_gpu
+
     def step():
+        if chain:
+            from fastselect_amd.parallel import _chain_column_sums
+            plan.ref_temp()
+            _chain_column_sums(plan, p, local)
+            return
+        if world > 1 and on_gpu:
+            # the plan runs on its own stream: last step's all-reduce of sums
+            # (on torch's stream) must have finished before it writes them
+            torch.cuda.current_stream().synchronize()
         plan.score(sums.data_ptr())
         if world > 1:
             dist.all_reduce(sums, op=dist.ReduceOp.SUM)

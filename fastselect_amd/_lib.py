@@ -44,6 +44,7 @@ EXPORTED = (
     "fs_plan_create", "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features",
     "fs_plan_pass1", "fs_plan_select", "fs_plan_pass2", "fs_plan_decision_guard", "fs_plan_set_rows",
     "fs_plan_ref_mask_words", "fs_plan_ref_masks", "fs_plan_ref_pass2", "fs_plan_ref_sums",
+    "fs_plan_ref_temp",
     "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_calibration_ex", "fs_plan_weighted_pairs", "fs_plan_kernel_ms",
     "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
     "fs_surf_score_devices", "fs_set_accumulation", "fs_get_accumulation", "fs_test_hook",
@@ -136,6 +137,7 @@ def _load() -> ctypes.CDLL:
     lib.fs_plan_ref_masks.argtypes = [_vp, _vp, _i64]
     lib.fs_plan_ref_pass2.argtypes = [_vp, _vp, _vp, _i64, _i64]
     lib.fs_plan_ref_sums.argtypes = [_vp, _vp, _vp]
+    lib.fs_plan_ref_temp.argtypes = [_vp]
     lib.fs_plan_info.argtypes = [_vp, _i64p, _f64p, _i64p]
     lib.fs_plan_calibration.argtypes = [_vp, _f64p]
     lib.fs_plan_calibration_ex.argtypes = [_vp, _f64p, _int]
@@ -157,7 +159,7 @@ def _load() -> ctypes.CDLL:
                  "fs_relieff_score_rows", "fs_surf_score_rows", "fs_plan_create",
                  "fs_plan_create_relieff", "fs_plan_create_surf", "fs_plan_score", "fs_plan_set_features", "fs_plan_pass1", "fs_plan_select",
                  "fs_plan_pass2", "fs_plan_decision_guard", "fs_plan_ref_mask_words", "fs_plan_ref_masks",
-                 "fs_plan_ref_pass2", "fs_plan_ref_sums", "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs",
+                 "fs_plan_ref_pass2", "fs_plan_ref_sums", "fs_plan_ref_temp", "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs",
                  "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
                  "fs_surf_score_devices"):
         getattr(lib, name).restype = _int
@@ -689,3 +691,8 @@ class RowsPlan(Plan):
 
     def score(self, sums_ptr: int) -> None:
         check(_lib.fs_plan_score(self._h, _vp(sums_ptr)))
+
+    def ref_temp(self) -> None:
+        """Reference order: the score up to the float32 temp rows, whose column
+        sums ``ref_sums`` continues (``fs_plan_ref_temp``, ReliefF)."""
+        check(_lib.fs_plan_ref_temp(self._h))

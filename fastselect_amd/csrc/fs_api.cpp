@@ -782,9 +782,31 @@ int fs_plan_ref_pass2(fs_plan* pl, const uint64_t* masks, const double* counts, 
   return gpu::plan_ref_pass2(pl->g, masks, counts, row_begin, row_end);
 }
 
+// ReliefF / MultiSURF GPU plans in reference order (fs_plan_ref_temp, _sums)
+static int ref_rows_plan(fs_plan* pl, bool relieff_only, const char* what) {
+  if (!pl) {
+    set_error("plan is NULL");
+    return FS_EINVAL;
+  }
+  const bool ok_algo = pl->P.algo == ALGO_RELIEFF || (!relieff_only && pl->P.algo == ALGO_MULTISURF);
+  if (!ok_algo) {
+    set_error(std::string(what) + (relieff_only ? ": a ReliefF plan" : ": a ReliefF or MultiSURF plan"));
+    return FS_EINVAL;
+  }
+  if (!pl->g || !pl->P.ref_accum) {
+    set_error(std::string(what) + ": a GPU plan created in reference-order accumulation");
+    return FS_ENOTSUP;
+  }
+  return FS_OK;
+}
+
+int fs_plan_ref_temp(fs_plan* pl) {
+  const int rc = ref_rows_plan(pl, true, "fs_plan_ref_temp");
+  return rc ? rc : gpu::plan_ref_temp(pl->g);
+}
+
 int fs_plan_ref_sums(fs_plan* pl, const double* init, double* sums) {
-  int64_t need = 0;
-  int rc = fs_plan_ref_mask_words(pl, &need);
+  const int rc = ref_rows_plan(pl, false, "fs_plan_ref_sums");
   if (rc) return rc;
   if (!sums) {
     set_error("NULL sums buffer");

@@ -245,7 +245,8 @@ struct Plan {
   int32_t* bcnt = nullptr;
   float* temp = nullptr;        // the reference's temp rows [rows][Kp] (own block)
   size_t temp_cap = 0;
-  int64_t ref_rows = -1;        // rows of temp the last plan_ref_pass2 wrote (-1: none yet)
+  int64_t ref_rows = -1;        // rows of temp the last plan_ref_pass2 / _temp wrote (-1: none)
+  bool ref_defer = false;       // ReliefF reference order: stop at the temp rows (plan_ref_temp)
   float* rkeys = nullptr;       // ReliefF neighbour keys (own block)
   size_t rkeys_cap = 0;
   bool ref_seeded = false;      // ReliefF: the column sums continue from the sums buffer

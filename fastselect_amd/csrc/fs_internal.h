@@ -486,6 +486,7 @@ int plan_ref_masks(Plan* g, uint64_t* masks_dev);
 int plan_ref_pass2(Plan* g, const uint64_t* masks_dev, const double* counts_dev, int64_t row_lo,
                    int64_t row_hi);
 int plan_ref_sums(Plan* g, const double* init_dev, double* sums_dev);
+int plan_ref_temp(Plan* g);
 // After a step on 16-bit operands: decision risk from the step's summed
 // exchange vectors (device memory); above the bound the plan switches to
 // 32-bit operands and *switched = 1 (run the step again).  risk = -1: no check.

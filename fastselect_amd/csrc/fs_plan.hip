@@ -865,6 +865,16 @@ int surf_run_one(const Prepared& P, const void* x, int device, int64_t r_lo, int
 // ReliefF / SURF plans (resident scoring, fs_plan_score): float64 score sums
 // of the plan's focal rows into device memory; per-call buffers are freed
 // before returning.
+// Reference order, row-sharded ReliefF over ranks (fs_plan_ref_temp): the
+// plan's score up to its float32 temp rows; plan_ref_sums continues the
+// previous rank's column sums over them.
+int plan_ref_temp(Plan* g) {
+  g->ref_defer = true;
+  const int rc = plan_score(g, nullptr);
+  g->ref_defer = false;
+  return rc;
+}
+
 int plan_score(Plan* g, double* sums_dev) {
   FS_HIP(hipSetDevice(g->device));
   int rc;

@@ -1623,6 +1623,10 @@ int plan_score_relieff(Plan* g, double* sums_dev) {
     FS_TRY(refacc::relieff_rows(g->xk, g->Kp, g->krecip, g->kdisc, Q.n_kept, g->lab, dprior, C, k,
                                 nbr, nfound, g->r_lo, g->r_hi, g->rkeys, temp, g->stream));
     FS_HIP(hipEventRecord(g->ev[3], g->stream));
+    if (g->ref_defer) {  // fs_plan_ref_temp: the column sums come later (plan_ref_sums)
+      g->ref_rows = std::max<int64_t>(rows, 0);
+      return FS_OK;
+    }
     if (!g->ref_seeded) FS_HIP(hipMemsetAsync(sums_dev, 0, sizeof(double) * Q.n_kept, g->stream));
     if (rows <= 0) return FS_OK;
     return refacc::column_sums(temp, rows, g->Kp, Q.n_kept, g->ref_seeded ? sums_dev : nullptr,

@@ -392,7 +392,7 @@ class ShardedMultiSURF:
 
 
 def multisurf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", device=0,
-                     release_cache=True):
+                     release_cache=True, accumulation="fast"):
     """Score X on this rank's share of the tiles and return the full float32
     score vector (identical on every rank).  X reaches the GPUs once
     (``resident_x``: per-rank rows + an RCCL all-gather when sharded)."""
@@ -400,7 +400,7 @@ def multisurf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", dev
     with resident_x(x, backend, device):
         x, yv, recip, isd = prepare_inputs(x, y, discrete_limit, backend, device)
         job = ShardedMultiSURF(x, yv, recip, isd, use_star=use_star, backend=backend,
-                               device=device)
+                               device=device, accumulation=accumulation)
         try:
             s = job.step()
             return s.cpu().numpy()
@@ -461,8 +461,33 @@ def resident_cast(xd, x32, device=0):
         del buf
 
 
+def _chain_column_sums(plan, p, device):
+    """Reference order over the ranks: rank r continues the float32 column
+    sums of rank r - 1 over its temp rows (``fs_plan_ref_sums``) and hands
+    them to rank r + 1; every rank returns the last rank's sums (float64
+    host vector).  ``plan`` runs on its own stream and synchronises the host
+    after each call."""
+    import torch
+    dist, rank, world = _dist()
+    dev = torch.device("cuda", device)
+    host = dist.get_backend() == "gloo"
+    sums = torch.zeros(p, dtype=torch.float64, device=dev)
+    init = None
+    if rank > 0:
+        buf = torch.empty(p, dtype=torch.float64, device="cpu" if host else dev)
+        dist.recv(buf, src=rank - 1)
+        init = buf.to(dev)
+    torch.cuda.current_stream(dev).synchronize()   # init has landed (the plan's own stream)
+    plan.ref_sums(init.data_ptr() if init is not None else 0, sums.data_ptr())
+    out = sums.cpu() if host else sums
+    if rank < world - 1:
+        dist.send(out, dst=rank + 1)
+    dist.broadcast(out, src=world - 1)
+    return out.cpu().numpy()
+
+
 def relieff_scores(X, y, n_neighbors=3, discrete_limit=10, backend="gpu", device=0, n_jobs=-1,
-                   gather=None):
+                   gather=None, accumulation="fast"):
     """ReliefF feature scores with the focal samples sharded over the ranks:
     this rank scores ``shard_rows(n, rank, world)``, one all-reduce sums the
     slices.  Returns the full float32 score vector (identical on every rank)
@@ -470,22 +495,46 @@ def relieff_scores(X, y, n_neighbors=3, discrete_limit=10, backend="gpu", device
     float64 summation order.  X crosses the host link once over all ranks
     (``resident_x``: each rank uploads its n/N float64 rows, RCCL all-gathers
     the rest; the column statistics read that copy, and the float32 copy
-    the plan scores is cast from it on the device, ``resident_cast``)."""
+    the plan scores is cast from it on the device, ``resident_cast``).
+
+    accumulation='reference': the reference's float32 scores bit for bit.
+    Its column sum is one sequential float32 sum over the focal samples
+    (ReliefF.py:219-220), so over N ranks every rank forms its float32 temp
+    rows at once (``fs_plan_ref_temp``) and the running sums then pass from
+    rank to rank (``fs_plan_ref_sums``) instead of one all-reduce (GPU
+    backend; one rank: the one-shot call)."""
     from .ReliefF import relieff_inputs
     x = np.ascontiguousarray(X, dtype=np.float64)
     yv = np.asarray(y)
     n, p = x.shape
+    _lib.accumulation_code(accumulation)
     if np.unique(yv).size < 2:
         return np.zeros(p, dtype=np.float32)
     backend = _base.effective_backend(backend)
     _, rank, world = _dist()
+    chain = accumulation == "reference" and world > 1
+    if chain and backend != "gpu":
+        raise ValueError("accumulation='reference' over world > 1 ranks runs on the GPU "
+                         "backend (fs_plan_ref_temp / fs_plan_ref_sums)")
     with resident_x(x, backend, device, gather) as xd:
         x32, y_enc, recip, isd, priors = relieff_inputs(x, yv, discrete_limit, backend, device,
                                                         n_jobs)
-        with resident_cast(xd, x32, device):
-            sums = _lib.relieff_score(backend, x32, y_enc, recip, isd, n_neighbors, priors,
-                                      n_jobs, device=device, rows=shard_rows(n, rank, world))
-    return (_allreduce_sums(sums, backend, device) / n).astype(np.float32)
+        with resident_cast(xd, x32, device), _lib.accumulation(accumulation):
+            if not chain:
+                sums = _lib.relieff_score(backend, x32, y_enc, recip, isd, n_neighbors, priors,
+                                          n_jobs, device=device, rows=shard_rows(n, rank, world))
+            else:
+                plan = _lib.RowsPlan(backend, "relieff", x32, y_enc, recip, isd, k=n_neighbors,
+                                     class_probs=priors, rows=shard_rows(n, rank, world),
+                                     n_jobs=n_jobs, device=device)
+                try:
+                    plan.ref_temp()
+                    sums = _chain_column_sums(plan, p, device)
+                finally:
+                    plan.close()
+    if not chain:
+        sums = _allreduce_sums(sums, backend, device)
+    return (sums / n).astype(np.float32)
 
 
 def surf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", device=0, n_jobs=-1,

@@ -384,6 +384,12 @@ FS_API int fs_plan_ref_masks(fs_plan* plan, uint64_t* masks, int64_t words);
 FS_API int fs_plan_ref_pass2(fs_plan* plan, const uint64_t* masks, const double* counts,
                              int64_t row_begin, int64_t row_end);
 FS_API int fs_plan_ref_sums(fs_plan* plan, const double* init, double* sums);
+/* The same rank chain for row-sharded ReliefF (fs_plan_create_relieff over
+ * the rank's focal rows, reference order, GPU backend): fs_plan_ref_temp runs
+ * fs_plan_score up to the plan's float32 temp rows (ReliefF.py:208-218) on
+ * every rank at once, then fs_plan_ref_sums continues the previous rank's
+ * column sums over them (ReliefF.py:219-220: one sequential float32 sum). */
+FS_API int fs_plan_ref_temp(fs_plan* plan);
 /* Restrict the next pass2 of a MultiSURF plan to the focal samples
  * [row_begin, row_end) (as fs_multisurf_score_rows; a new plan scores
  * [0, n)).  pass1 / select are unchanged: thresholds and counts are global. */

@@ -272,3 +272,41 @@ def test_fullsize_two_ranks_bitexact(F, tmp_path, name):
     fx = _fixture(name)
     for r in range(2):
         assert_bitexact(np.load(f"{out}.{r}.npy"), fx["scores"])
+
+
+def _relieff_rank_worker(rank, world, port, out_path):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from fastselect_amd import parallel
+    X, y, k = make_tail_case(3)
+    np.save(f"{out_path}.rf.{rank}.npy",
+            parallel.relieff_scores(X, y, n_neighbors=k, backend="gpu", device=0,
+                                    accumulation="reference"))
+    X2, y2 = verdict_case("exp4z", 1100, 150, seed=4)
+    np.save(f"{out_path}.ms.{rank}.npy",
+            parallel.multisurf_scores(X2, y2, use_star=True, backend="gpu", device=0,
+                                      accumulation="reference"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_relieff_ranks_chain_the_column_sums_bitexact(F, oracle, tmp_path, world):
+    """Row-sharded ReliefF in reference order over world ranks (processes
+    sharing cuda:0, gloo): every rank's float32 temp rows at once
+    (fs_plan_ref_temp), then the column sums passed rank to rank
+    (fs_plan_ref_sums) -- the oracle's scores bit for bit on every rank; and
+    parallel.multisurf_scores(accumulation='reference') likewise."""
+    import torch.multiprocessing as mp
+
+    from test_gpu_dist import _port
+    out = str(tmp_path / "rf")
+    mp.spawn(_relieff_rank_worker, args=(world, _port(), out), nprocs=world, join=True)
+    X, y, k = make_tail_case(3)
+    ref = oracle.relieff_scores(X, y, n_neighbors=k)
+    X2, y2 = verdict_case("exp4z", 1100, 150, seed=4)
+    ref2 = oracle.multisurf_scores(X2, y2, use_star=True)
+    for r in range(world):
+        assert_bitexact(np.load(f"{out}.rf.{r}.npy"), ref)
+        assert_bitexact(np.load(f"{out}.ms.{r}.npy"), ref2)
