@@ -211,6 +211,8 @@ struct Plan {
   // ambiguous-pair refinement
   int2* list = nullptr;
   int64_t list_cap = 0;
+  double* pair_part = nullptr;  // k_exact_pairs_rows' per-pair sums between feature chunks
+  int64_t pair_part_cap = 0;
   unsigned long long* list_count = nullptr;
   int64_t n_refined = 0;
   int64_t n_tie_rows = 0;      // ReliefF rows re-ordered by k_rf_ties

@@ -73,22 +73,39 @@ __global__ __launch_bounds__(256) void k_flag_pairs(const double* __restrict__ D
   pairbuf_init(pb);
   const int2 tl = tiles[blockIdx.x];
   const int64_t i0 = (int64_t)tl.x * kTile, j0 = (int64_t)tl.y * kTile;
-  for (int e = threadIdx.x; e < kTile * kTile; e += 256) {
-    const int jj = e / kTile, ii = e % kTile;
-    const int64_t i = i0 + ii, j = j0 + jj;
-    bool amb = false;
-    if (!(i < n && j < n && (tl.x < tl.y || ii < jj))) {
-    } else if (algo == ALGO_MULTISURF) {
-      const double d = D[d_rd(tiled, win, n_pad, blockIdx.x, i0, j0, ii, jj)];
-      amb = __builtin_fabs(d - thr[i]) < delta || __builtin_fabs(d - thr[j]) < delta;
-    } else {
-      const double df = D[d_rd(tiled, win, n_pad, blockIdx.x, i0, j0, ii, jj)] * inv_sc;
-      const float ai = (float)thr[i], aj = (float)thr[j];
-      const double bi = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(ai) + 1u) - (double)ai);
-      const double bj = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(aj) + 1u) - (double)aj);
-      amb = __builtin_fabs(df - thr[i]) < bi || __builtin_fabs(df - thr[j]) < bj;
+  // a thread keeps one ii (e % kTile with e += 256) and reads kU entries of
+  // its column before testing any (the loads of the D block in flight)
+  constexpr int kU = 8;
+  const int ii = threadIdx.x % kTile;
+  const int64_t i = i0 + ii;
+  const double ti = i < n ? thr[i] : 0.0;
+  for (int e0 = threadIdx.x; e0 < kTile * kTile; e0 += 256 * kU) {
+    double dv[kU];
+    bool in[kU];
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int jj = (e0 + 256 * u) / kTile;
+      in[u] = i < n && j0 + jj < n && (tl.x < tl.y || ii < jj);
+      dv[u] = in[u] ? D[d_rd(tiled, win, n_pad, blockIdx.x, i0, j0, ii, jj)] : 0.0;
     }
-    if (amb) pairbuf_add(pb, i, j, list, cap, count);
+#pragma unroll
+    for (int u = 0; u < kU; u++) {
+      const int jj = (e0 + 256 * u) / kTile;
+      const int64_t j = j0 + jj;
+      const double d = dv[u];
+      if (!in[u]) continue;  // outside the triangle or the samples
+      bool amb;
+      if (algo == ALGO_MULTISURF) {
+        amb = __builtin_fabs(d - ti) < delta || __builtin_fabs(d - thr[j]) < delta;
+      } else {
+        const double df = d * inv_sc;
+        const float ai = (float)ti, aj = (float)thr[j];
+        const double bi = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(ai) + 1u) - (double)ai);
+        const double bj = delta + 4.0 * ((double)__uint_as_float(__float_as_uint(aj) + 1u) - (double)aj);
+        amb = __builtin_fabs(df - ti) < bi || __builtin_fabs(df - thr[j]) < bj;
+      }
+      if (amb) pairbuf_add(pb, i, j, list, cap, count);
+    }
   }
   pairbuf_flush(pb, list, cap, count);
 }
@@ -354,37 +371,53 @@ __global__ __launch_bounds__(256) void k_exact_pairs(
 
 // k_exact_pairs for the common layout -- every kept feature continuous, in
 // input order (src_col = identity), float32 X with a 16-byte row pitch --
-// reading both rows as float4 (16 B per lane, 4 KB per wave per row and
-// step, 8 loads in flight per lane) instead of a column-indexed dword
-// gather.  Same arithmetic per feature: f32 |a - b| * f32 recip, summed in
-// f64.  The list is sorted by (i, j), so consecutive waves share row i
-// through L2; row j is the HBM read.
-__global__ __launch_bounds__(256) void k_exact_pairs_rows(
+// reading both rows as float4 (16 B per lane, 8 loads in flight per lane)
+// instead of a column-indexed dword gather.  Same arithmetic per feature: f32
+// |a - b| * f32 recip, summed in f64.  One wave per pair, and as many waves as
+// pairs: the kernel is latency-bound (a wave's loads wait on its list entry),
+// so every pair's loads are in flight at once rather than a wave walking
+// several pairs in turn.  The list is sorted by (i, j), so neighbouring waves
+// share row i through L2.  Wide rows are walked in feature chunks, one launch
+// each ([c4_lo, c4_hi) in float4 units, the pair's partial sum carried in
+// part[k] between launches), so that a chunk of every row stays in the MALL
+// while all pairs read it.
+#ifndef FS_EXACT_CHUNK4
+#define FS_EXACT_CHUNK4 512
+#endif
+#ifndef FS_EXWG
+#define FS_EXWG 512
+#endif
+__global__ __launch_bounds__(FS_EXWG) void k_exact_pairs_rows(
     const float* __restrict__ x, int64_t p, const float* __restrict__ scl32, double sc,
     const int2* __restrict__ list, const unsigned long long* __restrict__ count, int64_t cap,
+    int64_t c4_lo, int64_t c4_hi, int first, int last, double* __restrict__ part,
     int64_t n_pad, int2 tw, int2 win, double* __restrict__ D, const double* __restrict__ thr,
     double thr_tol, unsigned int* __restrict__ unc) {
+  // the chunk's recip is the same for every pair: staged in LDS once per
+  // workgroup of FS_EXWG / 64 pairs instead of read from L2 by every wave
+  __shared__ float4 s4[FS_EXACT_CHUNK4];
   const int lane = threadIdx.x & 63;
-  const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * 256) >> 6;
+  const int64_t wave = ((int64_t)blockIdx.x * FS_EXWG + threadIdx.x) >> 6;
+  const int64_t nw = ((int64_t)gridDim.x * FS_EXWG) >> 6;
   const int64_t total = (int64_t)*count < cap ? (int64_t)*count : cap;
-  const int64_t p4 = p / 4;
-  const float4* __restrict__ s4 = (const float4*)scl32;
+  for (int64_t c = c4_lo + threadIdx.x; c < c4_hi; c += FS_EXWG)
+    s4[c - c4_lo] = ((const float4*)scl32)[c];
+  __syncthreads();
   for (int64_t k = wave; k < total; k += nw) {
     const int2 pr = list[k];
     const float4* __restrict__ xi = (const float4*)(x + (int64_t)pr.x * p);
     const float4* __restrict__ xj = (const float4*)(x + (int64_t)pr.y * p);
     double acc = 0.0;
     constexpr int kU = 4;
-    for (int64_t c0 = lane; c0 < p4; c0 += 64 * kU) {
+    for (int64_t c0 = c4_lo + lane; c0 < c4_hi; c0 += 64 * kU) {
       float4 a[kU], b[kU], w[kU];
 #pragma unroll
       for (int u = 0; u < kU; u++) {
         const int64_t c = c0 + 64 * u;
-        const bool in = c < p4;
+        const bool in = c < c4_hi;
         a[u] = in ? xi[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
         b[u] = in ? xj[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        w[u] = in ? s4[c] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        w[u] = in ? s4[c - c4_lo] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       }
 #pragma unroll
       for (int u = 0; u < kU; u++) {
@@ -396,8 +429,13 @@ __global__ __launch_bounds__(256) void k_exact_pairs_rows(
     }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
     if (lane == 0) {
-      store_pair(D, n_pad, tw, win, pr, acc * sc);
-      if (unc != nullptr) mark_uncertain(pr, acc * sc, thr, thr_tol, unc);
+      if (!first) acc = part[k] + acc;  // the earlier chunks' sum, then this chunk's
+      if (!last) {
+        part[k] = acc;
+      } else {
+        store_pair(D, n_pad, tw, win, pr, acc * sc);
+        if (unc != nullptr) mark_uncertain(pr, acc * sc, thr, thr_tol, unc);
+      }
     }
   }
 }
@@ -523,11 +561,31 @@ static int refine_pairs(Plan* g, int algo, double delta, double thr_tol = 0.0,
   if (g->n_refined == 0) return FS_OK;
   FS_TRY(sort_pair_list(g, g->n_refined));
   const unsigned grid = (unsigned)std::min<int64_t>((g->n_refined + 3) / 4, 8192);
-  if (g->rows_direct && !test_hooks().exact_gather)
-    k_exact_pairs_rows<<<grid, 256, 0, g->stream>>>((const float*)g->x, Q.p_in, g->scl32, Q.SC,
-                                                    g->list, g->list_count, g->list_cap, Q.n_pad,
-                                                    g->tw, g->win, g->D, g->thr, thr_tol, unc);
-  else if (g->x_is_f64)
+  if (g->rows_direct && !test_hooks().exact_gather) {
+    // feature chunks: chunk c of every row is read by all pairs before
+    // chunk c + 1
+    const int64_t p4 = Q.p_in / 4;
+    const int64_t ch4 = FS_EXACT_CHUNK4;  // the LDS copy of recip holds one chunk
+#ifndef FS_EXGRID
+#define FS_EXGRID (1 << 30)
+#endif
+    const int64_t per_wg = FS_EXWG / 64;
+    const unsigned rgrid = (unsigned)std::max<int64_t>(
+        1, std::min<int64_t>((g->n_refined + per_wg - 1) / per_wg, FS_EXGRID));
+    if (ch4 < p4 && g->n_refined > g->pair_part_cap) {
+      g->pair_part_cap = std::max<int64_t>(g->n_refined, g->list_cap);
+      FS_TRY(dalloc(g, &g->pair_part, g->pair_part_cap));
+    }
+    for (int64_t c4 = 0; c4 < p4; c4 += ch4) {
+      const int64_t hi4 = std::min(p4, c4 + ch4);
+      k_exact_pairs_rows<<<rgrid, FS_EXWG, 0, g->stream>>>(
+          (const float*)g->x, Q.p_in, g->scl32, Q.SC, g->list, g->list_count, g->list_cap, c4,
+          hi4, c4 == 0, hi4 == p4, g->pair_part, Q.n_pad, g->tw, g->win, g->D, g->thr, thr_tol,
+          unc);
+      FS_TRY(launch_check("k_exact_pairs_rows"));
+    }
+    return FS_OK;
+  } else if (g->x_is_f64)
     k_exact_pairs<double><<<grid, 256, 0, g->stream>>>(
         (const double*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, Q.SC, g->list,
         g->list_count, g->list_cap, Q.n_pad, g->tw, g->win, 0, g->D, nullptr, g->thr, thr_tol,
