@@ -534,15 +534,23 @@ int reduce_segments(const double* part, int64_t nrows, int64_t PW, const int64_t
 //    J (so the segments of a group start aligned at the chunk's end);
 //  * group = the segments of one chunk from kSchedRows consecutive row
 //    blocks (they share every J they hold);
-//  * block = one group x kSchedFb feature blocks x both halves (<= 32
-//    units, one per CU of an XCD), dealt to the XCD with the least work so
-//    far (workgroup w runs on XCD w % 8; each XCD's list is padded with
-//    empty units to the longest).
+//  * block = one group x kSchedFb feature blocks x both halves (<= 64
+//    units, two rounds of an XCD's 32 CUs), dealt to the XCD with the least
+//    work so far (workgroup w runs on XCD w % 8; each XCD's list is padded
+//    with empty units to the longest).
 // Concurrent units then share their B rows through the XCD's L2 (kSchedRows
 // row blocks x 2 halves read each) and their entry streams (kSchedFb
-// feature blocks read each).
-constexpr int kSchedRows = 8;
-constexpr int kSchedFb = 16 / kSchedRows;
+// feature blocks read each).  16 row blocks x 2 feature blocks against
+// round 4's 8 x 2: pass 2 0.2-0.6 ms shorter at cfg4 on two boxes
+// (profiles/r05/sched_ab.txt; 4 x 4 0.4-0.7 ms longer).
+#ifndef FS_SCHED_ROWS
+#define FS_SCHED_ROWS 16
+#endif
+#ifndef FS_SCHED_UNITS
+#define FS_SCHED_UNITS 32
+#endif
+constexpr int kSchedRows = FS_SCHED_ROWS;
+constexpr int kSchedFb = FS_SCHED_UNITS / kSchedRows;
 
 static int ensure_dev(Plan* g, void** buf, size_t* cap, size_t bytes) {
   if (bytes <= *cap) return FS_OK;
