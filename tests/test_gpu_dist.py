@@ -211,3 +211,33 @@ def test_two_ranks_decide_the_rerun_together(tmp_path):
     X, y = _uniform_family()
     one = F.MultiSURF(backend="gpu", n_features_to_select=10).fit(X, y).feature_importances_
     assert np.max(np.abs(a - one)) <= 1e-6 * np.max(np.abs(one))
+
+
+def test_job_on_a_caller_stream_matches_one_shot():
+    """ShardedMultiSURF on a caller's non-default stream runs its plan and
+    buffers there (with torch's default stream it makes a stream of its own):
+    the scores are the one-shot call's either way, and the result is ready on
+    the caller's stream."""
+    import torch
+    from sklearn.datasets import make_classification
+
+    from fastselect_amd import _lib
+    from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
+
+    X, y = make_classification(n_samples=1200, n_features=300, n_informative=20,
+                               n_redundant=30, random_state=11)
+    x, yv, recip, isd = prepare_inputs(X, y, backend="gpu", device=0)
+    ref = _lib.multisurf_score("gpu", x, yv, recip, None, False, isd)
+    torch.cuda.set_device(0)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        job = ShardedMultiSURF(x, yv, recip, isd, backend="gpu", device=0, shard=False)
+        assert job.stream == s
+        got = job.step().cpu().numpy()
+        job.close()
+    np.testing.assert_array_equal(got, ref)
+    job = ShardedMultiSURF(x, yv, recip, isd, backend="gpu", device=0, shard=False)
+    assert job.stream.cuda_stream != 0
+    got = job.step().cpu().numpy()
+    job.close()
+    np.testing.assert_array_equal(got, ref)
