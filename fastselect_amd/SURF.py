@@ -53,6 +53,14 @@ class SURF(TransformerMixin, BaseEstimator):
         the host).  None: device 0, as the reference; 'all': every visible
         device the job has work for (one per 4096 samples).  Not a reference
         parameter; ignored by backend='cpu'.
+    accumulation : {'fast', 'reference'}, default='fast'
+        'reference': the reference's float32 arithmetic in its n_jobs=1
+        order -- per sample the four float32 sums over neighbours in
+        ascending order (near hits, near misses, far hits, far misses), the
+        float32 score update and one sequential float32 sum over the samples
+        (SURF.py:139-218) -- its scores bit for bit.  'fast': each pair's two
+        directions folded into one weight, float64 partial sums.  Not a
+        reference parameter; 'reference' runs on one device.
     """
 
     def __init__(
@@ -64,6 +72,7 @@ class SURF(TransformerMixin, BaseEstimator):
         n_jobs: int = -1,
         verbose: bool = False,
         devices=None,
+        accumulation: str = "fast",
     ):
         self.n_features_to_select = n_features_to_select
         self.backend = backend
@@ -72,8 +81,10 @@ class SURF(TransformerMixin, BaseEstimator):
         self.n_jobs = n_jobs
         self.verbose = verbose
         self.devices = devices
+        self.accumulation = accumulation
 
     def _validate_parameters(self, n_samples, n_features):
+        _lib.accumulation_code(self.accumulation)
         return _base.resolve_n_select("SURF", self.backend, self.n_features_to_select,
                                       n_samples, n_features)
 
@@ -92,6 +103,7 @@ class SURF(TransformerMixin, BaseEstimator):
             self.effective_backend_ = self.backend
 
         self.devices_ = _base.fit_devices(self.devices, self.effective_backend_, n_samples)
+        _base.check_accumulation_devices(self.accumulation, self.devices_)
         dev0 = self.devices_[0] if self.devices_ else 0
         X = np.ascontiguousarray(X)
         # one upload of X for the whole fit (a multi-device fit uploads per device)
@@ -103,9 +115,10 @@ class SURF(TransformerMixin, BaseEstimator):
             algo_name = "SURF*" if self.use_star else "SURF"
             if self.verbose:
                 print(f"Running {algo_name} on the {self.effective_backend_.upper()} now...")
-            scores = _lib.surf_score(self.effective_backend_, X, y.astype(np.int32), recip_full,
-                                     self.use_star, self.is_discrete_, self.n_jobs,
-                                     devices=self.devices_)
+            with _lib.accumulation(self.accumulation):
+                scores = _lib.surf_score(self.effective_backend_, X, y.astype(np.int32),
+                                         recip_full, self.use_star, self.is_discrete_,
+                                         self.n_jobs, devices=self.devices_)
         self.feature_importances_ = scores
         self.top_features_ = _base.top_features(scores, n_select)
         if self.verbose:
@@ -126,8 +139,9 @@ class SURF(TransformerMixin, BaseEstimator):
         else:
             self.effective_backend_ = self.backend
         is_discrete, recip = surf_inputs(X, self.discrete_limit, self.effective_backend_)
-        plan = _lib.RowsPlan(self.effective_backend_, "surf", X, y.astype(np.int32), recip,
-                             is_discrete, use_star=self.use_star, n_jobs=self.n_jobs)
+        with _lib.accumulation(self.accumulation):  # the plan keeps its creation mode
+            plan = _lib.RowsPlan(self.effective_backend_, "surf", X, y.astype(np.int32), recip,
+                                 is_discrete, use_star=self.use_star, n_jobs=self.n_jobs)
         return ResidentRows(self, "SURF*" if self.use_star else "SURF", plan, n, is_discrete,
                             self.effective_backend_)
 

@@ -48,6 +48,7 @@ EXPORTED = (
     "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_calibration_ex", "fs_plan_weighted_pairs", "fs_plan_kernel_ms",
     "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
     "fs_surf_score_devices", "fs_set_accumulation", "fs_get_accumulation", "fs_test_hook",
+    "fs_multisurf_score_ex", "fs_relieff_score_ex", "fs_surf_score_ex",
 )
 
 
@@ -106,6 +107,10 @@ def _load() -> ctypes.CDLL:
                                      _f32p, _i64, _int, _f32p]
     lib.fs_surf_score.argtypes = [_int, _int, _f64p, _i64, _i64, _i32p, _f32p, _int, _u8p, _int,
                                   _f32p]
+    # the _ex calls: the same arguments plus the accumulation mode before the output
+    lib.fs_multisurf_score_ex.argtypes = list(lib.fs_multisurf_score.argtypes[:-1]) + [_int, _f32p]
+    lib.fs_relieff_score_ex.argtypes = list(lib.fs_relieff_score.argtypes[:-1]) + [_int, _f32p]
+    lib.fs_surf_score_ex.argtypes = list(lib.fs_surf_score.argtypes[:-1]) + [_int, _f32p]
     lib.fs_relieff_score_rows.argtypes = [_int, _int, _f32p, _i64, _i64, _i32p, _f32p, _u8p,
                                           _i64, _f32p, _i64, _int, _i64, _i64, _f64p]
     lib.fs_surf_score_rows.argtypes = [_int, _int, _f64p, _i64, _i64, _i32p, _f32p, _int, _u8p,
@@ -161,7 +166,8 @@ def _load() -> ctypes.CDLL:
                  "fs_plan_pass2", "fs_plan_decision_guard", "fs_plan_ref_mask_words", "fs_plan_ref_masks",
                  "fs_plan_ref_pass2", "fs_plan_ref_sums", "fs_plan_ref_temp", "fs_plan_info", "fs_plan_set_shard", "fs_multisurf_shards", "fs_plan_calibration", "fs_plan_weighted_pairs",
                  "fs_plan_destroy", "fs_multisurf_score_devices", "fs_relieff_score_devices",
-                 "fs_surf_score_devices"):
+                 "fs_surf_score_devices", "fs_multisurf_score_ex", "fs_relieff_score_ex",
+                 "fs_surf_score_ex"):
         getattr(lib, name).restype = _int
     return lib
 
@@ -694,5 +700,5 @@ class RowsPlan(Plan):
 
     def ref_temp(self) -> None:
         """Reference order: the score up to the float32 temp rows, whose column
-        sums ``ref_sums`` continues (``fs_plan_ref_temp``, ReliefF)."""
+        sums ``ref_sums`` continues (``fs_plan_ref_temp``; ReliefF, SURF)."""
         check(_lib.fs_plan_ref_temp(self._h))

@@ -46,18 +46,14 @@ using namespace fs;
 static int map_prep_rc(int rc) { return rc == 0 ? FS_OK : FS_EINVAL; }
 
 // The calling thread's accumulation mode into a prepared problem
-// (fs_set_accumulation).  Reference order exists for MultiSURF and ReliefF,
-// whose per-sample sums and column sums have a fixed order (MultiSURF.py:
-// 198-253, ReliefF.py:181-220); MultiSURF then takes 32-bit pass-1 operands.
+// (fs_set_accumulation).  Reference order: MultiSURF's and ReliefF's
+// per-sample sums and column sums (MultiSURF.py:198-253, ReliefF.py:181-220),
+// SURF's in its n_jobs = 1 order (SURF.py:139-218: with more threads the
+// reference adds its per-thread rows in schedule order); MultiSURF then
+// takes 32-bit pass-1 operands.
 static int apply_accumulation(Prepared& P) {
   P.ref_accum = g_accum == FS_ACCUM_REFERENCE ? 1 : 0;
-  if (!P.ref_accum) return FS_OK;
-  if (P.algo == ALGO_SURF) {
-    set_error("reference-order accumulation is not defined for SURF: the reference sums its "
-              "per-thread score rows in thread-schedule order (SURF.py:195, 216)");
-    return FS_ENOTSUP;
-  }
-  if (P.algo == ALGO_MULTISURF) P.no_q16 = 1;
+  if (P.ref_accum && P.algo == ALGO_MULTISURF) P.no_q16 = 1;
   return FS_OK;
 }
 
@@ -372,7 +368,10 @@ static int surf_sums(int backend, int device, const double* x, int64_t n, int64_
   if (encode_labels_i32(P, y)) return FS_EINVAL;
   P.use_star = use_star ? 1 : 0;
   if ((rc = apply_accumulation(P)) != FS_OK) return rc;
-  if (devices) return gpu::rows_run_devices(P, x, devices, n_devices, r_lo, r_hi, sums);
+  if (devices) {
+    if ((rc = no_reference_devices()) != FS_OK) return rc;
+    return gpu::rows_run_devices(P, x, devices, n_devices, r_lo, r_hi, sums);
+  }
   if (backend == FS_BACKEND_GPU) return gpu::surf_run(P, x, device, r_lo, r_hi, sums);
   return cpu::surf_run(P, x, n_jobs, r_lo, r_hi, sums);
 }
@@ -484,6 +483,56 @@ int fs_surf_score_devices(const int* devices, int n_devices, const double* x, in
   if (rc != FS_OK) return rc;
   return surf_sums(FS_BACKEND_GPU, devices[0], x, n, p, y, recip, use_star, is_discrete, n_jobs,
                    row_begin, row_end, sums_out, devices, n_devices);
+}
+
+}  // extern "C"
+
+// The _ex one-shot calls: the accumulation mode is an argument, in force for
+// that call only (the calling thread's fs_set_accumulation mode is restored
+// on return, whatever it was).
+namespace {
+struct ScopedAccumulation {
+  int prev;
+  explicit ScopedAccumulation(int mode) : prev(g_accum) { g_accum = mode; }
+  ~ScopedAccumulation() { g_accum = prev; }
+};
+int check_mode(int mode) {
+  if (mode == FS_ACCUM_FAST || mode == FS_ACCUM_REFERENCE) return FS_OK;
+  set_error("accumulation must be FS_ACCUM_FAST or FS_ACCUM_REFERENCE");
+  return FS_EINVAL;
+}
+}  // namespace
+
+extern "C" {
+
+int fs_multisurf_score_ex(int backend, int device, const float* x, int64_t n, int64_t p,
+                          const double* y, const float* recip, const int64_t* feat_idx,
+                          int64_t n_kept, int use_star, const uint8_t* is_discrete, int n_jobs,
+                          int accumulation, float* scores_out) {
+  if (const int rc = check_mode(accumulation)) return rc;
+  ScopedAccumulation mode(accumulation);
+  return fs_multisurf_score(backend, device, x, n, p, y, recip, feat_idx, n_kept, use_star,
+                            is_discrete, n_jobs, scores_out);
+}
+
+int fs_relieff_score_ex(int backend, int device, const float* x, int64_t n, int64_t p,
+                        const int32_t* y_enc, const float* recip, const uint8_t* is_discrete,
+                        int64_t k, const float* class_probs, int64_t n_classes, int n_jobs,
+                        int accumulation, float* scores_out) {
+  if (const int rc = check_mode(accumulation)) return rc;
+  ScopedAccumulation mode(accumulation);
+  return fs_relieff_score(backend, device, x, n, p, y_enc, recip, is_discrete, k, class_probs,
+                          n_classes, n_jobs, scores_out);
+}
+
+int fs_surf_score_ex(int backend, int device, const double* x, int64_t n, int64_t p,
+                     const int32_t* y, const float* recip, int use_star,
+                     const uint8_t* is_discrete, int n_jobs, int accumulation,
+                     float* scores_out) {
+  if (const int rc = check_mode(accumulation)) return rc;
+  ScopedAccumulation mode(accumulation);
+  return fs_surf_score(backend, device, x, n, p, y, recip, use_star, is_discrete, n_jobs,
+                       scores_out);
 }
 
 }  // extern "C"
@@ -782,15 +831,15 @@ int fs_plan_ref_pass2(fs_plan* pl, const uint64_t* masks, const double* counts, 
   return gpu::plan_ref_pass2(pl->g, masks, counts, row_begin, row_end);
 }
 
-// ReliefF / MultiSURF GPU plans in reference order (fs_plan_ref_temp, _sums)
-static int ref_rows_plan(fs_plan* pl, bool relieff_only, const char* what) {
+// GPU plans in reference order: fs_plan_ref_temp takes the row plans
+// (ReliefF, SURF), fs_plan_ref_sums every kind
+static int ref_rows_plan(fs_plan* pl, bool rows_only, const char* what) {
   if (!pl) {
     set_error("plan is NULL");
     return FS_EINVAL;
   }
-  const bool ok_algo = pl->P.algo == ALGO_RELIEFF || (!relieff_only && pl->P.algo == ALGO_MULTISURF);
-  if (!ok_algo) {
-    set_error(std::string(what) + (relieff_only ? ": a ReliefF plan" : ": a ReliefF or MultiSURF plan"));
+  if (rows_only && pl->P.algo == ALGO_MULTISURF) {
+    set_error(std::string(what) + ": a ReliefF or SURF plan");
     return FS_EINVAL;
   }
   if (!pl->g || !pl->P.ref_accum) {

@@ -552,6 +552,40 @@ int surf_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int64_t
     for (int64_t j = 0; j < n; j++) s += Df[(size_t)i * n + j];
     avg[i] = (double)s / (double)(n - 1);
   });
+  if (P.ref_accum) {
+    // the reference's n_jobs = 1 order (fs_refacc.hip k_surf_chains): per
+    // focal sample four float32 chains over ascending j of the float32-stored
+    // float64 diffs, score_update in float32, then the float32 column sums
+    // (SURF.py:165-195, 216)
+    const double* X = (const double*)x;
+    const int64_t nk = P.n_kept, rows = r_hi - r_lo;
+    std::vector<float> temp((size_t)std::max<int64_t>(rows, 0) * nk);
+    parallel_for(rows, n_jobs, [&](int64_t r) {
+      const int64_t i = r_lo + r;
+      std::vector<float> acc((size_t)4 * nk, 0.0f);  // near hit, near miss, far hit, far miss
+      for (int64_t j = 0; j < n; j++) {
+        if (j == i) continue;
+        const bool near = (double)Df[(size_t)i * n + j] < avg[i];
+        const bool hit = P.labels[j] == P.labels[i];
+        if (!near && !P.use_star) continue;
+        float* a = acc.data() + (size_t)((near ? 0 : 2) + (hit ? 0 : 1)) * nk;
+        for (int64_t k = 0; k < nk; k++) {
+          const int64_t col = P.kept_col[k];
+          const double u = X[i * P.p_in + col], v = X[j * P.p_in + col];
+          a[k] += P.disc_in[col] ? (u != v ? 1.0f : 0.0f)
+                                 : (float)(std::fabs(u - v) * (double)P.recip_in[col]);
+        }
+      }
+      float* row = temp.data() + (size_t)r * nk;
+      for (int64_t k = 0; k < nk; k++) {
+        float u = acc[nk + k] - acc[k];
+        if (P.use_star) u += acc[2 * nk + k] - acc[3 * nk + k];
+        row[k] = u;
+      }
+    });
+    ref_column_sums(temp, rows, nk, scores);
+    return FS_OK;
+  }
   std::vector<PairW> pairs;
   for (int64_t i = 0; i < n; i++)
     for (int64_t j = i + 1; j < n; j++) {

@@ -238,6 +238,7 @@ struct Plan {
   // decision masks [n_pad][n_pad / 64][4] (plan buffer) and the per-batch
   // flagged-row counts of exact_thresholds
   float* xk = nullptr;
+  double* xk64 = nullptr;       // SURF: the kept columns of its float64 X [n_pad][Kp]
   int64_t Kp = 0;
   int64_t* kcol = nullptr;
   float* krecip = nullptr;
@@ -314,6 +315,10 @@ int run_pass2(Plan* g, double* scores_dev);
 int ref_masks(Plan* g);
 int ref_temp(Plan* g, int64_t rows, float** out);
 int ref_chains(Plan* g, const double* counts, double* scores);
+// SURF reference order (plan_score_surf): the focal rows' masks, chains and
+// float32 column sums (seeded by sums when g->ref_seeded; stopping at the
+// temp rows when g->ref_defer), after the distances and means.
+int surf_ref(Plan* g, double* sums);
 // dst[k] += src[k] over count doubles (k_accumulate)
 int accumulate(double* dst, const double* src, int64_t count, hipStream_t st);
 // sums[out_pos[c]] = the fixed-order sum of part[0..nrows)[c] (k_reduce)
@@ -327,7 +332,7 @@ int relieff_run_one(const Prepared& P, const void* x, int device, int64_t r_lo, 
 int plan_layout(Plan* g);
 int copy_sums(Plan* g, const double* sums_dev, double* sums_out);
 int surf_run_one(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
-                 double* sums_out);
+                 double* sums_out, const double* seed = nullptr);
 // the decision guard's last risk / re-run of this thread (plan_decision_guard)
 extern thread_local double g_last_risk;
 extern thread_local int g_last_rerun;

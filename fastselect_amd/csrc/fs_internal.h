@@ -544,6 +544,19 @@ namespace refacc {
 // Kp a multiple of 256.
 int gather_kept(const float* x, int64_t n, int64_t n_pad, int64_t p_in, const int64_t* kcol,
                 int64_t n_kept, int64_t Kp, float* xk, void* stream);
+// The same for SURF's float64 X (Kp a multiple of 128).
+int gather_kept64(const double* x, int64_t n, int64_t n_pad, int64_t p_in, const int64_t* kcol,
+                  int64_t n_kept, int64_t Kp, double* xk, void* stream);
+// SURF: near-hit / near-miss / far-hit / far-miss bit masks of the focal
+// rows [r_lo, r_hi) from their float32 distance rows and means (avg[n]):
+// masks[((i - r_lo) * (n_pad / 64) + word) * 4 + type].
+int surf_masks(const double* D, int64_t n, int64_t n_pad, const double* avg, const int32_t* lab,
+               int use_star, int64_t r_lo, int64_t r_hi, uint64_t* masks, void* stream);
+// temp[i - r_lo][k] = (near miss - near hit) [+ (far hit - far miss)], each
+// a float32 chain over ascending j (SURF.py:165-193).
+int surf_chains(const double* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
+                const uint8_t* blkdisc, const uint64_t* masks, int64_t n, int64_t n_pad,
+                int use_star, int64_t r_lo, int64_t r_hi, float* temp, void* stream);
 // Near-hit / miss-chain / far-miss bit masks of the owned tiles' pairs:
 // masks[(row * (n_pad / 64) + word) * 4 + type].
 int multisurf_masks(const double* D, int64_t n, int64_t n_pad, const void* tiles, int64_t n_tiles,

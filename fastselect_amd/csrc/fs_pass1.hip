@@ -1127,6 +1127,7 @@ int plan_score_surf(Plan* g, double* sums_dev) {
         g->D, Q.n, Q.n_pad, 1.0, g->r_lo, g->r_hi, g->thr);
     rc = launch_check("k_surf_avg");
   }
+  if (rc == FS_OK && Q.ref_accum) return surf_ref(g, sums_dev);  // fs_refacc.hip order
   if (rc == FS_OK) rc = run_weights(g, nullptr, ALGO_SURF, 1.0);
   if (rc == FS_OK) rc = run_pass2(g, sums_dev);
   return rc;

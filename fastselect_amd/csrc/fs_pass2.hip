@@ -744,6 +744,13 @@ int run_pass2(Plan* g, double* scores_dev) {
 // float32 sums, not yet divided by n).
 int ref_masks(Plan* g) {
   const Prepared& Q = g->P;
+  if (!g->masks) {  // the plan's own masks, on first use
+    const int at = g->alloc_target;
+    g->alloc_target = 0;
+    const int rc = dalloc(g, &g->masks, (size_t)ref_mask_words(g));
+    g->alloc_target = at;
+    FS_TRY(rc);
+  }
   return refacc::multisurf_masks(g->D, Q.n, Q.n_pad, g->tiles, g->n_tiles, g->thr, g->lab,
                                  Q.use_star, g->masks, g->stream);
 }
@@ -763,6 +770,41 @@ int ref_temp(Plan* g, int64_t rows, float** out) {
   }
   *out = g->temp;
   return FS_OK;
+}
+
+// SURF / SURF* in the reference's order (fs_refacc.hip): the masks of the
+// focal rows (a per-call buffer, rows x n_pad / 2 bytes: row-local
+// decisions), the four chains into the temp rows, then the float32 column
+// sums -- continuing from `sums` for a later row panel (ref_seeded), or left
+// for plan_ref_sums (ref_defer: row-sharded SURF over ranks).
+int surf_ref(Plan* g, double* sums) {
+  const Prepared& Q = g->P;
+  const int64_t rows = g->r_hi - g->r_lo;
+  if (!g->ref_defer && !g->ref_seeded)
+    FS_HIP(hipMemsetAsync(sums, 0, sizeof(double) * Q.n_kept, g->stream));
+  if (rows <= 0) {
+    g->ref_rows = 0;
+    return FS_OK;
+  }
+  uint64_t* m = nullptr;
+  g->alloc_target = 2;  // scratch of this plan_score
+  const int rc = dalloc(g, &m, (size_t)rows * (Q.n_pad / 64) * 4);
+  g->alloc_target = 0;
+  FS_TRY(rc);
+  float* temp = nullptr;
+  FS_TRY(ref_temp(g, rows, &temp));
+  FS_HIP(hipEventRecord(g->ev[2], g->stream));
+  FS_TRY(refacc::surf_masks(g->D, Q.n, Q.n_pad, g->thr, g->lab, Q.use_star, g->r_lo, g->r_hi, m,
+                            g->stream));
+  FS_TRY(refacc::surf_chains(g->xk64, g->Kp, g->krecip, g->kdisc, g->kblk, m, Q.n, Q.n_pad,
+                             Q.use_star, g->r_lo, g->r_hi, temp, g->stream));
+  FS_HIP(hipEventRecord(g->ev[3], g->stream));
+  if (g->ref_defer) {
+    g->ref_rows = rows;
+    return FS_OK;
+  }
+  return refacc::column_sums(temp, rows, g->Kp, Q.n_kept, g->ref_seeded ? sums : nullptr, sums,
+                             g->stream);
 }
 
 int ref_chains(Plan* g, const double* counts, double* scores) {

@@ -80,26 +80,33 @@ static int choose_sparse(const Plan* g, const Prepared& P) {
 // discreteness as the reference's kernels read them (MultiSURF.py:184-187,
 // ReliefF.py:151-154), and a flag per 256-feature block that holds a
 // discrete one.  Layout buffers: rebuilt with the feature subset.
+// SURF (float64 X, SURF.py:330-332): the same in float64, 128-padded, one
+// flag per 128-feature block (k_surf_chains' width).
 static int ref_layout(Plan* g) {
   const Prepared& Q = g->P;
-  if (g->x_is_f64) {
-    set_error("reference-order accumulation needs float32 X (MultiSURF / ReliefF)");
+  const bool surf = Q.algo == ALGO_SURF;
+  if (g->x_is_f64 != (surf ? 1 : 0)) {
+    set_error("reference-order accumulation: float32 X for MultiSURF / ReliefF, float64 for SURF");
     return FS_ENOTSUP;
   }
-  g->Kp = (Q.n_kept + 255) / 256 * 256;
+  const int64_t blk_w = surf ? 128 : 256;
+  g->Kp = (Q.n_kept + blk_w - 1) / blk_w * blk_w;
   std::vector<float> rec((size_t)g->Kp, 0.0f);
-  std::vector<uint8_t> dsc((size_t)g->Kp, 0), blk((size_t)(g->Kp / 256), 0);
+  std::vector<uint8_t> dsc((size_t)g->Kp, 0), blk((size_t)(g->Kp / blk_w), 0);
   for (int64_t k = 0; k < Q.n_kept; k++) {
     const int64_t col = Q.kept_col[k];
     rec[k] = Q.recip_in[col];
     dsc[k] = Q.disc_in[col] ? 1 : 0;
-    if (dsc[k]) blk[k / 256] = 1;
+    if (dsc[k]) blk[k / blk_w] = 1;
   }
   g->alloc_target = 1;
+  g->xk = nullptr;
+  g->xk64 = nullptr;
   int rc;
-  if ((rc = dalloc(g, &g->xk, (size_t)Q.n_pad * g->Kp)) || (rc = dalloc(g, &g->kcol, Q.n_kept)) ||
-      (rc = dalloc(g, &g->krecip, g->Kp)) || (rc = dalloc(g, &g->kdisc, g->Kp)) ||
-      (rc = dalloc(g, &g->kblk, g->Kp / 256))) {
+  if ((rc = surf ? dalloc(g, &g->xk64, (size_t)Q.n_pad * g->Kp)
+                 : dalloc(g, &g->xk, (size_t)Q.n_pad * g->Kp)) ||
+      (rc = dalloc(g, &g->kcol, Q.n_kept)) || (rc = dalloc(g, &g->krecip, g->Kp)) ||
+      (rc = dalloc(g, &g->kdisc, g->Kp)) || (rc = dalloc(g, &g->kblk, g->Kp / blk_w))) {
     g->alloc_target = 0;
     return rc;
   }
@@ -109,8 +116,10 @@ static int ref_layout(Plan* g) {
       (rc = h2d(g, g->kdisc, dsc.data(), dsc.size())) ||
       (rc = h2d(g, g->kblk, blk.data(), blk.size())))
     return rc;
-  rc = refacc::gather_kept((const float*)g->x, Q.n, Q.n_pad, Q.p_in, g->kcol, Q.n_kept, g->Kp,
-                           g->xk, g->stream);
+  rc = surf ? refacc::gather_kept64((const double*)g->x, Q.n, Q.n_pad, Q.p_in, g->kcol, Q.n_kept,
+                                    g->Kp, g->xk64, g->stream)
+            : refacc::gather_kept((const float*)g->x, Q.n, Q.n_pad, Q.p_in, g->kcol, Q.n_kept,
+                                  g->Kp, g->xk, g->stream);
   if (rc == FS_OK) FS_HIP(hipStreamSynchronize(g->stream));  // host vectors above
   return rc;
 }
@@ -212,7 +221,7 @@ int plan_layout(Plan* g) {
       (rc = h2d(g, g->dtab, Q.dtab.data(), Q.dtab.size())))
     return rc;
   if ((rc = size_exact_rows(g))) return rc;
-  if (Q.ref_accum && Q.algo != ALGO_SURF && (rc = ref_layout(g))) return rc;
+  if (Q.ref_accum && (rc = ref_layout(g))) return rc;
   if ((rc = calibrate_band(g))) return rc;
   if ((rc = row_guard(g))) return rc;
   if (g->calib[5] != 0.0 && (rc = apply_operand_width(g))) return rc;
@@ -417,12 +426,15 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
     g->thr_rows = (int)(g->thr_all ? Q.n : exact_thr_rows(Q.n, Q.pc + Q.pd));
     if ((rc = dalloc(g, &g->unc, Q.n_pad)) || (rc = dalloc(g, &g->urows, Q.n_pad + 1)))
       return fail(rc);
-    // reference-order accumulation: the decision masks (n_pad^2 / 2 bytes)
-    // and exact_thresholds' batch counts (every flagged row is fixed, in
-    // batches of thr_rows)
+    // reference-order accumulation: exact_thresholds' batch counts (every
+    // flagged row is fixed, in batches of thr_rows).  thr_rows changes with
+    // the feature layout (size_exact_rows) but never falls below
+    // kExactThrRows, so n / kExactThrRows + 2 batches cover every layout a
+    // later fs_plan_set_features may choose.  The decision masks
+    // (n_pad^2 / 2 bytes) are allocated on first use by the one-device pass 2
+    // (ref_masks): a multi-rank job writes into its own all-reduced buffer.
     if (Q.ref_accum &&
-        ((rc = dalloc(g, &g->masks, (size_t)Q.n_pad * (Q.n_pad / 64) * 4)) ||
-         (rc = dalloc(g, &g->bcnt, (size_t)(Q.n / std::max(g->thr_rows, 1) + 2)))))
+        (rc = dalloc(g, &g->bcnt, (size_t)(Q.n / kExactThrRows + 2))))
       return fail(rc);
   }
   g->sparse = choose_sparse(g, Q);
@@ -821,10 +833,27 @@ static int run_panels(const Prepared& P, int64_t r_lo, int64_t r_hi, int64_t pan
   return FS_OK;
 }
 
+// Reference order (ReliefF / SURF): one float32 column sum over all panels,
+// each panel's plan continuing the previous panel's sums (ReliefF.py:219-220,
+// SURF.py:195: one sequential sum over the focal samples).
+template <typename Fn>
+static int run_panels_chained(const Prepared& P, const void* x, int device, int64_t r_lo,
+                              int64_t r_hi, int64_t panel, double* sums_out, Fn&& one_seeded) {
+  std::vector<double> prev((size_t)P.n_kept, 0.0);
+  for (int64_t lo = r_lo; lo < r_hi;) {
+    const int64_t hi = std::min(r_hi, (lo / kTile * kTile) + panel);
+    FS_TRY(one_seeded(P, x, device, lo, hi, sums_out, lo == r_lo ? nullptr : prev.data()));
+    std::copy(sums_out, sums_out + P.n_kept, prev.begin());
+    lo = hi;
+  }
+  return FS_OK;
+}
+
 int surf_run(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
              double* sums_out) {
   const int64_t panel = row_panel_rows(P, device, r_hi - r_lo);
   if (r_hi - r_lo <= panel) return surf_run_one(P, x, device, r_lo, r_hi, sums_out);
+  if (P.ref_accum) return run_panels_chained(P, x, device, r_lo, r_hi, panel, sums_out, surf_run_one);
   return run_panels(P, r_lo, r_hi, panel, sums_out, [&](int64_t lo, int64_t hi, double* o) {
     return surf_run_one(P, x, device, lo, hi, o);
   });
@@ -834,28 +863,24 @@ int relieff_run(const Prepared& P, const void* x, int device, int64_t r_lo, int6
                 double* sums_out) {
   const int64_t panel = row_panel_rows(P, device, r_hi - r_lo);
   if (r_hi - r_lo <= panel) return relieff_run_one(P, x, device, r_lo, r_hi, sums_out);
-  if (P.ref_accum) {
-    // one float32 column sum over all panels, each continuing the last
-    std::vector<double> prev((size_t)P.n_kept, 0.0);
-    for (int64_t lo = r_lo; lo < r_hi;) {
-      const int64_t hi = std::min(r_hi, (lo / kTile * kTile) + panel);
-      FS_TRY(relieff_run_one(P, x, device, lo, hi, sums_out, lo == r_lo ? nullptr : prev.data()));
-      std::copy(sums_out, sums_out + P.n_kept, prev.begin());
-      lo = hi;
-    }
-    return FS_OK;
-  }
+  if (P.ref_accum) return run_panels_chained(P, x, device, r_lo, r_hi, panel, sums_out, relieff_run_one);
   return run_panels(P, r_lo, r_hi, panel, sums_out, [&](int64_t lo, int64_t hi, double* o) {
     return relieff_run_one(P, x, device, lo, hi, o);
   });
 }
 
 int surf_run_one(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,
-                 double* sums_out) {
+                 double* sums_out, const double* seed) {
   Plan* g = nullptr;
   FS_TRY(plan_create(&g, P, x, 1, device, 0, 1, 0, r_lo, r_hi));
   double* sc = nullptr;
   int rc = dalloc(g, &sc, g->P.n_kept);
+  if (rc == FS_OK && seed) {
+    // reference order, a later row panel: the float32 column sums go on from
+    // the previous panels' (SURF.py:195 is one sequential sum)
+    g->ref_seeded = true;
+    rc = h2d(g, sc, seed, (size_t)g->P.n_kept);
+  }
   if (rc == FS_OK) rc = plan_score_surf(g, sc);
   if (rc == FS_OK) rc = copy_sums(g, sc, sums_out);
   plan_destroy(g);

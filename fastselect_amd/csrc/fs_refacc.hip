@@ -27,9 +27,12 @@
 //   float64 hit / miss sums in that order, the float64 update, temp[i][k] =
 //   f32(update), and the same sequential float32 column sum.
 //
-// SURF stays on the default path: its per-thread private score rows
-// (SURF.py:195, 216) are summed in an order that depends on numba's thread
-// schedule, so no fixed order is the reference's.
+//   SURF / SURF* (SURF.py:139-218): the reference's order at n_jobs = 1 (its
+//   only fixed one: with more threads the per-thread private score rows are
+//   summed in schedule order) -- per focal sample four float32 chains in
+//   ascending j (near hit / near miss / far hit / far miss) of the float32-
+//   stored float64 diffs, score_update in float32, and one sequential float32
+//   sum over the samples: k_surf_masks, k_surf_chains, k_ref_colsum.
 //
 // Kernels (cfg4 figures in DESIGN.md §Reference-order accumulation):
 //   k_ref_gather   kept columns of X into a 256-padded row-major copy.  HBM
@@ -43,6 +46,11 @@
 //                  (v_sub, v_mul |.|, v_add).                     VALU / LDS
 //   k_ref_colsum   sequential float32 column sums, 64 rows of loads in
 //                  flight per lane.                                 latency
+//   k_surf_masks   SURF's four decision masks per focal row from its float32
+//                  D row and mean.                                     HBM
+//   k_surf_chains  k_ms_chains on float64 X: 128 features per workgroup,
+//                  2 per lane; per entry one ds_read_b128 and 2 x (v_add_f64,
+//                  v_mul_f64 |.|, v_cvt_f32_f64, v_add_f32).     VALU (f64)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -98,16 +106,18 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
 // ---- kept columns ------------------------------------------------------------
 // xk[j][k] = x[j][kcol[k]] for j < n, k < n_kept; 0 in the padding (rows up to
 // n_pad, columns up to Kp), so staged padding rows / lanes contribute nothing.
-__global__ __launch_bounds__(256) void k_ref_gather(const float* __restrict__ x, int64_t n,
+// float32 X (MultiSURF, ReliefF) or float64 X (SURF, SURF.py:330-332).
+template <typename T>
+__global__ __launch_bounds__(256) void k_ref_gather(const T* __restrict__ x, int64_t n,
                                                     int64_t n_pad, int64_t p_in,
                                                     const int64_t* __restrict__ kcol,
                                                     int64_t n_kept, int64_t Kp,
-                                                    float* __restrict__ xk) {
+                                                    T* __restrict__ xk) {
   const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (k >= Kp) return;
   const int64_t col = k < n_kept ? kcol[k] : -1;
   for (int64_t j = blockIdx.y; j < n_pad; j += gridDim.y)
-    xk[j * Kp + k] = (j < n && col >= 0) ? x[j * p_in + col] : 0.0f;
+    xk[j * Kp + k] = (j < n && col >= 0) ? x[j * p_in + col] : (T)0;
 }
 
 // ---- MultiSURF decisions as bit masks ------------------------------------------
@@ -543,15 +553,269 @@ __global__ __launch_bounds__(256) void k_rf_ref_update(
   }
 }
 
+// ---- SURF / SURF* ----------------------------------------------------------------
+// The reference's n_jobs = 1 order (SURF.py:139-218): for each focal sample i
+// in turn, four float32 vector sums over j in ascending order -- near hits,
+// near misses, far hits, far misses (the far ones for SURF* only) -- of the
+// float32-stored diffs f32(|x_i - x_j| * recip) (x float64, SURF.py:153-158),
+// then score_update = (near_miss - near_hit) [+ (far_hit - far_miss)] in
+// float32 and private_scores[0] += score_update: one sequential float32 sum
+// per feature over the focal samples (k_ref_colsum).  With several numba
+// threads the reference adds its per-thread rows in schedule order; n_jobs =
+// 1 is its one fixed order, and the one this mode replays.
+
+// Decisions of the focal rows [r_lo, r_hi) as bit masks:
+// masks[((i - r_lo) * nw + w) * 4 + t], t = 0 near hits, 1 near misses, 2 far
+// hits, 3 far misses (SURF*; 0 for SURF), bit b of word w = sample 64 w + b.
+// near: float32 D_ij < avg_i, j != i (SURF.py:170-189; the float32 D is the
+// float64 distance rounded, as k_surf_avg and pair_weight take it).  Grid
+// (ceil(rows / 4), ceil(nw / 64)): one wave per row and 64 words, lane l
+// reads sample 64 w + l of every word (coalesced) and keeps word w0 + l's
+// four ballots.  D: the plan's rows (full layout, row i = D + i n_pad).
+__global__ __launch_bounds__(256) void k_surf_masks(const double* __restrict__ D, int64_t n,
+                                                    int64_t n_pad, int64_t nw,
+                                                    const double* __restrict__ avg,
+                                                    const int32_t* __restrict__ lab, int use_star,
+                                                    int64_t r_lo, int64_t r_hi,
+                                                    uint64_t* __restrict__ masks) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = r_lo + (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= r_hi) return;  // uniform across the wave
+  const int64_t w0 = (int64_t)blockIdx.y * 64;
+  const int wn = nw - w0 < 64 ? (int)(nw - w0) : 64;
+  const double t = avg[i];
+  const int32_t li = lab[i];
+  const double* row = D + i * n_pad;
+  uint64_t keep[4] = {0, 0, 0, 0};
+  for (int u = 0; u < wn; u++) {
+    const int64_t j = (w0 + u) * 64 + lane;  // < n_pad: row j and lab[j] exist
+    const bool ok = j < n && j != i;
+    const bool near = ok && (double)(float)row[j] < t;
+    const bool hit = ok && lab[j] == li;
+    const bool far = use_star && ok && !near;
+    const uint64_t m0 = __ballot(near && hit), m1 = __ballot(near && !hit);
+    const uint64_t m2 = __ballot(far && hit), m3 = __ballot(far && !hit);
+    if (lane == u) {
+      keep[0] = m0;
+      keep[1] = m1;
+      keep[2] = m2;
+      keep[3] = m3;
+    }
+  }
+  if (lane < wn) {
+    uint64_t* o = masks + ((size_t)(i - r_lo) * nw + (size_t)(w0 + lane)) * 4;
+    *(ulonglong2*)(o + 0) = make_ulonglong2(keep[0], keep[1]);
+    *(ulonglong2*)(o + 2) = make_ulonglong2(keep[2], keep[3]);
+  }
+}
+
+// One entry of a SURF chain for the lane's 2 features: the reference's
+// float64 |x_i - x_j| * recip stored as float32 (1 / 0 for a discrete
+// feature), added in float32.
+template <bool DISC>
+__device__ __forceinline__ void surf_step(const double2 v, const double (&a)[2],
+                                          const double (&rc)[2], uint32_t dk, float (&acc)[2]) {
+  const double vb[2] = {v.x, v.y};
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    float d = (float)(__builtin_fabs(a[k] - vb[k]) * rc[k]);
+    if (DISC && ((dk >> k) & 1u)) d = a[k] != vb[k] ? 1.0f : 0.0f;
+    acc[k] += d;
+  }
+}
+
+// chain_walk's schedule (groups of 8, then 4, then the last 1-3 entries, each
+// group's LDS reads issued ahead of its arithmetic) for a SURF chain.
+template <bool DISC>
+__device__ __forceinline__ void surf_walk(uint64_t m, const double2* __restrict__ buf, int lane,
+                                          const double (&a)[2], const double (&rc)[2],
+                                          uint32_t dk, float (&acc)[2]) {
+  while (__builtin_popcountll(m) >= 8) {
+    int b[8];
+    double2 v[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) b[q] = pop_bit(m);
+#pragma unroll
+    for (int q = 0; q < 8; q++) v[q] = buf[b[q] * 64 + lane];
+#pragma unroll
+    for (int q = 0; q < 8; q++) surf_step<DISC>(v[q], a, rc, dk, acc);
+  }
+  while (__builtin_popcountll(m) >= 4) {
+    const int b0 = pop_bit(m), b1 = pop_bit(m), b2 = pop_bit(m), b3 = pop_bit(m);
+    const double2 v0 = buf[b0 * 64 + lane], v1 = buf[b1 * 64 + lane];
+    const double2 v2 = buf[b2 * 64 + lane], v3 = buf[b3 * 64 + lane];
+    surf_step<DISC>(v0, a, rc, dk, acc);
+    surf_step<DISC>(v1, a, rc, dk, acc);
+    surf_step<DISC>(v2, a, rc, dk, acc);
+    surf_step<DISC>(v3, a, rc, dk, acc);
+  }
+  while (m != 0) {
+    const int b0 = pop_bit(m);
+    surf_step<DISC>(buf[b0 * 64 + lane], a, rc, dk, acc);
+  }
+}
+
+// Chunk c's samples (64 rows x 128 float64 features = 1 KB each) into LDS,
+// one global_load_lds_dwordx4 per row, as stage_chunk.
+__device__ __forceinline__ void stage_chunk64(const double* __restrict__ xk, int64_t Kp,
+                                              int64_t f0, int wave, int lane, double2* buf,
+                                              int64_t c) {
+#pragma unroll
+  for (int s = 0; s < kChunk / kWaves; s++) {
+    const int t = wave * (kChunk / kWaves) + s;
+    const double* src = xk + (c * kChunk + t) * Kp + f0 + 2 * lane;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(buf + t * 64), 16,
+                                     0, 0);
+  }
+}
+
+// k_ms_chains' structure for SURF: grid (row blocks of kRowsWG focal rows of
+// [r_lo, r_hi), Kp / 128 feature blocks); wave w holds kRowsW rows -- x_i
+// (float64) and their 2 (SURF) or 4 (SURF*) float32 chains for the lane's
+// features 2 lane + k -- in VGPRs; the j chunks (one mask word each) staged
+// by global_load_lds, double-buffered; each row's chains walked in order
+// near hit, near miss, far hit, far miss (independent sums, so the order of
+// the walks does not matter, only the ascending j within each).
+constexpr int kFeat64 = 128;  // features per k_surf_chains workgroup (64 lanes x 2)
+template <bool STAR, bool DISC>
+__device__ __forceinline__ void surf_chains_body(
+    const double* __restrict__ xk, int64_t Kp, const float* __restrict__ krecip,
+    const uint8_t* __restrict__ kdisc, const uint64_t* __restrict__ masks, int64_t nw,
+    int64_t nch, int64_t r_lo, int64_t r_hi, float* __restrict__ temp, double2* bufA,
+    double2* bufB) {
+  constexpr int NC = STAR ? 4 : 2;  // chains per row
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int64_t f0 = (int64_t)blockIdx.y * kFeat64;
+  const int64_t row0 = r_lo + (int64_t)blockIdx.x * kRowsWG + wave * kRowsW;
+
+  double rc[2];
+  uint32_t dk = 0;
+#pragma unroll
+  for (int k = 0; k < 2; k++) {
+    rc[k] = (double)krecip[f0 + 2 * lane + k];
+    if (DISC) dk |= (kdisc[f0 + 2 * lane + k] ? 1u : 0u) << k;
+  }
+  double a[kRowsW][2];
+  float acc[kRowsW][NC][2];
+#pragma unroll
+  for (int r = 0; r < kRowsW; r++) {
+    const int64_t i = row0 + r;
+    const double2 v = i < r_hi ? *(const double2*)(xk + i * Kp + f0 + 2 * lane)
+                               : make_double2(0.0, 0.0);
+    a[r][0] = v.x;
+    a[r][1] = v.y;
+#pragma unroll
+    for (int t = 0; t < NC; t++) acc[r][t][0] = acc[r][t][1] = 0.0f;
+  }
+  // mask words of chunk c: lane 4 r + t <- masks[row0 + r - r_lo][c][t]
+  const int mr = lane >> 2, mt = lane & 3;
+  const bool mload = lane < 4 * kRowsW && row0 + mr < r_hi;
+  const uint64_t* mrow = masks + ((size_t)(row0 + (mload ? mr : 0) - r_lo) * nw) * 4 + mt;
+  auto rows_of = [&](const double2* buf, uint64_t mw) {
+#pragma unroll
+    for (int r = 0; r < kRowsW; r++)
+#pragma unroll
+      for (int t = 0; t < NC; t++)
+        surf_walk<DISC>(readlane64(mw, 4 * r + t), buf, lane, a[r], rc, dk, acc[r][t]);
+  };
+  uint64_t mw = mload ? chunk_word(mrow, 0) : 0ull;
+  stage_chunk64(xk, Kp, f0, wave, lane, bufA, 0);
+  __syncthreads();
+  for (int64_t c = 0; c < nch; c += 2) {
+    uint64_t mn = 0;
+    if (c + 1 < nch) {
+      mn = mload ? chunk_word(mrow, c + 1) : 0ull;
+      stage_chunk64(xk, Kp, f0, wave, lane, bufB, c + 1);
+    }
+    rows_of(bufA, mw);
+    __syncthreads();
+    if (c + 1 >= nch) break;
+    mw = mn;
+    if (c + 2 < nch) {
+      mn = mload ? chunk_word(mrow, c + 2) : 0ull;
+      stage_chunk64(xk, Kp, f0, wave, lane, bufA, c + 2);
+    }
+    rows_of(bufB, mw);
+    __syncthreads();
+    mw = mn;
+  }
+  // SURF.py:191-193: score_update = (near_miss - near_hit) [+ (far_hit - far_miss)]
+#pragma unroll
+  for (int r = 0; r < kRowsW; r++) {
+    const int64_t i = row0 + r;
+    if (i >= r_hi) continue;
+    float o[2];
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+      float u = acc[r][1][k] - acc[r][0][k];
+      if (STAR) u += acc[r][2 % NC][k] - acc[r][3 % NC][k];
+      o[k] = u;
+    }
+    *(float2*)(temp + (i - r_lo) * Kp + f0 + 2 * lane) = make_float2(o[0], o[1]);
+  }
+}
+
+template <bool STAR>
+__global__ __launch_bounds__(64 * kWaves) void k_surf_chains(
+    const double* __restrict__ xk, int64_t Kp, const float* __restrict__ krecip,
+    const uint8_t* __restrict__ kdisc, const uint8_t* __restrict__ blkdisc,
+    const uint64_t* __restrict__ masks, int64_t nw, int64_t nch, int64_t r_lo, int64_t r_hi,
+    float* __restrict__ temp) {
+  __shared__ double2 bufA[kChunk * 64];
+  __shared__ double2 bufB[kChunk * 64];
+  if (blkdisc[blockIdx.y])
+    surf_chains_body<STAR, true>(xk, Kp, krecip, kdisc, masks, nw, nch, r_lo, r_hi, temp, bufA,
+                                 bufB);
+  else
+    surf_chains_body<STAR, false>(xk, Kp, krecip, kdisc, masks, nw, nch, r_lo, r_hi, temp, bufA,
+                                  bufB);
+}
+
 }  // namespace
 
 int gather_kept(const float* x, int64_t n, int64_t n_pad, int64_t p_in, const int64_t* kcol,
                 int64_t n_kept, int64_t Kp, float* xk, void* stream) {
   const hipStream_t s = (hipStream_t)stream;
   const unsigned gy = (unsigned)(n_pad < 4096 ? n_pad : 4096);
-  k_ref_gather<<<dim3((unsigned)(Kp / 256), gy), 256, 0, s>>>(x, n, n_pad, p_in, kcol, n_kept,
-                                                                Kp, xk);
+  k_ref_gather<float><<<dim3((unsigned)(Kp / 256), gy), 256, 0, s>>>(x, n, n_pad, p_in, kcol,
+                                                                       n_kept, Kp, xk);
   return check("k_ref_gather");
+}
+
+int gather_kept64(const double* x, int64_t n, int64_t n_pad, int64_t p_in, const int64_t* kcol,
+                  int64_t n_kept, int64_t Kp, double* xk, void* stream) {
+  const hipStream_t s = (hipStream_t)stream;
+  const unsigned gy = (unsigned)(n_pad < 4096 ? n_pad : 4096);
+  k_ref_gather<double><<<dim3((unsigned)((Kp + 255) / 256), gy), 256, 0, s>>>(
+      x, n, n_pad, p_in, kcol, n_kept, Kp, xk);
+  return check("k_ref_gather<double>");
+}
+
+int surf_masks(const double* D, int64_t n, int64_t n_pad, const double* avg, const int32_t* lab,
+               int use_star, int64_t r_lo, int64_t r_hi, uint64_t* masks, void* stream) {
+  if (r_hi <= r_lo) return FS_OK;
+  const int64_t nw = n_pad / 64;
+  k_surf_masks<<<dim3((unsigned)((r_hi - r_lo + 3) / 4), (unsigned)((nw + 63) / 64)), 256, 0,
+                 (hipStream_t)stream>>>(D, n, n_pad, nw, avg, lab, use_star, r_lo, r_hi, masks);
+  return check("k_surf_masks");
+}
+
+int surf_chains(const double* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
+                const uint8_t* blkdisc, const uint64_t* masks, int64_t n, int64_t n_pad,
+                int use_star, int64_t r_lo, int64_t r_hi, float* temp, void* stream) {
+  if (r_hi <= r_lo) return FS_OK;
+  const dim3 grid((unsigned)((r_hi - r_lo + kRowsWG - 1) / kRowsWG), (unsigned)(Kp / kFeat64));
+  const int64_t nch = (n + kChunk - 1) / kChunk;
+  const hipStream_t s = (hipStream_t)stream;
+  if (use_star)
+    k_surf_chains<true><<<grid, 64 * kWaves, 0, s>>>(xk, Kp, krecip, kdisc, blkdisc, masks,
+                                                      n_pad / 64, nch, r_lo, r_hi, temp);
+  else
+    k_surf_chains<false><<<grid, 64 * kWaves, 0, s>>>(xk, Kp, krecip, kdisc, blkdisc, masks,
+                                                       n_pad / 64, nch, r_lo, r_hi, temp);
+  return check("k_surf_chains");
 }
 
 int multisurf_masks(const double* D, int64_t n, int64_t n_pad, const void* tiles, int64_t n_tiles,

@@ -538,17 +538,41 @@ def relieff_scores(X, y, n_neighbors=3, discrete_limit=10, backend="gpu", device
 
 
 def surf_scores(X, y, use_star=False, discrete_limit=10, backend="gpu", device=0, n_jobs=-1,
-                gather=None):
+                gather=None, accumulation="fast"):
     """SURF / SURF* feature scores with the focal samples sharded over the
     ranks (see ``relieff_scores``); X (float64, SURF.py:330-332) reaches the
-    GPUs by per-rank rows + one RCCL all-gather of float64 rows."""
+    GPUs by per-rank rows + one RCCL all-gather of float64 rows.
+
+    accumulation='reference': the reference's float32 scores (its n_jobs=1
+    order) bit for bit: every rank forms its float32 temp rows at once
+    (``fs_plan_ref_temp``) and the column sums pass from rank to rank in
+    sample order (SURF.py:195: one sequential float32 sum)."""
     from .SURF import surf_inputs
     x = np.ascontiguousarray(X, dtype=np.float64)
     n, p = x.shape
+    _lib.accumulation_code(accumulation)
     backend = _base.effective_backend(backend)
     _, rank, world = _dist()
+    chain = accumulation == "reference" and world > 1
+    if chain and backend != "gpu":
+        raise ValueError("accumulation='reference' over world > 1 ranks runs on the GPU "
+                         "backend (fs_plan_ref_temp / fs_plan_ref_sums)")
+    yi = np.asarray(y).astype(np.int32)
     with resident_x(x, backend, device, gather):
         isd, recip = surf_inputs(x, discrete_limit, backend, device)
-        sums = _lib.surf_score(backend, x, np.asarray(y).astype(np.int32), recip, use_star, isd,
-                               n_jobs, device=device, rows=shard_rows(n, rank, world))
-    return (_allreduce_sums(sums, backend, device) / n).astype(np.float32)
+        with _lib.accumulation(accumulation):
+            if not chain:
+                sums = _lib.surf_score(backend, x, yi, recip, use_star, isd, n_jobs,
+                                       device=device, rows=shard_rows(n, rank, world))
+            else:
+                plan = _lib.RowsPlan(backend, "surf", x, yi, recip, isd, use_star=use_star,
+                                     rows=shard_rows(n, rank, world), n_jobs=n_jobs,
+                                     device=device)
+                try:
+                    plan.ref_temp()
+                    sums = _chain_column_sums(plan, p, device)
+                finally:
+                    plan.close()
+    if not chain:
+        sums = _allreduce_sums(sums, backend, device)
+    return (sums / n).astype(np.float32)

@@ -18,13 +18,14 @@ class SURFstar(SURF):
     use_star = True
 
     def __init__(self, n_features_to_select=0.2, backend="auto", discrete_limit=10, n_jobs=-1,
-                 verbose=False, devices=None):
+                 verbose=False, devices=None, accumulation="fast"):
         self.n_features_to_select = n_features_to_select
         self.backend = backend
         self.discrete_limit = discrete_limit
         self.n_jobs = n_jobs
         self.verbose = verbose
         self.devices = devices
+        self.accumulation = accumulation
 
 
 class MultiSURFstar(MultiSURF):

@@ -81,15 +81,29 @@ extern "C" {
  *                       the float64 update over argsort-ordered neighbours and
  *                       the same column sums.  MultiSURF then runs pass 1 on
  *                       32-bit operands with exact thresholds for every
- *                       flagged row.  The scores are then the reference's
- *                       arithmetic bit for bit (tests/test_refacc*.py).  SURF
- *                       has no fixed reference order (its per-thread rows,
- *                       SURF.py:195, 216): FS_ENOTSUP.  The one-shot calls
- *                       and fs_*_score_devices run on one device (FS_ENOTSUP
- *                       otherwise); GPU MultiSURF plans with world > 1 run
- *                       pass 2 as fs_plan_ref_masks / fs_plan_ref_pass2 /
- *                       fs_plan_ref_sums (CPU backend: FS_ENOTSUP).
- * previous (nullable) receives the mode in force before the call.
+ *                       flagged row.  SURF / SURF*: the reference's order at
+ *                       n_jobs = 1 (its one fixed order; with more numba
+ *                       threads it adds per-thread rows in schedule order,
+ *                       SURF.py:195, 216): four float32 chains per sample in
+ *                       ascending j, score_update in float32, one sequential
+ *                       float32 sum over the samples (SURF.py:139-218).  The
+ *                       scores are then bit-identical to the oracle's
+ *                       sequential restatement of the reference's float32
+ *                       order (oracle/relief_oracle.c; tests/test_refacc*.py).
+ *                       The reference kernels are @njit(fastmath=True), which
+ *                       lets LLVM reassociate its float64 distance sums; no
+ *                       reference-produced fixture pins that level, so parity
+ *                       with numba's own bits is unpinned.  The
+ *                       one-shot calls and fs_*_score_devices with more than
+ *                       one device run on one device (FS_ENOTSUP otherwise);
+ *                       GPU MultiSURF plans with world > 1 run pass 2 as
+ *                       fs_plan_ref_masks / fs_plan_ref_pass2 /
+ *                       fs_plan_ref_sums, row plans (ReliefF, SURF) as
+ *                       fs_plan_ref_temp / fs_plan_ref_sums (CPU backend:
+ *                       FS_ENOTSUP).
+ * previous (nullable) receives the mode in force before the call.  The mode
+ * is per thread: a caller that scores from several threads passes it per
+ * call instead (fs_*_score_ex below).
  */
 FS_API int fs_set_accumulation(int mode, int* previous);
 FS_API int fs_get_accumulation(void);
@@ -234,6 +248,29 @@ FS_API int fs_relieff_score(int backend, int device, const float* x, int64_t n, 
 FS_API int fs_surf_score(int backend, int device, const double* x, int64_t n, int64_t p,
                   const int32_t* y, const float* recip, int use_star,
                   const uint8_t* is_discrete, int n_jobs, float* scores_out);
+
+/*
+ * The three one-shot calls with the accumulation mode as an argument
+ * (FS_ACCUM_FAST / FS_ACCUM_REFERENCE, as fs_set_accumulation documents),
+ * for that call only: the calling thread's fs_set_accumulation mode is
+ * neither read nor changed.  Other arguments as fs_multisurf_score /
+ * fs_relieff_score / fs_surf_score, which they replace for callers that do
+ * not own the thread they score on (the reference's host callers take no
+ * such mode: MultiSURF.py:256, ReliefF.py:222, SURF.py:198).
+ */
+FS_API int fs_multisurf_score_ex(int backend, int device, const float* x, int64_t n, int64_t p,
+                                 const double* y, const float* recip, const int64_t* feat_idx,
+                                 int64_t n_kept, int use_star, const uint8_t* is_discrete,
+                                 int n_jobs, int accumulation, float* scores_out);
+FS_API int fs_relieff_score_ex(int backend, int device, const float* x, int64_t n, int64_t p,
+                               const int32_t* y_enc, const float* recip,
+                               const uint8_t* is_discrete, int64_t k, const float* class_probs,
+                               int64_t n_classes, int n_jobs, int accumulation,
+                               float* scores_out);
+FS_API int fs_surf_score_ex(int backend, int device, const double* x, int64_t n, int64_t p,
+                            const int32_t* y, const float* recip, int use_star,
+                            const uint8_t* is_discrete, int n_jobs, int accumulation,
+                            float* scores_out);
 
 /*
  * Row-sharded ReliefF / SURF: the float64 score SUMS (not
@@ -384,11 +421,12 @@ FS_API int fs_plan_ref_masks(fs_plan* plan, uint64_t* masks, int64_t words);
 FS_API int fs_plan_ref_pass2(fs_plan* plan, const uint64_t* masks, const double* counts,
                              int64_t row_begin, int64_t row_end);
 FS_API int fs_plan_ref_sums(fs_plan* plan, const double* init, double* sums);
-/* The same rank chain for row-sharded ReliefF (fs_plan_create_relieff over
- * the rank's focal rows, reference order, GPU backend): fs_plan_ref_temp runs
- * fs_plan_score up to the plan's float32 temp rows (ReliefF.py:208-218) on
- * every rank at once, then fs_plan_ref_sums continues the previous rank's
- * column sums over them (ReliefF.py:219-220: one sequential float32 sum). */
+/* The same rank chain for row-sharded ReliefF and SURF (fs_plan_create_relieff
+ * / fs_plan_create_surf over the rank's focal rows, reference order, GPU
+ * backend): fs_plan_ref_temp runs fs_plan_score up to the plan's float32 temp
+ * rows (ReliefF.py:208-218, SURF.py:191-193) on every rank at once, then
+ * fs_plan_ref_sums continues the previous rank's column sums over them
+ * (ReliefF.py:219-220, SURF.py:195: one sequential float32 sum). */
 FS_API int fs_plan_ref_temp(fs_plan* plan);
 /* Restrict the next pass2 of a MultiSURF plan to the focal samples
  * [row_begin, row_end) (as fs_multisurf_score_rows; a new plan scores

@@ -9,7 +9,10 @@ BIT-IDENTICAL to the oracle's float32 arithmetic on
     one 1e7 outlier per column: MultiSURF*'s top-10 there is the reference's
     only when its float32 rounding is replayed);
   * the BASELINE configurations cfg2, cfg3 (2 and 3 classes) and cfg4 -- the
-    north star, 20000 x 20000 -- against the full-size oracle fixtures.
+    north star, 20000 x 20000 -- against the full-size oracle fixtures;
+  * SURF / SURF* in the reference's n_jobs=1 order (round 6, VERDICT r5
+    next #1): the same sweeps and verdict cases, row panels, rows slices,
+    ranks, TuRF, the cfg5 focal slices and the cfg5 whole fits.
 
 The oracle runs live for the small cases (oracle/_build, C, the box's host
 threads); the large ones use the committed fixtures with the sha256 of X.
@@ -74,6 +77,10 @@ def test_tail_sweep_bitexact(F, oracle, seed):
     assert_bitexact(
         fit_ref(F.ReliefF(backend="gpu", n_neighbors=k, accumulation="reference"), X, y),
         oracle.relieff_scores(X, y, n_neighbors=k))
+    for star in (False, True):
+        assert_bitexact(
+            fit_ref(F.SURF(backend="gpu", use_star=star, accumulation="reference"), X, y),
+            oracle.surf_scores(X, y, use_star=star))
 
 
 @pytest.mark.parametrize("seed", range(0, 40, 2))
@@ -89,6 +96,11 @@ def test_small_sweep_bitexact(F, oracle, seed):
             fit_ref(F.ReliefF(backend="gpu", n_neighbors=k, discrete_limit=dl,
                               accumulation="reference"), X, y),
             oracle.relieff_scores(X, y, n_neighbors=k, discrete_limit=dl))
+    for star in (False, True):
+        assert_bitexact(
+            fit_ref(F.SURF(backend="gpu", use_star=star, discrete_limit=dl,
+                           accumulation="reference"), X, y),
+            oracle.surf_scores(X, y, use_star=star, discrete_limit=dl))
 
 
 @pytest.mark.parametrize("kind", ["exp4z", "pareto1", "outlier"])
@@ -99,6 +111,55 @@ def test_verdict_cases_bitexact(F, oracle, kind):
         got = fit_ref(F.MultiSURF(backend="gpu", use_star=star, accumulation="reference"), X, y)
         assert_bitexact(got, ref)
         assert np.array_equal(np.argsort(got)[::-1][:10], np.argsort(ref)[::-1][:10])
+        ref = oracle.surf_scores(X, y, use_star=star)
+        got = fit_ref(F.SURF(backend="gpu", use_star=star, accumulation="reference"), X, y)
+        assert_bitexact(got, ref)
+        assert np.array_equal(np.argsort(got)[::-1][:10], np.argsort(ref)[::-1][:10])
+
+
+def test_surf_discrete_and_mixed_bitexact(F, oracle):
+    """SURF's discrete features add 1 / 0 to the chains (SURF.py:153-154):
+    discrete-only and mixed layouts, including a 128-feature block that
+    holds both kinds."""
+    rng = np.random.default_rng(17)
+    X = np.exp(1.5 * rng.standard_normal((700, 300)))
+    X[:, 100:140] = rng.integers(0, 4, (700, 40))
+    X[:, 250:] = rng.integers(0, 3, (700, 50))
+    y = rng.integers(0, 2, 700)
+    for star in (False, True):
+        assert_bitexact(
+            fit_ref(F.SURF(backend="gpu", use_star=star, accumulation="reference"), X, y),
+            oracle.surf_scores(X, y, use_star=star))
+    Xd = rng.integers(0, 5, (500, 130)).astype(np.float64)
+    for star in (False, True):
+        assert_bitexact(
+            fit_ref(F.SURF(backend="gpu", use_star=star, accumulation="reference"), Xd, y[:500]),
+            oracle.surf_scores(Xd, y[:500], use_star=star))
+
+
+def test_surf_panels_chain_the_column_sums(F, oracle, hooks):
+    """A one-shot SURF scored in row panels continues one float32 column sum
+    across the panels (each panel's plan seeded with the previous sums)."""
+    hooks("row_panel", 256)
+    X, y = verdict_case("exp4z", 1000, 90, seed=12)
+    for star in (False, True):
+        assert_bitexact(
+            fit_ref(F.SURF(backend="gpu", use_star=star, accumulation="reference"), X, y),
+            oracle.surf_scores(X, y, use_star=star))
+
+
+def test_surf_rows_slice_is_the_oracle_slice(F, oracle):
+    from fastselect_amd import _lib
+    from fastselect_amd.SURF import surf_inputs
+    X, y = verdict_case("outlier", 1500, 200, seed=5)
+    x = X.astype(np.float64)
+    isd, recip = surf_inputs(x, 10, "gpu")
+    for star in (False, True):
+        with _lib.accumulation("reference"):
+            sums = _lib.surf_score("gpu", x, y.astype(np.int32), recip, star, isd,
+                                   rows=(300, 1100))
+        assert_bitexact((sums / X.shape[0]).astype(np.float32),
+                        oracle.surf_scores(X, y, use_star=star, i_range=(300, 1100)))
 
 
 def test_relieff_panels_chain_the_column_sums(F, oracle, hooks):
@@ -183,7 +244,9 @@ def test_turf_resident_bitexact(F, oracle):
     cases = ((F.MultiSURF(backend="gpu", accumulation="reference"),
               lambda Z: oracle.multisurf_scores(Z, y)),
              (F.ReliefF(backend="gpu", n_neighbors=5, accumulation="reference"),
-              lambda Z: oracle.relieff_scores(Z, y, n_neighbors=5)))
+              lambda Z: oracle.relieff_scores(Z, y, n_neighbors=5)),
+             (F.SURFstar(backend="gpu", accumulation="reference"),
+              lambda Z: oracle.surf_scores(Z, y, use_star=True)))
     for base, score in cases:
         t = F.TuRF(base, n_features_to_select=12, pct_remove=0.3).fit(X, y)
         first, top = turf_oracle(score, X, 12, 0.3)
@@ -200,17 +263,38 @@ from test_gpu_baseline import _fixture, _inputs  # noqa: E402
     ("cfg3_relieff_k10", "relieff", {"n_neighbors": 10}),
     ("cfg3_relieff_k10_3class", "relieff", {"n_neighbors": 10}),
     ("cfg5_multisurfstar", "multisurf", {"use_star": True}),
+    ("cfg5_surf", "surf", {}),
+    ("cfg5_surfstar", "surf", {"use_star": True}),
     ("cfg4_multisurf", "multisurf", {}),
 ])
 def test_fullsize_bitexact(F, name, algo, kw):
     """The reference's scores bit for bit at the BASELINE sizes, cfg4 (the
-    north star, 20000 x 20000) included."""
+    north star, 20000 x 20000) and the cfg5 SURF / SURF* whole fits
+    (10000 x 50000, float64 X) included."""
     fx = _fixture(name)
     X, y = _inputs(fx)
-    cls = F.MultiSURF if algo == "multisurf" else F.ReliefF
+    cls = {"multisurf": F.MultiSURF, "relieff": F.ReliefF, "surf": F.SURF}[algo]
     est = cls(backend="gpu", accumulation="reference", n_features_to_select=10, **kw).fit(X, y)
     assert est.effective_backend_ == "gpu"
     assert_bitexact(est.feature_importances_, fx["scores"])
+
+
+@pytest.mark.parametrize("name", ["cfg5_surfstar_slice", "cfg5_surf_slice"])
+def test_cfg5_surf_slice_bitexact(F, name):
+    """The cfg5 SURF / SURF* focal slices (384 samples of 10000 x 50000)
+    through fs_surf_score_rows in reference order: the slice's float32
+    column sum, / n, bit for bit."""
+    from fastselect_amd import _lib
+    from fastselect_amd.SURF import surf_inputs
+    fx = _fixture(name)
+    X, y = _inputs(fx)
+    x = np.ascontiguousarray(X, dtype=np.float64)
+    isd, recip = surf_inputs(x, 10, "gpu")
+    lo, hi = (int(v) for v in fx["i_range"])
+    with _lib.accumulation("reference"):
+        sums = _lib.surf_score("gpu", x, np.asarray(y).astype(np.int32), recip,
+                               bool(fx["use_star"]), isd, rows=(lo, hi))
+    assert_bitexact((sums / x.shape[0]).astype(np.float32), fx["scores"])
 
 
 @pytest.mark.parametrize("name,fast_bound", [("cfg2_multisurf", 0), ("cfg4_multisurf", 40)])
@@ -287,6 +371,10 @@ def _relieff_rank_worker(rank, world, port, out_path):
     np.save(f"{out_path}.ms.{rank}.npy",
             parallel.multisurf_scores(X2, y2, use_star=True, backend="gpu", device=0,
                                       accumulation="reference"))
+    for star in (False, True):
+        np.save(f"{out_path}.sf{int(star)}.{rank}.npy",
+                parallel.surf_scores(X2, y2, use_star=star, backend="gpu", device=0,
+                                     accumulation="reference"))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -297,7 +385,8 @@ def test_relieff_ranks_chain_the_column_sums_bitexact(F, oracle, tmp_path, world
     sharing cuda:0, gloo): every rank's float32 temp rows at once
     (fs_plan_ref_temp), then the column sums passed rank to rank
     (fs_plan_ref_sums) -- the oracle's scores bit for bit on every rank; and
-    parallel.multisurf_scores(accumulation='reference') likewise."""
+    parallel.multisurf_scores / surf_scores(accumulation='reference')
+    likewise."""
     import torch.multiprocessing as mp
 
     from test_gpu_dist import _port
@@ -307,6 +396,9 @@ def test_relieff_ranks_chain_the_column_sums_bitexact(F, oracle, tmp_path, world
     ref = oracle.relieff_scores(X, y, n_neighbors=k)
     X2, y2 = verdict_case("exp4z", 1100, 150, seed=4)
     ref2 = oracle.multisurf_scores(X2, y2, use_star=True)
+    ref3 = [oracle.surf_scores(X2, y2, use_star=star) for star in (False, True)]
     for r in range(world):
         assert_bitexact(np.load(f"{out}.rf.{r}.npy"), ref)
         assert_bitexact(np.load(f"{out}.ms.{r}.npy"), ref2)
+        for star in (0, 1):
+            assert_bitexact(np.load(f"{out}.sf{star}.{r}.npy"), ref3[star])

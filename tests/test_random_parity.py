@@ -175,6 +175,10 @@ def run_tail_case(oracle, seed, backend):
         fit = SURF(backend=backend).fit(X, y).feature_importances_
         assert_parity_attributed(fit, oracle.surf_scores(X, y),
                                  oracle.surf_scores(X, y, accum="f64"), tol=TOL, k=5)
+        # the literal bar for SURF as well: its reference order (n_jobs=1)
+        # replays the reference's float32 sums, so the scores are the oracle's
+        ref = SURF(backend=backend, accumulation="reference").fit(X, y).feature_importances_
+        np.testing.assert_array_equal(ref, oracle.surf_scores(X, y))
         fit = ReliefF(backend=backend, n_neighbors=k).fit(X, y).feature_importances_
         assert_parity_attributed(fit, oracle.relieff_scores(X, y, n_neighbors=k),
                                  oracle.relieff_scores(X, y, n_neighbors=k, accum="f64"),

@@ -1,7 +1,8 @@
 """Reference-order accumulation (``accumulation='reference'``,
 fs_set_accumulation(FS_ACCUM_REFERENCE)) on the native CPU backend: the
 reference's float32 per-sample sums and float32 sequential column sums
-(MultiSURF.py:198-253, ReliefF.py:181-220), so the scores must equal the
+(MultiSURF.py:198-253, ReliefF.py:181-220; SURF / SURF* in the reference's
+n_jobs=1 order, SURF.py:139-218), so the scores must equal the
 oracle's (oracle/relief_oracle.c, the restatement of those lines) BIT FOR BIT
 -- including the inputs where the reference's own float32 error exceeds
 1e-5 of max |s| and the default mode can only be judged by the attributed
@@ -13,7 +14,7 @@ import warnings
 import numpy as np
 import pytest
 
-from fastselect_amd import SURF, MultiSURF, MultiSURFstar, ReliefF, TuRF, _lib
+from fastselect_amd import SURF, MultiSURF, MultiSURFstar, ReliefF, SURFstar, TuRF, _lib
 from test_random_parity import make_case, make_tail_case
 
 
@@ -61,6 +62,10 @@ def test_sweep_bitexact_cpu(oracle, seed):
     if X.shape[0] > k:
         assert_bitexact(fit_ref(ReliefF, X, y, backend="cpu", discrete_limit=dl, n_neighbors=k),
                         oracle.relieff_scores(X, y, n_neighbors=k, discrete_limit=dl))
+    assert_bitexact(fit_ref(SURF, X, y, backend="cpu", discrete_limit=dl),
+                    oracle.surf_scores(X, y, discrete_limit=dl))
+    assert_bitexact(fit_ref(SURFstar, X, y, backend="cpu", discrete_limit=dl),
+                    oracle.surf_scores(X, y, use_star=True, discrete_limit=dl))
 
 
 @pytest.mark.parametrize("seed", [0, 3, 7])
@@ -71,6 +76,9 @@ def test_tail_bitexact_cpu(oracle, seed):
                     oracle.multisurf_scores(X, y, use_star=True))
     assert_bitexact(fit_ref(ReliefF, X, y, backend="cpu", n_neighbors=k),
                     oracle.relieff_scores(X, y, n_neighbors=k))
+    for star in (False, True):
+        assert_bitexact(fit_ref(SURF, X, y, backend="cpu", use_star=star),
+                        oracle.surf_scores(X, y, use_star=star))
 
 
 @pytest.mark.parametrize("kind", ["exp4z", "pareto1", "outlier"])
@@ -79,6 +87,10 @@ def test_verdict_cases_bitexact_cpu(oracle, kind):
     for star in (False, True):
         ref = oracle.multisurf_scores(X, y, use_star=star)
         got = fit_ref(MultiSURF, X, y, backend="cpu", use_star=star)
+        assert_bitexact(got, ref)
+        assert np.array_equal(np.argsort(got)[::-1][:10], np.argsort(ref)[::-1][:10])
+        ref = oracle.surf_scores(X, y, use_star=star)
+        got = fit_ref(SURF, X, y, backend="cpu", use_star=star)
         assert_bitexact(got, ref)
         assert np.array_equal(np.argsort(got)[::-1][:10], np.argsort(ref)[::-1][:10])
 
@@ -103,6 +115,38 @@ def test_rows_slice_is_the_oracle_slice_cpu(oracle):
         sums = _lib.multisurf_score("cpu", x, yv, recip, None, False, isd, rows=(128, 384))
     ref = oracle.multisurf_scores(X, y, i_range=(128, 384))
     assert_bitexact((sums / X.shape[0]).astype(np.float32), ref)
+
+
+def test_surf_rows_slice_and_ex_call_cpu(oracle):
+    """fs_surf_score_rows in reference order is the float32 column sum of the
+    slice's rows (the oracle restricted to i_range); fs_surf_score_ex takes
+    the mode as an argument and leaves the thread's mode alone."""
+    import ctypes
+    X, y = verdict_case("pareto1", 400, 70, seed=3)
+    x = X.astype(np.float64)
+    rng = x.max(0) - x.min(0)                                  # SURF.py:352-355
+    rng[rng == 0] = 1.0
+    recip = (1.0 / rng).astype(np.float32)
+    isd = np.zeros(x.shape[1], np.uint8)
+    yi = y.astype(np.int32)
+    for star in (False, True):
+        with _lib.accumulation("reference"):
+            sums = _lib.surf_score("cpu", x, yi, recip, star, isd, rows=(128, 300))
+        assert_bitexact((sums / X.shape[0]).astype(np.float32),
+                        oracle.surf_scores(X, y, use_star=star, i_range=(128, 300)))
+        out = np.zeros(x.shape[1], np.float32)
+        L = _lib.lib()
+        f32p = ctypes.POINTER(ctypes.c_float)
+        _lib.check(L.fs_surf_score_ex(0, 0, x.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                      x.shape[0], x.shape[1],
+                                      yi.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                      recip.ctypes.data_as(f32p), int(star),
+                                      isd.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), -1, 1,
+                                      out.ctypes.data_as(f32p)))
+        assert L.fs_get_accumulation() == 0
+        assert_bitexact(out, oracle.surf_scores(X, y, use_star=star))
+    with pytest.raises(ValueError, match="accumulation"):
+        _lib.check(L.fs_surf_score_ex(0, 0, None, 0, 0, None, None, 0, None, -1, 7, None))
 
 
 def _recip_disc(X):
@@ -131,7 +175,9 @@ def test_turf_reference_mode_cpu(oracle):
     cases = ((MultiSURF(backend="cpu", accumulation="reference"),
               lambda Z: oracle.multisurf_scores(Z, y)),
              (ReliefF(backend="cpu", n_neighbors=5, accumulation="reference"),
-              lambda Z: oracle.relieff_scores(Z, y, n_neighbors=5)))
+              lambda Z: oracle.relieff_scores(Z, y, n_neighbors=5)),
+             (SURFstar(backend="cpu", accumulation="reference"),
+              lambda Z: oracle.surf_scores(Z, y, use_star=True)))
     for base, score in cases:
         t = TuRF(base, n_features_to_select=10, pct_remove=0.25).fit(X, y)
         first, top = turf_oracle(score, X, 10, 0.25)
@@ -160,10 +206,8 @@ def test_accumulation_errors():
         MultiSURF(backend="cpu", accumulation="f16").fit(X, y)
     with pytest.raises(ValueError, match="accumulation"):
         ReliefF(backend="cpu", accumulation=None).fit(X, y)
-    # SURF has no fixed reference order (per-thread rows, SURF.py:195, 216)
-    with _lib.accumulation("reference"):
-        with pytest.raises(RuntimeError, match="SURF"):
-            SURF(backend="cpu").fit(X, y)
+    with pytest.raises(ValueError, match="accumulation"):
+        SURF(backend="cpu", accumulation="exact").fit(X, y)
     # the mode is per thread and restored by the context manager
     assert _lib.lib().fs_get_accumulation() == 0
     with _lib.accumulation("reference"):
