@@ -704,6 +704,42 @@ static void relieff_select_row(const Prepared& P, const float* x, const std::vec
   (void)li;
 }
 
+// Reference order of ReliefF's neighbour lists (nbr[c], ascending keys
+// nkey[c]): every run of equal keys re-ordered as numba's quicksort argsort
+// of row i's exact keys orders those samples (numba_argsort_focus, focused on
+// them: the relative order of the focus samples is numba's exactly).
+static void ref_tie_order(const Prepared& P, const float* X, int64_t i,
+                          const std::vector<std::vector<float>>& nkey,
+                          std::vector<std::vector<int32_t>>& nbr) {
+  const int64_t n = P.n;
+  std::vector<float> key((size_t)n);
+  for (int64_t j = 0; j < n; j++) key[j] = j == i ? INFINITY : relieff_exact_key(P, X, i, j);
+  std::vector<uint8_t> focus((size_t)n, 0);
+  for (size_t c = 0; c < nbr.size(); c++)
+    for (size_t t = 1; t < nbr[c].size(); t++)
+      if (nkey[c][t] == nkey[c][t - 1]) focus[nbr[c][t]] = focus[nbr[c][t - 1]] = 1;
+  std::vector<int32_t> R((size_t)n);
+  for (int64_t j = 0; j < n; j++) R[j] = (int32_t)j;
+  numba_argsort_focus(n, R.data(), [&](int32_t j) { return key[j]; },
+                      [&](int64_t lo, int64_t hi) {
+                        for (int64_t t = lo; t <= hi; t++)
+                          if (focus[R[t]]) return true;
+                        return false;
+                      });
+  std::vector<int64_t> pos((size_t)n, 0);
+  for (int64_t t = 0; t < n; t++) pos[R[t]] = t;
+  for (size_t c = 0; c < nbr.size(); c++) {
+    std::vector<int32_t>& L = nbr[c];
+    for (size_t s = 0; s < L.size();) {
+      size_t e = s + 1;
+      while (e < L.size() && nkey[c][e] == nkey[c][s]) e++;
+      std::sort(L.begin() + s, L.begin() + e,
+                [&](int32_t a, int32_t b) { return pos[a] < pos[b]; });
+      s = e;
+    }
+  }
+}
+
 int relieff_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int64_t r_hi,
                 double* scores) {
   std::vector<uint32_t> xq;
@@ -726,12 +762,25 @@ int relieff_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int6
       const int64_t i = r_lo + r;
       std::vector<std::vector<int32_t>> nbr(C);
       relieff_select_row(P, X, D, i, amb, nbr);
+      std::vector<std::vector<float>> nkey(C);
+      bool dup = false;
       for (int c = 0; c < C; c++) {
         std::vector<std::pair<float, int32_t>> kv;
         for (int32_t j : nbr[c]) kv.push_back({relieff_exact_key(P, X, i, j), j});
         std::sort(kv.begin(), kv.end());
-        for (size_t t = 0; t < kv.size(); t++) nbr[c][t] = kv[t].second;
+        for (size_t t = 0; t < kv.size(); t++) {
+          nbr[c][t] = kv[t].second;
+          nkey[c].push_back(kv[t].first);
+          dup = dup || (t > 0 && kv[t].first == kv[t - 1].first);
+        }
       }
+      // Neighbours of one list at the same key: the reference takes them in
+      // numba's quicksort order of the whole row (ReliefF.py:157-175), which
+      // decides the order of its float64 sums below (ReliefF.py:181-207).
+      // With continuous features that order can change a sum's rounding, so
+      // replay the quicksort over the row's exact keys (as k_rf_ref_ties
+      // does); 0 / 1 diffs of an all-discrete layout add exactly in any order.
+      if (dup && P.pc > 0) ref_tie_order(P, X, i, nkey, nbr);
       const int32_t li = P.labels[i];
       double denom = 1.0 - P.class_prior[li];
       if (denom == 0.0) denom = 1.0;

@@ -572,13 +572,22 @@ int multisurf_chains(const float* xk, int64_t Kp, const float* krecip, const uin
 // (float) init[k] when init is not null; init may alias out), as a double.
 int column_sums(const float* temp, int64_t rows, int64_t Kp, int64_t n_kept, const double* init,
                 double* out, void* stream);
-// ReliefF: each (row, class) neighbour list put in argsort order (exact
-// keys; keys[(rows) * C * k] scratch), then temp[i - r_lo][k] = f32(update)
+// ReliefF: each (row, class) neighbour list in ascending exact key, equal
+// keys by sample index (keys[rows * C * k]: the sorted keys), dup[rows * C] =
+// 1 where a list holds equal keys (k_rf_ref_ties then orders those runs as
+// numba's quicksort does).
+int relieff_order(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
+                  int64_t n_kept, int C, int64_t k, int32_t* nbr, const int32_t* nfound,
+                  int64_t r_lo, int64_t r_hi, float* keys, int32_t* dup, void* stream);
+// keys[r][j] = the reference's key of (rows[r], j), +inf at j = rows[r].
+int relieff_row_keys(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
+                     int64_t n_kept, const int32_t* rows, int64_t nr, int64_t n, float* keys,
+                     void* stream);
+// temp[i - r_lo][k] = f32(update) over the lists in their order
 // (ReliefF.py:177-216).
-int relieff_rows(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
-                 int64_t n_kept, const int32_t* lab, const double* prior, int C, int64_t k,
-                 int32_t* nbr, const int32_t* nfound, int64_t r_lo, int64_t r_hi, float* keys,
-                 float* temp, void* stream);
+int relieff_update(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
+                   const int32_t* lab, const double* prior, int C, int64_t k, const int32_t* nbr,
+                   const int32_t* nfound, int64_t r_lo, int64_t r_hi, float* temp, void* stream);
 }  // namespace refacc
 }  // namespace gpu
 

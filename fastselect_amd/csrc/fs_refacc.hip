@@ -451,10 +451,24 @@ __global__ __launch_bounds__(64) void k_ref_colsum(const float* __restrict__ tem
 }
 
 // ---- ReliefF ---------------------------------------------------------------------
-// The reference's float32 key of neighbour entry e = ((i - r_lo) C + c) k + t
-// (t < nfound[i][c]): float32 diffs summed in float64 in feature order,
-// rounded to float32 (ReliefF.py:149-155).  One lane per entry, each summing
-// its own two rows sequentially.
+// The reference's float32 key of (i, j): float32 diffs summed in float64 in
+// kept-feature order, rounded to float32 (ReliefF.py:149-155).
+__device__ __forceinline__ float rf_ref_key(const float* __restrict__ xi,
+                                            const float* __restrict__ xj,
+                                            const float* __restrict__ krecip,
+                                            const uint8_t* __restrict__ kdisc, int64_t n_kept) {
+  double d = 0.0;
+  for (int64_t f = 0; f < n_kept; f++) {
+    if (kdisc[f])
+      d += xi[f] != xj[f] ? 1.0 : 0.0;
+    else
+      d += (double)(__builtin_fabsf(xi[f] - xj[f]) * krecip[f]);
+  }
+  return (float)d;
+}
+
+// The key of neighbour entry e = ((i - r_lo) C + c) k + t (t < nfound[i][c]).
+// One lane per entry, each summing its own two rows sequentially.
 __global__ __launch_bounds__(256) void k_rf_ref_keys(
     const float* __restrict__ xk, int64_t Kp, const float* __restrict__ krecip,
     const uint8_t* __restrict__ kdisc, int64_t n_kept, const int32_t* __restrict__ nbr,
@@ -467,26 +481,32 @@ __global__ __launch_bounds__(256) void k_rf_ref_keys(
   const int64_t i = r_lo + ic / C, c = ic % C;
   if (t >= nfound[i * C + c]) return;
   const int64_t j = nbr[(i * C + c) * k + t];
-  const float* xi = xk + i * Kp;
-  const float* xj = xk + j * Kp;
-  double d = 0.0;
-  for (int64_t f = 0; f < n_kept; f++) {
-    if (kdisc[f])
-      d += xi[f] != xj[f] ? 1.0 : 0.0;
-    else
-      d += (double)(__builtin_fabsf(xi[f] - xj[f]) * krecip[f]);
-  }
-  keys[e] = (float)d;
+  keys[e] = rf_ref_key(xk + i * Kp, xk + j * Kp, krecip, kdisc, n_kept);
 }
 
-// Each (i, c) list in argsort order: ascending key (equal keys by sample
-// index; numba's quicksort would order them by its pivots, which changes a
-// float64 sum of <= k float32 diffs only if both a key tie and a diff below
-// ~2^-22 of the sum occur).  Insertion sort, one thread per list.
+// Every key of the rows rows[r] (j = i: +inf, the reference's dists[i]),
+// for the tie rows' quicksort replay (k_rf_ref_ties).  Grid (rows,
+// ceil(n / 256)), one lane per sample j.
+__global__ __launch_bounds__(256) void k_rf_ref_rowkeys(
+    const float* __restrict__ xk, int64_t Kp, const float* __restrict__ krecip,
+    const uint8_t* __restrict__ kdisc, int64_t n_kept, const int32_t* __restrict__ rows,
+    int64_t n, float* __restrict__ keys) {
+  const int64_t r = blockIdx.x, i = rows[r];
+  const int64_t j = (int64_t)blockIdx.y * 256 + threadIdx.x;
+  if (j >= n) return;
+  keys[r * n + j] =
+      j == i ? __builtin_inff() : rf_ref_key(xk + i * Kp, xk + j * Kp, krecip, kdisc, n_kept);
+}
+
+// Each (i, c) list in ascending key order, equal keys by sample index (the
+// reference's argsort order up to ties: k_rf_ref_ties then re-orders each
+// run of equal keys as numba's quicksort does, ReliefF.py:157).  Insertion
+// sort, one thread per list; dup[list] = 1 when the list holds a run.
 __global__ __launch_bounds__(256) void k_rf_ref_sort(int32_t* __restrict__ nbr,
                                                      const int32_t* __restrict__ nfound,
                                                      float* __restrict__ keys, int64_t r_lo,
-                                                     int64_t r_hi, int C, int64_t k) {
+                                                     int64_t r_hi, int C, int64_t k,
+                                                     int32_t* __restrict__ dup) {
   const int64_t ic = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (ic >= (r_hi - r_lo) * C) return;
   const int64_t i = r_lo + ic / C, c = ic % C;
@@ -505,6 +525,9 @@ __global__ __launch_bounds__(256) void k_rf_ref_sort(int32_t* __restrict__ nbr,
     K[q] = kv;
     L[q] = jv;
   }
+  int32_t d = 0;
+  for (int64_t s = 1; s < m; s++) d |= K[s] == K[s - 1] ? 1 : 0;
+  dup[ic] = d;
 }
 
 // temp[i - r_lo][f] = f32(update) (ReliefF.py:177-216): hit_sum and each miss
@@ -851,24 +874,38 @@ int column_sums(const float* temp, int64_t rows, int64_t Kp, int64_t n_kept, con
   return check("k_ref_colsum");
 }
 
-int relieff_rows(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
-                 int64_t n_kept, const int32_t* lab, const double* prior, int C, int64_t k,
-                 int32_t* nbr, const int32_t* nfound, int64_t r_lo, int64_t r_hi, float* keys,
-                 float* temp, void* stream) {
-  if (r_hi <= r_lo) return FS_OK;
+int relieff_order(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
+                  int64_t n_kept, int C, int64_t k, int32_t* nbr, const int32_t* nfound,
+                  int64_t r_lo, int64_t r_hi, float* keys, int32_t* dup, void* stream) {
+  if (r_hi <= r_lo || k <= 0) return FS_OK;
   const hipStream_t s = (hipStream_t)stream;
   const int64_t lists = (r_hi - r_lo) * C;
-  if (k > 0) {
-    k_rf_ref_keys<<<(unsigned)((lists * k + 255) / 256), 256, 0, s>>>(
-        xk, Kp, krecip, kdisc, n_kept, nbr, nfound, r_lo, r_hi, C, k, keys);
-    int rc = check("k_rf_ref_keys");
-    if (rc != FS_OK) return rc;
-    k_rf_ref_sort<<<(unsigned)((lists + 255) / 256), 256, 0, s>>>(nbr, nfound, keys, r_lo, r_hi,
-                                                                  C, k);
-    if ((rc = check("k_rf_ref_sort")) != FS_OK) return rc;
-  }
-  k_rf_ref_update<<<dim3((unsigned)(Kp / 64), (unsigned)((r_hi - r_lo + 63) / 64)), 256, 0, s>>>(
-      xk, Kp, krecip, kdisc, lab, prior, C, k, nbr, nfound, r_lo, r_hi, temp);
+  k_rf_ref_keys<<<(unsigned)((lists * k + 255) / 256), 256, 0, s>>>(
+      xk, Kp, krecip, kdisc, n_kept, nbr, nfound, r_lo, r_hi, C, k, keys);
+  const int rc = check("k_rf_ref_keys");
+  if (rc != FS_OK) return rc;
+  k_rf_ref_sort<<<(unsigned)((lists + 255) / 256), 256, 0, s>>>(nbr, nfound, keys, r_lo, r_hi, C,
+                                                                k, dup);
+  return check("k_rf_ref_sort");
+}
+
+int relieff_row_keys(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
+                     int64_t n_kept, const int32_t* rows, int64_t nr, int64_t n, float* keys,
+                     void* stream) {
+  if (nr <= 0) return FS_OK;
+  k_rf_ref_rowkeys<<<dim3((unsigned)nr, (unsigned)((n + 255) / 256)), 256, 0,
+                     (hipStream_t)stream>>>(xk, Kp, krecip, kdisc, n_kept, rows, n, keys);
+  return check("k_rf_ref_rowkeys");
+}
+
+int relieff_update(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
+                   const int32_t* lab, const double* prior, int C, int64_t k, const int32_t* nbr,
+                   const int32_t* nfound, int64_t r_lo, int64_t r_hi, float* temp,
+                   void* stream) {
+  if (r_hi <= r_lo) return FS_OK;
+  k_rf_ref_update<<<dim3((unsigned)(Kp / 64), (unsigned)((r_hi - r_lo + 63) / 64)), 256, 0,
+                    (hipStream_t)stream>>>(xk, Kp, krecip, kdisc, lab, prior, C, k, nbr, nfound,
+                                           r_lo, r_hi, temp);
   return check("k_rf_ref_update");
 }
 

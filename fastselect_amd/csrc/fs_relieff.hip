@@ -1363,6 +1363,102 @@ __global__ __launch_bounds__(64) void k_rf_ties(const int32_t* __restrict__ rows
   }
 }
 
+// Reference order (fs_refacc.hip): runs of equal keys inside a row's
+// neighbour lists (sorted by key, then index) put in numba's quicksort order
+// (ReliefF.py:157-175 scans the argsort, so its float64 hit / miss sums of
+// ReliefF.py:181-207 add tied neighbours in that order).  One wave per row:
+// every sample of a run is a focus sample (R's sign bit), wave_argsort_focus
+// replays numba's quicksort over the row's exact keys (keys_all, +inf at i),
+// the focus samples are collected in their sorted order (ord, per-row
+// scratch of C k), and lane 0 re-orders each run by that order.  IN_LDS:
+// the keys and R in LDS (8 bytes per sample), else in the global scratch.
+template <bool IN_LDS>
+__global__ __launch_bounds__(64) void k_rf_ref_ties(
+    const int32_t* __restrict__ rows, int64_t n, const float* __restrict__ keys_all, int C,
+    int64_t k, int64_t r_lo, int32_t* __restrict__ nbr, const int32_t* __restrict__ nfound,
+    const float* __restrict__ lkeys, int32_t* __restrict__ R_all, int32_t* __restrict__ ord_all,
+    int* __restrict__ status) {
+  extern __shared__ uint32_t tie_lds[];
+  __shared__ int sort_rc;
+  const int lane = threadIdx.x;
+  const int64_t r = blockIdx.x;
+  const int64_t i = rows[r];
+  const float* key = keys_all + r * n;
+  int32_t* R = R_all + r * n;
+  int32_t* ord = ord_all + r * C * k;
+  if (IN_LDS) {
+    float* kl = (float*)tie_lds;
+    for (int64_t j = lane; j < n; j += 64) kl[j] = key[j];
+    key = kl;
+    R = (int32_t*)(tie_lds + n);
+  }
+  for (int64_t j = lane; j < n; j += 64) R[j] = (int32_t)j;
+  __syncthreads();
+  // focus samples: the members of a run of equal keys in one list (each
+  // sample is in one class's list at most once, so the lanes' stores are to
+  // distinct samples)
+  for (int64_t e = lane; e < (int64_t)C * k; e += 64) {
+    const int64_t c = e / k, t = e % k;
+    const int64_t m = nfound[i * C + c];
+    if (t >= m) continue;
+    const float* K = lkeys + ((i - r_lo) * C + c) * k;
+    if ((t > 0 && K[t] == K[t - 1]) || (t + 1 < m && K[t + 1] == K[t])) {
+      const int32_t j = nbr[(i * C + c) * k + t];
+      R[j] = (int32_t)((uint32_t)j | 0x80000000u);
+    }
+  }
+  __syncthreads();
+  {
+    __shared__ int32_t bufL[64], bufR[64];
+    const int rc = wave_argsort_focus(
+        n, R, [&](int32_t h) { return key[h & 0x7FFFFFFF]; }, bufL, bufR);
+    if (lane == 0) sort_rc = rc;
+  }
+  __syncthreads();
+  if (sort_rc != 0) {
+    if (lane == 0) atomicExch(status, 1);
+    return;
+  }
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int64_t cnt = 0;
+  for (int64_t t0 = 0; t0 < n; t0 += 64) {
+    const int64_t t = t0 + lane;
+    const int32_t h = t < n ? R[t] : 0;
+    const uint64_t m = __ballot(h < 0);
+    if (h < 0) ord[cnt + __popcll(m & below)] = h & 0x7FFFFFFF;
+    cnt += __popcll(m);
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (lane != 0) return;
+  for (int c = 0; c < C; c++) {
+    const int64_t m = nfound[i * C + c];
+    int32_t* L = nbr + (i * C + c) * k;
+    const float* K = lkeys + ((i - r_lo) * C + c) * k;
+    for (int64_t s = 0; s < m;) {
+      int64_t e = s + 1;
+      while (e < m && K[e] == K[s]) e++;
+      // insertion sort of L[s, e) by rank in ord
+      auto rank = [&](int32_t j) {
+        int64_t q = 0;
+        while (q < cnt && ord[q] != j) q++;
+        return q;
+      };
+      for (int64_t a = s + 1; a < e; a++) {
+        const int32_t v = L[a];
+        const int64_t rv = rank(v);
+        int64_t b = a;
+        while (b > s && rank(L[b - 1]) > rv) {
+          L[b] = L[b - 1];
+          b--;
+        }
+        L[b] = v;
+      }
+      s = e;
+    }
+  }
+}
+
 // acc_f(i) = -sum_hits d / h_found + sum_{c != y_i} (P_c / (1 - P_yi)) sum_misses_c d / k
 // (ReliefF.py:177-216) for the focal rows [r_lo, r_hi).  Grid (PW/64, row
 // blocks of kRfRows); 4 waves per workgroup, wave w handles rows w, w+4, ...
@@ -1572,6 +1668,75 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
   return FS_OK;
 }
 
+// Reference order: the rows whose neighbour lists hold runs of equal keys
+// (dup, from relieff_order) get those runs in numba's quicksort order
+// (k_rf_ref_ties over the row's exact keys).  Continuous data has a few such
+// rows (cfg3: none to a handful); integer-valued layouts many, but an
+// all-discrete layout's 0 / 1 diffs add exactly in any order, so the caller
+// skips it (pc == 0).
+static int relieff_ref_ties(Plan* g, int32_t* nbr, const int32_t* nfound, const int32_t* dup) {
+  const Prepared& Q = g->P;
+  const int C = Q.n_classes;
+  const int64_t k = Q.k_neighbors, n = Q.n, rows = g->r_hi - g->r_lo;
+  std::vector<int32_t> h((size_t)rows * C);
+  FS_HIP(hipMemcpyAsync(h.data(), dup, h.size() * sizeof(int32_t), hipMemcpyDeviceToHost,
+                        g->stream));
+  FS_HIP(hipStreamSynchronize(g->stream));
+  std::vector<int32_t> tie_rows;
+  for (int64_t r = 0; r < rows; r++)
+    for (int c = 0; c < C; c++)
+      if (h[r * C + c]) {
+        tie_rows.push_back((int32_t)(g->r_lo + r));
+        break;
+      }
+  if (trace_on())
+    std::fprintf(stderr, "[fs_trace] relieff reference order: %zu rows with tied keys\n",
+                 tie_rows.size());
+  if (tie_rows.empty()) return FS_OK;
+  const int64_t row_bytes = 8 * n + 4 * (int64_t)C * k;
+  const int64_t batch = std::max<int64_t>(
+      1, std::min<int64_t>((int64_t)tie_rows.size(), (int64_t)(512ll << 20) / row_bytes));
+  int32_t *drows = nullptr, *R = nullptr, *ord = nullptr;
+  float* keys = nullptr;
+  int* status = nullptr;
+  g->alloc_target = 2;
+  int rc;
+  if ((rc = dalloc(g, &drows, (size_t)batch)) || (rc = dalloc(g, &R, (size_t)(batch * n))) ||
+      (rc = dalloc(g, &keys, (size_t)(batch * n))) ||
+      (rc = dalloc(g, &ord, (size_t)(batch * C * k))) || (rc = dalloc(g, &status, 1))) {
+    g->alloc_target = 0;
+    return rc;
+  }
+  g->alloc_target = 0;
+  FS_HIP(hipMemsetAsync(status, 0, sizeof(int), g->stream));
+  // keys and R in LDS (8 B per sample) beside ~2.2 KB of static LDS
+  const bool in_lds = 8 * n + 2304 <= 160 * 1024;
+  if (in_lds)
+    FS_HIP(hipFuncSetAttribute((const void*)k_rf_ref_ties<true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(8 * n)));
+  for (int64_t r0 = 0; r0 < (int64_t)tie_rows.size(); r0 += batch) {
+    const int64_t nr = std::min<int64_t>(batch, (int64_t)tie_rows.size() - r0);
+    FS_TRY(h2d(g, drows, tie_rows.data() + r0, (size_t)nr));
+    FS_TRY(refacc::relieff_row_keys(g->xk, g->Kp, g->krecip, g->kdisc, Q.n_kept, drows, nr, n,
+                                    keys, g->stream));
+    if (in_lds)
+      k_rf_ref_ties<true><<<(unsigned)nr, 64, (size_t)(8 * n), g->stream>>>(
+          drows, n, keys, C, k, g->r_lo, nbr, nfound, g->rkeys, R, ord, status);
+    else
+      k_rf_ref_ties<false><<<(unsigned)nr, 64, 0, g->stream>>>(drows, n, keys, C, k, g->r_lo, nbr,
+                                                              nfound, g->rkeys, R, ord, status);
+    FS_TRY(launch_check("k_rf_ref_ties"));
+  }
+  int hstatus = 0;
+  FS_HIP(hipMemcpyAsync(&hstatus, status, sizeof(int), hipMemcpyDeviceToHost, g->stream));
+  FS_HIP(hipStreamSynchronize(g->stream));
+  if (hstatus != 0) {
+    set_error("ReliefF reference order: quicksort stack overflow");
+    return FS_EHIP;
+  }
+  return FS_OK;
+}
+
 // ReliefF score sums of the plan's focal rows into sums_dev[n_kept]:
 // pass 1, neighbour selection, then the neighbour-gather update.
 int plan_score_relieff(Plan* g, double* sums_dev) {
@@ -1620,8 +1785,16 @@ int plan_score_relieff(Plan* g, double* sums_dev) {
     }
     float* temp = nullptr;
     FS_TRY(ref_temp(g, rows, &temp));
-    FS_TRY(refacc::relieff_rows(g->xk, g->Kp, g->krecip, g->kdisc, Q.n_kept, g->lab, dprior, C, k,
-                                nbr, nfound, g->r_lo, g->r_hi, g->rkeys, temp, g->stream));
+    int32_t* dup = nullptr;
+    g->alloc_target = 2;
+    rc = dalloc(g, &dup, (size_t)std::max<int64_t>(rows * C, 1));
+    g->alloc_target = 0;
+    FS_TRY(rc);
+    FS_TRY(refacc::relieff_order(g->xk, g->Kp, g->krecip, g->kdisc, Q.n_kept, C, k, nbr, nfound,
+                                 g->r_lo, g->r_hi, g->rkeys, dup, g->stream));
+    if (rows > 0 && k > 1 && Q.pc > 0) FS_TRY(relieff_ref_ties(g, nbr, nfound, dup));
+    FS_TRY(refacc::relieff_update(g->xk, g->Kp, g->krecip, g->kdisc, g->lab, dprior, C, k, nbr,
+                                  nfound, g->r_lo, g->r_hi, temp, g->stream));
     FS_HIP(hipEventRecord(g->ev[3], g->stream));
     if (g->ref_defer) {  // fs_plan_ref_temp: the column sums come later (plan_ref_sums)
       g->ref_rows = std::max<int64_t>(rows, 0);

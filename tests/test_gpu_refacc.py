@@ -162,6 +162,25 @@ def test_surf_rows_slice_is_the_oracle_slice(F, oracle):
                         oracle.surf_scores(X, y, use_star=star, i_range=(300, 1100)))
 
 
+def test_relieff_tied_neighbours_in_quicksort_order(F, oracle):
+    """Neighbours at one key summed in numba's quicksort order
+    (k_rf_ref_ties; VERDICT r5 missing #3): the crafted rows whose float32
+    update depends on that order (tests/test_refacc.py tie_order_case; the
+    index order misses 10 of these 40), then a whole fit."""
+    from test_refacc import relieff_row, tie_order_case
+    for seed in range(40):
+        X, y, i = tie_order_case(seed)
+        assert_bitexact(relieff_row("gpu", X, y, i),
+                        oracle.relieff_scores(X, y, n_neighbors=3, discrete_limit=2,
+                                              i_range=(i, i + 1)))
+    for seed in (1, 12):
+        X, y, _ = tie_order_case(seed, n_fill=3000)
+        assert_bitexact(
+            fit_ref(F.ReliefF(backend="gpu", n_neighbors=3, discrete_limit=2,
+                              accumulation="reference"), X, y),
+            oracle.relieff_scores(X, y, n_neighbors=3, discrete_limit=2))
+
+
 def test_relieff_panels_chain_the_column_sums(F, oracle, hooks):
     """A one-shot ReliefF scored in row panels (the row_panel test hook
     forces their height) continues one float32 column sum across the panels."""

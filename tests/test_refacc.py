@@ -95,6 +95,53 @@ def test_verdict_cases_bitexact_cpu(oracle, kind):
         assert np.array_equal(np.argsort(got)[::-1][:10], np.argsort(ref)[::-1][:10])
 
 
+def tie_order_case(seed, n_fill=60):
+    """A focal sample whose three nearest hits share one key exactly (the
+    grid column) while one feature's diffs to them are 1, 2^-53, 2^-53:
+    summed in float64 as 1 + e + e they give 1, as e + e + 1 they give
+    1 + 2^-52, and the three misses sum to 1 -- so the focal row's float32
+    update is 0 or -2^-52 / 3 depending on the ORDER of the tied hits, which
+    the reference takes from numba's quicksort of the whole row
+    (ReliefF.py:157-207).  Far filler samples of both classes vary that
+    quicksort's path.  Returns X, y and the focal row (score it alone through
+    a one-row slice: the column sum of one row is its update)."""
+    eps = 2.0 ** -53
+    rng = np.random.default_rng(seed)
+    rows = [(0.0, 0.0, 0), (0.0, 1.0, 0), (1.0, eps, 0), (1.0, eps, 0),
+            (0.0, 1.0, 1), (0.25, 0.0, 1), (0.25, 0.0, 1)]
+    rows += [(rng.uniform(0.5, 1.0), 0.5 + eps * rng.integers(2, 40), int(rng.integers(0, 2)))
+             for _ in range(n_fill)]
+    perm = rng.permutation(len(rows))
+    X = np.array([rows[q][:2] for q in perm])
+    y = np.array([rows[q][2] for q in perm])
+    return X, y, int(np.flatnonzero(perm == 0)[0])
+
+
+def relieff_row(backend, X, y, i, k=3, dl=2):
+    """ReliefF reference-order score of focal row i alone (its float32
+    update, / n)."""
+    from fastselect_amd.ReliefF import relieff_inputs
+    x32, y_enc, recip, isd, cp = relieff_inputs(X, y, dl, backend)
+    with _lib.accumulation("reference"):
+        s = _lib.relieff_score(backend, x32, y_enc, recip, isd, k, cp, rows=(i, i + 1))
+    return (s / X.shape[0]).astype(np.float32)
+
+
+def test_relieff_tied_neighbours_in_quicksort_order_cpu(oracle):
+    """VERDICT r5 missing #3: neighbours at one key in numba's quicksort
+    order, not index order.  Of these 40 seeds, the index order gives a
+    different float32 update than the reference on 10 (measured before the
+    replay was built); every one must now be the oracle's bit for bit."""
+    for seed in range(40):
+        X, y, i = tie_order_case(seed)
+        assert_bitexact(relieff_row("cpu", X, y, i),
+                        oracle.relieff_scores(X, y, n_neighbors=3, discrete_limit=2,
+                                              i_range=(i, i + 1)))
+    X, y, _ = tie_order_case(1)
+    assert_bitexact(fit_ref(ReliefF, X, y, backend="cpu", n_neighbors=3, discrete_limit=2),
+                    oracle.relieff_scores(X, y, n_neighbors=3, discrete_limit=2))
+
+
 def test_relieff_classes_and_small_class_cpu(oracle):
     rng = np.random.default_rng(3)
     X = np.exp(2.0 * rng.standard_normal((400, 60)))
