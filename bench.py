@@ -535,6 +535,7 @@ def main():
     import torch
     import torch.distributed as dist
 
+    from fastselect_amd import _lib
     from fastselect_amd.parallel import ShardedMultiSURF, resident_x
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -679,11 +680,11 @@ def main():
             "hbm_peak_GBps": HBM_PEAK_GBPS,
         }
     job.close()
-    # the decision-finer 32-bit pass 1 (FS_Q16=0) beside the default step
-    # (VERDICT r2 next #6): same job, 32-bit operands forced
+    # the decision-finer 32-bit pass 1 beside the default step (VERDICT r2
+    # next #6): same job, 32-bit operands forced by the q16 test hook
     q32 = None
     if on_gpu and world == 1 and not args.no_q32 and not ref_mode:
-        os.environ["FS_Q16"] = "0"
+        _lib.set_test_hook("q16", 0)
         try:
             with resident_x(x, args.backend, local):
                 job32 = ShardedMultiSURF(x, y, recip, is_disc, use_star=args.star,
@@ -700,7 +701,7 @@ def main():
                    "steps": ks}
             job32.close()
         finally:
-            del os.environ["FS_Q16"]
+            _lib.set_test_hook("reset")
     # the reference-order step beside the default (its
     # cost at cfg2 / cfg4): same job, accumulation='reference'
     refacc = None

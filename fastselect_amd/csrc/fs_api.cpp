@@ -133,6 +133,9 @@ int fs_test_hook(const char* name, int64_t value) {
   const std::string k(name);
   if (k == "reset") h = TestHooks();
   else if (k == "ksplit") h.ksplit = value;
+  else if (k == "q16") h.q16 = value;
+  else if (k == "sparse") h.sparse = value;
+  else if (k == "shards") h.shards = value;
   else if (k == "q16_guard_off") h.q16_guard_off = value;
   else if (k == "thr_exact_all") h.thr_exact_all = value;
   else if (k == "exact_gather") h.exact_gather = value;
@@ -927,6 +930,10 @@ int fs_multisurf_shards(int device, int64_t n, int64_t p, int world, int* shards
     return FS_EINVAL;
   }
   *shards = 1;
+  if (test_hooks().shards >= 1) {
+    *shards = (int)std::min<int64_t>(test_hooks().shards, 4096);
+    return FS_OK;
+  }
   if (gpu::device_count() <= 0) return FS_OK;
   Prepared P;
   P.n = n;

@@ -120,9 +120,13 @@ struct Prepared {
 int accumulation_mode();
 
 // Overrides of internal choices for the tests (fs_test_hook, the one
-// test-only entry point; every field 0 = the product's own choice).  No
-// environment variable selects a kernel or a route.
+// test-only entry point; every field at its default = the product's own
+// choice).  No environment variable selects a kernel or a route (FS_TRACE
+// only prints phase times, FS_DEVICE_CACHE_MB sizes the block cache).
 struct TestHooks {
+  int64_t q16 = -1;            // 0 / 1: 32- / 16-bit pass-1 operands (choose_q16); no decision check
+  int64_t sparse = -1;         // 0 / 1: dense / sparse pass 2 (choose_sparse)
+  int64_t shards = 0;          // >= 1: MultiSURF tile shards per device (multisurf_shards)
   int64_t ksplit = 0;          // pass-1 K-split parts of every tile (choose_ksplit)
   int64_t q16_guard_off = 0;   // 1: no coherence / row guard on 16-bit operands
   int64_t thr_exact_all = 0;   // 1: every MultiSURF row's threshold exact (exact_thresholds)
@@ -500,7 +504,7 @@ int plan_set_rows(Plan* g, int64_t r_lo, int64_t r_hi);
 // new ones.  X and its quantised operands stay resident.
 int plan_set_shard(Plan* g, int rank, int world);
 // Tile shards per device for a MultiSURF job of `world` ranks so that the
-// tile buffers fit the device (1 = no sharding; FS_SHARDS forces it); with
+// tile buffers fit the device (1 = no sharding; the shards test hook forces it); with
 // share > 1 that many plans split the device's memory (repeated ordinals).
 int multisurf_shards(const Prepared& P, int device, int world, int share = 1);
 // ReliefF / SURF plans: float64 score sums of the plan's focal rows

@@ -39,16 +39,15 @@ void plan_destroy(Plan* g) {
 // so MultiSURF takes them only from kQ16MinRowsMS samples on.  MultiSURF*
 // is less sensitive (its far misses weigh the pairs between the two
 // thresholds both ways): 5.5e-7 at cfg4, 1.5e-6 at cfg5 (n = 10000,
-// p = 50000), so it takes them from kQ16MinRowsMSStar on.  FS_Q16=0/1 in
-// the environment forces the choice (tests).  SURF has its own float64 pass.
+// p = 50000), so it takes them from kQ16MinRowsMSStar on.  The q16 test
+// hook forces the choice.  SURF has its own float64 pass.
 constexpr int64_t kQ16MinRowsRF = 4096, kQ16MinRowsMS = 16384, kQ16MinRowsMSStar = 10000;
 static int choose_q16(const Prepared& P) {
   if (P.algo == ALGO_SURF || P.no_q16) return 0;
   // reference-order MultiSURF replays the reference's decisions: 32-bit
   // operands, whose thresholds need exact recomputation on a handful of rows
   if (P.algo == ALGO_MULTISURF && P.ref_accum) return 0;
-  const char* env = std::getenv("FS_Q16");
-  if (env && *env) return std::atoi(env) != 0 ? 1 : 0;
+  if (test_hooks().q16 >= 0) return test_hooks().q16 != 0 ? 1 : 0;
   const int64_t min_rows = P.algo == ALGO_RELIEFF ? kQ16MinRowsRF
                            : P.use_star           ? kQ16MinRowsMSStar
                                                   : kQ16MinRowsMS;
@@ -63,11 +62,10 @@ static int choose_q16(const Prepared& P) {
 // 142 -> 103 ms sparse); MultiSURF* ~62% (cfg5 91 ms dense vs 102 sparse);
 // SURF about break-even (cfg5), SURF* weighs nearly every pair.  A
 // row-sharded SURF plan zeroes the sides of the samples it does not own, so
-// it goes sparse.  FS_SPARSE=0/1 forces either (tests).
+// it goes sparse.  The sparse test hook forces either.
 static int choose_sparse(const Plan* g, const Prepared& P) {
   if (P.algo == ALGO_RELIEFF) return 0;
-  const char* env = std::getenv("FS_SPARSE");
-  if (env && *env) return std::atoi(env) != 0 ? 1 : 0;
+  if (test_hooks().sparse >= 0) return test_hooks().sparse != 0 ? 1 : 0;
   if (P.algo == ALGO_MULTISURF) return P.use_star ? 0 : 1;
   return (g->r_hi - g->r_lo < P.n) ? 1 : 0;  // SURF / SURF*: only when row-sharded
 }
@@ -538,10 +536,10 @@ static int finish_scores(Plan* g, double* scores_dev, float* scores_out) {
 // pass-2 weight streams, partials) of a rank's 1/world of the n_pad^2/2/128^2
 // tiles, against the free device memory left after the per-sample buffers
 // (X, quantised operands, pass-2 operands, correction terms: ~16 n PW
-// bytes) and a 15% reserve.  1 when everything fits; FS_SHARDS forces it.
+// bytes) and a 15% reserve.  1 when everything fits; the shards test hook
+// forces it.
 int multisurf_shards(const Prepared& P, int device, int world, int share) {
-  if (const char* e = std::getenv("FS_SHARDS"))
-    if (std::atoi(e) >= 1) return std::atoi(e);
+  if (test_hooks().shards >= 1) return (int)std::min<int64_t>(test_hooks().shards, 4096);
   size_t free_b = 0, total_b = 0;
   if (hipSetDevice(device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
     (void)hipGetLastError();
@@ -702,14 +700,13 @@ __global__ __launch_bounds__(256) void q16_decision_risk(const double* __restric
 // the same risk and decides alike).  Above kQ16MaxRisk the plan is switched
 // to 32-bit operands for good (its layout and shard rebuilt; X stays on the
 // device) and *switched = 1: the caller runs the step again.  risk = -1 when
-// there is nothing to check (32-bit operands, MultiSURF*, FS_Q16 forcing).
+// there is nothing to check (32-bit operands, MultiSURF*, the q16 test hook).
 int plan_decision_guard(Plan* g, const double* rowstats, const double* counts,
                         const double* sums, double* risk, int* switched) {
   *risk = -1.0;
   *switched = 0;
   const Prepared& Q = g->P;
-  const char* force = std::getenv("FS_Q16");
-  if (Q.algo != ALGO_MULTISURF || !g->use_q16 || Q.use_star || (force && *force)) return FS_OK;
+  if (Q.algo != ALGO_MULTISURF || !g->use_q16 || Q.use_star || test_hooks().q16 >= 0) return FS_OK;
   // a focal-row slice holds only its rows' partial sums: as the one-shot
   // slice calls (multisurf_rows, a partial multisurf_run_devices), no check
   // (max |score| of a partial sum would inflate the risk)

@@ -163,8 +163,6 @@ class ShardedMultiSURF:
 
     def __init__(self, x, y, recip, is_discrete, use_star=False, backend="gpu", device=0,
                  shard=True, rows=None, shards=None, accumulation="fast"):
-        import os
-
         import torch
         self.dist, self.rank, self.world = _dist() if shard else (None, 0, 1)
         _lib.accumulation_code(accumulation)
@@ -180,9 +178,8 @@ class ShardedMultiSURF:
         # tile shards per device (n beyond HBM): the device holds the distance
         # tiles of one shard at a time (fs_plan_set_shard, three rounds a step)
         if shards is None:
-            env = os.environ.get("FS_SHARDS")
-            shards = int(env) if env else (
-                _lib.multisurf_shards(self.n, self.p, self.world, device) if backend == "gpu" else 1)
+            shards = (_lib.multisurf_shards(self.n, self.p, self.world, device)
+                      if backend == "gpu" else 1)
         if backend == "gpu":
             torch.cuda.set_device(device)
             self.tdev = torch.device("cuda", device)

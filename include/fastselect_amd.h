@@ -113,7 +113,8 @@ FS_API int fs_get_accumulation(void);
  * follow, process-wide (tests/ uses it to reach routes the automatic choices
  * take only at other sizes; no product code calls it).  name = "reset"
  * restores every default; the others are listed in INTEGRATION.md §4
- * ("ksplit", "q16_guard_off", "thr_exact_all", "exact_gather", "row_panel",
+ * ("ksplit", "q16", "sparse", "shards", "q16_guard_off", "thr_exact_all",
+ * "exact_gather", "row_panel",
  * "rf_xlds", "rf_fcap", "ties_1w", "ties_coop", "colsort_bins12",
  * "colsort_global").  FS_EINVAL for an unknown name.  Not thread-safe
  * against concurrent scoring calls.
@@ -196,7 +197,7 @@ FS_API int fs_multisurf_score(int backend, int device, const float* x, int64_t n
  * scored on 16-bit pass-1 operands estimates how far the near/far decisions
  * its quantised thresholds could change move the scores, relative to their
  * largest magnitude (risk_out; -1 when not evaluated: 32-bit operands,
- * MultiSURF*, FS_Q16 set, CPU backend); above 5e-6 the call scores again on
+ * MultiSURF*, the q16 test hook set, CPU backend); above 5e-6 the call scores again on
  * 32-bit operands and rerun_out is 1.  Signal-free inputs (scores at the
  * noise floor of the decisions) are what trips it.
  */
@@ -445,7 +446,7 @@ FS_API int fs_plan_set_rows(fs_plan* plan, int64_t row_begin, int64_t row_end);
 FS_API int fs_plan_set_shard(fs_plan* plan, int rank, int world);
 /* Shards per device that keep a MultiSURF job of n samples, p features and
  * `world` ranks within the device's free memory (1 when it fits, or without
- * a GPU; FS_SHARDS overrides).  The one-shot fs_multisurf_score[_rows]
+ * a GPU; the shards test hook overrides).  The one-shot fs_multisurf_score[_rows]
  * shards by itself. */
 FS_API int fs_multisurf_shards(int device, int64_t n, int64_t p, int world, int* shards);
 /*

@@ -83,11 +83,11 @@ def test_gpu_decisions(kind, n, p, seed, all_rows, hooks):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["uniform", "classification"])
-def test_gpu_16bit_operands_exact_thresholds_everywhere(kind, monkeypatch, hooks):
+def test_gpu_16bit_operands_exact_thresholds_everywhere(kind, hooks):
     """16-bit pass-1 operands (thresholds 256x coarser than on 32-bit ones):
     with every threshold exact, the refinement band alone must bring each
     decision to the reference's."""
-    monkeypatch.setenv("FS_Q16", "1")
+    hooks("q16", 1)
     hooks("q16_guard_off", 1)
     X, y = _data(kind, 1200, 400, 5)
     _check(X, y, "gpu", hooks, True)

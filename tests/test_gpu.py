@@ -193,7 +193,7 @@ def test_relieff_unstaged_rows(oracle):
 
 
 @pytest.mark.parametrize("n", [2500, 33000])
-def test_relieff_exact_keys_lds_and_global(n, monkeypatch):
+def test_relieff_exact_keys_lds_and_global(n, hooks):
     """k_rf_select's in-kernel exact keys: candidate rows gathered into LDS
     in batches (default; one row per batch with the rf_xlds hook at 4*pc) or summed
     straight from HBM (rf_xlds = 0), and the
@@ -232,7 +232,7 @@ def test_relieff_ties_large_rows(oracle):
     assert_parity(s, oracle.relieff_scores(X, y, n_neighbors=10, discrete_limit=4), TOL)
 
 
-def test_relieff_ties_multiwave_matches_single_wave(monkeypatch):
+def test_relieff_ties_multiwave_matches_single_wave(hooks):
     """k_rf_ties_mw (whole-workgroup partitions of the ranges of >= 2048
     samples, then 16 waves taking the smaller ranges from a shared queue)
     against the one-wave replay (ties_1w test hook) and against workgroup
@@ -547,9 +547,9 @@ def test_two_ranks_share_one_gpu(tmp_path):
 
 @pytest.mark.parametrize("algo,star", [("multisurf", False), ("multisurf", True), ("surf", False),
                                        ("surf", True)])
-def test_sparse_pass2_matches_dense(monkeypatch, algo, star):
+def test_sparse_pass2_matches_dense(algo, star, hooks):
     """k_weights_sparse + k_score_sparse (non-zero pair weights only) against
-    the dense k_weights + k_score on the same data (FS_SPARSE forces either),
+    the dense k_weights + k_score on the same data (the sparse test hook forces either),
     with mixed continuous/discrete blocks so both the asm loop and the generic
     loop run; and both against the oracle."""
     from fastselect_amd import SURF, MultiSURF
@@ -561,17 +561,17 @@ def test_sparse_pass2_matches_dense(monkeypatch, algo, star):
     est = MultiSURF if algo == "multisurf" else SURF
     out = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("FS_SPARSE", mode)
+        hooks("sparse", int(mode))
         out[mode] = _fit(est, X, y, use_star=star)
     ref = (O.multisurf_scores if algo == "multisurf" else O.surf_scores)(X, y, use_star=star)
     assert scale_rel_err(out["1"], out["0"]) <= 1e-6
     assert_parity(out["1"], ref, TOL, k=10)
 
 
-def test_exact_pairs_row_reads_match_gather(monkeypatch, hooks):
+def test_exact_pairs_row_reads_match_gather(hooks):
     """k_exact_pairs_rows (float4 reads of whole rows, all-continuous
     float32 data in input order) against the column-indexed gather
-    (the exact_gather test hook forces it): the 16-bit pass 1 (FS_Q16=1) refines
+    (the exact_gather test hook forces it): the 16-bit pass 1 (q16 hook) refines
     hundreds of pairs here; 1500 features is not a multiple of 256.
     Both refine the same pairs, so the scores agree to f64 summation order."""
     from fastselect_amd.parallel import ShardedMultiSURF
@@ -579,7 +579,7 @@ def test_exact_pairs_row_reads_match_gather(monkeypatch, hooks):
                                n_redundant=40, random_state=11)
     x = X.astype(np.float32)
     recip = (1 / (x.max(0) - x.min(0))).astype(np.float32)
-    monkeypatch.setenv("FS_Q16", "1")
+    hooks("q16", 1)
     out = {}
     for mode in ("rows", "gather"):
         if mode == "gather":

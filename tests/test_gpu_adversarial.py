@@ -2,8 +2,8 @@
 (duplicated, integer-grid and collinear columns), against the oracle's
 scores in tests/golden/adversarial_*.npz (tests/golden/make_adversarial.py).
 
-n = 3000: both pass-1 operand widths are forced (FS_Q16=0: 32-bit,
-FS_Q16=1: 16-bit preferred; the coherence guard may veto it) and the
+n = 3000: both pass-1 operand widths are forced (q16 test hook 0: 32-bit,
+1: 16-bit preferred; the coherence guard may veto it) and the
 default runs too.  n = 16384: the default path, which takes 16-bit operands
 there unless the guard vetoes them.  Bar: 1e-5 scale-relative
 (MultiSURF.py:165-253) and the same top-k base columns (copies of one column
@@ -73,29 +73,29 @@ def _check(name, X, y, fx, base):
 
 @pytest.mark.parametrize("q16", ["0", "1", ""])
 @pytest.mark.parametrize("name", ["dup", "intgrid", "collinear"])
-def test_coherent_rounding_multisurf(name, q16, monkeypatch):
+def test_coherent_rounding_multisurf(name, q16, hooks):
     if name == "intgrid" and q16 == "1":
         pytest.skip("forced 16-bit below n = 16384: the threshold's sigma error alone is "
                     "~2e-5 at n = 3000 (DESIGN.md '16-bit pass 1'); intgrid_16k covers it")
     X, y, fx, base = _case(name)
     if q16:
-        monkeypatch.setenv("FS_Q16", q16)
+        hooks("q16", int(q16))
     else:
-        monkeypatch.delenv("FS_Q16", raising=False)
+        hooks("q16", -1)
     _check(name, X, y, fx, base)
 
 
 @pytest.mark.parametrize("name", ["dup_16k", "intgrid_16k", "collinear_16k"])
-def test_coherent_rounding_multisurf_default_16k(name, monkeypatch):
-    monkeypatch.delenv("FS_Q16", raising=False)
+def test_coherent_rounding_multisurf_default_16k(name, hooks):
+    hooks("q16", -1)
     X, y, fx, base = _case(name)
     _check(name, X, y, fx, base)
 
 
-def _calibration(X, y, monkeypatch, q16="1"):
+def _calibration(X, y, hooks, q16="1"):
     from fastselect_amd import _lib
     from fastselect_amd.parallel import prepare_inputs
-    monkeypatch.setenv("FS_Q16", q16)
+    hooks("q16", int(q16))
     x, yv, recip, isd = prepare_inputs(X, y, backend="gpu")
     plan = _lib.Plan("gpu", x, yv, recip, isd)
     try:
@@ -105,9 +105,9 @@ def _calibration(X, y, monkeypatch, q16="1"):
 
 
 @pytest.mark.parametrize("name", ["dup", "collinear"])
-def test_guard_vetoes_16bit_on_coherent_columns(name, monkeypatch):
+def test_guard_vetoes_16bit_on_coherent_columns(name, hooks):
     X, y, _, _ = _case(name)
-    c = _calibration(X, y, monkeypatch)
+    c = _calibration(X, y, hooks)
     assert c["guard"] and not c["q16"], c
     # reported on the 32-bit scale now.  Exact copies round identically at
     # any scale (the band widens beyond the model's); affine copies only on
@@ -117,11 +117,11 @@ def test_guard_vetoes_16bit_on_coherent_columns(name, monkeypatch):
         assert c["rms"] > 2.0 * c["model_sigma"] and c["band_vs_model"] > 1.0, c
 
 
-def test_calibration_keeps_model_band_on_ordinary_data(monkeypatch):
+def test_calibration_keeps_model_band_on_ordinary_data(hooks):
     from sklearn.datasets import make_classification
     X, y = make_classification(n_samples=3000, n_features=2000, n_informative=20,
                                n_redundant=50, random_state=3)
-    c = _calibration(X, y, monkeypatch)
+    c = _calibration(X, y, hooks)
     assert c["q16"] and not c["guard"], c
     # independent rounding: the measured rms is the model's sigma (1/6 per
     # feature at most) and the band stays the model's 12 sigma

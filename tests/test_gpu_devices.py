@@ -43,12 +43,12 @@ def test_multisurf_devices_equal_one_device(F, oracle, star, devs):
                   1e-5, 10)
 
 
-def test_multisurf_devices_with_tile_shards(F, monkeypatch):
+def test_multisurf_devices_with_tile_shards(F, hooks):
     """V = 2 tile shards per device (n beyond HBM) under two device threads:
     tile t belongs to thread / shard t % 4."""
     X, y = _data(1800, 400, 2)
     one = F.MultiSURF(backend="gpu", devices=[0]).fit(X, y).feature_importances_
-    monkeypatch.setenv("FS_SHARDS", "2")
+    hooks("shards", 2)
     many = F.MultiSURF(backend="gpu", devices=[0, 0]).fit(X, y).feature_importances_
     assert scale_rel_err(many, one) <= 1e-6
 

@@ -4,7 +4,7 @@ from n = 10000 samples.  Same bar
 as every parity test: 1e-5 scale-relative and identical top-k.
 
 ReliefF is exact with them (the band of exactly recomputed keys widens), so
-it is forced on (FS_Q16=1) at sizes the oracle runs in seconds.  MultiSURF's
+it is forced on (the q16 test hook) at sizes the oracle runs in seconds.  MultiSURF's
 thresholds carry a quantisation error whose score effect falls as ~n^-1.25
 (DESIGN.md §2): it is checked against the oracle at n = 16384 (its default
 size) and against the 32-bit path at n = 20000.
@@ -24,9 +24,9 @@ def _fit(cls, X, y, **kw):
     return est.feature_importances_
 
 
-def test_q16_mixed_blocks_relieff(oracle, monkeypatch):
+def test_q16_mixed_blocks_relieff(oracle, hooks):
     from fastselect_amd import ReliefF
-    monkeypatch.setenv("FS_Q16", "1")
+    hooks("q16", 1)
     rng = np.random.default_rng(5)
     n = 2000
     Xc = rng.standard_normal((n, 300)) * rng.uniform(0.1, 10, 300)
@@ -38,9 +38,9 @@ def test_q16_mixed_blocks_relieff(oracle, monkeypatch):
 
 
 @pytest.mark.parametrize("k,ncls", [(10, 2), (3, 3)])
-def test_q16_relieff_parity(oracle, monkeypatch, k, ncls):
+def test_q16_relieff_parity(oracle, k, ncls, hooks):
     from fastselect_amd import ReliefF
-    monkeypatch.setenv("FS_Q16", "1")
+    hooks("q16", 1)
     X, y = make_classification(n_samples=3000, n_features=500, n_informative=20,
                                n_redundant=20, n_classes=ncls, random_state=k)
     assert_parity(_fit(ReliefF, X, y, n_neighbors=k),
@@ -56,13 +56,13 @@ def test_q16_multisurf_default_at_16384(oracle):
     assert_parity(_fit(MultiSURF, X, y), oracle.multisurf_scores(X, y), TOL, k=10)
 
 
-def test_q16_agrees_with_u32_path(monkeypatch):
+def test_q16_agrees_with_u32_path(hooks):
     from fastselect_amd import MultiSURF, ReliefF
     X, y = make_classification(n_samples=20000, n_features=2000, n_informative=20,
                                n_redundant=50, random_state=42)
     out = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("FS_Q16", flag)
+        hooks("q16", int(flag))
         out[flag] = (_fit(MultiSURF, X, y), _fit(ReliefF, X, y, n_neighbors=10))
     for a, b in zip(out["0"], out["1"]):
         assert scale_rel_err(b, a) < 5e-6
@@ -86,7 +86,7 @@ def test_q16_multisurf_mixed_default_at_16384(oracle):
                       oracle.multisurf_scores(X, y, use_star=star), TOL, k=10)
 
 
-def test_q16_multisurf_star_default_at_10000(oracle, monkeypatch):
+def test_q16_multisurf_star_default_at_10000(oracle, hooks):
     """MultiSURF* takes the 16-bit pass from n = 10000: against the oracle
     (p = 96) and against the 32-bit path (p = 3000)."""
     from fastselect_amd import MultiSURF
@@ -98,7 +98,7 @@ def test_q16_multisurf_star_default_at_10000(oracle, monkeypatch):
                                n_redundant=100, random_state=42)
     out = {}
     for flag in ("0", "1"):
-        monkeypatch.setenv("FS_Q16", flag)
+        hooks("q16", int(flag))
         out[flag] = _fit(MultiSURF, X, y, use_star=True)
     assert scale_rel_err(out["1"], out["0"]) < 5e-6
     assert set(np.argsort(out["0"])[::-1][:10]) == set(np.argsort(out["1"])[::-1][:10])

@@ -246,10 +246,10 @@ def test_ranks_chain_the_column_sums_bitexact(F, oracle, tmp_path, world, rows):
                 assert_bitexact(np.load(f"{out}.{int(star)}.{r}{tag}.npy"), ref)
 
 
-def test_forced_tile_shards_bitexact(F, oracle, monkeypatch):
+def test_forced_tile_shards_bitexact(F, oracle, hooks):
     """n beyond HBM: the one-shot call in V tile shards writes every shard's
     decisions into the masks before the chains run."""
-    monkeypatch.setenv("FS_SHARDS", "3")
+    hooks("shards", 3)
     X, y = verdict_case("pareto1", 1300, 200, seed=8)
     for star in (False, True):
         assert_bitexact(

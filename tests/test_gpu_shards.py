@@ -3,7 +3,7 @@
 A MultiSURF job whose distance tiles do not fit the device runs in V shards,
 the device holding one shard's tiles at a time and recomputing them in each
 of the three rounds (MultiSURF.py:174-214 streams distance rows the same
-way).  Forced here at sizes the oracle checks (FS_SHARDS / shards=V) and
+way).  Forced here at sizes the oracle checks (the shards test hook / shards=V) and
 compared with the one-shard job and the oracle; the automatic choice
 (fs_multisurf_shards) is checked at sizes that do and do not fit 288 GB.
 """
@@ -25,17 +25,17 @@ def _inputs(n=1500, p=400, seed=21):
 
 
 @pytest.mark.parametrize("shards", [2, 5])
-def test_one_shot_in_shards_matches_oracle(oracle, monkeypatch, shards):
+def test_one_shot_in_shards_matches_oracle(oracle, shards, hooks):
     from fastselect_amd import _lib
     X, y, (x, yv, recip, isd) = _inputs()
     one = _lib.multisurf_score("gpu", x, yv, recip, None, False, isd)
-    monkeypatch.setenv("FS_SHARDS", str(shards))
+    hooks("shards", shards)
     many = _lib.multisurf_score("gpu", x, yv, recip, None, False, isd)
     assert scale_rel_err(many, one) < 1e-6
     assert_parity(many, oracle.multisurf_scores(X, y), TOL, k=10)
 
 
-def test_sharded_job_in_tile_shards(monkeypatch):
+def test_sharded_job_in_tile_shards():
     from fastselect_amd import _lib
     from fastselect_amd.parallel import ShardedMultiSURF
     X, y, (x, yv, recip, isd) = _inputs(n=2100, p=300, seed=4)
@@ -51,9 +51,9 @@ def test_sharded_job_in_tile_shards(monkeypatch):
         assert set(np.argsort(s)[::-1][:10]) == set(np.argsort(ref)[::-1][:10])
 
 
-def test_shard_count_follows_device_memory(monkeypatch):
+def test_shard_count_follows_device_memory(hooks):
     from fastselect_amd import _lib
-    monkeypatch.delenv("FS_SHARDS", raising=False)
+    hooks("shards", 0)
     assert _lib.multisurf_shards(20000, 20000) == 1          # cfg4: 3.2 GB of tiles
     assert _lib.multisurf_shards(400000, 20000) > 1          # ~1.3 TB of tiles
     assert _lib.multisurf_shards(400000, 20000, world=8) < _lib.multisurf_shards(400000, 20000)

@@ -239,13 +239,12 @@ def test_gloo_world2_with_two_tile_shards_each(tmp_path):
 def _uneven_shard_worker(rank, world, port, out_path):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    # each rank sizes its shard count from its own memory: here they disagree
-    os.environ["FS_SHARDS"] = str(1 + 2 * rank)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
     X, y = make_classification(n_samples=500, n_features=40, random_state=2)
     x, yv, recip, isd = prepare_inputs(X, y, backend="cpu")
-    job = ShardedMultiSURF(x, yv, recip, isd, backend="cpu")
+    # each rank sizes its shard count from its own memory: here they disagree
+    job = ShardedMultiSURF(x, yv, recip, isd, backend="cpu", shards=1 + 2 * rank)
     np.save(f"{out_path}.{rank}.npy", job.step().numpy())
     np.save(f"{out_path}.{rank}.v.npy", np.array(job.shards))
     job.close()
@@ -255,7 +254,7 @@ def _uneven_shard_worker(rank, world, port, out_path):
 
 def test_gloo_ranks_agree_on_the_shard_count(tmp_path):
     """ranks that size their tile-shard count differently
-    (FS_SHARDS 1 and 3 here; free memory on GPUs) must still deal the tiles
+    (shards=1 and 3 here; free memory on GPUs) must still deal the tiles
     by one ownership map -- the MAX over ranks -- or tiles are scored twice or
     never.  Equal to one process."""
     import torch.multiprocessing as mp

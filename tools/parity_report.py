@@ -72,20 +72,16 @@ def main():
         exact = np.load(f64, allow_pickle=False)["scores"] if os.path.exists(f64) else None
         variants = [("default", {})]
         if str(fx["algo"]) == "surf":  # the whole-fit (dense) pass 2 beside the sparse slice path
-            variants.append(("FS_SPARSE=0", {"FS_SPARSE": "0"}))
+            variants.append(("dense", {"sparse": 0}))
         if str(fx["algo"]) == "multisurf" and n >= 16384:  # 32-bit pass 1 beside the 16-bit default
-            variants.append(("FS_Q16=0", {"FS_Q16": "0"}))
-        for label, env in variants:
-            old = {k: os.environ.get(k) for k in env}
-            os.environ.update(env)
+            variants.append(("q32", {"q16": 0}))
+        from fastselect_amd import _lib
+        for label, hooks in variants:
             try:
-                s = gpu_scores(fx, X, y)
+                with _lib.test_hooks(**hooks):
+                    s = gpu_scores(fx, X, y)
             finally:
-                for k, v in old.items():
-                    if v is None:
-                        os.environ.pop(k, None)
-                    else:
-                        os.environ[k] = v
+                _lib.set_test_hook("reset")
             print(f"{os.path.basename(path):36s} {label:11s} n={n:6d} p={p:6d} rows=[{lo},{hi}) "
                   f"{summary(s, ref)} top-10 same: {topk_same(s, ref, 10)}", flush=True)
             if exact is not None:

@@ -1,4 +1,4 @@
-"""MultiSURF / ReliefF scores with 16-bit (FS_Q16=1) vs 32-bit (FS_Q16=0)
+"""MultiSURF / ReliefF scores with 16-bit (q16 test hook 1) vs 32-bit (0)
 pass-1 operands on the BASELINE configs: scale-relative difference and top-k
 agreement (the 32-bit path is the one pinned to the oracle at ~1e-7).
 
@@ -28,7 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default=",".join(CFG))
     a = ap.parse_args()
-    from fastselect_amd import MultiSURF, ReliefF
+    from fastselect_amd import MultiSURF, ReliefF, _lib
     for name in a.only.split(","):
         algo, n, p, R, star = CFG[name]
         X, y = make_classification(n_samples=n, n_features=p, n_informative=20, n_redundant=R,
@@ -36,7 +36,7 @@ def main():
         X = X.astype(np.float32)
         s = {}
         for flag in ("0", "1"):
-            os.environ["FS_Q16"] = flag
+            _lib.set_test_hook("q16", int(flag))
             if algo == "ms":
                 est = MultiSURF(backend="gpu", use_star=star, n_features_to_select=10)
             else:

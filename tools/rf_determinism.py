@@ -26,6 +26,7 @@ for act in (np.arange(300), np.array([0, 4, 63, 78, 95, 111, 166, 172, 243, 248]
             np.array([0, 63, 78, 95, 111, 166, 172, 243, 248, 261])):
     Xs = np.ascontiguousarray(X[:, act])
     _lib.set_test_hook("ksplit", int(os.environ.get("RF_DET_KSPLIT", "0")))
+    _lib.set_test_hook("q16", int(os.environ.get("RF_DET_Q16", "-1")))
     x, ye, recip, isd, pri = relieff_inputs(Xs, y, 6, "gpu")
     res = {{tuple(_lib.relieff_score("gpu", x, ye, recip, isd, 6, pri).tolist()) for r in range(12)}}
     out.append(len(res))
@@ -35,7 +36,7 @@ print("distinct results in 12 (full, 10 with the discrete column, 10 continuous)
 
 def main():
     for label, env in (("default", {}), ("ksplit=1", {"RF_DET_KSPLIT": "1"}),
-                       ("FS_Q16=1", {"FS_Q16": "1"}), ("trace", {"FS_TRACE": "1"})):
+                       ("q16=1", {"RF_DET_Q16": "1"}), ("trace", {"FS_TRACE": "1"})):
         e = dict(os.environ, **env)
         r = subprocess.run([sys.executable, "-c", CHILD.format(root=ROOT)], env=e,
                            capture_output=True, text=True, timeout=300)
