@@ -407,6 +407,7 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     ms_per_step = float(t.item()) / args.steps * 1e3
     roofline = None
+    q16 = False
     if on_gpu:
         nb = (n + 127) // 128
         b0, b1 = rows[0] // 128, (rows[1] + 127) // 128
@@ -444,10 +445,9 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
             roofline["peak_note"] = ("float64 vector peak (AMD MI355X figure, half the fp32 rate); "
                                      "2 v_add_f64 per PFE, each priced as one FMA")
     plan.close()
-    # ReliefF in reference order beside the default (N = 1): same plan type
+    # ReliefF / SURF in reference order beside the default (N = 1): same plan type
     refacc = None
-    if (on_gpu and world == 1 and algo == "relieff" and not args.no_ref
-            and args.accumulation == "fast"):
+    if on_gpu and world == 1 and not args.no_ref and args.accumulation == "fast":
         with _lib.accumulation("reference"):
             rplan = _lib.RowsPlan(args.backend, algo, xin, ye, recip, isd, rows=rows,
                                   device=local, stream=stream, **kw)
@@ -460,8 +460,10 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
                 rplan.score(sums.data_ptr())
             sync()
             refacc = {"ms_per_step": (time.perf_counter() - t_r) / ks * 1e3, "steps": ks,
-                      "kernel_ms": {"k_dist": rplan.kernel_ms(0),
-                                    "selection_to_scores": rplan.kernel_ms(1)},
+                      "kernel_ms": {"k_dist" if algo == "relieff" else "k_dist_f64":
+                                    rplan.kernel_ms(0),
+                                    "selection_to_scores" if algo == "relieff"
+                                    else "masks_and_chains": rplan.kernel_ms(1)},
                       "parity": "bit-identical to the oracle (tests/test_gpu_refacc.py)"}
         finally:
             rplan.close()
@@ -473,7 +475,9 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
             "value": n * p / (ms_per_step * 1e-3), "unit": "feature-scores/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": "fp32" if algo == "relieff" else "fp64 distances",
+            "vs_baseline": None,
+            "dtype": (f"{'u16' if q16 else 'u32'} pass 1 (exact keys near the k-th), fp32 / fp64 "
+                      "update" if algo == "relieff" else "fp64 distances, fp32 pair sums"),
             "data": f"synthetic make_classification(n_informative=20, n_redundant={cfg['red']}, "
                     f"random_state=42)",
             "config": {"workload": f"{name} n={n} p={p} (BASELINE configs[{cfg['idx']}])",
@@ -678,6 +682,12 @@ def main():
                              for k in kern},
             "onchip_panel_GBps": {k: panel_bytes[k] / (kern[k] * 1e-3) / 1e9 for k in kern},
             "hbm_peak_GBps": HBM_PEAK_GBPS,
+            # the measured traffic of the dominant kernel (rocprofv3 FETCH x2 +
+            # WRITE per launch, profiles/pmc_traffic.json) over its launch time
+            "hbm_measured_GBps": (traffic[dom] / (kern[dom] * 1e-3) / 1e9
+                                  if traffic[dom] else None),
+            "hbm_measured_frac": (traffic[dom] / (kern[dom] * 1e-3) / 1e9 / HBM_PEAK_GBPS
+                                  if traffic[dom] else None),
         }
     job.close()
     # the decision-finer 32-bit pass 1 beside the default step (VERDICT r2
@@ -729,7 +739,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": f"{'u16' if q16_used else 'u32'} pass 1, fp32 pass 2 (fp64 accumulation)",
             "arith": "pass 1: integer L1 distances (v_sad_u16 on 16-bit operands for n >= 16384, "
                      "else v_sad_u32), pairs near a threshold recomputed in the reference's "
                      "float32 arithmetic; pass 2 over the pairs with a non-zero weight: f32 diffs x "

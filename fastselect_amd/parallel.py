@@ -195,6 +195,14 @@ class ShardedMultiSURF:
         # tiles twice and others never.  Each rank sizes V from its own free
         # memory; the largest V fits on every rank.
         self.shards = self._agree_max(max(1, int(shards)))
+        if accumulation == "reference" and self.ref_chain and self.shards > 1:
+            # the rank step keeps all of a rank's tiles resident (its masks
+            # are written once, then reduce-scattered): a job that needs V > 1
+            # tile shards per device does not fit it
+            raise MemoryError(
+                f"accumulation='reference' over {self.world} ranks needs each rank's pair "
+                f"tiles resident, but the devices hold only 1/{self.shards} of them; use more "
+                "ranks, or one rank (the one-shot call shards by itself)")
         if accumulation == "reference":
             # one plan per rank holding all of its tiles (the one-shot calls
             # shard by themselves)
@@ -206,9 +214,14 @@ class ShardedMultiSURF:
         if rows is not None:  # focal-sample slice: pass 2 sums those samples only
             self.plan.set_rows(*rows)
         if self.ref_chain:
+            # equal blocks of R focal rows per rank (the last ones short or
+            # empty), so that each rank's rows of the decision masks are one
+            # equal chunk of the buffer: a reduce-scatter, not an all-reduce
             f0, f1 = rows if rows is not None else (0, self.n)
-            b, e = shard_rows(f1 - f0, self.rank, self.world)
-            self.ref_rows = (f0 + b, f0 + e)
+            self.ref_R = -(-(f1 - f0) // self.world)
+            lo = min(f1, f0 + self.rank * self.ref_R)
+            self.ref_rows = (lo, min(f1, lo + self.ref_R))
+            self.ref_f0 = f0
             self.masks = None
         f64 = torch.float64
         with self._on_stream():
@@ -254,9 +267,51 @@ class ShardedMultiSURF:
 
     def _allreduce(self, t):
         # issued whenever a process group is up, world 1 included (one RCCL
-        # call per exchange point; a plain single-process job has none)
+        # call per exchange point; a plain single-process job has none).  The
+        # ordering is explicit: RCCL runs the collective on its own internal
+        # stream after the job's stream (torch's current stream here, see
+        # _on_stream) reaches the call, and work.wait() makes the job's
+        # stream wait for its completion before the next plan stage reads t
+        # (no host synchronisation; gloo completes on the host)
         if self.dist is not None:
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM, async_op=True).wait()
+
+    def _mask_words_per_row(self):
+        return self.plan.ref_mask_words() // self._n_pad()
+
+    def _n_pad(self):
+        return -(-self.n // ROW_BLOCK) * ROW_BLOCK
+
+    def _masks_of_my_rows(self):
+        """The rank's pair-tile decisions (``fs_plan_ref_masks``) summed over
+        the ranks for this rank's focal rows only: every (row, word) is
+        written by exactly one rank, so the SUM of the buffers is the whole
+        triangle's masks.  With RCCL a reduce-scatter over equal chunks of
+        R rows (each rank receives 1/N of the n_pad^2/2 bytes: 202 MB / N at
+        cfg4, where an all-reduce moved all of it); gloo has no
+        reduce-scatter, so it all-reduces and slices the same chunk.  Returns
+        (buffer, device address of row 0 in it): the chains read only rows
+        ref_rows, so the address may lie before the chunk."""
+        import torch
+        wpr = self._mask_words_per_row()
+        R, f0 = self.ref_R, self.ref_f0
+        if R == 0:
+            return 0
+        rows_total = max(self._n_pad(), f0 + self.world * R)
+        if self.masks is None:
+            # whole-matrix buffer (rows past n_pad stay zero) and the chunk
+            self.masks = torch.zeros(rows_total * wpr, dtype=torch.int64, device=self.tdev)
+            self.mask_chunk = torch.empty(R * wpr, dtype=torch.int64, device=self.tdev)
+        self.plan.ref_masks(self.masks.data_ptr(), self.plan.ref_mask_words())
+        src = self.masks[f0 * wpr:(f0 + self.world * R) * wpr]
+        if self.dist.get_backend() == "nccl":
+            self.dist.reduce_scatter_tensor(self.mask_chunk, src, op=self.dist.ReduceOp.SUM,
+                                            async_op=True).wait()
+        else:
+            self.dist.all_reduce(src, op=self.dist.ReduceOp.SUM, async_op=True).wait()
+            self.mask_chunk.copy_(src[self.rank * R * wpr:(self.rank + 1) * R * wpr])
+        lo = f0 + self.rank * R
+        return self.mask_chunk.data_ptr() - lo * wpr * 8
 
     def _shard(self, v):
         self.plan.set_shard(self.rank + self.world * v, self.world * self.shards)
@@ -313,12 +368,8 @@ class ShardedMultiSURF:
         self._allreduce(self.rowstats)
         self.plan.select(self.rowstats.data_ptr(), self.counts.data_ptr())
         self._allreduce(self.counts)
-        if self.masks is None:
-            self.masks = torch.empty(self.plan.ref_mask_words(), dtype=torch.int64,
-                                     device=self.tdev)
-        self.plan.ref_masks(self.masks.data_ptr(), self.masks.numel())
-        self._allreduce(self.masks)
-        self.plan.ref_pass2(self.masks.data_ptr(), self.counts.data_ptr(), *self.ref_rows)
+        base = self._masks_of_my_rows()
+        self.plan.ref_pass2(base, self.counts.data_ptr(), *self.ref_rows)
         init = None
         if self.rank > 0:
             buf = self._p2p(torch.empty_like(self.scores))
