@@ -187,6 +187,20 @@ def test_cfg5_multisurfstar_whole_fit(lib):
     _attribute("cfg5_multisurfstar", est.feature_importances_, fx["scores"], False)
 
 
+@pytest.mark.parametrize("name,star", [("cfg5_surf", False), ("cfg5_surfstar", True)])
+def test_cfg5_surf_whole_fit(lib, name, star):
+    """SURF / SURF* at BASELINE configs[4] (10000 x 50000, float64 X) as one
+    whole fit against the oracle's whole-fit vector (VERDICT r5 missing #2:
+    k_surf_avg over every row and the whole column sum, not only the 384-row
+    slices below)."""
+    fx = _fixture(name)
+    assert bool(fx["use_star"]) == star
+    X, y = _inputs(fx)
+    est = lib.SURF(backend="gpu", use_star=star, n_features_to_select=TOPK).fit(X, y)
+    assert est.effective_backend_ == "gpu"
+    assert_parity(est.feature_importances_, fx["scores"], TOL, TOPK)
+
+
 @pytest.mark.parametrize("sparse", ["default", "0"])
 @pytest.mark.parametrize("name", ["cfg5_surfstar_slice", "cfg5_surf_slice"])
 def test_cfg5_surf_focal_slice(lib, name, sparse, hooks):
