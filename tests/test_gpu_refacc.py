@@ -257,6 +257,40 @@ def test_forced_tile_shards_bitexact(F, oracle, hooks):
             oracle.multisurf_scores(X, y, use_star=star))
 
 
+def test_plan_narrow_then_wide_features_bitexact(F, oracle):
+    """a reference-order plan created on a few features
+    and re-targeted to all of them (fs_plan_set_features) keeps fixing every
+    flagged row's threshold -- its batch counts are sized for any layout --
+    and scores the wide layout as a fresh plan would, bit for bit."""
+    import torch
+
+    from fastselect_amd import _lib
+    from fastselect_amd.parallel import prepare_inputs
+    X, y = verdict_case("exp4z", 4500, 240, seed=13)
+    x, yv, recip, isd = prepare_inputs(X, y, backend="gpu")
+    dev = torch.device("cuda", 0)
+    n, p = x.shape
+    rs = torch.zeros(3 * n, dtype=torch.float64, device=dev)
+    cnt = torch.zeros(2 * n, dtype=torch.float64, device=dev)
+    with _lib.accumulation("reference"):
+        plan = _lib.Plan("gpu", x, yv, recip, isd, feat_idx=np.arange(50))
+    try:
+        for fidx in (np.arange(50), None):
+            if fidx is None:
+                plan.set_features(None)
+            sc = torch.zeros(plan.n_kept, dtype=torch.float64, device=dev)
+            torch.cuda.synchronize()  # the plan runs on its own stream
+            plan.pass1(rs.data_ptr())
+            plan.select(rs.data_ptr(), cnt.data_ptr())
+            plan.pass2(cnt.data_ptr(), sc.data_ptr())
+            torch.cuda.synchronize()
+            got = (sc.cpu().numpy() / n).astype(np.float32)
+            Z = X if fidx is None else X[:, fidx]
+            assert_bitexact(got, oracle.multisurf_scores(Z, y))
+    finally:
+        plan.close()
+
+
 def test_turf_resident_bitexact(F, oracle):
     from test_refacc import turf_oracle
     X, y = verdict_case("exp4z", 1200, 120, seed=6)
