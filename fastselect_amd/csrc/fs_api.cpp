@@ -144,6 +144,7 @@ int fs_test_hook(const char* name, int64_t value) {
   else if (k == "rf_fcap") h.rf_fcap = value;
   else if (k == "ties_1w") h.ties_1w = value;
   else if (k == "ties_coop") h.ties_coop = value;
+  else if (k == "rf_ref_replay") h.rf_ref_replay = value;
   else if (k == "colsort_bins12") h.colsort_bins12 = value;
   else if (k == "colsort_global") h.colsort_global = value;
   else {

@@ -740,6 +740,34 @@ static void ref_tie_order(const Prepared& P, const float* X, int64_t i,
   }
 }
 
+// Whether another order of row i's tied lists could change their float64
+// sums (as k_rf_ref_order_matters): a list whose float32 diffs at some
+// feature are multiples of u = ulp(smallest non-zero diff) summing below
+// 2^53 u has every partial sum exact, in any order.
+static bool ref_order_matters(const Prepared& P, const float* X, int64_t i,
+                              const std::vector<std::vector<float>>& nkey,
+                              const std::vector<std::vector<int32_t>>& nbr) {
+  for (size_t c = 0; c < nbr.size(); c++) {
+    bool run = false;
+    for (size_t t = 1; t < nbr[c].size(); t++) run = run || nkey[c][t] == nkey[c][t - 1];
+    if (!run) continue;
+    for (int64_t f = 0; f < P.n_kept; f++) {
+      float vmin = INFINITY;
+      double s = 0.0;
+      for (int32_t j : nbr[c]) {
+        const float v = ref_diff(P, X, i, j, f);
+        if (v > 0.0f && v < vmin) vmin = v;
+        s += (double)v;
+      }
+      if (vmin == INFINITY) continue;
+      int e;
+      (void)std::frexp(vmin, &e);
+      if (s >= std::ldexp(1.0, e - 24 + 53)) return true;
+    }
+  }
+  return false;
+}
+
 int relieff_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int64_t r_hi,
                 double* scores) {
   std::vector<uint32_t> xq;
@@ -779,8 +807,11 @@ int relieff_run(const Prepared& P, const void* x, int n_jobs, int64_t r_lo, int6
       // decides the order of its float64 sums below (ReliefF.py:181-207).
       // With continuous features that order can change a sum's rounding, so
       // replay the quicksort over the row's exact keys (as k_rf_ref_ties
-      // does); 0 / 1 diffs of an all-discrete layout add exactly in any order.
-      if (dup && P.pc > 0) ref_tie_order(P, X, i, nkey, nbr);
+      // does) when it can (ref_order_matters); 0 / 1 diffs of an
+      // all-discrete layout add exactly in any order.
+      if (dup && P.pc > 0 &&
+          (test_hooks().rf_ref_replay || ref_order_matters(P, X, i, nkey, nbr)))
+        ref_tie_order(P, X, i, nkey, nbr);
       const int32_t li = P.labels[i];
       double denom = 1.0 - P.class_prior[li];
       if (denom == 0.0) denom = 1.0;

@@ -136,6 +136,7 @@ struct TestHooks {
   int64_t rf_fcap = -1;        // candidates listed per row in LDS (-1: 256)
   int64_t ties_1w = 0;         // 1: the one-wave quicksort replay
   int64_t ties_coop = 0;       // smallest range the tie workgroup partitions (0: 2048)
+  int64_t rf_ref_replay = 0;   // 1: reference-order quicksort replay of every tied row
   int64_t colsort_bins12 = 0;  // 1: 4096 bins at every n
   int64_t colsort_global = 0;  // 1: the large-n (device sort) route at every n
 };
@@ -587,6 +588,13 @@ int relieff_order(const float* xk, int64_t Kp, const float* krecip, const uint8_
 int relieff_row_keys(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,
                      int64_t n_kept, const int32_t* rows, int64_t nr, int64_t n, float* keys,
                      void* stream);
+// matters[r] = 1 when some list of row rows[r] flagged in dup could sum to
+// different float64 values in another order (a continuous feature whose
+// float32 diffs span 2^29 or more); 0 = any order gives the same sums.
+int relieff_order_matters(const float* xk, int64_t Kp, const float* krecip,
+                          const uint8_t* kdisc, int64_t n_kept, const int32_t* rows, int64_t nr,
+                          const int32_t* dup, const int32_t* nbr, const int32_t* nfound,
+                          int64_t r_lo, int C, int64_t k, int32_t* matters, void* stream);
 // temp[i - r_lo][k] = f32(update) over the lists in their order
 // (ReliefF.py:177-216).
 int relieff_update(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,

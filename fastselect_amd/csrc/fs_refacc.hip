@@ -530,6 +530,52 @@ __global__ __launch_bounds__(256) void k_rf_ref_sort(int32_t* __restrict__ nbr,
   dup[ic] = d;
 }
 
+// Whether the order of a row's tied neighbours can change its float64 sums
+// (ReliefF.py:181-207): for every list holding a run of equal keys (dup) and
+// every continuous feature, the list's float32 diffs are all multiples of
+// u = ulp(smallest non-zero diff) (a float32 value is a multiple of its own
+// ulp, and larger ones of u), so when their sum is below 2^53 u every partial
+// sum, in ANY order, is exactly representable in float64 -- the order cannot
+// matter.  Only a row where some sum reaches 2^53 u (diffs 2^29 or more
+// apart) needs numba's quicksort order (k_rf_ref_ties); 0 / 1 diffs of
+// discrete features are exact in any order.  Grid: one 256-thread workgroup
+// per candidate row, the threads over the features.
+__global__ __launch_bounds__(256) void k_rf_ref_order_matters(
+    const float* __restrict__ xk, int64_t Kp, const float* __restrict__ krecip,
+    const uint8_t* __restrict__ kdisc, int64_t n_kept, const int32_t* __restrict__ rows,
+    const int32_t* __restrict__ dup, const int32_t* __restrict__ nbr,
+    const int32_t* __restrict__ nfound, int64_t r_lo, int C, int64_t k,
+    int32_t* __restrict__ matters) {
+  __shared__ int any;
+  if (threadIdx.x == 0) any = 0;
+  __syncthreads();
+  const int64_t r = blockIdx.x, i = rows[r];
+  const float* xi = xk + i * Kp;
+  int m = 0;
+  for (int c = 0; c < C && !m; c++) {
+    if (!dup[(i - r_lo) * C + c]) continue;
+    const int64_t cnt = nfound[i * C + c];
+    const int32_t* L = nbr + (i * C + c) * k;
+    for (int64_t f = threadIdx.x; f < n_kept && !m; f += 256) {
+      if (kdisc[f]) continue;
+      float vmin = __builtin_inff();
+      double s = 0.0;
+      for (int64_t t = 0; t < cnt; t++) {
+        const float v = __builtin_fabsf(xi[f] - xk[(int64_t)L[t] * Kp + f]) * krecip[f];
+        if (v > 0.0f && v < vmin) vmin = v;
+        s += (double)v;
+      }
+      if (vmin == __builtin_inff()) continue;
+      int e;
+      (void)__builtin_frexpf(vmin, &e);  // vmin in [2^(e-1), 2^e): ulp 2^(e-24)
+      if (s >= __builtin_ldexp(1.0, e - 24 + 53)) m = 1;
+    }
+  }
+  if (m) any = 1;  // benign race: every writer stores 1
+  __syncthreads();
+  if (threadIdx.x == 0) matters[r] = any;
+}
+
 // temp[i - r_lo][f] = f32(update) (ReliefF.py:177-216): hit_sum and each miss
 // class's sum in float64 in argsort order, miss_sum += P_c / (1 - P_yi) * sum
 // in class order, update = -hit_sum / h_found + miss_sum / k.  Grid (Kp / 64
@@ -896,6 +942,16 @@ int relieff_row_keys(const float* xk, int64_t Kp, const float* krecip, const uin
   k_rf_ref_rowkeys<<<dim3((unsigned)nr, (unsigned)((n + 255) / 256)), 256, 0,
                      (hipStream_t)stream>>>(xk, Kp, krecip, kdisc, n_kept, rows, n, keys);
   return check("k_rf_ref_rowkeys");
+}
+
+int relieff_order_matters(const float* xk, int64_t Kp, const float* krecip,
+                          const uint8_t* kdisc, int64_t n_kept, const int32_t* rows, int64_t nr,
+                          const int32_t* dup, const int32_t* nbr, const int32_t* nfound,
+                          int64_t r_lo, int C, int64_t k, int32_t* matters, void* stream) {
+  if (nr <= 0) return FS_OK;
+  k_rf_ref_order_matters<<<(unsigned)nr, 256, 0, (hipStream_t)stream>>>(
+      xk, Kp, krecip, kdisc, n_kept, rows, dup, nbr, nfound, r_lo, C, k, matters);
+  return check("k_rf_ref_order_matters");
 }
 
 int relieff_update(const float* xk, int64_t Kp, const float* krecip, const uint8_t* kdisc,

@@ -1670,10 +1670,11 @@ static int relieff_select(Plan* g, const int64_t* dcc, int32_t* nbr, int32_t* nf
 
 // Reference order: the rows whose neighbour lists hold runs of equal keys
 // (dup, from relieff_order) get those runs in numba's quicksort order
-// (k_rf_ref_ties over the row's exact keys).  Continuous data has a few such
-// rows (cfg3: none to a handful); integer-valued layouts many, but an
-// all-discrete layout's 0 / 1 diffs add exactly in any order, so the caller
-// skips it (pc == 0).
+// (k_rf_ref_ties over the row's exact keys) -- when that order can change
+// the row's float64 sums at all (k_rf_ref_order_matters): continuous data
+// has many rows with float32 key ties among the k nearest, but diffs
+// within 2^29 of each other add exactly in any order; an all-discrete
+// layout's 0 / 1 diffs always do, so the caller skips it (pc == 0).
 static int relieff_ref_ties(Plan* g, int32_t* nbr, const int32_t* nfound, const int32_t* dup) {
   const Prepared& Q = g->P;
   const int C = Q.n_classes;
@@ -1689,9 +1690,40 @@ static int relieff_ref_ties(Plan* g, int32_t* nbr, const int32_t* nfound, const 
         tie_rows.push_back((int32_t)(g->r_lo + r));
         break;
       }
+  const size_t n_tied = tie_rows.size();
+  if (tie_rows.empty()) {
+    if (trace_on()) std::fprintf(stderr, "[fs_trace] relieff reference order: no tied keys\n");
+    return FS_OK;
+  }
+  int rc;
+  if (!test_hooks().rf_ref_replay) {
+    // the replay reads the row's n keys (n * n_kept diffs); first drop the
+    // rows whose sums come out the same in any order (k_rf_ref_order_matters,
+    // C * k * n_kept diffs) -- on continuous data, all of them
+    int32_t *crows = nullptr, *matters = nullptr;
+    g->alloc_target = 2;
+    if ((rc = dalloc(g, &crows, n_tied)) || (rc = dalloc(g, &matters, n_tied))) {
+      g->alloc_target = 0;
+      return rc;
+    }
+    g->alloc_target = 0;
+    FS_TRY(h2d(g, crows, tie_rows.data(), n_tied));
+    FS_TRY(refacc::relieff_order_matters(g->xk, g->Kp, g->krecip, g->kdisc, Q.n_kept, crows,
+                                         (int64_t)n_tied, dup, nbr, nfound, g->r_lo, C, k,
+                                         matters, g->stream));
+    std::vector<int32_t> hm(n_tied);
+    FS_HIP(hipMemcpyAsync(hm.data(), matters, n_tied * sizeof(int32_t), hipMemcpyDeviceToHost,
+                          g->stream));
+    FS_HIP(hipStreamSynchronize(g->stream));
+    size_t w = 0;
+    for (size_t r = 0; r < n_tied; r++)
+      if (hm[r]) tie_rows[w++] = tie_rows[r];
+    tie_rows.resize(w);
+  }
   if (trace_on())
-    std::fprintf(stderr, "[fs_trace] relieff reference order: %zu rows with tied keys\n",
-                 tie_rows.size());
+    std::fprintf(stderr,
+                 "[fs_trace] relieff reference order: %zu rows with tied keys, %zu replayed\n",
+                 n_tied, tie_rows.size());
   if (tie_rows.empty()) return FS_OK;
   const int64_t row_bytes = 8 * n + 4 * (int64_t)C * k;
   const int64_t batch = std::max<int64_t>(
@@ -1700,7 +1732,6 @@ static int relieff_ref_ties(Plan* g, int32_t* nbr, const int32_t* nfound, const 
   float* keys = nullptr;
   int* status = nullptr;
   g->alloc_target = 2;
-  int rc;
   if ((rc = dalloc(g, &drows, (size_t)batch)) || (rc = dalloc(g, &R, (size_t)(batch * n))) ||
       (rc = dalloc(g, &keys, (size_t)(batch * n))) ||
       (rc = dalloc(g, &ord, (size_t)(batch * C * k))) || (rc = dalloc(g, &status, 1))) {

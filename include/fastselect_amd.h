@@ -115,8 +115,8 @@ FS_API int fs_get_accumulation(void);
  * restores every default; the others are listed in INTEGRATION.md §4
  * ("ksplit", "q16", "sparse", "shards", "q16_guard_off", "thr_exact_all",
  * "exact_gather", "row_panel",
- * "rf_xlds", "rf_fcap", "ties_1w", "ties_coop", "colsort_bins12",
- * "colsort_global").  FS_EINVAL for an unknown name.  Not thread-safe
+ * "rf_xlds", "rf_fcap", "ties_1w", "ties_coop", "rf_ref_replay",
+ * "colsort_bins12", "colsort_global").  FS_EINVAL for an unknown name.  Not thread-safe
  * against concurrent scoring calls.
  */
 FS_API int fs_test_hook(const char* name, int64_t value);

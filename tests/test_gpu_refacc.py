@@ -181,6 +181,21 @@ def test_relieff_tied_neighbours_in_quicksort_order(F, oracle):
             oracle.relieff_scores(X, y, n_neighbors=3, discrete_limit=2))
 
 
+def test_relieff_tie_replay_only_where_order_matters(F, oracle, hooks):
+    """Rows whose tied neighbours' diffs add exactly in any order skip the
+    quicksort replay (k_rf_ref_order_matters): grid-valued continuous data,
+    ties on most rows, is the oracle's with the check and with the replay
+    forced on every tied row (rf_ref_replay)."""
+    rng = np.random.default_rng(8)
+    X = rng.integers(0, 12, (3000, 64)) / 11.0
+    y = rng.integers(0, 3, 3000)
+    ref = oracle.relieff_scores(X, y, n_neighbors=5, discrete_limit=2)
+    for replay in (0, 1):
+        hooks("rf_ref_replay", replay)
+        assert_bitexact(fit_ref(F.ReliefF(backend="gpu", n_neighbors=5, discrete_limit=2,
+                                          accumulation="reference"), X, y), ref)
+
+
 def test_relieff_panels_chain_the_column_sums(F, oracle, hooks):
     """A one-shot ReliefF scored in row panels (the row_panel test hook
     forces their height) continues one float32 column sum across the panels."""

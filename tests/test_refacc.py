@@ -142,6 +142,20 @@ def test_relieff_tied_neighbours_in_quicksort_order_cpu(oracle):
                     oracle.relieff_scores(X, y, n_neighbors=3, discrete_limit=2))
 
 
+def test_relieff_tie_replay_only_where_order_matters_cpu(oracle, hooks):
+    """Grid-valued continuous features tie neighbour keys on most rows, but
+    their diffs add exactly in any order, so the replay is skipped for them
+    (ref_order_matters): the result is the oracle's and the same as with the
+    replay forced on every tied row (the rf_ref_replay hook)."""
+    rng = np.random.default_rng(8)
+    X = rng.integers(0, 12, (600, 40)) / 11.0
+    y = rng.integers(0, 2, 600)
+    ref = oracle.relieff_scores(X, y, n_neighbors=5, discrete_limit=2)
+    assert_bitexact(fit_ref(ReliefF, X, y, backend="cpu", n_neighbors=5, discrete_limit=2), ref)
+    hooks("rf_ref_replay", 1)
+    assert_bitexact(fit_ref(ReliefF, X, y, backend="cpu", n_neighbors=5, discrete_limit=2), ref)
+
+
 def test_relieff_classes_and_small_class_cpu(oracle):
     rng = np.random.default_rng(3)
     X = np.exp(2.0 * rng.standard_normal((400, 60)))
