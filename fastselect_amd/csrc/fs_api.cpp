@@ -53,7 +53,7 @@ static int map_prep_rc(int rc) { return rc == 0 ? FS_OK : FS_EINVAL; }
 // takes 32-bit pass-1 operands.
 static int apply_accumulation(Prepared& P) {
   P.ref_accum = g_accum == FS_ACCUM_REFERENCE ? 1 : 0;
-  if (P.ref_accum && P.algo == ALGO_MULTISURF) P.no_q16 = 1;
+  if (P.ref_accum && P.algo == ALGO_MULTISURF && !test_hooks().ref_q16) P.no_q16 = 1;
   return FS_OK;
 }
 
@@ -145,6 +145,7 @@ int fs_test_hook(const char* name, int64_t value) {
   else if (k == "ties_1w") h.ties_1w = value;
   else if (k == "ties_coop") h.ties_coop = value;
   else if (k == "rf_ref_replay") h.rf_ref_replay = value;
+  else if (k == "ref_q16") h.ref_q16 = value;
   else if (k == "colsort_bins12") h.colsort_bins12 = value;
   else if (k == "colsort_global") h.colsort_global = value;
   else {
@@ -752,7 +753,7 @@ int fs_plan_set_features(fs_plan* pl, const int64_t* feat_idx, int64_t n_kept) {
   P.use_star = O.use_star;
   P.k_neighbors = O.k_neighbors;
   P.ref_accum = O.ref_accum;  // the plan's mode, fixed at creation
-  P.no_q16 = O.ref_accum && O.algo == ALGO_MULTISURF ? 1 : 0;
+  P.no_q16 = O.ref_accum && O.algo == ALGO_MULTISURF && !test_hooks().ref_q16 ? 1 : 0;
   if (gpu) {
     rc = gpu::plan_set_features(pl->g, P);
     if (rc != FS_OK) return rc;

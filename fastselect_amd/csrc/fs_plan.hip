@@ -46,7 +46,7 @@ static int choose_q16(const Prepared& P) {
   if (P.algo == ALGO_SURF || P.no_q16) return 0;
   // reference-order MultiSURF replays the reference's decisions: 32-bit
   // operands, whose thresholds need exact recomputation on a handful of rows
-  if (P.algo == ALGO_MULTISURF && P.ref_accum) return 0;
+  if (P.algo == ALGO_MULTISURF && P.ref_accum && !test_hooks().ref_q16) return 0;
   if (test_hooks().q16 >= 0) return test_hooks().q16 != 0 ? 1 : 0;
   const int64_t min_rows = P.algo == ALGO_RELIEFF ? kQ16MinRowsRF
                            : P.use_star           ? kQ16MinRowsMSStar
@@ -706,7 +706,10 @@ int plan_decision_guard(Plan* g, const double* rowstats, const double* counts,
   *risk = -1.0;
   *switched = 0;
   const Prepared& Q = g->P;
-  if (Q.algo != ALGO_MULTISURF || !g->use_q16 || Q.use_star || test_hooks().q16 >= 0) return FS_OK;
+  // reference order: every flagged row's threshold is exact, nothing to model
+  if (Q.algo != ALGO_MULTISURF || !g->use_q16 || Q.use_star || Q.ref_accum ||
+      test_hooks().q16 >= 0)
+    return FS_OK;
   // a focal-row slice holds only its rows' partial sums: as the one-shot
   // slice calls (multisurf_rows, a partial multisurf_run_devices), no check
   // (max |score| of a partial sum would inflate the risk)

@@ -115,7 +115,7 @@ FS_API int fs_get_accumulation(void);
  * restores every default; the others are listed in INTEGRATION.md §4
  * ("ksplit", "q16", "sparse", "shards", "q16_guard_off", "thr_exact_all",
  * "exact_gather", "row_panel",
- * "rf_xlds", "rf_fcap", "ties_1w", "ties_coop", "rf_ref_replay",
+ * "rf_xlds", "rf_fcap", "ties_1w", "ties_coop", "rf_ref_replay", "ref_q16",
  * "colsort_bins12", "colsort_global").  FS_EINVAL for an unknown name.  Not thread-safe
  * against concurrent scoring calls.
  */
