@@ -408,6 +408,7 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
     ms_per_step = float(t.item()) / args.steps * 1e3
     roofline = None
     q16 = False
+    surf_int = False
     if on_gpu:
         nb = (n + 127) // 128
         b0, b1 = rows[0] // 128, (rows[1] + 127) // 128
@@ -416,8 +417,11 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
         tiles = sum(1 for a in range(nb) for b in range(a, nb) if b0 <= a < b1 or b0 <= b < b1)
         pairs = min(tiles * 128.0 * 128.0, n * (n - 1) / 2.0)
         k_ms = float(np.mean(kms[0]))
-        name = "k_dist" if algo == "relieff" else "k_dist_f64"
-        peak = VALU_PEAK_TFLOPS if algo == "relieff" else VALU_F64_PEAK_TFLOPS
+        # SURF: integer distances resolved to the reference's float32 values
+        # (fs_surfint.hip) unless the plan's calibration kept float64 ones
+        surf_int = algo == "surf" and not plan.calibration()["surf_f64"]
+        name = "k_dist" if algo == "relieff" or surf_int else "k_dist_f64"
+        peak = VALU_PEAK_TFLOPS if algo == "relieff" or surf_int else VALU_F64_PEAK_TFLOPS
         # ReliefF's k_dist on 16-bit operands (n >= 4096): one v_sad_u16 per 2
         # PFE, one issue slot per PFE = 2 FMA-equivalent FLOPs (32-bit: 4)
         q16 = algo == "relieff" and bool(plan.calibration()["q16"])
@@ -441,6 +445,13 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
                 "PFE = 2 FMA-equivalent FLOPs against the fp32 vector peak" if q16 else
                 "k_dist on 32-bit operands: one half-rate v_sad_u32 per PFE = 4 FMA-equivalent "
                 "FLOPs against the fp32 vector peak")
+        elif surf_int:
+            roofline["kernel_ms"]["surf_resolve"] = float(np.mean(kms[2]))
+            roofline["refined_pairs"] = int(plan.info()[2])
+            roofline["peak_note"] = (
+                "k_dist on 32-bit operands: one half-rate v_sad_u32 per PFE = 4 FMA-equivalent "
+                "FLOPs against the fp32 vector peak; surf_resolve: the row means and the pairs "
+                "whose float32 distance they or a decision depend on, recomputed exactly")
         else:
             roofline["peak_note"] = ("float64 vector peak (AMD MI355X figure, half the fp32 rate); "
                                      "2 v_add_f64 per PFE, each priced as one FMA")
@@ -460,7 +471,7 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
                 rplan.score(sums.data_ptr())
             sync()
             refacc = {"ms_per_step": (time.perf_counter() - t_r) / ks * 1e3, "steps": ks,
-                      "kernel_ms": {"k_dist" if algo == "relieff" else "k_dist_f64":
+                      "kernel_ms": {"k_dist" if algo == "relieff" or surf_int else "k_dist_f64":
                                     rplan.kernel_ms(0),
                                     "selection_to_scores" if algo == "relieff"
                                     else "masks_and_chains": rplan.kernel_ms(1)},
@@ -477,7 +488,10 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "strong",
             "vs_baseline": None,
             "dtype": (f"{'u16' if q16 else 'u32'} pass 1 (exact keys near the k-th), fp32 / fp64 "
-                      "update" if algo == "relieff" else "fp64 distances, fp32 pair sums"),
+                      "update" if algo == "relieff" else
+                      "u32 pass 1 (the reference's fp32 distances resolved exactly: fp64 "
+                      "recomputation where a row sum or decision depends on one), fp32 pair sums"
+                      if surf_int else "fp64 distances, fp32 pair sums"),
             "data": f"synthetic make_classification(n_informative=20, n_redundant={cfg['red']}, "
                     f"random_state=42)",
             "config": {"workload": f"{name} n={n} p={p} (BASELINE configs[{cfg['idx']}])",

@@ -637,8 +637,8 @@ class Plan:
         m = _lib.fs_plan_calibration_ex(self._h, v, 8)
         check(min(m, 0))
         return {"q16": bool(v[0]), "rms": v[1], "max": v[2], "model_sigma": v[3],
-                "band_vs_model": v[4], "guard": bool(v[5]), "row_guard": v[5] == 2.0,
-                "row_bias_vs_limit": v[6], "SC": v[7]}
+                "band_vs_model": v[4], "guard": v[5] in (1.0, 2.0), "row_guard": v[5] == 2.0,
+                "surf_f64": v[5] == 3.0, "row_bias_vs_limit": v[6], "SC": v[7]}
 
     def weighted_pairs(self) -> int:
         """Owned pairs with a non-zero weight in the last pass 2 (-1: not counted)."""

@@ -173,7 +173,8 @@ struct Plan {
   float* epsT = nullptr;
   double* corr = nullptr;
   double* corr_part = nullptr;  // [rowcorr_slices][n_pad] k_rowcorr slice partials
-  double* xT64 = nullptr;      // SURF: float64 feature-major operands
+  double* xT64 = nullptr;      // SURF: float64 feature-major operands (the float64 route)
+  bool surf_int = false;        // SURF: integer distances resolved to float32 (fs_surfint.hip)
   double* D = nullptr;
   int tiled = 0;                // D in the tiled layout (MultiSURF; d_at)
   int64_t dplane = 0;           // doubles of one distance plane (D, each Dpart)
@@ -308,6 +309,9 @@ int row_guard(Plan* g);
 int apply_operand_width(Plan* g);
 int run_quantize_dist(Plan* g);
 int plan_score_surf(Plan* g, double* sums_dev);
+// fs_surfint.hip: after k_dist on a SURF plan's integer operands, the focal
+// rows' means into thr and every stored distance as its float32 value
+int surf_resolve(Plan* g);
 // fs_pass2.hip
 int shard_segments(Plan* g);
 int run_weights(Plan* g, const double* counts, int algo, double inv_sc);

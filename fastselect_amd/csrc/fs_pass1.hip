@@ -679,7 +679,9 @@ __global__ __launch_bounds__(64) void k_surf_avg(const double* __restrict__ D, i
 // Band calibration (calibrate_band): for each sampled pair, the quantised
 // distance's error against the reference's arithmetic, err = sum over the
 // continuous kept features of |q_i - q_j| - SC * f32(|x_i - x_j| * recip),
-// for the 16-bit scale (.x) and the 32-bit scale (.y).  q is formed exactly
+// for the 16-bit scale (.x) and the 32-bit scale (.y) -- SURF (scl64): the
+// float64 terms |x_i - x_j| * recip, .x the continuous part of the distance
+// (the float32 rounding the band must resolve, surf_int).  q is formed exactly
 // as k_quantize forms it; discrete features contribute no error.  One wave
 // per pair, fixed-order reduction (every rank computes the same values).
 template <typename T>
@@ -687,7 +689,8 @@ __global__ __launch_bounds__(256) void k_calib(
     const T* __restrict__ x, int64_t p_in, int64_t pc, const int64_t* __restrict__ src_col,
     const double* __restrict__ off, const double* __restrict__ qs16,
     const double* __restrict__ qs32, const float* __restrict__ scl32, double sc16, double sc32,
-    const int2* __restrict__ pairs, int64_t npairs, double2* __restrict__ err) {
+    const double* __restrict__ scl64, const int2* __restrict__ pairs, int64_t npairs,
+    double2* __restrict__ err) {
   const int lane = threadIdx.x & 63;
   const int64_t k = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
   if (k >= npairs) return;
@@ -703,6 +706,12 @@ __global__ __launch_bounds__(256) void k_calib(
     const uint32_t qb16 = (uint32_t)__dadd_rn(__dmul_rn(ub, qs16[c]), 0.5);
     const uint32_t qa32 = (uint32_t)__dadd_rn(__dmul_rn(ua, qs32[c]), 0.5);
     const uint32_t qb32 = (uint32_t)__dadd_rn(__dmul_rn(ub, qs32[c]), 0.5);
+    if (scl64) {  // SURF: float64 terms (SURF.py:156); .x = the distance itself
+      const double ref = __builtin_fabs(a - b) * scl64[c];
+      e16 += ref;
+      e32 += (qa32 > qb32 ? (double)(qa32 - qb32) : (double)(qb32 - qa32)) - sc32 * ref;
+      continue;
+    }
     const double ref = (double)(__builtin_fabsf((float)a - (float)b) * scl32[c]);
     e16 += (qa16 > qb16 ? (double)(qa16 - qb16) : (double)(qb16 - qa16)) - sc16 * ref;
     e32 += (qa32 > qb32 ? (double)(qa32 - qb32) : (double)(qb32 - qa32)) - sc32 * ref;
@@ -779,6 +788,60 @@ int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats) {
 // sigma/2 < 12 sigma), so ordinary data keeps its refinement cost.
 constexpr double kCoherence = 2.0;
 
+// SURF (surf_int, fs_surfint.hip): the band of y = D_q / SC from the sampled
+// 32-bit errors (.y), and the integer route only while the band stays below
+// one float32 ulp of the shorter sampled distances (.x, their 10th
+// percentile): beyond it most pairs keep several candidates and the row
+// sums stop at ~band / ulp times more pairs, so coherent rounding
+// (duplicated or same-grid columns) and few features (the band grows as
+// sqrt(pc), the ulp as pc) keep the float64 distances.  The surf_f64 test
+// hook forces either route (both give the same float32 distances).
+constexpr double kSurfIntMinWork = 5e9;
+static int surf_band(Plan* g, const std::vector<double2>& err) {
+  Prepared& Q = g->P;
+  double ss = 0.0, mx = 0.0;
+  std::vector<double> dist;
+  dist.reserve(err.size());
+  for (const double2& e : err) {
+    ss += e.y * e.y;
+    mx = std::max(mx, std::fabs(e.y));
+    dist.push_back(e.x);
+  }
+  const double rms = std::sqrt(ss / (double)std::max<size_t>(err.size(), 1));
+  Q.amb_delta = calibrated_delta(Q.amb_delta_model, Q.SC, rms, mx);
+  double ulp = 0.0;
+  if (!dist.empty()) {
+    const size_t k = dist.size() / 10;
+    std::nth_element(dist.begin(), dist.begin() + k, dist.end());
+    const float d10 = (float)dist[k];
+    if (d10 > 0.0f) {
+      int e = 0;
+      (void)std::frexp(d10, &e);
+      ulp = std::ldexp(1.0, e - 24);
+    }
+  }
+  // and only where pass 1 is worth the rounds: ~2x the float64 kernel's rate
+  // saves ~0.35 ms per 1e10 pair-features, a round of the row sums costs
+  // ~0.05 ms
+  const double work = 0.5 * (double)Q.n * (double)Q.n * (double)Q.pc;
+  if (test_hooks().surf_f64 < 0 && !(Q.amb_delta <= ulp && work >= kSurfIntMinWork))
+    g->surf_int = false;
+  g->calib[0] = 0.0;
+  g->calib[5] = g->surf_int ? 0.0 : 3.0;
+  g->calib[1] = rms;
+  g->calib[2] = mx;
+  g->calib[4] = Q.amb_delta / Q.amb_delta_model;
+  if (trace_on()) {
+    char msg[256];
+    snprintf(msg, sizeof msg,
+             "calibrate (SURF): rms32 %.1f max32 %.1f model sigma %.1f, band %.3g, ulp %.3g -> %s",
+             rms, mx, g->calib[3], Q.amb_delta, ulp,
+             g->surf_int ? "integer distances" : "float64 distances");
+    trace_mark(msg);
+  }
+  return FS_OK;
+}
+
 int calibrate_band(Plan* g) {
   Prepared& Q = g->P;
   g->calib[0] = Q.q16;
@@ -787,7 +850,10 @@ int calibrate_band(Plan* g) {
   g->calib[4] = 1.0;
   g->calib[5] = 0.0;
   g->calib[6] = 0.0;
-  if (Q.algo == ALGO_SURF || Q.pc == 0 || Q.n < 2) return FS_OK;
+  const bool surf = Q.algo == ALGO_SURF;
+  g->surf_int = surf && test_hooks().surf_f64 != 1 && Q.n >= 2;
+  if (surf && !g->surf_int) g->calib[5] = 3.0;
+  if (Q.pc == 0 || Q.n < 2) return FS_OK;
   const int64_t all_pairs = Q.n * (Q.n - 1) / 2;
   const int64_t S = std::min<int64_t>(kCalibPairs, all_pairs);
   std::vector<std::pair<int64_t, int64_t>> smp;
@@ -823,11 +889,11 @@ int calibrate_band(Plan* g) {
     if (g->x_is_f64)
       k_calib<double><<<grid, 256, 0, g->stream>>>((const double*)g->x, Q.p_in, Q.pc, g->src_col,
                                                    g->off, dqs, dqs + Q.PW, g->scl32, sc[0],
-                                                   sc[1], dpr, S, derr);
+                                                   sc[1], surf ? g->scl : nullptr, dpr, S, derr);
     else
       k_calib<float><<<grid, 256, 0, g->stream>>>((const float*)g->x, Q.p_in, Q.pc, g->src_col,
                                                   g->off, dqs, dqs + Q.PW, g->scl32, sc[0],
-                                                  sc[1], dpr, S, derr);
+                                                  sc[1], nullptr, dpr, S, derr);
     rc = launch_check("k_calib");
   }
   if (!rc && (hipMemcpyAsync(err.data(), derr, sizeof(double2) * S, hipMemcpyDeviceToHost,
@@ -842,6 +908,7 @@ int calibrate_band(Plan* g) {
     if (rc == FS_EHIP) set_error("band calibration: HIP call failed");
     return rc;
   }
+  if (surf) return surf_band(g, err);
   double ss[2] = {0.0, 0.0}, mx[2] = {0.0, 0.0};
   for (const double2& e : err) {
     const double v[2] = {e.x, e.y};
@@ -1019,7 +1086,7 @@ int run_quantize_dist(Plan* g) {
   const Prepared& Q = g->P;
   FS_HIP(hipSetDevice(g->device));
   dim3 gq((unsigned)(Q.PW / 64), (unsigned)(Q.n_pad / 64));
-  if (Q.algo == ALGO_SURF) {
+  if (Q.algo == ALGO_SURF && !g->surf_int) {
     k_quantize_f64<<<gq, 256, 0, g->stream>>>((const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW,
                                               Q.pc, g->src_col, g->off, g->scl, g->dtab_off,
                                               g->dtab, g->xT64, g->xs);
@@ -1033,20 +1100,26 @@ int run_quantize_dist(Plan* g) {
     }
     return FS_OK;
   }
+  // SURF's integer route (fs_surfint.hip) quantises as MultiSURF does: no
+  // mean correction, no K-split, float64 X
   const bool reuse = g->corr_ready && Q.algo == ALGO_MULTISURF;
   g->corr_ready = false;  // later steps quantise again (the terms overwrote epsT)
+  // quantisation errors for the mean correction (MultiSURF; ReliefF keeps
+  // them unused), none on SURF's integer route (no epsT)
+  const int64_t eps_lo = Q.algo == ALGO_SURF ? 0 : g->c_lo;
+  const int64_t eps_hi = Q.algo == ALGO_SURF ? 0 : g->c_hi;
   if (reuse) {
     // the row guard's operands and correction (row_guard): nothing to redo
     FS_HIP(hipEventRecord(g->ev_join, g->stream));
   } else if (g->x_is_f64) {
     k_quantize<double><<<gq, 256, 0, g->stream>>>(
         (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
-        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, g->c_lo, g->c_hi, g->xqT, g->xs,
+        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, eps_lo, eps_hi, g->xqT, g->xs,
         g->epsT);
   } else {
     k_quantize<float><<<gq, 256, 0, g->stream>>>(
         (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
-        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, g->c_lo, g->c_hi, g->xqT, g->xs,
+        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, eps_lo, eps_hi, g->xqT, g->xs,
         g->epsT);
   }
   if (!reuse) FS_TRY(launch_check("k_quantize"));
@@ -1121,8 +1194,13 @@ int plan_pass1(Plan* g, double* rowstats) {
 // SURF score sums of the plan's focal rows into sums_dev[n_kept].
 int plan_score_surf(Plan* g, double* sums_dev) {
   const Prepared& Q = g->P;
-  int rc = run_quantize_dist(g);  // float64 distances, real units
-  if (rc == FS_OK && g->r_hi > g->r_lo) {
+  int rc = run_quantize_dist(g);  // integer or float64 distances
+  if (rc == FS_OK && g->surf_int) {
+    // the means, then D as float32 values in real units (plan_kernel_ms 2)
+    FS_HIP(hipEventRecord(g->ev[4], g->stream));
+    rc = surf_resolve(g);
+    FS_HIP(hipEventRecord(g->ev[5], g->stream));
+  } else if (rc == FS_OK && g->r_hi > g->r_lo) {
     k_surf_avg<<<(unsigned)((g->r_hi - g->r_lo + 63) / 64), 64, 0, g->stream>>>(
         g->D, Q.n, Q.n_pad, 1.0, g->r_lo, g->r_hi, g->thr);
     rc = launch_check("k_surf_avg");

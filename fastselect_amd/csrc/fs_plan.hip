@@ -197,7 +197,7 @@ int plan_layout(Plan* g) {
       // last row when PW is narrower than the block
       (rc = dalloc(g, &g->xs, (size_t)(Q.n_pad + 2) * Q.PW + kXsSlack))) {
   } else if (Q.algo == ALGO_SURF) {
-    rc = dalloc(g, &g->xT64, (size_t)Q.PW * Q.n_pad);
+    // its operands follow the route the calibration picks (below)
   } else if ((rc = dalloc(g, &g->xqT, (size_t)Q.PW * Q.n_pad)) == FS_OK) {
     rc = dalloc(g, &g->epsT, (size_t)Q.PW * Q.n_pad);
   }
@@ -221,6 +221,13 @@ int plan_layout(Plan* g) {
   if ((rc = size_exact_rows(g))) return rc;
   if (Q.ref_accum && (rc = ref_layout(g))) return rc;
   if ((rc = calibrate_band(g))) return rc;
+  if (Q.algo == ALGO_SURF) {  // integer (u32) or float64 feature-major operands
+    g->alloc_target = 1;
+    rc = g->surf_int ? dalloc(g, &g->xqT, (size_t)Q.PW * Q.n_pad)
+                     : dalloc(g, &g->xT64, (size_t)Q.PW * Q.n_pad);
+    g->alloc_target = 0;
+    if (rc) return rc;
+  }
   if ((rc = row_guard(g))) return rc;
   if (g->calib[5] != 0.0 && (rc = apply_operand_width(g))) return rc;
   FS_HIP(hipStreamSynchronize(g->stream));

@@ -231,6 +231,8 @@ int set_integer_scale(Prepared& P, int q16) {
   // add up coherently (duplicated, collinear or same-grid columns).
   const double pcd = (double)P.pc;
   P.amb_delta = 12.0 * std::sqrt(pcd / 6.0 + 1.0) / sc + 4.0e-7 * std::sqrt(pcd);
+  // SURF's terms are float64 (SURF.py:156): the quantisation error alone
+  if (P.algo == ALGO_SURF) P.amb_delta = 12.0 * std::sqrt(pcd / 6.0 + 1.0) / sc;
   P.amb_delta_model = P.amb_delta;
   P.ranges_ready = 1;
   return 0;

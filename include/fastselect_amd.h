@@ -115,7 +115,7 @@ FS_API int fs_get_accumulation(void);
  * restores every default; the others are listed in INTEGRATION.md §4
  * ("ksplit", "q16", "sparse", "shards", "q16_guard_off", "thr_exact_all",
  * "exact_gather", "row_panel",
- * "rf_xlds", "rf_fcap", "ties_1w", "ties_coop", "rf_ref_replay", "ref_q16",
+ * "rf_xlds", "rf_fcap", "ties_1w", "ties_coop", "rf_ref_replay", "ref_q16", "surf_f64",
  * "colsort_bins12", "colsort_global").  FS_EINVAL for an unknown name.  Not thread-safe
  * against concurrent scoring calls.
  */
@@ -486,7 +486,10 @@ FS_API int fs_plan_info(const fs_plan* plan, int64_t* owned_tiles, double* pair_
  * sqrt(pc/6 + 1), [4] band / model band, [5] 1 if the coherence guard turned
  * 16-bit operands off, 2 if the per-row guard did (a row whose mean pass-1
  * error, measured by the mean correction, exceeds 12 standard deviations of
- * independent rounding).  fs_plan_calibration_ex writes min(n_out, 8)
+ * independent rounding); SURF plans (32-bit operands against its float64
+ * terms, fs_surfint.hip): [5] 0 on integer distances, 3 on float64 ones (the
+ * band above one float32 ulp of the shorter sampled distances, a small
+ * problem, or the surf_f64 test hook).  fs_plan_calibration_ex writes min(n_out, 8)
  * values -- the six above, then [6] that row guard's largest row bias over
  * its limit (0 when it did not run) and [7] SC, the integer units per
  * scaled-diff unit of pass 1 (the row statistics of fs_plan_pass1 are in
