@@ -15,11 +15,11 @@
 // near a float32 rounding midpoint.  Such a pair matters only where the
 // choice changes something the reference computes from it:
 //   * a row's float32 running sum: k_surf_avg_int adds both candidates and
-//     stops the row at the first pair where the two sums differ (about
-//     sum_k ulp(D) / ulp(s_k) ~ 0.07 * ln(n) of them per row at cfg5); that
-//     pair's distance is recomputed in the reference's arithmetic
-//     (k_surf_exact_pairs) and the row is summed again, until every row
-//     finishes -- a handful of rounds;
+//     lists the pairs where the two sums differ (about sum_k 2 b / ulp(s_k),
+//     ~2.4 per row at cfg5), following both sums past each; the listed
+//     distances are recomputed in the reference's arithmetic
+//     (k_surf_exact_pairs) and those rows summed again, until every row
+//     finishes without one -- 2 to 4 rounds;
 //   * a near / far decision: k_surf_decisions lists the pairs whose two
 //     candidates fall on both sides of a focal endpoint's mean;
 // then k_surf_normalize writes every distance as its float32 value (the
@@ -51,20 +51,26 @@ __device__ __forceinline__ void surf_candidates(double d, bool self, double inv_
 
 // Row means of the focal rows rows[0..nr): avg[i] = the float32 sequential
 // sum of row i's float32 distances over j (self included, 0), / (n - 1) in
-// float64 (SURF.py:162-163), as k_surf_avg.  A workgroup takes 64 rows: its
-// 256 threads stage the rows' next 64-column block as candidate pairs in LDS
-// (16 coalesced loads per thread, all in flight) while wave 0 adds the
-// previous block in j order, lane r along row r (double-buffered; the scan
-// is latency-bound, ~1 us a block).  Where the two candidates give different
-// running sums the row stops: (i, j) goes to pairs[slot] and i to
-// next_rows[slot] (slot from *next_count), for refinement and the next round.
-constexpr int kAvgCols = 64;
+// float64 (SURF.py:162-163), as k_surf_avg.  A workgroup takes 64 rows and
+// walks them in blocks of kAvgCols columns: every thread loads its 32
+// distances of the next block into registers, wave 0 adds the current block
+// from LDS in j order (lane r along row r) while those loads are in flight,
+// then the next block's candidate pairs go to the other LDS buffer -- the
+// scan is bound by load latency per block, so the blocks are wide.  Where
+// the two candidates give different running sums the row stops: (i, j) goes
+// to the pair list (counts[1]) for refinement and i to next_rows (counts[0])
+// for the next round.  (Following both sums past such a pair, up to 3 pairs
+// a round, took 5 rounds instead of 10 at cfg5 but tripled the cost of a
+// round: the add chain is issue-bound, one wave per SIMD.)
+constexpr int kAvgCols = 128;
+constexpr int kAvgPairsPerRound = 1;
+constexpr int kAvgPer = 64 * kAvgCols / 256;  // distances a thread stages per block
 __global__ __launch_bounds__(256) void k_surf_avg_int(const double* __restrict__ D, int64_t n,
                                                       int64_t n_pad, double inv_sc, double band,
                                                       const int32_t* __restrict__ rows, int64_t nr,
                                                       double* __restrict__ avg,
                                                       int32_t* __restrict__ next_rows,
-                                                      int32_t* __restrict__ next_count,
+                                                      int32_t* __restrict__ counts,
                                                       int2* __restrict__ pairs) {
   __shared__ float lo_s[2][64][kAvgCols + 1], hi_s[2][64][kAvgCols + 1];
   __shared__ int32_t rid[64];
@@ -74,44 +80,60 @@ __global__ __launch_bounds__(256) void k_surf_avg_int(const double* __restrict__
   const int nrows = nr - base < 64 ? (int)(nr - base) : 64;
   if (tid < 64) rid[tid] = tid < nrows ? rows[base + tid] : 0;
   __syncthreads();
-  // thread (wave w, lane l) stages rows w, w + 4, ..., w + 60 at column l
-  auto stage = [&](int buf, int64_t j0) {
-    const int64_t j = j0 + lane;
-    double d[16];
+  // thread (wave w, lane l) stages rows w, w + 4, ..., w + 60 at columns l
+  // and l + 64 of the block
+  double d[kAvgPer];
+  auto load = [&](int64_t j0) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const int r = wave + 4 * k;
+    for (int k = 0; k < kAvgPer; k++) {
+      const int r = wave + 4 * (k >> 1);
+      const int64_t j = j0 + lane + 64 * (k & 1);
       d[k] = (r < nrows && j < n) ? D[(int64_t)rid[r] * n_pad + j] : 0.0;
     }
+  };
+  auto put = [&](int buf, int64_t j0) {
 #pragma unroll
-    for (int k = 0; k < 16; k++) {
-      const int r = wave + 4 * k;
+    for (int k = 0; k < kAvgPer; k++) {
+      const int r = wave + 4 * (k >> 1);
+      const int c = lane + 64 * (k & 1);
+      const int64_t j = j0 + c;
       float lo = 0.0f, hi = 0.0f;
       if (r < nrows && j < n) surf_candidates(d[k], j == rid[r], inv_sc, band, lo, hi);
-      lo_s[buf][r][lane] = lo;
-      hi_s[buf][r][lane] = hi;
+      lo_s[buf][r][c] = lo;
+      hi_s[buf][r][c] = hi;
     }
   };
   const int64_t i = rid[lane];
   bool live = wave == 0 && lane < nrows;
   float s = 0.0f;
-  stage(0, 0);
+  load(0);
+  put(0, 0);
   __syncthreads();
   int buf = 0;
   for (int64_t j0 = 0, it = 0; j0 < n; j0 += kAvgCols, it++) {
-    if (j0 + kAvgCols < n) stage(buf ^ 1, j0 + kAvgCols);
+    const bool next = j0 + kAvgCols < n;
+    if (next) load(j0 + kAvgCols);
     if (wave == 0) {
       const int cnt = n - j0 < kAvgCols ? (int)(n - j0) : kAvgCols;
-      if (live) {
-        for (int c = 0; c < cnt; c++) {
-          const float lo = lo_s[buf][lane][c], hi = hi_s[buf][lane][c];
-          const float a = s + lo;
-          if (hi != lo && s + hi != a) {  // the sum depends on which one it is
-            const int slot = atomicAdd(next_count, 1);
-            next_rows[slot] = (int32_t)i;
-            pairs[slot] = make_int2((int)i, (int)(j0 + c));
-            live = false;
-            break;
+      // 8 columns' candidates read ahead of the dependent float32 adds; per
+      // column two adds and a compare, the stop taken by a uniform branch
+      for (int c0 = 0; c0 < cnt && __any(live); c0 += 8) {
+        float lo[8], hi[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          lo[u] = lo_s[buf][lane][c0 + u];  // c0 + u < kAvgCols: inside the padded row
+          hi[u] = hi_s[buf][lane][c0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const float a = s + lo[u];
+          const bool crit = live && c0 + u < cnt && a != s + hi[u];
+          if (__any(crit)) {
+            if (crit) {  // the sum depends on which one it is
+              pairs[atomicAdd(&counts[1], 1)] = make_int2((int)i, (int)(j0 + c0 + u));
+              next_rows[atomicAdd(&counts[0], 1)] = (int32_t)i;
+              live = false;
+            }
           }
           s = a;
         }
@@ -119,6 +141,7 @@ __global__ __launch_bounds__(256) void k_surf_avg_int(const double* __restrict__
       const bool more = __any(live);
       if (lane == 0) any_live[it & 1] = more ? 1 : 0;
     }
+    if (next) put(buf ^ 1, j0 + kAvgCols);
     __syncthreads();
     if (!any_live[it & 1]) break;  // every row stopped: the workgroup leaves together
     buf ^= 1;
@@ -180,11 +203,27 @@ __global__ __launch_bounds__(256) void k_surf_exact_pairs(
   const int2 pr = pairs[k];
   const double* xi = x + (int64_t)pr.x * p_in;
   const double* xj = x + (int64_t)pr.y * p_in;
-  double acc = 0.0;
-  for (int64_t c = lane; c < pc; c += 64) {
-    const int64_t col = src_col[c];
-    acc += __builtin_fabs(xi[col] - xj[col]) * scl[c];
+  // four chains (lane strides of 256 features), loads of all four in flight;
+  // added in a fixed order below
+  double a4[4] = {0.0, 0.0, 0.0, 0.0};
+  int64_t c = lane;
+  for (; c + 192 < pc; c += 256) {
+    double u[4], v[4], w[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int64_t col = src_col[c + 64 * q];
+      u[q] = xi[col];
+      v[q] = xj[col];
+      w[q] = scl[c + 64 * q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) a4[q] += __builtin_fabs(u[q] - v[q]) * w[q];
   }
+  for (; c < pc; c += 64) {
+    const int64_t col = src_col[c];
+    a4[0] += __builtin_fabs(xi[col] - xj[col]) * scl[c];
+  }
+  double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
   for (int64_t c = PC + lane; c < PC + pd; c += 64) {
     const int64_t col = src_col[c];
     acc += xi[col] != xj[col] ? 1.0 : 0.0;
@@ -214,13 +253,13 @@ int surf_resolve(Plan* g) {
   g->alloc_target = 2;
   int rc;
   if ((rc = dalloc(g, &ra, (size_t)rows)) || (rc = dalloc(g, &rb, (size_t)rows)) ||
-      (rc = dalloc(g, &cnt, 1))) {
+      (rc = dalloc(g, &cnt, 2))) {
     g->alloc_target = 0;
     return rc;
   }
   g->alloc_target = 0;
-  if (g->list_cap < rows) {  // one stopped row, one pair (the list lives with the plan)
-    g->list_cap = rows;
+  if (g->list_cap < kAvgPairsPerRound * rows) {  // the list lives with the plan
+    g->list_cap = kAvgPairsPerRound * rows;
     FS_TRY(dalloc(g, &g->list, (size_t)g->list_cap));
   }
   {
@@ -232,18 +271,18 @@ int surf_resolve(Plan* g) {
   // the row means, refining the pairs that decide a running sum
   int64_t cur = rows, rounds = 0, refined_sum = 0;
   while (cur > 0) {
-    FS_HIP(hipMemsetAsync(cnt, 0, sizeof(int32_t), g->stream));
+    FS_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), g->stream));
     k_surf_avg_int<<<(unsigned)((cur + 63) / 64), 256, 0, g->stream>>>(
         g->D, n, Q.n_pad, inv_sc, band, ra, cur, g->thr, rb, cnt, g->list);
     FS_TRY(launch_check("k_surf_avg_int"));
-    int32_t next = 0;
-    FS_HIP(hipMemcpyAsync(&next, cnt, sizeof(next), hipMemcpyDeviceToHost, g->stream));
+    int32_t next[2] = {0, 0};
+    FS_HIP(hipMemcpyAsync(next, cnt, sizeof(next), hipMemcpyDeviceToHost, g->stream));
     FS_HIP(hipStreamSynchronize(g->stream));
-    FS_TRY(exact_pairs(g, next));
+    FS_TRY(exact_pairs(g, next[1]));
     std::swap(ra, rb);
-    cur = next;
-    refined_sum += next;
-    if (++rounds > n) {  // every round settles one pair of each row it stops
+    cur = next[0];
+    refined_sum += next[1];
+    if (++rounds > n) {  // every round settles a pair of each row it sends on
       set_error("SURF distances: row means did not settle");
       return FS_EHIP;
     }
