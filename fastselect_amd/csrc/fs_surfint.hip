@@ -52,11 +52,11 @@ __device__ __forceinline__ void surf_candidates(double d, bool self, double inv_
 // Row means of the focal rows rows[0..nr): avg[i] = the float32 sequential
 // sum of row i's float32 distances over j (self included, 0), / (n - 1) in
 // float64 (SURF.py:162-163), as k_surf_avg.  A workgroup takes 64 rows and
-// walks them in blocks of kAvgCols columns: every thread loads its 32
-// distances of the next block into registers, wave 0 adds the current block
-// from LDS in j order (lane r along row r) while those loads are in flight,
-// then the next block's candidate pairs go to the other LDS buffer -- the
-// scan is bound by load latency per block, so the blocks are wide.  Where
+// walks them in blocks of kAvgCols columns: wave 0 adds the current block
+// from LDS in j order (lane r along row r) while waves 1-4 turn the next
+// block into candidate pairs in the other LDS buffer from registers loaded
+// a block earlier -- the dependent float32 adds of wave 0 are the round's
+// critical path, so nothing else runs on that wave.  Where
 // the two candidates give different running sums the row stops: (i, j) goes
 // to the pair list (counts[1]) for refinement and i to next_rows (counts[0])
 // for the next round.  (Following both sums past such a pair, up to 3 pairs
@@ -64,8 +64,8 @@ __device__ __forceinline__ void surf_candidates(double d, bool self, double inv_
 // round: the add chain is issue-bound, one wave per SIMD.)
 constexpr int kAvgCols = 128;
 constexpr int kAvgPairsPerRound = 1;
-constexpr int kAvgPer = 64 * kAvgCols / 256;  // distances a thread stages per block
-__global__ __launch_bounds__(256) void k_surf_avg_int(const double* __restrict__ D, int64_t n,
+constexpr int kAvgPer = 64 * kAvgCols / 256;  // distances a staging thread stages per block
+__global__ __launch_bounds__(320) void k_surf_avg_int(const double* __restrict__ D, int64_t n,
                                                       int64_t n_pad, double inv_sc, double band,
                                                       const int32_t* __restrict__ rows, int64_t nr,
                                                       double* __restrict__ avg,
@@ -75,30 +75,39 @@ __global__ __launch_bounds__(256) void k_surf_avg_int(const double* __restrict__
   __shared__ float lo_s[2][64][kAvgCols + 1], hi_s[2][64][kAvgCols + 1];
   __shared__ int32_t rid[64];
   __shared__ int any_live[2];  // by block parity: a slot is rewritten only after the next barrier
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave 0 sums; waves 1-4 stage (sw = 0..3)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, sw = wave - 1;
   const int64_t base = (int64_t)blockIdx.x * 64;
   const int nrows = nr - base < 64 ? (int)(nr - base) : 64;
-  if (tid < 64) rid[tid] = tid < nrows ? rows[base + tid] : 0;
+  if (tid < 64) rid[tid] = rows[base + (tid < nrows ? tid : 0)];  // padding: a stored row
   __syncthreads();
   // thread (wave w, lane l) stages rows w, w + 4, ..., w + 60 at columns l
-  // and l + 64 of the block
-  double d[kAvgPer];
-  auto load = [&](int64_t j0) {
+  // and l + 64 of the block: the 16 row pointers and indices live in
+  // registers (padding rows repeat the list's first row; never summed)
+  constexpr int kRowsPer = kAvgPer / 2;
+  const double* rowp[kRowsPer];
+  int32_t rowi[kRowsPer];
 #pragma unroll
-    for (int k = 0; k < kAvgPer; k++) {
-      const int r = wave + 4 * (k >> 1);
-      const int64_t j = j0 + lane + 64 * (k & 1);
-      d[k] = (r < nrows && j < n) ? D[(int64_t)rid[r] * n_pad + j] : 0.0;
-    }
+  for (int q = 0; q < kRowsPer; q++) {
+    rowi[q] = rid[(sw < 0 ? 0 : sw) + 4 * q];
+    rowp[q] = D + (int64_t)rowi[q] * n_pad + lane;
+  }
+  // two register sets: block b + 2 is loaded while block b is summed and
+  // block b + 1 (loaded one block earlier) goes to LDS
+  double dA[kAvgPer], dB[kAvgPer];
+  auto load = [&](double (&d)[kAvgPer], int64_t j0) {
+    const bool in0 = j0 + lane < n, in1 = j0 + lane + 64 < n;
+#pragma unroll
+    for (int k = 0; k < kAvgPer; k++) d[k] = ((k & 1) ? in1 : in0) ? rowp[k >> 1][j0 + 64 * (k & 1)] : 0.0;
   };
-  auto put = [&](int buf, int64_t j0) {
+  auto put = [&](int buf, const double (&d)[kAvgPer], int64_t j0) {
 #pragma unroll
     for (int k = 0; k < kAvgPer; k++) {
-      const int r = wave + 4 * (k >> 1);
+      const int r = sw + 4 * (k >> 1);
       const int c = lane + 64 * (k & 1);
       const int64_t j = j0 + c;
       float lo = 0.0f, hi = 0.0f;
-      if (r < nrows && j < n) surf_candidates(d[k], j == rid[r], inv_sc, band, lo, hi);
+      if (j < n) surf_candidates(d[k], j == rowi[k >> 1], inv_sc, band, lo, hi);
       lo_s[buf][r][c] = lo;
       hi_s[buf][r][c] = hi;
     }
@@ -106,45 +115,76 @@ __global__ __launch_bounds__(256) void k_surf_avg_int(const double* __restrict__
   const int64_t i = rid[lane];
   bool live = wave == 0 && lane < nrows;
   float s = 0.0f;
-  load(0);
-  put(0, 0);
-  __syncthreads();
-  int buf = 0;
-  for (int64_t j0 = 0, it = 0; j0 < n; j0 += kAvgCols, it++) {
-    const bool next = j0 + kAvgCols < n;
-    if (next) load(j0 + kAvgCols);
-    if (wave == 0) {
-      const int cnt = n - j0 < kAvgCols ? (int)(n - j0) : kAvgCols;
-      // 8 columns' candidates read ahead of the dependent float32 adds; per
-      // column two adds and a compare, the stop taken by a uniform branch
-      for (int c0 = 0; c0 < cnt && __any(live); c0 += 8) {
-        float lo[8], hi[8];
+  // wave 0: row lane's sum over block j0 (in LDS buffer buf)
+  auto sum = [&](int buf, int64_t j0) {
+    const int cnt = n - j0 < kAvgCols ? (int)(n - j0) : kAvgCols;
+    // 8 columns' candidates in registers, the next 8 read while these are
+    // added (the LDS latency off the dependent float32 adds)
+    float nlo[8], nhi[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      nlo[u] = lo_s[buf][lane][u];
+      nhi[u] = hi_s[buf][lane][u];
+    }
+    for (int c0 = 0; c0 < cnt && __any(live); c0 += 8) {
+      float lo[8], hi[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        lo[u] = nlo[u];
+        hi[u] = nhi[u];
+      }
+      if (c0 + 8 < kAvgCols) {
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          lo[u] = lo_s[buf][lane][c0 + u];  // c0 + u < kAvgCols: inside the padded row
-          hi[u] = hi_s[buf][lane][c0 + u];
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const float a = s + lo[u];
-          const bool crit = live && c0 + u < cnt && a != s + hi[u];
-          if (__any(crit)) {
-            if (crit) {  // the sum depends on which one it is
-              pairs[atomicAdd(&counts[1], 1)] = make_int2((int)i, (int)(j0 + c0 + u));
-              next_rows[atomicAdd(&counts[0], 1)] = (int32_t)i;
-              live = false;
-            }
-          }
-          s = a;
+          nlo[u] = lo_s[buf][lane][c0 + 8 + u];  // inside the padded row
+          nhi[u] = hi_s[buf][lane][c0 + 8 + u];
         }
       }
+      // branch-free per column: the first column of the 8 whose two sums
+      // differ (columns past n hold 0 / 0, never such a column); a row that
+      // met one stops there (its later sums are not used)
+      int stop = 8;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        const float a = s + lo[u];
+        const bool crit = a != s + hi[u];
+        stop = (crit && stop == 8) ? u : stop;
+        s = a;
+      }
+      const bool rec = live && stop < 8;
+      if (__any(rec)) {
+        if (rec) {  // the sum depends on which one it is
+          pairs[atomicAdd(&counts[1], 1)] = make_int2((int)i, (int)(j0 + c0 + stop));
+          next_rows[atomicAdd(&counts[0], 1)] = (int32_t)i;
+          live = false;
+        }
+      }
+    }
+  };
+  // one block: load j0 + 2 blocks into `ld`, sum j0 from `buf`, stage j0 + 1
+  // block from `st` into the other buffer; false when every row stopped
+  auto block = [&](int buf, int64_t j0, int64_t it, double (&ld)[kAvgPer],
+                   const double (&st)[kAvgPer]) {
+    if (sw >= 0 && j0 + 2 * kAvgCols < n) load(ld, j0 + 2 * kAvgCols);
+    if (wave == 0) {
+      sum(buf, j0);
       const bool more = __any(live);
       if (lane == 0) any_live[it & 1] = more ? 1 : 0;
     }
-    if (next) put(buf ^ 1, j0 + kAvgCols);
+    if (sw >= 0 && j0 + kAvgCols < n) put(buf ^ 1, st, j0 + kAvgCols);
     __syncthreads();
-    if (!any_live[it & 1]) break;  // every row stopped: the workgroup leaves together
-    buf ^= 1;
+    return any_live[it & 1] != 0;  // a slot is rewritten only after the next barrier
+  };
+  if (sw >= 0) {
+    load(dA, 0);
+    put(0, dA, 0);
+    if (kAvgCols < n) load(dA, kAvgCols);
+  }
+  __syncthreads();
+  for (int64_t j0 = 0, it = 0; j0 < n; j0 += 2 * kAvgCols, it += 2) {
+    if (!block(0, j0, it, dB, dA)) break;  // every row stopped: the workgroup leaves together
+    if (j0 + kAvgCols >= n) break;
+    if (!block(1, j0 + kAvgCols, it + 1, dA, dB)) break;
   }
   if (live) avg[i] = (double)s / (double)(n - 1);
 }
@@ -188,48 +228,46 @@ __global__ __launch_bounds__(256) void k_surf_normalize(double* __restrict__ D, 
 
 // The reference's float32 distance of each listed pair (SURF.py:151-160:
 // float64 |x_i - x_j| * recip over the continuous kept columns, 1 per
-// differing discrete one), one wave per pair, lanes over the features and a
-// fixed-order wave sum (float64: its order changes the float32 rounding only
-// within ~1e-16 of a midpoint, as k_dist_f64's).  Stored as -f in both
-// halves of the full layout where their rows are in the window.
+// differing discrete one), one 256-thread workgroup per pair -- a round's
+// last pairs are few, so the per-pair chain of loads sets the time: thread
+// t takes features t, t + 256, ..., four loads of each row in flight, and
+// the partial sums are added in a fixed order (float64: the order changes
+// the float32 rounding only within ~1e-16 of a midpoint, as k_dist_f64's).
+// Stored as -f in both halves of the full layout where their rows are in
+// the window.
 __global__ __launch_bounds__(256) void k_surf_exact_pairs(
     const double* __restrict__ x, int64_t p_in, int64_t pc, int64_t PC, int64_t pd,
     const int64_t* __restrict__ src_col, const double* __restrict__ scl,
-    const int2* __restrict__ pairs, int64_t count, double* __restrict__ D, int64_t n_pad,
-    int2 win) {
-  const int lane = threadIdx.x & 63;
-  const int64_t k = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
-  if (k >= count) return;
-  const int2 pr = pairs[k];
+    const int2* __restrict__ pairs, double* __restrict__ D, int64_t n_pad, int2 win) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x;
+  const int2 pr = pairs[blockIdx.x];
   const double* xi = x + (int64_t)pr.x * p_in;
   const double* xj = x + (int64_t)pr.y * p_in;
-  // four chains (lane strides of 256 features), loads of all four in flight;
-  // added in a fixed order below
   double a4[4] = {0.0, 0.0, 0.0, 0.0};
-  int64_t c = lane;
-  for (; c + 192 < pc; c += 256) {
+  int64_t c = tid;
+  for (; c + 768 < pc; c += 1024) {
     double u[4], v[4], w[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const int64_t col = src_col[c + 64 * q];
+      const int64_t col = src_col[c + 256 * q];
       u[q] = xi[col];
       v[q] = xj[col];
-      w[q] = scl[c + 64 * q];
+      w[q] = scl[c + 256 * q];
     }
 #pragma unroll
     for (int q = 0; q < 4; q++) a4[q] += __builtin_fabs(u[q] - v[q]) * w[q];
   }
-  for (; c < pc; c += 64) {
+  for (; c < pc; c += 256) {
     const int64_t col = src_col[c];
     a4[0] += __builtin_fabs(xi[col] - xj[col]) * scl[c];
   }
-  double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-  for (int64_t c = PC + lane; c < PC + pd; c += 64) {
-    const int64_t col = src_col[c];
-    acc += xi[col] != xj[col] ? 1.0 : 0.0;
+  for (int64_t c2 = PC + tid; c2 < PC + pd; c2 += 256) {
+    const int64_t col = src_col[c2];
+    a4[1] += xi[col] != xj[col] ? 1.0 : 0.0;
   }
-  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
-  if (lane != 0) return;
+  const double acc = block_sum_256((a4[0] + a4[1]) + (a4[2] + a4[3]), red);
+  if (tid != 0) return;
   const double v = -(double)(float)acc;  // -0.0 for a zero distance: still marked
   if (d_row_in(win, pr.x)) D[(int64_t)pr.x * n_pad + pr.y] = v;
   if (d_row_in(win, pr.y)) D[(int64_t)pr.y * n_pad + pr.x] = v;
@@ -238,9 +276,9 @@ __global__ __launch_bounds__(256) void k_surf_exact_pairs(
 static int exact_pairs(Plan* g, int64_t count) {
   const Prepared& Q = g->P;
   if (count <= 0) return FS_OK;
-  k_surf_exact_pairs<<<(unsigned)((count + 3) / 4), 256, 0, g->stream>>>(
-      (const double*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, g->list, count, g->D,
-      Q.n_pad, g->win);
+  k_surf_exact_pairs<<<(unsigned)count, 256, 0, g->stream>>>(
+      (const double*)g->x, Q.p_in, Q.pc, Q.PC, Q.pd, g->src_col, g->scl, g->list, g->D, Q.n_pad,
+      g->win);
   return launch_check("k_surf_exact_pairs");
 }
 
@@ -272,7 +310,7 @@ int surf_resolve(Plan* g) {
   int64_t cur = rows, rounds = 0, refined_sum = 0;
   while (cur > 0) {
     FS_HIP(hipMemsetAsync(cnt, 0, 2 * sizeof(int32_t), g->stream));
-    k_surf_avg_int<<<(unsigned)((cur + 63) / 64), 256, 0, g->stream>>>(
+    k_surf_avg_int<<<(unsigned)((cur + 63) / 64), 320, 0, g->stream>>>(
         g->D, n, Q.n_pad, inv_sc, band, ra, cur, g->thr, rb, cnt, g->list);
     FS_TRY(launch_check("k_surf_avg_int"));
     int32_t next[2] = {0, 0};
