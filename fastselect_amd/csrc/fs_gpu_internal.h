@@ -302,7 +302,7 @@ void stream_put(int device, hipStream_t s);
 hipEvent_t event_get(int device, bool timing);
 void event_put(int device, hipEvent_t e, bool timing);
 // fs_pass1.hip
-int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats);
+int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats, bool beside);
 int calibrate_band(Plan* g);
 int row_guard(Plan* g);
 // after a 32-bit switch: the operand scale and sort key on the device

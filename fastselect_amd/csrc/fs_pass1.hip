@@ -730,7 +730,14 @@ __global__ __launch_bounds__(256) void k_calib(
 // tile planes (~66.5 / p of the tile's compute time each); S > 1 only when
 // the model gains at least 3%.  (Splitting only the last round's tiles was
 // measured too: no better than S = 1 at cfg2, profiles/r02/ksplit_sweep.txt.)
-int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats) {
+// `beside`: MultiSURF's mean correction runs on the side stream during
+// k_dist, and when the tiles fill fewer than two rounds its workgroups take
+// the slots a finer split would even out -- cfg2 (820 tiles on 768 slots)
+// measured 4.51 / 4.22-4.23 / 4.22 / 4.39 / 4.31 / 4.33 / ~4.4 ms a step at
+// S = 1 / 2 / 3 / 4 / 5 / 6 / 8 (the model's pick), so S stops at 3 there
+// (profiles/r06/ksplit_ab.txt); SURF's integer route (no correction) keeps
+// the model's pick (cfg5s: 182.2 ms at S = 1, 178.1 at the pick).
+int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats, bool beside) {
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
       cus <= 0) {
@@ -760,6 +767,7 @@ int choose_ksplit(int64_t tiles, int device, int nchunks, int64_t feats) {
     (void)hipGetLastError();
   int best = 1;
   double best_eff = eff(1) + 0.03;
+  if (beside && (double)tiles < 2.0 * slots) max_sp = std::min(max_sp, 3);
   for (int sp = 2; sp <= max_sp && sp <= nchunks; sp++)
     if (eff(sp) > best_eff) {
       best_eff = eff(sp);

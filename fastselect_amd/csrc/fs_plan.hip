@@ -276,9 +276,11 @@ static int setup_shard(Plan* g, const std::vector<int32_t>& bi, const std::vecto
   // pass-1 chunk count and the per-tile work in feature units of 32-bit SAD
   const int64_t rows_q = (g->use_q16 ? Q.PC / 2 : Q.PC) + Q.PD;
   g->ksplit = choose_ksplit(g->n_tiles, g->device, (int)(rows_q / kBKQ),
-                            (g->use_q16 ? Q.pc / 2 : Q.pc) + Q.pd);
+                            (g->use_q16 ? Q.pc / 2 : Q.pc) + Q.pd,
+                            Q.algo == ALGO_MULTISURF && Q.pc > 0);
   if (test_hooks().ksplit >= 1) g->ksplit = (int)std::min<int64_t>(16, test_hooks().ksplit);
-  if (Q.algo == ALGO_SURF) g->ksplit = 1;  // k_dist_f64 has no K-split
+  // SURF: its integer route splits k_dist's tiles like MultiSURF's (the
+  // float64 route, k_dist_f64, has no K-split and ignores it)
   // ReliefF stores float32 keys (Dk), formed in k_dist's epilogue from whole
   // tiles: no K-split (partial sums cannot be keyed before they are added)
   const bool dkeys = Q.algo == ALGO_RELIEFF;

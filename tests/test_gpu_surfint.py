@@ -132,3 +132,24 @@ def test_rows_slices_and_panels(F, hooks):
     b = run()
     for u, v in zip(a, b):
         assert_bitexact(u, v)
+
+
+@pytest.mark.parametrize("parts", [2, 5])
+def test_integer_route_k_split(F, hooks, parts):
+    """SURF's integer route splits k_dist's tiles like MultiSURF's (the
+    partial distance blocks merged by k_dist_merge, exact integers): forced
+    K-splits give the float64 route's scores bit for bit, whole fit and a
+    rows slice."""
+    from fastselect_amd import _lib
+    from fastselect_amd.SURF import surf_inputs
+    X, y = _data("classif", n=1100, p=420, seed=13)
+    isd, recip = surf_inputs(X, 10, "gpu")
+    hooks("surf_f64", 1)
+    ref = (_fit(F, X, y, True),
+           _lib.surf_score("gpu", X, y.astype(np.int32), recip, True, isd, rows=(300, 700)))
+    hooks("surf_f64", 0)
+    hooks("ksplit", parts)
+    got = (_fit(F, X, y, True),
+           _lib.surf_score("gpu", X, y.astype(np.int32), recip, True, isd, rows=(300, 700)))
+    for u, v in zip(got, ref):
+        assert_bitexact(u, v)
