@@ -71,6 +71,18 @@ def test_surf_devices_equal_one_device(F, oracle, star):
     assert_parity(many.feature_importances_, oracle.surf_scores(X, y, use_star=star), 1e-5)
 
 
+def test_surf_devices_integer_route(F, hooks):
+    """Two device threads on SURF's integer distance route (forced; this size
+    would take the float64 route by itself): each thread's row plan resolves
+    its rows' float32 distances, and the scores are the float64 route's."""
+    X, y = _data(1500, 600, 4)
+    hooks("surf_f64", 1)
+    ref = F.SURF(backend="gpu", use_star=True, devices=[0, 0]).fit(X, y).feature_importances_
+    hooks("surf_f64", 0)
+    got = F.SURF(backend="gpu", use_star=True, devices=[0, 0]).fit(X, y).feature_importances_
+    assert np.array_equal(np.asarray(got), np.asarray(ref))
+
+
 def test_devices_bad_ordinal_is_a_value_error(F):
     from fastselect_amd import _lib
     X, y = _data(300, 80, 5)
