@@ -153,3 +153,29 @@ def test_integer_route_k_split(F, hooks, parts):
            _lib.surf_score("gpu", X, y.astype(np.int32), recip, True, isd, rows=(300, 700)))
     for u, v in zip(got, ref):
         assert_bitexact(u, v)
+
+
+@pytest.mark.parametrize("case", ["n2", "constant", "discrete", "single_class", "n129"])
+def test_integer_route_edge_cases(F, hooks, case):
+    """Edge inputs on the forced integer route against the float64 route:
+    two samples, constant columns, an all-discrete layout (distances are
+    mismatch counts, exact on both routes), one class, n = 129 (a
+    one-sample second block)."""
+    rng = np.random.default_rng(17)
+    n, p = {"n2": (2, 6), "n129": (129, 40)}.get(case, (300, 50))
+    X = rng.standard_normal((n, p))
+    y = rng.integers(0, 2, n)
+    if case == "constant":
+        X[:, ::3] = 1.5
+    elif case == "discrete":
+        X = rng.integers(0, 3, (n, p)).astype(np.float64)
+    elif case == "single_class":
+        y = np.zeros(n, dtype=int)
+    if case == "n2":
+        y = np.array([0, 1])
+    out = []
+    for route in (0, 1):
+        hooks("surf_f64", route)
+        out.append([_fit(F, X, y, star) for star in (False, True)])
+    for u, v in zip(*out):
+        assert_bitexact(u, v)
