@@ -189,6 +189,14 @@ struct Plan {
   unsigned long long* nnz = nullptr;  // non-zero weights of the last pass 2
   bool nnz_valid = false;
   int sparse = 0;               // pass 2 over non-zero weights only
+  // MultiSURF* / SURF* split (fs_starterm.hip): pass 2 weighs the near pairs
+  // only and the far pairs' all-pairs part comes per column from its sorted
+  // values: xsT (float32 pass-2 values, feature-major), the per-sample
+  // coefficients `alpha` and the per-column terms `tcol` k_reduce adds
+  bool star_split = false;
+  float* xsT = nullptr;
+  double* alpha = nullptr;
+  double* tcol = nullptr;
   double* spart = nullptr;       // pass-2 segment partials (own block, shard_segments)
   size_t spart_cap = 0;           // doubles of spart
   // sparse pass-2 schedule (build_sparse_schedule): tile order, segment
@@ -312,6 +320,11 @@ int plan_score_surf(Plan* g, double* sums_dev);
 // fs_surfint.hip: after k_dist on a SURF plan's integer operands, the focal
 // rows' means into thr and every stored distance as its float32 value
 int surf_resolve(Plan* g);
+// fs_starterm.hip: largest n / class count of the split, and the per-column
+// all-pairs terms of this plan's column share into g->tcol (counts: the
+// MultiSURF* neighbour counts, nullptr for SURF*), launched on st
+bool star_split_fits(int64_t n, int32_t n_classes);
+int star_terms(Plan* g, const double* counts, hipStream_t st);
 // fs_pass2.hip
 int shard_segments(Plan* g);
 int run_weights(Plan* g, const double* counts, int algo, double inv_sc);
@@ -325,9 +338,10 @@ int ref_chains(Plan* g, const double* counts, double* scores);
 int surf_ref(Plan* g, double* sums);
 // dst[k] += src[k] over count doubles (k_accumulate)
 int accumulate(double* dst, const double* src, int64_t count, hipStream_t st);
-// sums[out_pos[c]] = the fixed-order sum of part[0..nrows)[c] (k_reduce)
+// sums[out_pos[c]] = the fixed-order sum of part[0..nrows)[c] (k_reduce),
+// plus add[c] when add is given
 int reduce_segments(const double* part, int64_t nrows, int64_t PW, const int64_t* out_pos,
-                    double* sums, hipStream_t st);
+                    double* sums, hipStream_t st, const double* add = nullptr);
 // fs_relieff.hip
 int plan_score_relieff(Plan* g, double* sums_dev);
 int relieff_run_one(const Prepared& P, const void* x, int device, int64_t r_lo, int64_t r_hi,

@@ -139,6 +139,7 @@ struct TestHooks {
   int64_t rf_ref_replay = 0;   // 1: reference-order quicksort replay of every tied row
   int64_t ref_q16 = 0;         // 1: reference-order MultiSURF may take 16-bit operands
   int64_t surf_f64 = -1;       // 0 / 1: SURF on integer / float64 distances (surf_band)
+  int64_t star_split = -1;     // 0 / 1: MultiSURF* / SURF* dense star weights / near-only + column terms
   int64_t colsort_bins12 = 0;  // 1: 4096 bins at every n
   int64_t colsort_global = 0;  // 1: the large-n (device sort) route at every n
 };

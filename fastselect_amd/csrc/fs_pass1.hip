@@ -6,7 +6,8 @@ namespace fs {
 namespace gpu {
 
 // ---------------------------------------------------------------------------
-// Quantize: X -> xqT (u32, [PW][n_pad]) and xs (f32, [n_pad][PW])
+// Quantize: X -> xqT (u32, [PW][n_pad]) and xs (f32, [n_pad][PW]), and
+// with a star split (fs_starterm.hip) xs feature-major as well (xsT)
 // ---------------------------------------------------------------------------
 // With q16 the continuous rows of xqT are packed: word row c/2 holds features
 // c (low half) and c + 1 (high half), and the discrete rows follow at PC/2:
@@ -19,7 +20,7 @@ __global__ __launch_bounds__(256) void k_quantize(
     const double* __restrict__ qs, const double* __restrict__ scl,
     const int64_t* __restrict__ dtab_off, const double* __restrict__ dtab, int disc_bits,
     int64_t eps_lo, int64_t eps_hi, uint32_t* __restrict__ xqT, float* __restrict__ xs,
-    float* __restrict__ epsT) {
+    float* __restrict__ epsT, float* __restrict__ xsT) {
   __shared__ uint32_t tile[64][65];
   __shared__ float etile[64][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -30,6 +31,7 @@ __global__ __launch_bounds__(256) void k_quantize(
   // all 16 of this thread's loads are issued before any value is used
   constexpr int kR = 16;
   T xr[kR];
+  float vr[kR];
 #pragma unroll
   for (int k = 0; k < kR; k++) {
     const int64_t i = i0 + ty + 4 * k;
@@ -68,6 +70,7 @@ __global__ __launch_bounds__(256) void k_quantize(
       }
     }
     xs[i * PW + c] = v;
+    vr[k] = v;
     tile[r][tx] = q;
     etile[r][tx] = e;
   }
@@ -82,6 +85,13 @@ __global__ __launch_bounds__(256) void k_quantize(
   // quantisation errors only for this rank's share of the correction
   for (int r = ty; r < 64; r += 4)
     if (c0 + r >= eps_lo && c0 + r < eps_hi) epsT[(c0 + r) * n_pad + i0 + tx] = etile[tx][r];
+  if (xsT) {  // the pass-2 values transposed through etile
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kR; k++) etile[ty + 4 * k][tx] = vr[k];
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) xsT[(c0 + r) * n_pad + i0 + tx] = etile[tx][r];
+  }
 }
 
 // Mean-distance correction terms: exact per-column order, fs_colsort.hip
@@ -520,7 +530,8 @@ __global__ __launch_bounds__(256) void k_quantize_f64(
     const double* __restrict__ x, int64_t n, int64_t n_pad, int64_t p_in, int64_t PW, int64_t pc,
     const int64_t* __restrict__ src_col, const double* __restrict__ off,
     const double* __restrict__ scl, const int64_t* __restrict__ dtab_off,
-    const double* __restrict__ dtab, double* __restrict__ xT, float* __restrict__ xs) {
+    const double* __restrict__ dtab, double* __restrict__ xT, float* __restrict__ xs,
+    float* __restrict__ xsT) {
   __shared__ double tile[64][65];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int64_t c0 = (int64_t)blockIdx.x * 64, i0 = (int64_t)blockIdx.y * 64;
@@ -548,6 +559,8 @@ __global__ __launch_bounds__(256) void k_quantize_f64(
   }
   __syncthreads();
   for (int r = ty; r < 64; r += 4) xT[(c0 + r) * n_pad + i0 + tx] = tile[tx][r];
+  if (xsT)
+    for (int r = ty; r < 64; r += 4) xsT[(c0 + r) * n_pad + i0 + tx] = (float)tile[tx][r];
 }
 
 // ---------------------------------------------------------------------------
@@ -1071,11 +1084,11 @@ int row_guard(Plan* g) {
   if (g->x_is_f64)
     k_quantize<double><<<gq, 256, 0, g->stream>>>(
         (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
-        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, 0, Q.pc, g->xqT, g->xs, g->epsT);
+        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, 0, Q.pc, g->xqT, g->xs, g->epsT, g->xsT);
   else
     k_quantize<float><<<gq, 256, 0, g->stream>>>(
         (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
-        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, 0, Q.pc, g->xqT, g->xs, g->epsT);
+        g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, 0, Q.pc, g->xqT, g->xs, g->epsT, g->xsT);
   rc = launch_check("k_quantize (row guard)");
   if (!rc) rc = run_colsort(g, 0, Q.pc, g->stream);
   if (!rc) rc = run_rowcorr(g, 0, Q.pc, corr, g->stream);
@@ -1089,6 +1102,17 @@ int row_guard(Plan* g) {
   return FS_OK;
 }
 
+// SURF*'s star-split column terms (fs_starterm.hip) need only the operands
+// and the focal rows: on the side stream beside pass 1, joined by run_pass2
+// before k_reduce adds them
+static int fork_star_terms(Plan* g) {
+  FS_HIP(hipEventRecord(g->ev_fork, g->stream));
+  FS_HIP(hipStreamWaitEvent(g->side, g->ev_fork, 0));
+  FS_TRY(star_terms(g, nullptr, g->side));
+  FS_HIP(hipEventRecord(g->ev_join, g->side));
+  return FS_OK;
+}
+
 // quantize (+ mean correction terms) and pass 1 (distance tiles)
 int run_quantize_dist(Plan* g) {
   const Prepared& Q = g->P;
@@ -1097,8 +1121,9 @@ int run_quantize_dist(Plan* g) {
   if (Q.algo == ALGO_SURF && !g->surf_int) {
     k_quantize_f64<<<gq, 256, 0, g->stream>>>((const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW,
                                               Q.pc, g->src_col, g->off, g->scl, g->dtab_off,
-                                              g->dtab, g->xT64, g->xs);
+                                              g->dtab, g->xT64, g->xs, g->xsT);
     FS_TRY(launch_check("k_quantize_f64"));
+    if (g->star_split) FS_TRY(fork_star_terms(g));
     if (g->n_tiles > 0) {
       FS_HIP(hipEventRecord(g->ev[0], g->stream));
       k_dist_f64<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(
@@ -1123,12 +1148,12 @@ int run_quantize_dist(Plan* g) {
     k_quantize<double><<<gq, 256, 0, g->stream>>>(
         (const double*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
         g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, eps_lo, eps_hi, g->xqT, g->xs,
-        g->epsT);
+        g->epsT, g->xsT);
   } else {
     k_quantize<float><<<gq, 256, 0, g->stream>>>(
         (const float*)g->x, Q.n, Q.n_pad, Q.p_in, Q.PW, Q.PC, Q.q16, Q.pc, g->src_col, g->off,
         g->qs, g->scl, g->dtab_off, g->dtab, Q.disc_bits, eps_lo, eps_hi, g->xqT, g->xs,
-        g->epsT);
+        g->epsT, g->xsT);
   }
   if (!reuse) FS_TRY(launch_check("k_quantize"));
   if (Q.algo == ALGO_MULTISURF && !reuse) {
@@ -1149,6 +1174,7 @@ int run_quantize_dist(Plan* g) {
     FS_TRY(run_rowcorr(g, g->c_lo, g->c_hi, g->corr, g->side));
     FS_HIP(hipEventRecord(g->ev_join, g->side));
   }
+  if (Q.algo == ALGO_SURF && g->star_split) FS_TRY(fork_star_terms(g));
   if (g->n_tiles > 0) {
     FS_HIP(hipEventRecord(g->ev[0], g->stream));
     const int64_t n_split = g->ksplit > 1 ? g->n_tiles - g->kfull : 0;

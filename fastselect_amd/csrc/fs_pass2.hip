@@ -22,14 +22,26 @@ __device__ __forceinline__ float pair_weight(const double* __restrict__ D, int64
   if (!(i < n && j < n && upper)) return 0.0f;
   const double d = D[d_rd(tiled, win, n_pad, t, i0, j0, ii, jj)];  // == D[i][j]
   const bool hit = lab[i] == lab[j];
+  // use_star == 2: the star split (fs_starterm.hip) -- near pairs only, the
+  // star weight minus its all-pairs part: MultiSURF* near misses 2 / M_i,
+  // SURF* near pairs +-2; the far pairs' weight is in the per-column terms
+  const int ws = use_star == 2 ? 0 : use_star;
   double wi, wj;
   if (algo == ALGO_MULTISURF) {
-    wi = multisurf_weight(d < thr[i], hit, use_star, counts[2 * i], counts[2 * i + 1]);
-    wj = multisurf_weight(d < thr[j], hit, use_star, counts[2 * j], counts[2 * j + 1]);
+    wi = multisurf_weight(d < thr[i], hit, ws, counts[2 * i], counts[2 * i + 1]);
+    wj = multisurf_weight(d < thr[j], hit, ws, counts[2 * j], counts[2 * j + 1]);
+    if (use_star == 2 && !hit) {
+      wi *= 2.0;
+      wj *= 2.0;
+    }
   } else {  // SURF: float32 distance against the float64 mean
     const double df = (double)(float)(d * inv_sc);
-    wi = surf_weight(df < thr[i], hit, use_star);
-    wj = surf_weight(df < thr[j], hit, use_star);
+    wi = surf_weight(df < thr[i], hit, ws);
+    wj = surf_weight(df < thr[j], hit, ws);
+    if (use_star == 2) {
+      wi *= 2.0;
+      wj *= 2.0;
+    }
   }
   // Only focal samples in [r_lo, r_hi) contribute their side of a pair (row
   // sharding: another rank scores the other side); MultiSURF passes [0, n).
@@ -488,6 +500,7 @@ __global__ void k_accumulate(double* __restrict__ dst, const double* __restrict_
 constexpr int kReduceWaves = 16;
 __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part, int64_t nseg,
                                                  int64_t PW, const int64_t* __restrict__ out_pos,
+                                                 const double* __restrict__ add,
                                                  double* __restrict__ out) {
   __shared__ double red[kReduceWaves][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -504,7 +517,7 @@ __global__ __launch_bounds__(1024) void k_reduce(const double* __restrict__ part
 #pragma unroll
   for (int k = 0; k < 4; k++)
     q[k] = (red[4 * k][lane] + red[4 * k + 1][lane]) + (red[4 * k + 2][lane] + red[4 * k + 3][lane]);
-  out[o] = (q[0] + q[1]) + (q[2] + q[3]);
+  out[o] = ((q[0] + q[1]) + (q[2] + q[3])) + (add ? add[c] : 0.0);
 }
 
 int accumulate(double* dst, const double* src, int64_t count, hipStream_t st) {
@@ -514,8 +527,8 @@ int accumulate(double* dst, const double* src, int64_t count, hipStream_t st) {
 }
 
 int reduce_segments(const double* part, int64_t nrows, int64_t PW, const int64_t* out_pos,
-                    double* sums, hipStream_t st) {
-  k_reduce<<<(unsigned)((PW + 63) / 64), 1024, 0, st>>>(part, nrows, PW, out_pos, sums);
+                    double* sums, hipStream_t st, const double* add) {
+  k_reduce<<<(unsigned)((PW + 63) / 64), 1024, 0, st>>>(part, nrows, PW, out_pos, add, sums);
   return launch_check("k_reduce");
 }
 
@@ -686,19 +699,24 @@ int shard_segments(Plan* g) {
 // Pair weights of the owned tiles in the form pass 2 reads (dense or sparse).
 int run_weights(Plan* g, const double* counts, int algo, double inv_sc) {
   const Prepared& Q = g->P;
+  // the star split's per-column terms (this rank's column share, whatever
+  // tiles it owns); k_reduce adds them
+  // (SURF*: forked beside pass 1, run_quantize_dist)
+  if (g->star_split && algo == ALGO_MULTISURF) FS_TRY(star_terms(g, counts, g->stream));
   if (g->n_tiles == 0) return FS_OK;
+  const int star = g->star_split ? 2 : Q.use_star;
   if (g->sparse) {
     FS_HIP(hipMemsetAsync(g->nnz, 0, sizeof(unsigned long long), g->stream));
     g->nnz_valid = true;
     k_weights_sparse2<<<(unsigned)g->n_tiles, 64 * kSWaves, 0, g->stream>>>(
         g->D, Q.n, Q.n_pad, g->tiled, g->win, g->tiles, g->thr, g->lab, counts, algo,
-        Q.use_star, inv_sc, g->r_lo, g->r_hi, g->ent, g->nnz);
+        star, inv_sc, g->r_lo, g->r_hi, g->ent, g->nnz);
     return launch_check("k_weights_sparse2");
   }
   k_weights<<<(unsigned)g->n_tiles, 256, 0, g->stream>>>(g->D, Q.n, Q.n_pad, g->tiled, g->win,
                                                          g->tiles,
                                                          g->thr,
-                                                         g->lab, counts, algo, Q.use_star, inv_sc,
+                                                         g->lab, counts, algo, star, inv_sc,
                                                          g->r_lo, g->r_hi, g->Wt);
   return launch_check("k_weights");
 }
@@ -706,8 +724,13 @@ int run_weights(Plan* g, const double* counts, int algo, double inv_sc) {
 int run_pass2(Plan* g, double* scores_dev) {
   const Prepared& Q = g->P;
   const int64_t nfb = (Q.PW + 127) / 128;
+  const double* add = g->star_split ? g->tcol : nullptr;
   FS_HIP(hipMemsetAsync(scores_dev, 0, sizeof(double) * Q.n_kept, g->stream));
-  if (g->n_tiles == 0) return FS_OK;
+  if (add && Q.algo == ALGO_SURF) FS_HIP(hipStreamWaitEvent(g->stream, g->ev_join, 0));
+  if (g->n_tiles == 0) {
+    if (add) return reduce_segments(g->spart, 0, Q.PW, g->out_pos, scores_dev, g->stream, add);
+    return FS_OK;
+  }
   FS_HIP(hipEventRecord(g->ev[2], g->stream));
   const int64_t seg_per_xcd = (g->nseg + kXcds - 1) / kXcds;
   if (g->sparse) {
@@ -732,7 +755,7 @@ int run_pass2(Plan* g, double* scores_dev) {
   }
   FS_HIP(hipEventRecord(g->ev[3], g->stream));
   k_reduce<<<(unsigned)((Q.PW + 63) / 64), 1024, 0, g->stream>>>(g->spart, g->nsegpart, Q.PW,
-                                                                   g->out_pos, scores_dev);
+                                                                   g->out_pos, add, scores_dev);
   return launch_check("k_reduce");
 }
 

@@ -63,9 +63,24 @@ static int choose_q16(const Prepared& P) {
 // SURF about break-even (cfg5), SURF* weighs nearly every pair.  A
 // row-sharded SURF plan zeroes the sides of the samples it does not own, so
 // it goes sparse.  The sparse test hook forces either.
+// The star split (fs_starterm.hip) leaves pass 2 the near pairs only:
+// MultiSURF*'s 41.7% and SURF*'s 62.4% at cfg5 (profiles/r06/near_density.txt)
+// go sparse like MultiSURF's.
+// MultiSURF* / SURF* in fast accumulation: near pairs in pass 2, the far
+// pairs' all-pairs part per column from its sorted values (fs_starterm.hip),
+// for n <= 24576 and up to 8 classes (one workgroup sorts a column in LDS);
+// the star_split test hook forces either form where it fits.
+static bool choose_star_split(const Prepared& P) {
+  if (!P.use_star || P.ref_accum || P.algo == ALGO_RELIEFF) return false;
+  if (!star_split_fits(P.n, P.n_classes)) return false;
+  if (test_hooks().star_split >= 0) return test_hooks().star_split != 0;
+  return true;
+}
+
 static int choose_sparse(const Plan* g, const Prepared& P) {
   if (P.algo == ALGO_RELIEFF) return 0;
   if (test_hooks().sparse >= 0) return test_hooks().sparse != 0 ? 1 : 0;
+  if (g->star_split) return 1;
   if (P.algo == ALGO_MULTISURF) return P.use_star ? 0 : 1;
   return (g->r_hi - g->r_lo < P.n) ? 1 : 0;  // SURF / SURF*: only when row-sharded
 }
@@ -195,7 +210,9 @@ int plan_layout(Plan* g) {
       // tile) plus kXsSlack floats: the asm loop of a last, partial feature
       // block reads a whole block width of each B row, past the end of the
       // last row when PW is narrower than the block
-      (rc = dalloc(g, &g->xs, (size_t)(Q.n_pad + 2) * Q.PW + kXsSlack))) {
+      (rc = dalloc(g, &g->xs, (size_t)(Q.n_pad + 2) * Q.PW + kXsSlack)) ||
+      (g->star_split && ((rc = dalloc(g, &g->xsT, (size_t)Q.PW * Q.n_pad)) ||
+                         (rc = dalloc(g, &g->tcol, Q.PW))))) {
   } else if (Q.algo == ALGO_SURF) {
     // its operands follow the route the calibration picks (below)
   } else if ((rc = dalloc(g, &g->xqT, (size_t)Q.PW * Q.n_pad)) == FS_OK) {
@@ -444,7 +461,9 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
         (rc = dalloc(g, &g->bcnt, (size_t)(Q.n / kExactThrRows + 2))))
       return fail(rc);
   }
+  g->star_split = choose_star_split(Q);
   g->sparse = choose_sparse(g, Q);
+  if (g->star_split && (rc = dalloc(g, &g->alpha, Q.n_pad))) return fail(rc);
   if ((rc = setup_shard(g, bi, bj))) return fail(rc);
   trace_mark("plan: hipMalloc");
   std::vector<int32_t> lab(Q.n_pad, -1);

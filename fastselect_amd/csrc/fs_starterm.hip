@@ -1,0 +1,304 @@
+// fs_starterm.hip -- the star variants' far pairs without a dense pass 2.
+//
+// MultiSURF* (MultiSURF.py:217-251) weighs EVERY miss of focal sample i:
+// +1/M_i when near, -1/M'_i when far (M' = max(M, 1); a near miss implies
+// M >= 1, so M' = M there).  SURF* (SURF.py:180-193) weighs every pair: near
+// hit -1, near miss +1, far hit +1, far miss -1.  Both split into a near-only
+// part and an all-pairs part that does not depend on the decisions:
+//
+//   MultiSURF*  w_ij = [near] (hit ? -1/H_i : +2/M'_i)  -  [miss] / M'_i
+//   SURF*       w_ij = [near] (hit ? -2 : +2)           +  (hit ? +1 : -1)
+//
+// The near part is the sparse pass 2 (k_weights_sparse2 with use_star = 2:
+// cfg5 holds 41.7% near pairs for MultiSURF, 62.4% for SURF, against 62%
+// and 100% non-zero star weights; profiles/r06/near_density.txt).  The
+// all-pairs part of feature f is
+//
+//   U_f = sum_i alpha_i (gamma S_same(i) - S_all(i)),
+//   S_all(i) = sum_{j != i} d_f(i, j),   S_same(i) = the same over j of i's class
+//
+// (MultiSURF*: alpha = 1/M'_i, gamma = 1; SURF*: alpha = 1, gamma = 2;
+// alpha = 0 outside the plan's focal rows), which one sort of the column
+// gives: with v_k the k-th smallest value, P_k the sum of the values before
+// it and T the column total,  S_all = v_k (2k - n) - 2 P_k + T,  and the
+// same within a class from the class's own prefix sums (equal values add 0
+// on either side, so ties need no order).  A discrete column's d is
+// [v_i != v_j]: S_all = n - eq(v_i), S_same = n_c - eq_c(v_i), with the
+// equal-value counts from the sorted run bounds.
+//
+// One 1024-thread workgroup per column, n <= 24576 (kStMaxIpt items per
+// thread): the column's (key, 16-bit index) pairs sorted in LDS by rocPRIM's
+// block radix sort, one block scan of the values, one (count, sum) scan per
+// class, a fixed-order reduction -- deterministic, sums in float64 of the
+// float32 pass-2 values (the pair terms of the dense pass are float32 |a - b|
+// summed in float32; the split is the more precise of the two).
+#include <hip/hip_runtime.h>
+
+#include <rocprim/block/block_radix_sort.hpp>
+
+#include "fs_gpu_internal.h"
+
+namespace fs {
+namespace gpu {
+
+namespace {
+
+constexpr int kStThreads = 1024;
+constexpr int kStMaxIpt = 24;
+constexpr int kStMaxClasses = 8;
+constexpr int kStWaves = kStThreads / 64;
+
+// order-preserving float -> u32 (continuous values are >= 0, but any sign
+// sorts right); 0xFFFFFFFF is never produced (it would be a negative NaN)
+__device__ __forceinline__ uint32_t st_key(float v) {
+  const uint32_t u = __float_as_uint(v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float st_val(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+
+// Exclusive block scan of two doubles (counts are exact integers in a
+// double); fixed order, so the same column gives the same bits every run.
+__device__ __forceinline__ void st_scan2(double& a, double& b, double (*ws)[kStWaves],
+                                         double& ta, double& tb) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double x = a, y = b;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double tx = __shfl_up(x, o), ty = __shfl_up(y, o);
+    if (lane >= o) {
+      x += tx;
+      y += ty;
+    }
+  }
+  if (lane == 63) {
+    ws[0][wave] = x;
+    ws[1][wave] = y;
+  }
+  __syncthreads();
+  double pa = 0.0, pb = 0.0, sa = 0.0, sb = 0.0;
+#pragma unroll
+  for (int w = 0; w < kStWaves; w++) {
+    const double u = ws[0][w], v = ws[1][w];
+    if (w < wave) {
+      pa += u;
+      pb += v;
+    }
+    sa += u;
+    sb += v;
+  }
+  __syncthreads();  // ws is reused by the next scan
+  ta = sa;
+  tb = sb;
+  a = pa + x - a;
+  b = pb + y - b;
+}
+
+template <int IPT, bool DISC>
+struct StLds {
+  union {
+    typename rocprim::block_radix_sort<uint32_t, kStThreads, IPT, uint16_t>::storage_type sort;
+    struct {
+      uint32_t key[DISC ? kStThreads * IPT : 1];      // sorted keys (run bounds)
+      uint16_t cnt[DISC ? kStThreads * IPT + 2 : 1];  // class-c items before each position
+    } d;
+  } u;
+  double ws[2][kStWaves];
+};
+
+// first position in [lo, hi) whose key is >= k (upper: > k)
+template <bool UPPER>
+__device__ __forceinline__ int st_bound(const uint32_t* __restrict__ key, int lo, int hi,
+                                        uint32_t k) {
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (UPPER ? key[mid] <= k : key[mid] < k) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+template <int IPT, bool DISC>
+__global__ __launch_bounds__(kStThreads) void k_star_terms(
+    const float* __restrict__ xsT, int64_t n, int64_t n_pad, const int32_t* __restrict__ lab,
+    const double* __restrict__ alpha, int ncls, double gamma, int64_t c_first, int64_t s_lo,
+    int64_t s_hi, const int64_t* __restrict__ out_pos, double* __restrict__ tcol) {
+  using Sort = rocprim::block_radix_sort<uint32_t, kStThreads, IPT, uint16_t>;
+  __shared__ StLds<IPT, DISC> sm;
+  const int64_t c = c_first + blockIdx.x;
+  const int tid = threadIdx.x;
+  if (c < s_lo || c >= s_hi || out_pos[c] < 0) {
+    if (tid == 0) tcol[c] = 0.0;
+    return;
+  }
+  const int nn = (int)n;
+  const float* __restrict__ col = xsT + c * n_pad;
+  uint32_t key[IPT];
+  uint16_t idx[IPT];
+#pragma unroll
+  for (int j = 0; j < IPT; j++) {  // striped loads (coalesced); the sort ignores the arrangement
+    const int i = j * kStThreads + tid;
+    key[j] = i < nn ? (DISC ? __float_as_uint(col[i]) : st_key(col[i])) : 0xFFFFFFFFu;
+    idx[j] = (uint16_t)i;
+  }
+  Sort().sort(key, idx, sm.u.sort);  // blocked: positions tid * IPT + j; padding last
+  __syncthreads();                   // the sort's storage is reused below
+  const int base = tid * IPT;
+  // per item only its class and (discrete) run bounds stay in registers:
+  // the value decodes from the key, alpha reloads from L1 / L2
+  int cl[IPT];
+  double loc = 0.0;
+#pragma unroll
+  for (int j = 0; j < IPT; j++) {
+    const bool ok = base + j < nn;
+    cl[j] = ok ? lab[idx[j]] : -1;
+    if (!DISC) loc += ok ? (double)st_val(key[j]) : 0.0;
+  }
+  double acc = 0.0;
+  uint32_t run[DISC ? IPT : 1];  // lo | hi << 16
+  if (!DISC) {
+    double P = loc, zero = 0.0, T, z;
+    st_scan2(P, zero, sm.ws, T, z);
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+      if (base + j < nn) {
+        const double v = (double)st_val(key[j]);
+        acc -= alpha[idx[j]] * (v * (double)(2 * (base + j) - nn) - 2.0 * P + T);
+        P += v;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < IPT; j++)
+      if (base + j < nn) sm.u.d.key[base + j] = key[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+      const int p = base + j;
+      run[j] = 0u;
+      if (p < nn) {
+        const int lo = st_bound<false>(sm.u.d.key, 0, p, key[j]);
+        const int hi = st_bound<true>(sm.u.d.key, p + 1, nn, key[j]);
+        run[j] = (uint32_t)lo | ((uint32_t)hi << 16);
+        acc -= alpha[idx[j]] * (double)(nn - (hi - lo));
+      }
+    }
+  }
+  for (int k = 0; k < ncls; k++) {
+    double lc = 0.0, ls = 0.0;
+#pragma unroll
+    for (int j = 0; j < IPT; j++)
+      if (cl[j] == k) {
+        lc += 1.0;
+        if (!DISC) ls += (double)st_val(key[j]);
+      }
+    double tc, ts;
+    st_scan2(lc, ls, sm.ws, tc, ts);
+    if (!DISC) {
+#pragma unroll
+      for (int j = 0; j < IPT; j++)
+        if (cl[j] == k) {
+          const double v = (double)st_val(key[j]);
+          acc += gamma * alpha[idx[j]] * (v * (2.0 * lc - tc) - 2.0 * ls + ts);
+          lc += 1.0;
+          ls += v;
+        }
+    } else {
+      // class-k items before each position, then eq_k = cnt[hi] - cnt[lo]
+#pragma unroll
+      for (int j = 0; j < IPT; j++) {
+        if (base + j < nn) sm.u.d.cnt[base + j] = (uint16_t)lc;
+        if (cl[j] == k) lc += 1.0;
+      }
+      if (tid == 0) sm.u.d.cnt[nn] = (uint16_t)tc;
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < IPT; j++)
+        if (cl[j] == k) {
+          const int eq = (int)sm.u.d.cnt[run[j] >> 16] - (int)sm.u.d.cnt[run[j] & 0xFFFFu];
+          acc += gamma * alpha[idx[j]] * (tc - (double)eq);
+        }
+      __syncthreads();  // cnt is rewritten for the next class
+    }
+  }
+  // fixed-order reduction of acc
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) sm.ws[0][wave] = acc;
+  __syncthreads();
+  if (tid == 0) {
+    double s = 0.0;
+    for (int w = 0; w < kStWaves; w++) s += sm.ws[0][w];
+    tcol[c] = s;
+  }
+}
+
+// alpha_i: 1 / max(M_i, 1) (MultiSURF*, counts[2i + 1] = M_i) or 1 (SURF*)
+// on the focal rows [r_lo, r_hi), 0 elsewhere
+__global__ void k_star_alpha(int64_t n_pad, const double* __restrict__ counts, int64_t r_lo,
+                             int64_t r_hi, double* __restrict__ alpha) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n_pad) return;
+  double a = 0.0;
+  if (i >= r_lo && i < r_hi) {
+    if (counts) {
+      const double m = counts[2 * i + 1];
+      a = 1.0 / (m > 0.0 ? m : 1.0);
+    } else {
+      a = 1.0;
+    }
+  }
+  alpha[i] = a;
+}
+
+template <bool DISC>
+int launch_terms(Plan* g, int64_t c_first, int64_t ncols, int64_t s_lo, int64_t s_hi,
+                 double gamma, hipStream_t st) {
+  const Prepared& Q = g->P;
+  if (ncols <= 0) return FS_OK;
+  const unsigned grid = (unsigned)ncols;
+#define FS_ST(IPT)                                                                              \
+  k_star_terms<IPT, DISC><<<grid, kStThreads, 0, st>>>(                                      \
+      g->xsT, Q.n, Q.n_pad, g->lab, g->alpha, Q.n_classes, gamma, c_first, s_lo, s_hi,           \
+      g->out_pos, g->tcol)
+  const int64_t ipt = (Q.n + kStThreads - 1) / kStThreads;
+  if (ipt <= 4) FS_ST(4);
+  else if (ipt <= 8) FS_ST(8);
+  else if (ipt <= 10) FS_ST(10);
+  else if (ipt <= 12) FS_ST(12);
+  else if (ipt <= 16) FS_ST(16);
+  else if (ipt <= 20) FS_ST(20);
+  else FS_ST(24);
+#undef FS_ST
+  return launch_check(DISC ? "k_star_terms<disc>" : "k_star_terms");
+}
+
+}  // namespace
+
+bool star_split_fits(int64_t n, int32_t n_classes) {
+  return n >= 2 && n <= (int64_t)kStThreads * kStMaxIpt && n_classes >= 1 &&
+         n_classes <= kStMaxClasses;
+}
+
+int star_terms(Plan* g, const double* counts, hipStream_t st) {
+  const Prepared& Q = g->P;
+  if (!g->xsT || !g->alpha || !g->tcol || !star_split_fits(Q.n, Q.n_classes)) {
+    set_error("star split: plan without its buffers or outside the split's sizes");
+    return FS_EINVAL;
+  }
+  k_star_alpha<<<(unsigned)((Q.n_pad + 255) / 256), 256, 0, st>>>(Q.n_pad, counts, g->r_lo,
+                                                                 g->r_hi, g->alpha);
+  FS_TRY(launch_check("k_star_alpha"));
+  // this rank's share of the columns (tile-sharded MultiSURF: each rank adds
+  // its share before the sum all-reduce); a row plan covers every column for
+  // its own focal rows
+  const int64_t s_lo = Q.PW * g->rank / g->world, s_hi = Q.PW * (g->rank + 1) / g->world;
+  const double gamma = Q.algo == ALGO_SURF ? 2.0 : 1.0;
+  FS_TRY(launch_terms<false>(g, 0, Q.PC, s_lo, s_hi, gamma, st));
+  return launch_terms<true>(g, Q.PC, Q.PW - Q.PC, s_lo, s_hi, gamma, st);
+}
+
+}  // namespace gpu
+}  // namespace fs
