@@ -491,7 +491,9 @@ def bench_rows(args, cfg, world, rank, local, on_gpu, dist, sync, barrier, dist_
                       "update" if algo == "relieff" else
                       "u32 pass 1 (the reference's fp32 distances resolved exactly: fp64 "
                       "recomputation where a row sum or decision depends on one), fp32 pair sums"
-                      if surf_int else "fp64 distances, fp32 pair sums"),
+                      if surf_int else "fp64 distances, fp32 pair sums")
+                     + (" (SURF* star split: near pairs in pass 2, the far pairs per column from "
+                        "its sorted values in fp64)" if algo == "surf" and args.star else ""),
             "data": f"synthetic make_classification(n_informative=20, n_redundant={cfg['red']}, "
                     f"random_state=42)",
             "config": {"workload": f"{name} n={n} p={p} (BASELINE configs[{cfg['idx']}])",
@@ -757,7 +759,10 @@ def main():
             "arith": "pass 1: integer L1 distances (v_sad_u16 on 16-bit operands for n >= 16384, "
                      "else v_sad_u32), pairs near a threshold recomputed in the reference's "
                      "float32 arithmetic; pass 2 over the pairs with a non-zero weight: f32 diffs x "
-                     "f32 pair weights, f64 accumulation",
+                     "f32 pair weights, f64 accumulation"
+                     + ("; MultiSURF* star split: pass 2 over the near pairs, the far misses' "
+                        "all-pairs part per column from its sorted values (k_star_terms, f64)"
+                        if args.star else ""),
             "data": "synthetic make_classification(n_informative=20, n_redundant=100, random_state=42)",
             "config": {"workload": f"MultiSURF{'*' if args.star else ''} n={n} p={p} "
                                    f"(BASELINE configs[{cfg['idx']}])",

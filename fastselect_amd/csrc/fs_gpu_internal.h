@@ -142,6 +142,10 @@ struct Plan {
   // forked after k_quantize and joined before k_rowstats_reduce, beside k_dist
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // MultiSURF*: the star split's per-sample sums on a stream of their own
+  // (beside k_dist and the correction), joined by run_weights
+  hipStream_t side2 = nullptr;
+  hipEvent_t ev_star = nullptr;
   int64_t nb = 0, n_tiles = 0, seg_len = 1, nseg = 1;
   int64_t nsegpart = 1;         // rows of spart (nseg, or 2 * nseg for the v2 sparse pass)
   int ksplit = 1;               // pass-1 K-split parts of the tail tiles (k_dist)
@@ -321,10 +325,14 @@ int plan_score_surf(Plan* g, double* sums_dev);
 // rows' means into thr and every stored distance as its float32 value
 int surf_resolve(Plan* g);
 // fs_starterm.hip: largest n / class count of the split, and the per-column
-// all-pairs terms of this plan's column share into g->tcol (counts: the
-// MultiSURF* neighbour counts, nullptr for SURF*), launched on st
+// all-pairs terms of this plan's column share into g->tcol (SURF*; counts:
+// SURF*), launched on st.  MultiSURF* in two steps: star_sums (beside
+// pass 1: every sample's sum over the other classes, into xsT in place), then
+// star_reduce once the neighbour counts are known (alpha-weighted column sums)
 bool star_split_fits(int64_t n, int32_t n_classes);
 int star_terms(Plan* g, const double* counts, hipStream_t st);
+int star_sums(Plan* g, hipStream_t st);
+int star_reduce(Plan* g, const double* counts, hipStream_t st);
 // fs_pass2.hip
 int shard_segments(Plan* g);
 int run_weights(Plan* g, const double* counts, int algo, double inv_sc);

@@ -1175,6 +1175,15 @@ int run_quantize_dist(Plan* g) {
     FS_HIP(hipEventRecord(g->ev_join, g->side));
   }
   if (Q.algo == ALGO_SURF && g->star_split) FS_TRY(fork_star_terms(g));
+  if (Q.algo == ALGO_MULTISURF && g->star_split) {
+    // MultiSURF*'s per-sample sums over the other classes, on a third stream
+    // beside k_dist and the correction (run_weights waits for ev_star): they
+    // need only the operands (the counts weigh them in star_reduce)
+    FS_HIP(hipEventRecord(g->ev_fork, g->stream));
+    FS_HIP(hipStreamWaitEvent(g->side2, g->ev_fork, 0));
+    FS_TRY(star_sums(g, g->side2));
+    FS_HIP(hipEventRecord(g->ev_star, g->side2));
+  }
   if (g->n_tiles > 0) {
     FS_HIP(hipEventRecord(g->ev[0], g->stream));
     const int64_t n_split = g->ksplit > 1 ? g->n_tiles - g->kfull : 0;

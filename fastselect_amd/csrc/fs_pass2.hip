@@ -701,8 +701,12 @@ int run_weights(Plan* g, const double* counts, int algo, double inv_sc) {
   const Prepared& Q = g->P;
   // the star split's per-column terms (this rank's column share, whatever
   // tiles it owns); k_reduce adds them
-  // (SURF*: forked beside pass 1, run_quantize_dist)
-  if (g->star_split && algo == ALGO_MULTISURF) FS_TRY(star_terms(g, counts, g->stream));
+  // (SURF*: forked beside pass 1, run_quantize_dist; MultiSURF*: the
+  // per-sample sums too, weighed by the counts here)
+  if (g->star_split && algo == ALGO_MULTISURF) {
+    FS_HIP(hipStreamWaitEvent(g->stream, g->ev_star, 0));
+    FS_TRY(star_reduce(g, counts, g->stream));
+  }
   if (g->n_tiles == 0) return FS_OK;
   const int star = g->star_split ? 2 : Q.use_star;
   if (g->sparse) {

@@ -10,6 +10,7 @@ void plan_destroy(Plan* g) {
   if (g->stream) (void)hipStreamSynchronize(g->stream);
   trace_mark("kernels (to sync)");
   if (g->side) (void)hipStreamSynchronize(g->side);
+  if (g->side2) (void)hipStreamSynchronize(g->side2);
   for (void* q : g->owned) dev_free(q);
   for (void* q : g->owned_layout) dev_free(q);
   for (void* q : g->scratch) dev_free(q);
@@ -23,7 +24,9 @@ void plan_destroy(Plan* g) {
   for (auto& e : g->ev) event_put(g->device, e, true);
   event_put(g->device, g->ev_fork, false);
   event_put(g->device, g->ev_join, false);
+  event_put(g->device, g->ev_star, false);
   stream_put(g->device, g->side);
+  if (g->side2) stream_put(g->device, g->side2);
   if (g->own_stream) stream_put(g->device, g->stream);
   delete g;
   trace_mark("plan: free");
@@ -164,6 +167,7 @@ int plan_layout(Plan* g) {
   g->corr_ready = false;
   FS_HIP(hipStreamSynchronize(g->stream));
   if (g->side) FS_HIP(hipStreamSynchronize(g->side));
+  if (g->side2) FS_HIP(hipStreamSynchronize(g->side2));
   for (void* q : g->owned_layout) dev_free(q);
   g->owned_layout.clear();
   int rc;
@@ -345,6 +349,7 @@ int plan_set_shard(Plan* g, int rank, int world) {
   FS_HIP(hipSetDevice(g->device));
   FS_HIP(hipStreamSynchronize(g->stream));
   if (g->side) FS_HIP(hipStreamSynchronize(g->side));
+  if (g->side2) FS_HIP(hipStreamSynchronize(g->side2));
   for (void* q : g->owned_shard) dev_free(q);
   g->owned_shard.clear();
   g->D = g->Dpart = nullptr;
@@ -410,7 +415,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   for (auto& e : g->ev)
     if (!(e = event_get(device, true))) return fail(FS_EHIP);
   if (!(g->side = stream_get(device)) || !(g->ev_fork = event_get(device, false)) ||
-      !(g->ev_join = event_get(device, false)))
+      !(g->ev_join = event_get(device, false)) || !(g->ev_star = event_get(device, false)))
     return fail(FS_EHIP);
   const Prepared& Q = g->P;
   g->nb = Q.n_pad / kTile;
@@ -464,6 +469,8 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
   g->star_split = choose_star_split(Q);
   g->sparse = choose_sparse(g, Q);
   if (g->star_split && (rc = dalloc(g, &g->alpha, Q.n_pad))) return fail(rc);
+  if (g->star_split && Q.algo == ALGO_MULTISURF && !(g->side2 = stream_get(device)))
+    return fail(FS_EHIP);
   if ((rc = setup_shard(g, bi, bj))) return fail(rc);
   trace_mark("plan: hipMalloc");
   std::vector<int32_t> lab(Q.n_pad, -1);

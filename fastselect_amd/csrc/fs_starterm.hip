@@ -119,9 +119,16 @@ __device__ __forceinline__ int st_bound(const uint32_t* __restrict__ key, int lo
   return lo;
 }
 
-template <int IPT, bool DISC>
+// SUMS = false (SURF*): the column's term U_f into tcol.  SUMS = true
+// (MultiSURF*, before the counts are known): each sample's S_other(i) =
+// S_all(i) - S_same(i), summed class by class over the other classes
+// (G_k(i) = sum over class k of |v_i - v_j|, from class k's prefix at i's
+// position -- valid for a sample of any class), written over the column's
+// xsT values (the workgroup holds them in registers by then); star_reduce
+// weighs them with alpha.
+template <int IPT, bool DISC, bool SUMS>
 __global__ __launch_bounds__(kStThreads) void k_star_terms(
-    const float* __restrict__ xsT, int64_t n, int64_t n_pad, const int32_t* __restrict__ lab,
+    float* __restrict__ xsT, int64_t n, int64_t n_pad, const int32_t* __restrict__ lab,
     const double* __restrict__ alpha, int ncls, double gamma, int64_t c_first, int64_t s_lo,
     int64_t s_hi, const int64_t* __restrict__ out_pos, double* __restrict__ tcol) {
   using Sort = rocprim::block_radix_sort<uint32_t, kStThreads, IPT, uint16_t>;
@@ -129,11 +136,11 @@ __global__ __launch_bounds__(kStThreads) void k_star_terms(
   const int64_t c = c_first + blockIdx.x;
   const int tid = threadIdx.x;
   if (c < s_lo || c >= s_hi || out_pos[c] < 0) {
-    if (tid == 0) tcol[c] = 0.0;
+    if (!SUMS && tid == 0) tcol[c] = 0.0;
     return;
   }
   const int nn = (int)n;
-  const float* __restrict__ col = xsT + c * n_pad;
+  float* __restrict__ col = xsT + c * n_pad;
   uint32_t key[IPT];
   uint16_t idx[IPT];
 #pragma unroll
@@ -145,19 +152,21 @@ __global__ __launch_bounds__(kStThreads) void k_star_terms(
   Sort().sort(key, idx, sm.u.sort);  // blocked: positions tid * IPT + j; padding last
   __syncthreads();                   // the sort's storage is reused below
   const int base = tid * IPT;
-  // per item only its class and (discrete) run bounds stay in registers:
-  // the value decodes from the key, alpha reloads from L1 / L2
+  // per item only its class, (discrete) run bounds and (SUMS) its sum stay
+  // in registers: the value decodes from the key, alpha reloads from L1 / L2
   int cl[IPT];
+  float so[SUMS ? IPT : 1];
   double loc = 0.0;
 #pragma unroll
   for (int j = 0; j < IPT; j++) {
     const bool ok = base + j < nn;
     cl[j] = ok ? lab[idx[j]] : -1;
-    if (!DISC) loc += ok ? (double)st_val(key[j]) : 0.0;
+    if (SUMS) so[j] = 0.0f;
+    if (!DISC && !SUMS) loc += ok ? (double)st_val(key[j]) : 0.0;
   }
   double acc = 0.0;
   uint32_t run[DISC ? IPT : 1];  // lo | hi << 16
-  if (!DISC) {
+  if (!DISC && !SUMS) {
     double P = loc, zero = 0.0, T, z;
     st_scan2(P, zero, sm.ws, T, z);
 #pragma unroll
@@ -168,7 +177,7 @@ __global__ __launch_bounds__(kStThreads) void k_star_terms(
         P += v;
       }
     }
-  } else {
+  } else if (DISC) {
 #pragma unroll
     for (int j = 0; j < IPT; j++)
       if (base + j < nn) sm.u.d.key[base + j] = key[j];
@@ -181,7 +190,7 @@ __global__ __launch_bounds__(kStThreads) void k_star_terms(
         const int lo = st_bound<false>(sm.u.d.key, 0, p, key[j]);
         const int hi = st_bound<true>(sm.u.d.key, p + 1, nn, key[j]);
         run[j] = (uint32_t)lo | ((uint32_t)hi << 16);
-        acc -= alpha[idx[j]] * (double)(nn - (hi - lo));
+        if (!SUMS) acc -= alpha[idx[j]] * (double)(nn - (hi - lo));
       }
     }
   }
@@ -197,13 +206,19 @@ __global__ __launch_bounds__(kStThreads) void k_star_terms(
     st_scan2(lc, ls, sm.ws, tc, ts);
     if (!DISC) {
 #pragma unroll
-      for (int j = 0; j < IPT; j++)
+      for (int j = 0; j < IPT; j++) {
+        const double v = (double)st_val(key[j]);
+        const double G = v * (2.0 * lc - tc) - 2.0 * ls + ts;  // sum over class k of |v - v_j|
+        if (SUMS) {
+          if (cl[j] >= 0 && cl[j] != k) so[j] += (float)G;
+        } else if (cl[j] == k) {
+          acc += gamma * alpha[idx[j]] * G;
+        }
         if (cl[j] == k) {
-          const double v = (double)st_val(key[j]);
-          acc += gamma * alpha[idx[j]] * (v * (2.0 * lc - tc) - 2.0 * ls + ts);
           lc += 1.0;
           ls += v;
         }
+      }
     } else {
       // class-k items before each position, then eq_k = cnt[hi] - cnt[lo]
 #pragma unroll
@@ -214,13 +229,20 @@ __global__ __launch_bounds__(kStThreads) void k_star_terms(
       if (tid == 0) sm.u.d.cnt[nn] = (uint16_t)tc;
       __syncthreads();
 #pragma unroll
-      for (int j = 0; j < IPT; j++)
-        if (cl[j] == k) {
-          const int eq = (int)sm.u.d.cnt[run[j] >> 16] - (int)sm.u.d.cnt[run[j] & 0xFFFFu];
-          acc += gamma * alpha[idx[j]] * (tc - (double)eq);
-        }
+      for (int j = 0; j < IPT; j++) {
+        if (cl[j] < 0 || (SUMS ? cl[j] == k : cl[j] != k)) continue;
+        const int eq = (int)sm.u.d.cnt[run[j] >> 16] - (int)sm.u.d.cnt[run[j] & 0xFFFFu];
+        if (SUMS) so[j] += (float)(tc - (double)eq);
+        else acc += gamma * alpha[idx[j]] * (tc - (double)eq);
+      }
       __syncthreads();  // cnt is rewritten for the next class
     }
+  }
+  if (SUMS) {
+#pragma unroll
+    for (int j = 0; j < IPT; j++)
+      if (base + j < nn) col[idx[j]] = so[j];
+    return;
   }
   // fixed-order reduction of acc
   const int lane = tid & 63, wave = tid >> 6;
@@ -233,6 +255,44 @@ __global__ __launch_bounds__(kStThreads) void k_star_terms(
     for (int w = 0; w < kStWaves; w++) s += sm.ws[0][w];
     tcol[c] = s;
   }
+}
+
+// MultiSURF*'s column terms from the per-sample sums: tcol[c] = -sum_i
+// alpha_i S_other(i) over this share's columns, 4 columns per 256-thread
+// workgroup (alpha read once for the four), fixed-order reduction.
+constexpr int kGvCols = 4;
+__global__ __launch_bounds__(256) void k_star_gemv(const float* __restrict__ So, int64_t n,
+                                                   int64_t n_pad, int64_t PW,
+                                                   const double* __restrict__ alpha, int64_t s_lo,
+                                                   int64_t s_hi, const int64_t* __restrict__ out_pos,
+                                                   double* __restrict__ tcol) {
+  __shared__ double red[kGvCols][256];
+  const int tid = threadIdx.x;
+  const int64_t c0 = (int64_t)blockIdx.x * kGvCols;
+  bool live[kGvCols];
+  double acc[kGvCols];
+#pragma unroll
+  for (int q = 0; q < kGvCols; q++) {
+    const int64_t c = c0 + q;
+    live[q] = c < PW && c >= s_lo && c < s_hi && out_pos[c] >= 0;
+    acc[q] = 0.0;
+  }
+  for (int64_t i = tid; i < n; i += 256) {
+    const double a = alpha[i];
+#pragma unroll
+    for (int q = 0; q < kGvCols; q++)
+      if (live[q]) acc[q] += a * (double)So[(c0 + q) * n_pad + i];
+  }
+#pragma unroll
+  for (int q = 0; q < kGvCols; q++) red[q][tid] = acc[q];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w)
+#pragma unroll
+      for (int q = 0; q < kGvCols; q++) red[q][tid] += red[q][tid + w];
+    __syncthreads();
+  }
+  if (tid < kGvCols && c0 + tid < PW) tcol[c0 + tid] = live[tid] ? -red[tid][0] : 0.0;
 }
 
 // alpha_i: 1 / max(M_i, 1) (MultiSURF*, counts[2i + 1] = M_i) or 1 (SURF*)
@@ -253,14 +313,14 @@ __global__ void k_star_alpha(int64_t n_pad, const double* __restrict__ counts, i
   alpha[i] = a;
 }
 
-template <bool DISC>
+template <bool DISC, bool SUMS>
 int launch_terms(Plan* g, int64_t c_first, int64_t ncols, int64_t s_lo, int64_t s_hi,
                  double gamma, hipStream_t st) {
   const Prepared& Q = g->P;
   if (ncols <= 0) return FS_OK;
   const unsigned grid = (unsigned)ncols;
 #define FS_ST(IPT)                                                                              \
-  k_star_terms<IPT, DISC><<<grid, kStThreads, 0, st>>>(                                      \
+  k_star_terms<IPT, DISC, SUMS><<<grid, kStThreads, 0, st>>>(                                \
       g->xsT, Q.n, Q.n_pad, g->lab, g->alpha, Q.n_classes, gamma, c_first, s_lo, s_hi,           \
       g->out_pos, g->tcol)
   const int64_t ipt = (Q.n + kStThreads - 1) / kStThreads;
@@ -275,6 +335,30 @@ int launch_terms(Plan* g, int64_t c_first, int64_t ncols, int64_t s_lo, int64_t 
   return launch_check(DISC ? "k_star_terms<disc>" : "k_star_terms");
 }
 
+int check_split(const Plan* g) {
+  const Prepared& Q = g->P;
+  if (!g->xsT || !g->alpha || !g->tcol || !star_split_fits(Q.n, Q.n_classes)) {
+    set_error("star split: plan without its buffers or outside the split's sizes");
+    return FS_EINVAL;
+  }
+  return FS_OK;
+}
+
+// this rank's share of the columns (tile-sharded MultiSURF: each rank adds
+// its share before the sum all-reduce); a row plan covers every column for
+// its own focal rows
+void share(const Plan* g, int64_t& s_lo, int64_t& s_hi) {
+  s_lo = g->P.PW * g->rank / g->world;
+  s_hi = g->P.PW * (g->rank + 1) / g->world;
+}
+
+int run_alpha(Plan* g, const double* counts, hipStream_t st) {
+  const Prepared& Q = g->P;
+  k_star_alpha<<<(unsigned)((Q.n_pad + 255) / 256), 256, 0, st>>>(Q.n_pad, counts, g->r_lo,
+                                                                 g->r_hi, g->alpha);
+  return launch_check("k_star_alpha");
+}
+
 }  // namespace
 
 bool star_split_fits(int64_t n, int32_t n_classes) {
@@ -284,20 +368,33 @@ bool star_split_fits(int64_t n, int32_t n_classes) {
 
 int star_terms(Plan* g, const double* counts, hipStream_t st) {
   const Prepared& Q = g->P;
-  if (!g->xsT || !g->alpha || !g->tcol || !star_split_fits(Q.n, Q.n_classes)) {
-    set_error("star split: plan without its buffers or outside the split's sizes");
-    return FS_EINVAL;
-  }
-  k_star_alpha<<<(unsigned)((Q.n_pad + 255) / 256), 256, 0, st>>>(Q.n_pad, counts, g->r_lo,
-                                                                 g->r_hi, g->alpha);
-  FS_TRY(launch_check("k_star_alpha"));
-  // this rank's share of the columns (tile-sharded MultiSURF: each rank adds
-  // its share before the sum all-reduce); a row plan covers every column for
-  // its own focal rows
-  const int64_t s_lo = Q.PW * g->rank / g->world, s_hi = Q.PW * (g->rank + 1) / g->world;
+  FS_TRY(check_split(g));
+  FS_TRY(run_alpha(g, counts, st));
+  int64_t s_lo, s_hi;
+  share(g, s_lo, s_hi);
   const double gamma = Q.algo == ALGO_SURF ? 2.0 : 1.0;
-  FS_TRY(launch_terms<false>(g, 0, Q.PC, s_lo, s_hi, gamma, st));
-  return launch_terms<true>(g, Q.PC, Q.PW - Q.PC, s_lo, s_hi, gamma, st);
+  FS_TRY((launch_terms<false, false>(g, 0, Q.PC, s_lo, s_hi, gamma, st)));
+  return launch_terms<true, false>(g, Q.PC, Q.PW - Q.PC, s_lo, s_hi, gamma, st);
+}
+
+int star_sums(Plan* g, hipStream_t st) {
+  const Prepared& Q = g->P;
+  FS_TRY(check_split(g));
+  int64_t s_lo, s_hi;
+  share(g, s_lo, s_hi);
+  FS_TRY((launch_terms<false, true>(g, 0, Q.PC, s_lo, s_hi, 1.0, st)));
+  return launch_terms<true, true>(g, Q.PC, Q.PW - Q.PC, s_lo, s_hi, 1.0, st);
+}
+
+int star_reduce(Plan* g, const double* counts, hipStream_t st) {
+  const Prepared& Q = g->P;
+  FS_TRY(check_split(g));
+  FS_TRY(run_alpha(g, counts, st));
+  int64_t s_lo, s_hi;
+  share(g, s_lo, s_hi);
+  k_star_gemv<<<(unsigned)((Q.PW + kGvCols - 1) / kGvCols), 256, 0, st>>>(
+      g->xsT, Q.n, Q.n_pad, Q.PW, g->alpha, s_lo, s_hi, g->out_pos, g->tcol);
+  return launch_check("k_star_gemv");
 }
 
 }  // namespace gpu
