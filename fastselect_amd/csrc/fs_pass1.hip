@@ -1136,6 +1136,10 @@ int run_quantize_dist(Plan* g) {
   // SURF's integer route (fs_surfint.hip) quantises as MultiSURF does: no
   // mean correction, no K-split, float64 X
   const bool reuse = g->corr_ready && Q.algo == ALGO_MULTISURF;
+  // MultiSURF*'s per-sample sums overwrite xsT in place: a pass 1 run again
+  // (the deferred row guard's switch to 32-bit operands) quantises only after
+  // the previous sums are done with it
+  if (g->side2) FS_HIP(hipStreamWaitEvent(g->stream, g->ev_star, 0));
   g->corr_ready = false;  // later steps quantise again (the terms overwrote epsT)
   // quantisation errors for the mean correction (MultiSURF; ReliefF keeps
   // them unused), none on SURF's integer route (no epsT)
