@@ -511,22 +511,24 @@ def test_turf_resident_rows_gpu_equals_refits(name):
     np.testing.assert_allclose(fast.feature_importances_, slow.feature_importances_, atol=1e-7)
 
 
-def _two_rank_worker(rank, world, port, out_path):
+def _two_rank_worker(rank, world, port, out_path, star=False):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from fastselect_amd.parallel import multisurf_scores
     X, y = make_classification(n_samples=900, n_features=400, random_state=7)
-    s = multisurf_scores(X, y, use_star=False, backend="gpu", device=0)
+    s = multisurf_scores(X, y, use_star=star, backend="gpu", device=0)
     np.save(f"{out_path}.{rank}.npy", s)
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_ranks_share_one_gpu(tmp_path):
+@pytest.mark.parametrize("star", [False, True])
+def test_two_ranks_share_one_gpu(tmp_path, star):
     """The multi-process path with GPU plans: two ranks (both on cuda:0,
     gloo collectives on device tensors) each compute half the pair tiles;
-    every rank ends with the single-process scores."""
+    every rank ends with the single-process scores.  MultiSURF*: each rank
+    also adds the star split's column terms of its half of the columns."""
     import socket
 
     import torch.multiprocessing as mp
@@ -537,11 +539,11 @@ def test_two_ranks_share_one_gpu(tmp_path):
     port = s.getsockname()[1]
     s.close()
     out = str(tmp_path / "scores")
-    mp.spawn(_two_rank_worker, args=(2, port, out), nprocs=2, join=True)
+    mp.spawn(_two_rank_worker, args=(2, port, out, star), nprocs=2, join=True)
     a, b = np.load(out + ".0.npy"), np.load(out + ".1.npy")
     np.testing.assert_array_equal(a, b)
     X, y = make_classification(n_samples=900, n_features=400, random_state=7)
-    ref = MultiSURF(backend="gpu").fit(X, y).feature_importances_
+    ref = MultiSURF(backend="gpu", use_star=star).fit(X, y).feature_importances_
     assert scale_rel_err(a, ref) < 1e-6
 
 
