@@ -57,18 +57,6 @@ static int choose_q16(const Prepared& P) {
   return (P.n >= min_rows && P.pc >= kFeatPad) ? 1 : 0;
 }
 
-// Pass 2 on the non-zero pair weights only (k_weights_sparse +
-// k_score_sparse) or on every pair (k_weights + k_score).  The sparse loop
-// costs ~1.7x the dense one per evaluated pair (LDS row gather), so it pays
-// below ~58% density.  Measured (tools/bench_configs.py, one MI355X):
-// MultiSURF weighs the ~42% of pairs near one of their samples (cfg4 pass 2
-// 142 -> 103 ms sparse); MultiSURF* ~62% (cfg5 91 ms dense vs 102 sparse);
-// SURF about break-even (cfg5), SURF* weighs nearly every pair.  A
-// row-sharded SURF plan zeroes the sides of the samples it does not own, so
-// it goes sparse.  The sparse test hook forces either.
-// The star split (fs_starterm.hip) leaves pass 2 the near pairs only:
-// MultiSURF*'s 41.7% and SURF*'s 62.4% at cfg5 (profiles/r06/near_density.txt)
-// go sparse like MultiSURF's.
 // MultiSURF* / SURF* in fast accumulation: near pairs in pass 2, the far
 // pairs' all-pairs part per column from its sorted values (fs_starterm.hip),
 // for n <= 24576 and up to 8 classes (one workgroup sorts a column in LDS);
@@ -80,12 +68,29 @@ static bool choose_star_split(const Prepared& P) {
   return true;
 }
 
+// Pass 2 on the non-zero pair weights only (k_weights_sparse2 +
+// k_score_sparse2) or on every pair (k_weights + k_score).  Round 1's sparse
+// loop cost ~1.7x the dense one per evaluated pair; the v2 loop (round 4)
+// ~1.3x, so it pays below ~75% density.  MultiSURF weighs the ~42% of pairs
+// near one of their samples, SURF the ~62% (cfg5: the whole step 179.4 ->
+// 156.6 ms sparse, profiles/r06/starsplit/surf_sparse_ab.txt); the star
+// variants weigh every miss / every pair and go sparse through the star
+// split (profiles/r06/near_density.txt).  SURF below kSparseMinRowsSurf
+// samples keeps the dense loop: its pass 2 costs little there, and on the
+// heavy-tailed tail sweep (tests/test_random_parity.py, seed 2: n = 300-3000)
+// the sparse loop's float32 partials ended 4.8x closer to the float64 sums
+// than the reference's own, against the 5x the attributed bar asks.  The
+// sparse test hook forces either.
+constexpr int64_t kSparseMinRowsSurf = 4096;
 static int choose_sparse(const Plan* g, const Prepared& P) {
   if (P.algo == ALGO_RELIEFF) return 0;
   if (test_hooks().sparse >= 0) return test_hooks().sparse != 0 ? 1 : 0;
   if (g->star_split) return 1;
-  if (P.algo == ALGO_MULTISURF) return P.use_star ? 0 : 1;
-  return (g->r_hi - g->r_lo < P.n) ? 1 : 0;  // SURF / SURF*: only when row-sharded
+  if (!P.use_star) return (P.algo == ALGO_MULTISURF || P.n >= kSparseMinRowsSurf ||
+                           g->r_hi - g->r_lo < P.n) ? 1 : 0;
+  // the star weights without the split (n > 24576, > 8 classes): dense,
+  // unless a row-sharded SURF* plan zeroes the sides it does not own
+  return (P.algo == ALGO_SURF && g->r_hi - g->r_lo < P.n) ? 1 : 0;
 }
 
 // Feature-layout part of a plan: everything sized by the kept features

@@ -44,6 +44,11 @@ namespace gpu {
 namespace {
 
 constexpr int kStThreads = 1024;
+// minimum waves per SIMD the compiler plans registers for (A/B builds only:
+// make variant DEFS=-DFS_ST_MIN_WAVES=8 -> two workgroups per CU)
+#ifndef FS_ST_MIN_WAVES
+#define FS_ST_MIN_WAVES 1
+#endif
 constexpr int kStMaxIpt = 24;
 constexpr int kStMaxClasses = 8;
 constexpr int kStWaves = kStThreads / 64;
@@ -127,7 +132,7 @@ __device__ __forceinline__ int st_bound(const uint32_t* __restrict__ key, int lo
 // xsT values (the workgroup holds them in registers by then); star_reduce
 // weighs them with alpha.
 template <int IPT, bool DISC, bool SUMS>
-__global__ __launch_bounds__(kStThreads) void k_star_terms(
+__global__ __launch_bounds__(kStThreads, FS_ST_MIN_WAVES) void k_star_terms(
     float* __restrict__ xsT, int64_t n, int64_t n_pad, const int32_t* __restrict__ lab,
     const double* __restrict__ alpha, int ncls, double gamma, int64_t c_first, int64_t s_lo,
     int64_t s_hi, const int64_t* __restrict__ out_pos, double* __restrict__ tcol) {

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--nostar", action="store_true", help="the config's algorithm without star")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -27,7 +28,9 @@ def main():
     import bench
     from fastselect_amd import _lib
     from fastselect_amd.parallel import ShardedMultiSURF, prepare_inputs
-    cfg = bench.CONFIGS[a.config]
+    cfg = dict(bench.CONFIGS[a.config])
+    if a.nostar:
+        cfg["star"] = False
     X, y = bench.make_data(cfg["n"], cfg["p"], 42, cfg["red"])
     surf = cfg["algo"] == "surf"
     if surf:  # a resident SURF row plan (bench.py's cfg5s step)
