@@ -1108,7 +1108,7 @@ int row_guard(Plan* g) {
 static int fork_star_terms(Plan* g) {
   FS_HIP(hipEventRecord(g->ev_fork, g->stream));
   FS_HIP(hipStreamWaitEvent(g->side, g->ev_fork, 0));
-  FS_TRY(star_terms(g, nullptr, g->side));
+  FS_TRY(star_terms(g, g->side));
   FS_HIP(hipEventRecord(g->ev_join, g->side));
   return FS_OK;
 }

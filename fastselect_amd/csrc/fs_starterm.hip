@@ -371,15 +371,14 @@ bool star_split_fits(int64_t n, int32_t n_classes) {
          n_classes <= kStMaxClasses;
 }
 
-int star_terms(Plan* g, const double* counts, hipStream_t st) {
+int star_terms(Plan* g, hipStream_t st) {
   const Prepared& Q = g->P;
   FS_TRY(check_split(g));
-  FS_TRY(run_alpha(g, counts, st));
+  FS_TRY(run_alpha(g, nullptr, st));  // SURF*: alpha = 1 on the focal rows
   int64_t s_lo, s_hi;
   share(g, s_lo, s_hi);
-  const double gamma = Q.algo == ALGO_SURF ? 2.0 : 1.0;
-  FS_TRY((launch_terms<false, false>(g, 0, Q.PC, s_lo, s_hi, gamma, st)));
-  return launch_terms<true, false>(g, Q.PC, Q.PW - Q.PC, s_lo, s_hi, gamma, st);
+  FS_TRY((launch_terms<false, false>(g, 0, Q.PC, s_lo, s_hi, 2.0, st)));
+  return launch_terms<true, false>(g, Q.PC, Q.PW - Q.PC, s_lo, s_hi, 2.0, st);
 }
 
 int star_sums(Plan* g, hipStream_t st) {
