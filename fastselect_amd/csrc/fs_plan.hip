@@ -60,12 +60,20 @@ static int choose_q16(const Prepared& P) {
 // MultiSURF* / SURF* in fast accumulation: near pairs in pass 2, the far
 // pairs' all-pairs part per column from its sorted values (fs_starterm.hip),
 // for n <= 24576 and up to 8 classes (one workgroup sorts a column in LDS);
-// the star_split test hook forces either form where it fits.
-static bool choose_star_split(const Prepared& P) {
+// the star_split test hook forces either form where it fits.  Its
+// feature-major copy of the pass-2 values (xsT, n_pad x PW floats) is taken
+// only while it stays under a quarter of the device's free memory; a plan
+// that large keeps the dense star weights.
+static bool choose_star_split(const Prepared& P, int device) {
   if (!P.use_star || P.ref_accum || P.algo == ALGO_RELIEFF) return false;
   if (!star_split_fits(P.n, P.n_classes)) return false;
   if (test_hooks().star_split >= 0) return test_hooks().star_split != 0;
-  return true;
+  size_t free_b = 0, total_b = 0;
+  if (hipSetDevice(device) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return (double)P.n_pad * (double)P.PW * sizeof(float) <= 0.25 * (double)free_b;
 }
 
 // Pass 2 on the non-zero pair weights only (k_weights_sparse2 +
@@ -471,7 +479,7 @@ int plan_create(Plan** out, const Prepared& P, const void* x, int x_is_f64, int 
         (rc = dalloc(g, &g->bcnt, (size_t)(Q.n / kExactThrRows + 2))))
       return fail(rc);
   }
-  g->star_split = choose_star_split(Q);
+  g->star_split = choose_star_split(Q, device);
   g->sparse = choose_sparse(g, Q);
   if (g->star_split && (rc = dalloc(g, &g->alpha, Q.n_pad))) return fail(rc);
   if (g->star_split && Q.algo == ALGO_MULTISURF && !(g->side2 = stream_get(device)))
