@@ -100,10 +100,17 @@ __device__ __forceinline__ void st_scan2(double& a, double& b, double (*ws)[kStW
   b = pb + y - b;
 }
 
+// rocPRIM's block radix sort (8-bit digits, match ranking: 4 passes).  Its
+// scatters leave ~74% of the kernel's LDS-active cycles in bank conflicts at
+// cfg5 (profiles/r06/starsplit/pmc_cfg5m_table.txt); neither the padding
+// hint nor odd items per thread moved the step (starsplit/ipt_ab.txt)
+template <int IPT>
+using StSort = rocprim::block_radix_sort<uint32_t, kStThreads, IPT, uint16_t>;
+
 template <int IPT, bool DISC>
 struct StLds {
   union {
-    typename rocprim::block_radix_sort<uint32_t, kStThreads, IPT, uint16_t>::storage_type sort;
+    typename StSort<IPT>::storage_type sort;
     struct {
       uint32_t key[DISC ? kStThreads * IPT : 1];      // sorted keys (run bounds)
       uint16_t cnt[DISC ? kStThreads * IPT + 2 : 1];  // class-c items before each position
@@ -136,7 +143,7 @@ __global__ __launch_bounds__(kStThreads, FS_ST_MIN_WAVES) void k_star_terms(
     float* __restrict__ xsT, int64_t n, int64_t n_pad, const int32_t* __restrict__ lab,
     const double* __restrict__ alpha, int ncls, double gamma, int64_t c_first, int64_t s_lo,
     int64_t s_hi, const int64_t* __restrict__ out_pos, double* __restrict__ tcol) {
-  using Sort = rocprim::block_radix_sort<uint32_t, kStThreads, IPT, uint16_t>;
+  using Sort = StSort<IPT>;
   __shared__ StLds<IPT, DISC> sm;
   const int64_t c = c_first + blockIdx.x;
   const int tid = threadIdx.x;
