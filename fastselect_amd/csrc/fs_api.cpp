@@ -148,6 +148,7 @@ int fs_test_hook(const char* name, int64_t value) {
   else if (k == "ref_q16") h.ref_q16 = value;
   else if (k == "surf_f64") h.surf_f64 = value;
   else if (k == "star_split") h.star_split = value;
+  else if (k == "colsort_star") h.colsort_star = value;
   else if (k == "colsort_bins12") h.colsort_bins12 = value;
   else if (k == "colsort_global") h.colsort_global = value;
   else {

@@ -498,6 +498,121 @@ __global__ void k_colsort_offsets(int64_t n, int64_t nc, unsigned* __restrict__ 
   if (k <= nc) off[k] = (unsigned)(k * n);
 }
 
+// MultiSURF* with the star split (fs_starterm.hip): one sort of each
+// continuous column serves both the mean correction and the star split's
+// per-sample sums.  The column is ordered by the correction's key (the full
+// sort of k_colsort_full: exact eps, no bin rounding), its terms written as
+// there; then, in the same order, each sample's sum over the other classes
+// of |v_i - v_j| (v = the float32 pass-2 values, xsT) from per-class prefix
+// sums, written over xsT (star_reduce weighs them).  The key order is v's
+// order up to samples whose t agree to 2^-s quanta (v within an ulp): the
+// sums err by at most twice those pairs' |v_i - v_j|.
+__device__ __forceinline__ void cs_scan2(double& a, double& b, double (*ws)[kCsThreads / 64],
+                                         double& ta, double& tb) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  double x = a, y = b;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double tx = __shfl_up(x, o), ty = __shfl_up(y, o);
+    if (lane >= o) {
+      x += tx;
+      y += ty;
+    }
+  }
+  if (lane == 63) {
+    ws[0][wave] = x;
+    ws[1][wave] = y;
+  }
+  __syncthreads();
+  double pa = 0.0, pb = 0.0, sa = 0.0, sb = 0.0;
+#pragma unroll
+  for (int w = 0; w < kCsThreads / 64; w++) {
+    const double u = ws[0][w], v = ws[1][w];
+    if (w < wave) {
+      pa += u;
+      pb += v;
+    }
+    sa += u;
+    sb += v;
+  }
+  __syncthreads();
+  ta = sa;
+  tb = sb;
+  a = pa + x - a;
+  b = pb + y - b;
+}
+
+template <int IPT>
+__global__ __launch_bounds__(kCsThreads) void k_colsort_star(
+    const uint32_t* __restrict__ xqT, int64_t n, int64_t n_pad, int s, int q16, int64_t c_lo,
+    float* __restrict__ epsT, float* __restrict__ xsT, const int32_t* __restrict__ lab,
+    const int64_t* __restrict__ out_pos, int ncls) {
+  using Sort = rocprim::block_radix_sort<uint32_t, kCsThreads, IPT, uint16_t>;
+  __shared__ typename Sort::storage_type st;
+  __shared__ long long wsum[kCsThreads / 64];
+  __shared__ double ws2[2][kCsThreads / 64];
+  const int64_t c = c_lo + blockIdx.x;
+  float* __restrict__ e = epsT + c * n_pad;
+  float* __restrict__ xv = xsT + c * n_pad;
+  const int base = threadIdx.x * IPT;
+  uint32_t key[IPT];
+  uint16_t idx[IPT];
+#pragma unroll
+  for (int k = 0; k < IPT; k++) {
+    const int i = base + k;
+    key[k] = i < n ? cs_key(cs_col_q(xqT, c, i, n_pad, q16), cs_fx(e[i]), s) : 0xFFFFFFFFu;
+    idx[k] = (uint16_t)i;
+  }
+  Sort().sort(key, idx, st);
+  long long ef[IPT], loc = 0;
+#pragma unroll
+  for (int k = 0; k < IPT; k++) {
+    ef[k] = base + k < n ? cs_fx(e[idx[k]]) : 0;
+    loc += ef[k];
+  }
+  long long T;
+  long long P = cs_block_scan(loc, wsum, T);
+#pragma unroll
+  for (int k = 0; k < IPT; k++) {
+    const int pos = base + k;
+    if (pos < n) e[idx[k]] = cs_term(ef[k], pos, n, P, T);
+    P += ef[k];
+  }
+  if (out_pos[c] < 0) return;  // padding column: no star sums (uniform per workgroup)
+  float v[IPT], so[IPT];
+  int cl[IPT];
+#pragma unroll
+  for (int k = 0; k < IPT; k++) {
+    const bool ok = base + k < n;
+    v[k] = ok ? xv[idx[k]] : 0.0f;
+    cl[k] = ok ? lab[idx[k]] : -1;
+    so[k] = 0.0f;
+  }
+  for (int q = 0; q < ncls; q++) {
+    double lc = 0.0, ls = 0.0;
+#pragma unroll
+    for (int k = 0; k < IPT; k++)
+      if (cl[k] == q) {
+        lc += 1.0;
+        ls += (double)v[k];
+      }
+    double tc, ts;
+    cs_scan2(lc, ls, ws2, tc, ts);
+#pragma unroll
+    for (int k = 0; k < IPT; k++) {
+      const double vk = (double)v[k];
+      if (cl[k] >= 0 && cl[k] != q) so[k] += (float)(vk * (2.0 * lc - tc) - 2.0 * ls + ts);
+      if (cl[k] == q) {
+        lc += 1.0;
+        ls += vk;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < IPT; k++)
+    if (base + k < n) xv[idx[k]] = so[k];
+}
+
 // columns per batch of the large-n route: keys + indices double-buffered
 // (16 B per sample) within ~512 MB, at most 4096 columns
 int64_t batch_cols(int64_t n, int64_t ncols) {
@@ -540,6 +655,36 @@ size_t colsort_scratch_bytes(int64_t n, int64_t ncols) {
     return 0;
   }
   return batch_bytes(n, nb) + align256(temp);
+}
+
+int colsort_star_terms(const uint32_t* xqT, float* epsT, float* xsT, const int32_t* lab,
+                       const int64_t* out_pos, int ncls, int64_t n, int64_t n_pad, int64_t c_lo,
+                       int64_t c_hi, int q16, int key_shift, void* stream_v) {
+  hipStream_t stream = (hipStream_t)stream_v;
+  const int64_t nc = c_hi - c_lo;
+  if (nc <= 0 || n < 1) return 0;
+  if (n > (int64_t)kCsThreads * kCsMaxIpt) {
+    set_error("k_colsort_star: more samples than one workgroup sorts");
+    return -1;
+  }
+  const unsigned grid = (unsigned)nc;
+#define FS_CSS(IPT)                                                                            \
+  k_colsort_star<IPT><<<grid, kCsThreads, 0, stream>>>(xqT, n, n_pad, key_shift, q16, c_lo,     \
+                                                       epsT, xsT, lab, out_pos, ncls)
+  const int64_t ipt = (n + kCsThreads - 1) / kCsThreads;
+  if (ipt <= 4) FS_CSS(4);
+  else if (ipt <= 8) FS_CSS(8);
+  else if (ipt <= 10) FS_CSS(10);
+  else if (ipt <= 12) FS_CSS(12);
+  else if (ipt <= 16) FS_CSS(16);
+  else if (ipt <= 20) FS_CSS(20);
+  else FS_CSS(24);
+#undef FS_CSS
+  if (hipGetLastError() != hipSuccess) {
+    set_error("k_colsort_star: launch failed");
+    return -1;
+  }
+  return 0;
 }
 
 int colsort_terms(const uint32_t* xqT, float* epsT, int64_t n, int64_t n_pad, int64_t c_lo,

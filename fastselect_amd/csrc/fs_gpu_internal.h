@@ -327,12 +327,14 @@ int surf_resolve(Plan* g);
 // fs_starterm.hip: the star split's sizes (n <= 24576, up to 8 classes);
 // SURF*'s per-column all-pairs terms of this plan's focal rows into g->tcol
 // (star_terms, beside pass 1); MultiSURF*'s in two steps: star_sums (beside
-// pass 1: every sample's sum over the other classes, into xsT in place), then
+// pass 1: every sample's sum over the other classes, into xsT in place; the
+// continuous columns' come with the mean correction's sort, colsort_star_terms,
+// unless `continuous`), then
 // star_reduce once the neighbour counts are known (alpha-weighted column sums
 // of this rank's column share into g->tcol).  All launched on st.
 bool star_split_fits(int64_t n, int32_t n_classes);
 int star_terms(Plan* g, hipStream_t st);
-int star_sums(Plan* g, hipStream_t st);
+int star_sums(Plan* g, hipStream_t st, bool continuous);
 int star_reduce(Plan* g, const double* counts, hipStream_t st);
 // fs_pass2.hip
 int shard_segments(Plan* g);

@@ -140,6 +140,7 @@ struct TestHooks {
   int64_t ref_q16 = 0;         // 1: reference-order MultiSURF may take 16-bit operands
   int64_t surf_f64 = -1;       // 0 / 1: SURF on integer / float64 distances (surf_band)
   int64_t star_split = -1;     // 0 / 1: MultiSURF* / SURF* dense star weights / near-only + column terms
+  int64_t colsort_star = -1;   // 0: MultiSURF* split plans sort twice (binned correction + star sort)
   int64_t colsort_bins12 = 0;  // 1: 4096 bins at every n
   int64_t colsort_global = 0;  // 1: the large-n (device sort) route at every n
 };
@@ -472,12 +473,21 @@ bool colsort_lds(int64_t n);
 // workgroup's LDS holds them next to the column's entries (12288 < n <=
 // 20480: half the within-bin work of 4096 bins at cfg4's n = 20000), 12
 // elsewhere; the colsort_bins12 test hook keeps 12 everywhere.  Both
-// backends bin alike, so their terms stay identical.
+// backends bin alike, so their terms stay identical -- except MultiSURF*
+// plans with the star split on the GPU, which sort every column whole
+// (colsort_star_terms: the exact eps of every neighbour, not 2^-12 quanta).
 int colsort_bin_bits(int64_t n);
 size_t colsort_scratch_bytes(int64_t n, int64_t ncols);
 int colsort_terms(const uint32_t* xqT, float* epsT, int64_t n, int64_t n_pad, int64_t c_lo,
                   int64_t c_hi, int q16, int key_shift, void* scratch, size_t scratch_bytes,
                   void* stream);
+// MultiSURF* star split (n <= 24576): the same terms from a full sort of
+// every column (no bin rounding), and in that order each sample's sum over
+// the other classes of |v_i - v_j| written over xsT (fs_starterm.hip
+// star_reduce); padding columns (out_pos < 0) get the terms only.
+int colsort_star_terms(const uint32_t* xqT, float* epsT, float* xsT, const int32_t* lab,
+                       const int64_t* out_pos, int ncls, int64_t n, int64_t n_pad, int64_t c_lo,
+                       int64_t c_hi, int q16, int key_shift, void* stream);
 struct Plan;
 // Tile sharding (MultiSURF): tile t belongs to rank t % world.  Row
 // sharding (r_hi >= 0): the tiles touching the 128-row blocks of [r_lo, r_hi).

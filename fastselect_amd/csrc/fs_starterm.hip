@@ -275,8 +275,9 @@ __global__ __launch_bounds__(kStThreads, FS_ST_MIN_WAVES) void k_star_terms(
 constexpr int kGvCols = 4;
 __global__ __launch_bounds__(256) void k_star_gemv(const float* __restrict__ So, int64_t n,
                                                    int64_t n_pad, int64_t PW,
-                                                   const double* __restrict__ alpha, int64_t s_lo,
-                                                   int64_t s_hi, const int64_t* __restrict__ out_pos,
+                                                   const double* __restrict__ alpha, int64_t s0,
+                                                   int64_t s1, int64_t d0, int64_t d1,
+                                                   const int64_t* __restrict__ out_pos,
                                                    double* __restrict__ tcol) {
   __shared__ double red[kGvCols][256];
   const int tid = threadIdx.x;
@@ -286,7 +287,7 @@ __global__ __launch_bounds__(256) void k_star_gemv(const float* __restrict__ So,
 #pragma unroll
   for (int q = 0; q < kGvCols; q++) {
     const int64_t c = c0 + q;
-    live[q] = c < PW && c >= s_lo && c < s_hi && out_pos[c] >= 0;
+    live[q] = c < PW && ((c >= s0 && c < s1) || (c >= d0 && c < d1)) && out_pos[c] >= 0;
     acc[q] = 0.0;
   }
   for (int64_t i = tid; i < n; i += 256) {
@@ -356,12 +357,17 @@ int check_split(const Plan* g) {
   return FS_OK;
 }
 
-// this rank's share of the columns (tile-sharded MultiSURF: each rank adds
-// its share before the sum all-reduce); a row plan covers every column for
-// its own focal rows
-void share(const Plan* g, int64_t& s_lo, int64_t& s_hi) {
-  s_lo = g->P.PW * g->rank / g->world;
-  s_hi = g->P.PW * (g->rank + 1) / g->world;
+// this rank's columns of the split: the continuous ones of its mean
+// correction ([c_lo, c_hi): pc r / N ... pc (r + 1) / N, so that one sort
+// can serve both, fs_colsort.hip k_colsort_star) and PD r / N ... of the
+// discrete ones.  Tile-sharded MultiSURF* ranks add their columns' terms
+// before the sum all-reduce; a row plan (world 1) covers every column.
+void shares(const Plan* g, int64_t& c0, int64_t& c1, int64_t& d0, int64_t& d1) {
+  const Prepared& Q = g->P;
+  c0 = g->c_lo;
+  c1 = g->c_hi;
+  d0 = Q.PC + (Q.PW - Q.PC) * g->rank / g->world;
+  d1 = Q.PC + (Q.PW - Q.PC) * (g->rank + 1) / g->world;
 }
 
 int run_alpha(Plan* g, const double* counts, hipStream_t st) {
@@ -382,29 +388,29 @@ int star_terms(Plan* g, hipStream_t st) {
   const Prepared& Q = g->P;
   FS_TRY(check_split(g));
   FS_TRY(run_alpha(g, nullptr, st));  // SURF*: alpha = 1 on the focal rows
-  int64_t s_lo, s_hi;
-  share(g, s_lo, s_hi);
-  FS_TRY((launch_terms<false, false>(g, 0, Q.PC, s_lo, s_hi, 2.0, st)));
-  return launch_terms<true, false>(g, Q.PC, Q.PW - Q.PC, s_lo, s_hi, 2.0, st);
+  int64_t c0, c1, d0, d1;
+  shares(g, c0, c1, d0, d1);
+  FS_TRY((launch_terms<false, false>(g, 0, Q.PC, c0, c1, 2.0, st)));
+  return launch_terms<true, false>(g, Q.PC, Q.PW - Q.PC, d0, d1, 2.0, st);
 }
 
-int star_sums(Plan* g, hipStream_t st) {
+int star_sums(Plan* g, hipStream_t st, bool continuous) {
   const Prepared& Q = g->P;
   FS_TRY(check_split(g));
-  int64_t s_lo, s_hi;
-  share(g, s_lo, s_hi);
-  FS_TRY((launch_terms<false, true>(g, 0, Q.PC, s_lo, s_hi, 1.0, st)));
-  return launch_terms<true, true>(g, Q.PC, Q.PW - Q.PC, s_lo, s_hi, 1.0, st);
+  int64_t c0, c1, d0, d1;
+  shares(g, c0, c1, d0, d1);
+  if (continuous) FS_TRY((launch_terms<false, true>(g, 0, Q.PC, c0, c1, 1.0, st)));
+  return launch_terms<true, true>(g, Q.PC, Q.PW - Q.PC, d0, d1, 1.0, st);
 }
 
 int star_reduce(Plan* g, const double* counts, hipStream_t st) {
   const Prepared& Q = g->P;
   FS_TRY(check_split(g));
   FS_TRY(run_alpha(g, counts, st));
-  int64_t s_lo, s_hi;
-  share(g, s_lo, s_hi);
+  int64_t c0, c1, d0, d1;
+  shares(g, c0, c1, d0, d1);
   k_star_gemv<<<(unsigned)((Q.PW + kGvCols - 1) / kGvCols), 256, 0, st>>>(
-      g->xsT, Q.n, Q.n_pad, Q.PW, g->alpha, s_lo, s_hi, g->out_pos, g->tcol);
+      g->xsT, Q.n, Q.n_pad, Q.PW, g->alpha, c0, c1, d0, d1, g->out_pos, g->tcol);
   return launch_check("k_star_gemv");
 }
 

@@ -116,7 +116,7 @@ FS_API int fs_get_accumulation(void);
  * ("ksplit", "q16", "sparse", "shards", "q16_guard_off", "thr_exact_all",
  * "exact_gather", "row_panel",
  * "rf_xlds", "rf_fcap", "ties_1w", "ties_coop", "rf_ref_replay", "ref_q16", "surf_f64",
- * "colsort_bins12", "colsort_global", "star_split").  FS_EINVAL for an unknown name.  Not thread-safe
+ * "colsort_bins12", "colsort_global", "star_split", "colsort_star").  FS_EINVAL for an unknown name.  Not thread-safe
  * against concurrent scoring calls.
  */
 FS_API int fs_test_hook(const char* name, int64_t value);
